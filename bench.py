@@ -1,0 +1,137 @@
+#!/usr/bin/env python3
+"""Headline benchmark: ResNet-50 (CIFAR stem) training throughput, global batch 1024, DDP.
+
+BASELINE.json metric: "images/sec (whole node) ResNet-50 bs=1024 DDP at 1/2/4/8 MI355X;
+epoch time".  Reference number: ~680 img/s (derived from the reference's
+published epoch time with its tricks enabled).
+
+    python bench.py                               # 1 GPU, defaults
+    python -m torch.distributed.run --nnodes=1 --nproc-per-node 8 --master-addr 127.0.0.1 \
+        --master-port 29500 bench.py --gpus 8 --steps 50 --warmup 10
+
+One timed step = the full reference training step on synthetic CIFAR-shaped data and
+random-init weights: device-resident batch + GPU augmentation (crop/flip/normalise),
+input mixup, forward + mixup cross-entropy + backward (HIP engine, bf16), bucketed RCCL
+gradient all-reduce overlapped with backward, grad-norm clip (10.0), MADGRAD step
+(the reference's default optimizer for this path, resnet50_test.py:493).  Global batch is
+fixed at 1024 (per-GPU 1024/N, strong scaling).  W warmup steps are
+untimed; exactly K steps are timed between barrier + device synchronisation on both
+sides; the MAX time over ranks is reported.  Rank 0 prints one JSON line.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+BASELINE_IMG_S = 680.0  # ~680 img/s (reference w/ tricks, ~73 s/epoch)
+METRIC = "images/sec (whole node) ResNet-50 bs=1024 DDP at 1/2/4/8 MI355X; epoch time"
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=30)
+    ap.add_argument("--warmup", type=int, default=8)
+    ap.add_argument("--global-batch", type=int, default=1024)
+    ap.add_argument("--arch", default="resnet50")
+    ap.add_argument("--optimizer", default="madgrad")
+    ap.add_argument("--ngd", action="store_true")
+    ap.add_argument("--meta_learning", action="store_true")
+    ap.add_argument("--fsdp", action="store_true")
+    ap.add_argument("--precision", default="bf16")
+    ap.add_argument("--bucket-mb", type=float, default=8.0)
+    ap.add_argument("--comm-dtype", default="fp32")
+    ap.add_argument("--no-native", action="store_true", help="ablation: plain PyTorch ops (w/o tricks)")
+    ap.add_argument("--profile-steps", type=int, default=0)
+    return ap.parse_args()
+
+
+def main():
+    args = parse()
+    if args.no_native:
+        os.environ["FDT_NATIVE"] = "0"
+    import torch
+    import torch.distributed as dist
+
+    from faster_distributed_training_amd.train.resnet_trainer import ResNetConfig, ResNetTrainer
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if args.gpus != world and world > 1:
+        print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+    n = world
+    gb = args.global_batch
+    assert gb % n == 0, "global batch must divide evenly over ranks"
+    cfg = ResNetConfig(arch=args.arch, bs=gb // n, synthetic=True, eval=False, plot=False,
+                       distributed=n > 1, ngd=args.ngd, meta_learning=args.meta_learning,
+                       optimizer="ngd" if args.ngd else args.optimizer, fsdp=args.fsdp,
+                       precision=args.precision, bucket_mb=args.bucket_mb, comm_dtype=args.comm_dtype,
+                       fast_path=False if args.no_native else None)
+    tr = ResNetTrainer(cfg)
+    dev = tr.device
+    cuda = dev.type == "cuda"
+
+    def batches():
+        while True:
+            for b in tr.train_loader:
+                yield b
+
+    it = batches()
+    tr.model.train()
+
+    def sync():
+        if cuda:
+            torch.cuda.synchronize()
+        if dist.is_initialized():
+            from faster_distributed_training_amd.parallel.dist import barrier
+            barrier()
+            if cuda:
+                torch.cuda.synchronize()
+
+    for _ in range(args.warmup):
+        x, y = next(it)
+        tr.train_step(x, y)
+    sync()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        x, y = next(it)
+        tr.train_step(x, y)
+    sync()
+    elapsed = time.perf_counter() - t0
+    if dist.is_initialized():
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev if cuda else "cpu")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    ms = elapsed / args.steps * 1e3
+    value = gb * args.steps / elapsed
+    native = (os.environ.get("FDT_NATIVE", "1") != "0") and cuda
+    rec = {
+        "metric": METRIC,
+        "value": round(value, 2),
+        "unit": "images/sec",
+        "n_gpus": n,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms, 3),
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": round(value / BASELINE_IMG_S, 2),
+        "dtype": args.precision,
+        "data": "synthetic (CIFAR-10-shaped uint8, GPU augmentation), random-init weights",
+        "config": {"model": f"{args.arch} (CIFAR stem, 10 classes)", "global_batch": gb, "seq_len": None,
+                   "image_size": 32, "parallelism": f"{'fsdp' if args.fsdp else 'dp'}{n}",
+                   "optimizer": "ngd" if args.ngd else args.optimizer, "mixup": "meta" if args.meta_learning else "input",
+                   "native_kernels": native},
+        "epoch_time_s": round(50000.0 / value, 3),
+        "peak_mem_gb": round(torch.cuda.max_memory_allocated() / 2**30, 2) if cuda else None,
+    }
+    if tr.rank == 0:
+        print(json.dumps(rec), flush=True)
+    if dist.is_initialized():
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,70 @@
+// Host-side launcher prototypes of every HIP kernel in csrc/kernels/*.hip.
+// All pointers are device addresses passed as uint64_t (tensor.data_ptr()), `stream`
+// is the raw hipStream_t of the current torch stream; launchers are asynchronous,
+// allocation-free and graph-capture safe.
+#pragma once
+#include <cstdint>
+
+namespace fdt {
+// bn_kernels.hip
+void act_affine_fwd(uint64_t x, uint64_t s, uint64_t t, uint64_t out, long M, int C, int act, float alpha, int dt_in,
+                    int dt_out, uint64_t stream);
+int stats_num_blocks(long M, int C);
+void channel_stats_partial(uint64_t y, uint64_t part, long M, int C, int dt, uint64_t stream);
+void stats_finalize(uint64_t part, int nb, int C, double count, int mode, float eps, float momentum, uint64_t gamma,
+                    uint64_t beta, uint64_t run_mean, uint64_t run_var, uint64_t nbt, uint64_t out_s, uint64_t out_t,
+                    uint64_t save_mean, uint64_t save_aux, uint64_t stream);
+void act_bwd_reduce(uint64_t g, uint64_t x, uint64_t s, uint64_t t, uint64_t gx, uint64_t part, long M, int C, int act,
+                    float alpha, int dt, uint64_t stream);
+void reduce_partials(uint64_t part, int nb, int nq, int C, uint64_t out, uint64_t stream);
+void stats_bwd_coef(uint64_t gs, uint64_t gt, int C, double count, int mode, float eps, uint64_t save_mean,
+                    uint64_t save_aux, uint64_t gamma, uint64_t alpha, uint64_t beta, uint64_t ggamma, uint64_t gbeta,
+                    uint64_t stream);
+void affine_fold(uint64_t gy, uint64_t y, uint64_t alpha, uint64_t beta, uint64_t out, long M, int C, int dt,
+                 uint64_t stream);
+void residual_act_fwd(uint64_t ya, uint64_t sa, uint64_t ta, uint64_t yb, uint64_t sb, uint64_t tb, uint64_t xid,
+                      uint64_t out, long M, int C, int act, float alpha, int dt, uint64_t stream);
+void residual_act_bwd(uint64_t g, uint64_t out, uint64_t ya, uint64_t sa, uint64_t yb, uint64_t sb, uint64_t gya,
+                      uint64_t gyb, uint64_t part, long M, int C, int act, float alpha, int dt, uint64_t stream);
+// optim.hip
+void grad_sumsq(uint64_t g, long n, uint64_t inv_scale, int unscale, uint64_t part, int nb, uint64_t found_inf,
+                uint64_t stream);
+void grad_norm_finalize(uint64_t part, int nb, float max_norm, uint64_t out, uint64_t stream);
+void sgd_step(uint64_t p, uint64_t g, uint64_t buf, uint64_t shadow, long n, float lr, float momentum, float dampening,
+              float wd, int nesterov, int first, uint64_t gsc, uint64_t found_inf, int zero_grad, uint64_t stream);
+void madgrad_step(uint64_t p, uint64_t g, uint64_t gss, uint64_t s, uint64_t x0, uint64_t shadow, long n, float lr,
+                  float momentum, float wd, float eps, int decouple, long k, uint64_t gsc, uint64_t found_inf,
+                  int zero_grad, uint64_t stream);
+void mirror_madgrad_step(uint64_t p, uint64_t g, uint64_t gss, uint64_t z, uint64_t shadow, long n, float lr,
+                         float momentum, float wd, float eps, int decouple, long k, uint64_t gsc, uint64_t found_inf,
+                         int zero_grad, uint64_t stream);
+void adam_step(uint64_t p, uint64_t g, uint64_t m, uint64_t v, uint64_t shadow, long n, float lr, float b1, float b2,
+               float eps, float wd, int adamw, long step, uint64_t gsc, uint64_t found_inf, int zero_grad,
+               uint64_t stream);
+void cast_bf16(uint64_t x, uint64_t y, long n, uint64_t stream);
+// mixup.hip
+void mixup_fwd(uint64_t x, uint64_t perm, uint64_t lam, uint64_t out, int b, long inner, int dt, uint64_t stream);
+void mixup_bwd(uint64_t g, uint64_t x, uint64_t perm, uint64_t inv, uint64_t lam, uint64_t gx, uint64_t dlam, int b,
+               long inner, int dt, uint64_t stream);
+void mixup_ce_fwd(uint64_t logits, uint64_t ya, uint64_t yb, uint64_t lam, uint64_t loss, uint64_t glog, uint64_t dlam,
+                  int B, int C, int dt, uint64_t stream);
+// layernorm.hip
+void layernorm_fwd(uint64_t x, uint64_t a, uint64_t b, uint64_t y, uint64_t mean, uint64_t rstd, long rows, int d,
+                   float eps, int dt_x, int dt_y, int dt_w, uint64_t stream);
+void layernorm_bwd(uint64_t gy, uint64_t x, uint64_t a, uint64_t mean, uint64_t rstd, uint64_t gx, uint64_t part,
+                   long rows, int d, int nblk, int dt_g, int dt_x, int dt_w, float eps, uint64_t stream);
+// embedding.hip
+void embedding_fwd(uint64_t ids, uint64_t types, uint64_t pos_ids, uint64_t tok, uint64_t pos, uint64_t seg,
+                   uint64_t out, int B, int L, int d, float scale, int vt, int vp, int vs, uint64_t stream);
+void embedding_bwd(uint64_t g, uint64_t ids, uint64_t types, uint64_t pos_ids, uint64_t gt, uint64_t gp, uint64_t gs,
+                   int B, int L, int d, float scale, int vt, int vp, int vs, uint64_t stream);
+// mlp.hip
+void bias_relu_fwd(uint64_t pre, uint64_t b, uint64_t act, long rows, int cols, int dt, uint64_t stream);
+void relu_bwd_colsum(uint64_t gact, uint64_t pre, uint64_t gpre, uint64_t gb, long rows, int cols, int dt,
+                     uint64_t stream);
+// augment.hip
+void augment(uint64_t src, uint64_t idx, uint64_t labels_src, uint64_t labels_out, uint64_t out, int B, int H, int W,
+             int C, int Cout, int pad, int do_flip, uint64_t rng, float m0, float m1, float m2, float s0, float s1,
+             float s2, int nchw, int dt_out, uint64_t stream);
+void rng_advance(uint64_t rng, uint64_t stream);
+}  // namespace fdt

@@ -1,0 +1,558 @@
+// Per-channel normalisation kernels for the NHWC ResNet engine (ops/resnet_engine.py).
+//
+// A conv output y[M][C] (M = N*H*W, NHWC, bf16) is never normalised in place: the
+// engine keeps it raw and carries a per-channel affine (s[c], t[c]) that the CONSUMER
+// applies while loading (a = act(y*s + t)).  These kernels provide
+//   * batch statistics: per-block partial (sum, sumsq) slabs + an fp64 finalize that
+//     produces (s, t) for FusedConvBN numerics (unbiased var, 1/(sqrt(var)+eps);
+//     reference resnet.py:75-100) or BatchNorm2d numerics (biased var, affine, running
+//     stats update with the unbiased var);
+//   * the backward of that map: the consumer's act backward + per-channel reductions
+//     (sum g_pre*x, sum g_pre), the producer's coefficient kernel turning (g_s, g_t)
+//     into an affine correction g_y += alpha + beta*y, and its apply pass;
+//   * the residual join  out = act(y_a*s_a + t_a + [y_b*s_b + t_b | x])  fwd/bwd.
+// Partial slabs (not float atomics) keep the reductions deterministic and avoid
+// contention on the C channel addresses (MI355X_MICROARCH: one-row contention is 14x
+// slower).  All kernels stream 16 B per lane.
+#include "common.h"
+
+namespace fdt {
+
+constexpr int kBlk = 256;
+
+// Channel-group geometry for [M][C] with 8 channels per thread.
+struct ChanGeom {
+  int G;    // channel groups (C / 8)
+  int TPR;  // threads per row
+  int RPP;  // rows per pass (kBlk / TPR)
+  int gy;   // grid.y (channel-group tiles)
+};
+inline ChanGeom chan_geom(int C) {
+  FDT_CHECK(C % 8 == 0, "channel count must be a multiple of 8");
+  ChanGeom g;
+  g.G = C / 8;
+  g.TPR = g.G < kBlk ? g.G : kBlk;
+  FDT_CHECK((g.G <= kBlk && kBlk % g.G == 0) || (g.G % kBlk == 0),
+            "C/8 must divide 256 or be a multiple of 256");
+  g.RPP = kBlk / g.TPR;
+  g.gy = g.G / g.TPR;
+  return g;
+}
+
+// 8 consecutive per-channel fp32 parameters (c multiple of 8 -> two 16-B loads)
+__device__ __forceinline__ void load8f(const float* __restrict__ p, int c, float* v) {
+  float4 a = *reinterpret_cast<const float4*>(p + c), b = *reinterpret_cast<const float4*>(p + c + 4);
+  v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+}
+
+// ------------------------------------------------------------------ act(x*s+t)
+template <typename T, typename TO>
+__global__ __launch_bounds__(kBlk) void act_affine_fwd_kernel(const T* __restrict__ x, const float* __restrict__ s,
+                                                              const float* __restrict__ t, TO* __restrict__ out,
+                                                              long nvec, int C, int act, float alpha) {
+  long stride = (long)gridDim.x * blockDim.x;
+  for (long v = (long)blockIdx.x * blockDim.x + threadIdx.x; v < nvec; v += stride) {
+    long e = v * 8;
+    int c = (int)(e % C);
+    float a[8];
+    Vec8<T>::load(x + e, a);
+    if (s != nullptr) {
+      float4 s0 = *reinterpret_cast<const float4*>(s + c), s1 = *reinterpret_cast<const float4*>(s + c + 4);
+      float4 t0 = *reinterpret_cast<const float4*>(t + c), t1 = *reinterpret_cast<const float4*>(t + c + 4);
+      float sv[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
+      float tv[8] = {t0.x, t0.y, t0.z, t0.w, t1.x, t1.y, t1.z, t1.w};
+#pragma unroll
+      for (int i = 0; i < 8; ++i) a[i] = fmaf(a[i], sv[i], tv[i]);
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) a[i] = act_fwd(a[i], act, alpha);
+    Vec8<TO>::store(out + e, a);
+  }
+}
+
+// ------------------------------------------------------------------ stats partials
+// part[blk][q][C], q = 0: sum y, q = 1: sum y^2
+template <typename T>
+__global__ __launch_bounds__(kBlk) void channel_stats_partial_kernel(const T* __restrict__ y, float* __restrict__ part,
+                                                                     long M, int C, int TPR, int RPP, long rows_per_blk) {
+  __shared__ float sm[kBlk * 16];
+  const int tid = threadIdx.x;
+  const int gi = tid % TPR, rr = tid / TPR;
+  const int c0 = (blockIdx.y * TPR + gi) * 8;
+  const long r_begin = (long)blockIdx.x * rows_per_blk;
+  long r_end = r_begin + rows_per_blk;
+  if (r_end > M) r_end = M;
+  float s1[8] = {0, 0, 0, 0, 0, 0, 0, 0}, s2[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  for (long r = r_begin + rr; r < r_end; r += RPP) {
+    float v[8];
+    Vec8<T>::load(y + r * C + c0, v);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) { s1[i] += v[i]; s2[i] = fmaf(v[i], v[i], s2[i]); }
+  }
+#pragma unroll
+  for (int i = 0; i < 8; ++i) { sm[tid * 16 + i] = s1[i]; sm[tid * 16 + 8 + i] = s2[i]; }
+  __syncthreads();
+  // reduce over rr for each (gi, i): thread j handles j < TPR*16
+  for (int j = tid; j < TPR * 16; j += kBlk) {
+    int g = j / 16, i = j % 16;
+    float acc = 0.f;
+    for (int q = 0; q < RPP; ++q) acc += sm[(q * TPR + g) * 16 + i];
+    int c = (blockIdx.y * TPR + g) * 8 + (i & 7);
+    part[((long)blockIdx.x * 2 + (i >> 3)) * C + c] = acc;
+  }
+}
+
+// Sum nq partial rows over nb blocks in fp64: acc[q] = sum_{b = w, w+nw, ...} part[b][q][c]
+// (4-way unrolled so the independent loads are in flight together)
+template <int NQ>
+__device__ __forceinline__ void sum_partials_f64(const float* __restrict__ part, int nb, int C, int c, double* acc,
+                                                 int w, int nw) {
+  double a0[NQ], a1[NQ];
+#pragma unroll
+  for (int q = 0; q < NQ; ++q) { a0[q] = 0.0; a1[q] = 0.0; }
+  int b = w;
+  for (; b + nw < nb; b += 2 * nw) {
+    float v0[NQ], v1[NQ];
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+      v0[q] = part[((long)b * NQ + q) * C + c];
+      v1[q] = part[((long)(b + nw) * NQ + q) * C + c];
+    }
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) { a0[q] += (double)v0[q]; a1[q] += (double)v1[q]; }
+  }
+  if (b < nb) {
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) a0[q] += (double)part[((long)b * NQ + q) * C + c];
+  }
+#pragma unroll
+  for (int q = 0; q < NQ; ++q) acc[q] = a0[q] + a1[q];
+}
+
+constexpr int kRedWaves = 16;  // finalize / reduce kernels: 1024 threads per 64-channel tile
+
+// mode 0: FusedConvBN (unbiased var, s = 1/(sqrt(var)+eps), no affine)
+// mode 1: BatchNorm2d train (biased var + eps, affine gamma/beta, running stats update)
+// mode 2: BatchNorm2d eval  (running stats, affine)  -- part unused
+// save_mean[c], save_aux[c]: mode 0 -> sd ; modes 1/2 -> invstd
+__global__ __launch_bounds__(64 * kRedWaves) void stats_finalize_kernel(const float* __restrict__ part, int nb, int C, double count,
+                                                              int mode, float eps, float momentum,
+                                                              const float* __restrict__ gamma, const float* __restrict__ beta,
+                                                              float* __restrict__ run_mean, float* __restrict__ run_var,
+                                                              long long* __restrict__ nbt, float* __restrict__ out_s,
+                                                              float* __restrict__ out_t, float* __restrict__ save_mean,
+                                                              float* __restrict__ save_aux) {
+  __shared__ double sm[kRedWaves][64][2];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + lane;
+  double acc[2] = {0.0, 0.0};
+  if (c < C && mode != 2) sum_partials_f64<2>(part, nb, C, c, acc, w, kRedWaves);
+  sm[w][lane][0] = acc[0];
+  sm[w][lane][1] = acc[1];
+  __syncthreads();
+  if (w != 0 || c >= C) return;
+  double S = 0.0, Q = 0.0;
+#pragma unroll
+  for (int k = 0; k < kRedWaves; ++k) { S += sm[k][lane][0]; Q += sm[k][lane][1]; }
+  if (mode == 0) {
+    double mean = S / count;
+    double var = (Q - S * mean) / (count - 1.0);
+    if (var < 0.0) var = 0.0;
+    double sd = sqrt(var);
+    double sc = 1.0 / (sd + (double)eps);
+    out_s[c] = (float)sc;
+    out_t[c] = (float)(-mean * sc);
+    save_mean[c] = (float)mean;
+    save_aux[c] = (float)sd;
+  } else if (mode == 1) {
+    double mean = S / count;
+    double m2 = Q - S * mean;
+    if (m2 < 0.0) m2 = 0.0;
+    double var_b = m2 / count;
+    double var_u = count > 1.0 ? m2 / (count - 1.0) : var_b;
+    double inv = 1.0 / sqrt(var_b + (double)eps);
+    double g = gamma ? (double)gamma[c] : 1.0, b = beta ? (double)beta[c] : 0.0;
+    out_s[c] = (float)(g * inv);
+    out_t[c] = (float)(b - mean * g * inv);
+    save_mean[c] = (float)mean;
+    save_aux[c] = (float)inv;
+    if (run_mean) {
+      run_mean[c] = (float)((1.0 - momentum) * run_mean[c] + momentum * mean);
+      run_var[c] = (float)((1.0 - momentum) * run_var[c] + momentum * var_u);
+    }
+    if (nbt && c == 0) nbt[0] += 1;
+  } else {
+    double mean = run_mean[c];
+    double inv = 1.0 / sqrt((double)run_var[c] + (double)eps);
+    double g = gamma ? (double)gamma[c] : 1.0, b = beta ? (double)beta[c] : 0.0;
+    out_s[c] = (float)(g * inv);
+    out_t[c] = (float)(b - mean * g * inv);
+    save_mean[c] = (float)mean;
+    save_aux[c] = (float)inv;
+  }
+}
+
+// ------------------------------------------------------------------ consumer backward
+// Input transform a = act(x*s + t).  Given g = dL/da:
+//   g_pre = g * act'(x*s+t);  gx = g_pre * s;  part = [sum g_pre*x, sum g_pre]
+template <typename T>
+__global__ __launch_bounds__(kBlk) void act_bwd_reduce_kernel(const T* __restrict__ g, const T* __restrict__ x,
+                                                              const float* __restrict__ s, const float* __restrict__ t,
+                                                              T* __restrict__ gx, float* __restrict__ part, long M, int C,
+                                                              int TPR, int RPP, long rows_per_blk, int act, float alpha) {
+  __shared__ float sm[kBlk * 16];
+  const int tid = threadIdx.x;
+  const int gi = tid % TPR, rr = tid / TPR;
+  const int c0 = (blockIdx.y * TPR + gi) * 8;
+  float sv[8], tv[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) { sv[i] = s[c0 + i]; tv[i] = t[c0 + i]; }
+  const long r_begin = (long)blockIdx.x * rows_per_blk;
+  long r_end = r_begin + rows_per_blk;
+  if (r_end > M) r_end = M;
+  float a1[8] = {0, 0, 0, 0, 0, 0, 0, 0}, a0[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  for (long r = r_begin + rr; r < r_end; r += RPP) {
+    float gv[8], xv[8], o[8];
+    Vec8<T>::load(g + r * C + c0, gv);
+    Vec8<T>::load(x + r * C + c0, xv);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      float z = fmaf(xv[i], sv[i], tv[i]);
+      float gp = gv[i] * act_grad(z, act, alpha);
+      o[i] = gp * sv[i];
+      a1[i] = fmaf(gp, xv[i], a1[i]);
+      a0[i] += gp;
+    }
+    Vec8<T>::store(gx + r * C + c0, o);
+  }
+#pragma unroll
+  for (int i = 0; i < 8; ++i) { sm[tid * 16 + i] = a1[i]; sm[tid * 16 + 8 + i] = a0[i]; }
+  __syncthreads();
+  for (int j = tid; j < TPR * 16; j += kBlk) {
+    int gg = j / 16, i = j % 16;
+    float acc = 0.f;
+    for (int q = 0; q < RPP; ++q) acc += sm[(q * TPR + gg) * 16 + i];
+    int c = (blockIdx.y * TPR + gg) * 8 + (i & 7);
+    part[((long)blockIdx.x * 2 + (i >> 3)) * C + c] = acc;
+  }
+}
+
+// generic fp64 reduction of partial slabs: out[q][c] = sum_b part[b][q][c]
+template <int NQ>
+__global__ __launch_bounds__(64 * kRedWaves) void reduce_partials_kernel(const float* __restrict__ part, int nb, int C,
+                                                                         float* __restrict__ out) {
+  __shared__ double sm[kRedWaves][64][NQ];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + lane;
+  double acc[NQ];
+#pragma unroll
+  for (int q = 0; q < NQ; ++q) acc[q] = 0.0;
+  if (c < C) sum_partials_f64<NQ>(part, nb, C, c, acc, w, kRedWaves);
+#pragma unroll
+  for (int q = 0; q < NQ; ++q) sm[w][lane][q] = acc[q];
+  __syncthreads();
+  if (w != 0 || c >= C) return;
+#pragma unroll
+  for (int q = 0; q < NQ; ++q) {
+    double t = 0.0;
+#pragma unroll
+    for (int k = 0; k < kRedWaves; ++k) t += sm[k][lane][q];
+    out[(long)q * C + c] = (float)t;
+  }
+}
+
+// ------------------------------------------------------------------ producer backward
+// (g_s, g_t) -> affine correction of dL/dy:  g_y += alpha + beta * y
+// mode 0 (FusedConvBN): s = 1/(sd+eps), t = -mean*s
+//    beta = -(g_s - mean g_t) s^2 / ((N-1) sd),   alpha = -beta*mean - g_t s / N
+// mode 1 (BatchNorm2d): s = gamma*inv, t = b - mean*s, inv = (var_b+eps)^-1/2
+//    beta = -(g_s - mean g_t) gamma inv^3 / N,    alpha = -beta*mean - g_t s / N
+//    g_gamma = (g_s - mean g_t) inv,  g_beta = g_t
+// mode 2 (BatchNorm2d eval, running stats): beta = alpha = 0, g_gamma/g_beta as above
+__global__ void stats_bwd_coef_kernel(const float* __restrict__ gs, const float* __restrict__ gt, int C, double count,
+                                      int mode, float eps, const float* __restrict__ save_mean,
+                                      const float* __restrict__ save_aux, const float* __restrict__ gamma,
+                                      float* __restrict__ alpha, float* __restrict__ beta, float* __restrict__ ggamma,
+                                      float* __restrict__ gbeta) {
+  int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  double g_s = gs ? gs[c] : 0.0, g_t = gt ? gt[c] : 0.0;
+  double mean = save_mean[c], aux = save_aux[c];
+  if (mode == 0) {
+    double sd = aux;
+    double s = 1.0 / (sd + (double)eps);
+    double b = sd > 0.0 ? -(g_s - mean * g_t) * s * s / ((count - 1.0) * sd) : 0.0;
+    beta[c] = (float)b;
+    alpha[c] = (float)(-b * mean - g_t * s / count);
+  } else {
+    double inv = aux;
+    double g = gamma ? (double)gamma[c] : 1.0;
+    double s = g * inv;
+    if (mode == 1) {
+      double b = -(g_s - mean * g_t) * g * inv * inv * inv / count;
+      beta[c] = (float)b;
+      alpha[c] = (float)(-b * mean - g_t * s / count);
+    } else {
+      beta[c] = 0.f;
+      alpha[c] = 0.f;
+    }
+    if (ggamma) ggamma[c] = (float)((g_s - mean * g_t) * inv);
+    if (gbeta) gbeta[c] = (float)g_t;
+  }
+}
+
+// out = g_y + alpha[c] + beta[c] * y   (g_y may alias out)
+template <typename T>
+__global__ __launch_bounds__(kBlk) void affine_fold_kernel(const T* __restrict__ gy, const T* __restrict__ y,
+                                                           const float* __restrict__ alpha, const float* __restrict__ beta,
+                                                           T* __restrict__ out, long nvec, int C) {
+  long stride = (long)gridDim.x * blockDim.x;
+  for (long v = (long)blockIdx.x * blockDim.x + threadIdx.x; v < nvec; v += stride) {
+    long e = v * 8;
+    int c = (int)(e % C);
+    float gv[8], yv[8];
+    if (gy) Vec8<T>::load(gy + e, gv);
+    else {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) gv[i] = 0.f;
+    }
+    Vec8<T>::load(y + e, yv);
+    float av[8], bv[8];
+    load8f(alpha, c, av);
+    load8f(beta, c, bv);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) gv[i] += fmaf(bv[i], yv[i], av[i]);
+    Vec8<T>::store(out + e, gv);
+  }
+}
+
+// ------------------------------------------------------------------ residual join
+// out = act(ya*sa + ta + (yb ? yb*sb + tb : xid))
+template <typename T>
+__global__ __launch_bounds__(kBlk) void residual_act_fwd_kernel(const T* __restrict__ ya, const float* __restrict__ sa,
+                                                                const float* __restrict__ ta, const T* __restrict__ yb,
+                                                                const float* __restrict__ sb, const float* __restrict__ tb,
+                                                                const T* __restrict__ xid, T* __restrict__ out, long nvec,
+                                                                int C, int act, float alpha) {
+  long stride = (long)gridDim.x * blockDim.x;
+  for (long v = (long)blockIdx.x * blockDim.x + threadIdx.x; v < nvec; v += stride) {
+    long e = v * 8;
+    int c = (int)(e % C);
+    float a[8], b[8], s8[8], t8[8];
+    Vec8<T>::load(ya + e, a);
+    if (yb) {
+      Vec8<T>::load(yb + e, b);
+      load8f(sb, c, s8);
+      load8f(tb, c, t8);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) b[i] = fmaf(b[i], s8[i], t8[i]);
+    } else {
+      Vec8<T>::load(xid + e, b);
+    }
+    load8f(sa, c, s8);
+    load8f(ta, c, t8);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) a[i] = act_fwd(fmaf(a[i], s8[i], t8[i]) + b[i], act, alpha);
+    Vec8<T>::store(out + e, a);
+  }
+}
+
+// act'(z) from the activation OUTPUT o (ReLU: o>0; CELU: o>0 ? 1 : o/alpha + 1)
+__device__ __forceinline__ float act_grad_from_out(float o, int act, float alpha) {
+  if (act == kActRelu) return o > 0.f ? 1.f : 0.f;
+  if (act == kActCelu) return o > 0.f ? 1.f : o / alpha + 1.f;
+  return 1.f;
+}
+
+// g_pre = g * act'(out); gya = g_pre*sa; gyb = g_pre*sb (or g_pre if identity branch)
+// part[blk][3][C] = [sum g_pre*ya, sum g_pre, sum g_pre*yb]
+template <typename T>
+__global__ __launch_bounds__(kBlk) void residual_act_bwd_kernel(const T* __restrict__ g, const T* __restrict__ out,
+                                                                const T* __restrict__ ya, const float* __restrict__ sa,
+                                                                const T* __restrict__ yb, const float* __restrict__ sb,
+                                                                T* __restrict__ gya, T* __restrict__ gyb,
+                                                                float* __restrict__ part, long M, int C, int TPR, int RPP,
+                                                                long rows_per_blk, int act, float alpha) {
+  __shared__ float sm[kBlk * 24];
+  const int tid = threadIdx.x;
+  const int gi = tid % TPR, rr = tid / TPR;
+  const int c0 = (blockIdx.y * TPR + gi) * 8;
+  float sav[8], sbv[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) { sav[i] = sa[c0 + i]; sbv[i] = yb ? sb[c0 + i] : 1.f; }
+  const long r_begin = (long)blockIdx.x * rows_per_blk;
+  long r_end = r_begin + rows_per_blk;
+  if (r_end > M) r_end = M;
+  float p0[8] = {0, 0, 0, 0, 0, 0, 0, 0}, p1[8] = {0, 0, 0, 0, 0, 0, 0, 0}, p2[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  for (long r = r_begin + rr; r < r_end; r += RPP) {
+    const long e = r * C + c0;
+    float gv[8], ov[8], av[8], bv[8], oa[8], ob[8];
+    Vec8<T>::load(g + e, gv);
+    Vec8<T>::load(out + e, ov);
+    Vec8<T>::load(ya + e, av);
+    if (yb) Vec8<T>::load(yb + e, bv);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      float gp = gv[i] * act_grad_from_out(ov[i], act, alpha);
+      oa[i] = gp * sav[i];
+      ob[i] = gp * sbv[i];
+      p0[i] = fmaf(gp, av[i], p0[i]);
+      p1[i] += gp;
+      if (yb) p2[i] = fmaf(gp, bv[i], p2[i]);
+    }
+    Vec8<T>::store(gya + e, oa);
+    Vec8<T>::store(gyb + e, ob);
+  }
+#pragma unroll
+  for (int i = 0; i < 8; ++i) { sm[tid * 24 + i] = p0[i]; sm[tid * 24 + 8 + i] = p1[i]; sm[tid * 24 + 16 + i] = p2[i]; }
+  __syncthreads();
+  for (int j = tid; j < TPR * 24; j += kBlk) {
+    int gg = j / 24, i = j % 24;
+    float acc = 0.f;
+    for (int q = 0; q < RPP; ++q) acc += sm[(q * TPR + gg) * 24 + i];
+    int c = (blockIdx.y * TPR + gg) * 8 + (i & 7);
+    part[((long)blockIdx.x * 3 + (i >> 3)) * C + c] = acc;
+  }
+}
+
+// ------------------------------------------------------------------ launchers
+inline int ew_grid(long nvec) {
+  long g = (nvec + kBlk - 1) / kBlk;
+  if (g > 2048) g = 2048;  // grid-stride beyond ~8 blocks/CU
+  if (g < 1) g = 1;
+  return (int)g;
+}
+
+// rows per block so that the grid holds ~1024-4096 blocks of >= RPP rows
+inline long rows_per_block(long M, const ChanGeom& g) {
+  // ~512 partial rows per channel: enough blocks to fill 256 CUs (x gy channel tiles)
+  // while keeping the fp64 finalize short
+  long target_blocks = 512 / (g.gy > 0 ? g.gy : 1);
+  if (target_blocks < 128) target_blocks = 128;
+  long r = (M + target_blocks - 1) / target_blocks;
+  if (r < g.RPP) r = g.RPP;
+  r = (r + g.RPP - 1) / g.RPP * g.RPP;
+  return r;
+}
+
+int stats_num_blocks(long M, int C) {
+  ChanGeom g = chan_geom(C);
+  long r = rows_per_block(M, g);
+  return (int)((M + r - 1) / r);
+}
+
+#define DISPATCH_T(dt, ...)                                     \
+  switch (dt) {                                                 \
+    case kF32: { using T = float; __VA_ARGS__; break; }         \
+    case kBF16: { using T = bf16; __VA_ARGS__; break; }         \
+    case kF16: { using T = f16; __VA_ARGS__; break; }           \
+    default: throw std::runtime_error("bad dtype code");        \
+  }
+
+void act_affine_fwd(uint64_t x, uint64_t s, uint64_t t, uint64_t out, long M, int C, int act, float alpha, int dt_in,
+                    int dt_out, uint64_t stream) {
+  FDT_CHECK(C % 8 == 0, "C % 8");
+  long nvec = M * (long)C / 8;
+  if (nvec == 0) return;
+  DISPATCH_T(dt_in, {
+    using TI = T;
+    DISPATCH_T(dt_out, {
+      act_affine_fwd_kernel<TI, T><<<ew_grid(nvec), kBlk, 0, as_stream(stream)>>>(
+          P<const TI>(x), P<const float>(s), P<const float>(t), P<T>(out), nvec, C, act, alpha);
+    });
+  });
+  FDT_LAUNCH_CHECK();
+}
+
+void channel_stats_partial(uint64_t y, uint64_t part, long M, int C, int dt, uint64_t stream) {
+  ChanGeom g = chan_geom(C);
+  long r = rows_per_block(M, g);
+  dim3 grid((unsigned)((M + r - 1) / r), g.gy);
+  DISPATCH_T(dt, {
+    channel_stats_partial_kernel<T><<<grid, kBlk, 0, as_stream(stream)>>>(P<const T>(y), P<float>(part), M, C, g.TPR,
+                                                                         g.RPP, r);
+  });
+  FDT_LAUNCH_CHECK();
+}
+
+void stats_finalize(uint64_t part, int nb, int C, double count, int mode, float eps, float momentum, uint64_t gamma,
+                    uint64_t beta, uint64_t run_mean, uint64_t run_var, uint64_t nbt, uint64_t out_s, uint64_t out_t,
+                    uint64_t save_mean, uint64_t save_aux, uint64_t stream) {
+  stats_finalize_kernel<<<(C + 63) / 64, 64 * kRedWaves, 0, as_stream(stream)>>>(
+      P<const float>(part), nb, C, count, mode, eps, momentum, P<const float>(gamma), P<const float>(beta),
+      P<float>(run_mean), P<float>(run_var), P<long long>(nbt), P<float>(out_s), P<float>(out_t), P<float>(save_mean),
+      P<float>(save_aux));
+  FDT_LAUNCH_CHECK();
+}
+
+void act_bwd_reduce(uint64_t g, uint64_t x, uint64_t s, uint64_t t, uint64_t gx, uint64_t part, long M, int C, int act,
+                    float alpha, int dt, uint64_t stream) {
+  ChanGeom gg = chan_geom(C);
+  long r = rows_per_block(M, gg);
+  dim3 grid((unsigned)((M + r - 1) / r), gg.gy);
+  DISPATCH_T(dt, {
+    act_bwd_reduce_kernel<T><<<grid, kBlk, 0, as_stream(stream)>>>(P<const T>(g), P<const T>(x), P<const float>(s),
+                                                                  P<const float>(t), P<T>(gx), P<float>(part), M, C,
+                                                                  gg.TPR, gg.RPP, r, act, alpha);
+  });
+  FDT_LAUNCH_CHECK();
+}
+
+void reduce_partials(uint64_t part, int nb, int nq, int C, uint64_t out, uint64_t stream) {
+  const dim3 grid((C + 63) / 64);
+  switch (nq) {
+    case 1: reduce_partials_kernel<1><<<grid, 64 * kRedWaves, 0, as_stream(stream)>>>(P<const float>(part), nb, C, P<float>(out)); break;
+    case 2: reduce_partials_kernel<2><<<grid, 64 * kRedWaves, 0, as_stream(stream)>>>(P<const float>(part), nb, C, P<float>(out)); break;
+    case 3: reduce_partials_kernel<3><<<grid, 64 * kRedWaves, 0, as_stream(stream)>>>(P<const float>(part), nb, C, P<float>(out)); break;
+    default: throw std::runtime_error("reduce_partials: nq in [1,3]");
+  }
+  FDT_LAUNCH_CHECK();
+}
+
+void stats_bwd_coef(uint64_t gs, uint64_t gt, int C, double count, int mode, float eps, uint64_t save_mean,
+                    uint64_t save_aux, uint64_t gamma, uint64_t alpha, uint64_t beta, uint64_t ggamma, uint64_t gbeta,
+                    uint64_t stream) {
+  stats_bwd_coef_kernel<<<(C + 255) / 256, 256, 0, as_stream(stream)>>>(
+      P<const float>(gs), P<const float>(gt), C, count, mode, eps, P<const float>(save_mean), P<const float>(save_aux),
+      P<const float>(gamma), P<float>(alpha), P<float>(beta), P<float>(ggamma), P<float>(gbeta));
+  FDT_LAUNCH_CHECK();
+}
+
+void affine_fold(uint64_t gy, uint64_t y, uint64_t alpha, uint64_t beta, uint64_t out, long M, int C, int dt,
+                 uint64_t stream) {
+  long nvec = M * (long)C / 8;
+  if (nvec == 0) return;
+  DISPATCH_T(dt, {
+    affine_fold_kernel<T><<<ew_grid(nvec), kBlk, 0, as_stream(stream)>>>(
+        P<const T>(gy), P<const T>(y), P<const float>(alpha), P<const float>(beta), P<T>(out), nvec, C);
+  });
+  FDT_LAUNCH_CHECK();
+}
+
+void residual_act_fwd(uint64_t ya, uint64_t sa, uint64_t ta, uint64_t yb, uint64_t sb, uint64_t tb, uint64_t xid,
+                      uint64_t out, long M, int C, int act, float alpha, int dt, uint64_t stream) {
+  long nvec = M * (long)C / 8;
+  if (nvec == 0) return;
+  FDT_CHECK(yb != 0 || xid != 0, "residual needs a second branch");
+  DISPATCH_T(dt, {
+    residual_act_fwd_kernel<T><<<ew_grid(nvec), kBlk, 0, as_stream(stream)>>>(
+        P<const T>(ya), P<const float>(sa), P<const float>(ta), P<const T>(yb), P<const float>(sb), P<const float>(tb),
+        P<const T>(xid), P<T>(out), nvec, C, act, alpha);
+  });
+  FDT_LAUNCH_CHECK();
+}
+
+void residual_act_bwd(uint64_t g, uint64_t out, uint64_t ya, uint64_t sa, uint64_t yb, uint64_t sb, uint64_t gya,
+                      uint64_t gyb, uint64_t part, long M, int C, int act, float alpha, int dt, uint64_t stream) {
+  ChanGeom gg = chan_geom(C);
+  long r = rows_per_block(M, gg);
+  dim3 grid((unsigned)((M + r - 1) / r), gg.gy);
+  DISPATCH_T(dt, {
+    residual_act_bwd_kernel<T><<<grid, kBlk, 0, as_stream(stream)>>>(
+        P<const T>(g), P<const T>(out), P<const T>(ya), P<const float>(sa), P<const T>(yb), P<const float>(sb), P<T>(gya),
+        P<T>(gyb), P<float>(part), M, C, gg.TPR, gg.RPP, r, act, alpha);
+  });
+  FDT_LAUNCH_CHECK();
+}
+
+}  // namespace fdt

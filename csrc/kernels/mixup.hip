@@ -1,0 +1,145 @@
+// Mixup kernels (reference resnet50_test.py:355-457, transformer.py:71-80).
+//  * mixup_fwd:  out[i] = lam[i]*x[i] + (1-lam[i])*x[perm[i]]   (permuted gather + lerp)
+//  * mixup_bwd:  gx[i] = lam[i]*g[i] + (1-lam[inv[i]])*g[inv[i]]  (inverse-permutation
+//                gather: no atomics, deterministic); optional per-sample
+//                dlam[i] = sum_j g[i,j]*(x[i,j]-x[perm[i],j]) for the learnable meta-mixup.
+//  * mixup_ce_fwd: fused log-softmax cross entropy against two targets with per-sample
+//                lambda: loss, dlogits and dloss/dlam in one single-block kernel (the
+//                logits are tiny: B x 10 / B x 4), no host sync.
+#include "common.h"
+
+namespace fdt {
+
+template <typename T>
+__global__ __launch_bounds__(256) void mixup_fwd_kernel(const T* __restrict__ x, const int* __restrict__ perm,
+                                                        const float* __restrict__ lam, T* __restrict__ out, long inner) {
+  const int i = blockIdx.y;
+  const int j = perm[i];
+  const float l = lam[i];
+  const T* xi = x + (long)i * inner;
+  const T* xj = x + (long)j * inner;
+  T* o = out + (long)i * inner;
+  if (inner % 8 == 0) {
+    for (long v = (long)blockIdx.x * blockDim.x + threadIdx.x; v < inner / 8; v += (long)gridDim.x * blockDim.x) {
+      float a[8], b[8];
+      Vec8<T>::load(xi + v * 8, a);
+      Vec8<T>::load(xj + v * 8, b);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) a[k] = l * a[k] + (1.f - l) * b[k];
+      Vec8<T>::store(o + v * 8, a);
+    }
+  } else {
+    for (long e = (long)blockIdx.x * blockDim.x + threadIdx.x; e < inner; e += (long)gridDim.x * blockDim.x)
+      o[e] = from_f<T>(l * to_f(xi[e]) + (1.f - l) * to_f(xj[e]));
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void mixup_bwd_kernel(const T* __restrict__ g, const T* __restrict__ x,
+                                                        const int* __restrict__ perm, const int* __restrict__ inv,
+                                                        const float* __restrict__ lam, T* __restrict__ gx,
+                                                        float* __restrict__ dlam, long inner) {
+  __shared__ float sm[4];
+  const int i = blockIdx.x;
+  const int ii = inv[i], pj = perm[i];
+  const float li = lam[i], lk = 1.f - lam[ii];
+  const T* gi = g + (long)i * inner;
+  const T* gk = g + (long)ii * inner;
+  const T* xi = x + (long)i * inner;
+  const T* xp = x + (long)pj * inner;
+  T* o = gx + (long)i * inner;
+  float acc = 0.f;
+  for (long e = threadIdx.x; e < inner; e += blockDim.x) {
+    float gv = to_f(gi[e]);
+    o[e] = from_f<T>(li * gv + lk * to_f(gk[e]));
+    if (dlam) acc += gv * (to_f(xi[e]) - to_f(xp[e]));
+  }
+  if (dlam) {
+    acc = wave_sum(acc);
+    if ((threadIdx.x & 63) == 0) sm[threadIdx.x >> 6] = acc;
+    __syncthreads();
+    if (threadIdx.x == 0) dlam[i] = sm[0] + sm[1] + sm[2] + sm[3];
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(1024) void mixup_ce_kernel(const T* __restrict__ logits, const int* __restrict__ ya,
+                                                        const int* __restrict__ yb, const float* __restrict__ lam,
+                                                        float* __restrict__ loss, float* __restrict__ glog,
+                                                        float* __restrict__ dlam, int B, int C) {
+  __shared__ float sm[16];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  float tot = 0.f;
+  const float invB = 1.f / (float)B;
+  for (int r = w; r < B; r += nw) {
+    const T* row = logits + (long)r * C;
+    float mx = -INFINITY;
+    for (int c = lane; c < C; c += 64) mx = fmaxf(mx, to_f(row[c]));
+    mx = wave_max(mx);
+    float se = 0.f;
+    for (int c = lane; c < C; c += 64) se += __expf(to_f(row[c]) - mx);
+    se = wave_sum(se);
+    const float lse = mx + __logf(se);
+    const int a = ya[r], b = yb[r];
+    const float l = lam[r];
+    const float cea = lse - to_f(row[a]), ceb = lse - to_f(row[b]);
+    for (int c = lane; c < C; c += 64) {
+      float p = __expf(to_f(row[c]) - lse);
+      float t = (c == a ? l : 0.f) + (c == b ? 1.f - l : 0.f);
+      glog[(long)r * C + c] = (p - t) * invB;
+    }
+    if (lane == 0) {
+      tot += l * cea + (1.f - l) * ceb;
+      dlam[r] = (cea - ceb) * invB;
+    }
+  }
+  if (lane == 0) sm[w] = tot;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float t = 0.f;
+    for (int k = 0; k < nw; ++k) t += sm[k];
+    *loss = t * invB;
+  }
+}
+
+#define DISPATCH_T(dt, ...)                                     \
+  switch (dt) {                                                 \
+    case kF32: { using T = float; __VA_ARGS__; break; }         \
+    case kBF16: { using T = bf16; __VA_ARGS__; break; }         \
+    case kF16: { using T = f16; __VA_ARGS__; break; }           \
+    default: throw std::runtime_error("bad dtype code");        \
+  }
+
+void mixup_fwd(uint64_t x, uint64_t perm, uint64_t lam, uint64_t out, int b, long inner, int dt, uint64_t stream) {
+  long work = inner % 8 == 0 ? inner / 8 : inner;
+  int gx = (int)((work + 255) / 256);
+  if (gx > 64) gx = 64;
+  dim3 grid(gx, b);
+  DISPATCH_T(dt, {
+    mixup_fwd_kernel<T><<<grid, 256, 0, as_stream(stream)>>>(P<const T>(x), P<const int>(perm), P<const float>(lam),
+                                                            P<T>(out), inner);
+  });
+  FDT_LAUNCH_CHECK();
+}
+
+void mixup_bwd(uint64_t g, uint64_t x, uint64_t perm, uint64_t inv, uint64_t lam, uint64_t gx, uint64_t dlam, int b,
+               long inner, int dt, uint64_t stream) {
+  DISPATCH_T(dt, {
+    mixup_bwd_kernel<T><<<b, 256, 0, as_stream(stream)>>>(P<const T>(g), P<const T>(x), P<const int>(perm),
+                                                         P<const int>(inv), P<const float>(lam), P<T>(gx),
+                                                         P<float>(dlam), inner);
+  });
+  FDT_LAUNCH_CHECK();
+}
+
+void mixup_ce_fwd(uint64_t logits, uint64_t ya, uint64_t yb, uint64_t lam, uint64_t loss, uint64_t glog, uint64_t dlam,
+                  int B, int C, int dt, uint64_t stream) {
+  DISPATCH_T(dt, {
+    mixup_ce_kernel<T><<<1, 1024, 0, as_stream(stream)>>>(P<const T>(logits), P<const int>(ya), P<const int>(yb),
+                                                         P<const float>(lam), P<float>(loss), P<float>(glog),
+                                                         P<float>(dlam), B, C);
+  });
+  FDT_LAUNCH_CHECK();
+}
+
+}  // namespace fdt

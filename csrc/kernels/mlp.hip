@@ -1,0 +1,73 @@
+// FusedMLP elementwise stages (reference MLPScratch, transformer.py:292-338).
+//  bias_relu_fwd : pre += b (in place, kept for the mask); act = relu(pre)      one pass
+//  relu_bwd_colsum: gpre = gact * (pre > 0);  gb[c] += sum_rows gpre           one pass
+// The reference does the ReLU backward with a per-element Python loop and a host sync
+// per element (survey Q6); this is the whole of it in one launch.
+#include "common.h"
+
+namespace fdt {
+
+template <typename T>
+__global__ __launch_bounds__(256) void bias_relu_fwd_kernel(T* __restrict__ pre, const float* __restrict__ b,
+                                                            T* __restrict__ act, long n, int cols) {
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    float v = to_f(pre[i]);
+    if (b) {
+      v += b[i % cols];
+      pre[i] = from_f<T>(v);
+    }
+    act[i] = from_f<T>(fmaxf(v, 0.f));
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void relu_bwd_colsum_kernel(const T* __restrict__ gact, const T* __restrict__ pre,
+                                                              T* __restrict__ gpre, float* __restrict__ gb, long rows,
+                                                              int cols, int rows_per_blk) {
+  const long r0 = (long)blockIdx.y * rows_per_blk;
+  long r1 = r0 + rows_per_blk;
+  if (r1 > rows) r1 = rows;
+  for (int c = blockIdx.x * blockDim.x + threadIdx.x; c < cols; c += gridDim.x * blockDim.x) {
+    float acc = 0.f;
+    for (long r = r0; r < r1; ++r) {
+      long i = r * cols + c;
+      float g = to_f(pre[i]) > 0.f ? to_f(gact[i]) : 0.f;
+      gpre[i] = from_f<T>(g);
+      acc += g;
+    }
+    if (gb) atomicAdd(gb + c, acc);
+  }
+}
+
+#define DISPATCH_T(dt, ...)                                     \
+  switch (dt) {                                                 \
+    case kF32: { using T = float; __VA_ARGS__; break; }         \
+    case kBF16: { using T = bf16; __VA_ARGS__; break; }         \
+    case kF16: { using T = f16; __VA_ARGS__; break; }           \
+    default: throw std::runtime_error("bad dtype code");        \
+  }
+
+void bias_relu_fwd(uint64_t pre, uint64_t b, uint64_t act, long rows, int cols, int dt, uint64_t stream) {
+  long n = rows * cols;
+  if (n == 0) return;
+  int g = (int)((n + 255) / 256);
+  if (g > 2048) g = 2048;
+  DISPATCH_T(dt, {
+    bias_relu_fwd_kernel<T><<<g, 256, 0, as_stream(stream)>>>(P<T>(pre), P<const float>(b), P<T>(act), n, cols);
+  });
+  FDT_LAUNCH_CHECK();
+}
+
+void relu_bwd_colsum(uint64_t gact, uint64_t pre, uint64_t gpre, uint64_t gb, long rows, int cols, int dt,
+                     uint64_t stream) {
+  if (rows == 0) return;
+  const int rpb = 32;
+  dim3 grid((unsigned)((cols + 255) / 256), (unsigned)((rows + rpb - 1) / rpb));
+  DISPATCH_T(dt, {
+    relu_bwd_colsum_kernel<T><<<grid, 256, 0, as_stream(stream)>>>(P<const T>(gact), P<const T>(pre), P<T>(gpre),
+                                                                  P<float>(gb), rows, cols, rpb);
+  });
+  FDT_LAUNCH_CHECK();
+}
+
+}  // namespace fdt

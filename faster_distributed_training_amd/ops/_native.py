@@ -1,0 +1,77 @@
+"""Loader for the in-tree HIP extension ``_fdt_native`` (built by ``build_native.py``).
+
+Policy (MI355X-first, no silent fallbacks):
+
+* On a machine with a GPU, the fast path *requires* the extension: ``native()`` raises
+  if it is missing, so a GPU run never quietly degrades to eager PyTorch.
+* ``FDT_NATIVE=0`` disables the fast path explicitly (the "w/o tricks" ablation and the
+  CPU oracle path); that choice is visible in every benchmark line.
+* On CPU-only machines the pure-PyTorch reference implementations are used (they are
+  also the numerics oracle for the kernel tests).
+"""
+from __future__ import annotations
+
+import glob
+import importlib.util
+import os
+
+import torch
+
+_PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+_mod = None
+_err = None
+
+
+def _so_path():
+    cands = sorted(glob.glob(os.path.join(_PKG_DIR, "_fdt_native*.so")))
+    return cands[0] if cands else None
+
+
+def load():
+    """Import the extension (once).  Returns the module or None."""
+    global _mod, _err
+    if _mod is not None or _err is not None:
+        return _mod
+    path = _so_path()
+    if path is None:
+        _err = "extension _fdt_native not built (run `python build_native.py`)"
+        return None
+    try:
+        spec = importlib.util.spec_from_file_location("_fdt_native", path)
+        m = importlib.util.module_from_spec(spec)
+        spec.loader.exec_module(m)
+        _mod = m
+    except Exception as e:  # pragma: no cover - depends on build state
+        _err = f"failed to load {path}: {e}"
+    return _mod
+
+
+def enabled() -> bool:
+    """True when hot ops should run through the HIP kernels."""
+    if os.environ.get("FDT_NATIVE", "1") == "0":
+        return False
+    return torch.cuda.is_available()
+
+
+def native():
+    """The extension module; raises loudly if it is needed but unavailable."""
+    m = load()
+    if m is None:
+        raise RuntimeError(f"HIP fast path requested but {_err}")
+    return m
+
+
+def use_native(t: torch.Tensor) -> bool:
+    """Dispatch predicate for one op call: GPU tensor and fast path enabled."""
+    return t.is_cuda and enabled()
+
+
+def stream_ptr(device: torch.device | None = None) -> int:
+    """Raw hipStream_t of the current torch stream (kernels are enqueued on it, so
+    they order correctly with PyTorch work and are captured by HIP graphs)."""
+    idx = torch.cuda.current_device() if device is None else device.index
+    return torch._C._cuda_getCurrentRawStream(idx)
+
+
+def ptr(t: torch.Tensor | None) -> int:
+    return 0 if t is None else t.data_ptr()

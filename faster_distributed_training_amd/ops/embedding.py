@@ -1,0 +1,63 @@
+"""Summed token + position + segment embedding, scaled by sqrt(d_model)
+(reference ``Embeddings.forward``, ``transformer.py:150-156``).
+
+GPU: ``csrc/kernels/embedding.hip`` — one wave per token row gathers the three table rows
+with 16-B loads and writes the fp32 sum (one pass instead of three gathers + two adds +
+a scale); the backward scatters the row gradient into the three tables with float
+atomics shaped as whole 256-B rows (MI355X atomics run at ~1.3 TB/s for that shape).
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn.functional as F
+
+from . import _native
+
+
+def embedding_sum_reference(ids, types, pos_ids, tok_w, pos_w, seg_w, scale):
+    L = ids.size(1)
+    pos = F.embedding(pos_ids[:L], pos_w).unsqueeze(0)
+    seg = F.embedding(types[:, :L], seg_w)
+    tok = F.embedding(ids.long(), tok_w.float() if tok_w.dtype != torch.float32 else tok_w)
+    return (pos + tok + seg) * scale
+
+
+class _EmbeddingNative(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, ids, types, pos_ids, tok_w, pos_w, seg_w, scale):
+        nat = _native.native()
+        B, L = ids.shape
+        d = tok_w.shape[1]
+        ids32 = ids.to(torch.int32).contiguous()
+        ty32 = types[:, :L].to(torch.int32).contiguous()
+        pos32 = pos_ids[:L].to(torch.int32).contiguous()
+        out = torch.empty(B, L, d, device=ids.device, dtype=torch.float32)
+        nat.embedding_fwd(ids32.data_ptr(), ty32.data_ptr(), pos32.data_ptr(), tok_w.data_ptr(),
+                          pos_w.data_ptr(), seg_w.data_ptr(), out.data_ptr(), B, L, d, float(scale),
+                          tok_w.shape[0], pos_w.shape[0], seg_w.shape[0], _native.stream_ptr())
+        ctx.save_for_backward(ids32, ty32, pos32)
+        ctx.shapes = (tok_w.shape, pos_w.shape, seg_w.shape)
+        ctx.scale = scale
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        nat = _native.native()
+        ids32, ty32, pos32 = ctx.saved_tensors
+        B, L = ids32.shape
+        (vt, d), (vp, _), (vs, _) = ctx.shapes
+        g = g.contiguous().float()
+        gt = torch.zeros(vt, d, device=g.device, dtype=torch.float32)
+        gp = torch.zeros(vp, d, device=g.device, dtype=torch.float32)
+        gs = torch.zeros(vs, d, device=g.device, dtype=torch.float32)
+        nat.embedding_bwd(g.data_ptr(), ids32.data_ptr(), ty32.data_ptr(), pos32.data_ptr(), gt.data_ptr(),
+                          gp.data_ptr(), gs.data_ptr(), B, L, d, float(ctx.scale), vt, vp, vs,
+                          _native.stream_ptr())
+        return None, None, None, gt, gp, gs, None
+
+
+def embedding_sum(ids, types, pos_ids, tok_w, pos_w, seg_w, scale):
+    if (_native.use_native(ids) and tok_w.dtype == torch.float32 and tok_w.shape[1] % 256 == 0
+            and hasattr(_native.native(), "embedding_fwd")):
+        return _EmbeddingNative.apply(ids, types, pos_ids, tok_w, pos_w, seg_w, scale)
+    return embedding_sum_reference(ids, types, pos_ids, tok_w, pos_w, seg_w, scale)

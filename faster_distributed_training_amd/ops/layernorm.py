@@ -1,0 +1,70 @@
+"""LayerNorm with the reference's numerics (``transformer.py:230-242``):
+
+    y = a * (x - mean) / (std_unbiased + eps) + b,   eps = 1e-6 added to the *std*.
+
+GPU: one HIP kernel per direction (``csrc/kernels/layernorm.hip``): one row per wave
+(d = 512 -> 8 elements per lane, one 16-B load for bf16), fp32 statistics; the output
+is written directly in the autocast dtype (the residual stream may stay fp32, like the
+reference where the embedding output is fp32); the backward fuses both row reductions
+and writes per-block dgamma/dbeta partials (no atomics, deterministic).
+"""
+from __future__ import annotations
+
+import torch
+
+from . import _native
+
+DT = {torch.float32: 0, torch.bfloat16: 1, torch.float16: 2}
+
+
+def layer_norm_reference(x, a, b, eps=1e-6):
+    mean = x.mean(-1, keepdim=True)
+    std = x.std(-1, keepdim=True)
+    return a * (x - mean) / (std + eps) + b
+
+
+class _LayerNormNative(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, a, b, eps, out_dtype):
+        nat = _native.native()
+        shape = x.shape
+        d = shape[-1]
+        x2 = x.reshape(-1, d)
+        if not x2.is_contiguous():
+            x2 = x2.contiguous()
+        rows = x2.shape[0]
+        y = torch.empty(rows, d, device=x.device, dtype=out_dtype)
+        mean = torch.empty(rows, device=x.device, dtype=torch.float32)
+        rstd = torch.empty(rows, device=x.device, dtype=torch.float32)
+        nat.layernorm_fwd(x2.data_ptr(), a.data_ptr(), b.data_ptr(), y.data_ptr(), mean.data_ptr(),
+                          rstd.data_ptr(), rows, d, float(eps), DT[x2.dtype], DT[out_dtype], DT[a.dtype],
+                          _native.stream_ptr())
+        ctx.save_for_backward(x2, a, mean, rstd)
+        ctx.shape = shape
+        ctx.eps = eps
+        return y.view(*shape[:-1], d)
+
+    @staticmethod
+    def backward(ctx, gy):
+        nat = _native.native()
+        x2, a, mean, rstd = ctx.saved_tensors
+        rows, d = x2.shape
+        gy2 = gy.reshape(rows, d)
+        if not gy2.is_contiguous():
+            gy2 = gy2.contiguous()
+        gx = torch.empty_like(x2)
+        nblk = max(1, min(512, (rows + 31) // 32))
+        part = torch.empty(2, nblk, d, device=x2.device, dtype=torch.float32)
+        nat.layernorm_bwd(gy2.data_ptr(), x2.data_ptr(), a.data_ptr(), mean.data_ptr(), rstd.data_ptr(),
+                          gx.data_ptr(), part.data_ptr(), rows, d, nblk, DT[gy2.dtype], DT[x2.dtype],
+                          DT[a.dtype], float(ctx.eps), _native.stream_ptr())
+        ga, gb = part.sum(1).unbind(0)
+        return gx.view(ctx.shape), ga.to(a.dtype), gb.to(a.dtype), None, None
+
+
+def layer_norm_unbiased(x, a, b, eps=1e-6):
+    if (_native.use_native(x) and x.shape[-1] % 64 == 0 and 64 <= x.shape[-1] <= 2048
+            and x.dtype in DT and a.dtype == torch.float32):
+        out_dtype = torch.get_autocast_dtype("cuda") if torch.is_autocast_enabled("cuda") else x.dtype
+        return _LayerNormNative.apply(x, a, b, eps, out_dtype)
+    return layer_norm_reference(x, a, b, eps)

@@ -1,0 +1,203 @@
+"""Mixup family (reference ``resnet50_test.py:355-457``, ``transformer.py:71-80``).
+
+* ``mixup_data`` (A1): scalar lambda ~ Beta(alpha, alpha) drawn on the host (no device
+  sync), ``lam*x + (1-lam)*x[perm]``.
+* ``MetaMixup`` (A2): per-sample lambda = sigmoid(theta), theta ~ U(0,1).  The reference
+  re-creates theta every step and never optimises it (survey Q3): ``learnable=False``
+  reproduces that; ``learnable=True`` keeps one theta registered with the optimiser.
+* ``AttentionMixup`` (A3): per-element lambda map with ||lambda_i||^2 sample weight.
+* ``mixup_criterion`` / ``mixup_criterion_meta`` (K7): lambda-weighted cross entropy.
+  The reference meta criterion broadcasts to (B,1,1,B) (Q4); that equals
+  ``mean(lam) * CE_a + (1-mean(lam)) * CE_b`` which ``faithful=True`` computes; the fixed
+  form is the per-sample weighted mean.
+
+GPU: ``csrc/kernels/mixup.hip`` fuses the permuted gather and the interpolation
+(forward) and, in backward, computes dx through the inverse permutation (a gather, no
+atomics) plus the per-sample d(lambda) reduction; the mixup cross entropy is one kernel
+producing the loss and d(logits) together.
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from . import _native
+
+DT = {torch.float32: 0, torch.bfloat16: 1, torch.float16: 2}
+
+
+def sample_lambda(alpha: float, generator: torch.Generator | None = None) -> float:
+    if alpha > 0:
+        # Beta(a,a) via two Gammas on the host: one scalar per step, no device sync.
+        g1 = torch._standard_gamma(torch.tensor([alpha], dtype=torch.float64), generator=generator)
+        g2 = torch._standard_gamma(torch.tensor([alpha], dtype=torch.float64), generator=generator)
+        return float(g1 / (g1 + g2))
+    return float(alpha)
+
+
+def _lam_tensor(lam, x):
+    """Normalise lambda to a per-sample fp32 vector (B,) or a full per-element map."""
+    b = x.shape[0]
+    if isinstance(lam, (float, int)):
+        return torch.full((b,), float(lam), device=x.device, dtype=torch.float32), "scalar"
+    if lam.numel() == b:
+        return lam.reshape(b).float(), "sample"
+    return lam, "element"
+
+
+class _MixupNative(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, perm, lam_vec, lam_requires_grad):
+        nat = _native.native()
+        xc = x.contiguous()
+        b = xc.shape[0]
+        inner = xc.numel() // b
+        out = torch.empty_like(xc)
+        perm32 = perm.to(torch.int32).contiguous()
+        nat.mixup_fwd(xc.data_ptr(), perm32.data_ptr(), lam_vec.data_ptr(), out.data_ptr(), b, inner,
+                      DT[xc.dtype], _native.stream_ptr())
+        ctx.save_for_backward(xc, perm32, lam_vec)
+        ctx.lrg = lam_requires_grad
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        nat = _native.native()
+        xc, perm32, lam_vec = ctx.saved_tensors
+        b = xc.shape[0]
+        inner = xc.numel() // b
+        g = g.contiguous()
+        inv = torch.empty_like(perm32)
+        inv[perm32.long()] = torch.arange(b, device=g.device, dtype=torch.int32)
+        gx = torch.empty_like(xc)
+        glam = torch.empty(b, device=g.device, dtype=torch.float32) if ctx.lrg else None
+        nat.mixup_bwd(g.data_ptr(), xc.data_ptr(), perm32.data_ptr(), inv.data_ptr(), lam_vec.data_ptr(),
+                      gx.data_ptr(), _native.ptr(glam), b, inner, DT[xc.dtype], _native.stream_ptr())
+        return gx, None, glam, None
+
+
+def mixup_interpolate(x: torch.Tensor, perm: torch.Tensor, lam) -> torch.Tensor:
+    """lam * x + (1 - lam) * x[perm]; lam scalar, (B,)-shaped, or full map."""
+    lv, kind = _lam_tensor(lam, x)
+    if kind != "element" and _native.use_native(x) and x.dtype in DT:
+        return _MixupNative.apply(x, perm, lv, bool(getattr(lam, "requires_grad", False)))
+    if kind == "scalar":
+        return float(lam) * x + (1 - float(lam)) * x[perm]
+    shape = (x.shape[0],) + (1,) * (x.dim() - 1) if kind == "sample" else x.shape
+    lv = lv.reshape(shape).to(x.dtype)
+    return lv * x + (1 - lv) * x[perm]
+
+
+def mixup_data(x, y, alpha=0.99, intra_only=False, generator=None):
+    """(mixed_x, y_a, y_b, lam) — reference ``mixup_data`` (``resnet50_test.py:355-376``).
+    ``intra_only`` keeps same-label pairs unmixed (vectorised, no per-sample loop)."""
+    lam = sample_lambda(alpha, generator)
+    b = x.size(0)
+    perm = torch.randperm(b, device=x.device)
+    if intra_only:
+        same = (y == y[perm]).float()
+        lam_vec = same + (1 - same) * lam
+        mixed = mixup_interpolate(x, perm, lam_vec)
+    else:
+        mixed = mixup_interpolate(x, perm, lam)
+    return mixed, y, y[perm], lam
+
+
+class MetaMixup(nn.Module):
+    """Per-sample learnable-lambda mixup (A2, ``resnet50_test.py:388-401``)."""
+
+    def __init__(self, batch_size, device=None, learnable=False):
+        super().__init__()
+        self.lam = nn.Parameter(torch.rand(batch_size, 1, 1, 1, device=device))
+        with torch.no_grad():
+            self.lam.clamp_(0.0, 1.0)
+        self.lam.requires_grad_(learnable)
+        self.batch_size = batch_size
+        self.learnable = learnable
+
+    def resample(self):
+        """Faithful mode: fresh theta ~ U(0,1) every step (the reference re-instantiates)."""
+        with torch.no_grad():
+            self.lam.uniform_(0.0, 1.0)
+
+    def forward(self, x, y):
+        if not self.learnable:
+            self.resample()
+        b = x.size(0)
+        perm = torch.randperm(b, device=x.device)
+        lam = torch.sigmoid(self.lam[:b])
+        mixed = mixup_interpolate(x, perm, lam.view(b))
+        return mixed, y, y[perm], lam
+
+
+class AttentionMixup(nn.Module):
+    """Per-pixel lambda map (A3, ``resnet50_test.py:404-424``; defined but unused there)."""
+
+    def __init__(self, batch_size, width, height, channel=3, device=None):
+        super().__init__()
+        self.lam = nn.Parameter(torch.rand(batch_size, channel, width, height, device=device))
+        with torch.no_grad():
+            self.lam.clamp_(0.0, 1.0)
+
+    def forward(self, x, y):
+        b = x.size(0)
+        perm = torch.randperm(b, device=x.device)
+        lam_attn = torch.sigmoid(self.lam[:b])
+        mixed = lam_attn * x + (1 - lam_attn) * x[perm]
+        lam_scale = (lam_attn.reshape(b, -1) ** 2).sum(1)
+        return mixed, y, y[perm], lam_scale
+
+
+# ----------------------------------------------------------------------------- losses
+
+class _MixupCENative(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, logits, ya, yb, lam_vec, weights_mean):
+        nat = _native.native()
+        lg = logits.contiguous()
+        b, c = lg.shape
+        loss = torch.empty((), device=lg.device, dtype=torch.float32)
+        glog = torch.empty(b, c, device=lg.device, dtype=torch.float32)
+        dlam = torch.empty(b, device=lg.device, dtype=torch.float32)
+        nat.mixup_ce_fwd(lg.data_ptr(), ya.to(torch.int32).contiguous().data_ptr(),
+                         yb.to(torch.int32).contiguous().data_ptr(), lam_vec.data_ptr(), loss.data_ptr(),
+                         glog.data_ptr(), dlam.data_ptr(), b, c, DT[lg.dtype], _native.stream_ptr())
+        ctx.save_for_backward(glog, dlam)
+        ctx.dt = logits.dtype
+        return loss
+
+    @staticmethod
+    def backward(ctx, gl):
+        glog, dlam = ctx.saved_tensors
+        glam = dlam * gl if ctx.needs_input_grad[3] else None
+        return (glog * gl).to(ctx.dt), None, None, glam, None
+
+
+def mixup_cross_entropy(logits, y_a, y_b, lam_vec):
+    """mean_i [lam_i CE(p_i, ya_i) + (1-lam_i) CE(p_i, yb_i)]."""
+    if (_native.use_native(logits) and logits.dim() == 2 and logits.shape[1] <= 1024
+            and logits.dtype in DT and hasattr(_native.native(), "mixup_ce_fwd")):
+        return _MixupCENative.apply(logits, y_a, y_b, lam_vec.float().contiguous(), False)
+    lf = logits.float()
+    ce_a = F.cross_entropy(lf, y_a, reduction="none")
+    ce_b = F.cross_entropy(lf, y_b, reduction="none")
+    return (lam_vec * ce_a + (1 - lam_vec) * ce_b).mean()
+
+
+def mixup_criterion(criterion, pred, y_a, y_b, lam):
+    """Scalar-lambda criterion (``resnet50_test.py:451-452``).  ``criterion`` is accepted
+    for API parity; cross entropy is computed by the fused kernel."""
+    lv = torch.full((pred.shape[0],), float(lam), device=pred.device, dtype=torch.float32)
+    if criterion is not None and not isinstance(criterion, nn.CrossEntropyLoss):
+        return lam * criterion(pred, y_a) + (1 - lam) * criterion(pred, y_b)
+    return mixup_cross_entropy(pred, y_a, y_b, lv)
+
+
+def mixup_criterion_meta(criterion, pred, y_a, y_b, lam, faithful=False):
+    """Per-sample-lambda criterion (``resnet50_test.py:455-457``); see module doc (Q4)."""
+    b = pred.shape[0]
+    lv = lam.reshape(b).float()
+    if faithful:
+        lv = lv.mean().expand(b).contiguous()
+    return mixup_cross_entropy(pred, y_a, y_b, lv)

@@ -1,0 +1,332 @@
+"""Fused optimizers over the flat parameter buffer (``utils/flat.py``).
+
+Each optimizer is a real ``torch.optim.Optimizer`` (so ``torch.optim.lr_scheduler``
+works unchanged: MultiStepLR / CosineAnnealingLR / OneCycleLR / StepLR as the
+reference uses, survey A10) whose ``step`` is ONE HIP launch over the whole model:
+grad * clip-coefficient (device scalar) -> found-inf skip (device flag) -> weight decay
+-> update -> bf16 shadow write -> grad zeroing (``csrc/kernels/optim.hip``).
+The CPU path runs the same math with torch ops (also the kernel-test oracle).
+
+Reference update rules:
+* SGD / momentum / dampening / nesterov: ``ngd_optimizer.py:478-506`` (the NGD tail) and
+  ``tuning/resnet50_tuning.py:437`` (plain SGD);
+* MADGRAD (``resnet50_test.py:493``) and MirrorMADGRAD (``transformer_test.py:220``) come
+  from the external ``madgrad`` package, which is not installed here: MADGRAD follows
+  Defazio & Jelassi 2021 (dual averaging, cube-root denominator, momentum as primal
+  averaging, x0 recomputed when momentum == 0); MirrorMADGRAD uses the mirror-descent
+  form z <- z - lamb*g/rms_{k+1}, p <- (1-ck) p + ck z.  Parity with the package is
+  unpinned (no copy available offline); see tests/test_optim.py.
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+
+from ..ops import _native
+from ..utils.flat import FlatParams
+
+
+def _sp():
+    return _native.stream_ptr()
+
+
+def _p(t):
+    return 0 if t is None else t.data_ptr()
+
+
+class FlatOptimizer(torch.optim.Optimizer):
+    def __init__(self, flat: FlatParams, defaults: dict, zero_grad_in_step: bool = True):
+        self.flat = flat
+        super().__init__(flat.params, defaults)
+        self.zero_grad_in_step = zero_grad_in_step
+        self.k = 0  # completed steps
+        self._native = flat.data.is_cuda and _native.enabled()
+
+    @property
+    def group(self):
+        return self.param_groups[0]
+
+    def zero_grad(self, set_to_none: bool = False):  # noqa: ARG002 - views must persist
+        self.flat.zero_grad()
+
+    def _state_buf(self, name, init="zeros"):
+        st = self.state.setdefault("__flat__", {})
+        if name not in st:
+            if init == "zeros":
+                st[name] = torch.zeros_like(self.flat.data)
+            elif init == "copy":
+                st[name] = self.flat.data.clone()
+        return st[name]
+
+    def step(self, closure=None, grad_scale: torch.Tensor | None = None, found_inf: torch.Tensor | None = None):
+        loss = closure() if closure is not None else None
+        self._step(grad_scale, found_inf)
+        self.k += 1
+        return loss
+
+    # ------------------------------------------------------------ state dict
+    def state_dict(self):
+        sd = super().state_dict()
+        sd["k"] = self.k
+        return sd
+
+    def load_state_dict(self, sd):
+        sd = dict(sd)
+        self.k = int(sd.pop("k", 0))
+        super().load_state_dict(sd)
+
+    def _cpu_common(self, grad_scale, found_inf):
+        if found_inf is not None and bool(found_inf.item() != 0):
+            return None
+        g = self.flat.grad
+        if grad_scale is not None:
+            g = g * grad_scale.to(g.device)
+        return g
+
+    def _finish_cpu(self):
+        self.flat.refresh_shadow()
+        if self.zero_grad_in_step:
+            self.flat.grad.zero_()
+
+
+class SGD(FlatOptimizer):
+    def __init__(self, flat, lr=0.1, momentum=0.0, dampening=0.0, weight_decay=0.0, nesterov=False, **kw):
+        if nesterov and (momentum <= 0 or dampening != 0):
+            raise ValueError("Nesterov momentum requires a momentum and zero dampening")
+        super().__init__(flat, dict(lr=lr, momentum=momentum, dampening=dampening, weight_decay=weight_decay,
+                                    nesterov=nesterov), **kw)
+
+    def _step(self, grad_scale, found_inf, d_override=None):
+        g = self.group
+        buf = self._state_buf("momentum_buffer") if g["momentum"] != 0 else None
+        first = int(self.state["__flat__"].get("initialized", 0) == 0) if buf is not None else 0
+        if self._native and d_override is None:
+            _native.native().sgd_step(
+                self.flat.data.data_ptr(), self.flat.grad.data_ptr(), _p(buf), _p(self.flat.shadow), self.flat.numel,
+                float(g["lr"]), float(g["momentum"]), float(g["dampening"]), float(g["weight_decay"]),
+                int(g["nesterov"]), first, _p(grad_scale), _p(found_inf), int(self.zero_grad_in_step), _sp())
+        else:
+            gr = self._cpu_common(grad_scale, found_inf) if d_override is None else d_override
+            if gr is None:
+                return
+            p = self.flat.data
+            d = gr + g["weight_decay"] * p if g["weight_decay"] != 0 else gr.clone()
+            if buf is not None:
+                if first:
+                    buf.copy_(d)
+                else:
+                    buf.mul_(g["momentum"]).add_(d, alpha=1 - g["dampening"])
+                d = d + g["momentum"] * buf if g["nesterov"] else buf
+            p.add_(d, alpha=-g["lr"])
+            self._finish_cpu()
+        if buf is not None:
+            self.state["__flat__"]["initialized"] = 1
+
+
+class MADGRAD(FlatOptimizer):
+    def __init__(self, flat, lr=1e-2, momentum=0.9, weight_decay=0.0, eps=1e-6, decouple_decay=False, **kw):
+        if not 0.0 <= momentum < 1.0:
+            raise ValueError("momentum must be in [0, 1)")
+        super().__init__(flat, dict(lr=lr, momentum=momentum, weight_decay=weight_decay, eps=eps,
+                                    decouple_decay=decouple_decay), **kw)
+
+    def _step(self, grad_scale, found_inf):
+        g = self.group
+        gss = self._state_buf("grad_sum_sq")
+        s = self._state_buf("s")
+        x0 = self._state_buf("x0", init="copy") if g["momentum"] != 0 else None
+        if self._native:
+            _native.native().madgrad_step(
+                self.flat.data.data_ptr(), self.flat.grad.data_ptr(), gss.data_ptr(), s.data_ptr(), _p(x0),
+                _p(self.flat.shadow), self.flat.numel, float(g["lr"]), float(g["momentum"]), float(g["weight_decay"]),
+                float(g["eps"]), int(g["decouple_decay"]), self.k, _p(grad_scale), _p(found_inf),
+                int(self.zero_grad_in_step), _sp())
+            return
+        gr = self._cpu_common(grad_scale, found_inf)
+        if gr is None:
+            return
+        p = self.flat.data
+        eps, lr = g["eps"], g["lr"] + g["eps"]
+        lamb = lr * math.sqrt(self.k + 1)
+        ck = 1 - g["momentum"]
+        if g["weight_decay"] != 0 and not g["decouple_decay"]:
+            gr = gr + g["weight_decay"] * p
+        if g["momentum"] == 0:
+            x0v = p + s / (gss.pow(1 / 3) + eps)
+        else:
+            x0v = x0
+        gss.addcmul_(gr, gr, value=lamb)
+        rms = gss.pow(1 / 3).add_(eps)
+        if g["weight_decay"] != 0 and g["decouple_decay"]:
+            p.mul_(1 - lr * g["weight_decay"])
+        s.add_(gr, alpha=lamb)
+        z = x0v - s / rms
+        if g["momentum"] == 0:
+            p.copy_(z)
+        else:
+            p.mul_(1 - ck).add_(z, alpha=ck)
+        self._finish_cpu()
+
+
+class MirrorMADGRAD(FlatOptimizer):
+    def __init__(self, flat, lr=1e-2, momentum=0.9, weight_decay=0.0, eps=0.0, decouple_decay=False, **kw):
+        super().__init__(flat, dict(lr=lr, momentum=momentum, weight_decay=weight_decay, eps=eps,
+                                    decouple_decay=decouple_decay), **kw)
+
+    def _step(self, grad_scale, found_inf):
+        g = self.group
+        gss = self._state_buf("grad_sum_sq")
+        z = self._state_buf("z", init="copy")
+        if self._native:
+            _native.native().mirror_madgrad_step(
+                self.flat.data.data_ptr(), self.flat.grad.data_ptr(), gss.data_ptr(), z.data_ptr(),
+                _p(self.flat.shadow), self.flat.numel, float(g["lr"]), float(g["momentum"]), float(g["weight_decay"]),
+                float(g["eps"]), int(g["decouple_decay"]), self.k, _p(grad_scale), _p(found_inf),
+                int(self.zero_grad_in_step), _sp())
+            return
+        gr = self._cpu_common(grad_scale, found_inf)
+        if gr is None:
+            return
+        p = self.flat.data
+        eps, lr = g["eps"], g["lr"] + g["eps"]
+        lamb = lr * math.sqrt(self.k + 1)
+        ck = 1 - g["momentum"]
+        if g["weight_decay"] != 0 and not g["decouple_decay"]:
+            gr = gr + g["weight_decay"] * p
+        gss.addcmul_(gr, gr, value=lamb)
+        rms = gss.pow(1 / 3).add_(eps)
+        step = torch.where(rms > 0, lamb * gr / torch.where(rms > 0, rms, torch.ones_like(rms)), torch.zeros_like(rms))
+        z.sub_(step)
+        if g["weight_decay"] != 0 and g["decouple_decay"]:
+            z.mul_(1 - lr * g["weight_decay"])
+        p.mul_(1 - ck).add_(z, alpha=ck)
+        self._finish_cpu()
+
+
+class Adam(FlatOptimizer):
+    def __init__(self, flat, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.0, adamw=False, **kw):
+        super().__init__(flat, dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay, adamw=adamw), **kw)
+
+    def _step(self, grad_scale, found_inf):
+        g = self.group
+        m = self._state_buf("exp_avg")
+        v = self._state_buf("exp_avg_sq")
+        b1, b2 = g["betas"]
+        step = self.k + 1
+        if self._native:
+            _native.native().adam_step(
+                self.flat.data.data_ptr(), self.flat.grad.data_ptr(), m.data_ptr(), v.data_ptr(), _p(self.flat.shadow),
+                self.flat.numel, float(g["lr"]), float(b1), float(b2), float(g["eps"]), float(g["weight_decay"]),
+                int(g["adamw"]), step, _p(grad_scale), _p(found_inf), int(self.zero_grad_in_step), _sp())
+            return
+        gr = self._cpu_common(grad_scale, found_inf)
+        if gr is None:
+            return
+        p = self.flat.data
+        if g["weight_decay"] != 0:
+            if g["adamw"]:
+                p.mul_(1 - g["lr"] * g["weight_decay"])
+            else:
+                gr = gr + g["weight_decay"] * p
+        m.mul_(b1).add_(gr, alpha=1 - b1)
+        v.mul_(b2).addcmul_(gr, gr, value=1 - b2)
+        p.addcdiv_(m / (1 - b1 ** step), (v / (1 - b2 ** step)).sqrt_().add_(g["eps"]), value=-g["lr"])
+        self._finish_cpu()
+
+
+# ------------------------------------------------------------------ clipping / AMP
+class GradClipper:
+    """clip_grad_norm_ over the flat gradient with the result kept ON DEVICE
+    (``coef`` is passed to the optimizer kernel): no host sync, unlike
+    ``torch.nn.utils.clip_grad_norm_`` + GradScaler's found_inf check in the reference
+    (``resnet50_test.py:544-548``).  Also performs GradScaler's unscale + inf check."""
+
+    def __init__(self, flat: FlatParams, nblocks: int = 1024, process_group=None, sharded: bool = False):
+        self.flat = flat
+        self.sharded = sharded  # FSDP: grads are a per-rank shard -> all-reduce the sum of squares
+        self.pg = process_group
+        dev = flat.device
+        self.nb = nblocks
+        self.part = torch.empty(nblocks, device=dev, dtype=torch.float32)
+        self.out = torch.zeros(2, device=dev, dtype=torch.float32)  # [norm, coef]
+        self.found_inf = torch.zeros(1, device=dev, dtype=torch.int32)
+
+    @property
+    def norm(self):
+        return self.out[0]
+
+    @property
+    def coef(self):
+        return self.out[1:2]
+
+    def __call__(self, max_norm: float, inv_scale: torch.Tensor | None = None, check_inf: bool = False):
+        g = self.flat.grad
+        if g.is_cuda and _native.enabled():
+            nat = _native.native()
+            if check_inf:
+                self.found_inf.zero_()
+            nat.grad_sumsq(g.data_ptr(), g.numel(), _p(inv_scale), int(inv_scale is not None), self.part.data_ptr(),
+                           self.nb, _p(self.found_inf) if check_inf else 0, _sp())
+            if self.sharded:
+                return self._sharded_finalize(self.part.sum(), max_norm)
+            nat.grad_norm_finalize(self.part.data_ptr(), self.nb, float(max_norm), self.out.data_ptr(), _sp())
+        else:
+            if inv_scale is not None:
+                g.mul_(inv_scale)
+            if check_inf:
+                self.found_inf.fill_(int(not torch.isfinite(g).all()))
+            if self.sharded:
+                return self._sharded_finalize(g.double().pow(2).sum().float(), max_norm)
+            norm = g.double().pow(2).sum().sqrt()
+            self.out[0] = norm.float()
+            c = (max_norm / (norm + 1e-6)).clamp(max=1.0) if max_norm > 0 else torch.ones((), dtype=torch.float64)
+            self.out[1] = c.float()
+        return self.out[0]
+
+    def _sharded_finalize(self, sumsq, max_norm):
+        import torch.distributed as dist
+        t = sumsq.reshape(1).float()
+        dist.all_reduce(t, group=self.pg)
+        norm = t.sqrt()
+        coef = (max_norm / (norm + 1e-6)).clamp(max=1.0) if max_norm > 0 else torch.ones_like(norm)
+        self.out[0:1].copy_(norm)
+        self.out[1:2].copy_(coef)
+        return self.out[0]
+
+
+class DeviceGradScaler:
+    """fp16 loss scaling with all state on the device (replaces
+    ``torch.cuda.amp.GradScaler`` / fairscale ``ShardedGradScaler``,
+    ``resnet50_test.py:705-706``, ``transformer_test.py:368``).  ``found_inf`` is
+    all-reduced (MAX) across ranks when distributed, like ShardedGradScaler."""
+
+    def __init__(self, device, init_scale=2.0**16, growth_factor=2.0, backoff_factor=0.5, growth_interval=2000,
+                 enabled=True):
+        self.enabled = enabled
+        self.scale = torch.full((1,), init_scale if enabled else 1.0, device=device, dtype=torch.float32)
+        self.growth_tracker = torch.zeros(1, device=device, dtype=torch.int32)
+        self.gf, self.bf, self.gi = growth_factor, backoff_factor, growth_interval
+
+    def scale_loss(self, loss):
+        return loss * self.scale.to(loss.dtype) if self.enabled else loss
+
+    def inv_scale(self):
+        return (1.0 / self.scale) if self.enabled else None
+
+    def sync_found_inf(self, found_inf):
+        import torch.distributed as dist
+        if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+            dist.all_reduce(found_inf, op=dist.ReduceOp.MAX)
+
+    def update(self, found_inf):
+        if not self.enabled:
+            return
+        torch._amp_update_scale_(self.scale, self.growth_tracker, found_inf.float(), self.gf, self.bf, self.gi)
+
+    def state_dict(self):
+        return {"scale": self.scale.clone(), "growth_tracker": self.growth_tracker.clone()}
+
+    def load_state_dict(self, sd):
+        self.scale.copy_(sd["scale"])
+        self.growth_tracker.copy_(sd["growth_tracker"])

@@ -1,0 +1,169 @@
+"""Distributed data parallel: bucketed gradient all-reduce overlapped with backward.
+
+Replaces ``torch.nn.parallel.DistributedDataParallel`` as used by the reference
+(``resnet50_test.py:716``: default 25 MB buckets, ``broadcast_buffers=True``; survey P5,
+X2-X4) with a reducer designed around the flat gradient buffer (``utils/flat.py``):
+
+* buckets are contiguous slices of the flat fp32 gradient (gradient-as-bucket-view:
+  no flatten/unflatten copies), in reverse registration order = backward order;
+* each parameter's post-accumulate-grad hook counts down its bucket; a full bucket is
+  launched immediately as an async ``all_reduce`` on RCCL's stream (backend ``nccl`` is
+  RCCL on ROCm), so communication overlaps the rest of backward;
+* ``finish()`` (call after ``backward``) launches any bucket left (unused params) and
+  makes the compute stream wait on RCCL — no host blocking on GPU;
+* averaging uses ``ReduceOp.AVG`` on RCCL (no extra scaling pass), ``SUM`` + scale on
+  gloo; optional bf16 wire format halves bytes on xGMI.
+
+Bucket sizing for MI355X: an 8-GPU node connects every GPU to every other by one xGMI
+link (7 x ~153 GB/s per GPU).  RCCL's multi-channel algorithms spread a large message
+over all links, so per-bucket cost is latency-dominated below a few MB and bandwidth-
+dominated above; the exposed cost is the LAST bucket.  Default: a 1 MB first bucket
+(communication starts after the classifier/last stage) then 8 MB buckets — ResNet-50's
+89.6 MB fp32 gradient becomes ~12 buckets vs the reference's 5 x 25 MB, so the tail that
+cannot overlap is ~8 MB (~15 µs at 7-link bandwidth) instead of ~25 MB.
+"""
+from __future__ import annotations
+
+import torch
+import torch.distributed as dist
+
+from ..ops import _native
+from ..utils.flat import FlatParams
+
+
+def plan_buckets_py(sizes, first_cap, cap):
+    """Python twin of the native ``plan_buckets`` (csrc/runtime/runtime.cpp)."""
+    buckets, cur, acc, limit = [], [], 0, first_cap
+    for i in range(len(sizes) - 1, -1, -1):
+        cur.append(i)
+        acc += sizes[i]
+        if acc >= limit:
+            buckets.append(cur)
+            cur, acc, limit = [], 0, cap
+    if cur:
+        buckets.append(cur)
+    return buckets
+
+
+def plan_buckets(sizes, first_cap, cap):
+    nat = _native.load()
+    if nat is not None:
+        return [list(b) for b in nat.plan_buckets(list(map(int, sizes)), int(first_cap), int(cap))]
+    return plan_buckets_py(sizes, first_cap, cap)
+
+
+class BucketReducer:
+    def __init__(self, flat: FlatParams, module=None, process_group=None, bucket_mb: float = 8.0,
+                 first_bucket_mb: float = 1.0, comm_dtype: torch.dtype | None = None,
+                 broadcast_buffers: bool = True, broadcast_init: bool = True):
+        self.flat = flat
+        self.module = module
+        self.pg = process_group
+        self.ws = dist.get_world_size(process_group)
+        self.comm_dtype = comm_dtype
+        self.broadcast_buffers = broadcast_buffers
+        backend = dist.get_backend(process_group)
+        self.use_avg = backend == "nccl"
+        # flat slots are in REVERSE registration order already; plan over registration
+        # order so the planner's "reverse" walk yields flat (=backward) order.
+        slots = flat.slots[::-1]
+        sizes = [s.numel * 4 for s in slots]
+        plan = plan_buckets(sizes, int(first_bucket_mb * 2**20), int(bucket_mb * 2**20))
+        self.buckets = []  # (start, end, [slot indices in flat order])
+        n_slots = len(slots)
+        for b in plan:
+            flat_idx = [n_slots - 1 - i for i in b]
+            start = min(flat.slots[i].offset for i in flat_idx)
+            last = max(flat_idx)
+            end = flat.slots[last].offset + flat.slots[last].numel
+            end = min((end + 63) // 64 * 64, flat.numel)
+            self.buckets.append((start, end, flat_idx))
+        # make buckets tile the buffer exactly (padding elements travel with a bucket)
+        for k in range(len(self.buckets) - 1):
+            s, _, idx = self.buckets[k]
+            self.buckets[k] = (s, self.buckets[k + 1][0], idx)
+        if self.buckets:
+            s, _, idx = self.buckets[-1]
+            self.buckets[-1] = (s, flat.numel, idx)
+        self.bucket_of = {}
+        for b, (_, _, idx) in enumerate(self.buckets):
+            for i in idx:
+                self.bucket_of[id(flat.slots[i].param)] = b
+        self.pending = [len(idx) for (_, _, idx) in self.buckets]
+        self.works = [None] * len(self.buckets)
+        self.tmp = [None] * len(self.buckets)
+        self._hooks = [s.param.register_post_accumulate_grad_hook(self._hook) for s in flat.slots]
+        self.enabled = True
+        if broadcast_init:
+            self.broadcast_parameters()
+
+    # ------------------------------------------------------------------ hooks
+    def _hook(self, p):
+        if not self.enabled:
+            return
+        b = self.bucket_of[id(p)]
+        self.pending[b] -= 1
+        if self.pending[b] == 0:
+            self._launch(b)
+
+    def _launch(self, b):
+        if self.works[b] is not None:
+            return
+        s, e, _ = self.buckets[b]
+        view = self.flat.grad[s:e]
+        if self.comm_dtype is not None and self.comm_dtype != view.dtype:
+            buf = view.to(self.comm_dtype)
+            self.tmp[b] = buf
+        else:
+            buf = view
+        op = dist.ReduceOp.AVG if self.use_avg else dist.ReduceOp.SUM
+        self.works[b] = dist.all_reduce(buf, op=op, group=self.pg, async_op=True)
+
+    def finish(self):
+        """Complete the gradient all-reduce (call once after backward)."""
+        for b in range(len(self.buckets)):
+            if self.works[b] is None:
+                self._launch(b)
+        for b, w in enumerate(self.works):
+            w.wait()
+            s, e, _ = self.buckets[b]
+            if self.tmp[b] is not None:
+                self.flat.grad[s:e].copy_(self.tmp[b])
+                self.tmp[b] = None
+            if not self.use_avg:
+                self.flat.grad[s:e].div_(self.ws)
+        self.works = [None] * len(self.buckets)
+        self.pending = [len(idx) for (_, _, idx) in self.buckets]
+
+    # ------------------------------------------------------------------ sync
+    @torch.no_grad()
+    def broadcast_parameters(self, src: int = 0):
+        """X2: one broadcast of the whole flat parameter buffer (+ buffers)."""
+        dist.broadcast(self.flat.data, src, group=self.pg)
+        self.flat.refresh_shadow()
+        self.sync_buffers(src)
+
+    @torch.no_grad()
+    def sync_buffers(self, src: int = 0):
+        """X3: broadcast BatchNorm running statistics (DDP's broadcast_buffers)."""
+        if self.module is None:
+            return
+        bufs = [b for b in self.module.buffers() if b.dtype.is_floating_point]
+        if not bufs:
+            return
+        flat = torch.cat([b.reshape(-1) for b in bufs])
+        dist.broadcast(flat, src, group=self.pg)
+        off = 0
+        for b in bufs:
+            n = b.numel()
+            b.copy_(flat[off:off + n].view_as(b))
+            off += n
+
+    def remove(self):
+        for h in self._hooks:
+            h.remove()
+        self._hooks = []
+
+    @property
+    def bucket_sizes_mb(self):
+        return [(e - s) * 4 / 2**20 for (s, e, _) in self.buckets]

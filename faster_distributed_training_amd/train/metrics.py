@@ -1,0 +1,127 @@
+"""Metrics / logging / plotting (survey C2, C3, §5 observability).
+
+* ``DeviceMeter``: per-step loss / lambda-weighted accuracy accumulated ON DEVICE (the
+  reference syncs 4-5 times per batch for its tqdm descriptor, ``resnet50_test.py:550-566``);
+  read once per epoch (or every ``log_interval`` steps), all-reduced in one collective.
+* ``StepTimer``: HIP-event timing of steps/phases, read once per epoch.
+* ``JsonlLogger``: rank-0 JSON-lines metrics (step, epoch, img/s, loss, acc, peak mem).
+* ``draw_graph``: the reference's matplotlib curves (``utils.py:54-69``), rank 0 only
+  (the reference wrote the same PNG from every rank, Q16).
+"""
+from __future__ import annotations
+
+import json
+import os
+import time
+
+import numpy as np
+import torch
+
+from ..utils.env import is_rank0
+
+
+class DeviceMeter:
+    def __init__(self, device):
+        self.device = device
+        self.reset()
+
+    def reset(self):
+        self.loss = torch.zeros((), device=self.device, dtype=torch.float32)
+        self.correct = torch.zeros((), device=self.device, dtype=torch.float32)
+        self.total = torch.zeros((), device=self.device, dtype=torch.float32)
+        self.steps = 0
+
+    @torch.no_grad()
+    def update(self, loss, logits, y_a, y_b=None, lam=1.0):
+        pred = logits.argmax(1)
+        self.loss += loss.detach().float()
+        if y_b is None:
+            self.correct += (pred == y_a).sum().float()
+        elif isinstance(lam, torch.Tensor) and lam.numel() > 1:
+            lv = lam.reshape(-1).float()
+            self.correct += (lv * (pred == y_a).float()).sum() + ((1 - lv) * (pred == y_b).float()).sum()
+        else:
+            lv = float(lam)
+            self.correct += lv * (pred == y_a).sum().float() + (1 - lv) * (pred == y_b).sum().float()
+        self.total += float(logits.shape[0])
+        self.steps += 1
+
+    def reduced(self):
+        from ..parallel.dist import all_reduce_metrics
+        t = torch.stack([self.loss, self.correct, self.total])
+        all_reduce_metrics(t)
+        loss, correct, total = t.tolist()
+        from ..parallel.dist import world
+        steps = max(1, self.steps)
+        return {"loss": loss / steps / world(), "acc": 100.0 * correct / max(total, 1.0),
+                "correct": correct, "total": total}
+
+
+class StepTimer:
+    """Wall-clock + HIP-event timer (events recorded on the current stream, resolved
+    lazily: no synchronisation inside the timed loop)."""
+
+    def __init__(self, cuda: bool):
+        self.cuda = cuda
+        self.events = []
+
+    def mark(self):
+        if self.cuda:
+            e = torch.cuda.Event(enable_timing=True)
+            e.record()
+            self.events.append(e)
+        else:
+            self.events.append(time.perf_counter())
+
+    def intervals_ms(self):
+        if len(self.events) < 2:
+            return []
+        if self.cuda:
+            torch.cuda.synchronize()
+            return [a.elapsed_time(b) for a, b in zip(self.events[:-1], self.events[1:])]
+        return [(b - a) * 1e3 for a, b in zip(self.events[:-1], self.events[1:])]
+
+
+class JsonlLogger:
+    def __init__(self, path: str | None):
+        self.path = path if is_rank0() else None
+        if self.path:
+            os.makedirs(os.path.dirname(os.path.abspath(self.path)), exist_ok=True)
+
+    def log(self, **kw):
+        if self.path:
+            kw.setdefault("time", time.time())
+            with open(self.path, "a") as f:
+                f.write(json.dumps(kw) + "\n")
+
+
+def peak_memory_gb(device=None) -> float:
+    if torch.cuda.is_available():
+        return torch.cuda.max_memory_allocated(device) / 1024**3
+    return 0.0
+
+
+def draw_graph(xs, ys, labels, title, metric, out_dir="."):
+    """Reference ``draw_graph`` (``utils.py:54-69``): writes ``<title>.png``."""
+    if not is_rank0():
+        return None
+    import matplotlib
+    matplotlib.use("Agg")
+    import matplotlib.pyplot as plt
+    plt.figure(figsize=(12, 8))
+    if isinstance(xs[0], (list, np.ndarray)):
+        for x_list, y_list, label in zip(xs, ys, labels):
+            plt.plot(x_list, y_list, label=label, linewidth=2)
+        plt.xticks(xs[0])
+    else:
+        plt.plot(xs, ys, label=labels, linewidth=2)
+        plt.xticks(xs)
+    plt.xlabel("Epoch/Iteration")
+    plt.ylabel(metric)
+    plt.title(title)
+    plt.legend()
+    plt.grid()
+    path = os.path.join(out_dir, title + ".png")
+    plt.savefig(path)
+    plt.close()
+    return path

@@ -1,0 +1,308 @@
+"""ResNet / CIFAR-10 training driver (reference ``resnet50_test.py:460-740``; T1, T2, T5).
+
+Per step (all on device, no host synchronisation):
+  batch (device-resident CIFAR + GPU augment) -> mixup (A1) or meta-mixup (A2) ->
+  forward (HIP engine, bf16) -> fused mixup cross-entropy -> backward (DDP buckets
+  all-reduced on RCCL while backward runs) -> clip-norm coefficient on device ->
+  one fused optimizer launch (MADGRAD / SGD / NGD / Adam) -> device-side metrics.
+Per epoch: metric all-reduce (one collective), scheduler step, eval, rank-0
+best checkpoint in the reference schema, JSONL log, plots at the end.
+"""
+from __future__ import annotations
+
+import math
+import os
+import time
+from dataclasses import dataclass, field
+
+import numpy as np
+import torch
+import torch.nn as nn
+
+from ..data.cifar import CLASSES, CIFAR10, DeviceCIFARLoader, synthetic_cifar
+from ..models import resnet as resnet_models
+from ..ops.mixup import MetaMixup, mixup_criterion, mixup_criterion_meta, mixup_data
+from ..optim.flat_optim import MADGRAD, SGD, Adam, DeviceGradScaler, GradClipper, MirrorMADGRAD
+from ..optim.ngd import NGD
+from ..parallel import dist as pdist
+from ..utils.env import default_device, print0, seed_everything
+from ..utils.flat import FlatParams
+from . import checkpoint as ckpt
+from .metrics import DeviceMeter, JsonlLogger, StepTimer, draw_graph, peak_memory_gb
+
+
+@dataclass
+class ResNetConfig:
+    arch: str = "resnet50"
+    num_classes: int = 10
+    bs: int = 128                      # per process (reference --bs)
+    lr: float = 0.02
+    epoch: int = 50
+    alpha: float = 0.99                # Beta(alpha, alpha) for mixup
+    meta_learning: bool = False
+    learnable_meta: bool = False       # Q3 fix: optimise the meta-mixup lambda
+    distributed: bool = False
+    ngd: bool = False
+    optimizer: str = "auto"            # auto: ngd->NGD, else MADGRAD (reference defaults)
+    weight_decay: float | None = None  # auto: NGD 1e-4, MADGRAD 5e-6, SGD 5e-4
+    momentum: float = 0.9
+    clip: float = 10.0
+    precision: str = "bf16"            # bf16 | fp16 (GradScaler) | fp32
+    synthetic: bool = False
+    data_root: str = "./data"
+    seed: int = 123456
+    faithful: bool = False
+    lr_scaling: str = "world"          # world | faithful4 | none   (Q11)
+    bucket_mb: float = 8.0
+    first_bucket_mb: float = 1.0
+    comm_dtype: str = "fp32"
+    fsdp: bool = False
+    scheduler: str = "auto"
+    resume: bool = False
+    checkpoint_dir: str = "./checkpoint"
+    steps_per_epoch: int = 0           # 0 = full epoch
+    eval: bool = True
+    log_path: str | None = None
+    plot: bool = True
+    workers: int = 2                   # accepted for CLI parity (no worker processes needed)
+    fast_path: bool | None = None      # None = HIP engine when on GPU
+    extra: dict = field(default_factory=dict)
+
+
+def build_model(cfg: ResNetConfig, device):
+    model = getattr(resnet_models, cfg.arch)(cfg.num_classes)
+    model.fast_path = cfg.fast_path
+    return model.to(device)
+
+
+class ResNetTrainer:
+    def __init__(self, cfg: ResNetConfig):
+        self.cfg = cfg
+        self.rank, self.world = 0, 1
+        if cfg.distributed or int(os.environ.get("WORLD_SIZE", "1")) > 1:
+            if not pdist.is_dist():
+                pdist.setup_norank()
+            self.rank, self.world = pdist.rank(), pdist.world()
+            cfg.distributed = self.world > 1
+        self.device = default_device()
+        seed_everything(cfg.seed)  # identical init on every rank
+        self.model = build_model(cfg, self.device)
+        self.best_acc, self.start_epoch = ckpt.load_best_performance(self.ckpt_path, cfg.num_classes, cfg.resume)
+        if cfg.resume:
+            ck = ckpt.load_checkpoint(self.ckpt_path)
+            ckpt.load_model_state(self.model, ck["net"])
+        self.meta = None
+        if cfg.meta_learning:
+            self.meta = MetaMixup(cfg.bs, device=self.device, learnable=cfg.learnable_meta)
+        params_owner = self.model if not (self.meta and cfg.learnable_meta) else nn.ModuleList([self.model, self.meta])
+        self.flat = FlatParams(params_owner, device=self.device)
+        self.reducer = None
+        self.fsdp = None
+        if cfg.distributed:
+            if cfg.fsdp:
+                from ..parallel.fsdp import FlatShardedDP
+                self.fsdp = FlatShardedDP(self.flat, self.model)
+            else:
+                from ..parallel.ddp import BucketReducer
+                cdt = {"fp32": None, "bf16": torch.bfloat16}[cfg.comm_dtype]
+                self.reducer = BucketReducer(self.flat, self.model, bucket_mb=cfg.bucket_mb,
+                                             first_bucket_mb=cfg.first_bucket_mb, comm_dtype=cdt)
+        seed_everything(cfg.seed, self.rank)  # per-rank data/mixup randomness
+        self.space = self.fsdp.view if self.fsdp is not None else self.flat
+        self.optimizer, self.scheduler = self._build_optimizer()
+        self.clipper = GradClipper(self.space, sharded=self.fsdp is not None)
+        self.scaler = DeviceGradScaler(self.device, enabled=(cfg.precision == "fp16"))
+        self._build_data()
+        self.meter = DeviceMeter(self.device)
+        self.logger = JsonlLogger(cfg.log_path)
+        self.training_acc, self.testing_acc, self.epoch_time = [], [], []
+        self.global_step = 0
+
+    # ------------------------------------------------------------------ setup
+    @property
+    def ckpt_path(self):
+        return os.path.join(self.cfg.checkpoint_dir, "resnet_ckpt.pth")
+
+    def _lr(self):
+        lr = self.cfg.lr
+        if self.cfg.distributed:
+            if self.cfg.lr_scaling == "faithful4":
+                lr *= 4  # reference hard-codes 4 GPUs (resnet50_test.py:482-485)
+            elif self.cfg.lr_scaling == "world":
+                lr *= self.world
+        return lr
+
+    def _build_optimizer(self):
+        cfg = self.cfg
+        lr = self._lr()
+        kind = cfg.optimizer
+        if kind == "auto":
+            kind = "ngd" if cfg.ngd else "madgrad"
+        if kind == "ngd":
+            wd = 1e-4 if cfg.weight_decay is None else cfg.weight_decay
+            opt = NGD(self.space, lr=lr, momentum=cfg.momentum, weight_decay=wd)
+        elif kind == "madgrad":
+            wd = 5e-6 if cfg.weight_decay is None else cfg.weight_decay
+            opt = MADGRAD(self.space, lr=lr, momentum=cfg.momentum, weight_decay=wd)
+        elif kind == "mirror_madgrad":
+            wd = 0.0 if cfg.weight_decay is None else cfg.weight_decay
+            opt = MirrorMADGRAD(self.space, lr=lr, momentum=cfg.momentum, weight_decay=wd)
+        elif kind == "sgd":
+            wd = 5e-4 if cfg.weight_decay is None else cfg.weight_decay
+            opt = SGD(self.space, lr=lr, momentum=cfg.momentum, weight_decay=wd)
+        elif kind in ("adam", "adamw"):
+            wd = 0.0 if cfg.weight_decay is None else cfg.weight_decay
+            opt = Adam(self.space, lr=lr, weight_decay=wd, adamw=(kind == "adamw"))
+        else:
+            raise ValueError(kind)
+        sched = cfg.scheduler
+        if sched == "auto":
+            sched = "multistep" if kind == "ngd" else "cosine"
+        if sched == "multistep":
+            s = torch.optim.lr_scheduler.MultiStepLR(opt, [10, 20], gamma=0.2)
+        elif sched == "cosine":
+            s = torch.optim.lr_scheduler.CosineAnnealingLR(opt, T_max=200)
+        elif sched.startswith("step"):
+            gamma = float(cfg.extra.get("gamma", 0.75))
+            s = torch.optim.lr_scheduler.StepLR(opt, 2, gamma=gamma)
+        elif sched == "none":
+            s = None
+        else:
+            raise ValueError(sched)
+        return opt, s
+
+    def _build_data(self):
+        cfg = self.cfg
+        if cfg.synthetic:
+            tr = synthetic_cifar(50000, cfg.num_classes, seed=1)
+            te = synthetic_cifar(10000, cfg.num_classes, seed=2)
+        else:
+            if self.rank == 0:
+                CIFAR10(cfg.data_root, train=True, download=True)
+            pdist.barrier()
+            a, b = CIFAR10(cfg.data_root, train=True), CIFAR10(cfg.data_root, train=False)
+            tr, te = (a.data, a.targets), (b.data, b.targets)
+        sub = cfg.extra.get("subset_stride")  # tuning: strided 10% subset (C7)
+        if sub:
+            tr = (tr[0][::sub], tr[1][::sub])
+            te = (te[0][::sub], te[1][::sub])
+        self.train_loader = DeviceCIFARLoader(tr[0], tr[1], cfg.bs, self.device, train=True, rank=self.rank,
+                                              world_size=self.world, seed=cfg.seed)
+        # eval: every rank evaluates the full test set like the reference (no sharding)
+        self.test_loader = DeviceCIFARLoader(te[0], te[1], cfg.bs, self.device, train=False, shuffle=False,
+                                             drop_last=False)
+
+    # ------------------------------------------------------------------ steps
+    def _autocast(self):
+        p = self.cfg.precision
+        if p == "fp32":
+            return torch.autocast(self.device.type, enabled=False)
+        dt = torch.bfloat16 if p == "bf16" else torch.float16
+        return torch.autocast(self.device.type, dtype=dt, enabled=(self.device.type == "cuda" or p == "bf16"))
+
+    def train_step(self, x, y):
+        cfg = self.cfg
+        if self.meta is not None:
+            x, ya, yb, lam = self.meta(x, y)
+        else:
+            x, ya, yb, lam = mixup_data(x, y, cfg.alpha)
+        with self._autocast():
+            out = self.model(x)
+            if self.meta is not None:
+                loss = mixup_criterion_meta(None, out, ya, yb, lam, faithful=cfg.faithful)
+            else:
+                loss = mixup_criterion(None, out, ya, yb, lam)
+        self.scaler.scale_loss(loss).backward()
+        if self.reducer is not None:
+            self.reducer.finish()
+        if self.fsdp is not None:
+            self.fsdp.finish_backward()
+        fp16 = self.scaler.enabled
+        self.clipper(cfg.clip, inv_scale=self.scaler.inv_scale(), check_inf=fp16)
+        found = None
+        if fp16:
+            self.scaler.sync_found_inf(self.clipper.found_inf)
+            found = self.clipper.found_inf
+        self.optimizer.step(grad_scale=self.clipper.coef, found_inf=found)
+        if fp16:
+            self.scaler.update(found)
+        if self.fsdp is not None:
+            self.fsdp.after_step()
+        self.meter.update(loss, out.detach(), ya, yb, lam.detach() if isinstance(lam, torch.Tensor) else lam)
+        self.global_step += 1
+        return loss
+
+    def train_epoch(self, epoch):
+        self.model.train()
+        self.meter.reset()
+        self.train_loader.set_epoch(epoch)  # Q10 fix
+        if self.reducer is not None and self.reducer.broadcast_buffers:
+            self.reducer.sync_buffers()
+        if self.device.type == "cuda":
+            torch.cuda.synchronize()
+            torch.cuda.reset_peak_memory_stats()
+        t0 = time.monotonic()
+        n = 0
+        for i, (x, y) in enumerate(self.train_loader):
+            if self.cfg.steps_per_epoch and i >= self.cfg.steps_per_epoch:
+                break
+            self.train_step(x, y)
+            n += 1
+        if self.device.type == "cuda":
+            torch.cuda.synchronize()
+        dt = time.monotonic() - t0
+        m = self.meter.reduced()
+        imgs = n * self.cfg.bs * self.world
+        rec = dict(epoch=epoch, steps=n, epoch_time_s=dt, img_per_s=imgs / max(dt, 1e-9), train_loss=m["loss"],
+                   train_acc=m["acc"], peak_mem_gb=peak_memory_gb(), lr=self.optimizer.group["lr"])
+        print0(f"epoch {epoch}: {n} steps in {dt:.2f}s ({rec['img_per_s']:.0f} img/s) loss {m['loss']:.4f} "
+               f"acc {m['acc']:.2f}%  peak mem {rec['peak_mem_gb']:.2f} GB")
+        self.logger.log(**rec)
+        self.training_acc.append(m["acc"])
+        self.epoch_time.append(dt)
+        return rec
+
+    @torch.no_grad()
+    def test(self, epoch):
+        self.model.eval()
+        correct = torch.zeros((), device=self.device)
+        total = torch.zeros((), device=self.device)
+        loss_sum = torch.zeros((), device=self.device)
+        crit = nn.CrossEntropyLoss(reduction="sum")
+        for x, y in self.test_loader:
+            with self._autocast():
+                out = self.model(x)
+            loss_sum += crit(out.float(), y)
+            correct += (out.argmax(1) == y).sum()
+            total += y.numel()
+        acc = 100.0 * float(correct) / max(float(total), 1.0)
+        self.testing_acc.append(acc)
+        print0(f"test epoch {epoch}: acc {acc:.2f}% loss {float(loss_sum) / max(float(total), 1):.4f}")
+        if acc > self.best_acc:
+            prefix = self.cfg.distributed or (not self.cfg.distributed and self.cfg.faithful)
+            extra = {"optimizer": self.optimizer.state_dict()} if self.cfg.extra.get("save_optimizer") else None
+            ckpt.save_checkpoint(self.ckpt_path, self.model, acc, epoch, module_prefix=prefix, extra=extra)
+            self.best_acc = acc
+        self.logger.log(epoch=epoch, test_acc=acc)
+        return acc
+
+    def fit(self):
+        for epoch in range(self.start_epoch, self.start_epoch + self.cfg.epoch):
+            self.train_epoch(epoch)
+            if self.cfg.eval:
+                self.test(epoch)
+            if self.scheduler is not None:
+                self.scheduler.step()
+        if self.cfg.plot:
+            xs = np.arange(self.start_epoch, self.start_epoch + len(self.training_acc))
+            if self.testing_acc:
+                draw_graph([xs, xs], [self.training_acc, self.testing_acc], ["training", "testing"],
+                           "Resnet accuracy curve", "accuracy")
+            draw_graph(xs, self.epoch_time, "training time", "Resnet time for training", "time(sec.)")
+        return self
+
+
+def main_ddp(cfg: ResNetConfig):
+    t = ResNetTrainer(cfg).fit()
+    pdist.cleanup()
+    return t

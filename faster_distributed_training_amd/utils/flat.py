@@ -1,0 +1,115 @@
+"""Flat parameter / gradient storage.
+
+All trainable parameters of a model are re-homed into ONE contiguous fp32 buffer
+(``FlatParams.data``) and their gradients into another (``FlatParams.grad``); every
+``p.data`` / ``p.grad`` becomes a view.  Consequences on MI355X:
+
+* optimizers (``optim/``), gradient clipping and AMP unscale are single fused HIP
+  launches over the whole model (23.5M elements for ResNet-50) instead of
+  69 tensors x several ops;
+* the DDP reducer's buckets are contiguous slices of ``grad`` (gradient-as-bucket-view,
+  no flatten/unflatten copies), laid out in *reverse* registration order so they fill
+  in backward order;
+* FSDP shards and checkpoint I/O are slices of the same buffer;
+* an optional bf16 shadow copy (``shadow``) is rewritten by the optimizer kernel itself
+  so compute kernels read bf16 weights without a per-step cast pass.
+
+``p.grad`` must never be replaced (no ``zero_grad(set_to_none=True)``): use
+``FlatParams.zero_grad()``; autograd then accumulates in place into the views.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+
+import torch
+import torch.nn as nn
+
+ALIGN = 64  # elements; keeps every view 256-B aligned for 16-B vector access
+
+
+@dataclass
+class Slot:
+    name: str
+    param: nn.Parameter
+    offset: int
+    numel: int
+    shape: torch.Size
+
+
+class FlatParams:
+    def __init__(self, module_or_params, device=None, reverse=True, with_shadow=False, names=None):
+        if isinstance(module_or_params, nn.Module):
+            named = [(n, p) for n, p in module_or_params.named_parameters() if p.requires_grad]
+        else:
+            plist = list(module_or_params)
+            named = [(names[i] if names else f"p{i}", p) for i, p in enumerate(plist)]
+        if reverse:
+            named = named[::-1]
+        self.slots: list[Slot] = []
+        off = 0
+        for n, p in named:
+            k = p.numel()
+            self.slots.append(Slot(n, p, off, k, p.shape))
+            off += (k + ALIGN - 1) // ALIGN * ALIGN
+        self.numel = off
+        dev = device if device is not None else (named[0][1].device if named else torch.device("cpu"))
+        self.device = torch.device(dev)
+        self.data = torch.zeros(self.numel, device=self.device, dtype=torch.float32)
+        self.grad = torch.zeros(self.numel, device=self.device, dtype=torch.float32)
+        self.shadow = torch.zeros(self.numel, device=self.device, dtype=torch.bfloat16) if with_shadow else None
+        with torch.no_grad():
+            for s in self.slots:
+                v = self.data[s.offset:s.offset + s.numel].view(s.shape)
+                v.copy_(s.param.data.to(self.device, torch.float32))
+                s.param.data = v
+                s.param.grad = self.grad[s.offset:s.offset + s.numel].view(s.shape)
+        self.refresh_shadow()
+        self._by_param = {id(s.param): s for s in self.slots}
+
+    # ------------------------------------------------------------------ helpers
+    @property
+    def params(self):
+        return [s.param for s in self.slots]
+
+    def slot_of(self, p) -> Slot:
+        return self._by_param[id(p)]
+
+    def grad_view(self, p):
+        s = self.slot_of(p)
+        return self.grad[s.offset:s.offset + s.numel].view(s.shape)
+
+    def shadow_view(self, p):
+        if self.shadow is None:
+            return None
+        s = self.slot_of(p)
+        return self.shadow[s.offset:s.offset + s.numel].view(s.shape)
+
+    def zero_grad(self):
+        self.grad.zero_()
+        self.rebind_grads()
+
+    def rebind_grads(self):
+        """Re-attach grad views if something replaced ``p.grad`` (e.g. a foreign
+        ``zero_grad(set_to_none=True)``)."""
+        for s in self.slots:
+            g = s.param.grad
+            want = self.grad[s.offset:s.offset + s.numel]
+            if g is None or g.data_ptr() != want.data_ptr():
+                if g is not None:
+                    want.view(s.shape).copy_(g)
+                s.param.grad = want.view(s.shape)
+
+    def refresh_shadow(self):
+        if self.shadow is not None:
+            with torch.no_grad():
+                self.shadow.copy_(self.data)
+
+    def load_from_params(self):
+        """Re-sync after params were assigned new storage (e.g. load_state_dict on a
+        module whose params were replaced)."""
+        with torch.no_grad():
+            for s in self.slots:
+                if s.param.data.data_ptr() != self.data[s.offset:].data_ptr():
+                    self.data[s.offset:s.offset + s.numel].copy_(s.param.data.reshape(-1))
+                    s.param.data = self.data[s.offset:s.offset + s.numel].view(s.shape)
+        self.refresh_shadow()
