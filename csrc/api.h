@@ -4,6 +4,7 @@
 // allocation-free and graph-capture safe.
 #pragma once
 #include <cstdint>
+#include <vector>
 
 namespace fdt {
 // bn_kernels.hip
@@ -67,4 +68,21 @@ void augment(uint64_t src, uint64_t idx, uint64_t labels_src, uint64_t labels_ou
              int C, int Cout, int pad, int do_flip, uint64_t rng, float m0, float m1, float m2, float s0, float s1,
              float s2, int nchw, int dt_out, uint64_t stream);
 void rng_advance(uint64_t rng, uint64_t stream);
+// conv_igemm.hip
+void conv_igemm(uint64_t x, uint64_t x2, uint64_t ps, uint64_t pt, uint64_t w, uint64_t out, uint64_t part,
+                uint64_t ex, uint64_t es, uint64_t et, long Nb, int Hi, int Wi, int Cx, int Ho, int Wo, int S,
+                const std::vector<int>& dh, const std::vector<int>& dw, const std::vector<int>& wt, int Cout, int ldw,
+                int Hout, int Wout, int OS, int oy, int ox, int pro, int pro_act, float pro_alpha, int epi, int epi_act,
+                float epi_alpha, int BM, int BN, uint64_t stream);
+int conv_num_row_blocks(long M, int BM);
+// conv_wgrad.hip
+void conv_wgrad(uint64_t g, uint64_t y, uint64_t al, uint64_t be, uint64_t x, uint64_t xs, uint64_t xt, uint64_t slab,
+                long Nb, int Hi, int Wi, int Cx, int Ho, int Wo, int S, const std::vector<int>& dh,
+                const std::vector<int>& dw, int Cout, int ldw, int act, float act_alpha, int BM, int BN, int nsplit,
+                uint64_t stream);
+void wgrad_reduce(uint64_t slab, uint64_t out, int nsplit, int Cout, int Cin, int ntaps, int Cxp, int accumulate,
+                  uint64_t stream);
+void pack_weights(const std::vector<uint64_t>& src, const std::vector<uint64_t>& wf, const std::vector<uint64_t>& wd,
+                  const std::vector<int>& cout, const std::vector<int>& cin, const std::vector<int>& cxp,
+                  const std::vector<int>& ntaps, uint64_t stream);
 }  // namespace fdt

@@ -4,6 +4,7 @@
 // load next to any torch on the box.  Python wrappers in faster_distributed_training_amd/ops
 // validate shapes/dtypes on the host before calling in.
 #include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
 
 #include "api.h"
 #include "runtime/runtime_api.h"
@@ -25,6 +26,12 @@ PYBIND11_MODULE(_fdt_native, m) {
   DEF(affine_fold);
   DEF(residual_act_fwd);
   DEF(residual_act_bwd);
+  // implicit-GEMM convolution engine
+  DEF(conv_igemm);
+  DEF(conv_num_row_blocks);
+  DEF(conv_wgrad);
+  DEF(wgrad_reduce);
+  DEF(pack_weights);
   // optimizers
   DEF(grad_sumsq);
   DEF(grad_norm_finalize);

@@ -1,0 +1,552 @@
+// Implicit-GEMM convolution for the NHWC ResNet engine on MI355X (gfx950 / CDNA4).
+//
+// One kernel template covers every forward convolution and every data-gradient
+// (dgrad) convolution of the network:
+//
+//   C^T[ch][px] = sum_k  W[ch][k] * X[px][k],   k = (tap, ci),  px = output pixel
+//
+// The weight tile is the MFMA "A" operand (rows = output channels) and the activation
+// tile the "B" operand (columns = pixels), so an accumulator lane holds 4-channel runs
+// of ONE pixel: after a permlane32 swap every lane owns 8 consecutive channels of one
+// NHWC row and the epilogue reads/writes 16 B per lane (T21).  mfma_f32_32x32x16_bf16,
+// 4 waves (2 x 2) per 256-thread workgroup, BK = 64-element K tiles double-buffered in
+// LDS with register-staged prefetch (loads for tile k+1 are issued before the MFMAs of
+// tile k, the prologue math and LDS write happen after them, one barrier per tile),
+// XOR-swizzled LDS rows (conflict-free ds_read_b128 for the fragment reads), XCD-aware
+// workgroup remap so tiles sharing activation rows sit on one L2.
+//
+// Fusion (the reason this is not a library call):
+//  * prologue on the activation operand, applied while staging to LDS:
+//      PRO_AFFINE_ACT  x -> act(x*s[c] + t[c])   (the producer's lazy batch-norm)
+//      PRO_FOLD        g -> g + alpha[c] + beta[c]*y  (batch-norm backward correction)
+//    zero padding is applied AFTER the transform (the conv pads the normalised input);
+//  * epilogue:
+//      EPI_STATS   y (bf16) + per-block per-channel (sum y, sum y^2) slabs -> BN stats
+//      EPI_ACTBWD  dgrad through the producer's lazy act(x*s+t): gx = g*act'(z)*s and
+//                  per-channel (sum g_pre*x, sum g_pre) slabs
+//      EPI_STORE / EPI_ADD  plain bf16 store / accumulate into an existing gradient.
+//
+// Strided convolutions: forward uses the input stride S; the dgrad of a stride-2
+// convolution is split by output parity into 4 dense classes (each its own tap table and
+// output row map: hi = ho*OS + oy), so no MFMA work is spent on structural zeros.
+//
+// Reference semantics being accelerated: resnet.py:72-113 (FusedConvBN forward and its
+// hand-derived backward), resnet.py:201-227 (strided conv + BatchNorm2d blocks).
+#include "common.h"
+#include <vector>
+
+namespace fdt {
+namespace conv {
+
+typedef short bf16x8_t __attribute__((ext_vector_type(8)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+enum Pro : int { kProNone = 0, kProAffineAct = 1, kProFold = 2 };
+enum Epi : int { kEpiStats = 0, kEpiActBwd = 1, kEpiStore = 2, kEpiAdd = 3 };
+
+struct ConvArgs {
+  const bf16* x;     // activation operand [Nb][Hi][Wi][Cx]   (PRO_FOLD: the gradient G)
+  const bf16* x2;    // PRO_FOLD: the producer output Y (same shape as x)
+  const float* ps;   // prologue per-channel scale: s (AFFINE_ACT) or alpha (FOLD)   [Cx]
+  const float* pt;   // prologue per-channel shift: t (AFFINE_ACT) or beta  (FOLD)   [Cx]
+  const bf16* w;     // packed weights [Cout][ldw], k-index = wt[tap]*Cx + ci
+  bf16* out;         // [Nb][Hout][Wout][Cout]
+  float* part;       // per-block partial slabs [nbm][2][Cout]
+  const bf16* ex;    // ACTBWD: producer raw output x (shape of out); ADD: unused (out is read)
+  const float* es;   // ACTBWD: producer scale s [Cout]
+  const float* et;   // ACTBWD: producer shift t [Cout]
+  long M;            // Nb*Ho*Wo GEMM rows
+  int Hi, Wi, Cx, log2Cx;
+  int Ho, Wo, S;
+  int ntaps, K, Cout, ldw;
+  int Hout, Wout, OS, oy, ox;
+  int pro_act;
+  float pro_alpha;
+  int epi_act;
+  float epi_alpha;
+  int nbm, nbn;
+  int8_t dh[12], dw[12], wt[12];
+};
+
+__device__ __forceinline__ uint32_t pk_bf16(float lo, float hi) { return pack_bf16x2(lo, hi); }
+
+template <int CPR>
+__device__ __forceinline__ int swz(int row) {
+  // conflict-free ds_read_b128 of one 16-B chunk from 32 consecutive rows (see file header)
+  if constexpr (CPR == 8) return (row >> 1) & 7;
+  else return (row >> 2) & 3;
+}
+
+__device__ __forceinline__ int xcd_remap(int bid, int nblk) {
+  const int q = nblk >> 3, r = nblk & 7, xcd = bid & 7;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+}
+
+// Reduce-scatter of 16 per-lane values across the 32 lanes of each wave half:
+// on return lane l holds the half-sum of value index (l >> 1) & 15.
+__device__ __forceinline__ float rs16(float (&v)[16], int lane) {
+  float w8[8], w4[4], w2[2];
+  const bool b4 = lane & 16, b3 = lane & 8, b2 = lane & 4, b1 = lane & 2;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    float send = b4 ? v[j] : v[j + 8];
+    float keep = b4 ? v[j + 8] : v[j];
+    w8[j] = keep + __shfl_xor(send, 16, 64);
+  }
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    float send = b3 ? w8[j] : w8[j + 4];
+    float keep = b3 ? w8[j + 4] : w8[j];
+    w4[j] = keep + __shfl_xor(send, 8, 64);
+  }
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    float send = b2 ? w4[j] : w4[j + 2];
+    float keep = b2 ? w4[j + 2] : w4[j];
+    w2[j] = keep + __shfl_xor(send, 4, 64);
+  }
+  float send = b1 ? w2[0] : w2[1];
+  float keep = b1 ? w2[1] : w2[0];
+  float w1 = keep + __shfl_xor(send, 2, 64);
+  return w1 + __shfl_xor(w1, 1, 64);
+}
+
+__device__ __forceinline__ void swap32(float& a, float& b) {
+  auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(a), __float_as_uint(b), false, false);
+  a = __uint_as_float(r[0]);
+  b = __uint_as_float(r[1]);
+}
+
+template <int BM, int BN, int BK, int PRO, int EPI, bool PURE>
+__global__ __launch_bounds__(256) void igemm_kernel(const ConvArgs a) {
+  constexpr int CPR = BK / 8;        // 16-B chunks per LDS row
+  constexpr int RPR = 256 / CPR;     // rows covered by one load round
+  constexpr int NXL = BM / RPR;      // activation chunks per thread per tile
+  constexpr int NWL = BN / RPR;      // weight chunks per thread per tile
+  constexpr int TM = BM / 64, TN = BN / 64;
+  constexpr int XT = BM * BK, WT = BN * BK;
+  static_assert(NXL >= 1 && NWL >= 1, "tile too small for 256 threads");
+
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  bf16* tiles = reinterpret_cast<bf16*>(smem);                       // [2][WT + XT]
+  float* pst = reinterpret_cast<float*>(smem + 2 * (XT + WT) * 2);   // [2][Cx] (PRO != none)
+  float* red = pst + (PRO != kProNone ? 2 * a.Cx : 0);               // [2 waves][2][BN]
+  int* tapt = reinterpret_cast<int*>(red + 4 * BN);                  // [12]: dh | dw<<8 | wt<<16
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wn = wid & 1, wm = wid >> 1;
+  const int id = xcd_remap(blockIdx.x, a.nbm * a.nbn);
+  const int bn = id % a.nbn, bm = id / a.nbn;
+  const long m0 = (long)bm * BM;
+  const int n0 = bn * BN;
+
+  if constexpr (PRO != kProNone) {
+    for (int i = tid; i < a.Cx; i += 256) {
+      pst[i] = a.ps[i];
+      pst[a.Cx + i] = a.pt[i];
+    }
+  }
+  if (tid < 12) tapt[tid] = (int)(uint8_t)a.dh[tid] | ((int)(uint8_t)a.dw[tid] << 8) | ((int)(uint8_t)a.wt[tid] << 16);
+
+  // ---- per-thread activation rows (fixed across K tiles)
+  const int cc = tid % CPR;  // this thread's 16-B chunk column inside a K tile
+  long xrow[NXL];            // PURE: pixel index; else n*Hi (row base)
+  int ohs[NXL], ows[NXL];
+  bool rv[NXL];
+#pragma unroll
+  for (int j = 0; j < NXL; ++j) {
+    const long m = m0 + tid / CPR + j * RPR;
+    rv[j] = m < a.M;
+    if constexpr (PURE) {
+      xrow[j] = m;
+      ohs[j] = ows[j] = 0;
+    } else {
+      const long hw = (long)a.Ho * a.Wo;
+      const long n = m / hw;
+      const int rem = (int)(m - n * hw);
+      const int oh = rem / a.Wo, ow = rem - (rem / a.Wo) * a.Wo;
+      xrow[j] = n * a.Hi;
+      ohs[j] = oh * a.S;
+      ows[j] = ow * a.S;
+    }
+  }
+  __syncthreads();
+
+  uint4 rx[NXL], rx2[PRO == kProFold ? NXL : 1], rw[NWL];
+  bool xv[NXL];
+  int kci = 0;  // channel index of this thread's chunk in the tile being staged
+
+  auto load_tile = [&](int kt) {
+    const int k = kt * BK + cc * 8;
+    const int tap = k >> a.log2Cx;
+    const int ci = k & (a.Cx - 1);
+    kci = ci;
+    const bool tok = tap < a.ntaps;
+    int dh = 0, dw = 0, wt = 0;
+    if (!PURE && tok) {
+      const int e = tapt[tap];
+      dh = (int)(int8_t)(e & 0xff);
+      dw = (int)(int8_t)((e >> 8) & 0xff);
+      wt = (e >> 16) & 0xff;
+    }
+#pragma unroll
+    for (int j = 0; j < NXL; ++j) {
+      bool v = rv[j] && tok;
+      long off;
+      if constexpr (PURE) {
+        off = xrow[j] * a.Cx + ci;
+      } else {
+        const int ih = ohs[j] + dh, iw = ows[j] + dw;
+        v = v && (unsigned)ih < (unsigned)a.Hi && (unsigned)iw < (unsigned)a.Wi;
+        off = ((xrow[j] + ih) * a.Wi + iw) * a.Cx + ci;
+      }
+      xv[j] = v;
+      if (v) {
+        rx[j] = *reinterpret_cast<const uint4*>(a.x + off);
+        if constexpr (PRO == kProFold) rx2[j] = *reinterpret_cast<const uint4*>(a.x2 + off);
+      } else {
+        rx[j] = make_uint4(0, 0, 0, 0);
+        if constexpr (PRO == kProFold) rx2[j] = make_uint4(0, 0, 0, 0);
+      }
+    }
+    const long wk = (long)(PURE ? 0 : wt) * a.Cx + ci;
+#pragma unroll
+    for (int j = 0; j < NWL; ++j) {
+      const int row = tid / CPR + j * RPR;
+      if (tok) rw[j] = *reinterpret_cast<const uint4*>(a.w + (long)(n0 + row) * a.ldw + wk);
+      else rw[j] = make_uint4(0, 0, 0, 0);
+    }
+  };
+
+  auto store_tile = [&](int buf) {
+    bf16* Wl = tiles + buf * (WT + XT);
+    bf16* Xl = Wl + WT;
+#pragma unroll
+    for (int j = 0; j < NWL; ++j) {
+      const int row = tid / CPR + j * RPR;
+      *reinterpret_cast<uint4*>(Wl + row * BK + 8 * (cc ^ swz<CPR>(row))) = rw[j];
+    }
+    float sv[8], tv[8];
+    if constexpr (PRO != kProNone) {
+      const float4* sp = reinterpret_cast<const float4*>(pst + kci);
+      const float4* tp = reinterpret_cast<const float4*>(pst + a.Cx + kci);
+      float4 s0 = sp[0], s1 = sp[1], t0 = tp[0], t1 = tp[1];
+      sv[0] = s0.x; sv[1] = s0.y; sv[2] = s0.z; sv[3] = s0.w; sv[4] = s1.x; sv[5] = s1.y; sv[6] = s1.z; sv[7] = s1.w;
+      tv[0] = t0.x; tv[1] = t0.y; tv[2] = t0.z; tv[3] = t0.w; tv[4] = t1.x; tv[5] = t1.y; tv[6] = t1.z; tv[7] = t1.w;
+    }
+#pragma unroll
+    for (int j = 0; j < NXL; ++j) {
+      const int row = tid / CPR + j * RPR;
+      uint4 o = rx[j];
+      if constexpr (PRO == kProAffineAct) {
+        if (xv[j]) {
+          float v[8];
+          const uint32_t u[4] = {o.x, o.y, o.z, o.w};
+#pragma unroll
+          for (int q = 0; q < 4; ++q) { v[2 * q] = bf16_lo(u[q]); v[2 * q + 1] = bf16_hi(u[q]); }
+#pragma unroll
+          for (int q = 0; q < 8; ++q) v[q] = act_fwd(fmaf(v[q], sv[q], tv[q]), a.pro_act, a.pro_alpha);
+          o = make_uint4(pk_bf16(v[0], v[1]), pk_bf16(v[2], v[3]), pk_bf16(v[4], v[5]), pk_bf16(v[6], v[7]));
+        }
+      } else if constexpr (PRO == kProFold) {
+        if (xv[j]) {
+          float g[8], y[8];
+          const uint32_t u[4] = {o.x, o.y, o.z, o.w};
+          const uint32_t uy[4] = {rx2[j].x, rx2[j].y, rx2[j].z, rx2[j].w};
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            g[2 * q] = bf16_lo(u[q]); g[2 * q + 1] = bf16_hi(u[q]);
+            y[2 * q] = bf16_lo(uy[q]); y[2 * q + 1] = bf16_hi(uy[q]);
+          }
+#pragma unroll
+          for (int q = 0; q < 8; ++q) g[q] += fmaf(tv[q], y[q], sv[q]);  // g + alpha + beta*y
+          o = make_uint4(pk_bf16(g[0], g[1]), pk_bf16(g[2], g[3]), pk_bf16(g[4], g[5]), pk_bf16(g[6], g[7]));
+        }
+      }
+      *reinterpret_cast<uint4*>(Xl + row * BK + 8 * (cc ^ swz<CPR>(row))) = o;
+    }
+  };
+
+  f32x16 acc[TN][TM];
+#pragma unroll
+  for (int i = 0; i < TN; ++i)
+#pragma unroll
+    for (int j = 0; j < TM; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  const int nkt = (a.K + BK - 1) / BK;
+  if (nkt > 0) {
+    load_tile(0);
+    store_tile(0);
+    __syncthreads();
+  }
+  for (int kt = 0; kt < nkt; ++kt) {
+    const int buf = kt & 1;
+    if (kt + 1 < nkt) load_tile(kt + 1);
+    const bf16* Wl = tiles + buf * (WT + XT);
+    const bf16* Xl = Wl + WT;
+#pragma unroll
+    for (int ks = 0; ks < BK / 16; ++ks) {
+      const int ch = ks * 2 + (lane >> 5);
+      bf16x8_t wf[TN], xf[TM];
+#pragma unroll
+      for (int i = 0; i < TN; ++i) {
+        const int row = wn * (BN / 2) + i * 32 + (lane & 31);
+        wf[i] = *reinterpret_cast<const bf16x8_t*>(Wl + row * BK + 8 * (ch ^ swz<CPR>(row)));
+      }
+#pragma unroll
+      for (int j = 0; j < TM; ++j) {
+        const int row = wm * (BM / 2) + j * 32 + (lane & 31);
+        xf[j] = *reinterpret_cast<const bf16x8_t*>(Xl + row * BK + 8 * (ch ^ swz<CPR>(row)));
+      }
+#pragma unroll
+      for (int i = 0; i < TN; ++i)
+#pragma unroll
+        for (int j = 0; j < TM; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wf[i], xf[j], acc[i][j], 0, 0, 0);
+    }
+    if (kt + 1 < nkt) store_tile(buf ^ 1);
+    __syncthreads();
+  }
+
+  // ------------------------------------------------------------------ epilogue
+  const int h = lane >> 5;
+  long orow[TM];
+  bool ov[TM];
+#pragma unroll
+  for (int j = 0; j < TM; ++j) {
+    const long m = m0 + wm * (BM / 2) + j * 32 + (lane & 31);
+    ov[j] = m < a.M;
+    if (a.OS == 1 && a.oy == 0 && a.ox == 0 && a.Hout == a.Ho && a.Wout == a.Wo) {
+      orow[j] = m;
+    } else {
+      const long hw = (long)a.Ho * a.Wo;
+      const long n = m / hw;
+      const int rem = (int)(m - n * hw);
+      const int oh = rem / a.Wo, ow = rem - (rem / a.Wo) * a.Wo;
+      orow[j] = (n * a.Hout + oh * a.OS + a.oy) * a.Wout + ow * a.OS + a.ox;
+    }
+  }
+
+  if constexpr (EPI == kEpiStats) {
+#pragma unroll
+    for (int i = 0; i < TN; ++i) {
+      float s1[16], s2[16];
+#pragma unroll
+      for (int r = 0; r < 16; ++r) { s1[r] = 0.f; s2[r] = 0.f; }
+      const int cb = n0 + wn * (BN / 2) + i * 32;
+#pragma unroll
+      for (int j = 0; j < TM; ++j) {
+        float c[16];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          c[r] = acc[i][j][r];
+          s1[r] += c[r];
+          s2[r] = fmaf(c[r], c[r], s2[r]);
+        }
+#pragma unroll
+        for (int p = 0; p < 2; ++p) {
+          const int g = 2 * p;
+          uint32_t a0 = pk_bf16(c[4 * g], c[4 * g + 1]), a1 = pk_bf16(c[4 * g + 2], c[4 * g + 3]);
+          uint32_t b0 = pk_bf16(c[4 * g + 4], c[4 * g + 5]), b1 = pk_bf16(c[4 * g + 6], c[4 * g + 7]);
+          auto r0 = __builtin_amdgcn_permlane32_swap(a0, b0, false, false);
+          auto r1 = __builtin_amdgcn_permlane32_swap(a1, b1, false, false);
+          if (ov[j])
+            *reinterpret_cast<uint4*>(a.out + orow[j] * a.Cout + cb + 8 * g + 8 * h) =
+                make_uint4(r0[0], r1[0], r0[1], r1[1]);
+        }
+      }
+      const float t1 = rs16(s1, lane), t2 = rs16(s2, lane);
+      if ((lane & 1) == 0) {
+        const int r = (lane >> 1) & 15;
+        const int cl = wn * (BN / 2) + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+        red[(wm * 2 + 0) * BN + cl] = t1;
+        red[(wm * 2 + 1) * BN + cl] = t2;
+      }
+    }
+    __syncthreads();
+    for (int e = tid; e < 2 * BN; e += 256) {
+      const int q = e / BN, c = e - q * BN;
+      a.part[((long)bm * 2 + q) * a.Cout + n0 + c] = red[q * BN + c] + red[(2 + q) * BN + c];
+    }
+  } else if constexpr (EPI == kEpiActBwd) {
+#pragma unroll
+    for (int i = 0; i < TN; ++i) {
+      float s1[16], s0[16];
+#pragma unroll
+      for (int r = 0; r < 16; ++r) { s1[r] = 0.f; s0[r] = 0.f; }
+      const int cb = n0 + wn * (BN / 2) + i * 32;
+#pragma unroll
+      for (int j = 0; j < TM; ++j) {
+#pragma unroll
+        for (int p = 0; p < 2; ++p) {
+          const int g = 2 * p;
+          float v[8];
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            float lo = acc[i][j][4 * g + q], hi = acc[i][j][4 * g + 4 + q];
+            swap32(lo, hi);
+            v[q] = lo;
+            v[4 + q] = hi;
+          }
+          const int c = cb + 8 * g + 8 * h;
+          if (ov[j]) {
+            float xv8[8], sv[8], tv[8], o[8];
+            Vec8<bf16>::load(a.ex + orow[j] * a.Cout + c, xv8);
+            const float4* sp = reinterpret_cast<const float4*>(a.es + c);
+            const float4* tp = reinterpret_cast<const float4*>(a.et + c);
+            float4 sa = sp[0], sb = sp[1], ta = tp[0], tb = tp[1];
+            sv[0] = sa.x; sv[1] = sa.y; sv[2] = sa.z; sv[3] = sa.w; sv[4] = sb.x; sv[5] = sb.y; sv[6] = sb.z; sv[7] = sb.w;
+            tv[0] = ta.x; tv[1] = ta.y; tv[2] = ta.z; tv[3] = ta.w; tv[4] = tb.x; tv[5] = tb.y; tv[6] = tb.z; tv[7] = tb.w;
+#pragma unroll
+            for (int q = 0; q < 8; ++q) {
+              const float z = fmaf(xv8[q], sv[q], tv[q]);
+              const float gp = v[q] * act_grad(z, a.epi_act, a.epi_alpha);
+              o[q] = gp * sv[q];
+              s1[p * 8 + q] = fmaf(gp, xv8[q], s1[p * 8 + q]);
+              s0[p * 8 + q] += gp;
+            }
+            Vec8<bf16>::store(a.out + orow[j] * a.Cout + c, o);
+          }
+        }
+      }
+      const float t1 = rs16(s1, lane), t0 = rs16(s0, lane);
+      if ((lane & 1) == 0) {
+        const int r = (lane >> 1) & 15;
+        const int cl = wn * (BN / 2) + i * 32 + 16 * (r >> 3) + 8 * h + (r & 7);
+        red[(wm * 2 + 0) * BN + cl] = t1;
+        red[(wm * 2 + 1) * BN + cl] = t0;
+      }
+    }
+    __syncthreads();
+    for (int e = tid; e < 2 * BN; e += 256) {
+      const int q = e / BN, c = e - q * BN;
+      a.part[((long)bm * 2 + q) * a.Cout + n0 + c] = red[q * BN + c] + red[(2 + q) * BN + c];
+    }
+  } else {  // STORE / ADD
+#pragma unroll
+    for (int i = 0; i < TN; ++i) {
+      const int cb = n0 + wn * (BN / 2) + i * 32;
+#pragma unroll
+      for (int j = 0; j < TM; ++j) {
+#pragma unroll
+        for (int p = 0; p < 2; ++p) {
+          const int g = 2 * p;
+          float v[8];
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            float lo = acc[i][j][4 * g + q], hi = acc[i][j][4 * g + 4 + q];
+            swap32(lo, hi);
+            v[q] = lo;
+            v[4 + q] = hi;
+          }
+          const int c = cb + 8 * g + 8 * h;
+          if (ov[j]) {
+            bf16* dst = a.out + orow[j] * a.Cout + c;
+            if constexpr (EPI == kEpiAdd) {
+              float e8[8];
+              Vec8<bf16>::load(dst, e8);
+#pragma unroll
+              for (int q = 0; q < 8; ++q) v[q] += e8[q];
+            }
+            Vec8<bf16>::store(dst, v);
+          }
+        }
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------- host side
+struct Cfg {
+  int BM, BN;
+};
+
+template <int BM, int BN, int PRO, int EPI, bool PURE>
+static void launch_one(const ConvArgs& a, size_t lds, hipStream_t st) {
+  auto kern = igemm_kernel<BM, BN, 64, PRO, EPI, PURE>;
+  static size_t attr_set = 64 * 1024;  // default dynamic-LDS limit; raise only when needed
+  if (lds > attr_set) {
+    FDT_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                      (int)lds));
+    attr_set = lds;
+  }
+  hipLaunchKernelGGL(kern, dim3(a.nbm * a.nbn), dim3(256), lds, st, a);
+  FDT_LAUNCH_CHECK();
+}
+
+template <int BM, int BN, int PRO, int EPI>
+static void launch_pure(const ConvArgs& a, bool pure, size_t lds, hipStream_t st) {
+  if (pure) launch_one<BM, BN, PRO, EPI, true>(a, lds, st);
+  else launch_one<BM, BN, PRO, EPI, false>(a, lds, st);
+}
+
+template <int PRO, int EPI>
+static void launch_tile(const ConvArgs& a, int BM, int BN, bool pure, hipStream_t st) {
+  size_t lds = (size_t)2 * (BM + BN) * 64 * 2 + (PRO != kProNone ? 2 * a.Cx * 4 : 0) + 4 * BN * 4 + 64;
+  if (BM == 128 && BN == 128) launch_pure<128, 128, PRO, EPI>(a, pure, lds, st);
+  else if (BM == 128 && BN == 64) launch_pure<128, 64, PRO, EPI>(a, pure, lds, st);
+  else if (BM == 64 && BN == 128) launch_pure<64, 128, PRO, EPI>(a, pure, lds, st);
+  else if (BM == 64 && BN == 64) launch_pure<64, 64, PRO, EPI>(a, pure, lds, st);
+  else if (BM == 256 && BN == 64) launch_pure<256, 64, PRO, EPI>(a, pure, lds, st);
+  else FDT_CHECK(false, "unsupported conv tile");
+}
+
+}  // namespace conv
+
+// Python-facing launcher.  taps: list of (dh, dw, wt) triples encoded as int8 arrays.
+void conv_igemm(uint64_t x, uint64_t x2, uint64_t ps, uint64_t pt, uint64_t w, uint64_t out, uint64_t part,
+                uint64_t ex, uint64_t es, uint64_t et, long Nb, int Hi, int Wi, int Cx, int Ho, int Wo, int S,
+                const std::vector<int>& dh, const std::vector<int>& dw, const std::vector<int>& wt, int Cout, int ldw,
+                int Hout, int Wout, int OS, int oy, int ox, int pro, int pro_act, float pro_alpha, int epi, int epi_act,
+                float epi_alpha, int BM, int BN, uint64_t stream) {
+  using namespace conv;
+  ConvArgs a{};
+  a.x = P<const bf16>(x);
+  a.x2 = P<const bf16>(x2);
+  a.ps = P<const float>(ps);
+  a.pt = P<const float>(pt);
+  a.w = P<const bf16>(w);
+  a.out = P<bf16>(out);
+  a.part = P<float>(part);
+  a.ex = P<const bf16>(ex);
+  a.es = P<const float>(es);
+  a.et = P<const float>(et);
+  FDT_CHECK(Cx >= 8 && (Cx & (Cx - 1)) == 0, "Cx must be a power of two >= 8");
+  FDT_CHECK(Cout % BN == 0, "Cout must be a multiple of BN");
+  FDT_CHECK(dh.size() == dw.size() && dh.size() == wt.size() && dh.size() <= 12, "bad tap table");
+  FDT_CHECK(ldw % 8 == 0, "weight row stride must be a multiple of 8");
+  a.M = Nb * (long)Ho * Wo;
+  a.Hi = Hi; a.Wi = Wi; a.Cx = Cx;
+  a.log2Cx = 31 - __builtin_clz((unsigned)Cx);
+  a.Ho = Ho; a.Wo = Wo; a.S = S;
+  a.ntaps = (int)dh.size();
+  a.K = a.ntaps * Cx;
+  a.Cout = Cout; a.ldw = ldw;
+  a.Hout = Hout; a.Wout = Wout; a.OS = OS; a.oy = oy; a.ox = ox;
+  a.pro_act = pro_act; a.pro_alpha = pro_alpha;
+  a.epi_act = epi_act; a.epi_alpha = epi_alpha;
+  for (size_t i = 0; i < dh.size(); ++i) {
+    a.dh[i] = (int8_t)dh[i];
+    a.dw[i] = (int8_t)dw[i];
+    a.wt[i] = (int8_t)wt[i];
+  }
+  a.nbm = (int)((a.M + BM - 1) / BM);
+  a.nbn = Cout / BN;
+  const bool pure = a.ntaps == 1 && dh[0] == 0 && dw[0] == 0 && wt[0] == 0 && S == 1 && Hi == Ho && Wi == Wo;
+  hipStream_t st = as_stream(stream);
+  if (a.M == 0) return;
+#define FDT_CONV_CASE(P_, E_) \
+  if (pro == P_ && epi == E_) { launch_tile<P_, E_>(a, BM, BN, pure, st); return; }
+  FDT_CONV_CASE(kProNone, kEpiStats)
+  FDT_CONV_CASE(kProAffineAct, kEpiStats)
+  FDT_CONV_CASE(kProFold, kEpiActBwd)
+  FDT_CONV_CASE(kProFold, kEpiStore)
+  FDT_CONV_CASE(kProFold, kEpiAdd)
+#undef FDT_CONV_CASE
+  FDT_CHECK(false, "unsupported (prologue, epilogue) combination");
+}
+
+int conv_num_row_blocks(long M, int BM) { return (int)((M + BM - 1) / BM); }
+
+}  // namespace fdt

@@ -1,0 +1,442 @@
+// Weight gradient of the NHWC implicit-GEMM convolutions (gfx950 / CDNA4), plus the
+// per-step weight packing kernel.
+//
+//   dW[co][k] = sum_px  G~[px][co] * A[px][k],   k = (tap, ci)
+//   G~ = g + alpha[co] + beta[co]*y   (batch-norm backward correction, PRO_FOLD)
+//   A  = act(x*s + t) at the tap's input pixel (zero outside the image)
+//
+// Both operands are pixel-major in HBM with channels contiguous, and the reduction runs
+// over pixels, so each 32-pixel K tile is staged [px][ch] (16-B channel chunks, an XOR
+// swizzle on the chunk index keyed by the pixel row) and the MFMA fragments are read
+// with the gfx950 transposing LDS read ds_read_b64_tr_b16 (two per fragment: pixels
+// 8h..8h+3 and 8h+4..8h+7 of one channel column), conflict-free per 32-lane half.
+// mfma_f32_32x32x16_bf16, 256 threads (2 x 2 waves), double-buffered LDS with
+// register-staged prefetch, one barrier per K tile.  The pixel range is split over
+// blockIdx.z; each split writes an fp32 slab that `wgrad_reduce` sums (fixed order ->
+// deterministic) into the fp32 OIHW gradient of the flat gradient buffer.
+//
+// Reference semantics: the conv2d(X^T, g^T) weight gradient of resnet.py:21-34 and the
+// autograd of nn.Conv2d for the strided convolutions.
+#include "common.h"
+#include <vector>
+#include <algorithm>
+
+namespace fdt {
+namespace wg {
+
+typedef short bf16x8_t __attribute__((ext_vector_type(8)));
+typedef short bf16x4_t __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef __attribute__((address_space(3))) bf16x4_t lds_bf16x4;
+
+struct WgArgs {
+  const bf16* g;     // [M][Cout]  gradient wrt conv output (pre-correction)
+  const bf16* y;     // [M][Cout]  conv output (for the correction)
+  const float* al;   // alpha [Cout]  (nullptr: no correction)
+  const float* be;   // beta  [Cout]
+  const bf16* x;     // [Nb][Hi][Wi][Cx]  conv input (raw)
+  const float* xs;   // s [Cx] (nullptr: identity input transform)
+  const float* xt;   // t [Cx]
+  float* slab;       // [nsplit][Cout][ldw]
+  long M;            // Nb*Ho*Wo
+  int Hi, Wi, Cx, log2Cx, Ho, Wo, S;
+  int ntaps, Cout, ldw, act;
+  float act_alpha;
+  int nbm, nbn, nsplit;
+  long px_per_split;  // multiple of 32
+  int8_t dh[12], dw[12];
+};
+
+__device__ __forceinline__ int xcd_remap(int bid, int nblk) {
+  const int q = nblk >> 3, r = nblk & 7, xcd = bid & 7;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+}
+
+// chunk swizzle for a [32 px][RB bytes] tile: conflict-free ds_read_b64_tr_b16
+template <int RB>
+__device__ __forceinline__ int tswz(int px) {
+  if constexpr (RB == 256) return 4 * (px & 3);
+  else return 4 * ((px >> 1) & 1);
+}
+
+template <int BM, int BN, bool FOLD, bool XAFF>
+__global__ __launch_bounds__(256) void wgrad_kernel(const WgArgs a) {
+  constexpr int BK = 32;                       // pixels per K tile
+  constexpr int GC = BM / 8, XC = BN / 8;      // 16-B chunks per LDS row
+  constexpr int GR = 256 / GC, XR = 256 / XC;  // rows per load round
+  constexpr int NG = BK / GR, NX = BK / XR;    // chunks per thread per tile
+  constexpr int TM = BM / 64, TN = BN / 64;
+  constexpr int GT = BK * BM, XT = BK * BN;
+  static_assert(NG >= 1 && NX >= 1, "bad wgrad tile");
+
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  bf16* tiles = reinterpret_cast<bf16*>(smem);  // [2][GT + XT]
+  float* prm = reinterpret_cast<float*>(smem + 2 * (GT + XT) * 2);  // al|be [BM] , xs|xt [Cx]
+  int* tapt = reinterpret_cast<int*>(prm + 2 * BM + (XAFF ? 2 * a.Cx : 0));
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wn = wid & 1, wm = wid >> 1;
+  const int nt = a.nbm * a.nbn;
+  const int id = xcd_remap(blockIdx.x, nt);
+  const int bn = id % a.nbn, bm = id / a.nbn;
+  const int co0 = bm * BM, k0 = bn * BN;
+  const long p_begin = (long)blockIdx.y * a.px_per_split;
+  long p_end = p_begin + a.px_per_split;
+  if (p_end > a.M) p_end = a.M;
+
+  if constexpr (FOLD) {
+    for (int i = tid; i < BM; i += 256) { prm[i] = a.al[co0 + i]; prm[BM + i] = a.be[co0 + i]; }
+  }
+  if constexpr (XAFF) {
+    for (int i = tid; i < a.Cx; i += 256) { prm[2 * BM + i] = a.xs[i]; prm[2 * BM + a.Cx + i] = a.xt[i]; }
+  }
+  if (tid < 12) tapt[tid] = (int)(uint8_t)a.dh[tid] | ((int)(uint8_t)a.dw[tid] << 8);
+
+  // per-thread fixed chunk columns
+  const int gcc = tid % GC, xcc = tid % XC;
+  // X chunk column -> (tap, ci) for this block's k columns (fixed across K tiles)
+  const int kx = k0 + xcc * 8;
+  const int xtap = kx >> a.log2Cx, xci = kx & (a.Cx - 1);
+  const bool xtok = xtap < a.ntaps;
+  __syncthreads();
+  int xdh = 0, xdw = 0;
+  if (xtok) {
+    const int e = tapt[xtap];
+    xdh = (int)(int8_t)(e & 0xff);
+    xdw = (int)(int8_t)((e >> 8) & 0xff);
+  }
+  float xsv[8], xtv[8];
+  if constexpr (XAFF) {
+#pragma unroll
+    for (int q = 0; q < 8; ++q) { xsv[q] = prm[2 * BM + xci + q]; xtv[q] = prm[2 * BM + a.Cx + xci + q]; }
+  }
+  float alv[8], bev[8];
+  if constexpr (FOLD) {
+#pragma unroll
+    for (int q = 0; q < 8; ++q) { alv[q] = prm[gcc * 8 + q]; bev[q] = prm[BM + gcc * 8 + q]; }
+  }
+
+  // pixel decomposition of this thread's X rows, advanced incrementally by BK per tile
+  const long hw = (long)a.Ho * a.Wo;
+  long xn[NX];
+  int xoh[NX], xow[NX];
+#pragma unroll
+  for (int j = 0; j < NX; ++j) {
+    const long p = p_begin + tid / XC + j * XR;
+    xn[j] = p / hw;
+    const int rem = (int)(p - xn[j] * hw);
+    xoh[j] = rem / a.Wo;
+    xow[j] = rem - xoh[j] * a.Wo;
+  }
+
+  uint4 rg[NG], ry[FOLD ? NG : 1], rx[NX];
+  bool gvld[NG], xvld[NX];
+  long ptile = p_begin;
+
+  auto load_tile = [&](long pt) {
+#pragma unroll
+    for (int j = 0; j < NG; ++j) {
+      const long p = pt + tid / GC + j * GR;
+      gvld[j] = p < p_end;
+      const long off = p * a.Cout + co0 + gcc * 8;
+      if (gvld[j]) {
+        rg[j] = *reinterpret_cast<const uint4*>(a.g + off);
+        if constexpr (FOLD) ry[j] = *reinterpret_cast<const uint4*>(a.y + off);
+      } else {
+        rg[j] = make_uint4(0, 0, 0, 0);
+        if constexpr (FOLD) ry[j] = make_uint4(0, 0, 0, 0);
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < NX; ++j) {
+      const long p = pt + tid / XC + j * XR;
+      const int ih = xoh[j] * a.S + xdh, iw = xow[j] * a.S + xdw;
+      bool v = xtok && p < p_end && (unsigned)ih < (unsigned)a.Hi && (unsigned)iw < (unsigned)a.Wi;
+      xvld[j] = v;
+      if (v) rx[j] = *reinterpret_cast<const uint4*>(a.x + ((xn[j] * a.Hi + ih) * a.Wi + iw) * a.Cx + xci);
+      else rx[j] = make_uint4(0, 0, 0, 0);
+      // advance this row's pixel by BK
+      xow[j] += BK;
+      while (xow[j] >= a.Wo) { xow[j] -= a.Wo; if (++xoh[j] >= a.Ho) { xoh[j] = 0; ++xn[j]; } }
+    }
+  };
+
+  auto store_tile = [&](int buf) {
+    bf16* Gl = tiles + buf * (GT + XT);
+    bf16* Xl = Gl + GT;
+#pragma unroll
+    for (int j = 0; j < NG; ++j) {
+      const int row = tid / GC + j * GR;
+      uint4 o = rg[j];
+      if constexpr (FOLD) {
+        if (gvld[j]) {
+          const uint32_t u[4] = {o.x, o.y, o.z, o.w}, uy[4] = {ry[j].x, ry[j].y, ry[j].z, ry[j].w};
+          float v[8];
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            v[2 * q] = bf16_lo(u[q]) + fmaf(bev[2 * q], bf16_lo(uy[q]), alv[2 * q]);
+            v[2 * q + 1] = bf16_hi(u[q]) + fmaf(bev[2 * q + 1], bf16_hi(uy[q]), alv[2 * q + 1]);
+          }
+          o = make_uint4(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]), pack_bf16x2(v[4], v[5]),
+                         pack_bf16x2(v[6], v[7]));
+        }
+      }
+      *reinterpret_cast<uint4*>(Gl + row * BM + 8 * (gcc ^ tswz<BM * 2>(row))) = o;
+    }
+#pragma unroll
+    for (int j = 0; j < NX; ++j) {
+      const int row = tid / XC + j * XR;
+      uint4 o = rx[j];
+      if constexpr (XAFF) {
+        if (xvld[j]) {
+          const uint32_t u[4] = {o.x, o.y, o.z, o.w};
+          float v[8];
+#pragma unroll
+          for (int q = 0; q < 4; ++q) { v[2 * q] = bf16_lo(u[q]); v[2 * q + 1] = bf16_hi(u[q]); }
+#pragma unroll
+          for (int q = 0; q < 8; ++q) v[q] = act_fwd(fmaf(v[q], xsv[q], xtv[q]), a.act, a.act_alpha);
+          o = make_uint4(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]), pack_bf16x2(v[4], v[5]),
+                         pack_bf16x2(v[6], v[7]));
+        }
+      }
+      *reinterpret_cast<uint4*>(Xl + row * BN + 8 * (xcc ^ tswz<BN * 2>(row))) = o;
+    }
+  };
+
+  f32x16 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  const int nkt = p_end > p_begin ? (int)((p_end - p_begin + BK - 1) / BK) : 0;
+  if (nkt > 0) {
+    load_tile(ptile);
+    store_tile(0);
+    __syncthreads();
+  }
+  // transposed fragment read: 16-lane group gl supplies rows q (lane 4q+p) and columns 4p..4p+3
+  const int gq = (lane & 15) >> 2, gp = lane & 3;
+  const int h = lane >> 5;
+  const int colg = ((lane >> 4) & 1) * 16;  // group 1/3 -> columns 16..31 of the 32-col subtile
+  for (int kt = 0; kt < nkt; ++kt) {
+    const int buf = kt & 1;
+    ptile += BK;
+    if (kt + 1 < nkt) load_tile(ptile);
+    const bf16* Gl = tiles + buf * (GT + XT);
+    const bf16* Xl = Gl + GT;
+#pragma unroll
+    for (int ks = 0; ks < BK / 16; ++ks) {
+      bf16x8_t af[TM], bfv[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int col = wm * (BM / 2) + i * 32 + colg + 4 * gp;  // channel column of this lane's 4-wide piece
+        bf16x4_t lo, hi;
+        {
+          const int row = ks * 16 + 8 * h + gq;
+          const int ch = col >> 3;
+          const bf16* p = Gl + row * BM + 8 * (ch ^ tswz<BM * 2>(row)) + (col & 7);
+          lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_bf16x4*)(p));
+        }
+        {
+          const int row = ks * 16 + 8 * h + 4 + gq;
+          const int ch = col >> 3;
+          const bf16* p = Gl + row * BM + 8 * (ch ^ tswz<BM * 2>(row)) + (col & 7);
+          hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_bf16x4*)(p));
+        }
+        af[i] = bf16x8_t{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      }
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int col = wn * (BN / 2) + j * 32 + colg + 4 * gp;
+        bf16x4_t lo, hi;
+        {
+          const int row = ks * 16 + 8 * h + gq;
+          const bf16* p = Xl + row * BN + 8 * ((col >> 3) ^ tswz<BN * 2>(row)) + (col & 7);
+          lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_bf16x4*)(p));
+        }
+        {
+          const int row = ks * 16 + 8 * h + 4 + gq;
+          const bf16* p = Xl + row * BN + 8 * ((col >> 3) ^ tswz<BN * 2>(row)) + (col & 7);
+          hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_bf16x4*)(p));
+        }
+        bfv[j] = bf16x8_t{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      }
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bfv[j], acc[i][j], 0, 0, 0);
+    }
+    if (kt + 1 < nkt) store_tile(buf ^ 1);
+    __syncthreads();
+  }
+
+  // epilogue: C[co][k]: lane column k = lane&31, rows co = (r&3) + 8(r>>2) + 4h
+  float* dst = a.slab + (long)blockIdx.y * a.Cout * a.ldw;
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int kk = k0 + wn * (BN / 2) + j * 32 + (lane & 31);
+      if (kk < a.ldw) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int co = co0 + wm * (BM / 2) + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+          dst[(long)co * a.ldw + kk] = acc[i][j][r];
+        }
+      }
+    }
+}
+
+// slab [nsplit][Cout][ntaps*Cxp] -> fp32 OIHW grad [Cout][Cin][KH][KW] (fixed split order)
+__global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restrict__ slab, float* __restrict__ out,
+                                                           int nsplit, int Cout, int Cin, int ntaps, int Cxp,
+                                                           int accumulate) {
+  const long n = (long)Cout * Cin * ntaps;
+  const long ld = (long)ntaps * Cxp;
+  const long sstride = (long)Cout * ld;
+  for (long e = (long)blockIdx.x * blockDim.x + threadIdx.x; e < n; e += (long)gridDim.x * blockDim.x) {
+    const int t = (int)(e % ntaps);
+    const long r = e / ntaps;
+    const int ci = (int)(r % Cin);
+    const int co = (int)(r / Cin);
+    const long src = (long)co * ld + (long)t * Cxp + ci;
+    float s = 0.f;
+    for (int k = 0; k < nsplit; ++k) s += slab[k * sstride + src];
+    out[e] = accumulate ? out[e] + s : s;
+  }
+}
+
+// ---------------------------------------------------------------------- weight packing
+struct PackEntry {
+  const float* src;  // fp32 OIHW
+  bf16* wf;          // [Cout][ntaps][Cxp]      (forward)
+  bf16* wd;          // [Cin][ntaps][Cout]      (dgrad; nullptr to skip)
+  int Cout, Cin, Cxp, ntaps;
+  long blk0;          // first block of this entry
+};
+
+constexpr int kMaxPack = 64;  // keeps the kernel-argument table under 4 KB
+struct PackTable {
+  PackEntry e[kMaxPack];
+  int n;
+};
+
+__global__ __launch_bounds__(256) void pack_weights_kernel(const PackTable tab) {
+  // binary search the entry of this block
+  int lo = 0, hi = tab.n - 1;
+  while (lo < hi) {
+    int mid = (lo + hi + 1) >> 1;
+    if (tab.e[mid].blk0 <= (long)blockIdx.x) lo = mid; else hi = mid - 1;
+  }
+  const PackEntry& E = tab.e[lo];
+  const long nf = (long)E.Cout * E.ntaps * E.Cxp;
+  const long i = ((long)blockIdx.x - E.blk0) * 256 + threadIdx.x;
+  if (i >= nf) return;
+  // forward layout element i = (co, t, ci')
+  const int ci = (int)(i % E.Cxp);
+  const long r = i / E.Cxp;
+  const int t = (int)(r % E.ntaps);
+  const int co = (int)(r / E.ntaps);
+  float v = 0.f;
+  if (ci < E.Cin) v = E.src[((long)co * E.Cin + ci) * E.ntaps + t];
+  E.wf[i] = __float2bfloat16(v);
+  if (E.wd != nullptr && ci < E.Cin) E.wd[((long)ci * E.ntaps + t) * E.Cout + co] = __float2bfloat16(v);
+}
+
+}  // namespace wg
+
+void conv_wgrad(uint64_t g, uint64_t y, uint64_t al, uint64_t be, uint64_t x, uint64_t xs, uint64_t xt, uint64_t slab,
+                long Nb, int Hi, int Wi, int Cx, int Ho, int Wo, int S, const std::vector<int>& dh,
+                const std::vector<int>& dw, int Cout, int ldw, int act, float act_alpha, int BM, int BN, int nsplit,
+                uint64_t stream) {
+  using namespace wg;
+  WgArgs a{};
+  a.g = P<const bf16>(g); a.y = P<const bf16>(y);
+  a.al = P<const float>(al); a.be = P<const float>(be);
+  a.x = P<const bf16>(x); a.xs = P<const float>(xs); a.xt = P<const float>(xt);
+  a.slab = P<float>(slab);
+  FDT_CHECK(Cx >= 8 && (Cx & (Cx - 1)) == 0, "Cx must be a power of two >= 8");
+  FDT_CHECK(Cout % BM == 0, "Cout must be a multiple of BM");
+  FDT_CHECK(dh.size() == dw.size() && dh.size() <= 12, "bad tap table");
+  FDT_CHECK(nsplit >= 1, "nsplit >= 1");
+  FDT_CHECK((al == 0) == (be == 0) && (xs == 0) == (xt == 0), "paired params");
+  a.M = Nb * (long)Ho * Wo;
+  a.Hi = Hi; a.Wi = Wi; a.Cx = Cx; a.log2Cx = 31 - __builtin_clz((unsigned)Cx);
+  a.Ho = Ho; a.Wo = Wo; a.S = S;
+  a.ntaps = (int)dh.size(); a.Cout = Cout; a.ldw = ldw; a.act = act; a.act_alpha = act_alpha;
+  FDT_CHECK(ldw >= a.ntaps * Cx, "ldw too small");
+  for (size_t i = 0; i < dh.size(); ++i) { a.dh[i] = (int8_t)dh[i]; a.dw[i] = (int8_t)dw[i]; }
+  a.nbm = Cout / BM;
+  a.nbn = (ldw + BN - 1) / BN;
+  long per = (a.M + nsplit - 1) / nsplit;
+  per = (per + 31) / 32 * 32;
+  a.px_per_split = per;
+  a.nsplit = nsplit;
+  const bool fold = al != 0, xaff = xs != 0;
+  size_t lds = (size_t)2 * 32 * (BM + BN) * 2 + 2 * BM * 4 + (xaff ? 2 * Cx * 4 : 0) + 64;
+  dim3 grid(a.nbm * a.nbn, nsplit);
+  hipStream_t st = as_stream(stream);
+#define FDT_WG(BM_, BN_, F_, X_)                                                                          \
+  if (BM == BM_ && BN == BN_ && fold == F_ && xaff == X_) {                                             \
+    auto k = wgrad_kernel<BM_, BN_, F_, X_>;                                                           \
+    static size_t set = 64 * 1024;                                                                      \
+    if (lds > set) {                                                                                    \
+      FDT_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(k),                               \
+                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));         \
+      set = lds;                                                                                        \
+    }                                                                                                   \
+    hipLaunchKernelGGL(k, grid, dim3(256), lds, st, a);                                                 \
+    FDT_LAUNCH_CHECK();                                                                                 \
+    return;                                                                                             \
+  }
+#define FDT_WG_T(BM_, BN_) FDT_WG(BM_, BN_, true, true) FDT_WG(BM_, BN_, true, false) \
+  FDT_WG(BM_, BN_, false, true) FDT_WG(BM_, BN_, false, false)
+  FDT_WG_T(128, 128)
+  FDT_WG_T(64, 128)
+  FDT_WG_T(128, 64)
+  FDT_WG_T(64, 64)
+#undef FDT_WG_T
+#undef FDT_WG
+  FDT_CHECK(false, "unsupported wgrad tile");
+}
+
+void wgrad_reduce(uint64_t slab, uint64_t out, int nsplit, int Cout, int Cin, int ntaps, int Cxp, int accumulate,
+                  uint64_t stream) {
+  long n = (long)Cout * Cin * ntaps;
+  int grid = (int)std::min<long>((n + 255) / 256, 4096);
+  hipLaunchKernelGGL(wg::wgrad_reduce_kernel, dim3(grid), dim3(256), 0, as_stream(stream), P<const float>(slab),
+                     P<float>(out), nsplit, Cout, Cin, ntaps, Cxp, accumulate);
+  FDT_LAUNCH_CHECK();
+}
+
+// entries: list of (src, wf, wd, Cout, Cin, Cxp, ntaps); one launch for all of them
+void pack_weights(const std::vector<uint64_t>& src, const std::vector<uint64_t>& wf, const std::vector<uint64_t>& wd,
+                  const std::vector<int>& cout, const std::vector<int>& cin, const std::vector<int>& cxp,
+                  const std::vector<int>& ntaps, uint64_t stream) {
+  using namespace wg;
+  const size_t n = src.size();
+  size_t i = 0;
+  while (i < n) {
+    PackTable tab{};
+    long blk = 0;
+    int k = 0;
+    for (; i < n && k < kMaxPack; ++i, ++k) {
+      PackEntry& E = tab.e[k];
+      E.src = P<const float>(src[i]);
+      E.wf = P<bf16>(wf[i]);
+      E.wd = P<bf16>(wd[i]);
+      E.Cout = cout[i]; E.Cin = cin[i]; E.Cxp = cxp[i]; E.ntaps = ntaps[i];
+      E.blk0 = blk;
+      blk += ((long)E.Cout * E.ntaps * E.Cxp + 255) / 256;
+    }
+    tab.n = k;
+    if (blk == 0) continue;
+    hipLaunchKernelGGL(pack_weights_kernel, dim3((unsigned)blk), dim3(256), 0, as_stream(stream), tab);
+    FDT_LAUNCH_CHECK();
+  }
+}
+
+}  // namespace fdt

@@ -1,0 +1,225 @@
+"""Host side of the hand-written implicit-GEMM convolution kernels (csrc/kernels/conv_igemm.hip,
+csrc/kernels/conv_wgrad.hip).
+
+Tensors are NHWC bf16 (``[N, H, W, C]`` contiguous).  Weights are packed once per step
+by ``pack_weights`` from the fp32 OIHW master copy (flat parameter buffer) into
+
+* ``wf``: ``[Cout][KH*KW][Cxp]`` — forward operand, K-contiguous per output channel
+  (``Cxp`` = input channels padded to a power of two >= 8, e.g. 3 -> 8 for the stem);
+* ``wd``: ``[Cin][KH*KW][Cout]`` — data-gradient operand.
+
+Geometry helpers turn (kernel, stride, pad) into the tap tables the kernels consume:
+forward ``ih = oh*S + dh``; dgrad of a stride-1 conv is a conv of the gradient with the
+taps mirrored; dgrad of a stride-2 conv is split into 4 output-parity classes.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+from functools import lru_cache
+
+import torch
+
+from . import _native
+
+PRO_NONE, PRO_AFFINE_ACT, PRO_FOLD = 0, 1, 2
+EPI_STATS, EPI_ACTBWD, EPI_STORE, EPI_ADD = 0, 1, 2, 3
+
+
+def _sp():
+    return _native.stream_ptr()
+
+
+def _p(t):
+    return 0 if t is None else t.data_ptr()
+
+
+def pad_channels(c: int) -> int:
+    p = 8
+    while p < c:
+        p *= 2
+    return p
+
+
+@lru_cache(maxsize=None)
+def taps_fwd(k: int, pad: int):
+    dh, dw, wt = [], [], []
+    for kh in range(k):
+        for kw in range(k):
+            dh.append(kh - pad)
+            dw.append(kw - pad)
+            wt.append(kh * k + kw)
+    return dh, dw, wt
+
+
+@lru_cache(maxsize=None)
+def dgrad_classes(k: int, stride: int, pad: int):
+    """[(py, px, dh, dw, wt)]: output-parity classes of the transposed convolution.
+    For each class the valid taps satisfy (p + pad - kh) % stride == 0 and read the
+    gradient at  ho = a + (p + pad - kh) / stride  (a = class-grid row)."""
+    out = []
+    for py in range(stride):
+        for px in range(stride):
+            dh, dw, wt = [], [], []
+            for kh in range(k):
+                if (py + pad - kh) % stride:
+                    continue
+                for kw in range(k):
+                    if (px + pad - kw) % stride:
+                        continue
+                    dh.append((py + pad - kh) // stride)
+                    dw.append((px + pad - kw) // stride)
+                    wt.append(kh * k + kw)
+            out.append((py, px, dh, dw, wt))
+    return out
+
+
+def pick_tile(M: int, N: int, cands=((128, 128), (128, 64), (64, 128), (64, 64)), want: int = 512):
+    best = None
+    for bm, bn in cands:
+        if N % bn:
+            continue
+        nb = -(-M // bm) * (N // bn)
+        if nb >= want:
+            return bm, bn
+        if best is None or nb > best[0]:
+            best = (nb, bm, bn)
+    return best[1], best[2]
+
+
+@dataclass
+class ConvShape:
+    cin: int
+    cout: int
+    k: int
+    stride: int
+    pad: int
+
+    @property
+    def cxp(self):
+        return pad_channels(self.cin)
+
+    @property
+    def ntaps(self):
+        return self.k * self.k
+
+
+def out_hw(h, w, shp: ConvShape):
+    return ((h + 2 * shp.pad - shp.k) // shp.stride + 1, (w + 2 * shp.pad - shp.k) // shp.stride + 1)
+
+
+def conv_fwd(x, wf, shp: ConvShape, s=None, t=None, act=0, alpha=1.0, tile=None):
+    """y = conv(act(x*s+t)) (or conv(x) when s is None and act == 0); returns
+    (y [N,Ho,Wo,Cout] bf16, part [nbm,2,Cout] fp32 per-block (sum y, sum y^2))."""
+    nat = _native.native()
+    N, H, W, C = x.shape
+    assert C == shp.cxp and x.dtype == torch.bfloat16 and x.is_contiguous()
+    Ho, Wo = out_hw(H, W, shp)
+    M = N * Ho * Wo
+    bm, bn = tile or pick_tile(M, shp.cout)
+    y = torch.empty(N, Ho, Wo, shp.cout, device=x.device, dtype=torch.bfloat16)
+    part = torch.empty(nat.conv_num_row_blocks(M, bm), 2, shp.cout, device=x.device, dtype=torch.float32)
+    dh, dw, wt = taps_fwd(shp.k, shp.pad)
+    pro = PRO_AFFINE_ACT if (s is not None or act != 0) else PRO_NONE
+    if pro == PRO_AFFINE_ACT and s is None:
+        s = torch.ones(C, device=x.device, dtype=torch.float32)
+        t = torch.zeros(C, device=x.device, dtype=torch.float32)
+    nat.conv_igemm(x.data_ptr(), 0, _p(s), _p(t), wf.data_ptr(), y.data_ptr(), part.data_ptr(), 0, 0, 0,
+                   N, H, W, C, Ho, Wo, shp.stride, list(dh), list(dw), list(wt), shp.cout, shp.ntaps * shp.cxp,
+                   Ho, Wo, 1, 0, 0, pro, int(act), float(alpha), EPI_STATS, 0, 1.0, bm, bn, _sp())
+    return y, part
+
+
+def conv_dgrad(g, y, al, be, wd, shp: ConvShape, x_shape, epi=EPI_STORE, out=None, ex=None, es=None, et=None,
+               act=0, alpha=1.0, tile=None):
+    """Data gradient of y = conv(a): dA = conv^T(g + al + be*y).
+
+    epi: EPI_STORE -> write dA; EPI_ADD -> out += dA; EPI_ACTBWD -> through the lazy
+    input a = act(ex*es + et): out = dA*act'(.)*es, returns per-block partial slabs
+    [nbm, 2, Cin] of (sum g_pre*ex, sum g_pre)."""
+    nat = _native.native()
+    N, Hy, Wy, Cy = g.shape
+    assert Cy == shp.cout and g.is_contiguous() and y.is_contiguous()
+    Nx, Hx, Wx, Cx = x_shape
+    assert Cx == shp.cin
+    if out is None:
+        out = torch.empty(N, Hx, Wx, shp.cin, device=g.device, dtype=torch.bfloat16)
+    parts = []
+    classes = dgrad_classes(shp.k, shp.stride, shp.pad)
+    for (py, px, dh, dw, wt) in classes:
+        Ha = (Hx - py + shp.stride - 1) // shp.stride
+        Wa = (Wx - px + shp.stride - 1) // shp.stride
+        M = N * Ha * Wa
+        if len(dh) == 0 and epi == EPI_ADD:
+            continue
+        bm, bn = tile or pick_tile(M, shp.cin)
+        part = None
+        if epi == EPI_ACTBWD:
+            part = torch.empty(nat.conv_num_row_blocks(M, bm), 2, shp.cin, device=g.device, dtype=torch.float32)
+            parts.append(part)
+        nat.conv_igemm(g.data_ptr(), y.data_ptr(), _p(al), _p(be), wd.data_ptr(), out.data_ptr(), _p(part),
+                       _p(ex), _p(es), _p(et), N, Hy, Wy, Cy, Ha, Wa, 1, list(dh), list(dw), list(wt), shp.cin,
+                       shp.ntaps * shp.cout, Hx, Wx, shp.stride, py, px, PRO_FOLD, 0, 1.0, epi, int(act),
+                       float(alpha), bm, bn, _sp())
+    if epi == EPI_ACTBWD:
+        return out, (parts[0] if len(parts) == 1 else torch.cat(parts, 0))
+    return out, None
+
+
+def wgrad_split(M: int, tiles: int, want: int = 512, min_px: int = 1024) -> int:
+    s = max(1, want // max(tiles, 1))
+    s = min(s, max(1, M // min_px))
+    return s
+
+
+def conv_wgrad(g, y, al, be, x, shp: ConvShape, out, xs=None, xt=None, act=0, alpha=1.0, accumulate=False,
+               tile=None, nsplit=None, slab=None):
+    """out (fp32 OIHW [Cout, Cin, k, k]) = dL/dW of y = conv(act(x*xs+xt)) given
+    g (gradient wrt y, corrected by al + be*y in the kernel)."""
+    nat = _native.native()
+    N, Hy, Wy, Cy = g.shape
+    Nx, H, W, Cx = x.shape
+    assert Cx == shp.cxp and Cy == shp.cout
+    M = N * Hy * Wy
+    ldw = shp.ntaps * shp.cxp
+    if tile is None:
+        bm = 128 if shp.cout % 128 == 0 else 64
+        bn = 128 if ldw >= 128 else 64
+    else:
+        bm, bn = tile
+    tiles = (shp.cout // bm) * (-(-ldw // bn))
+    ns = nsplit or wgrad_split(M, tiles)
+    if slab is None or slab.numel() < ns * shp.cout * ldw:
+        slab = torch.empty(ns * shp.cout * ldw, device=g.device, dtype=torch.float32)
+    dh, dw, _ = taps_fwd(shp.k, shp.pad)
+    if xs is None and act != 0:
+        xs = torch.ones(Cx, device=x.device, dtype=torch.float32)
+        xt = torch.zeros(Cx, device=x.device, dtype=torch.float32)
+    nat.conv_wgrad(g.data_ptr(), y.data_ptr(), _p(al), _p(be), x.data_ptr(), _p(xs), _p(xt), slab.data_ptr(),
+                   N, H, W, Cx, Hy, Wy, shp.stride, list(dh), list(dw), shp.cout, ldw, int(act), float(alpha),
+                   bm, bn, ns, _sp())
+    nat.wgrad_reduce(slab.data_ptr(), out.data_ptr(), ns, shp.cout, shp.cin, shp.ntaps, shp.cxp, int(accumulate),
+                     _sp())
+    return out
+
+
+def pack_weights(entries):
+    """entries: iterable of (w fp32 OIHW, wf bf16, wd bf16 or None, ConvShape); one launch."""
+    nat = _native.native()
+    src, wf, wd, co, ci, cx, nt = [], [], [], [], [], [], []
+    for w, f, d, shp in entries:
+        assert w.is_contiguous() and w.dtype == torch.float32
+        src.append(w.data_ptr())
+        wf.append(f.data_ptr())
+        wd.append(_p(d))
+        co.append(shp.cout)
+        ci.append(shp.cin)
+        cx.append(shp.cxp)
+        nt.append(shp.ntaps)
+    if src:
+        nat.pack_weights(src, wf, wd, co, ci, cx, nt, _sp())
+
+
+def alloc_packed(shp: ConvShape, device, dgrad=True):
+    wf = torch.empty(shp.cout, shp.ntaps, shp.cxp, device=device, dtype=torch.bfloat16)
+    wd = torch.empty(shp.cin, shp.ntaps, shp.cout, device=device, dtype=torch.bfloat16) if dgrad else None
+    return wf, wd

@@ -1,0 +1,172 @@
+"""Numerics of the hand-written implicit-GEMM conv kernels (fwd / dgrad / wgrad) against a
+plain PyTorch fp32 reference of the same op (inputs rounded to bf16 on both sides)."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+from faster_distributed_training_amd.ops import conv_igemm as ci
+
+pytestmark = pytest.mark.gpu
+
+BF = torch.bfloat16
+
+
+def rel(a, b):
+    a, b = a.float(), b.float()
+    return ((a - b).norm() / (b.norm() + 1e-12)).item()
+
+
+def act_ref(z, act, alpha):
+    if act == 1:
+        return torch.relu(z)
+    if act == 2:
+        return F.celu(z, alpha)
+    return z
+
+
+def make(shape_nhwc, dev, scale=1.0):
+    return (torch.randn(*shape_nhwc, device=dev) * scale).to(BF)
+
+
+def nchw(x):
+    return x.permute(0, 3, 1, 2).float()
+
+
+def nhwc(x):
+    return x.permute(0, 2, 3, 1)
+
+
+def padc(x, c):
+    if x.shape[-1] == c:
+        return x.contiguous()
+    return F.pad(x, (0, c - x.shape[-1])).contiguous()
+
+
+FWD_CASES = [
+    # (N, H, Cin, Cout, k, stride, pad)
+    (4, 8, 64, 128, 1, 1, 0),
+    (2, 8, 64, 64, 3, 1, 1),
+    (2, 16, 128, 128, 3, 2, 1),
+    (2, 8, 64, 256, 1, 2, 0),
+    (2, 8, 3, 64, 3, 1, 1),     # stem (Cin padded to 8)
+    (3, 5, 64, 64, 3, 1, 1),    # M tail (75 rows)
+    (2, 4, 512, 512, 3, 1, 1),
+]
+
+
+@pytest.mark.parametrize("case", FWD_CASES)
+@pytest.mark.parametrize("mode", ["plain", "relu", "celu"])
+def test_conv_fwd(cuda, case, mode):
+    N, H, Cin, Cout, k, stride, pad = case
+    torch.manual_seed(0)
+    shp = ci.ConvShape(Cin, Cout, k, stride, pad)
+    x = padc(make((N, H, H, Cin), cuda), shp.cxp)
+    w = torch.randn(Cout, Cin, k, k, device=cuda) / (Cin * k * k) ** 0.5
+    wf, wd = ci.alloc_packed(shp, cuda, dgrad=Cin >= 8)
+    ci.pack_weights([(w, wf, wd, shp)])
+    if mode == "plain":
+        s = t = None
+        act, alpha = 0, 1.0
+        a = x[..., :Cin].float()
+    else:
+        s = torch.rand(shp.cxp, device=cuda) + 0.5
+        t = torch.randn(shp.cxp, device=cuda) * 0.3
+        act, alpha = (1, 1.0) if mode == "relu" else (2, 0.075)
+        a = act_ref(x.float() * s + t, act, alpha).to(BF).float()[..., :Cin]
+    for tile in [None, (64, 64), (128, 64)]:
+        if tile and Cout % tile[1]:
+            continue
+        y, part = ci.conv_fwd(x, wf, shp, s, t, act, alpha, tile=tile)
+        ref = nhwc(F.conv2d(nchw(a), w.to(BF).float(), stride=stride, padding=pad))
+        assert rel(y, ref) < 1e-2, (tile, rel(y, ref))
+        ps = part.sum(0)
+        yf = ref.reshape(-1, Cout)
+        assert rel(ps[0], yf.sum(0)) < 2e-3
+        assert rel(ps[1], (yf * yf).sum(0)) < 2e-3
+
+
+DGRAD_CASES = [
+    (4, 8, 64, 128, 1, 1, 0),
+    (2, 8, 64, 64, 3, 1, 1),
+    (2, 16, 128, 128, 3, 2, 1),
+    (2, 8, 64, 256, 1, 2, 0),
+    (3, 5, 64, 64, 3, 1, 1),
+]
+
+
+@pytest.mark.parametrize("case", DGRAD_CASES)
+@pytest.mark.parametrize("epi", ["store", "add", "actbwd"])
+def test_conv_dgrad(cuda, case, epi):
+    N, H, Cin, Cout, k, stride, pad = case
+    torch.manual_seed(1)
+    shp = ci.ConvShape(Cin, Cout, k, stride, pad)
+    w = torch.randn(Cout, Cin, k, k, device=cuda) / (Cin * k * k) ** 0.5
+    wf, wd = ci.alloc_packed(shp, cuda)
+    ci.pack_weights([(w, wf, wd, shp)])
+    Ho, Wo = ci.out_hw(H, H, shp)
+    g = make((N, Ho, Wo, Cout), cuda)
+    y = make((N, Ho, Wo, Cout), cuda)
+    al = torch.randn(Cout, device=cuda) * 0.1
+    be = torch.randn(Cout, device=cuda) * 0.1
+    gt = (g.float() + al + be * y.float()).to(BF).float()
+    ref = nhwc(torch.nn.grad.conv2d_input((N, Cin, H, H), w.to(BF).float(), nchw(gt), stride=stride, padding=pad))
+    xs = (N, H, H, Cin)
+    if epi == "store":
+        out, _ = ci.conv_dgrad(g, y, al, be, wd, shp, xs, epi=ci.EPI_STORE)
+        assert rel(out, ref) < 1e-2
+    elif epi == "add":
+        prev = make(xs, cuda)
+        out = prev.clone()
+        ci.conv_dgrad(g, y, al, be, wd, shp, xs, epi=ci.EPI_ADD, out=out)
+        assert rel(out, ref + prev.float()) < 1e-2
+    else:
+        ex = make(xs, cuda)
+        es = torch.rand(Cin, device=cuda) + 0.5
+        et = torch.randn(Cin, device=cuda) * 0.3
+        z = ex.float() * es + et
+        gp = ref * (z > 0).float()
+        out, part = ci.conv_dgrad(g, y, al, be, wd, shp, xs, epi=ci.EPI_ACTBWD, ex=ex, es=es, et=et, act=1)
+        assert rel(out, gp * es) < 1e-2
+        ps = part.sum(0)
+        assert rel(ps[0], (gp * ex.float()).reshape(-1, Cin).sum(0)) < 1e-2
+        assert rel(ps[1], gp.reshape(-1, Cin).sum(0)) < 1e-2
+
+
+WGRAD_CASES = [
+    (4, 8, 64, 128, 1, 1, 0),
+    (2, 8, 64, 64, 3, 1, 1),
+    (2, 16, 128, 128, 3, 2, 1),
+    (2, 8, 64, 256, 1, 2, 0),
+    (2, 8, 3, 64, 3, 1, 1),
+    (3, 5, 64, 64, 3, 1, 1),
+]
+
+
+@pytest.mark.parametrize("case", WGRAD_CASES)
+@pytest.mark.parametrize("mode", ["plain", "affine"])
+def test_conv_wgrad(cuda, case, mode):
+    N, H, Cin, Cout, k, stride, pad = case
+    torch.manual_seed(2)
+    shp = ci.ConvShape(Cin, Cout, k, stride, pad)
+    x = padc(make((N, H, H, Cin), cuda), shp.cxp)
+    Ho, Wo = ci.out_hw(H, H, shp)
+    g = make((N, Ho, Wo, Cout), cuda)
+    y = make((N, Ho, Wo, Cout), cuda)
+    if mode == "plain":
+        al = be = xs = xt = None
+        act = 0
+        gt = g.float()
+        a = x.float()[..., :Cin]
+    else:
+        al = torch.randn(Cout, device=cuda) * 0.1
+        be = torch.randn(Cout, device=cuda) * 0.1
+        xs = torch.rand(shp.cxp, device=cuda) + 0.5
+        xt = torch.randn(shp.cxp, device=cuda) * 0.3
+        act = 1
+        gt = (g.float() + al + be * y.float()).to(BF).float()
+        a = torch.relu(x.float() * xs + xt).to(BF).float()[..., :Cin]
+    ref = torch.nn.grad.conv2d_weight(nchw(a), (Cout, Cin, k, k), nchw(gt), stride=stride, padding=pad)
+    for ns in [1, 3]:
+        out = torch.empty(Cout, Cin, k, k, device=cuda)
+        ci.conv_wgrad(g, y, al, be, x, shp, out, xs, xt, act, nsplit=ns)
+        assert rel(out, ref) < 5e-3, (ns, rel(out, ref))

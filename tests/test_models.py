@@ -1,0 +1,165 @@
+"""Model definitions: parameter schema (checkpoint compatibility) and forward /
+backward numerics against the reference modules (CPU, fp32/fp64)."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+from faster_distributed_training_amd.models import resnet as R
+from faster_distributed_training_amd.models import transformer as T
+from faster_distributed_training_amd.ops.conv_bn import FusedConvBN2DFunction, conv_bn_reference
+
+from reference_oracle import load
+
+
+def test_resnet50_param_counts():
+    m = R.resnet50(10)
+    sd = m.state_dict()
+    assert len(sd) == 90
+    assert sum(p.numel() for p in m.parameters()) == 23_477_194
+    assert len(list(m.parameters())) == 69
+    assert sd["conv1.0.conv_weight"].shape == (64, 3, 3, 3)
+    assert sd["fc.weight"].shape == (10, 2048)
+    assert "conv3_x.0.residual_function.3.running_mean" in sd
+    assert "conv2_x.0.shortcut.1.num_batches_tracked" in sd
+
+
+@pytest.mark.parametrize("arch", ["resnet18", "resnet50"])
+def test_resnet_state_dict_matches_reference(arch):
+    ref = load("resnet")
+    a = getattr(R, arch)(10).state_dict()
+    b = getattr(ref, arch)(10).state_dict()
+    assert list(a.keys()) == list(b.keys())
+    for k in a:
+        assert a[k].shape == b[k].shape and a[k].dtype == b[k].dtype, k
+
+
+def test_transformer_state_dict_matches_reference():
+    ref = load("transformer")
+    torch.manual_seed(0)
+    a = T.Transformer(4, 1000).state_dict()
+    b = ref.Transformer(4, 1000).state_dict()
+    assert list(a.keys()) == list(b.keys())
+    for k in a:
+        assert a[k].shape == b[k].shape, k
+
+
+def test_transformer_param_count():
+    m = T.Transformer(4, 30522)
+    assert sum(p.numel() for p in m.parameters()) == 29_299_716
+    assert len(m.state_dict()) == 105
+
+
+def test_fused_conv_bn_gradcheck():
+    torch.manual_seed(0)
+    X = torch.randn(2, 3, 8, 8, dtype=torch.float64, requires_grad=True)
+    W = torch.randn(5, 3, 3, 3, dtype=torch.float64, requires_grad=True)
+    assert torch.autograd.gradcheck(FusedConvBN2DFunction.apply, (X, W, 1, 1))
+
+
+def test_fused_conv_bn_matches_reference_function():
+    ref = load("resnet")
+    torch.manual_seed(0)
+    X = torch.randn(4, 8, 6, 6, dtype=torch.float64, requires_grad=True)
+    W = torch.randn(6, 8, 3, 3, dtype=torch.float64, requires_grad=True)
+    g = torch.randn(4, 6, 6, 6, dtype=torch.float64)
+    out_a = conv_bn_reference(X, W, 1, 1, 1e-3)
+    gx_a, gw_a = torch.autograd.grad(out_a, (X, W), g)
+    out_b = ref.FusedConvBN2DFunction.apply(X, W, 1, 1, 1e-3)
+    gx_b, gw_b = torch.autograd.grad(out_b, (X, W), g)
+    assert torch.allclose(out_a, out_b, atol=1e-10)
+    assert torch.allclose(gx_a, gx_b, atol=1e-8)
+    assert torch.allclose(gw_a, gw_b, atol=1e-8)
+
+
+@pytest.mark.parametrize("arch", ["resnet18", "resnet50"])
+def test_resnet_forward_backward_matches_reference(arch):
+    ref = load("resnet")
+    torch.manual_seed(0)
+    mb = getattr(ref, arch)(10).double()
+    ma = getattr(R, arch)(10).double()
+    ma.load_state_dict(mb.state_dict())
+    ma.fast_path = False
+    x = torch.randn(4, 3, 32, 32, dtype=torch.float64)
+    y = torch.randint(0, 10, (4,))
+    la = F.cross_entropy(ma(x), y)
+    lb = F.cross_entropy(mb(x), y)
+    assert torch.allclose(la, lb, rtol=1e-9, atol=1e-10)
+    la.backward()
+    lb.backward()
+    for (n, pa), (_, pb) in zip(ma.named_parameters(), mb.named_parameters()):
+        assert ((pa.grad - pb.grad).norm() / pb.grad.norm()).item() < 1e-6, n
+
+
+def test_flops_per_image():
+    m = R.resnet50(10)
+    f = R.flops_per_image(m)
+    assert abs(f / 2.60e9 - 1) < 0.01
+
+
+def test_transformer_pieces_match_reference():
+    ref = load("transformer")
+    torch.manual_seed(0)
+    x = torch.randn(2, 7, 64, dtype=torch.float64)
+    lna, lnb = T.LayerNorm(64).double(), ref.LayerNorm(64).double()
+    with torch.no_grad():
+        lna.a_2.uniform_()
+        lnb.a_2.copy_(lna.a_2)
+    assert torch.allclose(lna(x), lnb(x), atol=1e-10)
+    # embeddings (token + position + segment, x sqrt(d))
+    ea, eb = T.Embeddings(64, 50, 16).double(), ref.Embeddings(64, 50, 16).double()
+    ea.load_state_dict(eb.state_dict())
+    ids = torch.randint(0, 50, (2, 7))
+    types = torch.randint(0, 3, (2, 7))
+    idx = torch.arange(16)
+    eb_out = eb(ids, types, idx)
+    assert torch.allclose(ea(ids, types, idx), eb_out.to(torch.float64), atol=1e-6)
+
+
+def test_fused_mlp_bias_grad_fix_and_faithful():
+    torch.manual_seed(0)
+    m = T.FusedMLP(8, 16, 4).double()
+    x = torch.randn(5, 8, dtype=torch.float64)
+    out = m(x)
+    ref = F.linear(torch.relu(F.linear(x, m.W1, m.b1[0])), m.W2, m.b2[0])
+    assert torch.allclose(out, ref)
+    g = torch.randn_like(out)
+    out.backward(g)
+    gb2 = g.sum(0, keepdim=True)
+    assert torch.allclose(m.b2.grad, gb2)
+    mf = T.FusedMLP(8, 16, 4, faithful=True).double()
+    mf.load_state_dict(m.state_dict())
+    mf(x).backward(g)
+    assert torch.allclose(mf.b2.grad, gb2 / 5)  # reference averages bias grads (Q5)
+
+
+def test_transformer_forward_shapes_and_eval_no_mixup():
+    torch.manual_seed(0)
+    m = T.Transformer(4, 100, n_layers=2, d_model=64, d_ff=128, d_hidden=64, maxlen=32, h=4)
+    ids = torch.randint(0, 100, (3, 10))
+    types = torch.zeros(3, 10, dtype=torch.long)
+    mask = torch.ones(3, 1, 1, 10)
+    mask[0, ..., 7:] = 0
+    logits, perm, lam = m(ids, types, torch.arange(32), mask)
+    assert logits.shape == (3, 4) and perm.shape == (3,)
+    m.eval()
+    l1, p1, lam1 = m(ids, types, torch.arange(32), mask)
+    l2, _, _ = m(ids, types, torch.arange(32), mask)
+    assert lam1 == 1.0 and torch.equal(p1, torch.arange(3))
+    assert torch.allclose(l1, l2)
+
+
+def test_attention_masking_is_real():
+    from faster_distributed_training_amd.ops.attention import attention_reference
+    torch.manual_seed(0)
+    q, k, v = (torch.randn(2, 6, 2, 8) for _ in range(3))
+    mask = torch.ones(2, 6)
+    mask[:, 4:] = 0
+    out = attention_reference(q, k, v, mask)
+    # changing masked keys/values must not change the output
+    k2, v2 = k.clone(), v.clone()
+    k2[:, 4:] = 100.0
+    v2[:, 4:] = -50.0
+    assert torch.allclose(out, attention_reference(q, k2, v2, mask), atol=1e-6)
+    # faithful mask value (-1e-9) reproduces the reference bug (no masking)
+    a = attention_reference(q, k, v, mask, mask_value=-1e-9)
+    assert not torch.allclose(a, attention_reference(q, k2, v2, mask, mask_value=-1e-9))
