@@ -18,6 +18,7 @@ void stats_finalize(uint64_t part, int nb, int C, double count, int mode, float 
 void act_bwd_reduce(uint64_t g, uint64_t x, uint64_t s, uint64_t t, uint64_t gx, uint64_t part, long M, int C, int act,
                     float alpha, int dt, uint64_t stream);
 void reduce_partials(uint64_t part, int nb, int nq, int C, uint64_t out, uint64_t stream);
+int partials_compact(uint64_t part, int nb, int W, int R, uint64_t out, uint64_t stream);
 void stats_bwd_coef(uint64_t gs, uint64_t gt, int C, double count, int mode, float eps, uint64_t save_mean,
                     uint64_t save_aux, uint64_t gamma, uint64_t alpha, uint64_t beta, uint64_t ggamma, uint64_t gbeta,
                     uint64_t stream);
@@ -73,13 +74,13 @@ void conv_igemm(uint64_t x, uint64_t x2, uint64_t ps, uint64_t pt, uint64_t w, u
                 uint64_t ex, uint64_t es, uint64_t et, long Nb, int Hi, int Wi, int Cx, int Ho, int Wo, int S,
                 const std::vector<int>& dh, const std::vector<int>& dw, const std::vector<int>& wt, int Cout, int ldw,
                 int Hout, int Wout, int OS, int oy, int ox, int pro, int pro_act, float pro_alpha, int epi, int epi_act,
-                float epi_alpha, int BM, int BN, uint64_t stream);
+                float epi_alpha, int BM, int BN, int BK, uint64_t stream);
 int conv_num_row_blocks(long M, int BM);
 // conv_wgrad.hip
 void conv_wgrad(uint64_t g, uint64_t y, uint64_t al, uint64_t be, uint64_t x, uint64_t xs, uint64_t xt, uint64_t slab,
                 long Nb, int Hi, int Wi, int Cx, int Ho, int Wo, int S, const std::vector<int>& dh,
-                const std::vector<int>& dw, int Cout, int ldw, int act, float act_alpha, int BM, int BN, int nsplit,
-                uint64_t stream);
+                const std::vector<int>& dw, int Cout, int ldw, int act, float act_alpha, int BM, int BN, int BK,
+                int nsplit, uint64_t stream);
 void wgrad_reduce(uint64_t slab, uint64_t out, int nsplit, int Cout, int Cin, int ntaps, int Cxp, int accumulate,
                   uint64_t stream);
 void pack_weights(const std::vector<uint64_t>& src, const std::vector<uint64_t>& wf, const std::vector<uint64_t>& wd,

@@ -22,6 +22,7 @@ PYBIND11_MODULE(_fdt_native, m) {
   DEF(stats_finalize);
   DEF(act_bwd_reduce);
   DEF(reduce_partials);
+  DEF(partials_compact);
   DEF(stats_bwd_coef);
   DEF(affine_fold);
   DEF(residual_act_fwd);

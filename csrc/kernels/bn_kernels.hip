@@ -261,6 +261,31 @@ __global__ __launch_bounds__(64 * kRedWaves) void reduce_partials_kernel(const f
   }
 }
 
+// ------------------------------------------------------------------ slab compaction
+// part [nb][W] -> out [ceil(nb/R)][W]: out[k][w] = sum_{r in chunk k} part[r][w] (fp32,
+// fixed order).  The conv epilogues emit one slab row per workgroup (thousands of rows
+// at batch 1024); compacting with a wide grid first keeps the fp64 finalize short and
+// the whole reduction at HBM speed instead of a handful of workgroups.
+__global__ __launch_bounds__(256) void partials_compact_kernel(const float* __restrict__ part, int nb, int W,
+                                                               int R, float* __restrict__ out) {
+  const int w = blockIdx.x * 256 + threadIdx.x;
+  const int k = blockIdx.y;
+  if (w >= W) return;
+  const int r0 = k * R;
+  int r1 = r0 + R;
+  if (r1 > nb) r1 = nb;
+  float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+  int r = r0;
+  for (; r + 3 < r1; r += 4) {
+    a0 += part[(long)r * W + w];
+    a1 += part[(long)(r + 1) * W + w];
+    a2 += part[(long)(r + 2) * W + w];
+    a3 += part[(long)(r + 3) * W + w];
+  }
+  for (; r < r1; ++r) a0 += part[(long)r * W + w];
+  out[(long)k * W + w] = (a0 + a1) + (a2 + a3);
+}
+
 // ------------------------------------------------------------------ producer backward
 // (g_s, g_t) -> affine correction of dL/dy:  g_y += alpha + beta * y
 // mode 0 (FusedConvBN): s = 1/(sd+eps), t = -mean*s
@@ -296,8 +321,9 @@ __global__ void stats_bwd_coef_kernel(const float* __restrict__ gs, const float*
       beta[c] = 0.f;
       alpha[c] = 0.f;
     }
-    if (ggamma) ggamma[c] = (float)((g_s - mean * g_t) * inv);
-    if (gbeta) gbeta[c] = (float)g_t;
+    // accumulate (+=) into the parameter gradients (flat gradient views)
+    if (ggamma) ggamma[c] += (float)((g_s - mean * g_t) * inv);
+    if (gbeta) gbeta[c] += (float)g_t;
   }
 }
 
@@ -496,6 +522,15 @@ void act_bwd_reduce(uint64_t g, uint64_t x, uint64_t s, uint64_t t, uint64_t gx,
                                                                   gg.TPR, gg.RPP, r, act, alpha);
   });
   FDT_LAUNCH_CHECK();
+}
+
+int partials_compact(uint64_t part, int nb, int W, int R, uint64_t out, uint64_t stream) {
+  const int nk = (nb + R - 1) / R;
+  if (nb == 0 || W == 0) return 0;
+  partials_compact_kernel<<<dim3((W + 255) / 256, nk), 256, 0, as_stream(stream)>>>(P<const float>(part), nb, W, R,
+                                                                                     P<float>(out));
+  FDT_LAUNCH_CHECK();
+  return nk;
 }
 
 void reduce_partials(uint64_t part, int nb, int nq, int C, uint64_t out, uint64_t stream) {

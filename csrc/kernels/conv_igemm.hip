@@ -128,8 +128,10 @@ __global__ __launch_bounds__(256) void igemm_kernel(const ConvArgs a) {
   static_assert(NXL >= 1 && NWL >= 1, "tile too small for 256 threads");
 
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  bf16* tiles = reinterpret_cast<bf16*>(smem);                       // [2][WT + XT]
-  float* pst = reinterpret_cast<float*>(smem + 2 * (XT + WT) * 2);   // [2][Cx] (PRO != none)
+  const int nkt = (a.K + BK - 1) / BK;
+  const int nbuf = nkt > 1 ? 2 : 1;                                  // K <= BK: one LDS buffer
+  bf16* tiles = reinterpret_cast<bf16*>(smem);                       // [nbuf][WT + XT]
+  float* pst = reinterpret_cast<float*>(smem + nbuf * (XT + WT) * 2);  // [2][Cx] (PRO != none)
   float* red = pst + (PRO != kProNone ? 2 * a.Cx : 0);               // [2 waves][2][BN]
   int* tapt = reinterpret_cast<int*>(red + 4 * BN);                  // [12]: dh | dw<<8 | wt<<16
 
@@ -275,7 +277,6 @@ __global__ __launch_bounds__(256) void igemm_kernel(const ConvArgs a) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
-  const int nkt = (a.K + BK - 1) / BK;
   if (nkt > 0) {
     load_tile(0);
     store_tile(0);
@@ -462,9 +463,9 @@ struct Cfg {
   int BM, BN;
 };
 
-template <int BM, int BN, int PRO, int EPI, bool PURE>
+template <int BM, int BN, int BK, int PRO, int EPI, bool PURE>
 static void launch_one(const ConvArgs& a, size_t lds, hipStream_t st) {
-  auto kern = igemm_kernel<BM, BN, 64, PRO, EPI, PURE>;
+  auto kern = igemm_kernel<BM, BN, BK, PRO, EPI, PURE>;
   static size_t attr_set = 64 * 1024;  // default dynamic-LDS limit; raise only when needed
   if (lds > attr_set) {
     FDT_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -475,21 +476,23 @@ static void launch_one(const ConvArgs& a, size_t lds, hipStream_t st) {
   FDT_LAUNCH_CHECK();
 }
 
-template <int BM, int BN, int PRO, int EPI>
+template <int BM, int BN, int BK, int PRO, int EPI>
 static void launch_pure(const ConvArgs& a, bool pure, size_t lds, hipStream_t st) {
-  if (pure) launch_one<BM, BN, PRO, EPI, true>(a, lds, st);
-  else launch_one<BM, BN, PRO, EPI, false>(a, lds, st);
+  if (pure) launch_one<BM, BN, BK, PRO, EPI, true>(a, lds, st);
+  else launch_one<BM, BN, BK, PRO, EPI, false>(a, lds, st);
 }
 
 template <int PRO, int EPI>
-static void launch_tile(const ConvArgs& a, int BM, int BN, bool pure, hipStream_t st) {
-  size_t lds = (size_t)2 * (BM + BN) * 64 * 2 + (PRO != kProNone ? 2 * a.Cx * 4 : 0) + 4 * BN * 4 + 64;
-  if (BM == 128 && BN == 128) launch_pure<128, 128, PRO, EPI>(a, pure, lds, st);
-  else if (BM == 128 && BN == 64) launch_pure<128, 64, PRO, EPI>(a, pure, lds, st);
-  else if (BM == 64 && BN == 128) launch_pure<64, 128, PRO, EPI>(a, pure, lds, st);
-  else if (BM == 64 && BN == 64) launch_pure<64, 64, PRO, EPI>(a, pure, lds, st);
-  else if (BM == 256 && BN == 64) launch_pure<256, 64, PRO, EPI>(a, pure, lds, st);
-  else FDT_CHECK(false, "unsupported conv tile");
+static void launch_tile(const ConvArgs& a, int BM, int BN, int BK, bool pure, hipStream_t st) {
+  const int nkt = (a.K + BK - 1) / BK;
+  const size_t nbuf = nkt > 1 ? 2 : 1;
+  size_t lds = nbuf * (BM + BN) * BK * 2 + (PRO != kProNone ? 2 * a.Cx * 4 : 0) + 4 * BN * 4 + 64;
+#define FDT_T(BM_, BN_, BK_) \
+  if (BM == BM_ && BN == BN_ && BK == BK_) { launch_pure<BM_, BN_, BK_, PRO, EPI>(a, pure, lds, st); return; }
+  FDT_T(128, 128, 64) FDT_T(128, 64, 64) FDT_T(64, 128, 64) FDT_T(64, 64, 64) FDT_T(256, 64, 64)
+  FDT_T(128, 128, 32) FDT_T(128, 64, 32) FDT_T(64, 128, 32) FDT_T(64, 64, 32) FDT_T(256, 128, 32)
+#undef FDT_T
+  FDT_CHECK(false, "unsupported conv tile");
 }
 
 }  // namespace conv
@@ -499,7 +502,7 @@ void conv_igemm(uint64_t x, uint64_t x2, uint64_t ps, uint64_t pt, uint64_t w, u
                 uint64_t ex, uint64_t es, uint64_t et, long Nb, int Hi, int Wi, int Cx, int Ho, int Wo, int S,
                 const std::vector<int>& dh, const std::vector<int>& dw, const std::vector<int>& wt, int Cout, int ldw,
                 int Hout, int Wout, int OS, int oy, int ox, int pro, int pro_act, float pro_alpha, int epi, int epi_act,
-                float epi_alpha, int BM, int BN, uint64_t stream) {
+                float epi_alpha, int BM, int BN, int BK, uint64_t stream) {
   using namespace conv;
   ConvArgs a{};
   a.x = P<const bf16>(x);
@@ -537,7 +540,7 @@ void conv_igemm(uint64_t x, uint64_t x2, uint64_t ps, uint64_t pt, uint64_t w, u
   hipStream_t st = as_stream(stream);
   if (a.M == 0) return;
 #define FDT_CONV_CASE(P_, E_) \
-  if (pro == P_ && epi == E_) { launch_tile<P_, E_>(a, BM, BN, pure, st); return; }
+  if (pro == P_ && epi == E_) { launch_tile<P_, E_>(a, BM, BN, BK, pure, st); return; }
   FDT_CONV_CASE(kProNone, kEpiStats)
   FDT_CONV_CASE(kProAffineAct, kEpiStats)
   FDT_CONV_CASE(kProFold, kEpiActBwd)

@@ -39,7 +39,7 @@ struct WgArgs {
   const float* xt;   // t [Cx]
   float* slab;       // [nsplit][Cout][ldw]
   long M;            // Nb*Ho*Wo
-  int Hi, Wi, Cx, log2Cx, Ho, Wo, S;
+  int Hi, Wi, Cx, log2Cx, Ho, Wo, S, log2Ho, log2Wo;
   int ntaps, Cout, ldw, act;
   float act_alpha;
   int nbm, nbn, nsplit;
@@ -59,9 +59,10 @@ __device__ __forceinline__ int tswz(int px) {
   else return 4 * ((px >> 1) & 1);
 }
 
-template <int BM, int BN, bool FOLD, bool XAFF>
+// ADDR: 0 = 1x1 stride-1 (input pixel == output pixel), 1 = power-of-two Ho/Wo (shifts),
+//       2 = general (integer division)
+template <int BM, int BN, int BK, bool FOLD, bool XAFF, int ADDR>
 __global__ __launch_bounds__(256) void wgrad_kernel(const WgArgs a) {
-  constexpr int BK = 32;                       // pixels per K tile
   constexpr int GC = BM / 8, XC = BN / 8;      // 16-B chunks per LDS row
   constexpr int GR = 256 / GC, XR = 256 / XC;  // rows per load round
   constexpr int NG = BK / GR, NX = BK / XR;    // chunks per thread per tile
@@ -116,18 +117,8 @@ __global__ __launch_bounds__(256) void wgrad_kernel(const WgArgs a) {
     for (int q = 0; q < 8; ++q) { alv[q] = prm[gcc * 8 + q]; bev[q] = prm[BM + gcc * 8 + q]; }
   }
 
-  // pixel decomposition of this thread's X rows, advanced incrementally by BK per tile
   const long hw = (long)a.Ho * a.Wo;
-  long xn[NX];
-  int xoh[NX], xow[NX];
-#pragma unroll
-  for (int j = 0; j < NX; ++j) {
-    const long p = p_begin + tid / XC + j * XR;
-    xn[j] = p / hw;
-    const int rem = (int)(p - xn[j] * hw);
-    xoh[j] = rem / a.Wo;
-    xow[j] = rem - xoh[j] * a.Wo;
-  }
+  const int lw = a.log2Wo, lhw = a.log2Wo + a.log2Ho;
 
   uint4 rg[NG], ry[FOLD ? NG : 1], rx[NX];
   bool gvld[NG], xvld[NX];
@@ -150,14 +141,30 @@ __global__ __launch_bounds__(256) void wgrad_kernel(const WgArgs a) {
 #pragma unroll
     for (int j = 0; j < NX; ++j) {
       const long p = pt + tid / XC + j * XR;
-      const int ih = xoh[j] * a.S + xdh, iw = xow[j] * a.S + xdw;
-      bool v = xtok && p < p_end && (unsigned)ih < (unsigned)a.Hi && (unsigned)iw < (unsigned)a.Wi;
+      bool v = xtok && p < p_end;
+      long off;
+      if constexpr (ADDR == 0) {
+        off = p * a.Cx + xci;
+      } else {
+        long n;
+        int oh, ow;
+        if constexpr (ADDR == 1) {
+          n = p >> lhw;
+          oh = (int)(p >> lw) & (a.Ho - 1);
+          ow = (int)p & (a.Wo - 1);
+        } else {
+          n = p / hw;
+          const int rem = (int)(p - n * hw);
+          oh = rem / a.Wo;
+          ow = rem - oh * a.Wo;
+        }
+        const int ih = oh * a.S + xdh, iw = ow * a.S + xdw;
+        v = v && (unsigned)ih < (unsigned)a.Hi && (unsigned)iw < (unsigned)a.Wi;
+        off = ((n * a.Hi + ih) * a.Wi + iw) * a.Cx + xci;
+      }
       xvld[j] = v;
-      if (v) rx[j] = *reinterpret_cast<const uint4*>(a.x + ((xn[j] * a.Hi + ih) * a.Wi + iw) * a.Cx + xci);
+      if (v) rx[j] = *reinterpret_cast<const uint4*>(a.x + off);
       else rx[j] = make_uint4(0, 0, 0, 0);
-      // advance this row's pixel by BK
-      xow[j] += BK;
-      while (xow[j] >= a.Wo) { xow[j] -= a.Wo; if (++xoh[j] >= a.Ho) { xoh[j] = 0; ++xn[j]; } }
     }
   };
 
@@ -290,22 +297,38 @@ __global__ __launch_bounds__(256) void wgrad_kernel(const WgArgs a) {
     }
 }
 
-// slab [nsplit][Cout][ntaps*Cxp] -> fp32 OIHW grad [Cout][Cin][KH][KW] (fixed split order)
+// slab [nsplit][Cout][ntaps*Cxp] -> fp32 OIHW grad [Cout][Cin][KH][KW] (fixed split order).
+// One workgroup per 64 consecutive slab columns of one output channel: lane = column
+// (coalesced slab reads), the 4 waves take interleaved splits, LDS combines them.
 __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restrict__ slab, float* __restrict__ out,
                                                            int nsplit, int Cout, int Cin, int ntaps, int Cxp,
                                                            int accumulate) {
-  const long n = (long)Cout * Cin * ntaps;
-  const long ld = (long)ntaps * Cxp;
+  __shared__ float red[4][64];
+  const int ld = ntaps * Cxp;
+  const int cblk = (ld + 63) / 64;
+  const int co = blockIdx.x / cblk;
+  const int col = (blockIdx.x - co * cblk) * 64 + (threadIdx.x & 63);
+  const int w = threadIdx.x >> 6;
   const long sstride = (long)Cout * ld;
-  for (long e = (long)blockIdx.x * blockDim.x + threadIdx.x; e < n; e += (long)gridDim.x * blockDim.x) {
-    const int t = (int)(e % ntaps);
-    const long r = e / ntaps;
-    const int ci = (int)(r % Cin);
-    const int co = (int)(r / Cin);
-    const long src = (long)co * ld + (long)t * Cxp + ci;
-    float s = 0.f;
-    for (int k = 0; k < nsplit; ++k) s += slab[k * sstride + src];
-    out[e] = accumulate ? out[e] + s : s;
+  float a0 = 0.f, a1 = 0.f;
+  if (col < ld) {
+    const float* p = slab + (long)co * ld + col;
+    int k = w;
+    for (; k + 4 < nsplit; k += 8) {
+      a0 += p[k * sstride];
+      a1 += p[(k + 4) * sstride];
+    }
+    if (k < nsplit) a0 += p[k * sstride];
+  }
+  red[w][threadIdx.x & 63] = a0 + a1;
+  __syncthreads();
+  if (w == 0 && col < ld) {
+    const float s = (red[0][threadIdx.x] + red[1][threadIdx.x]) + (red[2][threadIdx.x] + red[3][threadIdx.x]);
+    const int t = col / Cxp, ci = col - t * Cxp;
+    if (ci < Cin) {
+      const long e = ((long)co * Cin + ci) * ntaps + t;
+      out[e] = accumulate ? out[e] + s : s;
+    }
   }
 }
 
@@ -350,8 +373,8 @@ __global__ __launch_bounds__(256) void pack_weights_kernel(const PackTable tab) 
 
 void conv_wgrad(uint64_t g, uint64_t y, uint64_t al, uint64_t be, uint64_t x, uint64_t xs, uint64_t xt, uint64_t slab,
                 long Nb, int Hi, int Wi, int Cx, int Ho, int Wo, int S, const std::vector<int>& dh,
-                const std::vector<int>& dw, int Cout, int ldw, int act, float act_alpha, int BM, int BN, int nsplit,
-                uint64_t stream) {
+                const std::vector<int>& dw, int Cout, int ldw, int act, float act_alpha, int BM, int BN, int BK,
+                int nsplit, uint64_t stream) {
   using namespace wg;
   WgArgs a{};
   a.g = P<const bf16>(g); a.y = P<const bf16>(y);
@@ -366,22 +389,27 @@ void conv_wgrad(uint64_t g, uint64_t y, uint64_t al, uint64_t be, uint64_t x, ui
   a.M = Nb * (long)Ho * Wo;
   a.Hi = Hi; a.Wi = Wi; a.Cx = Cx; a.log2Cx = 31 - __builtin_clz((unsigned)Cx);
   a.Ho = Ho; a.Wo = Wo; a.S = S;
+  auto ispow2 = [](int v) { return v > 0 && (v & (v - 1)) == 0; };
+  a.log2Ho = ispow2(Ho) ? 31 - __builtin_clz((unsigned)Ho) : 0;
+  a.log2Wo = ispow2(Wo) ? 31 - __builtin_clz((unsigned)Wo) : 0;
+  const int addr = (dh.size() == 1 && dh[0] == 0 && dw[0] == 0 && S == 1 && Hi == Ho && Wi == Wo)
+                       ? 0 : ((ispow2(Ho) && ispow2(Wo)) ? 1 : 2);
   a.ntaps = (int)dh.size(); a.Cout = Cout; a.ldw = ldw; a.act = act; a.act_alpha = act_alpha;
   FDT_CHECK(ldw >= a.ntaps * Cx, "ldw too small");
   for (size_t i = 0; i < dh.size(); ++i) { a.dh[i] = (int8_t)dh[i]; a.dw[i] = (int8_t)dw[i]; }
   a.nbm = Cout / BM;
   a.nbn = (ldw + BN - 1) / BN;
   long per = (a.M + nsplit - 1) / nsplit;
-  per = (per + 31) / 32 * 32;
+  per = (per + BK - 1) / BK * BK;
   a.px_per_split = per;
   a.nsplit = nsplit;
   const bool fold = al != 0, xaff = xs != 0;
-  size_t lds = (size_t)2 * 32 * (BM + BN) * 2 + 2 * BM * 4 + (xaff ? 2 * Cx * 4 : 0) + 64;
+  size_t lds = (size_t)2 * BK * (BM + BN) * 2 + 2 * BM * 4 + (xaff ? 2 * Cx * 4 : 0) + 64;
   dim3 grid(a.nbm * a.nbn, nsplit);
   hipStream_t st = as_stream(stream);
-#define FDT_WG(BM_, BN_, F_, X_)                                                                          \
-  if (BM == BM_ && BN == BN_ && fold == F_ && xaff == X_) {                                             \
-    auto k = wgrad_kernel<BM_, BN_, F_, X_>;                                                           \
+#define FDT_WG(BM_, BN_, BK_, F_, X_, A_)                                                                 \
+  if (BM == BM_ && BN == BN_ && BK == BK_ && fold == F_ && xaff == X_ && addr == A_) {                  \
+    auto k = wgrad_kernel<BM_, BN_, BK_, F_, X_, A_>;                                                   \
     static size_t set = 64 * 1024;                                                                      \
     if (lds > set) {                                                                                    \
       FDT_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(k),                               \
@@ -392,21 +420,28 @@ void conv_wgrad(uint64_t g, uint64_t y, uint64_t al, uint64_t be, uint64_t x, ui
     FDT_LAUNCH_CHECK();                                                                                 \
     return;                                                                                             \
   }
-#define FDT_WG_T(BM_, BN_) FDT_WG(BM_, BN_, true, true) FDT_WG(BM_, BN_, true, false) \
-  FDT_WG(BM_, BN_, false, true) FDT_WG(BM_, BN_, false, false)
-  FDT_WG_T(128, 128)
-  FDT_WG_T(64, 128)
-  FDT_WG_T(128, 64)
-  FDT_WG_T(64, 64)
+#define FDT_WG_A(BM_, BN_, BK_, F_, X_) FDT_WG(BM_, BN_, BK_, F_, X_, 0) FDT_WG(BM_, BN_, BK_, F_, X_, 1) \
+  FDT_WG(BM_, BN_, BK_, F_, X_, 2)
+#define FDT_WG_T(BM_, BN_, BK_) FDT_WG_A(BM_, BN_, BK_, true, true) FDT_WG_A(BM_, BN_, BK_, true, false) \
+  FDT_WG_A(BM_, BN_, BK_, false, true) FDT_WG_A(BM_, BN_, BK_, false, false)
+  FDT_WG_T(128, 128, 32)
+  FDT_WG_T(64, 128, 32)
+  FDT_WG_T(128, 64, 32)
+  FDT_WG_T(64, 64, 32)
+  FDT_WG_T(128, 128, 64)
+  FDT_WG_T(64, 128, 64)
+  FDT_WG_T(128, 64, 64)
+  FDT_WG_T(64, 64, 64)
 #undef FDT_WG_T
+#undef FDT_WG_A
 #undef FDT_WG
   FDT_CHECK(false, "unsupported wgrad tile");
 }
 
 void wgrad_reduce(uint64_t slab, uint64_t out, int nsplit, int Cout, int Cin, int ntaps, int Cxp, int accumulate,
                   uint64_t stream) {
-  long n = (long)Cout * Cin * ntaps;
-  int grid = (int)std::min<long>((n + 255) / 256, 4096);
+  const int ld = ntaps * Cxp;
+  const int grid = Cout * ((ld + 63) / 64);
   hipLaunchKernelGGL(wg::wgrad_reduce_kernel, dim3(grid), dim3(256), 0, as_stream(stream), P<const float>(slab),
                      P<float>(out), nsplit, Cout, Cin, ntaps, Cxp, accumulate);
   FDT_LAUNCH_CHECK();

@@ -214,15 +214,17 @@ class DeviceCIFARLoader:
         B = idx.numel()
         if self._gpu:
             nat = _native.native()
-            out = torch.empty(B, 32, 32, 3, device=self.device, dtype=self.out_dtype)
+            # NHWC with channels zero-padded to 8: the conv engine's stem operand layout
+            cp = 8
+            out = torch.empty(B, 32, 32, cp, device=self.device, dtype=self.out_dtype)
             lab = torch.empty(B, device=self.device, dtype=torch.int32)
             train = self.train and self.augment
             nat.augment(self.images.data_ptr(), idx.data_ptr(), self.labels.data_ptr(), lab.data_ptr(),
-                        out.data_ptr(), B, 32, 32, 3, 3, self.pad if train else 0, int(train and self.flip),
+                        out.data_ptr(), B, 32, 32, 3, cp, self.pad if train else 0, int(train and self.flip),
                         self.rng.data_ptr(), *CIFAR_MEAN, *CIFAR_STD, 0,
                         1 if self.out_dtype == torch.bfloat16 else 0, _native.stream_ptr())
             nat.rng_advance(self.rng.data_ptr(), _native.stream_ptr())
-            return out.permute(0, 3, 1, 2), lab.long()
+            return out[..., :3].permute(0, 3, 1, 2), lab.long()
         imgs = self.images[idx.long()].cpu()
         x = augment_cpu(imgs, self._cpu_gen, pad=self.pad, flip=self.flip, train=self.train and self.augment,
                         out_dtype=torch.float32)

@@ -11,8 +11,9 @@ interchangeable (``resnet.py:147-313``; key schema in survey §2.8):
 * shortcut ``Conv2d 1x1 (stride s) + BatchNorm2d`` when the shape changes (``resnet.py:220-224``)
 * BasicBlock uses CELU(0.075) (``resnet.py:147-190``)
 
-On MI355X the whole network runs through ``ops/resnet_engine.py`` (NHWC bf16, HIP
-kernels, batch-norm normalisation fused into the consumer's operand load); the
+On MI355X the whole network body runs through ``ops/resnet_fused.py`` (NHWC bf16,
+hand-written MFMA implicit-GEMM conv kernels with batch-norm statistics in the epilogue
+and normalisation + activation fused into the consumer's operand load); the
 ``nn.Sequential`` structure below is the CPU/oracle path and defines the state_dict.
 """
 from __future__ import annotations
@@ -168,7 +169,7 @@ class ResNet(nn.Module):
 
     def forward(self, x):
         if self.use_fast_path(x):
-            from ..ops.resnet_engine import resnet_engine_forward
+            from ..ops.resnet_fused import resnet_engine_forward
             return resnet_engine_forward(self, x)
         return self.forward_reference(x)
 

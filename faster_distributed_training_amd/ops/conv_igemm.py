@@ -14,6 +14,8 @@ taps mirrored; dgrad of a stride-2 conv is split into 4 output-parity classes.
 """
 from __future__ import annotations
 
+import json
+import os
 from dataclasses import dataclass
 from functools import lru_cache
 
@@ -73,17 +75,48 @@ def dgrad_classes(k: int, stride: int, pad: int):
     return out
 
 
-def pick_tile(M: int, N: int, cands=((128, 128), (128, 64), (64, 128), (64, 64)), want: int = 512):
+def pick_tile(M: int, N: int, cands=((128, 128), (128, 64), (64, 128), (64, 64)), want: int = 512, bk: int = 64):
+    """Heuristic (BM, BN, BK) when no tuned entry exists: the largest tile that still
+    gives ~2 workgroups per CU."""
     best = None
     for bm, bn in cands:
         if N % bn:
             continue
         nb = -(-M // bm) * (N // bn)
         if nb >= want:
-            return bm, bn
+            return bm, bn, bk
         if best is None or nb > best[0]:
             best = (nb, bm, bn)
-    return best[1], best[2]
+    return best[1], best[2], bk
+
+
+_TUNED = None
+_TUNED_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "conv_tuned.json")
+
+
+def tune_key(batch: int, h: int, shp) -> str:
+    return f"{batch}:{h}:{shp.cin}:{shp.cout}:{shp.k}:{shp.stride}:{shp.pad}"
+
+
+def tuned(op: str, batch: int, h: int, shp):
+    """Tuned launch config (scripts/tune_conv.py) for this exact problem, or None."""
+    global _TUNED
+    if _TUNED is None:
+        try:
+            with open(_TUNED_PATH) as f:
+                _TUNED = json.load(f)
+        except (OSError, ValueError):
+            _TUNED = {}
+    ent = _TUNED.get(tune_key(batch, h, shp), {}).get(op)
+    return ent
+
+
+def _tile3(tile, M, N):
+    if tile is None:
+        return pick_tile(M, N)
+    if len(tile) == 2:
+        return tile[0], tile[1], 64
+    return tuple(tile)
 
 
 @dataclass
@@ -115,7 +148,10 @@ def conv_fwd(x, wf, shp: ConvShape, s=None, t=None, act=0, alpha=1.0, tile=None)
     assert C == shp.cxp and x.dtype == torch.bfloat16 and x.is_contiguous()
     Ho, Wo = out_hw(H, W, shp)
     M = N * Ho * Wo
-    bm, bn = tile or pick_tile(M, shp.cout)
+    if tile is None:
+        ent = tuned("fwd", N, H, shp)
+        tile = tuple(ent["tile"]) if ent else None
+    bm, bn, bk = _tile3(tile, M, shp.cout)
     y = torch.empty(N, Ho, Wo, shp.cout, device=x.device, dtype=torch.bfloat16)
     part = torch.empty(nat.conv_num_row_blocks(M, bm), 2, shp.cout, device=x.device, dtype=torch.float32)
     dh, dw, wt = taps_fwd(shp.k, shp.pad)
@@ -125,7 +161,7 @@ def conv_fwd(x, wf, shp: ConvShape, s=None, t=None, act=0, alpha=1.0, tile=None)
         t = torch.zeros(C, device=x.device, dtype=torch.float32)
     nat.conv_igemm(x.data_ptr(), 0, _p(s), _p(t), wf.data_ptr(), y.data_ptr(), part.data_ptr(), 0, 0, 0,
                    N, H, W, C, Ho, Wo, shp.stride, list(dh), list(dw), list(wt), shp.cout, shp.ntaps * shp.cxp,
-                   Ho, Wo, 1, 0, 0, pro, int(act), float(alpha), EPI_STATS, 0, 1.0, bm, bn, _sp())
+                   Ho, Wo, 1, 0, 0, pro, int(act), float(alpha), EPI_STATS, 0, 1.0, bm, bn, bk, _sp())
     return y, part
 
 
@@ -144,6 +180,9 @@ def conv_dgrad(g, y, al, be, wd, shp: ConvShape, x_shape, epi=EPI_STORE, out=Non
     if out is None:
         out = torch.empty(N, Hx, Wx, shp.cin, device=g.device, dtype=torch.bfloat16)
     parts = []
+    if tile is None:
+        ent = tuned("dgrad", N, Hx, shp)
+        tile = tuple(ent["tile"]) if ent else None
     classes = dgrad_classes(shp.k, shp.stride, shp.pad)
     for (py, px, dh, dw, wt) in classes:
         Ha = (Hx - py + shp.stride - 1) // shp.stride
@@ -151,7 +190,7 @@ def conv_dgrad(g, y, al, be, wd, shp: ConvShape, x_shape, epi=EPI_STORE, out=Non
         M = N * Ha * Wa
         if len(dh) == 0 and epi == EPI_ADD:
             continue
-        bm, bn = tile or pick_tile(M, shp.cin)
+        bm, bn, bk = _tile3(tile, M, shp.cin)
         part = None
         if epi == EPI_ACTBWD:
             part = torch.empty(nat.conv_num_row_blocks(M, bm), 2, shp.cin, device=g.device, dtype=torch.float32)
@@ -159,7 +198,7 @@ def conv_dgrad(g, y, al, be, wd, shp: ConvShape, x_shape, epi=EPI_STORE, out=Non
         nat.conv_igemm(g.data_ptr(), y.data_ptr(), _p(al), _p(be), wd.data_ptr(), out.data_ptr(), _p(part),
                        _p(ex), _p(es), _p(et), N, Hy, Wy, Cy, Ha, Wa, 1, list(dh), list(dw), list(wt), shp.cin,
                        shp.ntaps * shp.cout, Hx, Wx, shp.stride, py, px, PRO_FOLD, 0, 1.0, epi, int(act),
-                       float(alpha), bm, bn, _sp())
+                       float(alpha), bm, bn, bk, _sp())
     if epi == EPI_ACTBWD:
         return out, (parts[0] if len(parts) == 1 else torch.cat(parts, 0))
     return out, None
@@ -182,10 +221,18 @@ def conv_wgrad(g, y, al, be, x, shp: ConvShape, out, xs=None, xt=None, act=0, al
     M = N * Hy * Wy
     ldw = shp.ntaps * shp.cxp
     if tile is None:
+        ent = tuned("wgrad", N, H, shp)
+        if ent:
+            tile = tuple(ent["tile"])
+            nsplit = nsplit or ent["nsplit"]
+    if tile is None:
         bm = 128 if shp.cout % 128 == 0 else 64
         bn = 128 if ldw >= 128 else 64
+        bk = 64
+    elif len(tile) == 2:
+        (bm, bn), bk = tile, 64
     else:
-        bm, bn = tile
+        bm, bn, bk = tile
     tiles = (shp.cout // bm) * (-(-ldw // bn))
     ns = nsplit or wgrad_split(M, tiles)
     if slab is None or slab.numel() < ns * shp.cout * ldw:
@@ -196,7 +243,7 @@ def conv_wgrad(g, y, al, be, x, shp: ConvShape, out, xs=None, xt=None, act=0, al
         xt = torch.zeros(Cx, device=x.device, dtype=torch.float32)
     nat.conv_wgrad(g.data_ptr(), y.data_ptr(), _p(al), _p(be), x.data_ptr(), _p(xs), _p(xt), slab.data_ptr(),
                    N, H, W, Cx, Hy, Wy, shp.stride, list(dh), list(dw), shp.cout, ldw, int(act), float(alpha),
-                   bm, bn, ns, _sp())
+                   bm, bn, bk, ns, _sp())
     nat.wgrad_reduce(slab.data_ptr(), out.data_ptr(), ns, shp.cout, shp.cin, shp.ntaps, shp.cxp, int(accumulate),
                      _sp())
     return out

@@ -77,11 +77,31 @@ class _MixupNative(torch.autograd.Function):
         return gx, None, glam, None
 
 
+def padded_channels_last(x: torch.Tensor):
+    """If x (N,C,H,W) is the channel-slice view of a zero-padded NHWC buffer (N,H,W,cp)
+    — the layout the device CIFAR loader emits for the conv engine — return cp."""
+    if x.dim() != 4:
+        return None
+    N, C, H, W = x.shape
+    s = x.stride()
+    if s[1] == 1 and s[3] >= C and s[2] == W * s[3] and s[0] == H * W * s[3]:
+        return s[3]
+    return None
+
+
 def mixup_interpolate(x: torch.Tensor, perm: torch.Tensor, lam) -> torch.Tensor:
     """lam * x + (1 - lam) * x[perm]; lam scalar, (B,)-shaped, or full map."""
     lv, kind = _lam_tensor(lam, x)
     if kind != "element" and _native.use_native(x) and x.dtype in DT:
-        return _MixupNative.apply(x, perm, lv, bool(getattr(lam, "requires_grad", False)))
+        lrg = bool(getattr(lam, "requires_grad", False))
+        cp = padded_channels_last(x)
+        if cp is not None:
+            # mix the whole padded per-sample block (pad channels stay zero) and keep the layout
+            N, C, H, W = x.shape
+            base = torch.as_strided(x, (N, H * W * cp), (H * W * cp, 1))
+            out = _MixupNative.apply(base, perm, lv, lrg)
+            return torch.as_strided(out, (N, C, H, W), (H * W * cp, 1, W * cp, cp))
+        return _MixupNative.apply(x, perm, lv, lrg)
     if kind == "scalar":
         return float(lam) * x + (1 - float(lam)) * x[perm]
     shape = (x.shape[0],) + (1,) * (x.dim() - 1) if kind == "sample" else x.shape
@@ -160,8 +180,12 @@ class _MixupCENative(torch.autograd.Function):
         loss = torch.empty((), device=lg.device, dtype=torch.float32)
         glog = torch.empty(b, c, device=lg.device, dtype=torch.float32)
         dlam = torch.empty(b, device=lg.device, dtype=torch.float32)
-        nat.mixup_ce_fwd(lg.data_ptr(), ya.to(torch.int32).contiguous().data_ptr(),
-                         yb.to(torch.int32).contiguous().data_ptr(), lam_vec.data_ptr(), loss.data_ptr(),
+        # keep the int32 label copies referenced until the launch is enqueued: a temporary
+        # freed inside the argument list can be recycled by the caching allocator for the
+        # second copy (ya and yb would then alias)
+        ya32 = ya.to(torch.int32).contiguous()
+        yb32 = yb.to(torch.int32).contiguous()
+        nat.mixup_ce_fwd(lg.data_ptr(), ya32.data_ptr(), yb32.data_ptr(), lam_vec.data_ptr(), loss.data_ptr(),
                          glog.data_ptr(), dlam.data_ptr(), b, c, DT[lg.dtype], _native.stream_ptr())
         ctx.save_for_backward(glog, dlam)
         ctx.dt = logits.dtype

@@ -1,0 +1,399 @@
+"""MI355X execution engine for the ResNet family: the whole network body (stem + all residual
+blocks) is ONE autograd node whose forward and backward are explicit sequences of the
+hand-written HIP kernels.
+
+Why one node: the reference runs ~7 kernels and 3-4 activation passes per FusedConvBN in
+forward and ~15 in backward, recomputing the conv (resnet.py:72-113, survey CS4).  Here
+each convolution is one implicit-GEMM MFMA kernel whose prologue applies the producer's
+batch-norm + activation while staging the operand (a conv output is never normalised in
+memory) and whose epilogue emits the per-channel statistics of its own output.  Backward
+is likewise one dgrad kernel (prologue: the batch-norm backward correction
+g + alpha + beta*y; epilogue: the consumer activation backward + the producer's
+statistics reductions) and one wgrad kernel per convolution.  Owning the whole body lets
+the engine
+
+* accumulate the two data-gradient contributions of a block input (residual path and
+  shortcut) inside the second dgrad's epilogue (no autograd sum kernel),
+* write weight / BN-affine gradients straight into the flat gradient buffer and signal
+  DDP bucket readiness itself (``grad_ready``), in backward order,
+* pack every conv weight to bf16 GEMM layouts in one launch per step,
+* stay free of host synchronisation and allocation-order dependence, so a whole train
+  step can be captured in a HIP graph.
+
+Numerics follow the reference exactly where it defines the model: FusedConvBN uses batch
+statistics in train AND eval with unbiased variance and (y-mean)/(sqrt(var)+1e-3)
+(resnet.py:75-100); nn.BatchNorm2d uses biased variance, affine, running statistics with
+momentum (resnet.py:204-206, 221-223).  Compute is bf16 MFMA with fp32 accumulation and
+fp32/fp64 statistics.
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn as nn
+
+from . import _native
+from . import conv_igemm as ci
+
+ACT_NONE, ACT_RELU, ACT_CELU = 0, 1, 2
+MODE_FCBN, MODE_BN_TRAIN, MODE_BN_EVAL = 0, 1, 2
+BF16 = torch.bfloat16
+
+# Parameters whose gradient the engine writes itself call these hooks (the DDP reducer
+# registers here in addition to autograd's post-accumulate-grad hooks).
+_GRAD_READY_HOOKS: dict[int, list] = {}
+
+
+def register_grad_ready_hook(param, fn):
+    _GRAD_READY_HOOKS.setdefault(id(param), []).append(fn)
+
+    class _Handle:
+        def remove(self_inner):
+            lst = _GRAD_READY_HOOKS.get(id(param), [])
+            if fn in lst:
+                lst.remove(fn)
+    return _Handle()
+
+
+def grad_ready(param):
+    for fn in _GRAD_READY_HOOKS.get(id(param), ()):
+        fn(param)
+
+
+def _sp():
+    return _native.stream_ptr()
+
+
+def _p(t):
+    return 0 if t is None else t.data_ptr()
+
+
+def _f32(n, dev):
+    return torch.empty(n, device=dev, dtype=torch.float32)
+
+
+class Unit:
+    """One convolution + its normalisation."""
+
+    def __init__(self, conv, bn, act_out):
+        from ..models.resnet import FusedConvBN
+        if isinstance(conv, FusedConvBN):
+            self.w = conv.conv_weight
+            stride, pad = 1, conv.padding
+            self.bn = None
+            self.eps = conv.eps
+        else:
+            assert isinstance(conv, nn.Conv2d) and isinstance(bn, nn.BatchNorm2d)
+            self.w = conv.weight
+            stride, pad = conv.stride[0], conv.padding[0]
+            self.bn = bn
+            self.eps = bn.eps
+        cout, cin, k, _ = self.w.shape
+        self.shp = ci.ConvShape(cin, cout, k, stride, pad)
+        self.act_out = act_out  # activation the consumer applies to this unit's normalised output
+        self.wf = self.wd = None
+
+    def mode(self, training):
+        if self.bn is None:
+            return MODE_FCBN
+        use_batch = training or not self.bn.track_running_stats
+        return MODE_BN_TRAIN if use_batch else MODE_BN_EVAL
+
+    def ensure_packed_buffers(self, dev, need_dgrad):
+        if self.wf is None or self.wf.device != dev:
+            self.wf, self.wd = ci.alloc_packed(self.shp, dev, dgrad=need_dgrad and self.shp.cin >= 8)
+
+
+def _act_of(m):
+    if isinstance(m, nn.ReLU):
+        return (ACT_RELU, 1.0)
+    if isinstance(m, nn.CELU):
+        return (ACT_CELU, float(m.alpha))
+    return None
+
+
+def _chain(seq: nn.Sequential):
+    """nn.Sequential of (FusedConvBN | Conv2d+BatchNorm2d | activation) -> [Unit]."""
+    mods = list(seq)
+    units = []
+    i = 0
+    while i < len(mods):
+        m = mods[i]
+        a = _act_of(m)
+        if a is not None:
+            assert units, "activation before any conv"
+            units[-1].act_out = a
+            i += 1
+            continue
+        if isinstance(m, nn.Conv2d):
+            units.append(Unit(m, mods[i + 1], (ACT_NONE, 1.0)))
+            i += 2
+        else:
+            units.append(Unit(m, None, (ACT_NONE, 1.0)))
+            i += 1
+    return units
+
+
+class Block:
+    def __init__(self, blk):
+        from ..models.resnet import BottleNeck
+        self.units = _chain(blk.residual_function)
+        sc = _chain(blk.shortcut) if len(blk.shortcut) > 0 else []
+        assert len(sc) <= 1
+        self.shortcut = sc[0] if sc else None
+        self.join = (ACT_RELU, 1.0) if isinstance(blk, BottleNeck) else (ACT_CELU, 0.075)
+
+
+class Plan:
+    def __init__(self, model):
+        stem_seq = model.conv1
+        self.stem = Unit(stem_seq[0], None, _act_of(stem_seq[1]))
+        self.blocks = [Block(b) for stage in (model.conv2_x, model.conv3_x, model.conv4_x, model.conv5_x)
+                       for b in stage]
+        self.units = [self.stem] + [u for b in self.blocks for u in (b.units + ([b.shortcut] if b.shortcut else []))]
+
+    def pack(self, dev, need_dgrad=True):
+        ents = []
+        for u in self.units:
+            u.ensure_packed_buffers(dev, need_dgrad and u is not self.stem)
+            ents.append((u.w.detach(), u.wf, u.wd, u.shp))
+        ci.pack_weights(ents)
+
+
+# ------------------------------------------------------------------ kernels glue
+def compact(part, rows=64):
+    """[nb, q, C] per-workgroup slabs -> [ceil(nb/rows), q, C] (one wide pass) when large."""
+    if part is None or part.shape[0] <= 2 * rows:
+        return part
+    nb = part.shape[0]
+    nk = -(-nb // rows)
+    out = torch.empty(nk, *part.shape[1:], device=part.device, dtype=torch.float32)
+    _native.native().partials_compact(part.data_ptr(), nb, part[0].numel(), rows, out.data_ptr(), _sp())
+    return out
+
+
+def finalize_stats(part, u: Unit, M, training, dev):
+    nat = _native.native()
+    C = u.shp.cout
+    s, t, sm, sa = _f32(C, dev), _f32(C, dev), _f32(C, dev), _f32(C, dev)
+    mode = u.mode(training)
+    bn = u.bn
+    if bn is not None:
+        mom = bn.momentum if bn.momentum is not None else 0.1
+        track = training and bn.track_running_stats
+        rm = bn.running_mean if (track or mode == MODE_BN_EVAL) else None
+        rv = bn.running_var if (track or mode == MODE_BN_EVAL) else None
+        nbt = bn.num_batches_tracked if track else None
+        gamma, beta = bn.weight, bn.bias
+    else:
+        mom, rm, rv, nbt, gamma, beta = 0.0, None, None, None, None, None
+    part = compact(part) if mode != MODE_BN_EVAL else part
+    nb = part.shape[0] if (part is not None and mode != MODE_BN_EVAL) else 0
+    nat.stats_finalize(_p(part) if nb else 0, nb, C, float(M), mode, float(u.eps), float(mom), _p(gamma), _p(beta),
+                       _p(rm), _p(rv), _p(nbt), s.data_ptr(), t.data_ptr(), sm.data_ptr(), sa.data_ptr(), _sp())
+    return s, t, sm, sa
+
+
+def reduce_parts(part, nq, C, dev):
+    nat = _native.native()
+    part = compact(part)
+    out = torch.empty(nq, C, device=dev, dtype=torch.float32)
+    nat.reduce_partials(part.data_ptr(), part.shape[0], nq, C, out.data_ptr(), _sp())
+    return out
+
+
+def bwd_coef(u: Unit, gs, gt, sm, sa, M, training, dev):
+    """(g_s, g_t) of the normalisation of y -> correction (alpha, beta) of dL/dy; BN affine
+    gradients are accumulated into the flat gradient buffer."""
+    nat = _native.native()
+    C = u.shp.cout
+    al, be = _f32(C, dev), _f32(C, dev)
+    mode = u.mode(training)
+    gamma = u.bn.weight if u.bn is not None else None
+    gg = gb = None
+    if u.bn is not None:
+        for p in (u.bn.weight, u.bn.bias):
+            if p.requires_grad and p.grad is None:
+                p.grad = torch.zeros_like(p)
+        gg = u.bn.weight.grad if u.bn.weight.requires_grad else None
+        gb = u.bn.bias.grad if u.bn.bias.requires_grad else None
+    nat.stats_bwd_coef(gs.data_ptr(), gt.data_ptr(), C, float(M), mode, float(u.eps), sm.data_ptr(), sa.data_ptr(),
+                       _p(gamma), al.data_ptr(), be.data_ptr(), _p(gg), _p(gb), _sp())
+    if u.bn is not None:
+        grad_ready(u.bn.weight)
+        grad_ready(u.bn.bias)
+    return al, be
+
+
+def wgrad_into(u: Unit, g, y, al, be, x, xs, xt, act):
+    if u.w.grad is None:
+        u.w.grad = torch.zeros_like(u.w)
+    ci.conv_wgrad(g, y, al, be, x, u.shp, u.w.grad, xs, xt, act[0], act[1], accumulate=True)
+    grad_ready(u.w)
+
+
+def _rows(t):
+    return t.numel() // t.shape[-1]
+
+
+# ------------------------------------------------------------------ autograd node
+class ResNetBodyFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x_nhwc, plan: Plan, training: bool, need_grad: bool):
+        nat = _native.native()
+        dev = x_nhwc.device
+        plan.pack(dev, need_dgrad=need_grad)
+        recs = []
+        # stem: conv -> FCBN stats -> materialised CELU output
+        st = plan.stem
+        y0, part = ci.conv_fwd(x_nhwc, st.wf, st.shp)
+        M0 = _rows(y0)
+        s0, t0, sm0, sa0 = finalize_stats(part, st, M0, training, dev)
+        h = torch.empty_like(y0)
+        nat.act_affine_fwd(y0.data_ptr(), s0.data_ptr(), t0.data_ptr(), h.data_ptr(), M0, st.shp.cout,
+                           st.act_out[0], float(st.act_out[1]), 1, 1, _sp())
+        stem_rec = (x_nhwc, y0, s0, t0, sm0, sa0)
+        for b in plan.blocks:
+            x_in = h
+            ys = []
+            raw, s, t, act = x_in, None, None, (ACT_NONE, 1.0)
+            for u in b.units:
+                y, part = ci.conv_fwd(raw, u.wf, u.shp, s, t, act[0], act[1])
+                M = _rows(y)
+                su, tu, smu, sau = finalize_stats(part, u, M, training, dev)
+                ys.append((y, su, tu, smu, sau, M))
+                raw, s, t, act = y, su, tu, u.act_out
+            y3, s3, t3 = ys[-1][0], ys[-1][1], ys[-1][2]
+            sc = None
+            if b.shortcut is not None:
+                u = b.shortcut
+                ysc, part = ci.conv_fwd(x_in, u.wf, u.shp)
+                M = _rows(ysc)
+                ssc, tsc, smsc, sasc = finalize_stats(part, u, M, training, dev)
+                sc = (ysc, ssc, tsc, smsc, sasc, M)
+            out = torch.empty_like(y3)
+            C = y3.shape[-1]
+            nat.residual_act_fwd(y3.data_ptr(), s3.data_ptr(), t3.data_ptr(), _p(sc[0] if sc else None),
+                                 _p(sc[1] if sc else None), _p(sc[2] if sc else None),
+                                 0 if sc else x_in.data_ptr(), out.data_ptr(), _rows(y3), C, b.join[0],
+                                 float(b.join[1]), 1, _sp())
+            if need_grad:
+                recs.append((x_in, ys, sc, out))
+            h = out
+        if need_grad:
+            ctx.plan, ctx.training = plan, training
+            ctx.recs, ctx.stem_rec = recs, stem_rec
+        return h
+
+    @staticmethod
+    def backward(ctx, g_out):
+        nat = _native.native()
+        plan, training = ctx.plan, ctx.training
+        g = g_out.contiguous()
+        dev = g.device
+        for b, (x_in, ys, sc, out) in zip(reversed(plan.blocks), reversed(ctx.recs)):
+            y3, s3 = ys[-1][0], ys[-1][1]
+            C = y3.shape[-1]
+            M = _rows(y3)
+            nb = nat.stats_num_blocks(M, C)
+            part = torch.empty(nb, 3, C, device=dev, dtype=torch.float32)
+            gya = torch.empty_like(y3)
+            gyb = torch.empty_like(out)  # shortcut-branch grad, or the identity grad of x_in
+            nat.residual_act_bwd(g.data_ptr(), out.data_ptr(), y3.data_ptr(), s3.data_ptr(),
+                                 _p(sc[0] if sc else None), _p(sc[1] if sc else None), gya.data_ptr(),
+                                 gyb.data_ptr(), part.data_ptr(), M, C, b.join[0], float(b.join[1]), 1, _sp())
+            red = reduce_parts(part, 3, C, dev)
+            gs, gt = red[0], red[1]
+            g_cur = gya
+            g_x = None if sc is not None else gyb
+            # residual chain, last unit first
+            for i in range(len(b.units) - 1, -1, -1):
+                u = b.units[i]
+                y, su, tu, smu, sau, Mu = ys[i]
+                al, be = bwd_coef(u, gs, gt, smu, sau, Mu, training, dev)
+                if i > 0:
+                    yp, sp_, tp, _, _, _ = ys[i - 1]
+                    actp = b.units[i - 1].act_out
+                    g_prev, pp = ci.conv_dgrad(g_cur, y, al, be, u.wd, u.shp, tuple(yp.shape), epi=ci.EPI_ACTBWD,
+                                               ex=yp, es=sp_, et=tp, act=actp[0], alpha=actp[1])
+                    r2 = reduce_parts(pp, 2, u.shp.cin, dev)
+                    wgrad_into(u, g_cur, y, al, be, yp, sp_, tp, actp)
+                    gs, gt = r2[0], r2[1]
+                    g_cur = g_prev
+                else:
+                    if g_x is None:
+                        g_x, _ = ci.conv_dgrad(g_cur, y, al, be, u.wd, u.shp, tuple(x_in.shape), epi=ci.EPI_STORE)
+                    else:
+                        ci.conv_dgrad(g_cur, y, al, be, u.wd, u.shp, tuple(x_in.shape), epi=ci.EPI_ADD, out=g_x)
+                    wgrad_into(u, g_cur, y, al, be, x_in, None, None, (ACT_NONE, 1.0))
+            if sc is not None:
+                u = b.shortcut
+                ysc, ssc, tsc, smsc, sasc, Msc = sc
+                al, be = bwd_coef(u, red[2], red[1], smsc, sasc, Msc, training, dev)
+                ci.conv_dgrad(gyb, ysc, al, be, u.wd, u.shp, tuple(x_in.shape), epi=ci.EPI_ADD, out=g_x)
+                wgrad_into(u, gyb, ysc, al, be, x_in, None, None, (ACT_NONE, 1.0))
+            g = g_x
+        # stem: act backward + statistics -> wgrad on the input image
+        x_img, y0, s0, t0, sm0, sa0 = ctx.stem_rec
+        st = plan.stem
+        M0 = _rows(y0)
+        C0 = st.shp.cout
+        nb = nat.stats_num_blocks(M0, C0)
+        part = torch.empty(nb, 2, C0, device=dev, dtype=torch.float32)
+        gy0 = torch.empty_like(y0)
+        nat.act_bwd_reduce(g.data_ptr(), y0.data_ptr(), s0.data_ptr(), t0.data_ptr(), gy0.data_ptr(),
+                           part.data_ptr(), M0, C0, st.act_out[0], float(st.act_out[1]), 1, _sp())
+        red = reduce_parts(part, 2, C0, dev)
+        al, be = bwd_coef(st, red[0], red[1], sm0, sa0, M0, training, dev)
+        wgrad_into(st, gy0, y0, al, be, x_img, None, None, (ACT_NONE, 1.0))
+        ctx.recs = ctx.stem_rec = None
+        return None, None, None, None
+
+
+def to_engine_input(x: torch.Tensor, cxp: int = 8) -> torch.Tensor:
+    """(N,3,H,W) image batch (any layout/dtype) -> (N,H,W,cxp) bf16 zero-padded NHWC.
+    Zero-copy when x is the channel-sliced NCHW view of such a buffer (the device CIFAR
+    loader produces exactly that)."""
+    N, C, H, W = x.shape
+    if x.dtype == BF16 and x.stride() == (H * W * cxp, 1, W * cxp, cxp):
+        return torch.as_strided(x, (N, H, W, cxp), (H * W * cxp, W * cxp, cxp, 1))
+    out = torch.zeros(N, H, W, cxp, device=x.device, dtype=BF16)
+    out[..., :C] = x.permute(0, 2, 3, 1)
+    return out
+
+
+def resnet_engine_forward(model, x):
+    """Forward of ``models.resnet.ResNet`` through the engine; returns logits."""
+    plan = getattr(model, "_plan", None)
+    if plan is None:
+        plan = model._plan = Plan(model)
+    xin = to_engine_input(x, plan.stem.shp.cxp)
+    need_grad = torch.is_grad_enabled() and any(p.requires_grad for p in model.parameters())
+    if need_grad:
+        # the engine writes weight gradients itself; autograd sees one node whose only
+        # differentiable input is a dummy (the image batch needs no gradient)
+        dummy = torch.empty(0, device=x.device, requires_grad=True)
+        body = _BodyWithDummy.apply(xin, dummy, plan, model.training)
+    else:
+        body = ResNetBodyFn.forward(_NoCtx(), xin, plan, model.training, False)
+    pooled = body.float().mean(dim=(1, 2))
+    return model.fc(pooled)
+
+
+class _NoCtx:
+    pass
+
+
+class _BodyWithDummy(torch.autograd.Function):
+    """Gives the body node a differentiable input so autograd calls its backward even
+    though the image batch does not require grad."""
+
+    @staticmethod
+    def forward(ctx, xin, dummy, plan, training):
+        ctx.inner = _NoCtx()
+        out = ResNetBodyFn.forward(ctx.inner, xin, plan, training, True)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        ResNetBodyFn.backward(ctx.inner, g)
+        return None, None, None, None

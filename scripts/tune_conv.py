@@ -1,0 +1,108 @@
+#!/usr/bin/env python3
+"""Tile sweep for the implicit-GEMM conv kernels on the ResNet-50 shapes.
+
+For every (op, batch, shape) it times every legal (BM, BN, BK[, nsplit]) configuration on
+the GPU (HIP events, random data) and writes the fastest into
+``faster_distributed_training_amd/ops/conv_tuned.json`` — the table the engine consults
+before falling back to ``conv_igemm.pick_tile``.
+
+    python scripts/tune_conv.py --batches 1024 128 [--out path]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import torch
+
+from faster_distributed_training_amd.ops import conv_igemm as ci
+from bench_conv import SHAPES, timeit
+
+FWD_TILES = [(128, 128, 64), (128, 64, 64), (64, 128, 64), (64, 64, 64), (256, 64, 64),
+             (128, 128, 32), (128, 64, 32), (64, 128, 32), (64, 64, 32), (256, 128, 32)]
+WG_TILES = [(128, 128, 32), (64, 128, 32), (128, 64, 32), (64, 64, 32),
+            (128, 128, 64), (64, 128, 64), (128, 64, 64), (64, 64, 64)]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--batches", type=int, nargs="+", default=[1024, 128])
+    ap.add_argument("--reps", type=int, default=10)
+    ap.add_argument("--out", default=os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                                  "faster_distributed_training_amd", "ops", "conv_tuned.json"))
+    a = ap.parse_args()
+    dev = torch.device("cuda")
+    table = {}
+    if os.path.exists(a.out):
+        with open(a.out) as f:
+            table = json.load(f)
+    for N in a.batches:
+        for (H, Cin, Cout, k, s, p, _cnt) in SHAPES:
+            shp = ci.ConvShape(Cin, Cout, k, s, p)
+            torch.manual_seed(0)
+            x = torch.randn(N, H, H, shp.cxp, device=dev).to(torch.bfloat16)
+            w = torch.randn(Cout, Cin, k, k, device=dev) / (Cin * k * k) ** 0.5
+            wf, wd = ci.alloc_packed(shp, dev, dgrad=Cin >= 8)
+            ci.pack_weights([(w, wf, wd, shp)])
+            Ho, Wo = ci.out_hw(H, H, shp)
+            g = torch.randn(N, Ho, Wo, Cout, device=dev).to(torch.bfloat16)
+            yy = torch.randn(N, Ho, Wo, Cout, device=dev).to(torch.bfloat16)
+            al = torch.zeros(Cout, device=dev)
+            be = torch.zeros(Cout, device=dev)
+            sv = torch.ones(shp.cxp, device=dev)
+            tv = torch.zeros(shp.cxp, device=dev)
+            ex = torch.randn(N, H, H, Cin, device=dev).to(torch.bfloat16) if Cin >= 8 else None
+            es = torch.ones(Cin, device=dev)
+            et = torch.zeros(Cin, device=dev)
+            gw = torch.empty(Cout, Cin, k, k, device=dev)
+            key = ci.tune_key(N, H, shp)
+            res = {}
+            best = None
+            for t in FWD_TILES:
+                if Cout % t[1]:
+                    continue
+                ms = timeit(lambda: ci.conv_fwd(x, wf, shp, sv, tv, 1, 1.0, tile=t), a.reps)
+                if best is None or ms < best[0]:
+                    best = (ms, t)
+            res["fwd"] = dict(tile=best[1], us=round(best[0] * 1e3, 1))
+            if Cin >= 8:
+                best = None
+                for t in FWD_TILES:
+                    if Cin % t[1]:
+                        continue
+                    ms = timeit(lambda: ci.conv_dgrad(g, yy, al, be, wd, shp, (N, H, H, Cin), epi=ci.EPI_ACTBWD,
+                                                      ex=ex, es=es, et=et, act=1, tile=t), a.reps)
+                    if best is None or ms < best[0]:
+                        best = (ms, t)
+                res["dgrad"] = dict(tile=best[1], us=round(best[0] * 1e3, 1))
+            best = None
+            ldw = shp.ntaps * shp.cxp
+            slab = torch.empty(1024 * Cout * ldw // 4 + 1, device=dev)
+            for t in WG_TILES:
+                if Cout % t[0] or (t[1] == 128 and ldw < 128):
+                    continue
+                tiles = (Cout // t[0]) * (-(-ldw // t[1]))
+                base = ci.wgrad_split(N * Ho * Wo, tiles)
+                for ns in sorted({max(1, base // 2), base, base * 2}):
+                    if ns * Cout * ldw > slab.numel():
+                        continue
+                    ms = timeit(lambda: ci.conv_wgrad(g, yy, al, be, x, shp, gw, sv, tv, 1, tile=t, nsplit=ns,
+                                                      slab=slab), a.reps)
+                    if best is None or ms < best[0]:
+                        best = (ms, t, ns)
+            res["wgrad"] = dict(tile=best[1], nsplit=best[2], us=round(best[0] * 1e3, 1))
+            table[key] = res
+            print(key, json.dumps(res), flush=True)
+            del x, g, yy, ex, slab
+            torch.cuda.empty_cache()
+    with open(a.out, "w") as f:
+        json.dump(table, f, indent=1, sort_keys=True)
+    print("wrote", a.out)
+
+
+if __name__ == "__main__":
+    main()

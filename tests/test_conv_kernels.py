@@ -73,7 +73,7 @@ def test_conv_fwd(cuda, case, mode):
         t = torch.randn(shp.cxp, device=cuda) * 0.3
         act, alpha = (1, 1.0) if mode == "relu" else (2, 0.075)
         a = act_ref(x.float() * s + t, act, alpha).to(BF).float()[..., :Cin]
-    for tile in [None, (64, 64), (128, 64)]:
+    for tile in [None, (64, 64, 64), (128, 64, 32), (256, 128, 32), (256, 64, 64)]:
         if tile and Cout % tile[1]:
             continue
         y, part = ci.conv_fwd(x, wf, shp, s, t, act, alpha, tile=tile)
@@ -112,8 +112,9 @@ def test_conv_dgrad(cuda, case, epi):
     ref = nhwc(torch.nn.grad.conv2d_input((N, Cin, H, H), w.to(BF).float(), nchw(gt), stride=stride, padding=pad))
     xs = (N, H, H, Cin)
     if epi == "store":
-        out, _ = ci.conv_dgrad(g, y, al, be, wd, shp, xs, epi=ci.EPI_STORE)
-        assert rel(out, ref) < 1e-2
+        for tile in [None, (64, 64, 32), (128, 64, 64)]:
+            out, _ = ci.conv_dgrad(g, y, al, be, wd, shp, xs, epi=ci.EPI_STORE, tile=tile)
+            assert rel(out, ref) < 1e-2, tile
     elif epi == "add":
         prev = make(xs, cuda)
         out = prev.clone()
@@ -166,7 +167,9 @@ def test_conv_wgrad(cuda, case, mode):
         gt = (g.float() + al + be * y.float()).to(BF).float()
         a = torch.relu(x.float() * xs + xt).to(BF).float()[..., :Cin]
     ref = torch.nn.grad.conv2d_weight(nchw(a), (Cout, Cin, k, k), nchw(gt), stride=stride, padding=pad)
-    for ns in [1, 3]:
+    for ns, tile in [(1, None), (3, None), (2, (64, 64, 32)), (1, (128, 128, 64))]:
+        if tile and Cout % tile[0]:
+            continue
         out = torch.empty(Cout, Cin, k, k, device=cuda)
-        ci.conv_wgrad(g, y, al, be, x, shp, out, xs, xt, act, nsplit=ns)
-        assert rel(out, ref) < 5e-3, (ns, rel(out, ref))
+        ci.conv_wgrad(g, y, al, be, x, shp, out, xs, xt, act, nsplit=ns, tile=tile)
+        assert rel(out, ref) < 5e-3, (ns, tile, rel(out, ref))

@@ -13,138 +13,6 @@ def rel(a, b):
     return ((a - b).norm() / (b.norm() + 1e-12)).item()
 
 
-# ---------------------------------------------------------------- normalisation engine
-@pytest.mark.parametrize("C", [64, 256, 2048])
-def test_batch_stats_fcbn(cuda, C):
-    from faster_distributed_training_amd.ops import resnet_engine as E
-    y = (torch.randn(4096, C, device=cuda) * 3 + 1.5).to(torch.bfloat16)
-    s, t, m, sd = E.batch_stats(y, E.MODE_FCBN, 1e-3)
-    yf = y.float()
-    mean = yf.mean(0)
-    sdr = yf.var(0, unbiased=True).sqrt()
-    assert rel(m, mean) < 1e-5
-    assert rel(sd, sdr) < 1e-5
-    assert rel(s, 1 / (sdr + 1e-3)) < 1e-5
-    assert rel(t, -mean / (sdr + 1e-3)) < 1e-4
-
-
-def test_batch_stats_bn_running(cuda):
-    from faster_distributed_training_amd.ops import resnet_engine as E
-    C = 128
-    y = torch.randn(8, 16, 16, C, device=cuda).to(torch.bfloat16)
-    bn = torch.nn.BatchNorm2d(C).to(cuda)
-    with torch.no_grad():
-        bn.weight.uniform_(0.5, 1.5)
-        bn.bias.uniform_(-0.5, 0.5)
-    rm, rv = bn.running_mean.clone(), bn.running_var.clone()
-    nbt = bn.num_batches_tracked.clone()
-    s, t, m, inv = E.batch_stats(y, E.MODE_BN_TRAIN, bn.eps, 0.1, bn.weight, bn.bias, rm, rv, nbt)
-    ref = bn.train()(y.float().permute(0, 3, 1, 2))
-    out = (y.float() * s + t).permute(0, 3, 1, 2)
-    assert rel(out, ref) < 1e-4
-    assert rel(rm, bn.running_mean) < 1e-5 and rel(rv, bn.running_var) < 1e-5
-    assert int(nbt) == int(bn.num_batches_tracked)
-
-
-@pytest.mark.parametrize("act", [0, 1, 2])
-def test_act_bwd_reduce(cuda, act):
-    from faster_distributed_training_amd.ops import _native
-    C, M = 256, 2048
-    nat = _native.native()
-    x = torch.randn(M, C, device=cuda).to(torch.bfloat16)
-    s = torch.rand(C, device=cuda) + 0.5
-    t = torch.randn(C, device=cuda) * 0.3
-    g = torch.randn(M, C, device=cuda).to(torch.bfloat16)
-    gx = torch.empty_like(x)
-    nb = nat.stats_num_blocks(M, C)
-    part = torch.empty(nb, 2, C, device=cuda)
-    nat.act_bwd_reduce(g.data_ptr(), x.data_ptr(), s.data_ptr(), t.data_ptr(), gx.data_ptr(), part.data_ptr(), M, C,
-                       act, 0.075, 1, _native.stream_ptr())
-    red = torch.empty(2, C, device=cuda)
-    nat.reduce_partials(part.data_ptr(), nb, 2, C, red.data_ptr(), _native.stream_ptr())
-    xs = x.float().requires_grad_()
-    ss = s.clone().requires_grad_()
-    ts = t.clone().requires_grad_()
-    z = xs * ss + ts
-    a = [lambda v: v, torch.relu, lambda v: F.celu(v, 0.075)][act](z)
-    a.backward(g.float())
-    assert rel(gx, xs.grad) < 1e-2
-    assert rel(red[0], ss.grad) < 1e-3
-    assert rel(red[1], ts.grad) < 1e-3
-
-
-def test_residual_join_fwd_bwd(cuda):
-    from faster_distributed_training_amd.ops.resnet_engine import ResidualJoinFn
-    C, M = 512, 1024
-    ya = torch.randn(M, C, device=cuda).to(torch.bfloat16).requires_grad_()
-    yb = torch.randn(M, C, device=cuda).to(torch.bfloat16).requires_grad_()
-    sa, ta, sb, tb = [(torch.rand(C, device=cuda) + 0.5).requires_grad_() for _ in range(4)]
-    out = ResidualJoinFn.apply(ya, sa, ta, yb, sb, tb, None, 1, 1.0)
-    g = torch.randn_like(out)
-    out.backward(g)
-    leaves = [ya.detach().float().requires_grad_(), sa.detach().requires_grad_(), ta.detach().requires_grad_(),
-              yb.detach().float().requires_grad_(), sb.detach().requires_grad_(), tb.detach().requires_grad_()]
-    ref = torch.relu(leaves[0] * leaves[1] + leaves[2] + leaves[3] * leaves[4] + leaves[5])
-    ref.backward(g.float())
-    assert rel(out, ref) < 1e-2
-    for got, want in zip([ya.grad, sa.grad, ta.grad, yb.grad, sb.grad, tb.grad], [l.grad for l in leaves]):
-        assert rel(got, want) < 2e-2
-
-
-# ---------------------------------------------------------------- whole network
-def _pair(arch, cuda):
-    from faster_distributed_training_amd.models import resnet as R
-    torch.manual_seed(0)
-    m_ref = getattr(R, arch)(10).to(cuda)
-    m_eng = getattr(R, arch)(10).to(cuda)
-    m_eng.load_state_dict(m_ref.state_dict())
-    m_ref.fast_path = False
-    m_eng.fast_path = True
-    return m_ref, m_eng
-
-
-@pytest.mark.parametrize("arch", ["resnet18", "resnet50"])
-def test_resnet_engine_fp32_matches_reference(cuda, arch):
-    """The engine in fp32 computes exactly the reference function (tight tolerance)."""
-    m_ref, m_eng = _pair(arch, cuda)
-    m_eng.engine_dtype = torch.float32
-    torch.backends.cudnn.allow_tf32 = False
-    x = torch.randn(32, 3, 32, 32, device=cuda)
-    y = torch.randint(0, 10, (32,), device=cuda)
-    out_r, out_e = m_ref(x), m_eng(x)
-    assert rel(out_e, out_r) < 2e-3
-    F.cross_entropy(out_r, y).backward()
-    F.cross_entropy(out_e, y).backward()
-    for (n, pr), (_, pe) in zip(m_ref.named_parameters(), m_eng.named_parameters()):
-        assert rel(pe.grad, pr.grad) < 2e-2, n
-    for (n, br), (_, be) in zip(m_ref.named_buffers(), m_eng.named_buffers()):
-        if br.dtype.is_floating_point:
-            assert rel(be, br) < 1e-3, n
-        else:
-            assert int(be) == int(br), n
-
-
-@pytest.mark.parametrize("arch", ["resnet18", "resnet50"])
-def test_resnet_engine_bf16_error_budget(cuda, arch):
-    """bf16 engine error vs the fp32 reference stays within 2x the error of the
-    reference itself run under bf16 autocast."""
-    m_ref, m_eng = _pair(arch, cuda)
-    x = torch.randn(64, 3, 32, 32, device=cuda)
-    y = torch.randint(0, 10, (64,), device=cuda)
-    out_r = m_ref(x)
-    with torch.autocast("cuda", dtype=torch.bfloat16):
-        out_rb = m_ref(x)
-    out_e = m_eng(x)
-    e_ref = rel(out_rb, out_r)
-    e_eng = rel(out_e, out_r)
-    assert e_eng < max(2.0 * e_ref, 5e-2), (e_eng, e_ref)
-    F.cross_entropy(out_r.float(), y).backward()
-    F.cross_entropy(out_e.float(), y).backward()
-    for (n, pr), (_, pe) in zip(m_ref.named_parameters(), m_eng.named_parameters()):
-        cos = F.cosine_similarity(pr.grad.flatten().float(), pe.grad.flatten().float(), dim=0).item()
-        assert cos > 0.9, (n, cos)
-
-
 # ---------------------------------------------------------------- optimizers
 @pytest.mark.parametrize("kind", ["sgd", "madgrad", "mirror", "adam"])
 def test_flat_optimizers_match_cpu(cuda, kind):
