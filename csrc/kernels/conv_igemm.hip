@@ -66,6 +66,8 @@ struct ConvArgs {
   float epi_alpha;
   int nbm, nbn;
   int8_t dh[12], dw[12], wt[12];
+  long Nb_HiWi_Cx_bytes;  // bytes of the activation operand(s)
+  long w_bytes;           // bytes of the packed weights
 };
 
 __device__ __forceinline__ uint32_t pk_bf16(float lo, float hi) { return pack_bf16x2(lo, hi); }
@@ -117,7 +119,28 @@ __device__ __forceinline__ void swap32(float& a, float& b) {
   b = __uint_as_float(r[1]);
 }
 
-template <int BM, int BN, int BK, int PRO, int EPI, bool PURE>
+// Activation helpers specialised at compile time (ACT: 0 none, 1 ReLU, 2 CELU(alpha)).
+template <int ACT>
+__device__ __forceinline__ float actf(float z, float alpha, float inv_alpha) {
+  if constexpr (ACT == kActRelu) return fmaxf(z, 0.f);
+  else if constexpr (ACT == kActCelu) return z > 0.f ? z : alpha * (__expf(z * inv_alpha) - 1.f);
+  else return z;
+}
+template <int ACT>
+__device__ __forceinline__ float actg(float z, float inv_alpha) {
+  if constexpr (ACT == kActRelu) return z > 0.f ? 1.f : 0.f;
+  else if constexpr (ACT == kActCelu) return z > 0.f ? 1.f : __expf(z * inv_alpha);
+  else return 1.f;
+}
+
+__device__ __forceinline__ uint4 ld_buf16(__amdgpu_buffer_rsrc_t r, uint32_t byte_off) {
+  auto v = __builtin_amdgcn_raw_buffer_load_b128(r, byte_off, 0, 0);
+  return *reinterpret_cast<uint4*>(&v);
+}
+
+constexpr uint32_t kOOB = 0xFFFFFFF0u;  // byte offset past any buffer: the load returns zeros
+
+template <int BM, int BN, int BK, int PRO, int EPI, bool PURE, int ACT>
 __global__ __launch_bounds__(256) void igemm_kernel(const ConvArgs a) {
   constexpr int CPR = BK / 8;        // 16-B chunks per LDS row
   constexpr int RPR = 256 / CPR;     // rows covered by one load round
@@ -129,11 +152,12 @@ __global__ __launch_bounds__(256) void igemm_kernel(const ConvArgs a) {
 
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int nkt = (a.K + BK - 1) / BK;
-  const int nbuf = nkt > 1 ? 2 : 1;                                  // K <= BK: one LDS buffer
-  bf16* tiles = reinterpret_cast<bf16*>(smem);                       // [nbuf][WT + XT]
+  const int nbuf = nkt > 1 ? 2 : 1;                                    // K <= BK: one LDS buffer
+  bf16* tiles = reinterpret_cast<bf16*>(smem);                         // [nbuf][WT + XT]
   float* pst = reinterpret_cast<float*>(smem + nbuf * (XT + WT) * 2);  // [2][Cx] (PRO != none)
-  float* red = pst + (PRO != kProNone ? 2 * a.Cx : 0);               // [2 waves][2][BN]
-  int* tapt = reinterpret_cast<int*>(red + 4 * BN);                  // [12]: dh | dw<<8 | wt<<16
+  float* red = pst + (PRO != kProNone ? 2 * a.Cx : 0);                 // [2 waves][2][BN]
+  int* tapt = reinterpret_cast<int*>(red + 4 * BN);                    // [12]: tap pixel offset
+  int* tapw = tapt + 12;                                               // [12]: dh | dw<<8 | wt<<16
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wn = wid & 1, wm = wid >> 1;
@@ -141,6 +165,16 @@ __global__ __launch_bounds__(256) void igemm_kernel(const ConvArgs a) {
   const int bn = id % a.nbn, bm = id / a.nbn;
   const long m0 = (long)bm * BM;
   const int n0 = bn * BN;
+  const float inv_alpha = ACT == kActCelu ? 1.f / (PRO == kProAffineAct ? a.pro_alpha : a.epi_alpha) : 1.f;
+
+  // buffer descriptors (wave-uniform, built from kernel arguments): 32-bit offsets and
+  // hardware bounds checking -> zero padding / K tails need no branches
+  const __amdgpu_buffer_rsrc_t rx_d = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)a.x, (short)0, (int)(a.Nb_HiWi_Cx_bytes), 0x00020000);
+  const __amdgpu_buffer_rsrc_t ry_d = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(PRO == kProFold ? a.x2 : a.x), (short)0, (int)(a.Nb_HiWi_Cx_bytes), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rw_d = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)a.w, (short)0, (int)(a.w_bytes), 0x00020000);
 
   if constexpr (PRO != kProNone) {
     for (int i = tid; i < a.Cx; i += 256) {
@@ -148,90 +182,89 @@ __global__ __launch_bounds__(256) void igemm_kernel(const ConvArgs a) {
       pst[a.Cx + i] = a.pt[i];
     }
   }
-  if (tid < 12) tapt[tid] = (int)(uint8_t)a.dh[tid] | ((int)(uint8_t)a.dw[tid] << 8) | ((int)(uint8_t)a.wt[tid] << 16);
+  if (tid < 12) {
+    const int dh = a.dh[tid], dw = a.dw[tid];
+    tapt[tid] = dh * a.Wi + dw;
+    tapw[tid] = (int)(uint8_t)a.dh[tid] | ((int)(uint8_t)a.dw[tid] << 8) | ((int)(uint8_t)a.wt[tid] << 16);
+  }
 
-  // ---- per-thread activation rows (fixed across K tiles)
+  // ---- per-thread activation rows (fixed across K tiles): pixel index of tap (0,0)
   const int cc = tid % CPR;  // this thread's 16-B chunk column inside a K tile
-  long xrow[NXL];            // PURE: pixel index; else n*Hi (row base)
-  int ohs[NXL], ows[NXL];
+  int pixb[NXL], ohs[NXL], ows[NXL];
   bool rv[NXL];
 #pragma unroll
   for (int j = 0; j < NXL; ++j) {
     const long m = m0 + tid / CPR + j * RPR;
     rv[j] = m < a.M;
     if constexpr (PURE) {
-      xrow[j] = m;
+      pixb[j] = (int)m;
       ohs[j] = ows[j] = 0;
     } else {
-      const long hw = (long)a.Ho * a.Wo;
-      const long n = m / hw;
-      const int rem = (int)(m - n * hw);
+      const int hw = a.Ho * a.Wo;
+      const int mi = rv[j] ? (int)m : 0;
+      const int n = mi / hw;
+      const int rem = mi - n * hw;
       const int oh = rem / a.Wo, ow = rem - (rem / a.Wo) * a.Wo;
-      xrow[j] = n * a.Hi;
       ohs[j] = oh * a.S;
       ows[j] = ow * a.S;
+      pixb[j] = (n * a.Hi + ohs[j]) * a.Wi + ows[j];
     }
   }
   __syncthreads();
 
-  uint4 rx[NXL], rx2[PRO == kProFold ? NXL : 1], rw[NWL];
-  bool xv[NXL];
-  int kci = 0;  // channel index of this thread's chunk in the tile being staged
+  // one register stage = the global loads of one K tile (staged to LDS after the MFMAs
+  // of the previous tile).  Two stages alternate so that the loads of tile k+2 are in
+  // flight during the MFMAs of tiles k and k+1.
+  struct Stage {
+    uint4 rx[NXL], rx2[PRO == kProFold ? NXL : 1], rw[NWL];
+    bool xv[NXL];
+    int kci;
+  };
 
-  auto load_tile = [&](int kt) {
+  auto load_tile = [&](Stage& S, int kt) {
     const int k = kt * BK + cc * 8;
     const int tap = k >> a.log2Cx;
     const int ci = k & (a.Cx - 1);
-    kci = ci;
+    S.kci = ci;
     const bool tok = tap < a.ntaps;
-    int dh = 0, dw = 0, wt = 0;
+    int dh = 0, dw = 0, wt = 0, toff = 0;
     if (!PURE && tok) {
-      const int e = tapt[tap];
+      const int e = tapw[tap];
       dh = (int)(int8_t)(e & 0xff);
       dw = (int)(int8_t)((e >> 8) & 0xff);
       wt = (e >> 16) & 0xff;
+      toff = tapt[tap];
     }
 #pragma unroll
     for (int j = 0; j < NXL; ++j) {
       bool v = rv[j] && tok;
-      long off;
-      if constexpr (PURE) {
-        off = xrow[j] * a.Cx + ci;
-      } else {
-        const int ih = ohs[j] + dh, iw = ows[j] + dw;
-        v = v && (unsigned)ih < (unsigned)a.Hi && (unsigned)iw < (unsigned)a.Wi;
-        off = ((xrow[j] + ih) * a.Wi + iw) * a.Cx + ci;
-      }
-      xv[j] = v;
-      if (v) {
-        rx[j] = *reinterpret_cast<const uint4*>(a.x + off);
-        if constexpr (PRO == kProFold) rx2[j] = *reinterpret_cast<const uint4*>(a.x2 + off);
-      } else {
-        rx[j] = make_uint4(0, 0, 0, 0);
-        if constexpr (PRO == kProFold) rx2[j] = make_uint4(0, 0, 0, 0);
-      }
+      if constexpr (!PURE)
+        v = v && (unsigned)(ohs[j] + dh) < (unsigned)a.Hi && (unsigned)(ows[j] + dw) < (unsigned)a.Wi;
+      S.xv[j] = v;
+      const uint32_t off = v ? (((uint32_t)(pixb[j] + toff) << a.log2Cx) + ci) * 2u : kOOB;
+      S.rx[j] = ld_buf16(rx_d, off);
+      if constexpr (PRO == kProFold) S.rx2[j] = ld_buf16(ry_d, off);
     }
-    const long wk = (long)(PURE ? 0 : wt) * a.Cx + ci;
+    const uint32_t wk = (uint32_t)((PURE ? 0 : wt) * a.Cx + ci);
 #pragma unroll
     for (int j = 0; j < NWL; ++j) {
       const int row = tid / CPR + j * RPR;
-      if (tok) rw[j] = *reinterpret_cast<const uint4*>(a.w + (long)(n0 + row) * a.ldw + wk);
-      else rw[j] = make_uint4(0, 0, 0, 0);
+      S.rw[j] = ld_buf16(rw_d, tok ? ((uint32_t)(n0 + row) * (uint32_t)a.ldw + wk) * 2u : kOOB);
     }
   };
 
-  auto store_tile = [&](int buf) {
+  auto store_tile = [&](const Stage& S, int buf) {
     bf16* Wl = tiles + buf * (WT + XT);
     bf16* Xl = Wl + WT;
 #pragma unroll
     for (int j = 0; j < NWL; ++j) {
       const int row = tid / CPR + j * RPR;
-      *reinterpret_cast<uint4*>(Wl + row * BK + 8 * (cc ^ swz<CPR>(row))) = rw[j];
+      *reinterpret_cast<uint4*>(Wl + row * BK + 8 * (cc ^ swz<CPR>(row))) = S.rw[j];
     }
     float sv[8], tv[8];
     if constexpr (PRO != kProNone) {
-      const float4* sp = reinterpret_cast<const float4*>(pst + kci);
-      const float4* tp = reinterpret_cast<const float4*>(pst + a.Cx + kci);
+      const float4* sp = reinterpret_cast<const float4*>(pst + S.kci);
+      const float4* tp = reinterpret_cast<const float4*>(pst + a.Cx + S.kci);
       float4 s0 = sp[0], s1 = sp[1], t0 = tp[0], t1 = tp[1];
       sv[0] = s0.x; sv[1] = s0.y; sv[2] = s0.z; sv[3] = s0.w; sv[4] = s1.x; sv[5] = s1.y; sv[6] = s1.z; sv[7] = s1.w;
       tv[0] = t0.x; tv[1] = t0.y; tv[2] = t0.z; tv[3] = t0.w; tv[4] = t1.x; tv[5] = t1.y; tv[6] = t1.z; tv[7] = t1.w;
@@ -239,31 +272,31 @@ __global__ __launch_bounds__(256) void igemm_kernel(const ConvArgs a) {
 #pragma unroll
     for (int j = 0; j < NXL; ++j) {
       const int row = tid / CPR + j * RPR;
-      uint4 o = rx[j];
+      uint4 o = S.rx[j];
       if constexpr (PRO == kProAffineAct) {
-        if (xv[j]) {
-          float v[8];
-          const uint32_t u[4] = {o.x, o.y, o.z, o.w};
+        // act(x*s+t), then zero where the conv pads (select, no branch)
+        float v[8];
+        const uint32_t u[4] = {o.x, o.y, o.z, o.w};
 #pragma unroll
-          for (int q = 0; q < 4; ++q) { v[2 * q] = bf16_lo(u[q]); v[2 * q + 1] = bf16_hi(u[q]); }
+        for (int q = 0; q < 4; ++q) { v[2 * q] = bf16_lo(u[q]); v[2 * q + 1] = bf16_hi(u[q]); }
 #pragma unroll
-          for (int q = 0; q < 8; ++q) v[q] = act_fwd(fmaf(v[q], sv[q], tv[q]), a.pro_act, a.pro_alpha);
-          o = make_uint4(pk_bf16(v[0], v[1]), pk_bf16(v[2], v[3]), pk_bf16(v[4], v[5]), pk_bf16(v[6], v[7]));
-        }
+        for (int q = 0; q < 8; ++q) v[q] = actf<ACT>(fmaf(v[q], sv[q], tv[q]), a.pro_alpha, inv_alpha);
+        o = make_uint4(pk_bf16(v[0], v[1]), pk_bf16(v[2], v[3]), pk_bf16(v[4], v[5]), pk_bf16(v[6], v[7]));
+        if (!S.xv[j]) o = make_uint4(0, 0, 0, 0);
       } else if constexpr (PRO == kProFold) {
-        if (xv[j]) {
-          float g[8], y[8];
-          const uint32_t u[4] = {o.x, o.y, o.z, o.w};
-          const uint32_t uy[4] = {rx2[j].x, rx2[j].y, rx2[j].z, rx2[j].w};
+        // g + alpha + beta*y (padding: g = y = 0 from the bounds-checked load -> masked)
+        float g[8], y[8];
+        const uint32_t u[4] = {o.x, o.y, o.z, o.w};
+        const uint32_t uy[4] = {S.rx2[j].x, S.rx2[j].y, S.rx2[j].z, S.rx2[j].w};
 #pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            g[2 * q] = bf16_lo(u[q]); g[2 * q + 1] = bf16_hi(u[q]);
-            y[2 * q] = bf16_lo(uy[q]); y[2 * q + 1] = bf16_hi(uy[q]);
-          }
-#pragma unroll
-          for (int q = 0; q < 8; ++q) g[q] += fmaf(tv[q], y[q], sv[q]);  // g + alpha + beta*y
-          o = make_uint4(pk_bf16(g[0], g[1]), pk_bf16(g[2], g[3]), pk_bf16(g[4], g[5]), pk_bf16(g[6], g[7]));
+        for (int q = 0; q < 4; ++q) {
+          g[2 * q] = bf16_lo(u[q]); g[2 * q + 1] = bf16_hi(u[q]);
+          y[2 * q] = bf16_lo(uy[q]); y[2 * q + 1] = bf16_hi(uy[q]);
         }
+#pragma unroll
+        for (int q = 0; q < 8; ++q) g[q] += fmaf(tv[q], y[q], sv[q]);
+        o = make_uint4(pk_bf16(g[0], g[1]), pk_bf16(g[2], g[3]), pk_bf16(g[4], g[5]), pk_bf16(g[6], g[7]));
+        if (!S.xv[j]) o = make_uint4(0, 0, 0, 0);
       }
       *reinterpret_cast<uint4*>(Xl + row * BK + 8 * (cc ^ swz<CPR>(row))) = o;
     }
@@ -277,14 +310,7 @@ __global__ __launch_bounds__(256) void igemm_kernel(const ConvArgs a) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
-  if (nkt > 0) {
-    load_tile(0);
-    store_tile(0);
-    __syncthreads();
-  }
-  for (int kt = 0; kt < nkt; ++kt) {
-    const int buf = kt & 1;
-    if (kt + 1 < nkt) load_tile(kt + 1);
+  auto compute = [&](int buf) {
     const bf16* Wl = tiles + buf * (WT + XT);
     const bf16* Xl = Wl + WT;
 #pragma unroll
@@ -306,26 +332,49 @@ __global__ __launch_bounds__(256) void igemm_kernel(const ConvArgs a) {
 #pragma unroll
         for (int j = 0; j < TM; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wf[i], xf[j], acc[i][j], 0, 0, 0);
     }
-    if (kt + 1 < nkt) store_tile(buf ^ 1);
+  };
+
+  // prologue: tile 0 -> LDS buf 0; tile 1 pending in B; tile 2 in flight in A
+  Stage SA, SB;
+  if (nkt > 0) {
+    load_tile(SA, 0);
+    if (nkt > 1) load_tile(SB, 1);
+    store_tile(SA, 0);
+    if (nkt > 2) load_tile(SA, 2);
     __syncthreads();
+  }
+  for (int kt = 0; kt < nkt; kt += 2) {
+    // even tile kt in buf 0; SB holds kt+1, SA holds kt+2 (in flight)
+    compute(0);
+    if (kt + 1 >= nkt) break;
+    store_tile(SB, 1);
+    __syncthreads();
+    if (kt + 3 < nkt) load_tile(SB, kt + 3);
+    // odd tile kt+1 in buf 1; SA holds kt+2, SB holds kt+3 (in flight)
+    compute(1);
+    if (kt + 2 >= nkt) break;
+    store_tile(SA, 0);
+    __syncthreads();
+    if (kt + 4 < nkt) load_tile(SA, kt + 4);
   }
 
   // ------------------------------------------------------------------ epilogue
   const int h = lane >> 5;
-  long orow[TM];
+  uint32_t orow[TM];
   bool ov[TM];
 #pragma unroll
   for (int j = 0; j < TM; ++j) {
     const long m = m0 + wm * (BM / 2) + j * 32 + (lane & 31);
     ov[j] = m < a.M;
+    const int mi = ov[j] ? (int)m : 0;
     if (a.OS == 1 && a.oy == 0 && a.ox == 0 && a.Hout == a.Ho && a.Wout == a.Wo) {
-      orow[j] = m;
+      orow[j] = (uint32_t)mi;
     } else {
-      const long hw = (long)a.Ho * a.Wo;
-      const long n = m / hw;
-      const int rem = (int)(m - n * hw);
+      const int hw = a.Ho * a.Wo;
+      const int n = mi / hw;
+      const int rem = mi - n * hw;
       const int oh = rem / a.Wo, ow = rem - (rem / a.Wo) * a.Wo;
-      orow[j] = (n * a.Hout + oh * a.OS + a.oy) * a.Wout + ow * a.OS + a.ox;
+      orow[j] = (uint32_t)((n * a.Hout + oh * a.OS + a.oy) * a.Wout + ow * a.OS + a.ox);
     }
   }
 
@@ -353,7 +402,7 @@ __global__ __launch_bounds__(256) void igemm_kernel(const ConvArgs a) {
           auto r0 = __builtin_amdgcn_permlane32_swap(a0, b0, false, false);
           auto r1 = __builtin_amdgcn_permlane32_swap(a1, b1, false, false);
           if (ov[j])
-            *reinterpret_cast<uint4*>(a.out + orow[j] * a.Cout + cb + 8 * g + 8 * h) =
+            *reinterpret_cast<uint4*>(a.out + orow[j] * (uint32_t)a.Cout + cb + 8 * g + 8 * h) =
                 make_uint4(r0[0], r1[0], r0[1], r1[1]);
         }
       }
@@ -393,7 +442,7 @@ __global__ __launch_bounds__(256) void igemm_kernel(const ConvArgs a) {
           const int c = cb + 8 * g + 8 * h;
           if (ov[j]) {
             float xv8[8], sv[8], tv[8], o[8];
-            Vec8<bf16>::load(a.ex + orow[j] * a.Cout + c, xv8);
+            Vec8<bf16>::load(a.ex + orow[j] * (uint32_t)a.Cout + c, xv8);
             const float4* sp = reinterpret_cast<const float4*>(a.es + c);
             const float4* tp = reinterpret_cast<const float4*>(a.et + c);
             float4 sa = sp[0], sb = sp[1], ta = tp[0], tb = tp[1];
@@ -402,12 +451,12 @@ __global__ __launch_bounds__(256) void igemm_kernel(const ConvArgs a) {
 #pragma unroll
             for (int q = 0; q < 8; ++q) {
               const float z = fmaf(xv8[q], sv[q], tv[q]);
-              const float gp = v[q] * act_grad(z, a.epi_act, a.epi_alpha);
+              const float gp = v[q] * actg<ACT>(z, inv_alpha);
               o[q] = gp * sv[q];
               s1[p * 8 + q] = fmaf(gp, xv8[q], s1[p * 8 + q]);
               s0[p * 8 + q] += gp;
             }
-            Vec8<bf16>::store(a.out + orow[j] * a.Cout + c, o);
+            Vec8<bf16>::store(a.out + orow[j] * (uint32_t)a.Cout + c, o);
           }
         }
       }
@@ -443,7 +492,7 @@ __global__ __launch_bounds__(256) void igemm_kernel(const ConvArgs a) {
           }
           const int c = cb + 8 * g + 8 * h;
           if (ov[j]) {
-            bf16* dst = a.out + orow[j] * a.Cout + c;
+            bf16* dst = a.out + orow[j] * (uint32_t)a.Cout + c;
             if constexpr (EPI == kEpiAdd) {
               float e8[8];
               Vec8<bf16>::load(dst, e8);
@@ -463,9 +512,9 @@ struct Cfg {
   int BM, BN;
 };
 
-template <int BM, int BN, int BK, int PRO, int EPI, bool PURE>
+template <int BM, int BN, int BK, int PRO, int EPI, bool PURE, int ACT>
 static void launch_one(const ConvArgs& a, size_t lds, hipStream_t st) {
-  auto kern = igemm_kernel<BM, BN, BK, PRO, EPI, PURE>;
+  auto kern = igemm_kernel<BM, BN, BK, PRO, EPI, PURE, ACT>;
   static size_t attr_set = 64 * 1024;  // default dynamic-LDS limit; raise only when needed
   if (lds > attr_set) {
     FDT_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -476,19 +525,19 @@ static void launch_one(const ConvArgs& a, size_t lds, hipStream_t st) {
   FDT_LAUNCH_CHECK();
 }
 
-template <int BM, int BN, int BK, int PRO, int EPI>
+template <int BM, int BN, int BK, int PRO, int EPI, int ACT>
 static void launch_pure(const ConvArgs& a, bool pure, size_t lds, hipStream_t st) {
-  if (pure) launch_one<BM, BN, BK, PRO, EPI, true>(a, lds, st);
-  else launch_one<BM, BN, BK, PRO, EPI, false>(a, lds, st);
+  if (pure) launch_one<BM, BN, BK, PRO, EPI, true, ACT>(a, lds, st);
+  else launch_one<BM, BN, BK, PRO, EPI, false, ACT>(a, lds, st);
 }
 
-template <int PRO, int EPI>
+template <int PRO, int EPI, int ACT>
 static void launch_tile(const ConvArgs& a, int BM, int BN, int BK, bool pure, hipStream_t st) {
   const int nkt = (a.K + BK - 1) / BK;
   const size_t nbuf = nkt > 1 ? 2 : 1;
-  size_t lds = nbuf * (BM + BN) * BK * 2 + (PRO != kProNone ? 2 * a.Cx * 4 : 0) + 4 * BN * 4 + 64;
+  size_t lds = nbuf * (BM + BN) * BK * 2 + (PRO != kProNone ? 2 * a.Cx * 4 : 0) + 4 * BN * 4 + 128;
 #define FDT_T(BM_, BN_, BK_) \
-  if (BM == BM_ && BN == BN_ && BK == BK_) { launch_pure<BM_, BN_, BK_, PRO, EPI>(a, pure, lds, st); return; }
+  if (BM == BM_ && BN == BN_ && BK == BK_) { launch_pure<BM_, BN_, BK_, PRO, EPI, ACT>(a, pure, lds, st); return; }
   FDT_T(128, 128, 64) FDT_T(128, 64, 64) FDT_T(64, 128, 64) FDT_T(64, 64, 64) FDT_T(256, 64, 64)
   FDT_T(128, 128, 32) FDT_T(128, 64, 32) FDT_T(64, 128, 32) FDT_T(64, 64, 32) FDT_T(256, 128, 32)
 #undef FDT_T
@@ -534,18 +583,27 @@ void conv_igemm(uint64_t x, uint64_t x2, uint64_t ps, uint64_t pt, uint64_t w, u
     a.dw[i] = (int8_t)dw[i];
     a.wt[i] = (int8_t)wt[i];
   }
+  a.Nb_HiWi_Cx_bytes = Nb * (long)Hi * Wi * Cx * 2;
+  a.w_bytes = (long)Cout * ldw * 2;
+  FDT_CHECK(a.Nb_HiWi_Cx_bytes < 0x7FFFFFF0L && a.w_bytes < 0x7FFFFFF0L && Nb * (long)Hout * Wout * Cout < 0x7FFFFFFFL,
+            "conv operand exceeds the 2 GiB buffer-descriptor range");
   a.nbm = (int)((a.M + BM - 1) / BM);
   a.nbn = Cout / BN;
   const bool pure = a.ntaps == 1 && dh[0] == 0 && dw[0] == 0 && wt[0] == 0 && S == 1 && Hi == Ho && Wi == Wo;
   hipStream_t st = as_stream(stream);
   if (a.M == 0) return;
-#define FDT_CONV_CASE(P_, E_) \
-  if (pro == P_ && epi == E_) { launch_tile<P_, E_>(a, BM, BN, BK, pure, st); return; }
-  FDT_CONV_CASE(kProNone, kEpiStats)
-  FDT_CONV_CASE(kProAffineAct, kEpiStats)
-  FDT_CONV_CASE(kProFold, kEpiActBwd)
-  FDT_CONV_CASE(kProFold, kEpiStore)
-  FDT_CONV_CASE(kProFold, kEpiAdd)
+  const int act = pro == kProAffineAct ? pro_act : (epi == kEpiActBwd ? epi_act : 0);
+#define FDT_CONV_CASE(P_, E_, A_) \
+  if (pro == P_ && epi == E_ && act == A_) { launch_tile<P_, E_, A_>(a, BM, BN, BK, pure, st); return; }
+  FDT_CONV_CASE(kProNone, kEpiStats, kActNone)
+  FDT_CONV_CASE(kProAffineAct, kEpiStats, kActRelu)
+  FDT_CONV_CASE(kProAffineAct, kEpiStats, kActCelu)
+  FDT_CONV_CASE(kProAffineAct, kEpiStats, kActNone)
+  FDT_CONV_CASE(kProFold, kEpiActBwd, kActRelu)
+  FDT_CONV_CASE(kProFold, kEpiActBwd, kActCelu)
+  FDT_CONV_CASE(kProFold, kEpiActBwd, kActNone)
+  FDT_CONV_CASE(kProFold, kEpiStore, kActNone)
+  FDT_CONV_CASE(kProFold, kEpiAdd, kActNone)
 #undef FDT_CONV_CASE
   FDT_CHECK(false, "unsupported (prologue, epilogue) combination");
 }
