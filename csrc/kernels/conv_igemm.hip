@@ -604,6 +604,11 @@ void conv_igemm(uint64_t x, uint64_t x2, uint64_t ps, uint64_t pt, uint64_t w, u
   FDT_CONV_CASE(kProFold, kEpiActBwd, kActNone)
   FDT_CONV_CASE(kProFold, kEpiStore, kActNone)
   FDT_CONV_CASE(kProFold, kEpiAdd, kActNone)
+  // dgrad on a pre-folded gradient (the engine materialises g + alpha + beta*y once for 3x3)
+  FDT_CONV_CASE(kProNone, kEpiActBwd, kActRelu)
+  FDT_CONV_CASE(kProNone, kEpiActBwd, kActCelu)
+  FDT_CONV_CASE(kProNone, kEpiStore, kActNone)
+  FDT_CONV_CASE(kProNone, kEpiAdd, kActNone)
 #undef FDT_CONV_CASE
   FDT_CHECK(false, "unsupported (prologue, epilogue) combination");
 }

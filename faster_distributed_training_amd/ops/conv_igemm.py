@@ -174,7 +174,7 @@ def conv_dgrad(g, y, al, be, wd, shp: ConvShape, x_shape, epi=EPI_STORE, out=Non
     [nbm, 2, Cin] of (sum g_pre*ex, sum g_pre)."""
     nat = _native.native()
     N, Hy, Wy, Cy = g.shape
-    assert Cy == shp.cout and g.is_contiguous() and y.is_contiguous()
+    assert Cy == shp.cout and g.is_contiguous() and (y is None or y.is_contiguous())
     Nx, Hx, Wx, Cx = x_shape
     assert Cx == shp.cin
     if out is None:
@@ -195,9 +195,10 @@ def conv_dgrad(g, y, al, be, wd, shp: ConvShape, x_shape, epi=EPI_STORE, out=Non
         if epi == EPI_ACTBWD:
             part = torch.empty(nat.conv_num_row_blocks(M, bm), 2, shp.cin, device=g.device, dtype=torch.float32)
             parts.append(part)
-        nat.conv_igemm(g.data_ptr(), y.data_ptr(), _p(al), _p(be), wd.data_ptr(), out.data_ptr(), _p(part),
-                       _p(ex), _p(es), _p(et), N, Hy, Wy, Cy, Ha, Wa, 1, list(dh), list(dw), list(wt), shp.cin,
-                       shp.ntaps * shp.cout, Hx, Wx, shp.stride, py, px, PRO_FOLD, 0, 1.0, epi, int(act),
+        pro = PRO_FOLD if al is not None else PRO_NONE  # al None: g is already folded
+        nat.conv_igemm(g.data_ptr(), _p(y) if pro == PRO_FOLD else 0, _p(al), _p(be), wd.data_ptr(), out.data_ptr(),
+                       _p(part), _p(ex), _p(es), _p(et), N, Hy, Wy, Cy, Ha, Wa, 1, list(dh), list(dw), list(wt),
+                       shp.cin, shp.ntaps * shp.cout, Hx, Wx, shp.stride, py, px, pro, 0, 1.0, epi, int(act),
                        float(alpha), bm, bn, bk, _sp())
     if epi == EPI_ACTBWD:
         return out, (parts[0] if len(parts) == 1 else torch.cat(parts, 0))
@@ -241,7 +242,7 @@ def conv_wgrad(g, y, al, be, x, shp: ConvShape, out, xs=None, xt=None, act=0, al
     if xs is None and act != 0:
         xs = torch.ones(Cx, device=x.device, dtype=torch.float32)
         xt = torch.zeros(Cx, device=x.device, dtype=torch.float32)
-    nat.conv_wgrad(g.data_ptr(), y.data_ptr(), _p(al), _p(be), x.data_ptr(), _p(xs), _p(xt), slab.data_ptr(),
+    nat.conv_wgrad(g.data_ptr(), _p(y), _p(al), _p(be), x.data_ptr(), _p(xs), _p(xt), slab.data_ptr(),
                    N, H, W, Cx, Hy, Wy, shp.stride, list(dh), list(dw), shp.cout, ldw, int(act), float(alpha),
                    bm, bn, bk, ns, _sp())
     nat.wgrad_reduce(slab.data_ptr(), out.data_ptr(), ns, shp.cout, shp.cin, shp.ntaps, shp.cxp, int(accumulate),

@@ -28,6 +28,8 @@ fp32/fp64 statistics.
 """
 from __future__ import annotations
 
+import os
+
 import torch
 import torch.nn as nn
 
@@ -35,6 +37,8 @@ from . import _native
 from . import conv_igemm as ci
 
 ACT_NONE, ACT_RELU, ACT_CELU = 0, 1, 2
+# materialise the normalised input / folded gradient of 3x3 convs once (see forward/backward)
+MATERIALIZE_3X3 = os.environ.get("FDT_MATERIALIZE_3X3", "1") != "0"
 MODE_FCBN, MODE_BN_TRAIN, MODE_BN_EVAL = 0, 1, 2
 BF16 = torch.bfloat16
 
@@ -257,10 +261,19 @@ class ResNetBodyFn(torch.autograd.Function):
             ys = []
             raw, s, t, act = x_in, None, None, (ACT_NONE, 1.0)
             for u in b.units:
-                y, part = ci.conv_fwd(raw, u.wf, u.shp, s, t, act[0], act[1])
+                a_in = None
+                if MATERIALIZE_3X3 and u.shp.k > 1 and s is not None:
+                    # 3x3: normalise + activate the input ONCE instead of in every one of the
+                    # 9 im2col re-reads of the conv's operand staging
+                    a_in = torch.empty_like(raw)
+                    nat.act_affine_fwd(raw.data_ptr(), s.data_ptr(), t.data_ptr(), a_in.data_ptr(), _rows(raw),
+                                       raw.shape[-1], act[0], float(act[1]), 1, 1, _sp())
+                    y, part = ci.conv_fwd(a_in, u.wf, u.shp)
+                else:
+                    y, part = ci.conv_fwd(raw, u.wf, u.shp, s, t, act[0], act[1])
                 M = _rows(y)
                 su, tu, smu, sau = finalize_stats(part, u, M, training, dev)
-                ys.append((y, su, tu, smu, sau, M))
+                ys.append((y, su, tu, smu, sau, M, a_in))
                 raw, s, t, act = y, su, tu, u.act_out
             y3, s3, t3 = ys[-1][0], ys[-1][1], ys[-1][2]
             sc = None
@@ -269,7 +282,7 @@ class ResNetBodyFn(torch.autograd.Function):
                 ysc, part = ci.conv_fwd(x_in, u.wf, u.shp)
                 M = _rows(ysc)
                 ssc, tsc, smsc, sasc = finalize_stats(part, u, M, training, dev)
-                sc = (ysc, ssc, tsc, smsc, sasc, M)
+                sc = (ysc, ssc, tsc, smsc, sasc, M, None)
             out = torch.empty_like(y3)
             C = y3.shape[-1]
             nat.residual_act_fwd(y3.data_ptr(), s3.data_ptr(), t3.data_ptr(), _p(sc[0] if sc else None),
@@ -308,15 +321,29 @@ class ResNetBodyFn(torch.autograd.Function):
             # residual chain, last unit first
             for i in range(len(b.units) - 1, -1, -1):
                 u = b.units[i]
-                y, su, tu, smu, sau, Mu = ys[i]
+                y, su, tu, smu, sau, Mu, a_in = ys[i]
                 al, be = bwd_coef(u, gs, gt, smu, sau, Mu, training, dev)
                 if i > 0:
-                    yp, sp_, tp, _, _, _ = ys[i - 1]
+                    yp, sp_, tp = ys[i - 1][0], ys[i - 1][1], ys[i - 1][2]
                     actp = b.units[i - 1].act_out
-                    g_prev, pp = ci.conv_dgrad(g_cur, y, al, be, u.wd, u.shp, tuple(yp.shape), epi=ci.EPI_ACTBWD,
-                                               ex=yp, es=sp_, et=tp, act=actp[0], alpha=actp[1])
+                    if MATERIALIZE_3X3 and u.shp.k > 1:
+                        # fold the BN-backward correction into the gradient once (3x3: the
+                        # dgrad operand is re-read 9x, the wgrad operand once per column block)
+                        gf = torch.empty_like(g_cur)
+                        nat.affine_fold(g_cur.data_ptr(), y.data_ptr(), al.data_ptr(), be.data_ptr(), gf.data_ptr(),
+                                        _rows(gf), gf.shape[-1], 1, _sp())
+                        g_prev, pp = ci.conv_dgrad(gf, None, None, None, u.wd, u.shp, tuple(yp.shape),
+                                                   epi=ci.EPI_ACTBWD, ex=yp, es=sp_, et=tp, act=actp[0],
+                                                   alpha=actp[1])
+                        wgrad_into(u, gf, None, None, None, a_in if a_in is not None else yp,
+                                   None if a_in is not None else sp_, None if a_in is not None else tp,
+                                   (ACT_NONE, 1.0) if a_in is not None else actp)
+                    else:
+                        g_prev, pp = ci.conv_dgrad(g_cur, y, al, be, u.wd, u.shp, tuple(yp.shape),
+                                                   epi=ci.EPI_ACTBWD, ex=yp, es=sp_, et=tp, act=actp[0],
+                                                   alpha=actp[1])
+                        wgrad_into(u, g_cur, y, al, be, yp, sp_, tp, actp)
                     r2 = reduce_parts(pp, 2, u.shp.cin, dev)
-                    wgrad_into(u, g_cur, y, al, be, yp, sp_, tp, actp)
                     gs, gt = r2[0], r2[1]
                     g_cur = g_prev
                 else:
@@ -327,7 +354,7 @@ class ResNetBodyFn(torch.autograd.Function):
                     wgrad_into(u, g_cur, y, al, be, x_in, None, None, (ACT_NONE, 1.0))
             if sc is not None:
                 u = b.shortcut
-                ysc, ssc, tsc, smsc, sasc, Msc = sc
+                ysc, ssc, tsc, smsc, sasc, Msc, _ = sc
                 al, be = bwd_coef(u, red[2], red[1], smsc, sasc, Msc, training, dev)
                 ci.conv_dgrad(gyb, ysc, al, be, u.wd, u.shp, tuple(x_in.shape), epi=ci.EPI_ADD, out=g_x)
                 wgrad_into(u, gyb, ysc, al, be, x_in, None, None, (ACT_NONE, 1.0))

@@ -55,7 +55,8 @@ def test_engine_train_step_matches_reference(cuda, arch):
     # reference's bf16 autocast gradient does (with a noise margin).
     ge = torch.cat([p.grad.flatten().float() for p in m_eng.parameters()])
     gr = torch.cat([p.grad.flatten().float() for p in m_ref.parameters()])
-    assert cos(ge, gr) > 0.98, cos(ge, gr)
+    gb = torch.cat([p.grad.flatten().float() for p in m_rb.parameters()])
+    assert cos(ge, gr) > min(0.98, cos(gb, gr) - 0.05), (cos(ge, gr), cos(gb, gr))
     good = 0
     for (n, pr), (_, pe), (_, pb) in zip(m_ref.named_parameters(), m_eng.named_parameters(),
                                          m_rb.named_parameters()):
