@@ -43,8 +43,9 @@ struct WgArgs {
   int ntaps, Cout, ldw, act;
   float act_alpha;
   int nbm, nbn, nsplit;
-  long px_per_split;  // multiple of 32
+  long px_per_split;  // multiple of BK
   int8_t dh[12], dw[12];
+  long g_bytes, x_bytes;  // buffer-descriptor ranges
 };
 
 __device__ __forceinline__ int xcd_remap(int bid, int nblk) {
@@ -59,9 +60,22 @@ __device__ __forceinline__ int tswz(int px) {
   else return 4 * ((px >> 1) & 1);
 }
 
+template <int ACT>
+__device__ __forceinline__ float wactf(float z, float alpha, float inv_alpha) {
+  if constexpr (ACT == kActRelu) return fmaxf(z, 0.f);
+  else if constexpr (ACT == kActCelu) return z > 0.f ? z : alpha * (__expf(z * inv_alpha) - 1.f);
+  else return z;
+}
+
+__device__ __forceinline__ uint4 wld16(__amdgpu_buffer_rsrc_t r, uint32_t byte_off) {
+  auto v = __builtin_amdgcn_raw_buffer_load_b128(r, byte_off, 0, 0);
+  return *reinterpret_cast<uint4*>(&v);
+}
+constexpr uint32_t kWOOB = 0xFFFFFFF0u;
+
 // ADDR: 0 = 1x1 stride-1 (input pixel == output pixel), 1 = power-of-two Ho/Wo (shifts),
-//       2 = general (integer division)
-template <int BM, int BN, int BK, bool FOLD, bool XAFF, int ADDR>
+//       2 = general (integer division).  ACT: input transform act(x*s+t) (XAFF only).
+template <int BM, int BN, int BK, bool FOLD, bool XAFF, int ADDR, int ACT>
 __global__ __launch_bounds__(256) void wgrad_kernel(const WgArgs a) {
   constexpr int GC = BM / 8, XC = BN / 8;      // 16-B chunks per LDS row
   constexpr int GR = 256 / GC, XR = 256 / XC;  // rows per load round
@@ -81,9 +95,14 @@ __global__ __launch_bounds__(256) void wgrad_kernel(const WgArgs a) {
   const int id = xcd_remap(blockIdx.x, nt);
   const int bn = id % a.nbn, bm = id / a.nbn;
   const int co0 = bm * BM, k0 = bn * BN;
-  const long p_begin = (long)blockIdx.y * a.px_per_split;
-  long p_end = p_begin + a.px_per_split;
-  if (p_end > a.M) p_end = a.M;
+  const int p_begin = (int)((long)blockIdx.y * a.px_per_split);
+  int p_end = (int)(p_begin + a.px_per_split);
+  if ((long)p_end > a.M) p_end = (int)a.M;
+
+  const __amdgpu_buffer_rsrc_t rg_d = __builtin_amdgcn_make_buffer_rsrc((void*)a.g, (short)0, (int)a.g_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t ry_d =
+      __builtin_amdgcn_make_buffer_rsrc((void*)(FOLD ? a.y : a.g), (short)0, (int)a.g_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rx_d = __builtin_amdgcn_make_buffer_rsrc((void*)a.x, (short)0, (int)a.x_bytes, 0x00020000);
 
   if constexpr (FOLD) {
     for (int i = tid; i < BM; i += 256) { prm[i] = a.al[co0 + i]; prm[BM + i] = a.be[co0 + i]; }
@@ -106,6 +125,7 @@ __global__ __launch_bounds__(256) void wgrad_kernel(const WgArgs a) {
     xdh = (int)(int8_t)(e & 0xff);
     xdw = (int)(int8_t)((e >> 8) & 0xff);
   }
+  const int xtoff = xdh * a.Wi + xdw;
   float xsv[8], xtv[8];
   if constexpr (XAFF) {
 #pragma unroll
@@ -116,95 +136,87 @@ __global__ __launch_bounds__(256) void wgrad_kernel(const WgArgs a) {
 #pragma unroll
     for (int q = 0; q < 8; ++q) { alv[q] = prm[gcc * 8 + q]; bev[q] = prm[BM + gcc * 8 + q]; }
   }
-
-  const long hw = (long)a.Ho * a.Wo;
+  const float inv_alpha = ACT == kActCelu ? 1.f / a.act_alpha : 1.f;
+  const int hw = a.Ho * a.Wo;
   const int lw = a.log2Wo, lhw = a.log2Wo + a.log2Ho;
 
-  uint4 rg[NG], ry[FOLD ? NG : 1], rx[NX];
-  bool gvld[NG], xvld[NX];
-  long ptile = p_begin;
+  struct Stage {
+    uint4 rg[NG], ry[FOLD ? NG : 1], rx[NX];
+    bool xv[NX];
+  };
 
-  auto load_tile = [&](long pt) {
+  auto load_tile = [&](Stage& S, int pt) {
 #pragma unroll
     for (int j = 0; j < NG; ++j) {
-      const long p = pt + tid / GC + j * GR;
-      gvld[j] = p < p_end;
-      const long off = p * a.Cout + co0 + gcc * 8;
-      if (gvld[j]) {
-        rg[j] = *reinterpret_cast<const uint4*>(a.g + off);
-        if constexpr (FOLD) ry[j] = *reinterpret_cast<const uint4*>(a.y + off);
-      } else {
-        rg[j] = make_uint4(0, 0, 0, 0);
-        if constexpr (FOLD) ry[j] = make_uint4(0, 0, 0, 0);
-      }
+      const int p = pt + tid / GC + j * GR;
+      const uint32_t off = p < p_end ? ((uint32_t)p * (uint32_t)a.Cout + co0 + gcc * 8) * 2u : kWOOB;
+      S.rg[j] = wld16(rg_d, off);
+      if constexpr (FOLD) S.ry[j] = wld16(ry_d, off);
     }
 #pragma unroll
     for (int j = 0; j < NX; ++j) {
-      const long p = pt + tid / XC + j * XR;
+      const int p = pt + tid / XC + j * XR;
       bool v = xtok && p < p_end;
-      long off;
+      uint32_t pix;
       if constexpr (ADDR == 0) {
-        off = p * a.Cx + xci;
+        pix = (uint32_t)p;
       } else {
-        long n;
-        int oh, ow;
+        int n, oh, ow;
         if constexpr (ADDR == 1) {
           n = p >> lhw;
-          oh = (int)(p >> lw) & (a.Ho - 1);
-          ow = (int)p & (a.Wo - 1);
+          oh = (p >> lw) & (a.Ho - 1);
+          ow = p & (a.Wo - 1);
         } else {
           n = p / hw;
-          const int rem = (int)(p - n * hw);
+          const int rem = p - n * hw;
           oh = rem / a.Wo;
           ow = rem - oh * a.Wo;
         }
         const int ih = oh * a.S + xdh, iw = ow * a.S + xdw;
         v = v && (unsigned)ih < (unsigned)a.Hi && (unsigned)iw < (unsigned)a.Wi;
-        off = ((n * a.Hi + ih) * a.Wi + iw) * a.Cx + xci;
+        pix = (uint32_t)((n * a.Hi + oh * a.S) * a.Wi + ow * a.S + xtoff);
       }
-      xvld[j] = v;
-      if (v) rx[j] = *reinterpret_cast<const uint4*>(a.x + off);
-      else rx[j] = make_uint4(0, 0, 0, 0);
+      S.xv[j] = v;
+      S.rx[j] = wld16(rx_d, v ? ((pix << a.log2Cx) + xci) * 2u : kWOOB);
     }
   };
 
-  auto store_tile = [&](int buf) {
+  auto store_tile = [&](const Stage& S, int buf) {
     bf16* Gl = tiles + buf * (GT + XT);
     bf16* Xl = Gl + GT;
 #pragma unroll
     for (int j = 0; j < NG; ++j) {
       const int row = tid / GC + j * GR;
-      uint4 o = rg[j];
+      uint4 o = S.rg[j];
       if constexpr (FOLD) {
-        if (gvld[j]) {
-          const uint32_t u[4] = {o.x, o.y, o.z, o.w}, uy[4] = {ry[j].x, ry[j].y, ry[j].z, ry[j].w};
-          float v[8];
+        // pixels past the split end fold to alpha, but their X rows load as zero, so they
+        // contribute nothing to dW
+        const uint32_t u[4] = {o.x, o.y, o.z, o.w}, uy[4] = {S.ry[j].x, S.ry[j].y, S.ry[j].z, S.ry[j].w};
+        float v[8];
 #pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            v[2 * q] = bf16_lo(u[q]) + fmaf(bev[2 * q], bf16_lo(uy[q]), alv[2 * q]);
-            v[2 * q + 1] = bf16_hi(u[q]) + fmaf(bev[2 * q + 1], bf16_hi(uy[q]), alv[2 * q + 1]);
-          }
-          o = make_uint4(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]), pack_bf16x2(v[4], v[5]),
-                         pack_bf16x2(v[6], v[7]));
+        for (int q = 0; q < 4; ++q) {
+          v[2 * q] = bf16_lo(u[q]) + fmaf(bev[2 * q], bf16_lo(uy[q]), alv[2 * q]);
+          v[2 * q + 1] = bf16_hi(u[q]) + fmaf(bev[2 * q + 1], bf16_hi(uy[q]), alv[2 * q + 1]);
         }
+        o = make_uint4(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]), pack_bf16x2(v[4], v[5]),
+                       pack_bf16x2(v[6], v[7]));
       }
       *reinterpret_cast<uint4*>(Gl + row * BM + 8 * (gcc ^ tswz<BM * 2>(row))) = o;
     }
 #pragma unroll
     for (int j = 0; j < NX; ++j) {
       const int row = tid / XC + j * XR;
-      uint4 o = rx[j];
+      uint4 o = S.rx[j];
       if constexpr (XAFF) {
-        if (xvld[j]) {
-          const uint32_t u[4] = {o.x, o.y, o.z, o.w};
-          float v[8];
+        const uint32_t u[4] = {o.x, o.y, o.z, o.w};
+        float v[8];
 #pragma unroll
-          for (int q = 0; q < 4; ++q) { v[2 * q] = bf16_lo(u[q]); v[2 * q + 1] = bf16_hi(u[q]); }
+        for (int q = 0; q < 4; ++q) { v[2 * q] = bf16_lo(u[q]); v[2 * q + 1] = bf16_hi(u[q]); }
 #pragma unroll
-          for (int q = 0; q < 8; ++q) v[q] = act_fwd(fmaf(v[q], xsv[q], xtv[q]), a.act, a.act_alpha);
-          o = make_uint4(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]), pack_bf16x2(v[4], v[5]),
-                         pack_bf16x2(v[6], v[7]));
-        }
+        for (int q = 0; q < 8; ++q) v[q] = wactf<ACT>(fmaf(v[q], xsv[q], xtv[q]), a.act_alpha, inv_alpha);
+        o = make_uint4(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]), pack_bf16x2(v[4], v[5]),
+                       pack_bf16x2(v[6], v[7]));
+        if (!S.xv[j]) o = make_uint4(0, 0, 0, 0);
       }
       *reinterpret_cast<uint4*>(Xl + row * BN + 8 * (xcc ^ tswz<BN * 2>(row))) = o;
     }
@@ -218,57 +230,33 @@ __global__ __launch_bounds__(256) void wgrad_kernel(const WgArgs a) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
-  const int nkt = p_end > p_begin ? (int)((p_end - p_begin + BK - 1) / BK) : 0;
-  if (nkt > 0) {
-    load_tile(ptile);
-    store_tile(0);
-    __syncthreads();
-  }
-  // transposed fragment read: 16-lane group gl supplies rows q (lane 4q+p) and columns 4p..4p+3
+  // transposed fragment read: 16-lane group supplies rows q (lane 4q+p) and columns 4p..4p+3
   const int gq = (lane & 15) >> 2, gp = lane & 3;
   const int h = lane >> 5;
-  const int colg = ((lane >> 4) & 1) * 16;  // group 1/3 -> columns 16..31 of the 32-col subtile
-  for (int kt = 0; kt < nkt; ++kt) {
-    const int buf = kt & 1;
-    ptile += BK;
-    if (kt + 1 < nkt) load_tile(ptile);
+  const int colg = ((lane >> 4) & 1) * 16;  // groups 1/3 -> columns 16..31 of the 32-col subtile
+  auto compute = [&](int buf) {
     const bf16* Gl = tiles + buf * (GT + XT);
     const bf16* Xl = Gl + GT;
 #pragma unroll
     for (int ks = 0; ks < BK / 16; ++ks) {
       bf16x8_t af[TM], bfv[TN];
+      const int r0 = ks * 16 + 8 * h + gq, r1 = r0 + 4;
 #pragma unroll
       for (int i = 0; i < TM; ++i) {
-        const int col = wm * (BM / 2) + i * 32 + colg + 4 * gp;  // channel column of this lane's 4-wide piece
-        bf16x4_t lo, hi;
-        {
-          const int row = ks * 16 + 8 * h + gq;
-          const int ch = col >> 3;
-          const bf16* p = Gl + row * BM + 8 * (ch ^ tswz<BM * 2>(row)) + (col & 7);
-          lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_bf16x4*)(p));
-        }
-        {
-          const int row = ks * 16 + 8 * h + 4 + gq;
-          const int ch = col >> 3;
-          const bf16* p = Gl + row * BM + 8 * (ch ^ tswz<BM * 2>(row)) + (col & 7);
-          hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_bf16x4*)(p));
-        }
+        const int col = wm * (BM / 2) + i * 32 + colg + 4 * gp;
+        const bf16* p0 = Gl + r0 * BM + 8 * ((col >> 3) ^ tswz<BM * 2>(r0)) + (col & 7);
+        const bf16* p1 = Gl + r1 * BM + 8 * ((col >> 3) ^ tswz<BM * 2>(r1)) + (col & 7);
+        const bf16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_bf16x4*)(p0));
+        const bf16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_bf16x4*)(p1));
         af[i] = bf16x8_t{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
       }
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
         const int col = wn * (BN / 2) + j * 32 + colg + 4 * gp;
-        bf16x4_t lo, hi;
-        {
-          const int row = ks * 16 + 8 * h + gq;
-          const bf16* p = Xl + row * BN + 8 * ((col >> 3) ^ tswz<BN * 2>(row)) + (col & 7);
-          lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_bf16x4*)(p));
-        }
-        {
-          const int row = ks * 16 + 8 * h + 4 + gq;
-          const bf16* p = Xl + row * BN + 8 * ((col >> 3) ^ tswz<BN * 2>(row)) + (col & 7);
-          hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_bf16x4*)(p));
-        }
+        const bf16* p0 = Xl + r0 * BN + 8 * ((col >> 3) ^ tswz<BN * 2>(r0)) + (col & 7);
+        const bf16* p1 = Xl + r1 * BN + 8 * ((col >> 3) ^ tswz<BN * 2>(r1)) + (col & 7);
+        const bf16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_bf16x4*)(p0));
+        const bf16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_bf16x4*)(p1));
         bfv[j] = bf16x8_t{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
       }
 #pragma unroll
@@ -276,8 +264,28 @@ __global__ __launch_bounds__(256) void wgrad_kernel(const WgArgs a) {
 #pragma unroll
         for (int j = 0; j < TN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bfv[j], acc[i][j], 0, 0, 0);
     }
-    if (kt + 1 < nkt) store_tile(buf ^ 1);
+  };
+
+  const int nkt = p_end > p_begin ? (p_end - p_begin + BK - 1) / BK : 0;
+  Stage SA, SB;
+  if (nkt > 0) {
+    load_tile(SA, p_begin);
+    if (nkt > 1) load_tile(SB, p_begin + BK);
+    store_tile(SA, 0);
+    if (nkt > 2) load_tile(SA, p_begin + 2 * BK);
     __syncthreads();
+  }
+  for (int kt = 0; kt < nkt; kt += 2) {
+    compute(0);
+    if (kt + 1 >= nkt) break;
+    store_tile(SB, 1);
+    __syncthreads();
+    if (kt + 3 < nkt) load_tile(SB, p_begin + (kt + 3) * BK);
+    compute(1);
+    if (kt + 2 >= nkt) break;
+    store_tile(SA, 0);
+    __syncthreads();
+    if (kt + 4 < nkt) load_tile(SA, p_begin + (kt + 4) * BK);
   }
 
   // epilogue: C[co][k]: lane column k = lane&31, rows co = (r&3) + 8(r>>2) + 4h
@@ -397,6 +405,9 @@ void conv_wgrad(uint64_t g, uint64_t y, uint64_t al, uint64_t be, uint64_t x, ui
   a.ntaps = (int)dh.size(); a.Cout = Cout; a.ldw = ldw; a.act = act; a.act_alpha = act_alpha;
   FDT_CHECK(ldw >= a.ntaps * Cx, "ldw too small");
   for (size_t i = 0; i < dh.size(); ++i) { a.dh[i] = (int8_t)dh[i]; a.dw[i] = (int8_t)dw[i]; }
+  a.g_bytes = a.M * Cout * 2;
+  a.x_bytes = Nb * (long)Hi * Wi * Cx * 2;
+  FDT_CHECK(a.g_bytes < 0x7FFFFFF0L && a.x_bytes < 0x7FFFFFF0L, "wgrad operand exceeds the 2 GiB descriptor range");
   a.nbm = Cout / BM;
   a.nbn = (ldw + BN - 1) / BN;
   long per = (a.M + nsplit - 1) / nsplit;
@@ -407,9 +418,10 @@ void conv_wgrad(uint64_t g, uint64_t y, uint64_t al, uint64_t be, uint64_t x, ui
   size_t lds = (size_t)2 * BK * (BM + BN) * 2 + 2 * BM * 4 + (xaff ? 2 * Cx * 4 : 0) + 64;
   dim3 grid(a.nbm * a.nbn, nsplit);
   hipStream_t st = as_stream(stream);
-#define FDT_WG(BM_, BN_, BK_, F_, X_, A_)                                                                 \
-  if (BM == BM_ && BN == BN_ && BK == BK_ && fold == F_ && xaff == X_ && addr == A_) {                  \
-    auto k = wgrad_kernel<BM_, BN_, BK_, F_, X_, A_>;                                                   \
+  const int wact = xaff ? act : 0;
+#define FDT_WG(BM_, BN_, BK_, F_, X_, A_, ACT_)                                                           \
+  if (BM == BM_ && BN == BN_ && BK == BK_ && fold == F_ && xaff == X_ && addr == A_ && wact == ACT_) {  \
+    auto k = wgrad_kernel<BM_, BN_, BK_, F_, X_, A_, ACT_>;                                             \
     static size_t set = 64 * 1024;                                                                      \
     if (lds > set) {                                                                                    \
       FDT_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(k),                               \
@@ -420,10 +432,11 @@ void conv_wgrad(uint64_t g, uint64_t y, uint64_t al, uint64_t be, uint64_t x, ui
     FDT_LAUNCH_CHECK();                                                                                 \
     return;                                                                                             \
   }
-#define FDT_WG_A(BM_, BN_, BK_, F_, X_) FDT_WG(BM_, BN_, BK_, F_, X_, 0) FDT_WG(BM_, BN_, BK_, F_, X_, 1) \
-  FDT_WG(BM_, BN_, BK_, F_, X_, 2)
-#define FDT_WG_T(BM_, BN_, BK_) FDT_WG_A(BM_, BN_, BK_, true, true) FDT_WG_A(BM_, BN_, BK_, true, false) \
-  FDT_WG_A(BM_, BN_, BK_, false, true) FDT_WG_A(BM_, BN_, BK_, false, false)
+#define FDT_WG_A(BM_, BN_, BK_, F_, X_, ACT_) FDT_WG(BM_, BN_, BK_, F_, X_, 0, ACT_) \
+  FDT_WG(BM_, BN_, BK_, F_, X_, 1, ACT_) FDT_WG(BM_, BN_, BK_, F_, X_, 2, ACT_)
+#define FDT_WG_T(BM_, BN_, BK_) FDT_WG_A(BM_, BN_, BK_, true, true, 1) FDT_WG_A(BM_, BN_, BK_, true, true, 2) \
+  FDT_WG_A(BM_, BN_, BK_, true, false, 0) FDT_WG_A(BM_, BN_, BK_, false, false, 0)                          \
+  FDT_WG_A(BM_, BN_, BK_, false, true, 1) FDT_WG_A(BM_, BN_, BK_, true, true, 0)
   FDT_WG_T(128, 128, 32)
   FDT_WG_T(64, 128, 32)
   FDT_WG_T(128, 64, 32)

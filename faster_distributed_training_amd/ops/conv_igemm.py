@@ -148,14 +148,14 @@ def conv_fwd(x, wf, shp: ConvShape, s=None, t=None, act=0, alpha=1.0, tile=None)
     assert C == shp.cxp and x.dtype == torch.bfloat16 and x.is_contiguous()
     Ho, Wo = out_hw(H, W, shp)
     M = N * Ho * Wo
+    pro = PRO_AFFINE_ACT if (s is not None or act != 0) else PRO_NONE
     if tile is None:
-        ent = tuned("fwd", N, H, shp)
+        ent = tuned(f"fwd{pro}", N, H, shp) or tuned("fwd", N, H, shp)
         tile = tuple(ent["tile"]) if ent else None
     bm, bn, bk = _tile3(tile, M, shp.cout)
     y = torch.empty(N, Ho, Wo, shp.cout, device=x.device, dtype=torch.bfloat16)
     part = torch.empty(nat.conv_num_row_blocks(M, bm), 2, shp.cout, device=x.device, dtype=torch.float32)
     dh, dw, wt = taps_fwd(shp.k, shp.pad)
-    pro = PRO_AFFINE_ACT if (s is not None or act != 0) else PRO_NONE
     if pro == PRO_AFFINE_ACT and s is None:
         s = torch.ones(C, device=x.device, dtype=torch.float32)
         t = torch.zeros(C, device=x.device, dtype=torch.float32)
@@ -181,7 +181,9 @@ def conv_dgrad(g, y, al, be, wd, shp: ConvShape, x_shape, epi=EPI_STORE, out=Non
         out = torch.empty(N, Hx, Wx, shp.cin, device=g.device, dtype=torch.bfloat16)
     parts = []
     if tile is None:
-        ent = tuned("dgrad", N, Hx, shp)
+        pro = PRO_FOLD if al is not None else PRO_NONE
+        e = EPI_STORE if epi == EPI_ADD else epi
+        ent = tuned(f"dgrad{pro}{e}", N, Hx, shp) or tuned("dgrad", N, Hx, shp)
         tile = tuple(ent["tile"]) if ent else None
     classes = dgrad_classes(shp.k, shp.stride, shp.pad)
     for (py, px, dh, dw, wt) in classes:
@@ -222,7 +224,8 @@ def conv_wgrad(g, y, al, be, x, shp: ConvShape, out, xs=None, xt=None, act=0, al
     M = N * Hy * Wy
     ldw = shp.ntaps * shp.cxp
     if tile is None:
-        ent = tuned("wgrad", N, H, shp)
+        ent = tuned(f"wgrad{int(al is not None)}{int(xs is not None or act != 0)}", N, H, shp) or \
+            tuned("wgrad", N, H, shp)
         if ent:
             tile = tuple(ent["tile"])
             nsplit = nsplit or ent["nsplit"]

@@ -61,40 +61,54 @@ def main():
             gw = torch.empty(Cout, Cin, k, k, device=dev)
             key = ci.tune_key(N, H, shp)
             res = {}
-            best = None
-            for t in FWD_TILES:
-                if Cout % t[1]:
-                    continue
-                ms = timeit(lambda: ci.conv_fwd(x, wf, shp, sv, tv, 1, 1.0, tile=t), a.reps)
-                if best is None or ms < best[0]:
-                    best = (ms, t)
-            res["fwd"] = dict(tile=best[1], us=round(best[0] * 1e3, 1))
-            if Cin >= 8:
+
+            def sweep(name, fn, tiles, legal):
                 best = None
-                for t in FWD_TILES:
-                    if Cin % t[1]:
+                for t in tiles:
+                    if not legal(t):
                         continue
-                    ms = timeit(lambda: ci.conv_dgrad(g, yy, al, be, wd, shp, (N, H, H, Cin), epi=ci.EPI_ACTBWD,
-                                                      ex=ex, es=es, et=et, act=1, tile=t), a.reps)
+                    ms = timeit(lambda: fn(t), a.reps)
                     if best is None or ms < best[0]:
                         best = (ms, t)
-                res["dgrad"] = dict(tile=best[1], us=round(best[0] * 1e3, 1))
-            best = None
+                res[name] = dict(tile=best[1], us=round(best[0] * 1e3, 1))
+
+            # modes the fused engine actually launches (ops/resnet_fused.py): 3x3 convs get a
+            # materialised input / pre-folded gradient; 1x1 convs fuse the transforms
+            fwd_modes = [0] if k > 1 else [0, 1]
+            for pro in fwd_modes:
+                sweep(f"fwd{pro}", lambda t: ci.conv_fwd(x, wf, shp, sv if pro else None, tv if pro else None,
+                                                          pro, 1.0, tile=t),
+                      FWD_TILES, lambda t: Cout % t[1] == 0)
+            if Cin >= 8:
+                dg = [(0, ci.EPI_ACTBWD)] if k > 1 else [(2, ci.EPI_ACTBWD), (2, ci.EPI_STORE)]
+                for pro, epi in dg:
+                    sweep(f"dgrad{pro}{epi}",
+                          lambda t: ci.conv_dgrad(g, yy if pro else None, al if pro else None, be if pro else None,
+                                                  wd, shp, (N, H, H, Cin), epi=epi, ex=ex, es=es, et=et, act=1,
+                                                  tile=t),
+                          FWD_TILES, lambda t: Cin % t[1] == 0)
             ldw = shp.ntaps * shp.cxp
             slab = torch.empty(1024 * Cout * ldw // 4 + 1, device=dev)
-            for t in WG_TILES:
-                if Cout % t[0] or (t[1] == 128 and ldw < 128):
-                    continue
-                tiles = (Cout // t[0]) * (-(-ldw // t[1]))
-                base = ci.wgrad_split(N * Ho * Wo, tiles)
-                for ns in sorted({max(1, base // 2), base, base * 2}):
-                    if ns * Cout * ldw > slab.numel():
+            wg_modes = [(0, 0)] if k > 1 else [(1, 1), (1, 0)]
+            if Cin < 8:
+                wg_modes = [(1, 0)]
+            for fold, xaff in wg_modes:
+                best = None
+                for t in WG_TILES:
+                    if Cout % t[0] or (t[1] == 128 and ldw < 128):
                         continue
-                    ms = timeit(lambda: ci.conv_wgrad(g, yy, al, be, x, shp, gw, sv, tv, 1, tile=t, nsplit=ns,
-                                                      slab=slab), a.reps)
-                    if best is None or ms < best[0]:
-                        best = (ms, t, ns)
-            res["wgrad"] = dict(tile=best[1], nsplit=best[2], us=round(best[0] * 1e3, 1))
+                    tiles = (Cout // t[0]) * (-(-ldw // t[1]))
+                    base = ci.wgrad_split(N * Ho * Wo, tiles)
+                    for ns in sorted({max(1, base // 2), base, base * 2}):
+                        if ns * Cout * ldw > slab.numel():
+                            continue
+                        ms = timeit(lambda: ci.conv_wgrad(g, yy if fold else None, al if fold else None,
+                                                          be if fold else None, x, shp, gw, sv if xaff else None,
+                                                          tv if xaff else None, xaff, tile=t, nsplit=ns, slab=slab),
+                                    a.reps)
+                        if best is None or ms < best[0]:
+                            best = (ms, t, ns)
+                res[f"wgrad{fold}{xaff}"] = dict(tile=best[1], nsplit=best[2], us=round(best[0] * 1e3, 1))
             table[key] = res
             print(key, json.dumps(res), flush=True)
             del x, g, yy, ex, slab
