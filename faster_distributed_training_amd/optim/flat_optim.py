@@ -66,15 +66,28 @@ class FlatOptimizer(torch.optim.Optimizer):
         return loss
 
     # ------------------------------------------------------------ state dict
+    # The optimizer state lives in whole-model flat buffers (self.state["__flat__"]), which
+    # torch.optim.Optimizer.state_dict() would not serialise (its state is keyed by
+    # parameter); save and restore them explicitly.
     def state_dict(self):
-        sd = super().state_dict()
-        sd["k"] = self.k
-        return sd
+        groups = [{k: v for k, v in g.items() if k != "params"} for g in self.param_groups]
+        flat = {k: (v.detach().clone() if torch.is_tensor(v) else v)
+                for k, v in self.state.get("__flat__", {}).items()}
+        return {"flat_state": flat, "param_groups": groups, "k": self.k, "numel": self.flat.numel}
 
     def load_state_dict(self, sd):
-        sd = dict(sd)
-        self.k = int(sd.pop("k", 0))
-        super().load_state_dict(sd)
+        if "flat_state" not in sd:  # a plain torch.optim state dict: hyper-parameters only
+            for g, sg in zip(self.param_groups, sd.get("param_groups", [])):
+                g.update({k: v for k, v in sg.items() if k != "params"})
+            return
+        if sd.get("numel", self.flat.numel) != self.flat.numel:
+            raise ValueError("optimizer state was saved for a different parameter layout")
+        for g, sg in zip(self.param_groups, sd["param_groups"]):
+            g.update(sg)
+        st = self.state.setdefault("__flat__", {})
+        for k, v in sd["flat_state"].items():
+            st[k] = v.to(self.flat.device) if torch.is_tensor(v) else v
+        self.k = int(sd.get("k", 0))
 
     def _cpu_common(self, grad_scale, found_inf):
         if found_inf is not None and bool(found_inf.item() != 0):

@@ -1,0 +1,54 @@
+"""Multi-process harness for distributed tests on the CPU (gloo backend, 127.0.0.1)."""
+from __future__ import annotations
+
+import os
+import socket
+import sys
+import traceback
+
+import torch.multiprocessing as mp
+
+
+def free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _entry(rank, world, port, fn, args, errq):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    os.environ["RANK"] = str(rank)
+    os.environ["LOCAL_RANK"] = str(rank)
+    os.environ["WORLD_SIZE"] = str(world)
+    os.environ["FDT_NATIVE"] = "0"
+    try:
+        import torch.distributed as dist
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        try:
+            fn(rank, world, *args)
+        finally:
+            dist.destroy_process_group()
+    except Exception:  # report to the parent
+        errq.put((rank, traceback.format_exc()))
+        sys.exit(1)
+
+
+def run_world(fn, world=2, args=(), timeout=240):
+    ctx = mp.get_context("spawn")
+    errq = ctx.SimpleQueue()
+    port = free_port()
+    procs = [ctx.Process(target=_entry, args=(r, world, port, fn, args, errq)) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout)
+    for p in procs:
+        if p.is_alive():
+            p.kill()
+            raise RuntimeError("distributed test timed out")
+    errs = []
+    while not errq.empty():
+        errs.append(errq.get())
+    if errs or any(p.exitcode != 0 for p in procs):
+        raise AssertionError("\n".join(f"rank {r}:\n{tb}" for r, tb in errs) or "a rank failed")
