@@ -1,0 +1,225 @@
+"""AG News text pipeline (reference ``transformer_test.py:59-149``, survey D6).
+
+Reference behaviour: torchtext ``AG_NEWS`` datapipes -> per-batch collate that strips HTML
+(``<...>``) and URLs, removes gensim stopwords, tokenises with ``bert-base-uncased``
+(``padding='longest'``, no truncation -> Q18) and returns
+``(input_ids, labels 1..4, token_type_ids, attention_mask)``; labels are shifted by -1 in
+the training loop; vocab = 30522.
+
+MI355X design:
+
+* the whole corpus is tokenised ONCE up front (not per batch in worker processes) into a
+  packed int32 token store ``(offsets, tokens)`` with per-sample lengths; a batch is a
+  gather + pad on the device (static shapes per length bucket);
+* sequences are truncated to ``max_len`` (512, the model's position table; fixes Q18);
+* ``length_buckets`` (e.g. 64/128/256/512) round each batch's padded length up so the
+  attention/GEMM shapes repeat (kernel tuning and HIP-graph friendly); ``None`` pads to
+  the longest sample in the batch exactly like the reference;
+* tokenizer: a local HuggingFace tokenizer (``bert-base-uncased`` from the HF cache or a
+  path) when available; otherwise ``HashWordPieceTokenizer`` — a dependency-free
+  lower-casing word tokenizer hashing words into the BERT id range with BERT's special
+  ids ([PAD]=0, [CLS]=101, [SEP]=102), so shapes, vocab size and masks match;
+* no network: CSV files (``train.csv``/``test.csv`` in the AG News layout
+  ``"class","title","description"``) are read from ``root`` when present, otherwise
+  ``synthetic_agnews`` provides an AG-News-shaped corpus (120k/7.6k samples, 4 classes,
+  AG-News-like length distribution, class-dependent vocabulary so models can learn).
+"""
+from __future__ import annotations
+
+import csv
+import os
+import re
+import zlib
+
+import numpy as np
+import torch
+
+VOCAB_SIZE = 30522
+PAD_ID, CLS_ID, SEP_ID = 0, 101, 102
+NUM_CLASSES = 4
+TRAIN_SIZE, TEST_SIZE = 120000, 7600
+
+_HTML = re.compile(r"<[^>]+>")
+_URL = re.compile(r"https?://\S+|www\.\S+")
+_WORD = re.compile(r"[a-z0-9]+(?:'[a-z]+)?|[^\sa-z0-9]")
+
+# A compact English stopword list (gensim's STOPWORDS is not installed here; this covers
+# the high-frequency function words it removes).
+STOPWORDS = frozenset("""a about above after again against all also am an and any are as at be because been before
+being below between both but by can could did do does doing down during each few for from further had has have having
+he her here hers herself him himself his how i if in into is it its itself just me more most my myself no nor not now
+of off on once only or other our ours ourselves out over own same she should so some such than that the their theirs
+them themselves then there these they this those through to too under until up very was we were what when where which
+while who whom why will with would you your yours yourself yourselves""".split())
+
+
+def clean_text(s: str) -> str:
+    """HTML strip + URL strip + stopword removal (reference ``transformer_test.py:73-79``)."""
+    s = _HTML.sub(" ", s)
+    s = _URL.sub(" ", s)
+    return " ".join(w for w in s.split() if w.lower() not in STOPWORDS)
+
+
+class HashWordPieceTokenizer:
+    """Deterministic offline tokenizer with BERT's id conventions."""
+
+    vocab_size = VOCAB_SIZE
+    first_regular = 1000  # BERT's [unused]/special block lives below
+
+    def _id(self, w: str) -> int:
+        return self.first_regular + zlib.crc32(w.encode()) % (VOCAB_SIZE - self.first_regular)
+
+    def encode(self, text: str, max_len: int = 512):
+        ids = [CLS_ID] + [self._id(w) for w in _WORD.findall(text.lower())]
+        ids = ids[: max_len - 1] + [SEP_ID]
+        return ids
+
+
+def get_tokenizer(name_or_path: str | None = "bert-base-uncased"):
+    """HF tokenizer from the local cache / a path if it loads offline, else the fallback."""
+    if name_or_path:
+        try:
+            os.environ.setdefault("HF_HUB_OFFLINE", "1")
+            from transformers import AutoTokenizer
+            tok = AutoTokenizer.from_pretrained(name_or_path, local_files_only=True)
+
+            class _HF:
+                vocab_size = tok.vocab_size
+
+                def encode(self, text, max_len=512):
+                    return tok(text, truncation=True, max_length=max_len)["input_ids"]
+            return _HF()
+        except Exception:
+            pass
+    return HashWordPieceTokenizer()
+
+
+def get_tokenizer_size(name_or_path: str | None = "bert-base-uncased") -> int:
+    """Reference ``get_tokenizer_size`` (``transformer_test.py:141-143``)."""
+    return get_tokenizer(name_or_path).vocab_size
+
+
+class TokenStore:
+    """Packed corpus: ``tokens`` (int32, concatenated), ``offsets`` [n+1], ``labels`` [n]
+    (0-based)."""
+
+    def __init__(self, seqs, labels):
+        lens = np.fromiter((len(s) for s in seqs), dtype=np.int64, count=len(seqs))
+        self.offsets = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
+        self.tokens = np.fromiter((t for s in seqs for t in s), dtype=np.int32, count=int(lens.sum()))
+        self.labels = np.asarray(labels, dtype=np.int64)
+        self.lengths = lens
+
+    def __len__(self):
+        return len(self.labels)
+
+    def sample(self, i):
+        return self.tokens[self.offsets[i]:self.offsets[i + 1]], int(self.labels[i])
+
+
+def read_agnews_csv(path: str):
+    """AG News CSV rows ``"class","title","description"`` -> (texts, 0-based labels)."""
+    texts, labels = [], []
+    with open(path, newline="", encoding="utf-8") as f:
+        for row in csv.reader(f):
+            if len(row) < 3:
+                continue
+            labels.append(int(row[0]) - 1)  # reference shifts labels by -1 (transformer_test.py:242)
+            texts.append(clean_text(row[1] + " " + row[2]))
+    return texts, labels
+
+
+def synthetic_agnews(n: int, seed: int = 0, max_len: int = 512, vocab: int = VOCAB_SIZE):
+    """AG-News-shaped corpus: lengths ~ the BERT-tokenised AG News distribution (mean ~45,
+    long tail to ~200), 4 balanced classes, each with a class-specific vocabulary slice
+    mixed into shared background tokens so a model can learn it."""
+    rng = np.random.default_rng(seed)
+    lens = np.clip(np.rint(rng.lognormal(mean=3.75, sigma=0.33, size=n)), 8, max_len - 2).astype(np.int64)
+    labels = rng.integers(0, NUM_CLASSES, size=n)
+    span = (vocab - 1000) // (NUM_CLASSES + 1)
+    seqs = []
+    for L, c in zip(lens, labels):
+        bg = rng.integers(1000, 1000 + span, size=L)
+        topic = rng.integers(1000 + span * (c + 1), 1000 + span * (c + 2), size=L)
+        pick = rng.random(L) < 0.3
+        body = np.where(pick, topic, bg)
+        seqs.append(np.concatenate([[CLS_ID], body, [SEP_ID]]).astype(np.int32))
+    return TokenStore(seqs, labels)
+
+
+def load_agnews(root: str = "./data", train: bool = True, tokenizer=None, max_len: int = 512,
+                synthetic: bool = False, seed: int = 0):
+    """TokenStore for the split: real CSV under ``root/ag_news`` if present (and not
+    ``synthetic``), otherwise the synthetic AG-News-shaped corpus."""
+    path = os.path.join(root, "ag_news", "train.csv" if train else "test.csv")
+    if not synthetic and os.path.isfile(path):
+        tok = tokenizer or get_tokenizer()
+        texts, labels = read_agnews_csv(path)
+        return TokenStore([tok.encode(t, max_len) for t in texts], labels)
+    return synthetic_agnews(TRAIN_SIZE if train else TEST_SIZE, seed=seed + (0 if train else 1), max_len=max_len)
+
+
+def _round_up(L, buckets):
+    if not buckets:
+        return L
+    for b in buckets:
+        if L <= b:
+            return b
+    return buckets[-1]
+
+
+class TextBatchLoader:
+    """Batches of ``(input_ids [B,L], labels [B], token_type_ids [B,L], attention_mask [B,L])``
+    with DistributedSampler semantics (seeded shared permutation, rank-strided shard,
+    ``set_epoch``, ``drop_last``).  The packed token store is uploaded to the device once;
+    each batch is one gather + pad."""
+
+    def __init__(self, store: TokenStore, batch_size: int, device, rank=0, world_size=1, shuffle=True,
+                 drop_last=True, seed=0, length_buckets=(64, 128, 256, 512)):
+        self.store = store
+        self.bs = batch_size
+        self.device = torch.device(device)
+        self.rank, self.world = rank, world_size
+        self.shuffle, self.drop_last, self.seed = shuffle, drop_last, seed
+        self.buckets = sorted(length_buckets) if length_buckets else None
+        self.epoch = 0
+        self.tokens = torch.from_numpy(store.tokens.astype(np.int64)).to(self.device)
+        self.offsets = torch.from_numpy(store.offsets).to(self.device)
+        self.lengths = torch.from_numpy(store.lengths)
+        self.labels = torch.from_numpy(store.labels).to(self.device)
+
+    def set_epoch(self, e):
+        self.epoch = e
+
+    def _indices(self):
+        n = len(self.store)
+        perm = (torch.randperm(n, generator=torch.Generator().manual_seed(self.seed + self.epoch))
+                if self.shuffle else torch.arange(n))
+        per = n // self.world if self.drop_last else -(-n // self.world)
+        if not self.drop_last and per * self.world > n:
+            perm = torch.cat([perm, perm[: per * self.world - n]])
+        return perm[self.rank:per * self.world:self.world]
+
+    def __len__(self):
+        per = len(self.store) // self.world if self.drop_last else -(-len(self.store) // self.world)
+        return per // self.bs if self.drop_last else -(-per // self.bs)
+
+    def batch(self, idx: torch.Tensor):
+        lens = self.lengths[idx]
+        L = _round_up(int(lens.max()), self.buckets)
+        B = idx.numel()
+        dev_idx = idx.to(self.device)
+        start = self.offsets[dev_idx]
+        ln = lens.to(self.device).clamp(max=L)
+        pos = torch.arange(L, device=self.device)
+        valid = pos.unsqueeze(0) < ln.unsqueeze(1)
+        gather = (start.unsqueeze(1) + pos.unsqueeze(0)).clamp(max=self.tokens.numel() - 1)
+        ids = torch.where(valid, self.tokens[gather], torch.zeros((), dtype=torch.long, device=self.device))
+        mask = valid.to(torch.long)
+        types = torch.zeros(B, L, dtype=torch.long, device=self.device)
+        return ids, self.labels[dev_idx], types, mask
+
+    def __iter__(self):
+        idx = self._indices()
+        for b in range(len(self)):
+            yield self.batch(idx[b * self.bs:(b + 1) * self.bs])

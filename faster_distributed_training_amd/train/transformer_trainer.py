@@ -1,0 +1,266 @@
+"""Transformer / AG News training driver (reference ``transformer_test.py:152-424``; T3, T4).
+
+Per step (device-resident, no host synchronisation): token batch (packed store, gather +
+pad to a length bucket) -> forward with in-model manifold mixup (A5) under bf16 autocast
+-> lambda-weighted cross entropy (fused kernel) -> backward (DDP buckets all-reduced
+during backward, or flat-sharded FSDP reduce-scatter after it) -> grad-norm clip (10.0)
+-> one fused optimizer launch (NGD / MirrorMADGRAD) -> OneCycle LR step.
+
+Reference quirks handled (survey §2.9): Q8 eval crash (tuple output) and mixup active in
+eval -> fixed; Q9 OneCycleLR stepped per epoch -> stepped per batch (``faithful`` keeps
+per-epoch); Q11 lr x4 -> lr x world (``faithful`` keeps x4); Q17 FSDP + NGD on a flat CPU
+shard -> the sharded optimizer owns whole, correctly shaped parameters; Q18 no truncation
+-> truncated to maxlen.
+"""
+from __future__ import annotations
+
+import os
+import time
+from dataclasses import dataclass, field
+
+import numpy as np
+import torch
+import torch.nn as nn
+
+from ..data.agnews import NUM_CLASSES, TextBatchLoader, get_tokenizer, load_agnews
+from ..models.transformer import Transformer
+from ..ops.mixup import mixup_criterion
+from ..optim.flat_optim import SGD, Adam, DeviceGradScaler, GradClipper, MirrorMADGRAD, MADGRAD
+from ..optim.ngd import NGD
+from ..parallel import dist as pdist
+from ..utils.env import default_device, print0, seed_everything
+from ..utils.flat import FlatParams
+from . import checkpoint as ckpt
+from .metrics import DeviceMeter, JsonlLogger, draw_graph, peak_memory_gb
+
+
+@dataclass
+class TransformerConfig:
+    batch_size: int = 128            # per process (reference --batch_size)
+    epoch: int = 50
+    lr: float = 1e-4
+    alpha: float = 0.99              # Beta(alpha, alpha) for manifold mixup
+    distributed: bool = False
+    ngd: bool = False
+    optimizer: str = "auto"          # auto: ngd -> NGD else MirrorMADGRAD (reference)
+    weight_decay: float | None = None
+    precision: str = "bf16"
+    synthetic: bool = False
+    data_root: str = "./data"
+    tokenizer: str | None = "bert-base-uncased"
+    seed: int = 123456
+    faithful: bool = False
+    fsdp: bool = False
+    bucket_mb: float = 8.0
+    resume: bool = False
+    checkpoint_dir: str = "./checkpoint"
+    steps_per_epoch: int = 0
+    eval: bool = True
+    log_path: str | None = None
+    plot: bool = True
+    workers: int = 2
+    n_layers: int = 6
+    d_model: int = 512
+    heads: int = 8
+    d_ff: int = 1024
+    d_hidden: int = 1024
+    maxlen: int = 512
+    length_buckets: tuple = (64, 128, 256, 512)
+    clip: float = 10.0
+    extra: dict = field(default_factory=dict)
+
+
+class TransformerTrainer:
+    def __init__(self, cfg: TransformerConfig):
+        self.cfg = cfg
+        self.rank, self.world = 0, 1
+        if cfg.distributed or int(os.environ.get("WORLD_SIZE", "1")) > 1:
+            if not pdist.is_dist():
+                pdist.setup_norank()
+            self.rank, self.world = pdist.rank(), pdist.world()
+            cfg.distributed = self.world > 1
+        self.device = default_device()
+        seed_everything(cfg.seed)
+        self.tokenizer = get_tokenizer(cfg.tokenizer) if not cfg.synthetic else None
+        vocab = self.tokenizer.vocab_size if self.tokenizer is not None else 30522
+        self.model = Transformer(NUM_CLASSES, vocab, n_layers=cfg.n_layers, h=cfg.heads, d_model=cfg.d_model,
+                                 d_ff=cfg.d_ff, d_hidden=cfg.d_hidden, maxlen=cfg.maxlen, alpha=cfg.alpha,
+                                 faithful=cfg.faithful).to(self.device)
+        self.best_acc, self.start_epoch = ckpt.load_best_performance(self.ckpt_path, NUM_CLASSES, cfg.resume)
+        if cfg.resume:
+            ckpt.load_model_state(self.model, ckpt.load_checkpoint(self.ckpt_path)["net"])
+        self.flat = FlatParams(self.model, device=self.device)
+        self.reducer = self.fsdp = None
+        if cfg.distributed:
+            if cfg.fsdp:
+                from ..parallel.fsdp import FlatShardedDP
+                self.fsdp = FlatShardedDP(self.flat, self.model)
+            else:
+                from ..parallel.ddp import BucketReducer
+                self.reducer = BucketReducer(self.flat, self.model, bucket_mb=cfg.bucket_mb)
+        seed_everything(cfg.seed, self.rank)
+        self.space = self.fsdp.view if self.fsdp is not None else self.flat
+        self._build_data()
+        self.optimizer, self.scheduler = self._build_optimizer()
+        self.clipper = GradClipper(self.space, sharded=self.fsdp is not None)
+        self.scaler = DeviceGradScaler(self.device, enabled=(cfg.precision == "fp16"))
+        self.meter = DeviceMeter(self.device)
+        self.logger = JsonlLogger(cfg.log_path)
+        self.pos_index = torch.arange(cfg.maxlen, device=self.device)  # transformer_test.py:228
+        self.training_acc, self.testing_acc, self.epoch_time = [], [], []
+
+    @property
+    def ckpt_path(self):
+        return os.path.join(self.cfg.checkpoint_dir, "transformer_ckpt.pth")
+
+    def _build_data(self):
+        cfg = self.cfg
+        tr = load_agnews(cfg.data_root, True, self.tokenizer, cfg.maxlen, cfg.synthetic, seed=1)
+        te = load_agnews(cfg.data_root, False, self.tokenizer, cfg.maxlen, cfg.synthetic, seed=1)
+        sub = cfg.extra.get("subset_stride")
+        if sub:
+            from ..data.agnews import TokenStore
+            tr = TokenStore([tr.sample(i)[0] for i in range(0, len(tr), sub)], tr.labels[::sub])
+            te = TokenStore([te.sample(i)[0] for i in range(0, len(te), sub)], te.labels[::sub])
+        self.train_loader = TextBatchLoader(tr, cfg.batch_size, self.device, rank=self.rank, world_size=self.world,
+                                            seed=cfg.seed, length_buckets=cfg.length_buckets)
+        # eval: every rank evaluates the full test set, as the reference does
+        self.test_loader = TextBatchLoader(te, cfg.batch_size, self.device, shuffle=False, drop_last=False,
+                                           length_buckets=cfg.length_buckets)
+
+    def _lr(self):
+        lr = self.cfg.lr
+        if self.cfg.distributed:
+            lr *= 4 if self.cfg.faithful else self.world  # reference hard-codes 4 (Q11)
+        return lr
+
+    def _build_optimizer(self):
+        cfg = self.cfg
+        lr = self._lr()
+        kind = cfg.optimizer
+        if kind == "auto":
+            kind = "ngd" if cfg.ngd else "mirror_madgrad"
+        wd = cfg.weight_decay
+        if kind == "ngd":
+            opt = NGD(self.space, lr=lr, weight_decay=wd or 0.0)
+        elif kind == "mirror_madgrad":
+            opt = MirrorMADGRAD(self.space, lr=lr, momentum=0.9, weight_decay=wd or 0.0)
+        elif kind == "madgrad":
+            opt = MADGRAD(self.space, lr=lr, momentum=0.9, weight_decay=wd or 0.0)
+        elif kind == "sgd":
+            opt = SGD(self.space, lr=lr, momentum=0.0, weight_decay=wd or 0.0)
+        elif kind in ("adam", "adamw"):
+            opt = Adam(self.space, lr=lr, weight_decay=wd or 0.0, adamw=kind == "adamw")
+        else:
+            raise ValueError(kind)
+        steps = self.cfg.steps_per_epoch or len(self.train_loader)
+        if cfg.extra.get("scheduler") == "multistep":  # tuning variant (tuning/transformer_tuning.py:204)
+            sch = torch.optim.lr_scheduler.MultiStepLR(opt, [10, 15], gamma=0.1)
+        else:
+            sch = torch.optim.lr_scheduler.OneCycleLR(opt, max_lr=5 * lr, epochs=cfg.epoch,
+                                                      steps_per_epoch=max(1, steps), cycle_momentum=True)
+        return opt, sch
+
+    def _autocast(self):
+        p = self.cfg.precision
+        if p == "fp32":
+            return torch.autocast(self.device.type, enabled=False)
+        dt = torch.bfloat16 if p == "bf16" else torch.float16
+        return torch.autocast(self.device.type, dtype=dt, enabled=(self.device.type == "cuda" or p == "bf16"))
+
+    def train_step(self, tokens, labels, types, masks):
+        cfg = self.cfg
+        mask = masks.view(masks.shape[0], 1, 1, masks.shape[1])
+        with self._autocast():
+            logits, perm, lam = self.model(tokens, types, self.pos_index, mask)
+            loss = mixup_criterion(None, logits, labels, labels[perm], lam)
+        self.scaler.scale_loss(loss).backward()
+        if self.reducer is not None:
+            self.reducer.finish()
+        if self.fsdp is not None:
+            self.fsdp.finish_backward()
+        fp16 = self.scaler.enabled
+        self.clipper(cfg.clip, inv_scale=self.scaler.inv_scale(), check_inf=fp16)
+        found = None
+        if fp16:
+            self.scaler.sync_found_inf(self.clipper.found_inf)
+            found = self.clipper.found_inf
+        self.optimizer.step(grad_scale=self.clipper.coef, found_inf=found)
+        if fp16:
+            self.scaler.update(found)
+        if self.fsdp is not None:
+            self.fsdp.after_step()
+        if not cfg.faithful and self.scheduler is not None and isinstance(
+                self.scheduler, torch.optim.lr_scheduler.OneCycleLR):
+            if self.scheduler.last_epoch + 1 < self.scheduler.total_steps:
+                self.scheduler.step()  # per batch, as OneCycleLR intends (Q9)
+        self.meter.update(loss, logits.detach(), labels, labels[perm], lam)
+        return loss
+
+    def train_epoch(self, epoch):
+        self.model.train()
+        self.meter.reset()
+        self.train_loader.set_epoch(epoch)
+        if self.device.type == "cuda":
+            torch.cuda.synchronize()
+            torch.cuda.reset_peak_memory_stats()
+        t0 = time.monotonic()
+        n = 0
+        for i, batch in enumerate(self.train_loader):
+            if self.cfg.steps_per_epoch and i >= self.cfg.steps_per_epoch:
+                break
+            self.train_step(*batch)
+            n += 1
+        if self.device.type == "cuda":
+            torch.cuda.synchronize()
+        dt = time.monotonic() - t0
+        m = self.meter.reduced()
+        samples = n * self.cfg.batch_size * self.world
+        rec = dict(epoch=epoch, steps=n, epoch_time_s=dt, samples_per_s=samples / max(dt, 1e-9), train_loss=m["loss"],
+                   train_acc=m["acc"], peak_mem_gb=peak_memory_gb(), lr=self.optimizer.group["lr"])
+        print0(f"epoch {epoch}: {n} steps in {dt:.2f}s ({rec['samples_per_s']:.0f} samples/s) loss {m['loss']:.4f} "
+               f"acc {m['acc']:.2f}%  peak mem {rec['peak_mem_gb']:.2f} GB")
+        self.logger.log(**rec)
+        self.training_acc.append(m["acc"])
+        self.epoch_time.append(dt)
+        return rec
+
+    @torch.no_grad()
+    def test(self, epoch):
+        """Reference ``test`` (``transformer_test.py:300-347``) with Q8 fixed: no mixup in
+        eval and the logits are taken from the returned tuple."""
+        self.model.eval()
+        correct = torch.zeros((), device=self.device)
+        total = torch.zeros((), device=self.device)
+        for i, (tokens, labels, types, masks) in enumerate(self.test_loader):
+            if self.cfg.extra.get("eval_steps") and i >= self.cfg.extra["eval_steps"]:
+                break
+            with self._autocast():
+                logits, _, _ = self.model(tokens, types, self.pos_index, masks.view(masks.shape[0], 1, 1, -1))
+            correct += (logits.argmax(1) == labels).sum()
+            total += labels.numel()
+        acc = 100.0 * float(correct) / max(float(total), 1.0)
+        self.testing_acc.append(acc)
+        print0(f"test epoch {epoch}: acc {acc:.2f}%")
+        if acc > self.best_acc:
+            ckpt.save_checkpoint(self.ckpt_path, self.model, acc, epoch, module_prefix=self.cfg.distributed)
+            self.best_acc = acc
+        self.logger.log(epoch=epoch, test_acc=acc)
+        return acc
+
+    def fit(self):
+        for epoch in range(self.start_epoch, self.start_epoch + self.cfg.epoch):
+            self.train_epoch(epoch)
+            if self.cfg.faithful and self.scheduler is not None:
+                self.scheduler.step()  # reference: once per epoch (transformer_test.py:291)
+            elif not isinstance(self.scheduler, torch.optim.lr_scheduler.OneCycleLR) and self.scheduler is not None:
+                self.scheduler.step()
+            if self.cfg.eval:
+                self.test(epoch)
+        if self.cfg.plot:
+            xs = np.arange(self.start_epoch, self.start_epoch + len(self.training_acc))
+            if self.testing_acc:
+                draw_graph([xs, xs], [self.training_acc, self.testing_acc], ["training", "testing"],
+                           "Transformer accuracy curve", "accuracy")
+            draw_graph(xs, self.epoch_time, "training time", "Transformer time for training", "time(sec.)")
+        return self
