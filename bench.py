@@ -46,6 +46,9 @@ def parse():
     ap.add_argument("--comm-dtype", default="fp32")
     ap.add_argument("--no-native", action="store_true", help="ablation: plain PyTorch ops (w/o tricks)")
     ap.add_argument("--profile-steps", type=int, default=0)
+    ap.add_argument("--model", default="resnet50", choices=["resnet50", "transformer"],
+                    help="transformer: secondary benchmark (BASELINE.json config 4, AG-News-shaped)")
+    ap.add_argument("--seq-bucket", type=int, default=128, help="transformer: padded sequence length")
     return ap.parse_args()
 
 
@@ -53,6 +56,8 @@ def main():
     args = parse()
     if args.no_native:
         os.environ["FDT_NATIVE"] = "0"
+    if args.model == "transformer":
+        return bench_transformer(args)
     import torch
     import torch.distributed as dist
 
@@ -127,6 +132,61 @@ def main():
         "epoch_time_s": round(50000.0 / value, 3),
         "peak_mem_gb": round(torch.cuda.max_memory_allocated() / 2**30, 2) if cuda else None,
     }
+    if tr.rank == 0:
+        print(json.dumps(rec), flush=True)
+    if dist.is_initialized():
+        dist.destroy_process_group()
+
+
+def bench_transformer(args):
+    """Transformer text classifier (6 layers, d 512, vocab 30522), AG-News-shaped synthetic
+    batches padded to one length bucket, global batch 256 (reference: 64 x 4 GPUs),
+    NGD optimizer (run_distributed.sh:3), bf16."""
+    import torch
+    import torch.distributed as dist
+
+    from faster_distributed_training_amd.train.transformer_trainer import TransformerConfig, TransformerTrainer
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    gb = 256 if args.global_batch == 1024 else args.global_batch
+    assert gb % world == 0
+    cfg = TransformerConfig(batch_size=gb // world, synthetic=True, eval=False, plot=False, distributed=world > 1,
+                            ngd=True, precision=args.precision, length_buckets=(args.seq_bucket,),
+                            bucket_mb=args.bucket_mb, fsdp=args.fsdp, epoch=1)
+    tr = TransformerTrainer(cfg)
+    dev = tr.device
+    cuda = dev.type == "cuda"
+    it = iter(tr.train_loader)
+    tr.model.train()
+
+    def sync():
+        if cuda:
+            torch.cuda.synchronize()
+        if dist.is_initialized():
+            from faster_distributed_training_amd.parallel.dist import barrier
+            barrier()
+
+    for _ in range(args.warmup):
+        tr.train_step(*next(it))
+    sync()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        tr.train_step(*next(it))
+    sync()
+    elapsed = time.perf_counter() - t0
+    if dist.is_initialized():
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev if cuda else "cpu")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    value = gb * args.steps / elapsed
+    rec = {"metric": "samples/sec (whole node) Transformer AG-News-shaped bs=256", "value": round(value, 2),
+           "unit": "samples/sec", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+           "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True, "scaling": "strong",
+           "vs_baseline": round(value / 66.0, 2), "dtype": args.precision,
+           "data": "synthetic (AG-News-shaped token batches), random-init weights",
+           "config": {"model": "transformer 6x512 (vocab 30522)", "global_batch": gb, "seq_len": args.seq_bucket,
+                      "parallelism": f"{'fsdp' if args.fsdp else 'dp'}{world}", "optimizer": "ngd"},
+           "peak_mem_gb": round(torch.cuda.max_memory_allocated() / 2**30, 2) if cuda else None}
     if tr.rank == 0:
         print(json.dumps(rec), flush=True)
     if dist.is_initialized():

@@ -86,4 +86,6 @@ void wgrad_reduce(uint64_t slab, uint64_t out, int nsplit, int Cout, int Cin, in
 void pack_weights(const std::vector<uint64_t>& src, const std::vector<uint64_t>& wf, const std::vector<uint64_t>& wd,
                   const std::vector<int>& cout, const std::vector<int>& cin, const std::vector<int>& cxp,
                   const std::vector<int>& ntaps, uint64_t stream);
+// eigh.hip
+void jacobi_eigh(uint64_t A, uint64_t w, uint64_t V, uint64_t table, int batch, int n, int max_sweeps, float tol, uint64_t stream);
 }  // namespace fdt

@@ -33,6 +33,7 @@ PYBIND11_MODULE(_fdt_native, m) {
   DEF(conv_wgrad);
   DEF(wgrad_reduce);
   DEF(pack_weights);
+  DEF(jacobi_eigh);
   // optimizers
   DEF(grad_sumsq);
   DEF(grad_norm_finalize);

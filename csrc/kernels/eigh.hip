@@ -1,0 +1,221 @@
+// Batched symmetric eigendecomposition for the NGD preconditioner (gfx950 / CDNA4).
+//
+// NGD (reference ngd_optimizer.py:265) needs eigh of many small symmetric R x R matrices
+// (R <= 80 by default) on every Fisher-update step; the reference calls LAPACK/cuSOLVER
+// once per (parameter, axis) with a host round-trip each.  Here one 1024-thread workgroup
+// owns one matrix: A and the eigenvector accumulator V live in LDS ([n][n+1] fp32, odd
+// stride against bank conflicts, 2 x 80 x 81 x 4 B = 52 KB at R = 80), and cyclic
+// two-sided Jacobi runs with the round-robin (tournament) ordering -- every round rotates
+// n/2 disjoint (p,q) pairs at once.
+//
+// Round structure (two barriers):
+//   1. one lane per pair computes (c, s) and the closed-form new diagonal entries;
+//   2. A <- J^T A J as independent 2x2 blocks: the pairs partition the indices, so every
+//      element belongs to exactly one (pair k1, pair k2) block and each block's update
+//      needs only its own four entries.  Only upper blocks (k1 <= k2) are computed; the
+//      result is written to both (k1,k2) and (k2,k1), keeping A exactly symmetric.  The
+//      diagonal block of a rotated pair is written in closed form (a_pq <- 0 exactly, a_pp
+//      and a_qq from t) -- without exact annihilation, fp32 rounding residue in a_pq stalls
+//      convergence at ~1e-4 relative.  V <- V J runs in the same phase.
+// Pairs with |a_pq| <= 1e-9 sqrt|a_pp a_qq| are zeroed without rotating.  Sweeps stop once
+// the off-diagonal Frobenius mass is below tol^2 * ||A||_F^2 (one LDS reduction per sweep;
+// typically 5-8 sweeps at R <= 128) or after max_sweeps.  Eigenvalues are returned
+// ascending with matching eigenvector columns (rank sort), the torch.linalg.eigh
+// convention.  No host synchronisation; graph-capturable.
+//
+// Ragged batches: an optional int table [batch][3] = (n, offset of the matrix in A/V,
+// offset of its eigenvalues in w) lets one launch cover every NGD shape group (different
+// ranks) -- the optimizer issues one eigh launch per axis level instead of one per group.
+#include "common.h"
+
+namespace fdt {
+
+constexpr int kEighThreads = 1024;
+constexpr int kEighMaxN = 128;
+constexpr int kEighMaxPairs = kEighMaxN / 2;
+// upper 2x2 blocks per thread: 64*65/2 = 2080 blocks / 1024 threads
+constexpr int kEighBlkPerThread = (kEighMaxPairs * (kEighMaxPairs + 1) / 2 + kEighThreads - 1) / kEighThreads;
+
+__global__ __launch_bounds__(kEighThreads) void jacobi_eigh_kernel(const float* __restrict__ Ain,
+                                                                   float* __restrict__ wout, float* __restrict__ Vout,
+                                                                   const int* __restrict__ table, int n_uniform,
+                                                                   int max_sweeps, float tol) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  const long mat = blockIdx.x;
+  int n = n_uniform;
+  long offA = mat * (long)n * n, offw = mat * n;
+  if (table) {
+    n = table[3 * mat];
+    offA = table[3 * mat + 1];
+    offw = table[3 * mat + 2];
+  }
+  const int ld = n + 1;
+  float4* prm = reinterpret_cast<float4*>(sm);                     // [64] (c, s, new a_pp, new a_qq)
+  int2* pidx = reinterpret_cast<int2*>(prm + kEighMaxPairs);        // [64] (p, q); q = -1 for the dummy
+  float* red = reinterpret_cast<float*>(pidx + kEighMaxPairs);      // [32]
+  int* rank = reinterpret_cast<int*>(red + 32);                     // [128]
+  float* A = reinterpret_cast<float*>(rank + kEighMaxN);            // [n][ld]
+  float* V = A + n * ld;                                            // [n][ld]
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wid = tid >> 6;
+  const float* src = Ain + offA;
+
+  for (int e = tid; e < n * n; e += kEighThreads) {
+    const int i = e / n, j = e - (e / n) * n;
+    // symmetrise from the upper triangle (torch UPLO='U' convention)
+    const float v = i <= j ? src[(long)i * n + j] : src[(long)j * n + i];
+    A[i * ld + j] = v;
+    V[i * ld + j] = (i == j) ? 1.f : 0.f;
+  }
+
+  const int m = (n + 1) & ~1;  // players (a dummy when n is odd)
+  const int npairs = m / 2;
+  const int nblk = npairs * (npairs + 1) / 2;
+
+  // this thread's upper blocks (k1 <= k2), decoded once
+  int bk1[kEighBlkPerThread], bk2[kEighBlkPerThread];
+#pragma unroll
+  for (int u = 0; u < kEighBlkPerThread; ++u) {
+    const int b = tid + u * kEighThreads;
+    int k2 = (int)((sqrtf(8.f * b + 1.f) - 1.f) * 0.5f);
+    while (k2 * (k2 + 1) / 2 > b) --k2;
+    while ((k2 + 1) * (k2 + 2) / 2 <= b) ++k2;
+    bk2[u] = b < nblk ? k2 : -1;
+    bk1[u] = b - k2 * (k2 + 1) / 2;
+  }
+  const int nvec = n * npairs;
+  __syncthreads();
+
+  for (int sweep = 0; sweep < max_sweeps; ++sweep) {
+    float o = 0.f, t = 0.f;
+    for (int e = tid; e < n * n; e += kEighThreads) {
+      const int i = e / n, j = e - (e / n) * n;
+      const float v = A[i * ld + j];
+      t += v * v;
+      if (i != j) o += v * v;
+    }
+    o = wave_sum(o);
+    t = wave_sum(t);
+    if (lane == 0) { red[wid] = o; red[16 + wid] = t; }
+    __syncthreads();
+    float off = 0.f, tot = 0.f;
+#pragma unroll
+    for (int w = 0; w < kEighThreads / 64; ++w) { off += red[w]; tot += red[16 + w]; }
+    __syncthreads();
+    if (off <= tol * tol * tot) break;
+
+    for (int r = 0; r < m - 1; ++r) {
+      // ---- 1. rotation per pair (tournament pairing: slot 0 fixed, slots 1..m-1 rotate)
+      if (tid < npairs) {
+        const int i = tid;
+        const int a = i == 0 ? 0 : 1 + (i - 1 + r) % (m - 1);
+        const int b = 1 + (m - 2 - i + r) % (m - 1);
+        int p = a < b ? a : b, q = a < b ? b : a;
+        float c = 1.f, s = 0.f, dp = 0.f, dq = 0.f;
+        if (q < n) {
+          const float apq = A[p * ld + q];
+          const float app = A[p * ld + p], aqq = A[q * ld + q];
+          dp = app;
+          dq = aqq;
+          if (fabsf(apq) > 1e-9f * sqrtf(fabsf(app * aqq)) && fabsf(apq) > 1e-30f) {
+            const float theta = (aqq - app) / (2.f * apq);
+            // t = sign(theta) / (|theta| + sqrt(theta^2 + 1)); 1/(2 theta) once theta^2 overflows
+            const float at = fabsf(theta);
+            const float tt = at < 1e18f ? copysignf(1.f, theta) / (at + sqrtf(theta * theta + 1.f)) : 0.5f / theta;
+            c = rsqrtf(tt * tt + 1.f);
+            s = tt * c;
+            dp = app - tt * apq;
+            dq = aqq + tt * apq;
+          }
+        } else {
+          q = -1;  // paired with the dummy: index p is not rotated this round
+        }
+        prm[i] = make_float4(c, s, dp, dq);
+        pidx[i] = make_int2(p, q);
+      }
+      __syncthreads();
+      // ---- 2. A <- J^T A J by 2x2 blocks (upper blocks, mirrored), V <- V J
+#pragma unroll
+      for (int u = 0; u < kEighBlkPerThread; ++u) {
+        const int k1 = bk1[u], k2 = bk2[u];
+        if (k2 < 0) continue;
+        const int2 i1 = pidx[k1], i2 = pidx[k2];
+        if (k1 == k2) {
+          if (i1.y >= 0) {  // rotated pair: closed form, exact zero off the diagonal
+            const float4 r1 = prm[k1];
+            A[i1.x * ld + i1.x] = r1.z;
+            A[i1.y * ld + i1.y] = r1.w;
+            A[i1.x * ld + i1.y] = 0.f;
+            A[i1.y * ld + i1.x] = 0.f;
+          }
+          continue;
+        }
+        const float4 r1 = prm[k1], r2 = prm[k2];
+        const bool h1 = i1.y >= 0, h2 = i2.y >= 0;
+        const float a00 = A[i1.x * ld + i2.x];
+        const float a01 = h2 ? A[i1.x * ld + i2.y] : 0.f;
+        const float a10 = h1 ? A[i1.y * ld + i2.x] : 0.f;
+        const float a11 = (h1 && h2) ? A[i1.y * ld + i2.y] : 0.f;
+        // rows (pair k1): row_p <- c row_p - s row_q, row_q <- s row_p + c row_q
+        const float b00 = r1.x * a00 - r1.y * a10, b01 = r1.x * a01 - r1.y * a11;
+        const float b10 = r1.y * a00 + r1.x * a10, b11 = r1.y * a01 + r1.x * a11;
+        // columns (pair k2)
+        const float n00 = r2.x * b00 - r2.y * b01, n01 = r2.y * b00 + r2.x * b01;
+        const float n10 = r2.x * b10 - r2.y * b11, n11 = r2.y * b10 + r2.x * b11;
+        A[i1.x * ld + i2.x] = n00;
+        A[i2.x * ld + i1.x] = n00;
+        if (h2) { A[i1.x * ld + i2.y] = n01; A[i2.y * ld + i1.x] = n01; }
+        if (h1) { A[i1.y * ld + i2.x] = n10; A[i2.x * ld + i1.y] = n10; }
+        if (h1 && h2) { A[i1.y * ld + i2.y] = n11; A[i2.y * ld + i1.y] = n11; }
+      }
+      for (int e = tid; e < nvec; e += kEighThreads) {
+        const int k = e / n, i = e - k * n;
+        const int2 pq = pidx[k];
+        if (pq.y < 0) continue;
+        const float4 rr = prm[k];
+        const float vip = V[i * ld + pq.x], viq = V[i * ld + pq.y];
+        V[i * ld + pq.x] = rr.x * vip - rr.y * viq;
+        V[i * ld + pq.y] = rr.y * vip + rr.x * viq;
+      }
+      __syncthreads();
+    }
+  }
+
+  // ascending order: eigenvalue j goes to slot rank(j) (ties broken by index)
+  float* wo = wout + offw;
+  float* vo = Vout + offA;
+  for (int j = tid; j < n; j += kEighThreads) {
+    const float d = A[j * ld + j];
+    int rk = 0;
+    for (int k = 0; k < n; ++k) {
+      const float dk = A[k * ld + k];
+      rk += (dk < d) || (dk == d && k < j);
+    }
+    rank[j] = rk;
+    wo[rk] = d;
+  }
+  __syncthreads();
+  for (int e = tid; e < n * n; e += kEighThreads) {
+    const int i = e / n, j = e - (e / n) * n;
+    vo[(long)i * n + rank[j]] = V[i * ld + j];
+  }
+}
+
+void jacobi_eigh(uint64_t A, uint64_t w, uint64_t V, uint64_t table, int batch, int n, int max_sweeps, float tol,
+                 uint64_t stream) {
+  // n: the uniform size, or (with a table) the largest n in the table (sizes the LDS)
+  FDT_CHECK(n >= 1 && n <= kEighMaxN, "jacobi_eigh: n must be in [1, 128]");
+  if (batch == 0) return;
+  const size_t lds = (size_t)2 * n * (n + 1) * 4 + kEighMaxPairs * (16 + 8) + 32 * 4 + kEighMaxN * 4;
+  static size_t set = 64 * 1024;
+  if (lds > set) {
+    FDT_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(jacobi_eigh_kernel),
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    set = lds;
+  }
+  hipLaunchKernelGGL(jacobi_eigh_kernel, dim3(batch), dim3(kEighThreads), lds, as_stream(stream), P<const float>(A),
+                     P<float>(w), P<float>(V), P<const int>(table), n, max_sweeps, tol);
+  FDT_LAUNCH_CHECK();
+}
+
+}  // namespace fdt

@@ -12,9 +12,11 @@ per-axis preconditioning -> SGD momentum).  Same mathematics, re-designed for MI
   ``.item()`` (~943 per step measured, survey A7) — trace(K), rho, tr(D), floors, the
   NaN guard — stays a device tensor; the update schedule depends only on the host step
   counter;
-* **eigendecomposition**: the rank x rank (<= 80) symmetric Z matrices of all groups go
-  through one batched call (``ops/eigh.py``: the HIP one-workgroup-per-matrix Jacobi
-  kernel on MI355X);
+* **eigendecomposition**: each preconditioner is written as a generator that yields its
+  rank x rank (<= 80) symmetric Z matrix and resumes with the eigenpairs; the optimizer
+  drives all shape groups in lock-step, so every Z of one axis level goes through ONE
+  ragged launch (``ops/eigh.py::eigh_many``: the HIP one-workgroup-per-matrix Jacobi
+  kernel on MI355X) instead of one solver call per (parameter, axis);
 * the final momentum/weight update is the fused flat SGD kernel (``optim/flat_optim.py``).
 """
 from __future__ import annotations
@@ -51,6 +53,30 @@ def orthonormal_special(rank: int, dim: int, dtype=torch.float32, device=None) -
     return torch.cat(blocks, dim=1)[:, :dim].contiguous()
 
 
+def drive(gens):
+    """Run preconditioner generators in lock-step: each yields a batch of Z matrices and
+    receives ``(eigenvalues, eigenvectors)``; all Z pending at the same time are solved by
+    one ``eigh_many`` launch.  Returns the generators' return values."""
+    from ..ops.eigh import eigh_many
+    results = [None] * len(gens)
+    pending = {}
+    for i, g in enumerate(gens):
+        try:
+            pending[i] = next(g)
+        except StopIteration as e:
+            results[i] = e.value
+    while pending:
+        idx = list(pending)
+        outs = eigh_many([pending[i] for i in idx])
+        pending = {}
+        for i, o in zip(idx, outs):
+            try:
+                pending[i] = gens[i].send(o)
+            except StopIteration as e:
+                results[i] = e.value
+    return results
+
+
 class NGState:
     """Batched state of G preconditioners sharing (dim, rank)."""
 
@@ -78,24 +104,27 @@ class NGState:
     # -------------------------------------------------------------- public
     def precondition(self, X: torch.Tensor) -> torch.Tensor:
         """X: [G, N, dim] -> preconditioned, same shape (Frobenius norm preserved)."""
+        return drive([self.precondition_gen(X)])[0]
+
+    def precondition_gen(self, X: torch.Tensor):
+        """Generator form of ``precondition`` (yields Z, receives eigenpairs)."""
         if self.t == 0:
             self._init_default()
             self.t = 1
             for _ in range(3):
-                self._precondition_scaled(X)
+                yield from self._precondition_scaled(X)
             self.t = 0
-        return self._precondition_scaled(X)
+        return (yield from self._precondition_scaled(X))
 
     def _precondition_scaled(self, X):
         ip = (X * X).sum(dim=(1, 2))
-        Y = self._step(X, ip)
+        Y = yield from self._step(X, ip)
         fp = (Y * Y).sum(dim=(1, 2))
         out = Y * torch.sqrt(ip / (fp + 1e-30)).view(-1, 1, 1)
         bad = torch.isnan(fp).view(-1, 1, 1)
         return torch.where(bad, X, out)
 
     def _step(self, X, trXX):
-        from ..ops.eigh import batched_eigh
         updating = self._updating()
         self.t += 1
         W, d, rho = self.W, self.d, self.rho
@@ -125,7 +154,7 @@ class NGState:
         o1 = ise.unsqueeze(2) * (ise * drho).unsqueeze(1)         # outer(ise, ise*drho)
         Z = K * (c1.view(-1, 1, 1) * oo) + L * (c2.view(-1, 1, 1) * (o1 + o1.transpose(1, 2)))
         Z = Z + torch.diag_embed(c3.unsqueeze(1) * drho * drho)
-        c, U = batched_eigh(Z)                                    # ascending
+        c, U = yield Z                                            # eigh, ascending
         c = c.flip(1)
         U = U.flip(2)
         c_floor = ((rho * (1.0 - eta)) ** 2) / zs
@@ -193,11 +222,14 @@ class _ShapeGroup:
 
     def precondition(self, G: torch.Tensor) -> torch.Tensor:
         """G: [P, *shape] stacked gradients -> preconditioned (same layout)."""
+        return drive([self.precondition_gen(G)])[0]
+
+    def precondition_gen(self, G: torch.Tensor):
         for ax, st in self.axes:
             a = ax + 1  # leading stack dim
             X = G.transpose(-1, a).contiguous()
             shp = X.shape
-            Y = st.precondition(X.view(shp[0], -1, shp[-1]))
+            Y = yield from st.precondition_gen(X.view(shp[0], -1, shp[-1]))
             G = Y.view(shp).transpose(-1, a)
         return G
 
@@ -245,11 +277,10 @@ class NGD(SGD):
         if g["ngd"]:
             if self.groups is None:
                 self._build_groups()
-            for sg, slots in self.groups:
-                if not sg.axes:
-                    continue
-                stacked = torch.stack([grad[s.offset:s.offset + s.numel].view(s.shape) for s in slots])
-                out = sg.precondition(stacked)
+            live = [(sg, slots) for sg, slots in self.groups if sg.axes]
+            gens = [sg.precondition_gen(torch.stack([grad[s.offset:s.offset + s.numel].view(s.shape) for s in slots]))
+                    for sg, slots in live]
+            for (sg, slots), out in zip(live, drive(gens)):
                 for i, s in enumerate(slots):
                     grad[s.offset:s.offset + s.numel].view(s.shape).copy_(out[i])
         wd = g["weight_decay"]

@@ -122,3 +122,17 @@ def test_engine_training_reduces_loss(cuda):
         opt.step()
         losses.append(loss.item())
     assert losses[-1] < 0.5 * losses[0], losses
+
+
+def test_transformer_train_step_on_gpu(cuda):
+    """A short AG-News-shaped run of the full transformer trainer on the GPU path
+    (LayerNorm / embedding / FusedMLP / mixup kernels)."""
+    from faster_distributed_training_amd.train.transformer_trainer import TransformerConfig, TransformerTrainer
+    cfg = TransformerConfig(batch_size=32, synthetic=True, eval=False, plot=False, ngd=True, epoch=1,
+                            steps_per_epoch=3, length_buckets=(128,), extra={"subset_stride": 50})
+    tr = TransformerTrainer(cfg)
+    losses = []
+    it = iter(tr.train_loader)
+    for _ in range(3):
+        losses.append(float(tr.train_step(*next(it))))
+    assert all(l == l and l < 10 for l in losses), losses
