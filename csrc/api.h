@@ -14,14 +14,19 @@ int stats_num_blocks(long M, int C);
 void channel_stats_partial(uint64_t y, uint64_t part, long M, int C, int dt, uint64_t stream);
 void stats_finalize(uint64_t part, int nb, int C, double count, int mode, float eps, float momentum, uint64_t gamma,
                     uint64_t beta, uint64_t run_mean, uint64_t run_var, uint64_t nbt, uint64_t out_s, uint64_t out_t,
-                    uint64_t save_mean, uint64_t save_aux, uint64_t stream);
+                    uint64_t save_mean, uint64_t save_aux, int zero_after, uint64_t stream);
 void act_bwd_reduce(uint64_t g, uint64_t x, uint64_t s, uint64_t t, uint64_t gx, uint64_t part, long M, int C, int act,
                     float alpha, int dt, uint64_t stream);
-void reduce_partials(uint64_t part, int nb, int nq, int C, uint64_t out, uint64_t stream);
+void reduce_partials(uint64_t part, int nb, int nq, int C, uint64_t out, int zero_after, uint64_t stream);
 int partials_compact(uint64_t part, int nb, int W, int R, uint64_t out, uint64_t stream);
 void stats_bwd_coef(uint64_t gs, uint64_t gt, int C, double count, int mode, float eps, uint64_t save_mean,
                     uint64_t save_aux, uint64_t gamma, uint64_t alpha, uint64_t beta, uint64_t ggamma, uint64_t gbeta,
                     uint64_t stream);
+void stats_bwd_finalize(uint64_t part, int nb, int nq, int C, int a_mode, float a_eps, double a_count, uint64_t a_sm,
+                        uint64_t a_sa, uint64_t a_gamma, uint64_t a_alpha, uint64_t a_beta, uint64_t a_gg,
+                        uint64_t a_gb, int b_mode, float b_eps, double b_count, uint64_t b_sm, uint64_t b_sa,
+                        uint64_t b_gamma, uint64_t b_alpha, uint64_t b_beta, uint64_t b_gg, uint64_t b_gb,
+                        uint64_t stream);
 void affine_fold(uint64_t gy, uint64_t y, uint64_t alpha, uint64_t beta, uint64_t out, long M, int C, int dt,
                  uint64_t stream);
 void residual_act_fwd(uint64_t ya, uint64_t sa, uint64_t ta, uint64_t yb, uint64_t sb, uint64_t tb, uint64_t xid,
@@ -80,7 +85,7 @@ int conv_num_row_blocks(long M, int BM);
 void conv_wgrad(uint64_t g, uint64_t y, uint64_t al, uint64_t be, uint64_t x, uint64_t xs, uint64_t xt, uint64_t slab,
                 long Nb, int Hi, int Wi, int Cx, int Ho, int Wo, int S, const std::vector<int>& dh,
                 const std::vector<int>& dw, int Cout, int ldw, int act, float act_alpha, int BM, int BN, int BK,
-                int nsplit, uint64_t stream);
+                int nsplit, int direct, uint64_t stream);
 void wgrad_reduce(uint64_t slab, uint64_t out, int nsplit, int Cout, int Cin, int ntaps, int Cxp, int accumulate,
                   uint64_t stream);
 void pack_weights(const std::vector<uint64_t>& src, const std::vector<uint64_t>& wf, const std::vector<uint64_t>& wd,
@@ -88,4 +93,10 @@ void pack_weights(const std::vector<uint64_t>& src, const std::vector<uint64_t>&
                   const std::vector<int>& ntaps, uint64_t stream);
 // eigh.hip
 void jacobi_eigh(uint64_t A, uint64_t w, uint64_t V, uint64_t table, int batch, int n, int max_sweeps, float tol, uint64_t stream);
+// attention.hip
+void attn_fwd(uint64_t q, uint64_t k, uint64_t v, const std::vector<long>& strides, uint64_t out, uint64_t lse,
+              uint64_t mask, int B, int L, int H, float fill, float p_drop, uint64_t seed, uint64_t stream);
+void attn_bwd(uint64_t q, uint64_t k, uint64_t v, const std::vector<long>& strides, uint64_t o, uint64_t dout,
+              uint64_t lse, uint64_t delta, uint64_t mask, uint64_t dq, uint64_t dk, uint64_t dv, int B, int L, int H,
+              float fill, float p_drop, uint64_t seed, uint64_t stream);
 }  // namespace fdt

@@ -24,6 +24,7 @@ PYBIND11_MODULE(_fdt_native, m) {
   DEF(reduce_partials);
   DEF(partials_compact);
   DEF(stats_bwd_coef);
+  DEF(stats_bwd_finalize);
   DEF(affine_fold);
   DEF(residual_act_fwd);
   DEF(residual_act_bwd);
@@ -34,6 +35,8 @@ PYBIND11_MODULE(_fdt_native, m) {
   DEF(wgrad_reduce);
   DEF(pack_weights);
   DEF(jacobi_eigh);
+  DEF(attn_fwd);
+  DEF(attn_bwd);
   // optimizers
   DEF(grad_sumsq);
   DEF(grad_norm_finalize);

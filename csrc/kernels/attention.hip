@@ -1,0 +1,478 @@
+// Fused multi-head attention for the Transformer classifier (gfx950 / CDNA4), head_dim 64.
+//
+// Reference: ScaledDotProduct (transformer.py:180-193): softmax(q k^T / sqrt(d_k), key
+// padding mask) -> dropout -> @ v, with L <= 512 and B x H = 64 x 8 per GPU.  PyTorch
+// materialises the B x H x L x L scores (plus the softmax and dropout masks) in HBM; here
+// nothing L x L ever leaves the chip.
+//
+// Layout: q, k, v are (B, L, H, 64) strided views of the projection outputs (no transpose
+// copies); O / dO / dQ / dK / dV are contiguous (B, L, H, 64); the log-sum-exp and
+// delta = rowsum(dO * O) are (B, H, L) fp32.  Scores live in the log2 domain
+// (x = s * log2(e)/sqrt(d)); exp2 everywhere.
+//
+// MFMA mapping (mfma_f32_32x32x16_bf16; C[row][col]: col = lane & 31, row = (r&3) + 8(r>>2)
+// + 4(lane>>5)): every product is oriented so that the accumulator of the first GEMM is
+// already the B operand of the next one (its k index = the accumulator's row index, in the
+// permuted order row(j) = 16s + 8(j>>2) + 4h + (j&3)); the other operand is read from a
+// transposed LDS image in that same permuted order (two 8-byte reads per lane).
+//   forward     S^T = K Q^T (query on the lane -> row max / sum are in-register plus one
+//               lane^32 exchange), online softmax, O^T += V^T P^T.          grid (L/128, H, B)
+//   bwd dK,dV   S = Q K^T, dP = dO V^T (key on the lane), dV^T += dO^T P, dK^T += Q^T dS:
+//               each wave owns 32 keys, the workgroup sweeps all queries.   grid (L/128, H, B)
+//   bwd dQ      S^T, dP^T as in forward, dQ^T += K^T dS^T: each wave owns 32 queries,
+//               the workgroup sweeps all keys (recomputes P instead of atomics / a dS
+//               round trip -- at L <= 512 the kernels are latency-, not FLOP-bound).
+// Masking: keys past L are absent; key-padding-masked keys get the fill value (-inf = true
+// mask; the reference's -1e-9 fill, survey Q7, is reproduced with fill = -1e-9).  Dropout:
+// a counter-based hash of (seed, b, h, q, key) -- the same keep mask in all kernels, no
+// mask tensor.
+#include "common.h"
+
+namespace fdt {
+namespace attn {
+
+typedef short bf16x8_t __attribute__((ext_vector_type(8)));
+typedef short bf16x4_t __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+constexpr int kD = 64;
+constexpr int kRowLd = kD + 8;  // [row][d] images: 144-B rows -> ds_read_b128 of 16 rows hits 64 distinct banks
+constexpr int kTLd = 64 + 4;    // [d][row] images: 136-B rows -> ds_read_b64 of 32 rows hits 64 distinct banks
+constexpr int kBlk = 128;       // queries (fwd, dq) / keys (dkdv) per workgroup: 4 waves x 32
+constexpr int kTile = 64;       // keys (fwd, dq) / queries (dkdv) staged per loop iteration
+
+struct Args {
+  const bf16* q;
+  const bf16* k;
+  const bf16* v;
+  long qb, ql, qh, kb, kl, kh, vb, vl, vh;  // element strides (batch, position, head); d contiguous
+  const bf16* o;                            // forward output [B][L][H][D]
+  const bf16* dout;                         // [B][L][H][D]
+  bf16* out;
+  bf16* dq;
+  bf16* dk;
+  bf16* dv;
+  const uint8_t* mask;  // [B][L] nonzero = keep; nullptr = no mask
+  float* lse;           // [B][H][L] log2-domain log-sum-exp
+  float* delta;         // [B][H][L]
+  int B, L, H;
+  float c2;           // log2(e) / sqrt(D)
+  float fill2;        // masked score in the log2 domain (-inf = true mask)
+  float scale;        // 1 / sqrt(D)
+  uint32_t drop_thr;  // drop iff hash < drop_thr (p * 2^32); 0 = no dropout
+  float keep_scale;   // 1 / (1 - p)
+  uint64_t seed;
+};
+
+__device__ __forceinline__ bool dropped(const Args& a, int bh, int q, int key) {
+  uint64_t x = (((uint64_t)bh * (uint64_t)a.L + (uint64_t)q) * (uint64_t)a.L + (uint64_t)key) ^ a.seed;
+  x ^= x >> 33;
+  x *= 0xff51afd7ed558ccdull;
+  x ^= x >> 33;
+  x *= 0xc4ceb9fe1a85ec53ull;
+  x ^= x >> 33;
+  return (uint32_t)x < a.drop_thr;
+}
+
+__device__ __forceinline__ bf16x8_t ld8(const bf16* p) { return *reinterpret_cast<const bf16x8_t*>(p); }
+
+// two 8-byte reads (k elements j = 0..3 and 4..7 of the permuted order) of a transposed image
+__device__ __forceinline__ bf16x8_t ld4x2(const bf16* p) {
+  const bf16x4_t lo = *reinterpret_cast<const bf16x4_t*>(p);
+  const bf16x4_t hi = *reinterpret_cast<const bf16x4_t*>(p + 8);
+  return __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+}
+
+__device__ __forceinline__ bf16x8_t pack8(const float* v) {
+  const uint4 u = make_uint4(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]), pack_bf16x2(v[4], v[5]),
+                             pack_bf16x2(v[6], v[7]));
+  return __builtin_bit_cast(bf16x8_t, u);
+}
+
+__device__ __forceinline__ f32x16 mfma(bf16x8_t a, bf16x8_t b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+
+__device__ __forceinline__ int crow(int r, int h) { return (r & 3) + 8 * (r >> 2) + 4 * h; }
+
+// rows [r0, r0 + 64) of a strided [L][64] matrix -> row image [64][kRowLd] and/or
+// transposed image [64][kTLd]; rows past L are zero.
+__device__ __forceinline__ void stage(bf16* rows, bf16* trans, const bf16* src, long ld, int r0, int L, int tid) {
+#pragma unroll
+  for (int it = 0; it < 2; ++it) {
+    const int c = tid + it * 256;
+    const int row = c >> 3, ch = c & 7;
+    uint4 v = make_uint4(0, 0, 0, 0);
+    if (r0 + row < L) v = *reinterpret_cast<const uint4*>(src + (long)(r0 + row) * ld + ch * 8);
+    if (rows) *reinterpret_cast<uint4*>(rows + row * kRowLd + ch * 8) = v;
+    if (trans) {
+      const uint32_t u[4] = {v.x, v.y, v.z, v.w};
+      uint16_t* t = reinterpret_cast<uint16_t*>(trans) + (ch * 8) * kTLd + row;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        t[(2 * e) * kTLd] = (uint16_t)(u[e] & 0xffffu);
+        t[(2 * e + 1) * kTLd] = (uint16_t)(u[e] >> 16);
+      }
+    }
+  }
+}
+
+// key-state of key index key: 1 keep, 0 masked (fill), -1 absent (past L)
+__device__ __forceinline__ int8_t key_state(const Args& a, int b, int key) {
+  if (key >= a.L) return -1;
+  return a.mask ? (int8_t)(a.mask[(long)b * a.L + key] != 0) : (int8_t)1;
+}
+
+__device__ __forceinline__ float masked_score(float s, int st, const Args& a) {
+  return st > 0 ? s * a.c2 : (st == 0 ? a.fill2 : -INFINITY);
+}
+
+// ------------------------------------------------------------------------------ forward
+__global__ __launch_bounds__(256) void attn_fwd_kernel(Args a) {
+  __shared__ __attribute__((aligned(16))) bf16 Ks[kTile * kRowLd];
+  __shared__ __attribute__((aligned(16))) bf16 Vt[kD * kTLd];
+  __shared__ int8_t ms[kTile];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5, l32 = lane & 31;
+  const int b = blockIdx.z, hd = blockIdx.y, bh = b * a.H + hd;
+  const int q = blockIdx.x * kBlk + w * 32 + l32;
+  const bool qv = q < a.L;
+  const bf16* qp = a.q + b * a.qb + (long)(qv ? q : a.L - 1) * a.ql + hd * a.qh;
+  bf16x8_t qf[4];
+#pragma unroll
+  for (int s = 0; s < 4; ++s) qf[s] = ld8(qp + 16 * s + 8 * h);
+  const bf16* kp = a.k + b * a.kb + hd * a.kh;
+  const bf16* vp = a.v + b * a.vb + hd * a.vh;
+  f32x16 oacc[2];
+#pragma unroll
+  for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) oacc[dt][r] = 0.f;
+  float m = -INFINITY, l = 0.f;
+
+  for (int k0 = 0; k0 < a.L; k0 += kTile) {
+    stage(Ks, nullptr, kp, a.kl, k0, a.L, tid);
+    stage(nullptr, Vt, vp, a.vl, k0, a.L, tid);
+    if (tid < kTile) ms[tid] = key_state(a, b, k0 + tid);
+    __syncthreads();
+    float x[2][16];
+    float mb = -INFINITY;
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      f32x16 s;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) s[r] = 0.f;
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) s = mfma(ld8(Ks + (32 * t + l32) * kRowLd + 16 * ks + 8 * h), qf[ks], s);
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        x[t][r] = masked_score(s[r], ms[32 * t + crow(r, h)], a);
+        mb = fmaxf(mb, x[t][r]);
+      }
+    }
+    mb = fmaxf(mb, __shfl_xor(mb, 32));
+    const float mn = fmaxf(m, mb);
+    const float mu = mn == -INFINITY ? 0.f : mn;
+    const float alpha = exp2f(m - mu);
+    float ls = 0.f;
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const float p = exp2f(x[t][r] - mu);
+        ls += p;
+        x[t][r] = p;
+      }
+    ls += __shfl_xor(ls, 32);
+    l = l * alpha + ls;
+    m = mn;
+#pragma unroll
+    for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) oacc[dt][r] *= alpha;
+    if (a.drop_thr) {
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+          x[t][r] = dropped(a, bh, q, k0 + 32 * t + crow(r, h)) ? 0.f : x[t][r] * a.keep_scale;
+    }
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int hs = 0; hs < 2; ++hs) {
+        const bf16x8_t pb = pack8(&x[t][8 * hs]);
+        const int kof = 32 * t + 16 * hs + 4 * h;
+#pragma unroll
+        for (int dt = 0; dt < 2; ++dt) oacc[dt] = mfma(ld4x2(Vt + (32 * dt + l32) * kTLd + kof), pb, oacc[dt]);
+      }
+    __syncthreads();
+  }
+
+  if (qv) {
+    const float inv = l > 0.f ? 1.f / l : 0.f;
+    bf16* op = a.out + (((long)b * a.L + q) * a.H + hd) * kD;
+#pragma unroll
+    for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const uint2 u = make_uint2(pack_bf16x2(oacc[dt][4 * g] * inv, oacc[dt][4 * g + 1] * inv),
+                                   pack_bf16x2(oacc[dt][4 * g + 2] * inv, oacc[dt][4 * g + 3] * inv));
+        *reinterpret_cast<uint2*>(op + 32 * dt + 8 * g + 4 * h) = u;
+      }
+    if (h == 0) a.lse[(long)bh * a.L + q] = l > 0.f ? m + log2f(l) : -INFINITY;
+  }
+}
+
+// ------------------------------------------------------------------------------ backward
+// delta[b][h][q] = sum_d dO * O   (one thread per (b, q, h) row of 64)
+__global__ __launch_bounds__(256) void attn_bwd_prep_kernel(Args a) {
+  const long row = (long)blockIdx.x * 256 + threadIdx.x;
+  if (row >= (long)a.B * a.L * a.H) return;
+  const bf16* o = a.o + row * kD;
+  const bf16* g = a.dout + row * kD;
+  float acc = 0.f;
+#pragma unroll
+  for (int c = 0; c < 8; ++c) {
+    const uint4 uo = *reinterpret_cast<const uint4*>(o + 8 * c);
+    const uint4 ug = *reinterpret_cast<const uint4*>(g + 8 * c);
+    const uint32_t po[4] = {uo.x, uo.y, uo.z, uo.w}, pg[4] = {ug.x, ug.y, ug.z, ug.w};
+#pragma unroll
+    for (int e = 0; e < 4; ++e) acc += bf16_lo(po[e]) * bf16_lo(pg[e]) + bf16_hi(po[e]) * bf16_hi(pg[e]);
+  }
+  const int hd = (int)(row % a.H);
+  const long bl = row / a.H;
+  const int qpos = (int)(bl % a.L);
+  const int b = (int)(bl / a.L);
+  a.delta[((long)b * a.H + hd) * a.L + qpos] = acc;
+}
+
+__global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(Args a) {
+  __shared__ __attribute__((aligned(16))) bf16 Qs[kTile * kRowLd];
+  __shared__ __attribute__((aligned(16))) bf16 Qt[kD * kTLd];
+  __shared__ __attribute__((aligned(16))) bf16 Gs[kTile * kRowLd];  // dO rows
+  __shared__ __attribute__((aligned(16))) bf16 Gt[kD * kTLd];       // dO transposed
+  __shared__ float lse_s[kTile], del_s[kTile];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5, l32 = lane & 31;
+  const int b = blockIdx.z, hd = blockIdx.y, bh = b * a.H + hd;
+  const int key = blockIdx.x * kBlk + w * 32 + l32;
+  const bool kv = key < a.L;
+  const int kc = kv ? key : a.L - 1;
+  bf16x8_t kf[4], vf[4];
+  {
+    const bf16* kp = a.k + b * a.kb + (long)kc * a.kl + hd * a.kh;
+    const bf16* vp = a.v + b * a.vb + (long)kc * a.vl + hd * a.vh;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      kf[s] = ld8(kp + 16 * s + 8 * h);
+      vf[s] = ld8(vp + 16 * s + 8 * h);
+    }
+  }
+  const int st = key_state(a, b, key);
+  const bf16* qbase = a.q + b * a.qb + hd * a.qh;
+  const long gl = (long)a.H * kD;  // row stride of the contiguous tensors
+  const bf16* gbase = a.dout + (long)b * a.L * gl + hd * kD;
+  f32x16 dk[2], dv[2];
+#pragma unroll
+  for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) { dk[dt][r] = 0.f; dv[dt][r] = 0.f; }
+
+  for (int q0 = 0; q0 < a.L; q0 += kTile) {
+    stage(Qs, Qt, qbase, a.ql, q0, a.L, tid);
+    stage(Gs, Gt, gbase, gl, q0, a.L, tid);
+    if (tid < kTile) {
+      const int qq = q0 + tid;
+      lse_s[tid] = qq < a.L ? a.lse[(long)bh * a.L + qq] : INFINITY;
+      del_s[tid] = qq < a.L ? a.delta[(long)bh * a.L + qq] : 0.f;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int qt = 0; qt < 2; ++qt) {
+      f32x16 S, dP;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) { S[r] = 0.f; dP[r] = 0.f; }
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) {
+        S = mfma(ld8(Qs + (32 * qt + l32) * kRowLd + 16 * ks + 8 * h), kf[ks], S);
+        dP = mfma(ld8(Gs + (32 * qt + l32) * kRowLd + 16 * ks + 8 * h), vf[ks], dP);
+      }
+      float p[16], ds[16];
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int qr = 32 * qt + crow(r, h);
+        const float lse2 = lse_s[qr];
+        const float pv = lse2 == -INFINITY ? 0.f : exp2f(masked_score(S[r], st, a) - lse2);
+        float z = 1.f;
+        if (a.drop_thr) z = dropped(a, bh, q0 + qr, key) ? 0.f : a.keep_scale;
+        p[r] = pv * z;
+        ds[r] = st > 0 ? pv * (dP[r] * z - del_s[qr]) : 0.f;
+      }
+#pragma unroll
+      for (int hs = 0; hs < 2; ++hs) {
+        const bf16x8_t pb = pack8(&p[8 * hs]);
+        const bf16x8_t sb = pack8(&ds[8 * hs]);
+        const int qof = 32 * qt + 16 * hs + 4 * h;
+#pragma unroll
+        for (int dt = 0; dt < 2; ++dt) {
+          dv[dt] = mfma(ld4x2(Gt + (32 * dt + l32) * kTLd + qof), pb, dv[dt]);
+          dk[dt] = mfma(ld4x2(Qt + (32 * dt + l32) * kTLd + qof), sb, dk[dt]);
+        }
+      }
+    }
+    __syncthreads();
+  }
+
+  if (kv) {
+    const long off = (((long)b * a.L + key) * a.H + hd) * kD;
+#pragma unroll
+    for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int d0 = 32 * dt + 8 * g + 4 * h;
+        *reinterpret_cast<uint2*>(a.dk + off + d0) =
+            make_uint2(pack_bf16x2(dk[dt][4 * g] * a.scale, dk[dt][4 * g + 1] * a.scale),
+                       pack_bf16x2(dk[dt][4 * g + 2] * a.scale, dk[dt][4 * g + 3] * a.scale));
+        *reinterpret_cast<uint2*>(a.dv + off + d0) =
+            make_uint2(pack_bf16x2(dv[dt][4 * g], dv[dt][4 * g + 1]), pack_bf16x2(dv[dt][4 * g + 2], dv[dt][4 * g + 3]));
+      }
+  }
+}
+
+__global__ __launch_bounds__(256) void attn_bwd_dq_kernel(Args a) {
+  __shared__ __attribute__((aligned(16))) bf16 Ks[kTile * kRowLd];
+  __shared__ __attribute__((aligned(16))) bf16 Vs[kTile * kRowLd];
+  __shared__ __attribute__((aligned(16))) bf16 Kt[kD * kTLd];
+  __shared__ int8_t ms[kTile];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5, l32 = lane & 31;
+  const int b = blockIdx.z, hd = blockIdx.y, bh = b * a.H + hd;
+  const int q = blockIdx.x * kBlk + w * 32 + l32;
+  const bool qv = q < a.L;
+  const int qc = qv ? q : a.L - 1;
+  bf16x8_t qf[4], gf[4];
+  {
+    const bf16* qp = a.q + b * a.qb + (long)qc * a.ql + hd * a.qh;
+    const bf16* gp = a.dout + (((long)b * a.L + qc) * a.H + hd) * kD;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      qf[s] = ld8(qp + 16 * s + 8 * h);
+      gf[s] = ld8(gp + 16 * s + 8 * h);
+    }
+  }
+  const float lse2 = qv ? a.lse[(long)bh * a.L + q] : INFINITY;
+  const float dl = qv ? a.delta[(long)bh * a.L + q] : 0.f;
+  const bf16* kp = a.k + b * a.kb + hd * a.kh;
+  const bf16* vp = a.v + b * a.vb + hd * a.vh;
+  f32x16 dq[2];
+#pragma unroll
+  for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) dq[dt][r] = 0.f;
+
+  for (int k0 = 0; k0 < a.L; k0 += kTile) {
+    stage(Ks, Kt, kp, a.kl, k0, a.L, tid);
+    stage(Vs, nullptr, vp, a.vl, k0, a.L, tid);
+    if (tid < kTile) ms[tid] = key_state(a, b, k0 + tid);
+    __syncthreads();
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      f32x16 S, dP;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) { S[r] = 0.f; dP[r] = 0.f; }
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) {
+        S = mfma(ld8(Ks + (32 * t + l32) * kRowLd + 16 * ks + 8 * h), qf[ks], S);
+        dP = mfma(ld8(Vs + (32 * t + l32) * kRowLd + 16 * ks + 8 * h), gf[ks], dP);
+      }
+      float ds[16];
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int kr = 32 * t + crow(r, h);
+        const int st = ms[kr];
+        const float pv = lse2 == -INFINITY ? 0.f : exp2f(masked_score(S[r], st, a) - lse2);
+        float z = 1.f;
+        if (a.drop_thr) z = dropped(a, bh, q, k0 + kr) ? 0.f : a.keep_scale;
+        ds[r] = st > 0 ? pv * (dP[r] * z - dl) : 0.f;
+      }
+#pragma unroll
+      for (int hs = 0; hs < 2; ++hs) {
+        const bf16x8_t sb = pack8(&ds[8 * hs]);
+        const int kof = 32 * t + 16 * hs + 4 * h;
+#pragma unroll
+        for (int dt = 0; dt < 2; ++dt) dq[dt] = mfma(ld4x2(Kt + (32 * dt + l32) * kTLd + kof), sb, dq[dt]);
+      }
+    }
+    __syncthreads();
+  }
+
+  if (qv) {
+    bf16* dp = a.dq + (((long)b * a.L + q) * a.H + hd) * kD;
+#pragma unroll
+    for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+      for (int g = 0; g < 4; ++g)
+        *reinterpret_cast<uint2*>(dp + 32 * dt + 8 * g + 4 * h) =
+            make_uint2(pack_bf16x2(dq[dt][4 * g] * a.scale, dq[dt][4 * g + 1] * a.scale),
+                       pack_bf16x2(dq[dt][4 * g + 2] * a.scale, dq[dt][4 * g + 3] * a.scale));
+  }
+}
+
+static Args make_args(uint64_t q, uint64_t k, uint64_t v, const std::vector<long>& st, uint64_t mask, int B, int L,
+                      int H, float fill, float p_drop, uint64_t seed) {
+  FDT_CHECK(st.size() == 9, "attention: 9 strides (q, k, v x batch, position, head)");
+  FDT_CHECK(L >= 1 && L <= 4096 && B >= 1 && H >= 1, "attention: bad shape");
+  FDT_CHECK(p_drop >= 0.f && p_drop < 1.f, "attention: dropout in [0, 1)");
+  Args a{};
+  a.q = P<const bf16>(q);
+  a.k = P<const bf16>(k);
+  a.v = P<const bf16>(v);
+  a.qb = st[0]; a.ql = st[1]; a.qh = st[2];
+  a.kb = st[3]; a.kl = st[4]; a.kh = st[5];
+  a.vb = st[6]; a.vl = st[7]; a.vh = st[8];
+  a.mask = P<const uint8_t>(mask);
+  a.B = B; a.L = L; a.H = H;
+  const float log2e = 1.4426950408889634f;
+  a.scale = 0.125f;  // 1/sqrt(64)
+  a.c2 = log2e * a.scale;
+  a.fill2 = fill * log2e;  // -inf stays -inf
+  a.drop_thr = (uint32_t)fminf(p_drop * 4294967296.f, 4294967295.f);
+  a.keep_scale = 1.f / (1.f - p_drop);
+  a.seed = seed;
+  return a;
+}
+
+}  // namespace attn
+
+void attn_fwd(uint64_t q, uint64_t k, uint64_t v, const std::vector<long>& strides, uint64_t out, uint64_t lse,
+              uint64_t mask, int B, int L, int H, float fill, float p_drop, uint64_t seed, uint64_t stream) {
+  using namespace attn;
+  Args a = make_args(q, k, v, strides, mask, B, L, H, fill, p_drop, seed);
+  a.out = P<bf16>(out);
+  a.lse = P<float>(lse);
+  hipLaunchKernelGGL(attn_fwd_kernel, dim3((L + kBlk - 1) / kBlk, H, B), dim3(256), 0, as_stream(stream), a);
+  FDT_LAUNCH_CHECK();
+}
+
+void attn_bwd(uint64_t q, uint64_t k, uint64_t v, const std::vector<long>& strides, uint64_t o, uint64_t dout,
+              uint64_t lse, uint64_t delta, uint64_t mask, uint64_t dq, uint64_t dk, uint64_t dv, int B, int L, int H,
+              float fill, float p_drop, uint64_t seed, uint64_t stream) {
+  using namespace attn;
+  Args a = make_args(q, k, v, strides, mask, B, L, H, fill, p_drop, seed);
+  a.o = P<const bf16>(o);
+  a.dout = P<const bf16>(dout);
+  a.lse = P<float>(lse);
+  a.delta = P<float>(delta);
+  a.dq = P<bf16>(dq);
+  a.dk = P<bf16>(dk);
+  a.dv = P<bf16>(dv);
+  hipStream_t st = as_stream(stream);
+  const long rows = (long)B * L * H;
+  hipLaunchKernelGGL(attn_bwd_prep_kernel, dim3((unsigned)((rows + 255) / 256)), dim3(256), 0, st, a);
+  FDT_LAUNCH_CHECK();
+  const dim3 grid((L + kBlk - 1) / kBlk, H, B);
+  hipLaunchKernelGGL(attn_bwd_dkdv_kernel, grid, dim3(256), 0, st, a);
+  FDT_LAUNCH_CHECK();
+  hipLaunchKernelGGL(attn_bwd_dq_kernel, grid, dim3(256), 0, st, a);
+  FDT_LAUNCH_CHECK();
+}
+
+}  // namespace fdt

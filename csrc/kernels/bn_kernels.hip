@@ -105,6 +105,14 @@ __global__ __launch_bounds__(kBlk) void channel_stats_partial_kernel(const T* __
 // Sum nq partial rows over nb blocks in fp64: acc[q] = sum_{b = w, w+nw, ...} part[b][q][c]
 // (4-way unrolled so the independent loads are in flight together)
 template <int NQ>
+__device__ __forceinline__ void zero_partials(float* part, int nb, int C, int c, int w, int nw) {
+  for (int b = w; b < nb; b += nw) {
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) part[((long)b * NQ + q) * C + c] = 0.f;
+  }
+}
+
+template <int NQ>
 __device__ __forceinline__ void sum_partials_f64(const float* __restrict__ part, int nb, int C, int c, double* acc,
                                                  int w, int nw) {
   double a0[NQ], a1[NQ];
@@ -135,7 +143,10 @@ constexpr int kRedWaves = 16;  // finalize / reduce kernels: 1024 threads per 64
 // mode 1: BatchNorm2d train (biased var + eps, affine gamma/beta, running stats update)
 // mode 2: BatchNorm2d eval  (running stats, affine)  -- part unused
 // save_mean[c], save_aux[c]: mode 0 -> sd ; modes 1/2 -> invstd
-__global__ __launch_bounds__(64 * kRedWaves) void stats_finalize_kernel(const float* __restrict__ part, int nb, int C, double count,
+// zero_after: re-zero the (slot) rows after reading them, so the next producer can
+// accumulate into the same workspace without a memset launch.
+__global__ __launch_bounds__(64 * kRedWaves) void stats_finalize_kernel(float* __restrict__ part, int nb, int C, double count,
+                                                              int zero_after,
                                                               int mode, float eps, float momentum,
                                                               const float* __restrict__ gamma, const float* __restrict__ beta,
                                                               float* __restrict__ run_mean, float* __restrict__ run_var,
@@ -147,6 +158,7 @@ __global__ __launch_bounds__(64 * kRedWaves) void stats_finalize_kernel(const fl
   const int c = blockIdx.x * 64 + lane;
   double acc[2] = {0.0, 0.0};
   if (c < C && mode != 2) sum_partials_f64<2>(part, nb, C, c, acc, w, kRedWaves);
+  if (c < C && zero_after) zero_partials<2>(part, nb, C, c, w, kRedWaves);
   sm[w][lane][0] = acc[0];
   sm[w][lane][1] = acc[1];
   __syncthreads();
@@ -233,14 +245,14 @@ __global__ __launch_bounds__(kBlk) void act_bwd_reduce_kernel(const T* __restric
     float acc = 0.f;
     for (int q = 0; q < RPP; ++q) acc += sm[(q * TPR + gg) * 16 + i];
     int c = (blockIdx.y * TPR + gg) * 8 + (i & 7);
-    part[((long)blockIdx.x * 2 + (i >> 3)) * C + c] = acc;
+    atomicAdd(&part[((long)(blockIdx.x & (kStatSlots - 1)) * 2 + (i >> 3)) * C + c], acc);
   }
 }
 
 // generic fp64 reduction of partial slabs: out[q][c] = sum_b part[b][q][c]
 template <int NQ>
-__global__ __launch_bounds__(64 * kRedWaves) void reduce_partials_kernel(const float* __restrict__ part, int nb, int C,
-                                                                         float* __restrict__ out) {
+__global__ __launch_bounds__(64 * kRedWaves) void reduce_partials_kernel(float* __restrict__ part, int nb, int C,
+                                                                         float* __restrict__ out, int zero_after) {
   __shared__ double sm[kRedWaves][64][NQ];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int c = blockIdx.x * 64 + lane;
@@ -248,6 +260,7 @@ __global__ __launch_bounds__(64 * kRedWaves) void reduce_partials_kernel(const f
 #pragma unroll
   for (int q = 0; q < NQ; ++q) acc[q] = 0.0;
   if (c < C) sum_partials_f64<NQ>(part, nb, C, c, acc, w, kRedWaves);
+  if (c < C && zero_after) zero_partials<NQ>(part, nb, C, c, w, kRedWaves);
 #pragma unroll
   for (int q = 0; q < NQ; ++q) sm[w][lane][q] = acc[q];
   __syncthreads();
@@ -294,36 +307,82 @@ __global__ __launch_bounds__(256) void partials_compact_kernel(const float* __re
 //    beta = -(g_s - mean g_t) gamma inv^3 / N,    alpha = -beta*mean - g_t s / N
 //    g_gamma = (g_s - mean g_t) inv,  g_beta = g_t
 // mode 2 (BatchNorm2d eval, running stats): beta = alpha = 0, g_gamma/g_beta as above
-__global__ void stats_bwd_coef_kernel(const float* __restrict__ gs, const float* __restrict__ gt, int C, double count,
-                                      int mode, float eps, const float* __restrict__ save_mean,
-                                      const float* __restrict__ save_aux, const float* __restrict__ gamma,
-                                      float* __restrict__ alpha, float* __restrict__ beta, float* __restrict__ ggamma,
-                                      float* __restrict__ gbeta) {
-  int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
-  double g_s = gs ? gs[c] : 0.0, g_t = gt ? gt[c] : 0.0;
-  double mean = save_mean[c], aux = save_aux[c];
-  if (mode == 0) {
-    double sd = aux;
-    double s = 1.0 / (sd + (double)eps);
-    double b = sd > 0.0 ? -(g_s - mean * g_t) * s * s / ((count - 1.0) * sd) : 0.0;
-    beta[c] = (float)b;
-    alpha[c] = (float)(-b * mean - g_t * s / count);
+struct CoefArgs {
+  int mode;
+  float eps;
+  double count;
+  const float* save_mean;
+  const float* save_aux;
+  const float* gamma;
+  float* alpha;
+  float* beta;
+  float* ggamma;
+  float* gbeta;
+};
+
+__device__ __forceinline__ void bwd_coef_one(const CoefArgs& a, int c, double g_s, double g_t) {
+  const double mean = a.save_mean[c], aux = a.save_aux[c];
+  const double count = a.count;
+  if (a.mode == 0) {
+    const double sd = aux;
+    const double s = 1.0 / (sd + (double)a.eps);
+    const double b = sd > 0.0 ? -(g_s - mean * g_t) * s * s / ((count - 1.0) * sd) : 0.0;
+    a.beta[c] = (float)b;
+    a.alpha[c] = (float)(-b * mean - g_t * s / count);
   } else {
-    double inv = aux;
-    double g = gamma ? (double)gamma[c] : 1.0;
-    double s = g * inv;
-    if (mode == 1) {
-      double b = -(g_s - mean * g_t) * g * inv * inv * inv / count;
-      beta[c] = (float)b;
-      alpha[c] = (float)(-b * mean - g_t * s / count);
+    const double inv = aux;
+    const double g = a.gamma ? (double)a.gamma[c] : 1.0;
+    const double s = g * inv;
+    if (a.mode == 1) {
+      const double b = -(g_s - mean * g_t) * g * inv * inv * inv / count;
+      a.beta[c] = (float)b;
+      a.alpha[c] = (float)(-b * mean - g_t * s / count);
     } else {
-      beta[c] = 0.f;
-      alpha[c] = 0.f;
+      a.beta[c] = 0.f;
+      a.alpha[c] = 0.f;
     }
     // accumulate (+=) into the parameter gradients (flat gradient views)
-    if (ggamma) ggamma[c] += (float)((g_s - mean * g_t) * inv);
-    if (gbeta) gbeta[c] += (float)g_t;
+    if (a.ggamma) a.ggamma[c] += (float)((g_s - mean * g_t) * inv);
+    if (a.gbeta) a.gbeta[c] += (float)g_t;
+  }
+}
+
+__global__ void stats_bwd_coef_kernel(const float* __restrict__ gs, const float* __restrict__ gt, int C, CoefArgs a) {
+  int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  bwd_coef_one(a, c, gs ? gs[c] : 0.0, gt ? gt[c] : 0.0);
+}
+
+// Slots [kStatSlots][NQ][C] -> fp64 sums -> BN-backward coefficients, in one launch:
+// unit A from (q0 = g_s, q1 = g_t); with NQ = 3 also unit B (the block's shortcut branch,
+// sharing g_t) from (q2, q1).  Re-zeroes the slots.
+template <int NQ>
+__global__ __launch_bounds__(64 * kRedWaves) void stats_bwd_finalize_kernel(float* __restrict__ part, int nb, int C,
+                                                                            CoefArgs A, CoefArgs B) {
+  __shared__ double sm[kRedWaves][64][NQ];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + lane;
+  double acc[NQ];
+#pragma unroll
+  for (int q = 0; q < NQ; ++q) acc[q] = 0.0;
+  if (c < C) {
+    sum_partials_f64<NQ>(part, nb, C, c, acc, w, kRedWaves);
+    zero_partials<NQ>(part, nb, C, c, w, kRedWaves);
+  }
+#pragma unroll
+  for (int q = 0; q < NQ; ++q) sm[w][lane][q] = acc[q];
+  __syncthreads();
+  if (w != 0 || c >= C) return;
+  double t[NQ];
+#pragma unroll
+  for (int q = 0; q < NQ; ++q) {
+    t[q] = 0.0;
+#pragma unroll
+    for (int k = 0; k < kRedWaves; ++k) t[q] += sm[k][lane][q];
+  }
+  bwd_coef_one(A, c, t[0], t[1]);
+  if constexpr (NQ == 3) {
+    if (B.alpha) bwd_coef_one(B, c, t[2], t[1]);
   }
 }
 
@@ -437,7 +496,7 @@ __global__ __launch_bounds__(kBlk) void residual_act_bwd_kernel(const T* __restr
     float acc = 0.f;
     for (int q = 0; q < RPP; ++q) acc += sm[(q * TPR + gg) * 24 + i];
     int c = (blockIdx.y * TPR + gg) * 8 + (i & 7);
-    part[((long)blockIdx.x * 3 + (i >> 3)) * C + c] = acc;
+    atomicAdd(&part[((long)(blockIdx.x & (kStatSlots - 1)) * 3 + (i >> 3)) * C + c], acc);
   }
 }
 
@@ -503,9 +562,9 @@ void channel_stats_partial(uint64_t y, uint64_t part, long M, int C, int dt, uin
 
 void stats_finalize(uint64_t part, int nb, int C, double count, int mode, float eps, float momentum, uint64_t gamma,
                     uint64_t beta, uint64_t run_mean, uint64_t run_var, uint64_t nbt, uint64_t out_s, uint64_t out_t,
-                    uint64_t save_mean, uint64_t save_aux, uint64_t stream) {
+                    uint64_t save_mean, uint64_t save_aux, int zero_after, uint64_t stream) {
   stats_finalize_kernel<<<(C + 63) / 64, 64 * kRedWaves, 0, as_stream(stream)>>>(
-      P<const float>(part), nb, C, count, mode, eps, momentum, P<const float>(gamma), P<const float>(beta),
+      P<float>(part), part ? nb : 0, C, count, zero_after, mode, eps, momentum, P<const float>(gamma), P<const float>(beta),
       P<float>(run_mean), P<float>(run_var), P<long long>(nbt), P<float>(out_s), P<float>(out_t), P<float>(save_mean),
       P<float>(save_aux));
   FDT_LAUNCH_CHECK();
@@ -533,23 +592,57 @@ int partials_compact(uint64_t part, int nb, int W, int R, uint64_t out, uint64_t
   return nk;
 }
 
-void reduce_partials(uint64_t part, int nb, int nq, int C, uint64_t out, uint64_t stream) {
+void reduce_partials(uint64_t part, int nb, int nq, int C, uint64_t out, int zero_after, uint64_t stream) {
   const dim3 grid((C + 63) / 64);
   switch (nq) {
-    case 1: reduce_partials_kernel<1><<<grid, 64 * kRedWaves, 0, as_stream(stream)>>>(P<const float>(part), nb, C, P<float>(out)); break;
-    case 2: reduce_partials_kernel<2><<<grid, 64 * kRedWaves, 0, as_stream(stream)>>>(P<const float>(part), nb, C, P<float>(out)); break;
-    case 3: reduce_partials_kernel<3><<<grid, 64 * kRedWaves, 0, as_stream(stream)>>>(P<const float>(part), nb, C, P<float>(out)); break;
+    case 1: reduce_partials_kernel<1><<<grid, 64 * kRedWaves, 0, as_stream(stream)>>>(P<float>(part), nb, C, P<float>(out), zero_after); break;
+    case 2: reduce_partials_kernel<2><<<grid, 64 * kRedWaves, 0, as_stream(stream)>>>(P<float>(part), nb, C, P<float>(out), zero_after); break;
+    case 3: reduce_partials_kernel<3><<<grid, 64 * kRedWaves, 0, as_stream(stream)>>>(P<float>(part), nb, C, P<float>(out), zero_after); break;
     default: throw std::runtime_error("reduce_partials: nq in [1,3]");
   }
   FDT_LAUNCH_CHECK();
+}
+
+static CoefArgs coef_args(int mode, float eps, double count, uint64_t save_mean, uint64_t save_aux, uint64_t gamma,
+                          uint64_t alpha, uint64_t beta, uint64_t ggamma, uint64_t gbeta) {
+  CoefArgs a;
+  a.mode = mode;
+  a.eps = eps;
+  a.count = count;
+  a.save_mean = P<const float>(save_mean);
+  a.save_aux = P<const float>(save_aux);
+  a.gamma = P<const float>(gamma);
+  a.alpha = P<float>(alpha);
+  a.beta = P<float>(beta);
+  a.ggamma = P<float>(ggamma);
+  a.gbeta = P<float>(gbeta);
+  return a;
 }
 
 void stats_bwd_coef(uint64_t gs, uint64_t gt, int C, double count, int mode, float eps, uint64_t save_mean,
                     uint64_t save_aux, uint64_t gamma, uint64_t alpha, uint64_t beta, uint64_t ggamma, uint64_t gbeta,
                     uint64_t stream) {
   stats_bwd_coef_kernel<<<(C + 255) / 256, 256, 0, as_stream(stream)>>>(
-      P<const float>(gs), P<const float>(gt), C, count, mode, eps, P<const float>(save_mean), P<const float>(save_aux),
-      P<const float>(gamma), P<float>(alpha), P<float>(beta), P<float>(ggamma), P<float>(gbeta));
+      P<const float>(gs), P<const float>(gt), C,
+      coef_args(mode, eps, count, save_mean, save_aux, gamma, alpha, beta, ggamma, gbeta));
+  FDT_LAUNCH_CHECK();
+}
+
+void stats_bwd_finalize(uint64_t part, int nb, int nq, int C, int a_mode, float a_eps, double a_count, uint64_t a_sm,
+                        uint64_t a_sa, uint64_t a_gamma, uint64_t a_alpha, uint64_t a_beta, uint64_t a_gg,
+                        uint64_t a_gb, int b_mode, float b_eps, double b_count, uint64_t b_sm, uint64_t b_sa,
+                        uint64_t b_gamma, uint64_t b_alpha, uint64_t b_beta, uint64_t b_gg, uint64_t b_gb,
+                        uint64_t stream) {
+  const CoefArgs A = coef_args(a_mode, a_eps, a_count, a_sm, a_sa, a_gamma, a_alpha, a_beta, a_gg, a_gb);
+  const CoefArgs B = coef_args(b_mode, b_eps, b_count, b_sm, b_sa, b_gamma, b_alpha, b_beta, b_gg, b_gb);
+  const dim3 grid((C + 63) / 64);
+  if (nq == 2) {
+    stats_bwd_finalize_kernel<2><<<grid, 64 * kRedWaves, 0, as_stream(stream)>>>(P<float>(part), nb, C, A, B);
+  } else if (nq == 3) {
+    stats_bwd_finalize_kernel<3><<<grid, 64 * kRedWaves, 0, as_stream(stream)>>>(P<float>(part), nb, C, A, B);
+  } else {
+    throw std::runtime_error("stats_bwd_finalize: nq in {2,3}");
+  }
   FDT_LAUNCH_CHECK();
 }
 

@@ -102,6 +102,12 @@ template <> struct Vec8<float> {
   }
 };
 
+// Per-channel statistics producers (conv epilogues, BN-backward reductions) add their
+// per-workgroup partial sums with fp32 atomics into kStatSlots rows (row = block index mod
+// kStatSlots, spreading contention); the fp64 finalize/reduce kernel sums the rows and
+// re-zeroes them.  Replaces per-workgroup slabs + a compaction pass.
+constexpr int kStatSlots = 64;
+
 // ---------------------------------------------------------------- wave reductions
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll

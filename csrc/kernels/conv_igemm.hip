@@ -51,7 +51,7 @@ struct ConvArgs {
   const float* pt;   // prologue per-channel shift: t (AFFINE_ACT) or beta  (FOLD)   [Cx]
   const bf16* w;     // packed weights [Cout][ldw], k-index = wt[tap]*Cx + ci
   bf16* out;         // [Nb][Hout][Wout][Cout]
-  float* part;       // per-block partial slabs [nbm][2][Cout]
+  float* part;       // statistics slots [kStatSlots][2][Cout], fp32 atomics (zeroed by the consumer)
   const bf16* ex;    // ACTBWD: producer raw output x (shape of out); ADD: unused (out is read)
   const float* es;   // ACTBWD: producer scale s [Cout]
   const float* et;   // ACTBWD: producer shift t [Cout]
@@ -417,7 +417,7 @@ __global__ __launch_bounds__(256) void igemm_kernel(const ConvArgs a) {
     __syncthreads();
     for (int e = tid; e < 2 * BN; e += 256) {
       const int q = e / BN, c = e - q * BN;
-      a.part[((long)bm * 2 + q) * a.Cout + n0 + c] = red[q * BN + c] + red[(2 + q) * BN + c];
+      atomicAdd(&a.part[((long)(bm & (kStatSlots - 1)) * 2 + q) * a.Cout + n0 + c], red[q * BN + c] + red[(2 + q) * BN + c]);
     }
   } else if constexpr (EPI == kEpiActBwd) {
 #pragma unroll
@@ -471,7 +471,7 @@ __global__ __launch_bounds__(256) void igemm_kernel(const ConvArgs a) {
     __syncthreads();
     for (int e = tid; e < 2 * BN; e += 256) {
       const int q = e / BN, c = e - q * BN;
-      a.part[((long)bm * 2 + q) * a.Cout + n0 + c] = red[q * BN + c] + red[(2 + q) * BN + c];
+      atomicAdd(&a.part[((long)(bm & (kStatSlots - 1)) * 2 + q) * a.Cout + n0 + c], red[q * BN + c] + red[(2 + q) * BN + c]);
     }
   } else {  // STORE / ADD
 #pragma unroll

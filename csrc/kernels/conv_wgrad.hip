@@ -37,7 +37,8 @@ struct WgArgs {
   const bf16* x;     // [Nb][Hi][Wi][Cx]  conv input (raw)
   const float* xs;   // s [Cx] (nullptr: identity input transform)
   const float* xt;   // t [Cx]
-  float* slab;       // [nsplit][Cout][ldw]
+  float* slab;       // [nsplit][Cout][ldw]; direct: the fp32 OIHW gradient itself
+  int direct;        // 1x1, Cx == Cin: every split atomically adds into the gradient (no reduce)
   long M;            // Nb*Ho*Wo
   int Hi, Wi, Cx, log2Cx, Ho, Wo, S, log2Ho, log2Wo;
   int ntaps, Cout, ldw, act;
@@ -289,7 +290,11 @@ __global__ __launch_bounds__(256) void wgrad_kernel(const WgArgs a) {
   }
 
   // epilogue: C[co][k]: lane column k = lane&31, rows co = (r&3) + 8(r>>2) + 4h
-  float* dst = a.slab + (long)blockIdx.y * a.Cout * a.ldw;
+  // direct (1x1 with Cx == Cin: slab row layout == OIHW): fp32 atomics accumulate every
+  // split straight into the gradient (each wave instruction = two 128-B row segments);
+  // otherwise a plain store into this split's slab for wgrad_reduce.
+  const bool direct = a.direct != 0;
+  float* dst = direct ? a.slab : a.slab + (long)blockIdx.y * a.Cout * a.ldw;
 #pragma unroll
   for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -299,7 +304,10 @@ __global__ __launch_bounds__(256) void wgrad_kernel(const WgArgs a) {
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const int co = co0 + wm * (BM / 2) + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-          dst[(long)co * a.ldw + kk] = acc[i][j][r];
+          if (direct)
+            atomicAdd(&dst[(long)co * a.ldw + kk], acc[i][j][r]);
+          else
+            dst[(long)co * a.ldw + kk] = acc[i][j][r];
         }
       }
     }
@@ -382,13 +390,15 @@ __global__ __launch_bounds__(256) void pack_weights_kernel(const PackTable tab) 
 void conv_wgrad(uint64_t g, uint64_t y, uint64_t al, uint64_t be, uint64_t x, uint64_t xs, uint64_t xt, uint64_t slab,
                 long Nb, int Hi, int Wi, int Cx, int Ho, int Wo, int S, const std::vector<int>& dh,
                 const std::vector<int>& dw, int Cout, int ldw, int act, float act_alpha, int BM, int BN, int BK,
-                int nsplit, uint64_t stream) {
+                int nsplit, int direct, uint64_t stream) {
   using namespace wg;
   WgArgs a{};
   a.g = P<const bf16>(g); a.y = P<const bf16>(y);
   a.al = P<const float>(al); a.be = P<const float>(be);
   a.x = P<const bf16>(x); a.xs = P<const float>(xs); a.xt = P<const float>(xt);
   a.slab = P<float>(slab);
+  a.direct = direct;
+  FDT_CHECK(!direct || (dh.size() == 1 && ldw == Cx), "direct wgrad needs a 1x1 conv with ldw == Cx");
   FDT_CHECK(Cx >= 8 && (Cx & (Cx - 1)) == 0, "Cx must be a power of two >= 8");
   FDT_CHECK(Cout % BM == 0, "Cout must be a multiple of BM");
   FDT_CHECK(dh.size() == dw.size() && dh.size() <= 12, "bad tap table");

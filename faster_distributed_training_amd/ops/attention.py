@@ -5,9 +5,9 @@ Reference numerics: ``softmax(q k^T / sqrt(d_k) masked_fill(mask == 0, fill)) ->
 -> @ v``.  The reference fill is ``-1e-9`` (a bug: nothing is masked, survey Q7); pass
 ``mask_value=-1e-9`` for that behaviour, default is a true mask.
 
-GPU: ``csrc/kernels/attention.hip`` — a flash-style fused kernel for head_dim 64 and
-L <= 512 (bf16 MFMA, online softmax, in-kernel counter-based dropout, no L x L
-materialisation); backward recomputes P from the saved log-sum-exp.
+GPU: ``csrc/kernels/attention.hip`` (wrapper ``ops/attention_native.py``) — flash-style
+fused kernels for head_dim 64 (bf16 MFMA, online softmax, in-kernel counter-based
+dropout, no L x L materialisation); backward recomputes P from the saved log-sum-exp.
 """
 from __future__ import annotations
 
@@ -36,17 +36,11 @@ def attention_reference(q, k, v, mask=None, dropout_p=0.0, mask_value=None, trai
 
 
 def scaled_dot_product_attention(q, k, v, mask=None, dropout_p=0.0, mask_value=None):
-    if _native.use_native(q) and q.size(-1) == 64 and q.size(1) <= 512:
-        nat = _native.load()
-        if nat is not None and hasattr(nat, "attn_fwd"):
-            from .attention_native import attention_native
-            return attention_native(q, k, v, mask, dropout_p, mask_value)
-    if q.is_cuda and mask_value is None:
-        # interim GPU path until the fused kernel covers the shape
-        am = None
-        if mask is not None:
-            am = (mask[:, None, None, :] != 0)
-        out = F.scaled_dot_product_attention(q.transpose(1, 2), k.transpose(1, 2), v.transpose(1, 2),
-                                             attn_mask=am, dropout_p=dropout_p)
-        return out.transpose(1, 2)
+    """q, k, v: (B, L, H, D); mask (B, L) 1 = keep.  MI355X: the fused HIP kernels for
+    bf16 head_dim 64 (the model's configuration under autocast); otherwise the PyTorch
+    reference composition (CPU oracle, fp32 runs)."""
+    if _native.use_native(q):
+        from . import attention_native as an
+        if an.supported(q, k, v):
+            return an.attention_native(q, k, v, mask, dropout_p, mask_value)
     return attention_reference(q, k, v, mask, dropout_p, mask_value)

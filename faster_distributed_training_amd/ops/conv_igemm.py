@@ -140,9 +140,19 @@ def out_hw(h, w, shp: ConvShape):
     return ((h + 2 * shp.pad - shp.k) // shp.stride + 1, (w + 2 * shp.pad - shp.k) // shp.stride + 1)
 
 
-def conv_fwd(x, wf, shp: ConvShape, s=None, t=None, act=0, alpha=1.0, tile=None):
+STAT_SLOTS = 64  # csrc/kernels/common.h kStatSlots
+
+
+def stat_slots(nq: int, C: int, device) -> torch.Tensor:
+    """A fresh zeroed statistics-slot buffer [STAT_SLOTS, nq, C] (the engine instead reuses
+    one persistent workspace that its finalize kernels re-zero)."""
+    return torch.zeros(STAT_SLOTS, nq, C, device=device, dtype=torch.float32)
+
+
+def conv_fwd(x, wf, shp: ConvShape, s=None, t=None, act=0, alpha=1.0, tile=None, part=None):
     """y = conv(act(x*s+t)) (or conv(x) when s is None and act == 0); returns
-    (y [N,Ho,Wo,Cout] bf16, part [nbm,2,Cout] fp32 per-block (sum y, sum y^2))."""
+    (y [N,Ho,Wo,Cout] bf16, part [STAT_SLOTS,2,Cout] fp32 slots whose row sum is
+    (sum y, sum y^2)).  ``part``: a zeroed slot buffer to accumulate into."""
     nat = _native.native()
     N, H, W, C = x.shape
     assert C == shp.cxp and x.dtype == torch.bfloat16 and x.is_contiguous()
@@ -154,7 +164,8 @@ def conv_fwd(x, wf, shp: ConvShape, s=None, t=None, act=0, alpha=1.0, tile=None)
         tile = tuple(ent["tile"]) if ent else None
     bm, bn, bk = _tile3(tile, M, shp.cout)
     y = torch.empty(N, Ho, Wo, shp.cout, device=x.device, dtype=torch.bfloat16)
-    part = torch.empty(nat.conv_num_row_blocks(M, bm), 2, shp.cout, device=x.device, dtype=torch.float32)
+    if part is None:
+        part = stat_slots(2, shp.cout, x.device)
     dh, dw, wt = taps_fwd(shp.k, shp.pad)
     if pro == PRO_AFFINE_ACT and s is None:
         s = torch.ones(C, device=x.device, dtype=torch.float32)
@@ -166,12 +177,13 @@ def conv_fwd(x, wf, shp: ConvShape, s=None, t=None, act=0, alpha=1.0, tile=None)
 
 
 def conv_dgrad(g, y, al, be, wd, shp: ConvShape, x_shape, epi=EPI_STORE, out=None, ex=None, es=None, et=None,
-               act=0, alpha=1.0, tile=None):
+               act=0, alpha=1.0, tile=None, part=None):
     """Data gradient of y = conv(a): dA = conv^T(g + al + be*y).
 
     epi: EPI_STORE -> write dA; EPI_ADD -> out += dA; EPI_ACTBWD -> through the lazy
-    input a = act(ex*es + et): out = dA*act'(.)*es, returns per-block partial slabs
-    [nbm, 2, Cin] of (sum g_pre*ex, sum g_pre)."""
+    input a = act(ex*es + et): out = dA*act'(.)*es, returns statistics slots
+    [STAT_SLOTS, 2, Cin] whose row sum is (sum g_pre*ex, sum g_pre) (``part``: a zeroed
+    slot buffer to accumulate into; every parity class of a strided conv adds to it)."""
     nat = _native.native()
     N, Hy, Wy, Cy = g.shape
     assert Cy == shp.cout and g.is_contiguous() and (y is None or y.is_contiguous())
@@ -179,7 +191,8 @@ def conv_dgrad(g, y, al, be, wd, shp: ConvShape, x_shape, epi=EPI_STORE, out=Non
     assert Cx == shp.cin
     if out is None:
         out = torch.empty(N, Hx, Wx, shp.cin, device=g.device, dtype=torch.bfloat16)
-    parts = []
+    if epi == EPI_ACTBWD and part is None:
+        part = stat_slots(2, shp.cin, g.device)
     if tile is None:
         pro = PRO_FOLD if al is not None else PRO_NONE
         e = EPI_STORE if epi == EPI_ADD else epi
@@ -193,18 +206,12 @@ def conv_dgrad(g, y, al, be, wd, shp: ConvShape, x_shape, epi=EPI_STORE, out=Non
         if len(dh) == 0 and epi == EPI_ADD:
             continue
         bm, bn, bk = _tile3(tile, M, shp.cin)
-        part = None
-        if epi == EPI_ACTBWD:
-            part = torch.empty(nat.conv_num_row_blocks(M, bm), 2, shp.cin, device=g.device, dtype=torch.float32)
-            parts.append(part)
         pro = PRO_FOLD if al is not None else PRO_NONE  # al None: g is already folded
         nat.conv_igemm(g.data_ptr(), _p(y) if pro == PRO_FOLD else 0, _p(al), _p(be), wd.data_ptr(), out.data_ptr(),
-                       _p(part), _p(ex), _p(es), _p(et), N, Hy, Wy, Cy, Ha, Wa, 1, list(dh), list(dw), list(wt),
+                       _p(part) if epi == EPI_ACTBWD else 0, _p(ex), _p(es), _p(et), N, Hy, Wy, Cy, Ha, Wa, 1, list(dh), list(dw), list(wt),
                        shp.cin, shp.ntaps * shp.cout, Hx, Wx, shp.stride, py, px, pro, 0, 1.0, epi, int(act),
                        float(alpha), bm, bn, bk, _sp())
-    if epi == EPI_ACTBWD:
-        return out, (parts[0] if len(parts) == 1 else torch.cat(parts, 0))
-    return out, None
+    return out, (part if epi == EPI_ACTBWD else None)
 
 
 def wgrad_split(M: int, tiles: int, want: int = 512, min_px: int = 1024) -> int:
@@ -239,7 +246,14 @@ def conv_wgrad(g, y, al, be, x, shp: ConvShape, out, xs=None, xt=None, act=0, al
         bm, bn, bk = tile
     tiles = (shp.cout // bm) * (-(-ldw // bn))
     ns = nsplit or wgrad_split(M, tiles)
-    if slab is None or slab.numel() < ns * shp.cout * ldw:
+    # 1x1 without channel padding: the slab row layout IS OIHW -> every split adds into
+    # `out` with fp32 atomics (no slab, no reduce launch)
+    direct = shp.ntaps == 1 and shp.cxp == shp.cin and out.is_contiguous()
+    if direct:
+        if not accumulate:
+            out.zero_()
+        slab = out
+    elif slab is None or slab.numel() < ns * shp.cout * ldw:
         slab = torch.empty(ns * shp.cout * ldw, device=g.device, dtype=torch.float32)
     dh, dw, _ = taps_fwd(shp.k, shp.pad)
     if xs is None and act != 0:
@@ -247,9 +261,10 @@ def conv_wgrad(g, y, al, be, x, shp: ConvShape, out, xs=None, xt=None, act=0, al
         xt = torch.zeros(Cx, device=x.device, dtype=torch.float32)
     nat.conv_wgrad(g.data_ptr(), _p(y), _p(al), _p(be), x.data_ptr(), _p(xs), _p(xt), slab.data_ptr(),
                    N, H, W, Cx, Hy, Wy, shp.stride, list(dh), list(dw), shp.cout, ldw, int(act), float(alpha),
-                   bm, bn, bk, ns, _sp())
-    nat.wgrad_reduce(slab.data_ptr(), out.data_ptr(), ns, shp.cout, shp.cin, shp.ntaps, shp.cxp, int(accumulate),
-                     _sp())
+                   bm, bn, bk, ns, int(direct), _sp())
+    if not direct:
+        nat.wgrad_reduce(slab.data_ptr(), out.data_ptr(), ns, shp.cout, shp.cin, shp.ntaps, shp.cxp,
+                         int(accumulate), _sp())
     return out
 
 

@@ -164,15 +164,20 @@ class Plan:
 
 
 # ------------------------------------------------------------------ kernels glue
-def compact(part, rows=64):
-    """[nb, q, C] per-workgroup slabs -> [ceil(nb/rows), q, C] (one wide pass) when large."""
-    if part is None or part.shape[0] <= 2 * rows:
-        return part
-    nb = part.shape[0]
-    nk = -(-nb // rows)
-    out = torch.empty(nk, *part.shape[1:], device=part.device, dtype=torch.float32)
-    _native.native().partials_compact(part.data_ptr(), nb, part[0].numel(), rows, out.data_ptr(), _sp())
-    return out
+_SLOTS: dict = {}
+
+
+def slots(nq, C, dev):
+    """The persistent statistics-slot workspace viewed as [STAT_SLOTS, nq, C].  Producers
+    (conv epilogues, BN-backward reductions) add into it with fp32 atomics; the consuming
+    finalize / reduce kernel sums it in fp64 and re-zeroes it, so the next producer needs
+    no memset.  One workspace suffices: every producer is consumed before the next one."""
+    need = ci.STAT_SLOTS * 3 * 2048
+    ws = _SLOTS.get(dev)
+    if ws is None or ws.numel() < max(need, ci.STAT_SLOTS * nq * C):
+        ws = torch.zeros(max(need, ci.STAT_SLOTS * nq * C), device=dev, dtype=torch.float32)
+        _SLOTS[dev] = ws
+    return ws[: ci.STAT_SLOTS * nq * C].view(ci.STAT_SLOTS, nq, C)
 
 
 def finalize_stats(part, u: Unit, M, training, dev):
@@ -190,28 +195,25 @@ def finalize_stats(part, u: Unit, M, training, dev):
         gamma, beta = bn.weight, bn.bias
     else:
         mom, rm, rv, nbt, gamma, beta = 0.0, None, None, None, None, None
-    part = compact(part) if mode != MODE_BN_EVAL else part
-    nb = part.shape[0] if (part is not None and mode != MODE_BN_EVAL) else 0
-    nat.stats_finalize(_p(part) if nb else 0, nb, C, float(M), mode, float(u.eps), float(mom), _p(gamma), _p(beta),
-                       _p(rm), _p(rv), _p(nbt), s.data_ptr(), t.data_ptr(), sm.data_ptr(), sa.data_ptr(), _sp())
+    # eval-mode BN reads no statistics but still re-zeroes the slots the conv filled
+    nat.stats_finalize(part.data_ptr(), part.shape[0], C, float(M), mode, float(u.eps), float(mom), _p(gamma),
+                       _p(beta), _p(rm), _p(rv), _p(nbt), s.data_ptr(), t.data_ptr(), sm.data_ptr(), sa.data_ptr(), 1,
+                       _sp())
     return s, t, sm, sa
 
 
 def reduce_parts(part, nq, C, dev):
     nat = _native.native()
-    part = compact(part)
     out = torch.empty(nq, C, device=dev, dtype=torch.float32)
-    nat.reduce_partials(part.data_ptr(), part.shape[0], nq, C, out.data_ptr(), _sp())
+    nat.reduce_partials(part.data_ptr(), part.shape[0], nq, C, out.data_ptr(), 1, _sp())
     return out
 
 
-def bwd_coef(u: Unit, gs, gt, sm, sa, M, training, dev):
-    """(g_s, g_t) of the normalisation of y -> correction (alpha, beta) of dL/dy; BN affine
-    gradients are accumulated into the flat gradient buffer."""
-    nat = _native.native()
+def _coef_args(u: Unit, sm, sa, M, training, dev):
+    """Kernel arguments of one unit's BN-backward coefficients; allocates (alpha, beta)
+    and the BN affine gradients (accumulated into the flat gradient buffer)."""
     C = u.shp.cout
     al, be = _f32(C, dev), _f32(C, dev)
-    mode = u.mode(training)
     gamma = u.bn.weight if u.bn is not None else None
     gg = gb = None
     if u.bn is not None:
@@ -220,12 +222,32 @@ def bwd_coef(u: Unit, gs, gt, sm, sa, M, training, dev):
                 p.grad = torch.zeros_like(p)
         gg = u.bn.weight.grad if u.bn.weight.requires_grad else None
         gb = u.bn.bias.grad if u.bn.bias.requires_grad else None
-    nat.stats_bwd_coef(gs.data_ptr(), gt.data_ptr(), C, float(M), mode, float(u.eps), sm.data_ptr(), sa.data_ptr(),
-                       _p(gamma), al.data_ptr(), be.data_ptr(), _p(gg), _p(gb), _sp())
-    if u.bn is not None:
-        grad_ready(u.bn.weight)
-        grad_ready(u.bn.bias)
-    return al, be
+    args = [u.mode(training), float(u.eps), float(M), sm.data_ptr(), sa.data_ptr(), _p(gamma), al.data_ptr(),
+            be.data_ptr(), _p(gg), _p(gb)]
+    return args, (al, be)
+
+
+_NO_UNIT = [0, 0.0, 1.0, 0, 0, 0, 0, 0, 0, 0]
+
+
+def bwd_finalize(part, nq, ua, sta, ub=None, stb=None, training=True, dev=None):
+    """Statistics slots [S, nq, C] of dL/dy reductions -> BN-backward corrections.
+
+    Unit ``ua`` takes (g_s, g_t) = rows (0, 1); with nq == 3 unit ``ub`` (the block's
+    shortcut) takes rows (2, 1).  ``st*`` = (save_mean, save_aux, M).  One launch; the slots
+    are re-zeroed.  Returns ((alpha_a, beta_a), (alpha_b, beta_b) or None)."""
+    nat = _native.native()
+    aa, ra = _coef_args(ua, sta[0], sta[1], sta[2], training, dev)
+    if ub is not None:
+        ab, rb = _coef_args(ub, stb[0], stb[1], stb[2], training, dev)
+    else:
+        ab, rb = _NO_UNIT, None
+    nat.stats_bwd_finalize(part.data_ptr(), part.shape[0], nq, ua.shp.cout, *aa, *ab, _sp())
+    for u in (ua, ub):
+        if u is not None and u.bn is not None:
+            grad_ready(u.bn.weight)
+            grad_ready(u.bn.bias)
+    return ra, rb
 
 
 def wgrad_into(u: Unit, g, y, al, be, x, xs, xt, act):
@@ -249,7 +271,7 @@ class ResNetBodyFn(torch.autograd.Function):
         recs = []
         # stem: conv -> FCBN stats -> materialised CELU output
         st = plan.stem
-        y0, part = ci.conv_fwd(x_nhwc, st.wf, st.shp)
+        y0, part = ci.conv_fwd(x_nhwc, st.wf, st.shp, part=slots(2, st.shp.cout, dev))
         M0 = _rows(y0)
         s0, t0, sm0, sa0 = finalize_stats(part, st, M0, training, dev)
         h = torch.empty_like(y0)
@@ -268,9 +290,9 @@ class ResNetBodyFn(torch.autograd.Function):
                     a_in = torch.empty_like(raw)
                     nat.act_affine_fwd(raw.data_ptr(), s.data_ptr(), t.data_ptr(), a_in.data_ptr(), _rows(raw),
                                        raw.shape[-1], act[0], float(act[1]), 1, 1, _sp())
-                    y, part = ci.conv_fwd(a_in, u.wf, u.shp)
+                    y, part = ci.conv_fwd(a_in, u.wf, u.shp, part=slots(2, u.shp.cout, dev))
                 else:
-                    y, part = ci.conv_fwd(raw, u.wf, u.shp, s, t, act[0], act[1])
+                    y, part = ci.conv_fwd(raw, u.wf, u.shp, s, t, act[0], act[1], part=slots(2, u.shp.cout, dev))
                 M = _rows(y)
                 su, tu, smu, sau = finalize_stats(part, u, M, training, dev)
                 ys.append((y, su, tu, smu, sau, M, a_in))
@@ -279,7 +301,7 @@ class ResNetBodyFn(torch.autograd.Function):
             sc = None
             if b.shortcut is not None:
                 u = b.shortcut
-                ysc, part = ci.conv_fwd(x_in, u.wf, u.shp)
+                ysc, part = ci.conv_fwd(x_in, u.wf, u.shp, part=slots(2, u.shp.cout, dev))
                 M = _rows(ysc)
                 ssc, tsc, smsc, sasc = finalize_stats(part, u, M, training, dev)
                 sc = (ysc, ssc, tsc, smsc, sasc, M, None)
@@ -307,44 +329,45 @@ class ResNetBodyFn(torch.autograd.Function):
             y3, s3 = ys[-1][0], ys[-1][1]
             C = y3.shape[-1]
             M = _rows(y3)
-            nb = nat.stats_num_blocks(M, C)
-            part = torch.empty(nb, 3, C, device=dev, dtype=torch.float32)
+            part = slots(3, C, dev)
             gya = torch.empty_like(y3)
             gyb = torch.empty_like(out)  # shortcut-branch grad, or the identity grad of x_in
             nat.residual_act_bwd(g.data_ptr(), out.data_ptr(), y3.data_ptr(), s3.data_ptr(),
                                  _p(sc[0] if sc else None), _p(sc[1] if sc else None), gya.data_ptr(),
                                  gyb.data_ptr(), part.data_ptr(), M, C, b.join[0], float(b.join[1]), 1, _sp())
-            red = reduce_parts(part, 3, C, dev)
-            gs, gt = red[0], red[1]
+            ul = b.units[-1]
+            (al, be), coef_sc = bwd_finalize(part, 3, ul, (ys[-1][3], ys[-1][4], ys[-1][5]),
+                                             b.shortcut, (sc[3], sc[4], sc[5]) if sc else None, training, dev)
             g_cur = gya
             g_x = None if sc is not None else gyb
-            # residual chain, last unit first
+            # residual chain, last unit first; (al, be) = BN-backward correction of unit i
             for i in range(len(b.units) - 1, -1, -1):
                 u = b.units[i]
                 y, su, tu, smu, sau, Mu, a_in = ys[i]
-                al, be = bwd_coef(u, gs, gt, smu, sau, Mu, training, dev)
                 if i > 0:
                     yp, sp_, tp = ys[i - 1][0], ys[i - 1][1], ys[i - 1][2]
                     actp = b.units[i - 1].act_out
+                    pp = slots(2, u.shp.cin, dev)
                     if MATERIALIZE_3X3 and u.shp.k > 1:
                         # fold the BN-backward correction into the gradient once (3x3: the
                         # dgrad operand is re-read 9x, the wgrad operand once per column block)
                         gf = torch.empty_like(g_cur)
                         nat.affine_fold(g_cur.data_ptr(), y.data_ptr(), al.data_ptr(), be.data_ptr(), gf.data_ptr(),
                                         _rows(gf), gf.shape[-1], 1, _sp())
-                        g_prev, pp = ci.conv_dgrad(gf, None, None, None, u.wd, u.shp, tuple(yp.shape),
-                                                   epi=ci.EPI_ACTBWD, ex=yp, es=sp_, et=tp, act=actp[0],
-                                                   alpha=actp[1])
+                        g_prev, _ = ci.conv_dgrad(gf, None, None, None, u.wd, u.shp, tuple(yp.shape),
+                                                  epi=ci.EPI_ACTBWD, ex=yp, es=sp_, et=tp, act=actp[0],
+                                                  alpha=actp[1], part=pp)
                         wgrad_into(u, gf, None, None, None, a_in if a_in is not None else yp,
                                    None if a_in is not None else sp_, None if a_in is not None else tp,
                                    (ACT_NONE, 1.0) if a_in is not None else actp)
                     else:
-                        g_prev, pp = ci.conv_dgrad(g_cur, y, al, be, u.wd, u.shp, tuple(yp.shape),
-                                                   epi=ci.EPI_ACTBWD, ex=yp, es=sp_, et=tp, act=actp[0],
-                                                   alpha=actp[1])
+                        g_prev, _ = ci.conv_dgrad(g_cur, y, al, be, u.wd, u.shp, tuple(yp.shape),
+                                                  epi=ci.EPI_ACTBWD, ex=yp, es=sp_, et=tp, act=actp[0],
+                                                  alpha=actp[1], part=pp)
                         wgrad_into(u, g_cur, y, al, be, yp, sp_, tp, actp)
-                    r2 = reduce_parts(pp, 2, u.shp.cin, dev)
-                    gs, gt = r2[0], r2[1]
+                    up = b.units[i - 1]
+                    (al, be), _ = bwd_finalize(pp, 2, up, (ys[i - 1][3], ys[i - 1][4], ys[i - 1][5]),
+                                               training=training, dev=dev)
                     g_cur = g_prev
                 else:
                     if g_x is None:
@@ -354,8 +377,8 @@ class ResNetBodyFn(torch.autograd.Function):
                     wgrad_into(u, g_cur, y, al, be, x_in, None, None, (ACT_NONE, 1.0))
             if sc is not None:
                 u = b.shortcut
-                ysc, ssc, tsc, smsc, sasc, Msc, _ = sc
-                al, be = bwd_coef(u, red[2], red[1], smsc, sasc, Msc, training, dev)
+                ysc = sc[0]
+                al, be = coef_sc
                 ci.conv_dgrad(gyb, ysc, al, be, u.wd, u.shp, tuple(x_in.shape), epi=ci.EPI_ADD, out=g_x)
                 wgrad_into(u, gyb, ysc, al, be, x_in, None, None, (ACT_NONE, 1.0))
             g = g_x
@@ -364,13 +387,11 @@ class ResNetBodyFn(torch.autograd.Function):
         st = plan.stem
         M0 = _rows(y0)
         C0 = st.shp.cout
-        nb = nat.stats_num_blocks(M0, C0)
-        part = torch.empty(nb, 2, C0, device=dev, dtype=torch.float32)
+        part = slots(2, C0, dev)
         gy0 = torch.empty_like(y0)
         nat.act_bwd_reduce(g.data_ptr(), y0.data_ptr(), s0.data_ptr(), t0.data_ptr(), gy0.data_ptr(),
                            part.data_ptr(), M0, C0, st.act_out[0], float(st.act_out[1]), 1, _sp())
-        red = reduce_parts(part, 2, C0, dev)
-        al, be = bwd_coef(st, red[0], red[1], sm0, sa0, M0, training, dev)
+        (al, be), _ = bwd_finalize(part, 2, st, (sm0, sa0, M0), training=training, dev=dev)
         wgrad_into(st, gy0, y0, al, be, x_img, None, None, (ACT_NONE, 1.0))
         ctx.recs = ctx.stem_rec = None
         return None, None, None, None
