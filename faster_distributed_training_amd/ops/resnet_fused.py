@@ -103,8 +103,10 @@ class Unit:
         return MODE_BN_TRAIN if use_batch else MODE_BN_EVAL
 
     def ensure_packed_buffers(self, dev, need_dgrad):
-        if self.wf is None or self.wf.device != dev:
-            self.wf, self.wd = ci.alloc_packed(self.shp, dev, dgrad=need_dgrad and self.shp.cin >= 8)
+        need_wd = need_dgrad and self.shp.cin >= 8
+        if self.wf is None or self.wf.device != dev or (need_wd and self.wd is None):
+            # (an eval / no-grad forward packs no dgrad layout; a later train step needs it)
+            self.wf, self.wd = ci.alloc_packed(self.shp, dev, dgrad=need_wd)
 
 
 def _act_of(m):

@@ -21,6 +21,11 @@ from ..utils.env import env_int, local_rank
 
 
 def _backend():
+    """``nccl`` (= RCCL) on GPUs, ``gloo`` on CPU; ``FDT_DIST_BACKEND`` overrides (e.g. gloo
+    to rehearse several ranks on one GPU, which RCCL does not allow)."""
+    be = os.environ.get("FDT_DIST_BACKEND")
+    if be:
+        return be
     return "nccl" if torch.cuda.is_available() else "gloo"
 
 

@@ -1,0 +1,31 @@
+"""Per-conv determinism: record every conv_fwd output in two identical no-grad forwards."""
+import os, sys, torch
+sys.path.insert(0, os.getcwd())
+from faster_distributed_training_amd.models import resnet as R
+from faster_distributed_training_amd.ops import conv_igemm as ci
+from faster_distributed_training_amd.ops import resnet_fused as RF
+dev = torch.device("cuda", 0)
+torch.manual_seed(0)
+m = R.resnet50(10).to(dev); m.fast_path = True
+g = torch.Generator().manual_seed(3)
+x = torch.randn(int(sys.argv[1]) if len(sys.argv) > 1 else 16, 3, 32, 32, generator=g).to(dev)
+rec = []
+orig = ci.conv_fwd
+def spy(xin, wf, shp, s=None, t=None, act=0, alpha=1.0, tile=None, part=None):
+    y, p = orig(xin, wf, shp, s, t, act, alpha, tile, part)
+    torch.cuda.synchronize()
+    rec.append((xin.clone(), y.clone(), p.sum(0).clone(), shp, None if s is None else s.clone(), None if t is None else t.clone()))
+    return y, p
+ci.conv_fwd = spy
+def rel(a, b): return ((a.float() - b.float()).norm() / (b.float().norm() + 1e-12)).item()
+with torch.no_grad():
+    m(x); r1 = rec; rec = []
+    m(x); r2 = rec
+for i, (a, b) in enumerate(zip(r1, r2)):
+    ex, ey, ep = rel(b[0], a[0]), rel(b[1], a[1]), rel(b[2], a[2])
+    es = 0 if a[4] is None else rel(b[4], a[4])
+    print(i, a[3].cin, a[3].cout, a[3].k, a[3].stride, f"in {ex:.2e} y {ey:.2e} stats {ep:.2e} s {es:.2e}", tuple(a[1].shape))
+# same-input re-run of a suspicious conv: bitwise?
+for i in range(len(r1)):
+    xin, y, p, shp, s, t = r1[i]
+    wf = None

@@ -15,13 +15,13 @@ def free_port() -> int:
         return s.getsockname()[1]
 
 
-def _entry(rank, world, port, fn, args, errq):
+def _entry(rank, world, port, fn, args, errq, native=False):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     os.environ["RANK"] = str(rank)
     os.environ["LOCAL_RANK"] = str(rank)
     os.environ["WORLD_SIZE"] = str(world)
-    os.environ["FDT_NATIVE"] = "0"
+    os.environ["FDT_NATIVE"] = "1" if native else "0"
     try:
         import torch.distributed as dist
         dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -34,11 +34,13 @@ def _entry(rank, world, port, fn, args, errq):
         sys.exit(1)
 
 
-def run_world(fn, world=2, args=(), timeout=240):
+def run_world(fn, world=2, args=(), timeout=240, native=False):
+    """Spawn ``world`` ranks (gloo).  native=True keeps the HIP fast path on (GPU tests:
+    every rank shares cuda:0 -- gloo, unlike RCCL, allows several ranks per device)."""
     ctx = mp.get_context("spawn")
     errq = ctx.SimpleQueue()
     port = free_port()
-    procs = [ctx.Process(target=_entry, args=(r, world, port, fn, args, errq)) for r in range(world)]
+    procs = [ctx.Process(target=_entry, args=(r, world, port, fn, args, errq, native)) for r in range(world)]
     for p in procs:
         p.start()
     for p in procs:
