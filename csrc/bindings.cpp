@@ -31,6 +31,7 @@ PYBIND11_MODULE(_fdt_native, m) {
   // implicit-GEMM convolution engine
   DEF(conv_igemm);
   DEF(conv_num_row_blocks);
+  DEF(conv_splitk_workspace);
   DEF(conv_wgrad);
   DEF(wgrad_reduce);
   DEF(pack_weights);

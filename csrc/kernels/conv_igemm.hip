@@ -26,6 +26,14 @@
 //                  per-channel (sum g_pre*x, sum g_pre) slabs
 //      EPI_STORE / EPI_ADD  plain bf16 store / accumulate into an existing gradient.
 //
+// Split-K (small-M layers: the 8x8 / 4x4 stages at the per-GPU batch of an 8-GPU run
+// have only 32-512 output tiles but K up to 4608): nsplit workgroups share one output tile,
+// each reducing a contiguous range of K tiles; all but the last to finish write their fp32
+// accumulators to a slab (in register order: [tile][split][reg/4][thread] float4, so the
+// reducer's thread t reads exactly its own registers' counterparts, coalesced), publish
+// with an agent-scope release + ticket; the last arriver acquires, adds the other slabs
+// and runs the normal fused epilogue.  Counters are reset by the last arriver.
+//
 // Strided convolutions: forward uses the input stride S; the dgrad of a stride-2
 // convolution is split by output parity into 4 dense classes (each its own tap table and
 // output row map: hi = ho*OS + oy), so no MFMA work is spent on structural zeros.
@@ -65,6 +73,9 @@ struct ConvArgs {
   int epi_act;
   float epi_alpha;
   int nbm, nbn;
+  int nsplit, kps;   // split-K: workgroups per output tile, K tiles per split
+  float* slab;       // split-K partials [tiles][nsplit][TN*TM*4][256] float4
+  int* cnt;          // split-K tickets [tiles], zero between launches
   int8_t dh[12], dw[12], wt[12];
   long Nb_HiWi_Cx_bytes;  // bytes of the activation operand(s)
   long w_bytes;           // bytes of the packed weights
@@ -161,7 +172,9 @@ __global__ __launch_bounds__(256) void igemm_kernel(const ConvArgs a) {
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wn = wid & 1, wm = wid >> 1;
-  const int id = xcd_remap(blockIdx.x, a.nbm * a.nbn);
+  // a tile's splits are consecutive ids -> the same XCD after the remap
+  const int rid = xcd_remap(blockIdx.x, a.nbm * a.nbn * a.nsplit);
+  const int id = rid / a.nsplit, split = rid - id * a.nsplit;
   const int bn = id % a.nbn, bm = id / a.nbn;
   const long m0 = (long)bm * BM;
   const int n0 = bn * BN;
@@ -334,28 +347,84 @@ __global__ __launch_bounds__(256) void igemm_kernel(const ConvArgs a) {
     }
   };
 
+  // this split's K tiles [kb, kb + nk)
+  const int kb = split * a.kps;
+  const int nk = min(nkt - kb, a.kps);
+
   // prologue: tile 0 -> LDS buf 0; tile 1 pending in B; tile 2 in flight in A
   Stage SA, SB;
-  if (nkt > 0) {
-    load_tile(SA, 0);
-    if (nkt > 1) load_tile(SB, 1);
+  if (nk > 0) {
+    load_tile(SA, kb);
+    if (nk > 1) load_tile(SB, kb + 1);
     store_tile(SA, 0);
-    if (nkt > 2) load_tile(SA, 2);
+    if (nk > 2) load_tile(SA, kb + 2);
     __syncthreads();
   }
-  for (int kt = 0; kt < nkt; kt += 2) {
+  for (int kt = 0; kt < nk; kt += 2) {
     // even tile kt in buf 0; SB holds kt+1, SA holds kt+2 (in flight)
     compute(0);
-    if (kt + 1 >= nkt) break;
+    if (kt + 1 >= nk) break;
     store_tile(SB, 1);
     __syncthreads();
-    if (kt + 3 < nkt) load_tile(SB, kt + 3);
+    if (kt + 3 < nk) load_tile(SB, kb + kt + 3);
     // odd tile kt+1 in buf 1; SA holds kt+2, SB holds kt+3 (in flight)
     compute(1);
-    if (kt + 2 >= nkt) break;
+    if (kt + 2 >= nk) break;
     store_tile(SA, 0);
     __syncthreads();
-    if (kt + 4 < nkt) load_tile(SA, kt + 4);
+    if (kt + 4 < nk) load_tile(SA, kb + kt + 4);
+  }
+
+  // ------------------------------------------------------------------ split-K combine
+  if (a.nsplit > 1) {
+    constexpr int NR4 = TN * TM * 4;  // float4 registers per thread
+    float4* slab = reinterpret_cast<float4*>(a.slab) + (long)id * a.nsplit * NR4 * 256;
+    {
+      float4* mine = slab + (long)split * NR4 * 256 + tid;
+#pragma unroll
+      for (int i = 0; i < TN; ++i)
+#pragma unroll
+        for (int j = 0; j < TM; ++j)
+#pragma unroll
+          for (int q = 0; q < 4; ++q)
+            mine[((i * TM + j) * 4 + q) * 256] =
+                make_float4(acc[i][j][4 * q], acc[i][j][4 * q + 1], acc[i][j][4 * q + 2], acc[i][j][4 * q + 3]);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    int* flag = reinterpret_cast<int*>(red);
+    if (tid == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      const int t = __hip_atomic_fetch_add(&a.cnt[id], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const int last = t == a.nsplit - 1;
+      if (last) {
+        __hip_atomic_store(&a.cnt[id], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      flag[0] = last;
+    }
+    __syncthreads();
+    const int last = flag[0];
+    __syncthreads();  // red is reused by the epilogue
+    if (!last) return;
+    for (int sp = 0; sp < a.nsplit; ++sp) {
+      if (sp == split) continue;
+      const float4* other = slab + (long)sp * NR4 * 256 + tid;
+#pragma unroll
+      for (int i = 0; i < TN; ++i)
+#pragma unroll
+        for (int j = 0; j < TM; ++j)
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const float4 v = other[((i * TM + j) * 4 + q) * 256];
+            acc[i][j][4 * q] += v.x;
+            acc[i][j][4 * q + 1] += v.y;
+            acc[i][j][4 * q + 2] += v.z;
+            acc[i][j][4 * q + 3] += v.w;
+          }
+    }
   }
 
   // ------------------------------------------------------------------ epilogue
@@ -521,7 +590,7 @@ static void launch_one(const ConvArgs& a, size_t lds, hipStream_t st) {
                                       (int)lds));
     attr_set = lds;
   }
-  hipLaunchKernelGGL(kern, dim3(a.nbm * a.nbn), dim3(256), lds, st, a);
+  hipLaunchKernelGGL(kern, dim3(a.nbm * a.nbn * a.nsplit), dim3(256), lds, st, a);
   FDT_LAUNCH_CHECK();
 }
 
@@ -551,7 +620,7 @@ void conv_igemm(uint64_t x, uint64_t x2, uint64_t ps, uint64_t pt, uint64_t w, u
                 uint64_t ex, uint64_t es, uint64_t et, long Nb, int Hi, int Wi, int Cx, int Ho, int Wo, int S,
                 const std::vector<int>& dh, const std::vector<int>& dw, const std::vector<int>& wt, int Cout, int ldw,
                 int Hout, int Wout, int OS, int oy, int ox, int pro, int pro_act, float pro_alpha, int epi, int epi_act,
-                float epi_alpha, int BM, int BN, int BK, uint64_t stream) {
+                float epi_alpha, int BM, int BN, int BK, int nsplit, uint64_t slab, uint64_t cnt, uint64_t stream) {
   using namespace conv;
   ConvArgs a{};
   a.x = P<const bf16>(x);
@@ -589,6 +658,16 @@ void conv_igemm(uint64_t x, uint64_t x2, uint64_t ps, uint64_t pt, uint64_t w, u
             "conv operand exceeds the 2 GiB buffer-descriptor range");
   a.nbm = (int)((a.M + BM - 1) / BM);
   a.nbn = Cout / BN;
+  {
+    const int nkt = (a.K + BK - 1) / BK;
+    if (nsplit < 1 || nkt <= 1) nsplit = 1;
+    if (nsplit > nkt && nkt >= 1) nsplit = nkt;
+    a.kps = nsplit == 1 ? (nkt > 1 ? nkt : 1) : (nkt + nsplit - 1) / nsplit;
+    a.nsplit = nsplit == 1 ? 1 : (nkt + a.kps - 1) / a.kps;  // no empty splits
+    a.slab = P<float>(slab);
+    a.cnt = P<int>(cnt);
+    FDT_CHECK(a.nsplit == 1 || (slab != 0 && cnt != 0), "split-K needs a slab and a zeroed ticket buffer");
+  }
   const bool pure = a.ntaps == 1 && dh[0] == 0 && dw[0] == 0 && wt[0] == 0 && S == 1 && Hi == Ho && Wi == Wo;
   hipStream_t st = as_stream(stream);
   if (a.M == 0) return;
@@ -614,5 +693,11 @@ void conv_igemm(uint64_t x, uint64_t x2, uint64_t ps, uint64_t pt, uint64_t w, u
 }
 
 int conv_num_row_blocks(long M, int BM) { return (int)((M + BM - 1) / BM); }
+
+// split-K workspace sizes for a launch: (slab floats, ticket ints)
+std::vector<long> conv_splitk_workspace(long M, int Cout, int BM, int BN, int nsplit) {
+  const long tiles = ((M + BM - 1) / BM) * (long)(Cout / BN);
+  return {tiles * nsplit * (BM / 64) * (BN / 64) * 16L * 256L, tiles};
+}
 
 }  // namespace fdt

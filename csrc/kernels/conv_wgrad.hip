@@ -363,7 +363,17 @@ struct PackTable {
   int n;
 };
 
+// One workgroup packs a 32 (co) x 64 (ci) x ntaps block: coalesced fp32 reads of the
+// OIHW source (ci, tap contiguous per co), a bf16 LDS image [co][tap][ci] (row stride
+// 66 elements: the co-strided reads of the dgrad pass hit distinct banks), then coalesced
+// row writes of both layouts (wf rows: 64 ci = 128 B; wd rows: 32 co = 64 B).
+constexpr int kPackCo = 32;
+constexpr int kPackT = 64;  // ci per block
+constexpr int kPackLd = kPackT + 2;
+constexpr int kPackMaxTaps = 9;
+
 __global__ __launch_bounds__(256) void pack_weights_kernel(const PackTable tab) {
+  __shared__ bf16 img[kPackCo * kPackMaxTaps * kPackLd];
   // binary search the entry of this block
   int lo = 0, hi = tab.n - 1;
   while (lo < hi) {
@@ -371,18 +381,42 @@ __global__ __launch_bounds__(256) void pack_weights_kernel(const PackTable tab) 
     if (tab.e[mid].blk0 <= (long)blockIdx.x) lo = mid; else hi = mid - 1;
   }
   const PackEntry& E = tab.e[lo];
-  const long nf = (long)E.Cout * E.ntaps * E.Cxp;
-  const long i = ((long)blockIdx.x - E.blk0) * 256 + threadIdx.x;
-  if (i >= nf) return;
-  // forward layout element i = (co, t, ci')
-  const int ci = (int)(i % E.Cxp);
-  const long r = i / E.Cxp;
-  const int t = (int)(r % E.ntaps);
-  const int co = (int)(r / E.ntaps);
-  float v = 0.f;
-  if (ci < E.Cin) v = E.src[((long)co * E.Cin + ci) * E.ntaps + t];
-  E.wf[i] = __float2bfloat16(v);
-  if (E.wd != nullptr && ci < E.Cin) E.wd[((long)ci * E.ntaps + t) * E.Cout + co] = __float2bfloat16(v);
+  const int T = E.ntaps;
+  const int nci = (E.Cxp + kPackT - 1) / kPackT;
+  const int b = (int)((long)blockIdx.x - E.blk0);
+  const int co0 = (b / nci) * kPackCo, ci0 = (b % nci) * kPackT;
+  const int tid = threadIdx.x;
+  const int nco = min(kPackCo, E.Cout - co0);
+  const int nci_v = min(kPackT, E.Cxp - ci0);   // columns of the (padded) forward layout
+  const int nci_s = max(0, min(kPackT, E.Cin - ci0));  // columns present in the source
+  // load: for each co row the source run [ci0, ci0 + nci_s) x T is contiguous
+  const int run = kPackT * T;
+  for (int e = tid; e < nco * run; e += 256) {
+    const int col = e / run, rem = e - col * run;
+    const int cl = rem / T, t = rem - cl * T;
+    float v = 0.f;
+    if (cl < nci_s) v = E.src[((long)(co0 + col) * E.Cin + ci0 + cl) * T + t];
+    img[(col * T + t) * kPackLd + cl] = __float2bfloat16(v);
+  }
+  __syncthreads();
+  // forward layout wf[co][t][ci] (Cxp-padded rows): ci fastest
+  for (int e = tid; e < nco * T * kPackT; e += 256) {
+    const int cl = e % kPackT, r = e / kPackT;  // r = col * T + t
+    if (cl < nci_v) {
+      const int col = r / T, t = r - col * T;
+      E.wf[((long)(co0 + col) * T + t) * E.Cxp + ci0 + cl] = img[r * kPackLd + cl];
+    }
+  }
+  // dgrad layout wd[ci][t][co]: co fastest
+  if (E.wd != nullptr) {
+    for (int e = tid; e < nci_s * T * kPackCo; e += 256) {
+      const int col = e % kPackCo, r = e / kPackCo;  // r = cl * T + t
+      if (col < nco) {
+        const int cl = r / T, t = r - cl * T;
+        E.wd[((long)(ci0 + cl) * T + t) * E.Cout + co0 + col] = img[(col * T + t) * kPackLd + cl];
+      }
+    }
+  }
 }
 
 }  // namespace wg
@@ -488,7 +522,8 @@ void pack_weights(const std::vector<uint64_t>& src, const std::vector<uint64_t>&
       E.wd = P<bf16>(wd[i]);
       E.Cout = cout[i]; E.Cin = cin[i]; E.Cxp = cxp[i]; E.ntaps = ntaps[i];
       E.blk0 = blk;
-      blk += ((long)E.Cout * E.ntaps * E.Cxp + 255) / 256;
+      FDT_CHECK(E.ntaps <= kPackMaxTaps, "pack_weights: at most 3x3 kernels");
+      blk += (long)((E.Cout + kPackCo - 1) / kPackCo) * ((E.Cxp + kPackT - 1) / kPackT);
     }
     tab.n = k;
     if (blk == 0) continue;

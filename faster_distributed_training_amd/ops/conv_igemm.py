@@ -111,6 +111,45 @@ def tuned(op: str, batch: int, h: int, shp):
     return ent
 
 
+# ---------------------------------------------------------------- split-K
+SPLITK = os.environ.get("FDT_SPLITK", "1") != "0"
+_SPLITK_WS: dict = {}
+
+
+def splitk_heuristic(tiles: int, nkt: int, want: int = 512, min_kt: int = 4, cap: int = 8) -> int:
+    """Workgroups per output tile for small-M convolutions: enough to put ~2 workgroups on
+    each of the 256 CUs, each split still reducing >= min_kt K tiles."""
+    if not SPLITK or tiles >= want * 3 // 4:
+        return 1
+    ns = -(-want // max(tiles, 1))
+    return max(1, min(ns, nkt // min_kt, cap))
+
+
+def splitk_workspace(dev, slab_floats: int, tiles: int):
+    """Persistent (slab, tickets) for split-K launches on ``dev``; tickets are zero between
+    launches (each tile's last arriver resets its ticket)."""
+    ws = _SPLITK_WS.get(dev)
+    if ws is None or ws[0].numel() < slab_floats or ws[1].numel() < tiles:
+        slab = torch.empty(max(slab_floats, ws[0].numel() if ws else 0), device=dev, dtype=torch.float32)
+        cnt = torch.zeros(max(tiles, ws[1].numel() if ws else 0, 4096), device=dev, dtype=torch.int32)
+        ws = _SPLITK_WS[dev] = (slab, cnt)
+    return ws
+
+
+def _splitk_args(ent, M, N, K, bm, bn, bk, dev):
+    """(nsplit, slab ptr, ticket ptr) for one launch: tuned entry's nsplit, else heuristic."""
+    tiles = -(-M // bm) * (N // bn)
+    nkt = -(-K // bk)
+    ns = int(ent.get("nsplit", 0)) if ent else 0
+    if ns <= 0:
+        ns = splitk_heuristic(tiles, nkt)
+    ns = max(1, min(ns, nkt))
+    if ns == 1:
+        return 1, 0, 0
+    slab, cnt = splitk_workspace(dev, tiles * ns * (bm // 64) * (bn // 64) * 16 * 256, tiles)
+    return ns, slab.data_ptr(), cnt.data_ptr()
+
+
 def _tile3(tile, M, N):
     if tile is None:
         return pick_tile(M, N)
@@ -149,7 +188,7 @@ def stat_slots(nq: int, C: int, device) -> torch.Tensor:
     return torch.zeros(STAT_SLOTS, nq, C, device=device, dtype=torch.float32)
 
 
-def conv_fwd(x, wf, shp: ConvShape, s=None, t=None, act=0, alpha=1.0, tile=None, part=None):
+def conv_fwd(x, wf, shp: ConvShape, s=None, t=None, act=0, alpha=1.0, tile=None, part=None, nsplit=None):
     """y = conv(act(x*s+t)) (or conv(x) when s is None and act == 0); returns
     (y [N,Ho,Wo,Cout] bf16, part [STAT_SLOTS,2,Cout] fp32 slots whose row sum is
     (sum y, sum y^2)).  ``part``: a zeroed slot buffer to accumulate into."""
@@ -159,10 +198,14 @@ def conv_fwd(x, wf, shp: ConvShape, s=None, t=None, act=0, alpha=1.0, tile=None,
     Ho, Wo = out_hw(H, W, shp)
     M = N * Ho * Wo
     pro = PRO_AFFINE_ACT if (s is not None or act != 0) else PRO_NONE
+    ent = None
     if tile is None:
         ent = tuned(f"fwd{pro}", N, H, shp) or tuned("fwd", N, H, shp)
         tile = tuple(ent["tile"]) if ent else None
     bm, bn, bk = _tile3(tile, M, shp.cout)
+    if nsplit is not None:
+        ent = {"nsplit": nsplit}
+    ns, slab_p, cnt_p = _splitk_args(ent, M, shp.cout, shp.ntaps * C, bm, bn, bk, x.device)
     y = torch.empty(N, Ho, Wo, shp.cout, device=x.device, dtype=torch.bfloat16)
     if part is None:
         part = stat_slots(2, shp.cout, x.device)
@@ -172,12 +215,13 @@ def conv_fwd(x, wf, shp: ConvShape, s=None, t=None, act=0, alpha=1.0, tile=None,
         t = torch.zeros(C, device=x.device, dtype=torch.float32)
     nat.conv_igemm(x.data_ptr(), 0, _p(s), _p(t), wf.data_ptr(), y.data_ptr(), part.data_ptr(), 0, 0, 0,
                    N, H, W, C, Ho, Wo, shp.stride, list(dh), list(dw), list(wt), shp.cout, shp.ntaps * shp.cxp,
-                   Ho, Wo, 1, 0, 0, pro, int(act), float(alpha), EPI_STATS, 0, 1.0, bm, bn, bk, _sp())
+                   Ho, Wo, 1, 0, 0, pro, int(act), float(alpha), EPI_STATS, 0, 1.0, bm, bn, bk, ns, slab_p, cnt_p,
+                   _sp())
     return y, part
 
 
 def conv_dgrad(g, y, al, be, wd, shp: ConvShape, x_shape, epi=EPI_STORE, out=None, ex=None, es=None, et=None,
-               act=0, alpha=1.0, tile=None, part=None):
+               act=0, alpha=1.0, tile=None, part=None, nsplit=None):
     """Data gradient of y = conv(a): dA = conv^T(g + al + be*y).
 
     epi: EPI_STORE -> write dA; EPI_ADD -> out += dA; EPI_ACTBWD -> through the lazy
@@ -193,11 +237,14 @@ def conv_dgrad(g, y, al, be, wd, shp: ConvShape, x_shape, epi=EPI_STORE, out=Non
         out = torch.empty(N, Hx, Wx, shp.cin, device=g.device, dtype=torch.bfloat16)
     if epi == EPI_ACTBWD and part is None:
         part = stat_slots(2, shp.cin, g.device)
+    ent = None
     if tile is None:
         pro = PRO_FOLD if al is not None else PRO_NONE
         e = EPI_STORE if epi == EPI_ADD else epi
         ent = tuned(f"dgrad{pro}{e}", N, Hx, shp) or tuned("dgrad", N, Hx, shp)
         tile = tuple(ent["tile"]) if ent else None
+    if nsplit is not None:
+        ent = {"nsplit": nsplit}
     classes = dgrad_classes(shp.k, shp.stride, shp.pad)
     for (py, px, dh, dw, wt) in classes:
         Ha = (Hx - py + shp.stride - 1) // shp.stride
@@ -206,11 +253,12 @@ def conv_dgrad(g, y, al, be, wd, shp: ConvShape, x_shape, epi=EPI_STORE, out=Non
         if len(dh) == 0 and epi == EPI_ADD:
             continue
         bm, bn, bk = _tile3(tile, M, shp.cin)
+        ns, slab_p, cnt_p = _splitk_args(ent, M, shp.cin, len(dh) * Cy, bm, bn, bk, g.device)
         pro = PRO_FOLD if al is not None else PRO_NONE  # al None: g is already folded
         nat.conv_igemm(g.data_ptr(), _p(y) if pro == PRO_FOLD else 0, _p(al), _p(be), wd.data_ptr(), out.data_ptr(),
-                       _p(part) if epi == EPI_ACTBWD else 0, _p(ex), _p(es), _p(et), N, Hy, Wy, Cy, Ha, Wa, 1, list(dh), list(dw), list(wt),
-                       shp.cin, shp.ntaps * shp.cout, Hx, Wx, shp.stride, py, px, pro, 0, 1.0, epi, int(act),
-                       float(alpha), bm, bn, bk, _sp())
+                       _p(part) if epi == EPI_ACTBWD else 0, _p(ex), _p(es), _p(et), N, Hy, Wy, Cy, Ha, Wa, 1,
+                       list(dh), list(dw), list(wt), shp.cin, shp.ntaps * shp.cout, Hx, Wx, shp.stride, py, px, pro, 0, 1.0, epi, int(act),
+                       float(alpha), bm, bn, bk, ns, slab_p, cnt_p, _sp())
     return out, (part if epi == EPI_ACTBWD else None)
 
 

@@ -11,6 +11,9 @@ X2-X4) with a reducer designed around the flat gradient buffer (``utils/flat.py`
   RCCL on ROCm), so communication overlaps the rest of backward;
 * ``finish()`` (call after ``backward``) launches any bucket left (unused params) and
   makes the compute stream wait on RCCL — no host blocking on GPU;
+* with the ResNet engine running its backward as captured HIP graphs, the engine cuts the
+  graph where a bucket completes and launches that bucket's all-reduce between segments
+  (``_hook(p, defer=True)``), so overlap survives graph replay;
 * averaging uses ``ReduceOp.AVG`` on RCCL (no extra scaling pass), ``SUM`` + scale on
   gloo; optional bf16 wire format halves bytes on xGMI.
 
@@ -102,13 +105,18 @@ class BucketReducer:
             self.broadcast_parameters()
 
     # ------------------------------------------------------------------ hooks
-    def _hook(self, p):
+    def _hook(self, p, defer=False):
+        """Gradient of ``p`` is final.  ``defer`` (the engine is capturing its backward into
+        HIP graphs): do the bookkeeping, return the launch as a callable instead."""
         if not self.enabled:
-            return
+            return None
         b = self.bucket_of[id(p)]
         self.pending[b] -= 1
         if self.pending[b] == 0:
+            if defer:
+                return lambda: self._launch(b)
             self._launch(b)
+        return None
 
     def _launch(self, b):
         if self.works[b] is not None:

@@ -66,12 +66,14 @@ class ResNetConfig:
     plot: bool = True
     workers: int = 2                   # accepted for CLI parity (no worker processes needed)
     fast_path: bool | None = None      # None = HIP engine when on GPU
+    graphs: bool = True                # run the engine body as captured HIP graphs (train steps)
     extra: dict = field(default_factory=dict)
 
 
 def build_model(cfg: ResNetConfig, device):
     model = getattr(resnet_models, cfg.arch)(cfg.num_classes)
     model.fast_path = cfg.fast_path
+    model.graph_engine = cfg.graphs
     return model.to(device)
 
 

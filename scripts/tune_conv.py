@@ -32,6 +32,9 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--batches", type=int, nargs="+", default=[1024, 128])
     ap.add_argument("--reps", type=int, default=10)
+    ap.add_argument("--max-m", type=int, default=0, help="only shapes with N*Ho*Wo <= this (0 = all)")
+    ap.add_argument("--splits", type=int, nargs="+", default=[1, 2, 4, 8],
+                    help="split-K candidates for fwd/dgrad when the tile grid is small")
     ap.add_argument("--out", default=os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
                                                   "faster_distributed_training_amd", "ops", "conv_tuned.json"))
     a = ap.parse_args()
@@ -43,6 +46,9 @@ def main():
     for N in a.batches:
         for (H, Cin, Cout, k, s, p, _cnt) in SHAPES:
             shp = ci.ConvShape(Cin, Cout, k, s, p)
+            Ho0, Wo0 = ci.out_hw(H, H, shp)
+            if a.max_m and N * Ho0 * Wo0 > a.max_m:
+                continue
             torch.manual_seed(0)
             x = torch.randn(N, H, H, shp.cxp, device=dev).to(torch.bfloat16)
             w = torch.randn(Cout, Cin, k, k, device=dev) / (Cin * k * k) ** 0.5
@@ -62,31 +68,35 @@ def main():
             key = ci.tune_key(N, H, shp)
             res = {}
 
-            def sweep(name, fn, tiles, legal):
+            prev = table.get(key, {})
+
+            def sweep(name, fn, tiles, legal, M, Nn):
                 best = None
                 for t in tiles:
                     if not legal(t):
                         continue
-                    ms = timeit(lambda: fn(t), a.reps)
-                    if best is None or ms < best[0]:
-                        best = (ms, t)
-                res[name] = dict(tile=best[1], us=round(best[0] * 1e3, 1))
+                    ntiles = -(-M // t[0]) * (Nn // t[1])
+                    for ns in (a.splits if ntiles < 768 else [1]):
+                        ms = timeit(lambda: fn(t, ns), a.reps)
+                        if best is None or ms < best[0]:
+                            best = (ms, t, ns)
+                res[name] = dict(tile=best[1], nsplit=best[2], us=round(best[0] * 1e3, 1))
 
             # modes the fused engine actually launches (ops/resnet_fused.py): 3x3 convs get a
             # materialised input / pre-folded gradient; 1x1 convs fuse the transforms
             fwd_modes = [0] if k > 1 else [0, 1]
             for pro in fwd_modes:
-                sweep(f"fwd{pro}", lambda t: ci.conv_fwd(x, wf, shp, sv if pro else None, tv if pro else None,
-                                                          pro, 1.0, tile=t),
-                      FWD_TILES, lambda t: Cout % t[1] == 0)
+                sweep(f"fwd{pro}", lambda t, ns: ci.conv_fwd(x, wf, shp, sv if pro else None, tv if pro else None,
+                                                              pro, 1.0, tile=t, nsplit=ns),
+                      FWD_TILES, lambda t: Cout % t[1] == 0, N * Ho * Wo, Cout)
             if Cin >= 8:
                 dg = [(0, ci.EPI_ACTBWD)] if k > 1 else [(2, ci.EPI_ACTBWD), (2, ci.EPI_STORE)]
                 for pro, epi in dg:
                     sweep(f"dgrad{pro}{epi}",
-                          lambda t: ci.conv_dgrad(g, yy if pro else None, al if pro else None, be if pro else None,
-                                                  wd, shp, (N, H, H, Cin), epi=epi, ex=ex, es=es, et=et, act=1,
-                                                  tile=t),
-                          FWD_TILES, lambda t: Cin % t[1] == 0)
+                          lambda t, ns: ci.conv_dgrad(g, yy if pro else None, al if pro else None,
+                                                      be if pro else None, wd, shp, (N, H, H, Cin), epi=epi, ex=ex,
+                                                      es=es, et=et, act=1, tile=t, nsplit=ns),
+                          FWD_TILES, lambda t: Cin % t[1] == 0, N * H * H // (s * s), Cin)
             ldw = shp.ntaps * shp.cxp
             slab = torch.empty(1024 * Cout * ldw // 4 + 1, device=dev)
             wg_modes = [(0, 0)] if k > 1 else [(1, 1), (1, 0)]
@@ -109,7 +119,8 @@ def main():
                         if best is None or ms < best[0]:
                             best = (ms, t, ns)
                 res[f"wgrad{fold}{xaff}"] = dict(tile=best[1], nsplit=best[2], us=round(best[0] * 1e3, 1))
-            table[key] = res
+            prev.update(res)
+            table[key] = prev
             print(key, json.dumps(res), flush=True)
             del x, g, yy, ex, slab
             torch.cuda.empty_cache()

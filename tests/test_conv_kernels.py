@@ -73,10 +73,11 @@ def test_conv_fwd(cuda, case, mode):
         t = torch.randn(shp.cxp, device=cuda) * 0.3
         act, alpha = (1, 1.0) if mode == "relu" else (2, 0.075)
         a = act_ref(x.float() * s + t, act, alpha).to(BF).float()[..., :Cin]
-    for tile in [None, (64, 64, 64), (128, 64, 32), (256, 128, 32), (256, 64, 64)]:
+    for tile, ns in [(None, None), ((64, 64, 64), 1), ((64, 64, 64), 3), ((128, 64, 32), None),
+                     ((128, 128, 64), 2), ((256, 128, 32), None), ((256, 64, 64), 1)]:
         if tile and Cout % tile[1]:
             continue
-        y, part = ci.conv_fwd(x, wf, shp, s, t, act, alpha, tile=tile)
+        y, part = ci.conv_fwd(x, wf, shp, s, t, act, alpha, tile=tile, nsplit=ns)
         ref = nhwc(F.conv2d(nchw(a), w.to(BF).float(), stride=stride, padding=pad))
         assert rel(y, ref) < 1e-2, (tile, rel(y, ref))
         ps = part.sum(0)
@@ -112,25 +113,28 @@ def test_conv_dgrad(cuda, case, epi):
     ref = nhwc(torch.nn.grad.conv2d_input((N, Cin, H, H), w.to(BF).float(), nchw(gt), stride=stride, padding=pad))
     xs = (N, H, H, Cin)
     if epi == "store":
-        for tile in [None, (64, 64, 32), (128, 64, 64)]:
-            out, _ = ci.conv_dgrad(g, y, al, be, wd, shp, xs, epi=ci.EPI_STORE, tile=tile)
-            assert rel(out, ref) < 1e-2, tile
+        for tile, ns in [(None, None), ((64, 64, 32), 1), ((64, 64, 32), 4), ((128, 64, 64), 2)]:
+            out, _ = ci.conv_dgrad(g, y, al, be, wd, shp, xs, epi=ci.EPI_STORE, tile=tile, nsplit=ns)
+            assert rel(out, ref) < 1e-2, (tile, ns)
     elif epi == "add":
         prev = make(xs, cuda)
-        out = prev.clone()
-        ci.conv_dgrad(g, y, al, be, wd, shp, xs, epi=ci.EPI_ADD, out=out)
-        assert rel(out, ref + prev.float()) < 1e-2
+        for ns in (1, 3):
+            out = prev.clone()
+            ci.conv_dgrad(g, y, al, be, wd, shp, xs, epi=ci.EPI_ADD, out=out, nsplit=ns)
+            assert rel(out, ref + prev.float()) < 1e-2, ns
     else:
         ex = make(xs, cuda)
         es = torch.rand(Cin, device=cuda) + 0.5
         et = torch.randn(Cin, device=cuda) * 0.3
         z = ex.float() * es + et
         gp = ref * (z > 0).float()
-        out, part = ci.conv_dgrad(g, y, al, be, wd, shp, xs, epi=ci.EPI_ACTBWD, ex=ex, es=es, et=et, act=1)
-        assert rel(out, gp * es) < 1e-2
-        ps = part.sum(0)
-        assert rel(ps[0], (gp * ex.float()).reshape(-1, Cin).sum(0)) < 1e-2
-        assert rel(ps[1], gp.reshape(-1, Cin).sum(0)) < 1e-2
+        for ns in (1, 4):
+            out, part = ci.conv_dgrad(g, y, al, be, wd, shp, xs, epi=ci.EPI_ACTBWD, ex=ex, es=es, et=et, act=1,
+                                      nsplit=ns)
+            assert rel(out, gp * es) < 1e-2, ns
+            ps = part.sum(0)
+            assert rel(ps[0], (gp * ex.float()).reshape(-1, Cin).sum(0)) < 1e-2
+            assert rel(ps[1], gp.reshape(-1, Cin).sum(0)) < 1e-2
 
 
 WGRAD_CASES = [
@@ -173,3 +177,19 @@ def test_conv_wgrad(cuda, case, mode):
         out = torch.empty(Cout, Cin, k, k, device=cuda)
         ci.conv_wgrad(g, y, al, be, x, shp, out, xs, xt, act, nsplit=ns, tile=tile)
         assert rel(out, ref) < 5e-3, (ns, tile, rel(out, ref))
+
+
+@pytest.mark.parametrize("cout,cin,k", [(64, 3, 3), (256, 64, 1), (512, 512, 3), (48, 72, 3), (2048, 512, 1)])
+def test_pack_weights_layouts(cuda, cout, cin, k):
+    """fp32 OIHW -> bf16 forward layout [Cout][taps][Cxp] (zero channel padding) and dgrad
+    layout [Cin][taps][Cout], against torch permutes."""
+    shp = ci.ConvShape(cin, cout, k, 1, k // 2)
+    w = torch.randn(cout, cin, k, k, device=cuda)
+    wf, wd = ci.alloc_packed(shp, cuda, dgrad=True)
+    ci.pack_weights([(w, wf, wd, shp)])
+    wb = w.to(BF)
+    ref_f = torch.zeros(cout, k * k, shp.cxp, device=cuda, dtype=BF)
+    ref_f[:, :, :cin] = wb.permute(0, 2, 3, 1).reshape(cout, k * k, cin)
+    assert torch.equal(wf.view(cout, k * k, shp.cxp), ref_f)
+    ref_d = wb.permute(1, 2, 3, 0).reshape(cin, k * k, cout)
+    assert torch.equal(wd.view(cin, k * k, cout)[:cin], ref_d)

@@ -66,3 +66,37 @@ def _worker(rank, world):
 
 def test_ddp_engine_two_ranks_one_gpu(cuda):
     run_world(_worker, world=2, native=True, timeout=400)
+
+
+def _graph_worker(rank, world):
+    import torch.distributed as dist
+    from faster_distributed_training_amd.models import resnet as R
+    from faster_distributed_training_amd.parallel.ddp import BucketReducer
+    from faster_distributed_training_amd.utils.flat import FlatParams
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    torch.manual_seed(rank)
+    m = R.resnet50(10).to(dev)
+    m.fast_path = True
+    m.graph_engine = True
+    flat = FlatParams(m, device=dev)
+    red = BucketReducer(flat, m, bucket_mb=4.0, first_bucket_mb=0.5)
+    x, y = _batch(rank)
+    for it in range(4):
+        flat.grad.zero_()
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            out = m(x.to(dev))
+        F.cross_entropy(out.float(), y.to(dev)).backward()
+        assert all(w is not None for w in red.works), (it, "bucket not launched")
+        red.finish()
+        assert torch.isfinite(flat.grad).all()
+        chk = torch.tensor([flat.grad.double().sum().item()])
+        alls = [torch.zeros_like(chk) for _ in range(world)]
+        dist.all_gather(alls, chk)
+        assert all(torch.equal(alls[0], t) for t in alls), it
+    st = list(m._plan._graphs.values())[0]
+    assert st.stage == "ready" and len(st.segments) > 2  # backward cut at bucket boundaries
+
+
+def test_ddp_engine_hip_graphs_two_ranks(cuda):
+    run_world(_graph_worker, world=2, native=True, timeout=400)
