@@ -35,13 +35,16 @@ def main():
     ap.add_argument("--max-m", type=int, default=0, help="only shapes with N*Ho*Wo <= this (0 = all)")
     ap.add_argument("--splits", type=int, nargs="+", default=[1, 2, 4, 8],
                     help="split-K candidates for fwd/dgrad when the tile grid is small")
+    ap.add_argument("--base", default=None, help="table to start from (default: --out if it exists, else the "
+                                                 "in-tree table)")
     ap.add_argument("--out", default=os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
                                                   "faster_distributed_training_amd", "ops", "conv_tuned.json"))
     a = ap.parse_args()
     dev = torch.device("cuda")
     table = {}
-    if os.path.exists(a.out):
-        with open(a.out) as f:
+    base = a.base or (a.out if os.path.exists(a.out) else ci._TUNED_PATH)
+    if os.path.exists(base):
+        with open(base) as f:
             table = json.load(f)
     for N in a.batches:
         for (H, Cin, Cout, k, s, p, _cnt) in SHAPES:
