@@ -234,25 +234,30 @@ __global__ __launch_bounds__(256) void igemm_kernel(const ConvArgs a) {
     int kci;
   };
 
-  auto load_tile = [&](Stage& S, int kt) {
+  // Loads are issued unconditionally (a K tile past this split's range, or past K, reads
+  // the OOB offset and returns zeros): no branch around a load, so hipcc's waitcnt pass
+  // can count the two in-flight stages exactly (vmcnt(N), not vmcnt(0)) -- a branch-guarded
+  // prefetch degenerates to a full-latency wait every K tile.
+  auto load_tile = [&](Stage& S, int kt, bool live) {
     const int k = kt * BK + cc * 8;
     const int tap = k >> a.log2Cx;
     const int ci = k & (a.Cx - 1);
     S.kci = ci;
-    const bool tok = tap < a.ntaps;
+    const bool tok = live && tap < a.ntaps;
     int dh = 0, dw = 0, wt = 0, toff = 0;
-    if (!PURE && tok) {
-      const int e = tapw[tap];
+    if constexpr (!PURE) {
+      const int tq = tap < 12 ? tap : 11;  // branch-free LDS lookup (masked by tok below)
+      const int e = tapw[tq];
       dh = (int)(int8_t)(e & 0xff);
       dw = (int)(int8_t)((e >> 8) & 0xff);
       wt = (e >> 16) & 0xff;
-      toff = tapt[tap];
+      toff = tapt[tq];
     }
 #pragma unroll
     for (int j = 0; j < NXL; ++j) {
-      bool v = rv[j] && tok;
+      bool v = rv[j] & tok;  // bitwise: no short-circuit branch around the load
       if constexpr (!PURE)
-        v = v && (unsigned)(ohs[j] + dh) < (unsigned)a.Hi && (unsigned)(ows[j] + dw) < (unsigned)a.Wi;
+        v = v & ((unsigned)(ohs[j] + dh) < (unsigned)a.Hi) & ((unsigned)(ows[j] + dw) < (unsigned)a.Wi);
       S.xv[j] = v;
       const uint32_t off = v ? (((uint32_t)(pixb[j] + toff) << a.log2Cx) + ci) * 2u : kOOB;
       S.rx[j] = ld_buf16(rx_d, off);
@@ -354,10 +359,13 @@ __global__ __launch_bounds__(256) void igemm_kernel(const ConvArgs a) {
   // prologue: tile 0 -> LDS buf 0; tile 1 pending in B; tile 2 in flight in A
   Stage SA, SB;
   if (nk > 0) {
-    load_tile(SA, kb);
-    if (nk > 1) load_tile(SB, kb + 1);
+    load_tile(SA, kb, true);
+    __builtin_amdgcn_sched_barrier(0);  // issue order SA, SB, SA' pinned (exact vmcnt counting)
+    load_tile(SB, kb + 1, nk > 1);
+    __builtin_amdgcn_sched_barrier(0);
     store_tile(SA, 0);
-    if (nk > 2) load_tile(SA, kb + 2);
+    load_tile(SA, kb + 2, nk > 2);
+    __builtin_amdgcn_sched_barrier(0);
     __syncthreads();
   }
   for (int kt = 0; kt < nk; kt += 2) {
@@ -366,13 +374,15 @@ __global__ __launch_bounds__(256) void igemm_kernel(const ConvArgs a) {
     if (kt + 1 >= nk) break;
     store_tile(SB, 1);
     __syncthreads();
-    if (kt + 3 < nk) load_tile(SB, kb + kt + 3);
+    load_tile(SB, kb + kt + 3, kt + 3 < nk);
+    __builtin_amdgcn_sched_barrier(0);  // keep the prefetch issued ahead of the MFMAs
     // odd tile kt+1 in buf 1; SA holds kt+2, SB holds kt+3 (in flight)
     compute(1);
     if (kt + 2 >= nk) break;
     store_tile(SA, 0);
     __syncthreads();
-    if (kt + 4 < nk) load_tile(SA, kb + kt + 4);
+    load_tile(SA, kb + kt + 4, kt + 4 < nk);
+    __builtin_amdgcn_sched_barrier(0);
   }
 
   // ------------------------------------------------------------------ split-K combine

@@ -146,6 +146,8 @@ __global__ __launch_bounds__(256) void wgrad_kernel(const WgArgs a) {
     bool xv[NX];
   };
 
+  // Unconditional issue (a tile past the split end reads the OOB offset -> zeros): no branch
+  // around a load, so hipcc counts the two in-flight stages exactly (vmcnt(N), not 0).
   auto load_tile = [&](Stage& S, int pt) {
 #pragma unroll
     for (int j = 0; j < NG; ++j) {
@@ -157,7 +159,7 @@ __global__ __launch_bounds__(256) void wgrad_kernel(const WgArgs a) {
 #pragma unroll
     for (int j = 0; j < NX; ++j) {
       const int p = pt + tid / XC + j * XR;
-      bool v = xtok && p < p_end;
+      bool v = xtok & (p < p_end);  // bitwise: no short-circuit branch around the load
       uint32_t pix;
       if constexpr (ADDR == 0) {
         pix = (uint32_t)p;
@@ -174,7 +176,7 @@ __global__ __launch_bounds__(256) void wgrad_kernel(const WgArgs a) {
           ow = rem - oh * a.Wo;
         }
         const int ih = oh * a.S + xdh, iw = ow * a.S + xdw;
-        v = v && (unsigned)ih < (unsigned)a.Hi && (unsigned)iw < (unsigned)a.Wi;
+        v = v & ((unsigned)ih < (unsigned)a.Hi) & ((unsigned)iw < (unsigned)a.Wi);
         pix = (uint32_t)((n * a.Hi + oh * a.S) * a.Wi + ow * a.S + xtoff);
       }
       S.xv[j] = v;
@@ -271,9 +273,12 @@ __global__ __launch_bounds__(256) void wgrad_kernel(const WgArgs a) {
   Stage SA, SB;
   if (nkt > 0) {
     load_tile(SA, p_begin);
-    if (nkt > 1) load_tile(SB, p_begin + BK);
+    __builtin_amdgcn_sched_barrier(0);  // issue order SA, SB, SA' pinned (exact vmcnt counting)
+    load_tile(SB, p_begin + BK);
+    __builtin_amdgcn_sched_barrier(0);
     store_tile(SA, 0);
-    if (nkt > 2) load_tile(SA, p_begin + 2 * BK);
+    load_tile(SA, p_begin + 2 * BK);
+    __builtin_amdgcn_sched_barrier(0);
     __syncthreads();
   }
   for (int kt = 0; kt < nkt; kt += 2) {
@@ -281,12 +286,14 @@ __global__ __launch_bounds__(256) void wgrad_kernel(const WgArgs a) {
     if (kt + 1 >= nkt) break;
     store_tile(SB, 1);
     __syncthreads();
-    if (kt + 3 < nkt) load_tile(SB, p_begin + (kt + 3) * BK);
+    load_tile(SB, p_begin + (kt + 3) * BK);
+    __builtin_amdgcn_sched_barrier(0);  // keep the prefetch issued ahead of the MFMAs
     compute(1);
     if (kt + 2 >= nkt) break;
     store_tile(SA, 0);
     __syncthreads();
-    if (kt + 4 < nkt) load_tile(SA, p_begin + (kt + 4) * BK);
+    load_tile(SA, p_begin + (kt + 4) * BK);
+    __builtin_amdgcn_sched_barrier(0);
   }
 
   // epilogue: C[co][k]: lane column k = lane&31, rows co = (r&3) + 8(r>>2) + 4h
