@@ -27,12 +27,12 @@ void stats_bwd_finalize(uint64_t part, int nb, int nq, int C, int a_mode, float 
                         uint64_t a_gb, int b_mode, float b_eps, double b_count, uint64_t b_sm, uint64_t b_sa,
                         uint64_t b_gamma, uint64_t b_alpha, uint64_t b_beta, uint64_t b_gg, uint64_t b_gb,
                         uint64_t stream);
-void affine_fold(uint64_t gy, uint64_t y, uint64_t alpha, uint64_t beta, uint64_t out, long M, int C, int dt,
-                 uint64_t stream);
+void affine_fold(uint64_t gy, uint64_t y, uint64_t alpha, uint64_t beta, uint64_t gs, uint64_t out, long M, int C,
+                 int dt, uint64_t stream);
 void residual_act_fwd(uint64_t ya, uint64_t sa, uint64_t ta, uint64_t yb, uint64_t sb, uint64_t tb, uint64_t xid,
-                      uint64_t out, long M, int C, int act, float alpha, int dt, uint64_t stream);
-void residual_act_bwd(uint64_t g, uint64_t out, uint64_t ya, uint64_t sa, uint64_t yb, uint64_t sb, uint64_t gya,
-                      uint64_t gyb, uint64_t part, long M, int C, int act, float alpha, int dt, uint64_t stream);
+                      uint64_t out, uint64_t mask, long M, int C, int act, float alpha, int dt, uint64_t stream);
+void residual_act_bwd(uint64_t g, uint64_t out, uint64_t mask, uint64_t ya, uint64_t yb, uint64_t gpre, uint64_t part,
+                      long M, int C, int act, float alpha, int dt, uint64_t stream);
 // optim.hip
 void grad_sumsq(uint64_t g, long n, uint64_t inv_scale, int unscale, uint64_t part, int nb, uint64_t found_inf,
                 uint64_t stream);
@@ -75,7 +75,7 @@ void augment(uint64_t src, uint64_t idx, uint64_t labels_src, uint64_t labels_ou
              float s2, int nchw, int dt_out, uint64_t stream);
 void rng_advance(uint64_t rng, uint64_t stream);
 // conv_igemm.hip
-void conv_igemm(uint64_t x, uint64_t x2, uint64_t ps, uint64_t pt, uint64_t w, uint64_t out, uint64_t part,
+void conv_igemm(uint64_t x, uint64_t x2, uint64_t ps, uint64_t pt, uint64_t pg, uint64_t w, uint64_t out, uint64_t part,
                 uint64_t ex, uint64_t es, uint64_t et, long Nb, int Hi, int Wi, int Cx, int Ho, int Wo, int S,
                 const std::vector<int>& dh, const std::vector<int>& dw, const std::vector<int>& wt, int Cout, int ldw,
                 int Hout, int Wout, int OS, int oy, int ox, int pro, int pro_act, float pro_alpha, int epi, int epi_act,
@@ -83,7 +83,8 @@ void conv_igemm(uint64_t x, uint64_t x2, uint64_t ps, uint64_t pt, uint64_t w, u
 int conv_num_row_blocks(long M, int BM);
 std::vector<long> conv_splitk_workspace(long M, int Cout, int BM, int BN, int nsplit);
 // conv_wgrad.hip
-void conv_wgrad(uint64_t g, uint64_t y, uint64_t al, uint64_t be, uint64_t x, uint64_t xs, uint64_t xt, uint64_t slab,
+void conv_wgrad(uint64_t g, uint64_t y, uint64_t al, uint64_t be, uint64_t gs, uint64_t x, uint64_t xs, uint64_t xt,
+                uint64_t slab,
                 long Nb, int Hi, int Wi, int Cx, int Ho, int Wo, int S, const std::vector<int>& dh,
                 const std::vector<int>& dw, int Cout, int ldw, int act, float act_alpha, int BM, int BN, int BK,
                 int nsplit, int direct, uint64_t stream);

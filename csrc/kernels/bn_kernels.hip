@@ -390,11 +390,13 @@ __global__ __launch_bounds__(64 * kRedWaves) void stats_bwd_finalize_kernel(floa
 template <typename T>
 __global__ __launch_bounds__(kBlk) void affine_fold_kernel(const T* __restrict__ gy, const T* __restrict__ y,
                                                            const float* __restrict__ alpha, const float* __restrict__ beta,
-                                                           T* __restrict__ out, long nvec, int C) {
+                                                           const float* __restrict__ gs, T* __restrict__ out, long nvec,
+                                                           int G) {
+  // out = gy*gs + alpha + beta*y  (gs nullptr: 1; gy nullptr: 0)
   long stride = (long)gridDim.x * blockDim.x;
   for (long v = (long)blockIdx.x * blockDim.x + threadIdx.x; v < nvec; v += stride) {
     long e = v * 8;
-    int c = (int)(e % C);
+    int c = (int)((unsigned long)v % (unsigned)G) * 8;
     float gv[8], yv[8];
     if (gy) Vec8<T>::load(gy + e, gv);
     else {
@@ -402,44 +404,70 @@ __global__ __launch_bounds__(kBlk) void affine_fold_kernel(const T* __restrict__
       for (int i = 0; i < 8; ++i) gv[i] = 0.f;
     }
     Vec8<T>::load(y + e, yv);
-    float av[8], bv[8];
+    float av[8], bv[8], sv[8];
     load8f(alpha, c, av);
     load8f(beta, c, bv);
+    if (gs) load8f(gs, c, sv);
+    else {
 #pragma unroll
-    for (int i = 0; i < 8; ++i) gv[i] += fmaf(bv[i], yv[i], av[i]);
+      for (int i = 0; i < 8; ++i) sv[i] = 1.f;
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) gv[i] = fmaf(gv[i], sv[i], fmaf(bv[i], yv[i], av[i]));
     Vec8<T>::store(out + e, gv);
   }
 }
 
 // ------------------------------------------------------------------ residual join
-// out = act(ya*sa + ta + (yb ? yb*sb + tb : xid))
+// out = act(ya*sa + ta + (yb ? yb*sb + tb : xid)).  mask (optional, ReLU joins): one byte per
+// 8-element vector, bit i = out[8v+i] > 0 -- the backward reads 1/16 of the bytes of `out`.
+// Two vectors per thread per iteration (more loads in flight); channel offset by 32-bit
+// modulo on the vector index (no 64-bit division).
+template <typename T>
+__device__ __forceinline__ void residual_fwd_vec(const T* __restrict__ ya, const float* __restrict__ sa,
+                                                 const float* __restrict__ ta, const T* __restrict__ yb,
+                                                 const float* __restrict__ sb, const float* __restrict__ tb,
+                                                 const T* __restrict__ xid, T* __restrict__ out,
+                                                 uint8_t* __restrict__ mask, long v, int G, int act, float alpha) {
+  const long e = v * 8;
+  const int c = (int)((unsigned long)v % (unsigned)G) * 8;
+  float a[8], b[8], s8[8], t8[8];
+  Vec8<T>::load(ya + e, a);
+  if (yb) {
+    Vec8<T>::load(yb + e, b);
+    load8f(sb, c, s8);
+    load8f(tb, c, t8);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) b[i] = fmaf(b[i], s8[i], t8[i]);
+  } else {
+    Vec8<T>::load(xid + e, b);
+  }
+  load8f(sa, c, s8);
+  load8f(ta, c, t8);
+  uint32_t m = 0;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    a[i] = act_fwd(fmaf(a[i], s8[i], t8[i]) + b[i], act, alpha);
+    m |= (a[i] > 0.f ? 1u : 0u) << i;
+  }
+  Vec8<T>::store(out + e, a);
+  if (mask) mask[v] = (uint8_t)m;
+}
+
 template <typename T>
 __global__ __launch_bounds__(kBlk) void residual_act_fwd_kernel(const T* __restrict__ ya, const float* __restrict__ sa,
                                                                 const float* __restrict__ ta, const T* __restrict__ yb,
                                                                 const float* __restrict__ sb, const float* __restrict__ tb,
-                                                                const T* __restrict__ xid, T* __restrict__ out, long nvec,
-                                                                int C, int act, float alpha) {
-  long stride = (long)gridDim.x * blockDim.x;
-  for (long v = (long)blockIdx.x * blockDim.x + threadIdx.x; v < nvec; v += stride) {
-    long e = v * 8;
-    int c = (int)(e % C);
-    float a[8], b[8], s8[8], t8[8];
-    Vec8<T>::load(ya + e, a);
-    if (yb) {
-      Vec8<T>::load(yb + e, b);
-      load8f(sb, c, s8);
-      load8f(tb, c, t8);
-#pragma unroll
-      for (int i = 0; i < 8; ++i) b[i] = fmaf(b[i], s8[i], t8[i]);
-    } else {
-      Vec8<T>::load(xid + e, b);
-    }
-    load8f(sa, c, s8);
-    load8f(ta, c, t8);
-#pragma unroll
-    for (int i = 0; i < 8; ++i) a[i] = act_fwd(fmaf(a[i], s8[i], t8[i]) + b[i], act, alpha);
-    Vec8<T>::store(out + e, a);
+                                                                const T* __restrict__ xid, T* __restrict__ out,
+                                                                uint8_t* __restrict__ mask, long nvec, int G, int act,
+                                                                float alpha) {
+  const long stride = (long)gridDim.x * blockDim.x;
+  long v = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  for (; v + stride < nvec; v += 2 * stride) {
+    residual_fwd_vec(ya, sa, ta, yb, sb, tb, xid, out, mask, v, G, act, alpha);
+    residual_fwd_vec(ya, sa, ta, yb, sb, tb, xid, out, mask, v + stride, G, act, alpha);
   }
+  if (v < nvec) residual_fwd_vec(ya, sa, ta, yb, sb, tb, xid, out, mask, v, G, act, alpha);
 }
 
 // act'(z) from the activation OUTPUT o (ReLU: o>0; CELU: o>0 ? 1 : o/alpha + 1)
@@ -449,44 +477,43 @@ __device__ __forceinline__ float act_grad_from_out(float o, int act, float alpha
   return 1.f;
 }
 
-// g_pre = g * act'(out); gya = g_pre*sa; gyb = g_pre*sb (or g_pre if identity branch)
-// part[blk][3][C] = [sum g_pre*ya, sum g_pre, sum g_pre*yb]
+// g_pre = g * act'(out) -- the ONE gradient both branches consume (the consumers scale it
+// by their own s through the fold prologue's gs):
+// part[blk][3][C] = [sum g_pre*ya, sum g_pre, sum g_pre*yb].  act' comes from the forward's
+// bit mask when given (ReLU), else from `out`.
 template <typename T>
 __global__ __launch_bounds__(kBlk) void residual_act_bwd_kernel(const T* __restrict__ g, const T* __restrict__ out,
-                                                                const T* __restrict__ ya, const float* __restrict__ sa,
-                                                                const T* __restrict__ yb, const float* __restrict__ sb,
-                                                                T* __restrict__ gya, T* __restrict__ gyb,
-                                                                float* __restrict__ part, long M, int C, int TPR, int RPP,
-                                                                long rows_per_blk, int act, float alpha) {
+                                                                const uint8_t* __restrict__ mask,
+                                                                const T* __restrict__ ya, const T* __restrict__ yb,
+                                                                T* __restrict__ gpre, float* __restrict__ part, long M,
+                                                                int C, int TPR, int RPP, long rows_per_blk, int act,
+                                                                float alpha) {
   __shared__ float sm[kBlk * 24];
   const int tid = threadIdx.x;
   const int gi = tid % TPR, rr = tid / TPR;
   const int c0 = (blockIdx.y * TPR + gi) * 8;
-  float sav[8], sbv[8];
-#pragma unroll
-  for (int i = 0; i < 8; ++i) { sav[i] = sa[c0 + i]; sbv[i] = yb ? sb[c0 + i] : 1.f; }
   const long r_begin = (long)blockIdx.x * rows_per_blk;
   long r_end = r_begin + rows_per_blk;
   if (r_end > M) r_end = M;
   float p0[8] = {0, 0, 0, 0, 0, 0, 0, 0}, p1[8] = {0, 0, 0, 0, 0, 0, 0, 0}, p2[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   for (long r = r_begin + rr; r < r_end; r += RPP) {
     const long e = r * C + c0;
-    float gv[8], ov[8], av[8], bv[8], oa[8], ob[8];
+    float gv[8], av[8], bv[8], ov[8];
     Vec8<T>::load(g + e, gv);
-    Vec8<T>::load(out + e, ov);
+    uint32_t m = 0;
+    if (mask) m = mask[e >> 3];
+    else Vec8<T>::load(out + e, ov);
     Vec8<T>::load(ya + e, av);
     if (yb) Vec8<T>::load(yb + e, bv);
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
-      float gp = gv[i] * act_grad_from_out(ov[i], act, alpha);
-      oa[i] = gp * sav[i];
-      ob[i] = gp * sbv[i];
+      const float gp = mask ? ((m >> i) & 1u ? gv[i] : 0.f) : gv[i] * act_grad_from_out(ov[i], act, alpha);
+      gv[i] = gp;
       p0[i] = fmaf(gp, av[i], p0[i]);
       p1[i] += gp;
       if (yb) p2[i] = fmaf(gp, bv[i], p2[i]);
     }
-    Vec8<T>::store(gya + e, oa);
-    Vec8<T>::store(gyb + e, ob);
+    Vec8<T>::store(gpre + e, gv);
   }
 #pragma unroll
   for (int i = 0; i < 8; ++i) { sm[tid * 24 + i] = p0[i]; sm[tid * 24 + 8 + i] = p1[i]; sm[tid * 24 + 16 + i] = p2[i]; }
@@ -646,39 +673,50 @@ void stats_bwd_finalize(uint64_t part, int nb, int nq, int C, int a_mode, float 
   FDT_LAUNCH_CHECK();
 }
 
-void affine_fold(uint64_t gy, uint64_t y, uint64_t alpha, uint64_t beta, uint64_t out, long M, int C, int dt,
-                 uint64_t stream) {
+void affine_fold(uint64_t gy, uint64_t y, uint64_t alpha, uint64_t beta, uint64_t gs, uint64_t out, long M, int C,
+                 int dt, uint64_t stream) {
+  FDT_CHECK(C % 8 == 0, "C % 8");
   long nvec = M * (long)C / 8;
   if (nvec == 0) return;
   DISPATCH_T(dt, {
     affine_fold_kernel<T><<<ew_grid(nvec), kBlk, 0, as_stream(stream)>>>(
-        P<const T>(gy), P<const T>(y), P<const float>(alpha), P<const float>(beta), P<T>(out), nvec, C);
+        P<const T>(gy), P<const T>(y), P<const float>(alpha), P<const float>(beta), P<const float>(gs), P<T>(out), nvec,
+        C / 8);
   });
   FDT_LAUNCH_CHECK();
 }
 
 void residual_act_fwd(uint64_t ya, uint64_t sa, uint64_t ta, uint64_t yb, uint64_t sb, uint64_t tb, uint64_t xid,
-                      uint64_t out, long M, int C, int act, float alpha, int dt, uint64_t stream) {
+                      uint64_t out, uint64_t mask, long M, int C, int act, float alpha, int dt, uint64_t stream) {
+  FDT_CHECK(C % 8 == 0, "C % 8");
   long nvec = M * (long)C / 8;
   if (nvec == 0) return;
   FDT_CHECK(yb != 0 || xid != 0, "residual needs a second branch");
+  FDT_CHECK(mask == 0 || act == kActRelu, "the activation bit mask is for ReLU joins");
+  long g = (nvec + 2 * kBlk - 1) / (2 * kBlk);  // two vectors per thread
+  if (g > 4096) g = 4096;
   DISPATCH_T(dt, {
-    residual_act_fwd_kernel<T><<<ew_grid(nvec), kBlk, 0, as_stream(stream)>>>(
+    residual_act_fwd_kernel<T><<<(int)g, kBlk, 0, as_stream(stream)>>>(
         P<const T>(ya), P<const float>(sa), P<const float>(ta), P<const T>(yb), P<const float>(sb), P<const float>(tb),
-        P<const T>(xid), P<T>(out), nvec, C, act, alpha);
+        P<const T>(xid), P<T>(out), P<uint8_t>(mask), nvec, C / 8, act, alpha);
   });
   FDT_LAUNCH_CHECK();
 }
 
-void residual_act_bwd(uint64_t g, uint64_t out, uint64_t ya, uint64_t sa, uint64_t yb, uint64_t sb, uint64_t gya,
-                      uint64_t gyb, uint64_t part, long M, int C, int act, float alpha, int dt, uint64_t stream) {
+void residual_act_bwd(uint64_t g, uint64_t out, uint64_t mask, uint64_t ya, uint64_t yb, uint64_t gpre, uint64_t part,
+                      long M, int C, int act, float alpha, int dt, uint64_t stream) {
+  FDT_CHECK(out != 0 || mask != 0, "residual_act_bwd needs the output or its mask");
   ChanGeom gg = chan_geom(C);
-  long r = rows_per_block(M, gg);
+  // ~1024 blocks: more waves in flight for this 4-5 stream kernel than the stats default
+  long target = 1024 / (gg.gy > 0 ? gg.gy : 1);
+  long r = (M + target - 1) / target;
+  if (r < gg.RPP) r = gg.RPP;
+  r = (r + gg.RPP - 1) / gg.RPP * gg.RPP;
   dim3 grid((unsigned)((M + r - 1) / r), gg.gy);
   DISPATCH_T(dt, {
     residual_act_bwd_kernel<T><<<grid, kBlk, 0, as_stream(stream)>>>(
-        P<const T>(g), P<const T>(out), P<const T>(ya), P<const float>(sa), P<const T>(yb), P<const float>(sb), P<T>(gya),
-        P<T>(gyb), P<float>(part), M, C, gg.TPR, gg.RPP, r, act, alpha);
+        P<const T>(g), P<const T>(out), P<const uint8_t>(mask), P<const T>(ya), P<const T>(yb), P<T>(gpre), P<float>(part),
+        M, C, gg.TPR, gg.RPP, r, act, alpha);
   });
   FDT_LAUNCH_CHECK();
 }

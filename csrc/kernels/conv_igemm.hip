@@ -18,7 +18,8 @@
 // Fusion (the reason this is not a library call):
 //  * prologue on the activation operand, applied while staging to LDS:
 //      PRO_AFFINE_ACT  x -> act(x*s[c] + t[c])   (the producer's lazy batch-norm)
-//      PRO_FOLD        g -> g + alpha[c] + beta[c]*y  (batch-norm backward correction)
+//      PRO_FOLD        g -> g*gs[c] + alpha[c] + beta[c]*y  (batch-norm backward correction;
+//                      gs lets the residual join store one un-scaled gradient for both branches)
 //    zero padding is applied AFTER the transform (the conv pads the normalised input);
 //  * epilogue:
 //      EPI_STATS   y (bf16) + per-block per-channel (sum y, sum y^2) slabs -> BN stats
@@ -57,6 +58,7 @@ struct ConvArgs {
   const bf16* x2;    // PRO_FOLD: the producer output Y (same shape as x)
   const float* ps;   // prologue per-channel scale: s (AFFINE_ACT) or alpha (FOLD)   [Cx]
   const float* pt;   // prologue per-channel shift: t (AFFINE_ACT) or beta  (FOLD)   [Cx]
+  const float* pg;   // FOLD: per-channel scale of g (nullptr = 1): g*pg + alpha + beta*y    [Cx]
   const bf16* w;     // packed weights [Cout][ldw], k-index = wt[tap]*Cx + ci
   bf16* out;         // [Nb][Hout][Wout][Cout]
   float* part;       // statistics slots [kStatSlots][2][Cout], fp32 atomics (zeroed by the consumer)
@@ -165,8 +167,9 @@ __global__ __launch_bounds__(256) void igemm_kernel(const ConvArgs a) {
   const int nkt = (a.K + BK - 1) / BK;
   const int nbuf = nkt > 1 ? 2 : 1;                                    // K <= BK: one LDS buffer
   bf16* tiles = reinterpret_cast<bf16*>(smem);                         // [nbuf][WT + XT]
-  float* pst = reinterpret_cast<float*>(smem + nbuf * (XT + WT) * 2);  // [2][Cx] (PRO != none)
-  float* red = pst + (PRO != kProNone ? 2 * a.Cx : 0);                 // [2 waves][2][BN]
+  float* pst = reinterpret_cast<float*>(smem + nbuf * (XT + WT) * 2);  // [2|3][Cx] (PRO != none)
+  constexpr int NPRM = PRO == kProFold ? 3 : (PRO != kProNone ? 2 : 0);
+  float* red = pst + NPRM * a.Cx;                                      // [2 waves][2][BN]
   int* tapt = reinterpret_cast<int*>(red + 4 * BN);                    // [12]: tap pixel offset
   int* tapw = tapt + 12;                                               // [12]: dh | dw<<8 | wt<<16
 
@@ -193,6 +196,7 @@ __global__ __launch_bounds__(256) void igemm_kernel(const ConvArgs a) {
     for (int i = tid; i < a.Cx; i += 256) {
       pst[i] = a.ps[i];
       pst[a.Cx + i] = a.pt[i];
+      if constexpr (PRO == kProFold) pst[2 * a.Cx + i] = a.pg ? a.pg[i] : 1.f;
     }
   }
   if (tid < 12) {
@@ -279,7 +283,12 @@ __global__ __launch_bounds__(256) void igemm_kernel(const ConvArgs a) {
       const int row = tid / CPR + j * RPR;
       *reinterpret_cast<uint4*>(Wl + row * BK + 8 * (cc ^ swz<CPR>(row))) = S.rw[j];
     }
-    float sv[8], tv[8];
+    float sv[8], tv[8], gv[8];
+    if constexpr (PRO == kProFold) {
+      const float4* gp = reinterpret_cast<const float4*>(pst + 2 * a.Cx + S.kci);
+      float4 g0 = gp[0], g1 = gp[1];
+      gv[0] = g0.x; gv[1] = g0.y; gv[2] = g0.z; gv[3] = g0.w; gv[4] = g1.x; gv[5] = g1.y; gv[6] = g1.z; gv[7] = g1.w;
+    }
     if constexpr (PRO != kProNone) {
       const float4* sp = reinterpret_cast<const float4*>(pst + S.kci);
       const float4* tp = reinterpret_cast<const float4*>(pst + a.Cx + S.kci);
@@ -312,7 +321,7 @@ __global__ __launch_bounds__(256) void igemm_kernel(const ConvArgs a) {
           y[2 * q] = bf16_lo(uy[q]); y[2 * q + 1] = bf16_hi(uy[q]);
         }
 #pragma unroll
-        for (int q = 0; q < 8; ++q) g[q] += fmaf(tv[q], y[q], sv[q]);
+        for (int q = 0; q < 8; ++q) g[q] = fmaf(g[q], gv[q], fmaf(tv[q], y[q], sv[q]));
         o = make_uint4(pk_bf16(g[0], g[1]), pk_bf16(g[2], g[3]), pk_bf16(g[4], g[5]), pk_bf16(g[6], g[7]));
         if (!S.xv[j]) o = make_uint4(0, 0, 0, 0);
       }
@@ -614,7 +623,7 @@ template <int PRO, int EPI, int ACT>
 static void launch_tile(const ConvArgs& a, int BM, int BN, int BK, bool pure, hipStream_t st) {
   const int nkt = (a.K + BK - 1) / BK;
   const size_t nbuf = nkt > 1 ? 2 : 1;
-  size_t lds = nbuf * (BM + BN) * BK * 2 + (PRO != kProNone ? 2 * a.Cx * 4 : 0) + 4 * BN * 4 + 128;
+  size_t lds = nbuf * (BM + BN) * BK * 2 + (PRO == kProFold ? 3 : (PRO != kProNone ? 2 : 0)) * a.Cx * 4 + 4 * BN * 4 + 128;
 #define FDT_T(BM_, BN_, BK_) \
   if (BM == BM_ && BN == BN_ && BK == BK_) { launch_pure<BM_, BN_, BK_, PRO, EPI, ACT>(a, pure, lds, st); return; }
   FDT_T(128, 128, 64) FDT_T(128, 64, 64) FDT_T(64, 128, 64) FDT_T(64, 64, 64) FDT_T(256, 64, 64)
@@ -626,7 +635,7 @@ static void launch_tile(const ConvArgs& a, int BM, int BN, int BK, bool pure, hi
 }  // namespace conv
 
 // Python-facing launcher.  taps: list of (dh, dw, wt) triples encoded as int8 arrays.
-void conv_igemm(uint64_t x, uint64_t x2, uint64_t ps, uint64_t pt, uint64_t w, uint64_t out, uint64_t part,
+void conv_igemm(uint64_t x, uint64_t x2, uint64_t ps, uint64_t pt, uint64_t pg, uint64_t w, uint64_t out, uint64_t part,
                 uint64_t ex, uint64_t es, uint64_t et, long Nb, int Hi, int Wi, int Cx, int Ho, int Wo, int S,
                 const std::vector<int>& dh, const std::vector<int>& dw, const std::vector<int>& wt, int Cout, int ldw,
                 int Hout, int Wout, int OS, int oy, int ox, int pro, int pro_act, float pro_alpha, int epi, int epi_act,
@@ -637,6 +646,7 @@ void conv_igemm(uint64_t x, uint64_t x2, uint64_t ps, uint64_t pt, uint64_t w, u
   a.x2 = P<const bf16>(x2);
   a.ps = P<const float>(ps);
   a.pt = P<const float>(pt);
+  a.pg = P<const float>(pg);
   a.w = P<const bf16>(w);
   a.out = P<bf16>(out);
   a.part = P<float>(part);

@@ -2,7 +2,8 @@
 // per-step weight packing kernel.
 //
 //   dW[co][k] = sum_px  G~[px][co] * A[px][k],   k = (tap, ci)
-//   G~ = g + alpha[co] + beta[co]*y   (batch-norm backward correction, PRO_FOLD)
+//   G~ = g*gs[co] + alpha[co] + beta[co]*y   (batch-norm backward correction, PRO_FOLD;
+//        gs = nullptr means 1)
 //   A  = act(x*s + t) at the tap's input pixel (zero outside the image)
 //
 // Both operands are pixel-major in HBM with channels contiguous, and the reduction runs
@@ -34,6 +35,7 @@ struct WgArgs {
   const bf16* y;     // [M][Cout]  conv output (for the correction)
   const float* al;   // alpha [Cout]  (nullptr: no correction)
   const float* be;   // beta  [Cout]
+  const float* gs;   // gradient scale [Cout] (nullptr: 1)
   const bf16* x;     // [Nb][Hi][Wi][Cx]  conv input (raw)
   const float* xs;   // s [Cx] (nullptr: identity input transform)
   const float* xt;   // t [Cx]
@@ -87,8 +89,8 @@ __global__ __launch_bounds__(256) void wgrad_kernel(const WgArgs a) {
 
   extern __shared__ __attribute__((aligned(16))) char smem[];
   bf16* tiles = reinterpret_cast<bf16*>(smem);  // [2][GT + XT]
-  float* prm = reinterpret_cast<float*>(smem + 2 * (GT + XT) * 2);  // al|be [BM] , xs|xt [Cx]
-  int* tapt = reinterpret_cast<int*>(prm + 2 * BM + (XAFF ? 2 * a.Cx : 0));
+  float* prm = reinterpret_cast<float*>(smem + 2 * (GT + XT) * 2);  // al|be|gs [BM] , xs|xt [Cx]
+  int* tapt = reinterpret_cast<int*>(prm + 3 * BM + (XAFF ? 2 * a.Cx : 0));
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wn = wid & 1, wm = wid >> 1;
@@ -106,10 +108,14 @@ __global__ __launch_bounds__(256) void wgrad_kernel(const WgArgs a) {
   const __amdgpu_buffer_rsrc_t rx_d = __builtin_amdgcn_make_buffer_rsrc((void*)a.x, (short)0, (int)a.x_bytes, 0x00020000);
 
   if constexpr (FOLD) {
-    for (int i = tid; i < BM; i += 256) { prm[i] = a.al[co0 + i]; prm[BM + i] = a.be[co0 + i]; }
+    for (int i = tid; i < BM; i += 256) {
+      prm[i] = a.al[co0 + i];
+      prm[BM + i] = a.be[co0 + i];
+      prm[2 * BM + i] = a.gs ? a.gs[co0 + i] : 1.f;
+    }
   }
   if constexpr (XAFF) {
-    for (int i = tid; i < a.Cx; i += 256) { prm[2 * BM + i] = a.xs[i]; prm[2 * BM + a.Cx + i] = a.xt[i]; }
+    for (int i = tid; i < a.Cx; i += 256) { prm[3 * BM + i] = a.xs[i]; prm[3 * BM + a.Cx + i] = a.xt[i]; }
   }
   if (tid < 12) tapt[tid] = (int)(uint8_t)a.dh[tid] | ((int)(uint8_t)a.dw[tid] << 8);
 
@@ -130,12 +136,16 @@ __global__ __launch_bounds__(256) void wgrad_kernel(const WgArgs a) {
   float xsv[8], xtv[8];
   if constexpr (XAFF) {
 #pragma unroll
-    for (int q = 0; q < 8; ++q) { xsv[q] = prm[2 * BM + xci + q]; xtv[q] = prm[2 * BM + a.Cx + xci + q]; }
+    for (int q = 0; q < 8; ++q) { xsv[q] = prm[3 * BM + xci + q]; xtv[q] = prm[3 * BM + a.Cx + xci + q]; }
   }
-  float alv[8], bev[8];
+  float alv[8], bev[8], gsv[8];
   if constexpr (FOLD) {
 #pragma unroll
-    for (int q = 0; q < 8; ++q) { alv[q] = prm[gcc * 8 + q]; bev[q] = prm[BM + gcc * 8 + q]; }
+    for (int q = 0; q < 8; ++q) {
+      alv[q] = prm[gcc * 8 + q];
+      bev[q] = prm[BM + gcc * 8 + q];
+      gsv[q] = prm[2 * BM + gcc * 8 + q];
+    }
   }
   const float inv_alpha = ACT == kActCelu ? 1.f / a.act_alpha : 1.f;
   const int hw = a.Ho * a.Wo;
@@ -198,8 +208,8 @@ __global__ __launch_bounds__(256) void wgrad_kernel(const WgArgs a) {
         float v[8];
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-          v[2 * q] = bf16_lo(u[q]) + fmaf(bev[2 * q], bf16_lo(uy[q]), alv[2 * q]);
-          v[2 * q + 1] = bf16_hi(u[q]) + fmaf(bev[2 * q + 1], bf16_hi(uy[q]), alv[2 * q + 1]);
+          v[2 * q] = fmaf(bf16_lo(u[q]), gsv[2 * q], fmaf(bev[2 * q], bf16_lo(uy[q]), alv[2 * q]));
+          v[2 * q + 1] = fmaf(bf16_hi(u[q]), gsv[2 * q + 1], fmaf(bev[2 * q + 1], bf16_hi(uy[q]), alv[2 * q + 1]));
         }
         o = make_uint4(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]), pack_bf16x2(v[4], v[5]),
                        pack_bf16x2(v[6], v[7]));
@@ -428,7 +438,8 @@ __global__ __launch_bounds__(256) void pack_weights_kernel(const PackTable tab) 
 
 }  // namespace wg
 
-void conv_wgrad(uint64_t g, uint64_t y, uint64_t al, uint64_t be, uint64_t x, uint64_t xs, uint64_t xt, uint64_t slab,
+void conv_wgrad(uint64_t g, uint64_t y, uint64_t al, uint64_t be, uint64_t gs, uint64_t x, uint64_t xs, uint64_t xt,
+                uint64_t slab,
                 long Nb, int Hi, int Wi, int Cx, int Ho, int Wo, int S, const std::vector<int>& dh,
                 const std::vector<int>& dw, int Cout, int ldw, int act, float act_alpha, int BM, int BN, int BK,
                 int nsplit, int direct, uint64_t stream) {
@@ -436,6 +447,7 @@ void conv_wgrad(uint64_t g, uint64_t y, uint64_t al, uint64_t be, uint64_t x, ui
   WgArgs a{};
   a.g = P<const bf16>(g); a.y = P<const bf16>(y);
   a.al = P<const float>(al); a.be = P<const float>(be);
+  a.gs = P<const float>(gs);
   a.x = P<const bf16>(x); a.xs = P<const float>(xs); a.xt = P<const float>(xt);
   a.slab = P<float>(slab);
   a.direct = direct;
@@ -466,7 +478,7 @@ void conv_wgrad(uint64_t g, uint64_t y, uint64_t al, uint64_t be, uint64_t x, ui
   a.px_per_split = per;
   a.nsplit = nsplit;
   const bool fold = al != 0, xaff = xs != 0;
-  size_t lds = (size_t)2 * BK * (BM + BN) * 2 + 2 * BM * 4 + (xaff ? 2 * Cx * 4 : 0) + 64;
+  size_t lds = (size_t)2 * BK * (BM + BN) * 2 + 3 * BM * 4 + (xaff ? 2 * Cx * 4 : 0) + 64;
   dim3 grid(a.nbm * a.nbn, nsplit);
   hipStream_t st = as_stream(stream);
   const int wact = xaff ? act : 0;

@@ -213,7 +213,7 @@ def conv_fwd(x, wf, shp: ConvShape, s=None, t=None, act=0, alpha=1.0, tile=None,
     if pro == PRO_AFFINE_ACT and s is None:
         s = torch.ones(C, device=x.device, dtype=torch.float32)
         t = torch.zeros(C, device=x.device, dtype=torch.float32)
-    nat.conv_igemm(x.data_ptr(), 0, _p(s), _p(t), wf.data_ptr(), y.data_ptr(), part.data_ptr(), 0, 0, 0,
+    nat.conv_igemm(x.data_ptr(), 0, _p(s), _p(t), 0, wf.data_ptr(), y.data_ptr(), part.data_ptr(), 0, 0, 0,
                    N, H, W, C, Ho, Wo, shp.stride, list(dh), list(dw), list(wt), shp.cout, shp.ntaps * shp.cxp,
                    Ho, Wo, 1, 0, 0, pro, int(act), float(alpha), EPI_STATS, 0, 1.0, bm, bn, bk, ns, slab_p, cnt_p,
                    _sp())
@@ -221,8 +221,8 @@ def conv_fwd(x, wf, shp: ConvShape, s=None, t=None, act=0, alpha=1.0, tile=None,
 
 
 def conv_dgrad(g, y, al, be, wd, shp: ConvShape, x_shape, epi=EPI_STORE, out=None, ex=None, es=None, et=None,
-               act=0, alpha=1.0, tile=None, part=None, nsplit=None):
-    """Data gradient of y = conv(a): dA = conv^T(g + al + be*y).
+               act=0, alpha=1.0, tile=None, part=None, nsplit=None, gs=None):
+    """Data gradient of y = conv(a): dA = conv^T(g*gs + al + be*y)  (gs None: 1).
 
     epi: EPI_STORE -> write dA; EPI_ADD -> out += dA; EPI_ACTBWD -> through the lazy
     input a = act(ex*es + et): out = dA*act'(.)*es, returns statistics slots
@@ -255,7 +255,9 @@ def conv_dgrad(g, y, al, be, wd, shp: ConvShape, x_shape, epi=EPI_STORE, out=Non
         bm, bn, bk = _tile3(tile, M, shp.cin)
         ns, slab_p, cnt_p = _splitk_args(ent, M, shp.cin, len(dh) * Cy, bm, bn, bk, g.device)
         pro = PRO_FOLD if al is not None else PRO_NONE  # al None: g is already folded
-        nat.conv_igemm(g.data_ptr(), _p(y) if pro == PRO_FOLD else 0, _p(al), _p(be), wd.data_ptr(), out.data_ptr(),
+        assert gs is None or pro == PRO_FOLD, "gs needs the fold prologue (al/be)"
+        nat.conv_igemm(g.data_ptr(), _p(y) if pro == PRO_FOLD else 0, _p(al), _p(be), _p(gs), wd.data_ptr(),
+                       out.data_ptr(),
                        _p(part) if epi == EPI_ACTBWD else 0, _p(ex), _p(es), _p(et), N, Hy, Wy, Cy, Ha, Wa, 1,
                        list(dh), list(dw), list(wt), shp.cin, shp.ntaps * shp.cout, Hx, Wx, shp.stride, py, px, pro, 0, 1.0, epi, int(act),
                        float(alpha), bm, bn, bk, ns, slab_p, cnt_p, _sp())
@@ -269,9 +271,9 @@ def wgrad_split(M: int, tiles: int, want: int = 512, min_px: int = 1024) -> int:
 
 
 def conv_wgrad(g, y, al, be, x, shp: ConvShape, out, xs=None, xt=None, act=0, alpha=1.0, accumulate=False,
-               tile=None, nsplit=None, slab=None):
+               tile=None, nsplit=None, slab=None, gs=None):
     """out (fp32 OIHW [Cout, Cin, k, k]) = dL/dW of y = conv(act(x*xs+xt)) given
-    g (gradient wrt y, corrected by al + be*y in the kernel)."""
+    g (gradient wrt y, corrected to g*gs + al + be*y in the kernel; gs None: 1)."""
     nat = _native.native()
     N, Hy, Wy, Cy = g.shape
     Nx, H, W, Cx = x.shape
@@ -307,7 +309,8 @@ def conv_wgrad(g, y, al, be, x, shp: ConvShape, out, xs=None, xt=None, act=0, al
     if xs is None and act != 0:
         xs = torch.ones(Cx, device=x.device, dtype=torch.float32)
         xt = torch.zeros(Cx, device=x.device, dtype=torch.float32)
-    nat.conv_wgrad(g.data_ptr(), _p(y), _p(al), _p(be), x.data_ptr(), _p(xs), _p(xt), slab.data_ptr(),
+    assert gs is None or al is not None, "gs needs the fold (al/be)"
+    nat.conv_wgrad(g.data_ptr(), _p(y), _p(al), _p(be), _p(gs), x.data_ptr(), _p(xs), _p(xt), slab.data_ptr(),
                    N, H, W, Cx, Hy, Wy, shp.stride, list(dh), list(dw), shp.cout, ldw, int(act), float(alpha),
                    bm, bn, bk, ns, int(direct), _sp())
     if not direct:

@@ -265,10 +265,10 @@ def bwd_finalize(part, nq, ua, sta, ub=None, stb=None, training=True, dev=None):
     return ra, rb
 
 
-def wgrad_into(u: Unit, g, y, al, be, x, xs, xt, act):
+def wgrad_into(u: Unit, g, y, al, be, x, xs, xt, act, gs=None):
     if u.w.grad is None:
         u.w.grad = torch.zeros_like(u.w)
-    ci.conv_wgrad(g, y, al, be, x, u.shp, u.w.grad, xs, xt, act[0], act[1], accumulate=True)
+    ci.conv_wgrad(g, y, al, be, x, u.shp, u.w.grad, xs, xt, act[0], act[1], accumulate=True, gs=gs)
     grad_ready(u.w)
 
 
@@ -322,12 +322,17 @@ class ResNetBodyFn(torch.autograd.Function):
                 sc = (ysc, ssc, tsc, smsc, sasc, M, None)
             out = torch.empty_like(y3)
             C = y3.shape[-1]
+            # ReLU joins also emit a 1-bit-per-element activation mask: the backward reads it
+            # instead of `out` (1/16 of the bytes)
+            mask = None
+            if need_grad and b.join[0] == ACT_RELU:
+                mask = torch.empty(out.numel() // 8, device=dev, dtype=torch.uint8)
             nat.residual_act_fwd(y3.data_ptr(), s3.data_ptr(), t3.data_ptr(), _p(sc[0] if sc else None),
                                  _p(sc[1] if sc else None), _p(sc[2] if sc else None),
-                                 0 if sc else x_in.data_ptr(), out.data_ptr(), _rows(y3), C, b.join[0],
+                                 0 if sc else x_in.data_ptr(), out.data_ptr(), _p(mask), _rows(y3), C, b.join[0],
                                  float(b.join[1]), 1, _sp())
             if need_grad:
-                recs.append((x_in, ys, sc, out))
+                recs.append((x_in, ys, sc, out, mask))
             h = out
         if need_grad:
             ctx.plan, ctx.training = plan, training
@@ -340,21 +345,24 @@ class ResNetBodyFn(torch.autograd.Function):
         plan, training = ctx.plan, ctx.training
         g = g_out.contiguous()
         dev = g.device
-        for b, (x_in, ys, sc, out) in zip(reversed(plan.blocks), reversed(ctx.recs)):
+        for b, (x_in, ys, sc, out, mask) in zip(reversed(plan.blocks), reversed(ctx.recs)):
             y3, s3 = ys[-1][0], ys[-1][1]
             C = y3.shape[-1]
             M = _rows(y3)
             part = slots(3, C, dev)
-            gya = torch.empty_like(y3)
-            gyb = torch.empty_like(out)  # shortcut-branch grad, or the identity grad of x_in
-            nat.residual_act_bwd(g.data_ptr(), out.data_ptr(), y3.data_ptr(), s3.data_ptr(),
-                                 _p(sc[0] if sc else None), _p(sc[1] if sc else None), gya.data_ptr(),
-                                 gyb.data_ptr(), part.data_ptr(), M, C, b.join[0], float(b.join[1]), 1, _sp())
+            # ONE gradient g_pre = g*act'(z) for both branches: each consumer folds in its own
+            # BN scale (gs = s3 / s_shortcut) in its prologue; for an identity block g_pre is
+            # also the x_in gradient the first unit's dgrad accumulates into
+            gpre = torch.empty_like(y3)
+            nat.residual_act_bwd(g.data_ptr(), 0 if mask is not None else out.data_ptr(), _p(mask), y3.data_ptr(),
+                                 _p(sc[0] if sc else None), gpre.data_ptr(), part.data_ptr(), M, C, b.join[0],
+                                 float(b.join[1]), 1, _sp())
             ul = b.units[-1]
             (al, be), coef_sc = bwd_finalize(part, 3, ul, (ys[-1][3], ys[-1][4], ys[-1][5]),
                                              b.shortcut, (sc[3], sc[4], sc[5]) if sc else None, training, dev)
-            g_cur = gya
-            g_x = None if sc is not None else gyb
+            g_cur, gs_cur = gpre, s3
+            assert sc is not None or len(b.units) > 1, "identity block needs >1 unit (g_pre aliasing)"
+            g_x = None if sc is not None else gpre
             # residual chain, last unit first; (al, be) = BN-backward correction of unit i
             for i in range(len(b.units) - 1, -1, -1):
                 u = b.units[i]
@@ -367,8 +375,8 @@ class ResNetBodyFn(torch.autograd.Function):
                         # fold the BN-backward correction into the gradient once (3x3: the
                         # dgrad operand is re-read 9x, the wgrad operand once per column block)
                         gf = torch.empty_like(g_cur)
-                        nat.affine_fold(g_cur.data_ptr(), y.data_ptr(), al.data_ptr(), be.data_ptr(), gf.data_ptr(),
-                                        _rows(gf), gf.shape[-1], 1, _sp())
+                        nat.affine_fold(g_cur.data_ptr(), y.data_ptr(), al.data_ptr(), be.data_ptr(), _p(gs_cur),
+                                        gf.data_ptr(), _rows(gf), gf.shape[-1], 1, _sp())
                         g_prev, _ = ci.conv_dgrad(gf, None, None, None, u.wd, u.shp, tuple(yp.shape),
                                                   epi=ci.EPI_ACTBWD, ex=yp, es=sp_, et=tp, act=actp[0],
                                                   alpha=actp[1], part=pp)
@@ -378,24 +386,26 @@ class ResNetBodyFn(torch.autograd.Function):
                     else:
                         g_prev, _ = ci.conv_dgrad(g_cur, y, al, be, u.wd, u.shp, tuple(yp.shape),
                                                   epi=ci.EPI_ACTBWD, ex=yp, es=sp_, et=tp, act=actp[0],
-                                                  alpha=actp[1], part=pp)
-                        wgrad_into(u, g_cur, y, al, be, yp, sp_, tp, actp)
+                                                  alpha=actp[1], part=pp, gs=gs_cur)
+                        wgrad_into(u, g_cur, y, al, be, yp, sp_, tp, actp, gs=gs_cur)
                     up = b.units[i - 1]
                     (al, be), _ = bwd_finalize(pp, 2, up, (ys[i - 1][3], ys[i - 1][4], ys[i - 1][5]),
                                                training=training, dev=dev)
-                    g_cur = g_prev
+                    g_cur, gs_cur = g_prev, None
                 else:
                     if g_x is None:
-                        g_x, _ = ci.conv_dgrad(g_cur, y, al, be, u.wd, u.shp, tuple(x_in.shape), epi=ci.EPI_STORE)
+                        g_x, _ = ci.conv_dgrad(g_cur, y, al, be, u.wd, u.shp, tuple(x_in.shape), epi=ci.EPI_STORE,
+                                               gs=gs_cur)
                     else:
-                        ci.conv_dgrad(g_cur, y, al, be, u.wd, u.shp, tuple(x_in.shape), epi=ci.EPI_ADD, out=g_x)
-                    wgrad_into(u, g_cur, y, al, be, x_in, None, None, (ACT_NONE, 1.0))
+                        ci.conv_dgrad(g_cur, y, al, be, u.wd, u.shp, tuple(x_in.shape), epi=ci.EPI_ADD, out=g_x,
+                                      gs=gs_cur)
+                    wgrad_into(u, g_cur, y, al, be, x_in, None, None, (ACT_NONE, 1.0), gs=gs_cur)
             if sc is not None:
                 u = b.shortcut
                 ysc = sc[0]
                 al, be = coef_sc
-                ci.conv_dgrad(gyb, ysc, al, be, u.wd, u.shp, tuple(x_in.shape), epi=ci.EPI_ADD, out=g_x)
-                wgrad_into(u, gyb, ysc, al, be, x_in, None, None, (ACT_NONE, 1.0))
+                ci.conv_dgrad(gpre, ysc, al, be, u.wd, u.shp, tuple(x_in.shape), epi=ci.EPI_ADD, out=g_x, gs=sc[1])
+                wgrad_into(u, gpre, ysc, al, be, x_in, None, None, (ACT_NONE, 1.0), gs=sc[1])
             g = g_x
         # stem: act backward + statistics -> wgrad on the input image
         x_img, y0, s0, t0, sm0, sa0 = ctx.stem_rec

@@ -193,3 +193,34 @@ def test_pack_weights_layouts(cuda, cout, cin, k):
     assert torch.equal(wf.view(cout, k * k, shp.cxp), ref_f)
     ref_d = wb.permute(1, 2, 3, 0).reshape(cin, k * k, cout)
     assert torch.equal(wd.view(cin, k * k, cout)[:cin], ref_d)
+
+
+@pytest.mark.parametrize("case", [(4, 8, 64, 128, 1, 1, 0), (2, 8, 64, 64, 3, 1, 1), (2, 8, 64, 256, 1, 2, 0)])
+def test_fold_gradient_scale(cuda, case):
+    """PRO_FOLD with a per-channel gradient scale gs (the residual join stores ONE
+    gradient; each branch folds in its own BN scale): g*gs + al + be*y in dgrad and wgrad."""
+    N, H, Cin, Cout, k, stride, pad = case
+    torch.manual_seed(3)
+    shp = ci.ConvShape(Cin, Cout, k, stride, pad)
+    w = torch.randn(Cout, Cin, k, k, device=cuda) / (Cin * k * k) ** 0.5
+    wf, wd = ci.alloc_packed(shp, cuda)
+    ci.pack_weights([(w, wf, wd, shp)])
+    Ho, Wo = ci.out_hw(H, H, shp)
+    g = make((N, Ho, Wo, Cout), cuda)
+    y = make((N, Ho, Wo, Cout), cuda)
+    al = torch.randn(Cout, device=cuda) * 0.1
+    be = torch.randn(Cout, device=cuda) * 0.1
+    gs = torch.rand(Cout, device=cuda) + 0.5
+    gt = (g.float() * gs + al + be * y.float()).to(BF).float()
+    xs_shape = (N, H, H, Cin)
+    ref = nhwc(torch.nn.grad.conv2d_input((N, Cin, H, H), w.to(BF).float(), nchw(gt), stride=stride, padding=pad))
+    for ns in (1, 3):
+        out, _ = ci.conv_dgrad(g, y, al, be, wd, shp, xs_shape, epi=ci.EPI_STORE, nsplit=ns, gs=gs)
+        assert rel(out, ref) < 1e-2, ns
+    x = padc(make(xs_shape, cuda), shp.cxp)
+    refw = torch.nn.grad.conv2d_weight(nchw(x.float()[..., :Cin]), (Cout, Cin, k, k), nchw(gt), stride=stride,
+                                       padding=pad)
+    for ns in (1, 2):
+        outw = torch.empty(Cout, Cin, k, k, device=cuda)
+        ci.conv_wgrad(g, y, al, be, x, shp, outw, nsplit=ns, gs=gs)
+        assert rel(outw, refw) < 5e-3, ns
