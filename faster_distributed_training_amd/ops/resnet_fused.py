@@ -43,37 +43,92 @@ MODE_FCBN, MODE_BN_TRAIN, MODE_BN_EVAL = 0, 1, 2
 BF16 = torch.bfloat16
 
 # Parameters whose gradient the engine writes itself call these hooks (the DDP reducer
-# registers here in addition to autograd's post-accumulate-grad hooks).
+# registers here in addition to autograd's post-accumulate-grad hooks).  A "deferrable"
+# hook (the reducer's) takes ``defer=True`` and returns its GPU action (a bucket
+# all-reduce) instead of launching it, so the engine can first join its weight-gradient
+# stream (below) -- and, while capturing, cut the HIP graph there.
 _GRAD_READY_HOOKS: dict[int, list] = {}
 
 
-def register_grad_ready_hook(param, fn):
-    _GRAD_READY_HOOKS.setdefault(id(param), []).append(fn)
+def register_grad_ready_hook(param, fn, deferrable=False):
+    ent = (fn, bool(deferrable))
+    _GRAD_READY_HOOKS.setdefault(id(param), []).append(ent)
 
     class _Handle:
         def remove(self_inner):
             lst = _GRAD_READY_HOOKS.get(id(param), [])
-            if fn in lst:
-                lst.remove(fn)
+            if ent in lst:
+                lst.remove(ent)
     return _Handle()
 
 
-# While a backward is being captured into HIP graphs, hooks run in "defer" mode: they do
-# their bookkeeping and return the GPU action (e.g. a bucket all-reduce) instead of
-# launching it; the recorder then cuts the graph there so the action runs between two
-# graph segments on every replay (communication keeps overlapping backward).
+# While a backward is being captured into HIP graphs, deferrable hooks return their GPU
+# action; the recorder cuts the graph there so the action runs between two graph segments
+# on every replay (communication keeps overlapping backward).
 _RECORDER = None
+
+# Optional (FDT_WGRAD_STREAM=1): weight gradients on a side stream, concurrent with the
+# data-gradient chain (the critical path).  Measured on MI355X (ResNet-50, graphs on):
+# bs 1024 29.2 -> 29.2 ms, bs 128 6.09 -> 6.53 ms -- co-running conv kernels slow each
+# other down (kernel-time sum +18 %) by as much as the overlap saves, so it is off.
+WGRAD_STREAM = os.environ.get("FDT_WGRAD_STREAM", "0") == "1"
+_SIDE_STREAMS: dict = {}
+_GS = None  # the _GradStreams of the backward in progress
+
+
+class _GradStreams:
+    """Fork/join bookkeeping of the weight-gradient side stream for one backward.  Tensors
+    the side stream reads are kept alive until the next join, so the caching allocator
+    cannot hand their memory to main-stream work that might run before the side reads."""
+
+    def __init__(self, main, side):
+        self.main, self.side, self.keep = main, side, []
+        self.pending = False
+
+    def fork(self, *tensors):
+        self.side.wait_stream(self.main)
+        self.keep.extend(t for t in tensors if t is not None)
+        self.pending = True
+
+    def join(self):
+        if self.pending:
+            self.main.wait_stream(self.side)
+            self.keep.clear()
+            self.pending = False
+
+
+def _side_stream(dev):
+    st = _SIDE_STREAMS.get(dev)
+    if st is None:
+        st = _SIDE_STREAMS[dev] = torch.cuda.Stream(device=dev)
+    return st
 
 
 def grad_ready(param):
-    rec = _RECORDER
-    if rec is not None:
-        acts = [a for a in (fn(param, defer=True) for fn in _GRAD_READY_HOOKS.get(id(param), ())) if a is not None]
-        if acts:
-            rec.cut(acts)
+    hooks = _GRAD_READY_HOOKS.get(id(param), ())
+    if not hooks:
         return
-    for fn in _GRAD_READY_HOOKS.get(id(param), ()):
-        fn(param)
+    gs = _GS
+    rec = _RECORDER
+    acts = []
+    for fn, deferrable in hooks:
+        if deferrable:
+            a = fn(param, defer=True)
+            if a is not None:
+                acts.append(a)
+        else:
+            if gs is not None:
+                gs.join()  # a generic hook may read the gradient on the main stream
+            fn(param)
+    if not acts:
+        return
+    if gs is not None:
+        gs.join()  # every gradient of the bucket is complete on the main stream
+    if rec is not None:
+        rec.cut(acts)
+    else:
+        for a in acts:
+            a()
 
 
 def _sp():
@@ -268,7 +323,13 @@ def bwd_finalize(part, nq, ua, sta, ub=None, stb=None, training=True, dev=None):
 def wgrad_into(u: Unit, g, y, al, be, x, xs, xt, act, gs=None):
     if u.w.grad is None:
         u.w.grad = torch.zeros_like(u.w)
-    ci.conv_wgrad(g, y, al, be, x, u.shp, u.w.grad, xs, xt, act[0], act[1], accumulate=True, gs=gs)
+    st = _GS
+    if st is None:
+        ci.conv_wgrad(g, y, al, be, x, u.shp, u.w.grad, xs, xt, act[0], act[1], accumulate=True, gs=gs)
+    else:
+        st.fork(g, y, al, be, x, xs, xt, gs)
+        with torch.cuda.stream(st.side):
+            ci.conv_wgrad(g, y, al, be, x, u.shp, u.w.grad, xs, xt, act[0], act[1], accumulate=True, gs=gs)
     grad_ready(u.w)
 
 
@@ -341,6 +402,18 @@ class ResNetBodyFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, g_out):
+        global _GS
+        if WGRAD_STREAM and g_out.is_cuda:
+            _GS = _GradStreams(torch.cuda.current_stream(), _side_stream(g_out.device))
+        try:
+            return ResNetBodyFn._backward(ctx, g_out)
+        finally:
+            if _GS is not None:
+                _GS.join()
+                _GS = None
+
+    @staticmethod
+    def _backward(ctx, g_out):
         nat = _native.native()
         plan, training = ctx.plan, ctx.training
         g = g_out.contiguous()

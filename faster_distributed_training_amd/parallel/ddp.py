@@ -99,7 +99,7 @@ class BucketReducer:
         # autograd-managed params fire the post-accumulate hook; params whose gradient the
         # fused ResNet engine writes directly fire the engine's grad-ready hook
         self._hooks = [s.param.register_post_accumulate_grad_hook(self._hook) for s in flat.slots]
-        self._hooks += [register_grad_ready_hook(s.param, self._hook) for s in flat.slots]
+        self._hooks += [register_grad_ready_hook(s.param, self._hook, deferrable=True) for s in flat.slots]
         self.enabled = True
         if broadcast_init:
             self.broadcast_parameters()
