@@ -15,6 +15,7 @@
 // contention on the C channel addresses (MI355X_MICROARCH: one-row contention is 14x
 // slower).  All kernels stream 16 B per lane.
 #include "common.h"
+#include "bn_math.h"
 
 namespace fdt {
 
@@ -139,25 +140,15 @@ __device__ __forceinline__ void sum_partials_f64(const float* __restrict__ part,
 
 constexpr int kRedWaves = 16;  // finalize / reduce kernels: 1024 threads per 64-channel tile
 
-// mode 0: FusedConvBN (unbiased var, s = 1/(sqrt(var)+eps), no affine)
-// mode 1: BatchNorm2d train (biased var + eps, affine gamma/beta, running stats update)
-// mode 2: BatchNorm2d eval  (running stats, affine)  -- part unused
-// save_mean[c], save_aux[c]: mode 0 -> sd ; modes 1/2 -> invstd
-// zero_after: re-zero the (slot) rows after reading them, so the next producer can
-// accumulate into the same workspace without a memset launch.
-__global__ __launch_bounds__(64 * kRedWaves) void stats_finalize_kernel(float* __restrict__ part, int nb, int C, double count,
-                                                              int zero_after,
-                                                              int mode, float eps, float momentum,
-                                                              const float* __restrict__ gamma, const float* __restrict__ beta,
-                                                              float* __restrict__ run_mean, float* __restrict__ run_var,
-                                                              long long* __restrict__ nbt, float* __restrict__ out_s,
-                                                              float* __restrict__ out_t, float* __restrict__ save_mean,
-                                                              float* __restrict__ save_aux) {
+// Modes and outputs: bn_math.h.  zero_after: re-zero the (slot) rows after reading them, so
+// the next producer can accumulate into the same workspace without a memset launch.
+__global__ __launch_bounds__(64 * kRedWaves) void stats_finalize_kernel(float* __restrict__ part, int nb, int C,
+                                                                        int zero_after, FinArgs f) {
   __shared__ double sm[kRedWaves][64][2];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int c = blockIdx.x * 64 + lane;
   double acc[2] = {0.0, 0.0};
-  if (c < C && mode != 2) sum_partials_f64<2>(part, nb, C, c, acc, w, kRedWaves);
+  if (c < C && f.mode != 2) sum_partials_f64<2>(part, nb, C, c, acc, w, kRedWaves);
   if (c < C && zero_after) zero_partials<2>(part, nb, C, c, w, kRedWaves);
   sm[w][lane][0] = acc[0];
   sm[w][lane][1] = acc[1];
@@ -166,42 +157,7 @@ __global__ __launch_bounds__(64 * kRedWaves) void stats_finalize_kernel(float* _
   double S = 0.0, Q = 0.0;
 #pragma unroll
   for (int k = 0; k < kRedWaves; ++k) { S += sm[k][lane][0]; Q += sm[k][lane][1]; }
-  if (mode == 0) {
-    double mean = S / count;
-    double var = (Q - S * mean) / (count - 1.0);
-    if (var < 0.0) var = 0.0;
-    double sd = sqrt(var);
-    double sc = 1.0 / (sd + (double)eps);
-    out_s[c] = (float)sc;
-    out_t[c] = (float)(-mean * sc);
-    save_mean[c] = (float)mean;
-    save_aux[c] = (float)sd;
-  } else if (mode == 1) {
-    double mean = S / count;
-    double m2 = Q - S * mean;
-    if (m2 < 0.0) m2 = 0.0;
-    double var_b = m2 / count;
-    double var_u = count > 1.0 ? m2 / (count - 1.0) : var_b;
-    double inv = 1.0 / sqrt(var_b + (double)eps);
-    double g = gamma ? (double)gamma[c] : 1.0, b = beta ? (double)beta[c] : 0.0;
-    out_s[c] = (float)(g * inv);
-    out_t[c] = (float)(b - mean * g * inv);
-    save_mean[c] = (float)mean;
-    save_aux[c] = (float)inv;
-    if (run_mean) {
-      run_mean[c] = (float)((1.0 - momentum) * run_mean[c] + momentum * mean);
-      run_var[c] = (float)((1.0 - momentum) * run_var[c] + momentum * var_u);
-    }
-    if (nbt && c == 0) nbt[0] += 1;
-  } else {
-    double mean = run_mean[c];
-    double inv = 1.0 / sqrt((double)run_var[c] + (double)eps);
-    double g = gamma ? (double)gamma[c] : 1.0, b = beta ? (double)beta[c] : 0.0;
-    out_s[c] = (float)(g * inv);
-    out_t[c] = (float)(b - mean * g * inv);
-    save_mean[c] = (float)mean;
-    save_aux[c] = (float)inv;
-  }
+  bn_finalize_channel(f, c, S, Q);
 }
 
 // ------------------------------------------------------------------ consumer backward
@@ -590,10 +546,11 @@ void channel_stats_partial(uint64_t y, uint64_t part, long M, int C, int dt, uin
 void stats_finalize(uint64_t part, int nb, int C, double count, int mode, float eps, float momentum, uint64_t gamma,
                     uint64_t beta, uint64_t run_mean, uint64_t run_var, uint64_t nbt, uint64_t out_s, uint64_t out_t,
                     uint64_t save_mean, uint64_t save_aux, int zero_after, uint64_t stream) {
-  stats_finalize_kernel<<<(C + 63) / 64, 64 * kRedWaves, 0, as_stream(stream)>>>(
-      P<float>(part), part ? nb : 0, C, count, zero_after, mode, eps, momentum, P<const float>(gamma), P<const float>(beta),
-      P<float>(run_mean), P<float>(run_var), P<long long>(nbt), P<float>(out_s), P<float>(out_t), P<float>(save_mean),
-      P<float>(save_aux));
+  FinArgs f{nullptr, mode, eps, momentum, count, P<const float>(gamma), P<const float>(beta), P<float>(run_mean),
+            P<float>(run_var), P<long long>(nbt), P<float>(out_s), P<float>(out_t), P<float>(save_mean),
+            P<float>(save_aux)};
+  stats_finalize_kernel<<<(C + 63) / 64, 64 * kRedWaves, 0, as_stream(stream)>>>(P<float>(part), part ? nb : 0, C,
+                                                                                 zero_after, f);
   FDT_LAUNCH_CHECK();
 }
 

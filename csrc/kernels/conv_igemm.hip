@@ -42,6 +42,7 @@
 // Reference semantics being accelerated: resnet.py:72-113 (FusedConvBN forward and its
 // hand-derived backward), resnet.py:201-227 (strided conv + BatchNorm2d blocks).
 #include "common.h"
+#include "bn_math.h"
 #include <vector>
 
 namespace fdt {
@@ -81,6 +82,7 @@ struct ConvArgs {
   int8_t dh[12], dw[12], wt[12];
   long Nb_HiWi_Cx_bytes;  // bytes of the activation operand(s)
   long w_bytes;           // bytes of the packed weights
+  FinArgs fin;            // EPI_STATS: fused batch-norm finalize (fin.cnt != nullptr)
 };
 
 __device__ __forceinline__ uint32_t pk_bf16(float lo, float hi) { return pack_bf16x2(lo, hi); }
@@ -507,6 +509,57 @@ __global__ __launch_bounds__(256) void igemm_kernel(const ConvArgs a) {
       const int q = e / BN, c = e - q * BN;
       atomicAdd(&a.part[((long)(bm & (kStatSlots - 1)) * 2 + q) * a.Cout + n0 + c], red[q * BN + c] + red[(2 + q) * BN + c]);
     }
+    if (a.fin.cnt != nullptr) {
+      // Fused finalize: the last of the nbm row tiles of this channel tile to arrive turns
+      // the slot sums of its BN channels into (s, t, save_mean, save_aux) and re-zeroes the
+      // slots -- no separate finalize launch.  Hand-off: every wave drains its (memory-side)
+      // atomics, barrier, one lane releases at agent scope and draws a ticket; the last
+      // arriver acquires and reads the slots with agent-scope atomic loads.
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      int* flag = reinterpret_cast<int*>(red);
+      if (tid == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const int t = __hip_atomic_fetch_add(&a.fin.cnt[bn], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const int last = t == a.nbm - 1;
+        if (last) {
+          __hip_atomic_store(&a.fin.cnt[bn], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        flag[0] = last;
+      }
+      __syncthreads();
+      if (flag[0]) {
+        constexpr int G = 256 / BN;  // slot groups per channel
+        double* dsm = reinterpret_cast<double*>(smem);  // the K-loop tiles are dead here
+        const int c = tid % BN, grp = tid / BN;
+        float* p0 = a.part + n0 + c;
+        double S = 0.0, Q = 0.0;
+        if (a.fin.mode != 2) {
+          for (int sl = grp; sl < kStatSlots; sl += G) {
+            S += (double)__hip_atomic_load(p0 + (long)(2 * sl) * a.Cout, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            Q += (double)__hip_atomic_load(p0 + (long)(2 * sl + 1) * a.Cout, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          }
+        }
+        for (int sl = grp; sl < kStatSlots; sl += G) {
+          p0[(long)(2 * sl) * a.Cout] = 0.f;
+          p0[(long)(2 * sl + 1) * a.Cout] = 0.f;
+        }
+        dsm[2 * tid] = S;
+        dsm[2 * tid + 1] = Q;
+        __syncthreads();
+        if (grp == 0) {
+#pragma unroll
+          for (int k = 1; k < G; ++k) {
+            S += dsm[2 * (k * BN + c)];
+            Q += dsm[2 * (k * BN + c) + 1];
+          }
+          bn_finalize_channel(a.fin, n0 + c, S, Q);
+        }
+      }
+    }
   } else if constexpr (EPI == kEpiActBwd) {
 #pragma unroll
     for (int i = 0; i < TN; ++i) {
@@ -639,9 +692,19 @@ void conv_igemm(uint64_t x, uint64_t x2, uint64_t ps, uint64_t pt, uint64_t pg, 
                 uint64_t ex, uint64_t es, uint64_t et, long Nb, int Hi, int Wi, int Cx, int Ho, int Wo, int S,
                 const std::vector<int>& dh, const std::vector<int>& dw, const std::vector<int>& wt, int Cout, int ldw,
                 int Hout, int Wout, int OS, int oy, int ox, int pro, int pro_act, float pro_alpha, int epi, int epi_act,
-                float epi_alpha, int BM, int BN, int BK, int nsplit, uint64_t slab, uint64_t cnt, uint64_t stream) {
+                float epi_alpha, int BM, int BN, int BK, int nsplit, uint64_t slab, uint64_t cnt,
+                const std::vector<uint64_t>& fin_p, const std::vector<double>& fin_s, uint64_t stream) {
   using namespace conv;
   ConvArgs a{};
+  if (!fin_p.empty()) {
+    // fused finalize: (cnt, gamma, beta, run_mean, run_var, nbt, s, t, save_mean, save_aux),
+    // scalars (mode, eps, momentum, count)
+    FDT_CHECK(fin_p.size() == 10 && fin_s.size() == 4 && epi == kEpiStats && fin_p[0] != 0, "bad fused-finalize args");
+    a.fin = FinArgs{P<int>(fin_p[0]), (int)fin_s[0], (float)fin_s[1], (float)fin_s[2], fin_s[3],
+                    P<const float>(fin_p[1]), P<const float>(fin_p[2]), P<float>(fin_p[3]), P<float>(fin_p[4]),
+                    P<long long>(fin_p[5]), P<float>(fin_p[6]), P<float>(fin_p[7]), P<float>(fin_p[8]),
+                    P<float>(fin_p[9])};
+  }
   a.x = P<const bf16>(x);
   a.x2 = P<const bf16>(x2);
   a.ps = P<const float>(ps);

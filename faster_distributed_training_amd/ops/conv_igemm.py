@@ -188,10 +188,12 @@ def stat_slots(nq: int, C: int, device) -> torch.Tensor:
     return torch.zeros(STAT_SLOTS, nq, C, device=device, dtype=torch.float32)
 
 
-def conv_fwd(x, wf, shp: ConvShape, s=None, t=None, act=0, alpha=1.0, tile=None, part=None, nsplit=None):
+def conv_fwd(x, wf, shp: ConvShape, s=None, t=None, act=0, alpha=1.0, tile=None, part=None, nsplit=None, fin=None):
     """y = conv(act(x*s+t)) (or conv(x) when s is None and act == 0); returns
     (y [N,Ho,Wo,Cout] bf16, part [STAT_SLOTS,2,Cout] fp32 slots whose row sum is
-    (sum y, sum y^2)).  ``part``: a zeroed slot buffer to accumulate into."""
+    (sum y, sum y^2)).  ``part``: a zeroed slot buffer to accumulate into.
+    ``fin`` = (pointer list, scalar list): the epilogue's last arriver per channel tile also
+    finalises the batch-norm statistics (bn_math.h) and re-zeroes ``part``."""
     nat = _native.native()
     N, H, W, C = x.shape
     assert C == shp.cxp and x.dtype == torch.bfloat16 and x.is_contiguous()
@@ -216,7 +218,7 @@ def conv_fwd(x, wf, shp: ConvShape, s=None, t=None, act=0, alpha=1.0, tile=None,
     nat.conv_igemm(x.data_ptr(), 0, _p(s), _p(t), 0, wf.data_ptr(), y.data_ptr(), part.data_ptr(), 0, 0, 0,
                    N, H, W, C, Ho, Wo, shp.stride, list(dh), list(dw), list(wt), shp.cout, shp.ntaps * shp.cxp,
                    Ho, Wo, 1, 0, 0, pro, int(act), float(alpha), EPI_STATS, 0, 1.0, bm, bn, bk, ns, slab_p, cnt_p,
-                   _sp())
+                   fin[0] if fin else [], fin[1] if fin else [], _sp())
     return y, part
 
 
@@ -260,7 +262,7 @@ def conv_dgrad(g, y, al, be, wd, shp: ConvShape, x_shape, epi=EPI_STORE, out=Non
                        out.data_ptr(),
                        _p(part) if epi == EPI_ACTBWD else 0, _p(ex), _p(es), _p(et), N, Hy, Wy, Cy, Ha, Wa, 1,
                        list(dh), list(dw), list(wt), shp.cin, shp.ntaps * shp.cout, Hx, Wx, shp.stride, py, px, pro, 0, 1.0, epi, int(act),
-                       float(alpha), bm, bn, bk, ns, slab_p, cnt_p, _sp())
+                       float(alpha), bm, bn, bk, ns, slab_p, cnt_p, [], [], _sp())
     return out, (part if epi == EPI_ACTBWD else None)
 
 

@@ -224,3 +224,53 @@ def test_fold_gradient_scale(cuda, case):
         outw = torch.empty(Cout, Cin, k, k, device=cuda)
         ci.conv_wgrad(g, y, al, be, x, shp, outw, nsplit=ns, gs=gs)
         assert rel(outw, refw) < 5e-3, ns
+
+
+@pytest.mark.parametrize("case", [(4, 8, 64, 128, 1, 1, 0), (2, 16, 128, 128, 3, 2, 1), (2, 4, 512, 512, 3, 1, 1)])
+@pytest.mark.parametrize("mode", [0, 1])
+def test_conv_fused_finalize(cuda, case, mode):
+    """The conv epilogue's last-arriver batch-norm finalize (fin=...) equals the standalone
+    finalize kernel on the same slot sums, re-zeroes the slots and resets its tickets (mode 0:
+    FusedConvBN; mode 1: BatchNorm2d with running statistics); with and without split-K."""
+    from faster_distributed_training_amd.ops import _native
+    nat = _native.native()
+    N, H, Cin, Cout, k, stride, pad = case
+    torch.manual_seed(4)
+    shp = ci.ConvShape(Cin, Cout, k, stride, pad)
+    x = padc(make((N, H, H, Cin), cuda), shp.cxp)
+    w = torch.randn(Cout, Cin, k, k, device=cuda) / (Cin * k * k) ** 0.5
+    wf, _ = ci.alloc_packed(shp, cuda, dgrad=False)
+    ci.pack_weights([(w, wf, None, shp)])
+    Ho, Wo = ci.out_hw(H, H, shp)
+    M = N * Ho * Wo
+    tickets = torch.zeros(64, device=cuda, dtype=torch.int32)
+    gamma = torch.rand(Cout, device=cuda) + 0.5
+    beta = torch.randn(Cout, device=cuda)
+    for tile, ns in [(None, None), ((64, 64, 64), 3), ((128, 128, 64), 1)]:
+        if tile and Cout % tile[1]:
+            continue
+        rm_a, rv_a = torch.zeros(Cout, device=cuda), torch.ones(Cout, device=cuda)
+        rm_b, rv_b = rm_a.clone(), rv_a.clone()
+        nbt_a = torch.zeros(1, device=cuda, dtype=torch.int64)
+        nbt_b = nbt_a.clone()
+        # reference: plain conv + standalone finalize kernel
+        y, part = ci.conv_fwd(x, wf, shp, tile=tile, nsplit=ns)
+        ref = [torch.empty(Cout, device=cuda) for _ in range(4)]
+        g_b = (gamma, beta, rm_a, rv_a, nbt_a) if mode == 1 else (None,) * 5
+        nat.stats_finalize(part.data_ptr(), part.shape[0], Cout, float(M), mode, 1e-3, 0.1,
+                           *[0 if t is None else t.data_ptr() for t in g_b], *[r.data_ptr() for r in ref], 1,
+                           _native.stream_ptr())
+        # fused
+        outs = [torch.empty(Cout, device=cuda) for _ in range(4)]
+        g_f = (gamma, beta, rm_b, rv_b, nbt_b) if mode == 1 else (None,) * 5
+        ptrs = [tickets.data_ptr()] + [0 if t is None else t.data_ptr() for t in g_f] + [o.data_ptr() for o in outs]
+        part2 = ci.stat_slots(2, Cout, cuda)
+        y2, _ = ci.conv_fwd(x, wf, shp, tile=tile, nsplit=ns, part=part2, fin=(ptrs, [float(mode), 1e-3, 0.1, float(M)]))
+        torch.cuda.synchronize()
+        assert torch.equal(y, y2)
+        for a, b in zip(ref, outs):
+            assert rel(b, a) < 1e-5, (tile, ns)
+        assert torch.count_nonzero(part2).item() == 0, "slots not re-zeroed"
+        assert torch.count_nonzero(tickets).item() == 0, "tickets not reset"
+        if mode == 1:
+            assert rel(rm_b, rm_a) < 1e-5 and rel(rv_b, rv_a) < 1e-5 and nbt_b.item() == 1
