@@ -389,25 +389,18 @@ constexpr int kPackT = 64;  // ci per block
 constexpr int kPackLd = kPackT + 2;
 constexpr int kPackMaxTaps = 9;
 
-__global__ __launch_bounds__(256) void pack_weights_kernel(const PackTable tab) {
-  __shared__ bf16 img[kPackCo * kPackMaxTaps * kPackLd];
-  // binary search the entry of this block
-  int lo = 0, hi = tab.n - 1;
-  while (lo < hi) {
-    int mid = (lo + hi + 1) >> 1;
-    if (tab.e[mid].blk0 <= (long)blockIdx.x) lo = mid; else hi = mid - 1;
-  }
-  const PackEntry& E = tab.e[lo];
-  const int T = E.ntaps;
+// T (taps per kernel: 1, 9, ...) is a compile-time constant in the body, so the per-element
+// index math is multiplies and shifts instead of integer divisions.
+template <int T>
+__device__ __forceinline__ void pack_block(const PackEntry& E, int b, bf16* img) {
   const int nci = (E.Cxp + kPackT - 1) / kPackT;
-  const int b = (int)((long)blockIdx.x - E.blk0);
   const int co0 = (b / nci) * kPackCo, ci0 = (b % nci) * kPackT;
   const int tid = threadIdx.x;
   const int nco = min(kPackCo, E.Cout - co0);
-  const int nci_v = min(kPackT, E.Cxp - ci0);   // columns of the (padded) forward layout
+  const int nci_v = min(kPackT, E.Cxp - ci0);          // columns of the (padded) forward layout
   const int nci_s = max(0, min(kPackT, E.Cin - ci0));  // columns present in the source
   // load: for each co row the source run [ci0, ci0 + nci_s) x T is contiguous
-  const int run = kPackT * T;
+  constexpr int run = kPackT * T;
   for (int e = tid; e < nco * run; e += 256) {
     const int col = e / run, rem = e - col * run;
     const int cl = rem / T, t = rem - cl * T;
@@ -434,6 +427,22 @@ __global__ __launch_bounds__(256) void pack_weights_kernel(const PackTable tab) 
       }
     }
   }
+}
+
+__global__ __launch_bounds__(256) void pack_weights_kernel(const PackTable tab) {
+  __shared__ bf16 img[kPackCo * kPackMaxTaps * kPackLd];
+  // binary search the entry of this block
+  int lo = 0, hi = tab.n - 1;
+  while (lo < hi) {
+    int mid = (lo + hi + 1) >> 1;
+    if (tab.e[mid].blk0 <= (long)blockIdx.x) lo = mid; else hi = mid - 1;
+  }
+  const PackEntry& E = tab.e[lo];
+  const int b = (int)((long)blockIdx.x - E.blk0);
+  if (E.ntaps == 1) pack_block<1>(E, b, img);
+  else if (E.ntaps == 9) pack_block<9>(E, b, img);
+  else if (E.ntaps == 4) pack_block<4>(E, b, img);
+  else pack_block<kPackMaxTaps>(E, b, img);  // unreachable: launcher checks ntaps in {1, 4, 9}
 }
 
 }  // namespace wg
@@ -541,7 +550,7 @@ void pack_weights(const std::vector<uint64_t>& src, const std::vector<uint64_t>&
       E.wd = P<bf16>(wd[i]);
       E.Cout = cout[i]; E.Cin = cin[i]; E.Cxp = cxp[i]; E.ntaps = ntaps[i];
       E.blk0 = blk;
-      FDT_CHECK(E.ntaps <= kPackMaxTaps, "pack_weights: at most 3x3 kernels");
+      FDT_CHECK(E.ntaps == 1 || E.ntaps == 4 || E.ntaps == 9, "pack_weights: 1x1, 2x2 or 3x3 kernels");
       blk += (long)((E.Cout + kPackCo - 1) / kPackCo) * ((E.Cxp + kPackT - 1) / kPackT);
     }
     tab.n = k;

@@ -66,10 +66,14 @@ template <typename T>
 __global__ __launch_bounds__(1024) void mixup_ce_kernel(const T* __restrict__ logits, const int* __restrict__ ya,
                                                         const int* __restrict__ yb, const float* __restrict__ lam,
                                                         float* __restrict__ loss, float* __restrict__ glog,
-                                                        float* __restrict__ dlam, int B, int C) {
-  __shared__ float sm[16];
+                                                        float* __restrict__ dlam, float* __restrict__ meter, int B,
+                                                        int C) {
+  // meter (optional): training accumulators [loss sum, lambda-weighted correct, samples]
+  // updated in place (one block: plain read-modify-write) -- the reference's per-batch
+  // accuracy bookkeeping (resnet50_test.py:550-558) without a dozen separate launches.
+  __shared__ float sm[16], smc[16];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
-  float tot = 0.f;
+  float tot = 0.f, corr = 0.f;
   const float invB = 1.f / (float)B;
   for (int r = w; r < B; r += nw) {
     const T* row = logits + (long)r * C;
@@ -81,6 +85,13 @@ __global__ __launch_bounds__(1024) void mixup_ce_kernel(const T* __restrict__ lo
     se = wave_sum(se);
     const float lse = mx + __logf(se);
     const int a = ya[r], b = yb[r];
+    int am = C;  // argmax, first occurrence (torch.argmax)
+    if (meter) {
+      for (int c = lane; c < C; c += 64)
+        if (to_f(row[c]) == mx) { am = c; break; }
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) am = min(am, __shfl_xor(am, o, 64));
+    }
     const float l = lam[r];
     const float cea = lse - to_f(row[a]), ceb = lse - to_f(row[b]);
     for (int c = lane; c < C; c += 64) {
@@ -91,14 +102,20 @@ __global__ __launch_bounds__(1024) void mixup_ce_kernel(const T* __restrict__ lo
     if (lane == 0) {
       tot += l * cea + (1.f - l) * ceb;
       dlam[r] = (cea - ceb) * invB;
+      corr += (am == a ? l : 0.f) + (am == b ? 1.f - l : 0.f);
     }
   }
-  if (lane == 0) sm[w] = tot;
+  if (lane == 0) { sm[w] = tot; smc[w] = corr; }
   __syncthreads();
   if (threadIdx.x == 0) {
-    float t = 0.f;
-    for (int k = 0; k < nw; ++k) t += sm[k];
+    float t = 0.f, cc = 0.f;
+    for (int k = 0; k < nw; ++k) { t += sm[k]; cc += smc[k]; }
     *loss = t * invB;
+    if (meter) {
+      meter[0] += t * invB;
+      meter[1] += cc;
+      meter[2] += (float)B;
+    }
   }
 }
 
@@ -133,11 +150,11 @@ void mixup_bwd(uint64_t g, uint64_t x, uint64_t perm, uint64_t inv, uint64_t lam
 }
 
 void mixup_ce_fwd(uint64_t logits, uint64_t ya, uint64_t yb, uint64_t lam, uint64_t loss, uint64_t glog, uint64_t dlam,
-                  int B, int C, int dt, uint64_t stream) {
+                  uint64_t meter, int B, int C, int dt, uint64_t stream) {
   DISPATCH_T(dt, {
     mixup_ce_kernel<T><<<1, 1024, 0, as_stream(stream)>>>(P<const T>(logits), P<const int>(ya), P<const int>(yb),
                                                          P<const float>(lam), P<float>(loss), P<float>(glog),
-                                                         P<float>(dlam), B, C);
+                                                         P<float>(dlam), P<float>(meter), B, C);
   });
   FDT_LAUNCH_CHECK();
 }

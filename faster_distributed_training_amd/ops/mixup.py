@@ -173,7 +173,7 @@ class AttentionMixup(nn.Module):
 
 class _MixupCENative(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, logits, ya, yb, lam_vec, weights_mean):
+    def forward(ctx, logits, ya, yb, lam_vec, weights_mean, meter_acc=None):
         nat = _native.native()
         lg = logits.contiguous()
         b, c = lg.shape
@@ -186,7 +186,8 @@ class _MixupCENative(torch.autograd.Function):
         ya32 = ya.to(torch.int32).contiguous()
         yb32 = yb.to(torch.int32).contiguous()
         nat.mixup_ce_fwd(lg.data_ptr(), ya32.data_ptr(), yb32.data_ptr(), lam_vec.data_ptr(), loss.data_ptr(),
-                         glog.data_ptr(), dlam.data_ptr(), b, c, DT[lg.dtype], _native.stream_ptr())
+                         glog.data_ptr(), dlam.data_ptr(), 0 if meter_acc is None else meter_acc.data_ptr(), b, c,
+                         DT[lg.dtype], _native.stream_ptr())
         ctx.save_for_backward(glog, dlam)
         ctx.dt = logits.dtype
         return loss
@@ -195,33 +196,39 @@ class _MixupCENative(torch.autograd.Function):
     def backward(ctx, gl):
         glog, dlam = ctx.saved_tensors
         glam = dlam * gl if ctx.needs_input_grad[3] else None
-        return (glog * gl).to(ctx.dt), None, None, glam, None
+        return (glog * gl).to(ctx.dt), None, None, glam, None, None
 
 
-def mixup_cross_entropy(logits, y_a, y_b, lam_vec):
-    """mean_i [lam_i CE(p_i, ya_i) + (1-lam_i) CE(p_i, yb_i)]."""
+def mixup_cross_entropy(logits, y_a, y_b, lam_vec, meter=None):
+    """mean_i [lam_i CE(p_i, ya_i) + (1-lam_i) CE(p_i, yb_i)].  ``meter``
+    (train.metrics.DeviceMeter): on the HIP path the same kernel also accumulates the
+    step's loss / lambda-weighted accuracy into it (``meter.fused`` is then set)."""
     if (_native.use_native(logits) and logits.dim() == 2 and logits.shape[1] <= 1024
             and logits.dtype in DT and hasattr(_native.native(), "mixup_ce_fwd")):
-        return _MixupCENative.apply(logits, y_a, y_b, lam_vec.float().contiguous(), False)
+        acc = None
+        if meter is not None and getattr(meter, "acc", None) is not None and meter.acc.device == logits.device:
+            acc = meter.acc
+            meter.fused = True
+        return _MixupCENative.apply(logits, y_a, y_b, lam_vec.float().contiguous(), False, acc)
     lf = logits.float()
     ce_a = F.cross_entropy(lf, y_a, reduction="none")
     ce_b = F.cross_entropy(lf, y_b, reduction="none")
     return (lam_vec * ce_a + (1 - lam_vec) * ce_b).mean()
 
 
-def mixup_criterion(criterion, pred, y_a, y_b, lam):
+def mixup_criterion(criterion, pred, y_a, y_b, lam, meter=None):
     """Scalar-lambda criterion (``resnet50_test.py:451-452``).  ``criterion`` is accepted
     for API parity; cross entropy is computed by the fused kernel."""
     lv = torch.full((pred.shape[0],), float(lam), device=pred.device, dtype=torch.float32)
     if criterion is not None and not isinstance(criterion, nn.CrossEntropyLoss):
         return lam * criterion(pred, y_a) + (1 - lam) * criterion(pred, y_b)
-    return mixup_cross_entropy(pred, y_a, y_b, lv)
+    return mixup_cross_entropy(pred, y_a, y_b, lv, meter=meter)
 
 
-def mixup_criterion_meta(criterion, pred, y_a, y_b, lam, faithful=False):
+def mixup_criterion_meta(criterion, pred, y_a, y_b, lam, faithful=False, meter=None):
     """Per-sample-lambda criterion (``resnet50_test.py:455-457``); see module doc (Q4)."""
     b = pred.shape[0]
     lv = lam.reshape(b).float()
     if faithful:
         lv = lv.mean().expand(b).contiguous()
-    return mixup_cross_entropy(pred, y_a, y_b, lv)
+    return mixup_cross_entropy(pred, y_a, y_b, lv, meter=meter)

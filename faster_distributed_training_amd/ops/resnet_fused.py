@@ -556,7 +556,7 @@ def resnet_engine_forward(model, x):
         body = _BodyWithDummy.apply(xin, dummy, plan, model.training)
     else:
         body = ResNetBodyFn.forward(_NoCtx(), xin, plan, model.training, False)
-    pooled = body.float().mean(dim=(1, 2))
+    pooled = body.mean(dim=(1, 2), dtype=torch.float32)  # fp32 accumulation, no fp32 copy of the body
     return model.fc(pooled)
 
 

@@ -21,34 +21,53 @@ from ..utils.env import is_rank0
 
 
 class DeviceMeter:
+    """Device-side training accumulators [loss sum, correct, samples]: no host sync per step.
+    The fused mixup cross-entropy kernel can add into ``acc`` itself (sets ``fused``); then
+    ``update`` only counts the step."""
+
     def __init__(self, device):
         self.device = device
         self.reset()
 
     def reset(self):
-        self.loss = torch.zeros((), device=self.device, dtype=torch.float32)
-        self.correct = torch.zeros((), device=self.device, dtype=torch.float32)
-        self.total = torch.zeros((), device=self.device, dtype=torch.float32)
+        self.acc = torch.zeros(3, device=self.device, dtype=torch.float32)
         self.steps = 0
+        self.fused = False
+
+    @property
+    def loss(self):
+        return self.acc[0]
+
+    @property
+    def correct(self):
+        return self.acc[1]
+
+    @property
+    def total(self):
+        return self.acc[2]
 
     @torch.no_grad()
     def update(self, loss, logits, y_a, y_b=None, lam=1.0):
+        self.steps += 1
+        if self.fused:  # the loss kernel already accumulated this step
+            self.fused = False
+            return
         pred = logits.argmax(1)
-        self.loss += loss.detach().float()
         if y_b is None:
-            self.correct += (pred == y_a).sum().float()
+            corr = (pred == y_a).sum().float()
         elif isinstance(lam, torch.Tensor) and lam.numel() > 1:
             lv = lam.reshape(-1).float()
-            self.correct += (lv * (pred == y_a).float()).sum() + ((1 - lv) * (pred == y_b).float()).sum()
+            corr = (lv * (pred == y_a).float()).sum() + ((1 - lv) * (pred == y_b).float()).sum()
         else:
             lv = float(lam)
-            self.correct += lv * (pred == y_a).sum().float() + (1 - lv) * (pred == y_b).sum().float()
-        self.total += float(logits.shape[0])
-        self.steps += 1
+            corr = lv * (pred == y_a).sum().float() + (1 - lv) * (pred == y_b).sum().float()
+        self.acc[0] += loss.detach().float().reshape(())
+        self.acc[1] += corr
+        self.acc[2] += float(logits.shape[0])
 
     def reduced(self):
         from ..parallel.dist import all_reduce_metrics
-        t = torch.stack([self.loss, self.correct, self.total])
+        t = self.acc.clone()
         all_reduce_metrics(t)
         loss, correct, total = t.tolist()
         from ..parallel.dist import world

@@ -211,9 +211,9 @@ class ResNetTrainer:
         with self._autocast():
             out = self.model(x)
             if self.meta is not None:
-                loss = mixup_criterion_meta(None, out, ya, yb, lam, faithful=cfg.faithful)
+                loss = mixup_criterion_meta(None, out, ya, yb, lam, faithful=cfg.faithful, meter=self.meter)
             else:
-                loss = mixup_criterion(None, out, ya, yb, lam)
+                loss = mixup_criterion(None, out, ya, yb, lam, meter=self.meter)
         self.scaler.scale_loss(loss).backward()
         if self.reducer is not None:
             self.reducer.finish()
