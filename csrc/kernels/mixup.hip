@@ -62,7 +62,9 @@ __global__ __launch_bounds__(256) void mixup_bwd_kernel(const T* __restrict__ g,
   }
 }
 
-template <typename T>
+// One row per THREAD when C <= 64 (CIFAR: 10 classes -- a wave per row would idle 54 of
+// its 64 lanes and serialise B/16 rows per wave), one row per WAVE otherwise.
+template <typename T, bool ROW_PER_THREAD>
 __global__ __launch_bounds__(1024) void mixup_ce_kernel(const T* __restrict__ logits, const int* __restrict__ ya,
                                                         const int* __restrict__ yb, const float* __restrict__ lam,
                                                         float* __restrict__ loss, float* __restrict__ glog,
@@ -75,34 +77,63 @@ __global__ __launch_bounds__(1024) void mixup_ce_kernel(const T* __restrict__ lo
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
   float tot = 0.f, corr = 0.f;
   const float invB = 1.f / (float)B;
-  for (int r = w; r < B; r += nw) {
-    const T* row = logits + (long)r * C;
-    float mx = -INFINITY;
-    for (int c = lane; c < C; c += 64) mx = fmaxf(mx, to_f(row[c]));
-    mx = wave_max(mx);
-    float se = 0.f;
-    for (int c = lane; c < C; c += 64) se += __expf(to_f(row[c]) - mx);
-    se = wave_sum(se);
-    const float lse = mx + __logf(se);
-    const int a = ya[r], b = yb[r];
-    int am = C;  // argmax, first occurrence (torch.argmax)
-    if (meter) {
-      for (int c = lane; c < C; c += 64)
-        if (to_f(row[c]) == mx) { am = c; break; }
-#pragma unroll
-      for (int o = 32; o > 0; o >>= 1) am = min(am, __shfl_xor(am, o, 64));
-    }
-    const float l = lam[r];
-    const float cea = lse - to_f(row[a]), ceb = lse - to_f(row[b]);
-    for (int c = lane; c < C; c += 64) {
-      float p = __expf(to_f(row[c]) - lse);
-      float t = (c == a ? l : 0.f) + (c == b ? 1.f - l : 0.f);
-      glog[(long)r * C + c] = (p - t) * invB;
-    }
-    if (lane == 0) {
+  if constexpr (ROW_PER_THREAD) {
+    for (int r = threadIdx.x; r < B; r += blockDim.x) {
+      const T* row = logits + (long)r * C;
+      // (the row is re-read from L1 per pass: a runtime-indexed register array would spill)
+      float mx = -INFINITY;
+      int am = 0;
+      for (int c = 0; c < C; ++c) {
+        const float x = to_f(row[c]);
+        if (x > mx) { mx = x; am = c; }  // strict >: first occurrence (torch.argmax)
+      }
+      float se = 0.f;
+      for (int c = 0; c < C; ++c) se += __expf(to_f(row[c]) - mx);
+      const float lse = mx + __logf(se);
+      const int a = ya[r], b = yb[r];
+      const float l = lam[r];
+      const float cea = lse - to_f(row[a]), ceb = lse - to_f(row[b]);
+      for (int c = 0; c < C; ++c) {
+        const float p = __expf(to_f(row[c]) - lse);
+        const float t = (c == a ? l : 0.f) + (c == b ? 1.f - l : 0.f);
+        glog[(long)r * C + c] = (p - t) * invB;
+      }
       tot += l * cea + (1.f - l) * ceb;
       dlam[r] = (cea - ceb) * invB;
       corr += (am == a ? l : 0.f) + (am == b ? 1.f - l : 0.f);
+    }
+    tot = wave_sum(tot);
+    corr = wave_sum(corr);
+  } else {
+    for (int r = w; r < B; r += nw) {
+      const T* row = logits + (long)r * C;
+      float mx = -INFINITY;
+      for (int c = lane; c < C; c += 64) mx = fmaxf(mx, to_f(row[c]));
+      mx = wave_max(mx);
+      float se = 0.f;
+      for (int c = lane; c < C; c += 64) se += __expf(to_f(row[c]) - mx);
+      se = wave_sum(se);
+      const float lse = mx + __logf(se);
+      const int a = ya[r], b = yb[r];
+      int am = C;  // argmax, first occurrence (torch.argmax)
+      if (meter) {
+        for (int c = lane; c < C; c += 64)
+          if (to_f(row[c]) == mx) { am = c; break; }
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) am = min(am, __shfl_xor(am, o, 64));
+      }
+      const float l = lam[r];
+      const float cea = lse - to_f(row[a]), ceb = lse - to_f(row[b]);
+      for (int c = lane; c < C; c += 64) {
+        float p = __expf(to_f(row[c]) - lse);
+        float t = (c == a ? l : 0.f) + (c == b ? 1.f - l : 0.f);
+        glog[(long)r * C + c] = (p - t) * invB;
+      }
+      if (lane == 0) {
+        tot += l * cea + (1.f - l) * ceb;
+        dlam[r] = (cea - ceb) * invB;
+        corr += (am == a ? l : 0.f) + (am == b ? 1.f - l : 0.f);
+      }
     }
   }
   if (lane == 0) { sm[w] = tot; smc[w] = corr; }
@@ -152,9 +183,14 @@ void mixup_bwd(uint64_t g, uint64_t x, uint64_t perm, uint64_t inv, uint64_t lam
 void mixup_ce_fwd(uint64_t logits, uint64_t ya, uint64_t yb, uint64_t lam, uint64_t loss, uint64_t glog, uint64_t dlam,
                   uint64_t meter, int B, int C, int dt, uint64_t stream) {
   DISPATCH_T(dt, {
-    mixup_ce_kernel<T><<<1, 1024, 0, as_stream(stream)>>>(P<const T>(logits), P<const int>(ya), P<const int>(yb),
-                                                         P<const float>(lam), P<float>(loss), P<float>(glog),
-                                                         P<float>(dlam), P<float>(meter), B, C);
+    if (C <= 64)
+      mixup_ce_kernel<T, true><<<1, 1024, 0, as_stream(stream)>>>(P<const T>(logits), P<const int>(ya), P<const int>(yb),
+                                                                  P<const float>(lam), P<float>(loss), P<float>(glog),
+                                                                  P<float>(dlam), P<float>(meter), B, C);
+    else
+      mixup_ce_kernel<T, false><<<1, 1024, 0, as_stream(stream)>>>(P<const T>(logits), P<const int>(ya), P<const int>(yb),
+                                                                   P<const float>(lam), P<float>(loss), P<float>(glog),
+                                                                   P<float>(dlam), P<float>(meter), B, C);
   });
   FDT_LAUNCH_CHECK();
 }

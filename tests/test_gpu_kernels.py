@@ -77,19 +77,23 @@ def test_mixup_kernels(cuda):
     assert abs(loss.item() - ref.item()) < 1e-5 and rel(logits.grad, l2.grad) < 1e-5
 
 
-def test_mixup_ce_fused_meter(cuda):
+@pytest.mark.parametrize("C", [10, 100])
+def test_mixup_ce_fused_meter(cuda, C):
     """The loss kernel's fused accuracy/loss accumulation equals DeviceMeter's own update
     (argmax first occurrence, lambda-weighted correct, samples), over two steps."""
     from faster_distributed_training_amd.ops.mixup import mixup_cross_entropy
     from faster_distributed_training_amd.train.metrics import DeviceMeter
     fused, plain = DeviceMeter(cuda), DeviceMeter(cuda)
     for step in range(2):
-        logits = torch.randn(96, 10, device=cuda).to(torch.bfloat16)
+        logits = torch.randn(96, C, device=cuda).to(torch.bfloat16)
         logits[:8] = 0.0  # ties: argmax must pick the first index
-        ya, yb = torch.randint(0, 10, (96,), device=cuda), torch.randint(0, 10, (96,), device=cuda)
+        ya, yb = torch.randint(0, C, (96,), device=cuda), torch.randint(0, C, (96,), device=cuda)
         lv = torch.rand(96, device=cuda)
         loss = mixup_cross_entropy(logits, ya, yb, lv, meter=fused)
         assert fused.fused
+        ref = (lv * F.cross_entropy(logits.float(), ya, reduction="none")
+               + (1 - lv) * F.cross_entropy(logits.float(), yb, reduction="none")).mean()
+        assert abs(loss.item() - ref.item()) < 1e-4
         fused.update(loss, logits, ya, yb, lv)
         plain.update(loss, logits, ya, yb, lv)
     assert fused.steps == plain.steps == 2
