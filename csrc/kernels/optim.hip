@@ -23,6 +23,13 @@ inline int opt_grid(long n4) {
 }
 
 __device__ __forceinline__ bool skip_step(const int* found_inf) { return found_inf && *found_inf != 0; }
+
+// A skipped (non-finite / fp16-overflow) step still clears the gradient when the optimizer
+// owns zero_grad: otherwise the bad values would accumulate into every following step.
+__device__ __forceinline__ void skip_zero(float* __restrict__ g, long n, int zero_grad) {
+  if (!zero_grad) return;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) g[i] = 0.f;
+}
 __device__ __forceinline__ float gscale(const float* p) { return p ? *p : 1.f; }
 
 __device__ __forceinline__ void store_shadow(bf16* sh, long i, float4 v) {
@@ -85,7 +92,7 @@ __global__ __launch_bounds__(kOB) void sgd_kernel(float* __restrict__ p, float* 
                                                   float dampening, float wd, int nesterov, int first,
                                                   const float* __restrict__ gsc, const int* __restrict__ found_inf,
                                                   int zero_grad) {
-  if (skip_step(found_inf)) return;
+  if (skip_step(found_inf)) { skip_zero(g, n4 * 4, zero_grad); return; }
   const float c = gscale(gsc);
   float4* p4 = reinterpret_cast<float4*>(p);
   float4* g4 = reinterpret_cast<float4*>(g);
@@ -124,7 +131,7 @@ __global__ __launch_bounds__(kOB) void madgrad_kernel(float* __restrict__ p, flo
                                                       float wd, float eps, int decouple, long k,
                                                       const float* __restrict__ gsc, const int* __restrict__ found_inf,
                                                       int zero_grad) {
-  if (skip_step(found_inf)) return;
+  if (skip_step(found_inf)) { skip_zero(g, n4 * 4, zero_grad); return; }
   const float c = gscale(gsc);
   const float lr_e = lr + eps;
   const float lamb = lr_e * sqrtf((float)(k + 1));
@@ -158,7 +165,7 @@ __global__ __launch_bounds__(kOB) void mirror_madgrad_kernel(float* __restrict__
                                                              float wd, float eps, int decouple, long k,
                                                              const float* __restrict__ gsc,
                                                              const int* __restrict__ found_inf, int zero_grad) {
-  if (skip_step(found_inf)) return;
+  if (skip_step(found_inf)) { skip_zero(g, n, zero_grad); return; }
   const float c = gscale(gsc);
   const float lr_e = lr + eps;
   const float lamb = lr_e * sqrtf((float)(k + 1));
@@ -186,7 +193,7 @@ __global__ __launch_bounds__(kOB) void adam_kernel(float* __restrict__ p, float*
                                                    float b1, float b2, float eps, float wd, int adamw, long step,
                                                    const float* __restrict__ gsc, const int* __restrict__ found_inf,
                                                    int zero_grad) {
-  if (skip_step(found_inf)) return;
+  if (skip_step(found_inf)) { skip_zero(g, n, zero_grad); return; }
   const float c = gscale(gsc);
   const float bc1 = 1.f - powf(b1, (float)step), bc2 = 1.f - powf(b2, (float)step);
   for (long i = (long)blockIdx.x * kOB + threadIdx.x; i < n; i += (long)gridDim.x * kOB) {

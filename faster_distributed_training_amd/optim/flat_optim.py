@@ -91,6 +91,8 @@ class FlatOptimizer(torch.optim.Optimizer):
 
     def _cpu_common(self, grad_scale, found_inf):
         if found_inf is not None and bool(found_inf.item() != 0):
+            if self.zero_grad_in_step:  # a skipped step still clears the gradient
+                self.flat.grad.zero_()
             return None
         g = self.flat.grad
         if grad_scale is not None:

@@ -180,7 +180,9 @@ class NGState:
 
     def load_state_dict(self, sd):
         self.t = int(sd["t"])
-        self.W, self.d, self.rho = sd["W"], sd["d"], sd["rho"]
+        def mv(v):
+            return v.to(self.device) if isinstance(v, torch.Tensor) else v
+        self.W, self.d, self.rho = mv(sd["W"]), mv(sd["d"]), mv(sd["rho"])
 
 
 class OnlineNaturalGradient:
@@ -268,7 +270,9 @@ class NGD(SGD):
     def _step(self, grad_scale, found_inf, d_override=None):
         g = self.group
         if found_inf is not None and bool(found_inf.item() != 0):
-            return  # GradScaler skip (fp16 mode only; bf16 training has no scaler)
+            if self.zero_grad_in_step:  # GradScaler skip (fp16 mode only); still clear the gradient
+                self.flat.grad.zero_()
+            return
         grad = self.flat.grad
         if grad_scale is not None:
             grad.mul_(grad_scale)
@@ -294,3 +298,15 @@ class NGD(SGD):
         if self.groups is None:
             return []
         return [[st.state_dict() for _, st in sg.axes] for sg, _ in self.groups]
+
+    def load_ngd_state_dict(self, sd):
+        """Restore per-axis preconditioner states saved by ``ngd_state_dict`` (same model)."""
+        if not sd:
+            return
+        if self.groups is None:
+            self._build_groups()
+        if len(sd) != len(self.groups):
+            raise ValueError("NGD state was saved for a different model")
+        for (sg, _), axes_sd in zip(self.groups, sd):
+            for (_, st), s in zip(sg.axes, axes_sd):
+                st.load_state_dict(s)

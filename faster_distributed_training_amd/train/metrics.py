@@ -144,3 +144,81 @@ def draw_graph(xs, ys, labels, title, metric, out_dir="."):
     plt.savefig(path)
     plt.close()
     return path
+
+
+class PhaseProfiler:
+    """``--profile_steps K`` (survey §5 tracing): per-phase device time of the first K train
+    steps from HIP events (one synchronisation at the end, none inside the steps), plus
+    roctx ranges around each phase so a ``rocprofv3 --marker-trace`` / timeline shows the
+    phase structure.  Phases are marked in order by the trainer: ``mark("fwd")`` etc."""
+
+    def __init__(self, steps: int, cuda: bool, logger=None):
+        self.steps, self.cuda, self.logger = int(steps), cuda, logger
+        self.done = 0
+        self.records = []  # per step: [(phase, start_event, end_event)]
+        self._cur = None
+        self._open = None
+        try:
+            from torch.cuda import nvtx  # roctx on ROCm builds
+            self._nvtx = nvtx if cuda else None
+        except Exception:  # noqa: BLE001 - tracing is optional
+            self._nvtx = None
+
+    @property
+    def active(self):
+        return self.done < self.steps
+
+    def _event(self):
+        e = torch.cuda.Event(enable_timing=True) if self.cuda else None
+        if e is not None:
+            e.record()
+        return e if e is not None else time.perf_counter()
+
+    def begin_step(self):
+        if not self.active:
+            return
+        self._cur = []
+        self._open = None
+
+    def mark(self, phase: str):
+        """Close the open phase (if any) and open ``phase``."""
+        if not self.active or self._cur is None:
+            return
+        now = self._event()
+        if self._open is not None:
+            self._cur.append((self._open[0], self._open[1], now))
+            if self._nvtx is not None:
+                self._nvtx.range_pop()
+        self._open = (phase, now)
+        if self._nvtx is not None:
+            self._nvtx.range_push(phase)
+
+    def end_step(self):
+        if not self.active or self._cur is None:
+            return
+        self.mark("_end")
+        if self._nvtx is not None:
+            self._nvtx.range_pop()
+        self.records.append(self._cur)
+        self._cur = None
+        self.done += 1
+        if self.done == self.steps:
+            self.report()
+
+    def summary(self):
+        if self.cuda:
+            torch.cuda.synchronize()
+        tot = {}
+        for rec in self.records:
+            for ph, a, b in rec:
+                ms = a.elapsed_time(b) if self.cuda else (b - a) * 1e3
+                tot[ph] = tot.get(ph, 0.0) + ms
+        n = max(1, len(self.records))
+        return {ph: round(v / n, 4) for ph, v in tot.items()}
+
+    def report(self):
+        s = self.summary()
+        from ..utils.env import print0
+        print0("profile (device ms/step over %d steps): %s" % (len(self.records), json.dumps(s)))
+        if self.logger is not None:
+            self.logger.log(profile_ms_per_step=s, profile_steps=len(self.records))

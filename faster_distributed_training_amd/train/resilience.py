@@ -1,0 +1,122 @@
+"""Failure handling around the training loop (survey §5: failure detection / checkpoint-
+resume; the reference only keeps a best-accuracy, weights-only checkpoint and relies on
+GradScaler's inf skip, resnet50_test.py:541-548, 664-690).
+
+* ``save_last`` / ``restore_last``: a rolling full-state checkpoint (``*_last.pth``) written
+  at the end of every epoch by rank 0 -- model (reference schema, so the reference loader
+  reads it), optimizer (flat state incl. NGD preconditioners), scheduler, loss scaler,
+  best accuracy, global step, and every RNG stream (python, numpy, torch CPU / device, the
+  device data loader's counter RNG) so a resumed run continues the same random sequence.
+  Loads use ``weights_only=True``; numpy/python RNG states are stored as tensors/ints.
+* ``--auto_resume``: at start-up a trainer restores ``*_last.pth`` if present and continues
+  with the next epoch -- combined with ``torchrun --max-restarts N`` (run_distributed.sh)
+  a crashed or killed rank restarts the job from the last completed epoch.
+* ``maybe_inject_fault``: fault-injection hook for tests (``FDT_FAULT_STEP=k`` raises on
+  global step k, optionally only on ``FDT_FAULT_RANK``).
+* Non-finite gradients (the device-side check in ``GradClipper``) make the optimizer
+  kernels skip the update without a host sync; trainers count skipped steps per epoch.
+"""
+from __future__ import annotations
+
+import os
+import random
+
+import numpy as np
+import torch
+
+from . import checkpoint as ckpt
+
+
+class InjectedFault(RuntimeError):
+    pass
+
+
+def maybe_inject_fault(global_step: int, rank: int = 0):
+    s = os.environ.get("FDT_FAULT_STEP")
+    if s is None or int(s) != global_step:
+        return
+    r = os.environ.get("FDT_FAULT_RANK")
+    if r is not None and int(r) != rank:
+        return
+    raise InjectedFault(f"injected fault at step {global_step} on rank {rank}")
+
+
+def last_path(best_path: str) -> str:
+    root, ext = os.path.splitext(best_path)
+    return root.replace("_ckpt", "") + "_last" + ext
+
+
+def _rng_state(trainer):
+    py = random.getstate()
+    npst = np.random.get_state()
+    st = {"py_version": int(py[0]), "py_state": torch.tensor(py[1], dtype=torch.int64),
+          "np_keys": torch.from_numpy(np.asarray(npst[1], dtype=np.int64)), "np_pos": int(npst[2]),
+          "np_has_gauss": int(npst[3]), "np_gauss": float(npst[4]),
+          "torch_cpu": torch.get_rng_state()}
+    if torch.cuda.is_available() and trainer.device.type == "cuda":
+        st["torch_cuda"] = torch.cuda.get_rng_state(trainer.device)
+    ld = getattr(trainer, "train_loader", None)
+    if ld is not None and isinstance(getattr(ld, "rng", None), torch.Tensor):
+        st["loader_rng"] = ld.rng.detach().cpu()
+    if ld is not None and isinstance(getattr(ld, "_cpu_gen", None), torch.Generator):
+        st["loader_cpu_gen"] = ld._cpu_gen.get_state()
+    return st
+
+
+def _set_rng_state(trainer, st):
+    random.setstate((st["py_version"], tuple(int(v) for v in st["py_state"].tolist()), None))
+    np.random.set_state(("MT19937", st["np_keys"].numpy().astype(np.uint32), st["np_pos"], st["np_has_gauss"],
+                         st["np_gauss"]))
+    torch.set_rng_state(st["torch_cpu"])
+    if "torch_cuda" in st and trainer.device.type == "cuda":
+        torch.cuda.set_rng_state(st["torch_cuda"], trainer.device)
+    ld = getattr(trainer, "train_loader", None)
+    if ld is not None and "loader_rng" in st:
+        ld.rng.copy_(st["loader_rng"].to(ld.rng.device))
+    if ld is not None and "loader_cpu_gen" in st:
+        ld._cpu_gen.set_state(st["loader_cpu_gen"])
+
+
+def save_last(trainer, epoch: int):
+    """Full training state after ``epoch`` completed (rank 0 writes, all ranks barrier)."""
+    extra = {"optimizer": trainer.optimizer.state_dict(), "global_step": int(trainer.global_step),
+             "best_acc": float(trainer.best_acc), "rng": _rng_state(trainer), "last": True}
+    if getattr(trainer, "scheduler", None) is not None:
+        extra["scheduler"] = trainer.scheduler.state_dict()
+    if getattr(trainer, "scaler", None) is not None:
+        extra["scaler"] = trainer.scaler.state_dict()
+    ngd = getattr(trainer.optimizer, "ngd_state_dict", None)
+    if ngd is not None:
+        extra["ngd"] = ngd()
+    meta = getattr(trainer, "meta", None)
+    if meta is not None:
+        extra["meta"] = {k: v.detach().cpu() for k, v in meta.state_dict().items()}
+    acc = trainer.testing_acc[-1] if getattr(trainer, "testing_acc", None) else 0.0
+    ckpt.save_checkpoint(trainer.last_path, trainer.model, acc, epoch, module_prefix=False, extra=extra)
+
+
+def restore_last(trainer) -> bool:
+    """Restore ``trainer.last_path`` if it exists; sets ``start_epoch`` to the epoch after
+    the saved one.  Returns whether a checkpoint was restored."""
+    path = trainer.last_path
+    if not os.path.isfile(path):
+        return False
+    ck = ckpt.load_checkpoint(path)
+    ckpt.load_model_state(trainer.model, ck["net"])
+    if hasattr(trainer.flat, "refresh_shadow"):
+        trainer.flat.refresh_shadow()
+    trainer.optimizer.load_state_dict(ck["optimizer"])
+    if "ngd" in ck and hasattr(trainer.optimizer, "load_ngd_state_dict"):
+        trainer.optimizer.load_ngd_state_dict(ck["ngd"])
+    if "scheduler" in ck and getattr(trainer, "scheduler", None) is not None:
+        trainer.scheduler.load_state_dict(ck["scheduler"])
+    if "scaler" in ck and getattr(trainer, "scaler", None) is not None:
+        trainer.scaler.load_state_dict(ck["scaler"])
+    if "meta" in ck and getattr(trainer, "meta", None) is not None:
+        trainer.meta.load_state_dict(ck["meta"])
+    trainer.global_step = int(ck.get("global_step", 0))
+    trainer.best_acc = max(float(trainer.best_acc), float(ck.get("best_acc", 0.0)))
+    trainer.start_epoch = int(ck["epoch"]) + 1
+    if "rng" in ck:
+        _set_rng_state(trainer, ck["rng"])
+    return True

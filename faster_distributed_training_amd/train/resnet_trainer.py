@@ -28,7 +28,8 @@ from ..parallel import dist as pdist
 from ..utils.env import default_device, print0, seed_everything
 from ..utils.flat import FlatParams
 from . import checkpoint as ckpt
-from .metrics import DeviceMeter, JsonlLogger, StepTimer, draw_graph, peak_memory_gb
+from . import resilience
+from .metrics import DeviceMeter, JsonlLogger, PhaseProfiler, draw_graph, peak_memory_gb
 
 
 @dataclass
@@ -67,6 +68,10 @@ class ResNetConfig:
     workers: int = 2                   # accepted for CLI parity (no worker processes needed)
     fast_path: bool | None = None      # None = HIP engine when on GPU
     graphs: bool = True                # run the engine body as captured HIP graphs (train steps)
+    auto_resume: bool = False          # restore *_last.pth (full state) if present; implies save_last
+    save_last: bool = False            # write the rolling full-state *_last.pth every epoch
+    nonfinite_guard: bool = True       # skip (on device) optimizer steps whose gradients are not finite
+    profile_steps: int = 0             # per-phase device timing (+ roctx ranges) of the first K steps
     extra: dict = field(default_factory=dict)
 
 
@@ -119,11 +124,19 @@ class ResNetTrainer:
         self.logger = JsonlLogger(cfg.log_path)
         self.training_acc, self.testing_acc, self.epoch_time = [], [], []
         self.global_step = 0
+        self.skipped = torch.zeros((), device=self.device, dtype=torch.int32)  # non-finite steps
+        self.profiler = PhaseProfiler(cfg.profile_steps, self.device.type == "cuda", self.logger)
+        if cfg.auto_resume and resilience.restore_last(self):
+            print0(f"auto-resume: restored {self.last_path}, continuing at epoch {self.start_epoch}")
 
     # ------------------------------------------------------------------ setup
     @property
     def ckpt_path(self):
         return os.path.join(self.cfg.checkpoint_dir, "resnet_ckpt.pth")
+
+    @property
+    def last_path(self):
+        return resilience.last_path(self.ckpt_path)
 
     def _lr(self):
         lr = self.cfg.lr
@@ -204,33 +217,49 @@ class ResNetTrainer:
 
     def train_step(self, x, y):
         cfg = self.cfg
+        prof = self.profiler
+        resilience.maybe_inject_fault(self.global_step, self.rank)
+        prof.begin_step()
+        prof.mark("mixup")
         if self.meta is not None:
             x, ya, yb, lam = self.meta(x, y)
         else:
             x, ya, yb, lam = mixup_data(x, y, cfg.alpha)
+        prof.mark("forward")
         with self._autocast():
             out = self.model(x)
+            prof.mark("loss")
             if self.meta is not None:
                 loss = mixup_criterion_meta(None, out, ya, yb, lam, faithful=cfg.faithful, meter=self.meter)
             else:
                 loss = mixup_criterion(None, out, ya, yb, lam, meter=self.meter)
+        prof.mark("backward")
         self.scaler.scale_loss(loss).backward()
+        prof.mark("grad_sync")
         if self.reducer is not None:
             self.reducer.finish()
         if self.fsdp is not None:
             self.fsdp.finish_backward()
+        prof.mark("optimizer")
         fp16 = self.scaler.enabled
-        self.clipper(cfg.clip, inv_scale=self.scaler.inv_scale(), check_inf=fp16)
-        found = None
-        if fp16:
+        # device-side non-finite check (same kernel as the norm): the optimizer kernels skip
+        # the update on a bad step, no host sync (NGD checks on the host: fp16 only)
+        guard = cfg.nonfinite_guard and not isinstance(self.optimizer, NGD)
+        check = fp16 or guard
+        self.clipper(cfg.clip, inv_scale=self.scaler.inv_scale(), check_inf=check)
+        found = self.clipper.found_inf if check else None
+        if fp16 or (check and self.fsdp is not None):
+            # fp16 / sharded gradients: every rank must take the same decision
             self.scaler.sync_found_inf(self.clipper.found_inf)
-            found = self.clipper.found_inf
         self.optimizer.step(grad_scale=self.clipper.coef, found_inf=found)
         if fp16:
             self.scaler.update(found)
+        if guard:
+            self.skipped += found.reshape(())
         if self.fsdp is not None:
             self.fsdp.after_step()
         self.meter.update(loss, out.detach(), ya, yb, lam.detach() if isinstance(lam, torch.Tensor) else lam)
+        prof.end_step()
         self.global_step += 1
         return loss
 
@@ -256,7 +285,9 @@ class ResNetTrainer:
         m = self.meter.reduced()
         imgs = n * self.cfg.bs * self.world
         rec = dict(epoch=epoch, steps=n, epoch_time_s=dt, img_per_s=imgs / max(dt, 1e-9), train_loss=m["loss"],
-                   train_acc=m["acc"], peak_mem_gb=peak_memory_gb(), lr=self.optimizer.group["lr"])
+                   train_acc=m["acc"], peak_mem_gb=peak_memory_gb(), lr=self.optimizer.group["lr"],
+                   skipped_steps=int(self.skipped.item()))
+        self.skipped.zero_()
         print0(f"epoch {epoch}: {n} steps in {dt:.2f}s ({rec['img_per_s']:.0f} img/s) loss {m['loss']:.4f} "
                f"acc {m['acc']:.2f}%  peak mem {rec['peak_mem_gb']:.2f} GB")
         self.logger.log(**rec)
@@ -295,6 +326,8 @@ class ResNetTrainer:
                 self.test(epoch)
             if self.scheduler is not None:
                 self.scheduler.step()
+            if self.cfg.save_last or self.cfg.auto_resume:
+                resilience.save_last(self, epoch)
         if self.cfg.plot:
             xs = np.arange(self.start_epoch, self.start_epoch + len(self.training_acc))
             if self.testing_acc:

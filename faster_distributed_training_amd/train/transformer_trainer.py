@@ -31,7 +31,8 @@ from ..parallel import dist as pdist
 from ..utils.env import default_device, print0, seed_everything
 from ..utils.flat import FlatParams
 from . import checkpoint as ckpt
-from .metrics import DeviceMeter, JsonlLogger, draw_graph, peak_memory_gb
+from . import resilience
+from .metrics import DeviceMeter, JsonlLogger, PhaseProfiler, draw_graph, peak_memory_gb
 
 
 @dataclass
@@ -67,6 +68,10 @@ class TransformerConfig:
     maxlen: int = 512
     length_buckets: tuple = (64, 128, 256, 512)
     clip: float = 10.0
+    auto_resume: bool = False        # restore *_last.pth (full state) if present; implies save_last
+    save_last: bool = False
+    nonfinite_guard: bool = True     # skip (on device) steps whose gradients are not finite
+    profile_steps: int = 0
     extra: dict = field(default_factory=dict)
 
 
@@ -108,10 +113,19 @@ class TransformerTrainer:
         self.logger = JsonlLogger(cfg.log_path)
         self.pos_index = torch.arange(cfg.maxlen, device=self.device)  # transformer_test.py:228
         self.training_acc, self.testing_acc, self.epoch_time = [], [], []
+        self.global_step = 0
+        self.skipped = torch.zeros((), device=self.device, dtype=torch.int32)
+        self.profiler = PhaseProfiler(cfg.profile_steps, self.device.type == "cuda", self.logger)
+        if cfg.auto_resume and resilience.restore_last(self):
+            print0(f"auto-resume: restored {self.last_path}, continuing at epoch {self.start_epoch}")
 
     @property
     def ckpt_path(self):
         return os.path.join(self.cfg.checkpoint_dir, "transformer_ckpt.pth")
+
+    @property
+    def last_path(self):
+        return resilience.last_path(self.ckpt_path)
 
     def _build_data(self):
         cfg = self.cfg
@@ -170,24 +184,35 @@ class TransformerTrainer:
 
     def train_step(self, tokens, labels, types, masks):
         cfg = self.cfg
+        prof = self.profiler
+        resilience.maybe_inject_fault(self.global_step, self.rank)
+        prof.begin_step()
+        prof.mark("forward")
         mask = masks.view(masks.shape[0], 1, 1, masks.shape[1])
         with self._autocast():
             logits, perm, lam = self.model(tokens, types, self.pos_index, mask)
+            prof.mark("loss")
             loss = mixup_criterion(None, logits, labels, labels[perm], lam)
+        prof.mark("backward")
         self.scaler.scale_loss(loss).backward()
+        prof.mark("grad_sync")
         if self.reducer is not None:
             self.reducer.finish()
         if self.fsdp is not None:
             self.fsdp.finish_backward()
+        prof.mark("optimizer")
         fp16 = self.scaler.enabled
-        self.clipper(cfg.clip, inv_scale=self.scaler.inv_scale(), check_inf=fp16)
-        found = None
-        if fp16:
+        guard = cfg.nonfinite_guard and not isinstance(self.optimizer, NGD)  # NGD: host check, fp16 only
+        check = fp16 or guard
+        self.clipper(cfg.clip, inv_scale=self.scaler.inv_scale(), check_inf=check)
+        found = self.clipper.found_inf if check else None
+        if fp16 or (check and self.fsdp is not None):
             self.scaler.sync_found_inf(self.clipper.found_inf)
-            found = self.clipper.found_inf
         self.optimizer.step(grad_scale=self.clipper.coef, found_inf=found)
         if fp16:
             self.scaler.update(found)
+        if guard:
+            self.skipped += found.reshape(())
         if self.fsdp is not None:
             self.fsdp.after_step()
         if not cfg.faithful and self.scheduler is not None and isinstance(
@@ -195,6 +220,8 @@ class TransformerTrainer:
             if self.scheduler.last_epoch + 1 < self.scheduler.total_steps:
                 self.scheduler.step()  # per batch, as OneCycleLR intends (Q9)
         self.meter.update(loss, logits.detach(), labels, labels[perm], lam)
+        prof.end_step()
+        self.global_step += 1
         return loss
 
     def train_epoch(self, epoch):
@@ -217,7 +244,9 @@ class TransformerTrainer:
         m = self.meter.reduced()
         samples = n * self.cfg.batch_size * self.world
         rec = dict(epoch=epoch, steps=n, epoch_time_s=dt, samples_per_s=samples / max(dt, 1e-9), train_loss=m["loss"],
-                   train_acc=m["acc"], peak_mem_gb=peak_memory_gb(), lr=self.optimizer.group["lr"])
+                   train_acc=m["acc"], peak_mem_gb=peak_memory_gb(), lr=self.optimizer.group["lr"],
+                   skipped_steps=int(self.skipped.item()))
+        self.skipped.zero_()
         print0(f"epoch {epoch}: {n} steps in {dt:.2f}s ({rec['samples_per_s']:.0f} samples/s) loss {m['loss']:.4f} "
                f"acc {m['acc']:.2f}%  peak mem {rec['peak_mem_gb']:.2f} GB")
         self.logger.log(**rec)
@@ -257,6 +286,8 @@ class TransformerTrainer:
                 self.scheduler.step()
             if self.cfg.eval:
                 self.test(epoch)
+            if self.cfg.save_last or self.cfg.auto_resume:
+                resilience.save_last(self, epoch)
         if self.cfg.plot:
             xs = np.arange(self.start_epoch, self.start_epoch + len(self.training_acc))
             if self.testing_acc:

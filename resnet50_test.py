@@ -51,6 +51,12 @@ def parse(argv=None):
     p.add_argument("--no_plot", action="store_true")
     p.add_argument("--checkpoint_dir", default="./checkpoint")
     p.add_argument("--log", default=None, help="JSONL metrics path")
+    p.add_argument("--auto_resume", action="store_true",
+                   help="restore the full-state checkpoint <dir>/resnet_last.pth if present (use with torchrun --max-restarts)")
+    p.add_argument("--save_last", action="store_true", help="write the full-state resnet_last.pth every epoch")
+    p.add_argument("--no_nonfinite_guard", action="store_true", help="do not skip steps with non-finite gradients")
+    p.add_argument("--profile_steps", default=0, type=int, help="per-phase device timing + roctx ranges of K steps")
+    p.add_argument("--no_graphs", action="store_true", help="launch the engine's kernels eagerly (no HIP graphs)")
     return p.parse_args(argv)
 
 
@@ -71,7 +77,9 @@ def config_from_args(a):
                         lr_scaling="faithful4" if a.faithful else "world", bucket_mb=a.bucket_mb,
                         comm_dtype=a.comm_dtype, fsdp=a.fsdp, scheduler=sched, resume=a.resume,
                         checkpoint_dir=a.checkpoint_dir, steps_per_epoch=a.steps, eval=not a.no_eval,
-                        log_path=a.log, plot=not a.no_plot, workers=a.workers, extra=extra)
+                        log_path=a.log, plot=not a.no_plot, workers=a.workers, auto_resume=a.auto_resume,
+                        save_last=a.save_last, nonfinite_guard=not a.no_nonfinite_guard,
+                        profile_steps=a.profile_steps, graphs=not a.no_graphs, extra=extra)
 
 
 def main(argv=None):

@@ -38,6 +38,27 @@ def test_flat_optimizers_match_cpu(cuda, kind):
     assert rel(fg.data.cpu(), fc.data) < 1e-5
 
 
+@pytest.mark.parametrize("kind", ["sgd", "madgrad", "mirror", "adam"])
+def test_skipped_step_clears_gradient(cuda, kind):
+    """found_inf set (non-finite gradients): the kernel leaves parameters and optimizer
+    state untouched but still zeroes the gradient, so the next step starts clean."""
+    from faster_distributed_training_amd.optim import flat_optim as O
+    from faster_distributed_training_amd.utils.flat import FlatParams
+    torch.manual_seed(1)
+    f = FlatParams(torch.nn.Linear(40, 24).to(cuda), device=cuda)
+    opt = {"sgd": lambda: O.SGD(f, lr=0.1, momentum=0.9), "madgrad": lambda: O.MADGRAD(f, lr=0.05),
+           "mirror": lambda: O.MirrorMADGRAD(f, lr=0.05), "adam": lambda: O.Adam(f, lr=1e-2)}[kind]()
+    f.grad.copy_(torch.randn(f.numel, device=cuda))
+    opt.step()
+    before = f.data.clone()
+    f.grad.fill_(float("nan"))
+    found = torch.ones(1, device=cuda, dtype=torch.int32)
+    opt.step(found_inf=found)
+    torch.cuda.synchronize()
+    assert torch.equal(f.data, before)
+    assert torch.count_nonzero(f.grad).item() == 0
+
+
 def test_grad_clipper(cuda):
     from faster_distributed_training_amd.optim.flat_optim import GradClipper
     from faster_distributed_training_amd.utils.flat import FlatParams

@@ -51,6 +51,11 @@ def parse(argv=None):
     p.add_argument("--no_plot", action="store_true")
     p.add_argument("--checkpoint_dir", default="./checkpoint")
     p.add_argument("--log", default=None)
+    p.add_argument("--auto_resume", action="store_true",
+                   help="restore <dir>/transformer_last.pth if present (use with torchrun --max-restarts)")
+    p.add_argument("--save_last", action="store_true", help="write the full-state transformer_last.pth every epoch")
+    p.add_argument("--no_nonfinite_guard", action="store_true")
+    p.add_argument("--profile_steps", default=0, type=int, help="per-phase device timing + roctx ranges of K steps")
     return p.parse_args(argv)
 
 
@@ -69,7 +74,9 @@ def config_from_args(a):
                              fsdp=a.fsdp, bucket_mb=a.bucket_mb, resume=a.resume, checkpoint_dir=a.checkpoint_dir,
                              steps_per_epoch=a.steps, eval=not a.no_eval, log_path=a.log, plot=not a.no_plot,
                              workers=a.workers, n_layers=a.layers, d_model=a.d_model, heads=heads,
-                             d_ff=2 * a.d_model, d_hidden=2 * a.d_model, extra=extra)
+                             d_ff=2 * a.d_model, d_hidden=2 * a.d_model, auto_resume=a.auto_resume,
+                             save_last=a.save_last, nonfinite_guard=not a.no_nonfinite_guard,
+                             profile_steps=a.profile_steps, extra=extra)
 
 
 def main(argv=None):
