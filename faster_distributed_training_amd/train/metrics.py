@@ -152,8 +152,10 @@ class PhaseProfiler:
     roctx ranges around each phase so a ``rocprofv3 --marker-trace`` / timeline shows the
     phase structure.  Phases are marked in order by the trainer: ``mark("fwd")`` etc."""
 
-    def __init__(self, steps: int, cuda: bool, logger=None):
+    def __init__(self, steps: int, cuda: bool, logger=None, skip: int = 3):
+        # skip: steps left unprofiled first (eager warm-up + HIP-graph capture of the engine)
         self.steps, self.cuda, self.logger = int(steps), cuda, logger
+        self.skip = int(skip) if steps > 0 else 0
         self.done = 0
         self.records = []  # per step: [(phase, start_event, end_event)]
         self._cur = None
@@ -176,6 +178,10 @@ class PhaseProfiler:
 
     def begin_step(self):
         if not self.active:
+            return
+        if self.skip > 0:
+            self.skip -= 1
+            self._cur = None
             return
         self._cur = []
         self._open = None

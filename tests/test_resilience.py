@@ -62,7 +62,7 @@ def test_nonfinite_step_is_skipped(tmp_path):
 def test_phase_profiler_reports(tmp_path):
     tr = ResNetTrainer(_cfg(tmp_path, profile_steps=2))
     it = iter(tr.train_loader)
-    for _ in range(3):
+    for _ in range(3 + 3):  # 3 warm-up steps are skipped
         tr.train_step(*next(it))
     s = tr.profiler.summary()
     assert {"mixup", "forward", "loss", "backward", "grad_sync", "optimizer"} <= set(s)
