@@ -159,6 +159,28 @@ def test_embedding(cuda):
     assert rel(tw.grad, t2.grad) < 1e-5 and rel(pw.grad, p2.grad) < 1e-5 and rel(sw.grad, s2.grad) < 1e-5
 
 
+def test_embedding_bwd_padding_heavy(cuda):
+    """Backward with a heavily repeated (padding) token whose rows carry zero gradient, many
+    rows per segment id and several workgroups (LDS segment path + position reduction)."""
+    from faster_distributed_training_amd.ops.embedding import _EmbeddingNative, embedding_sum_reference
+    V, d, B, L = 300, 512, 9, 40
+    tw = torch.randn(V, d, device=cuda, requires_grad=True)
+    pw = torch.randn(512, d, device=cuda, requires_grad=True)
+    sw = torch.randn(3, d, device=cuda, requires_grad=True)
+    ids = torch.randint(1, V, (B, L), device=cuda)
+    ids[:, 25:] = 0  # padding token
+    ty = torch.randint(0, 3, (B, L), device=cuda)
+    pos = torch.arange(512, device=cuda)
+    out = _EmbeddingNative.apply(ids, ty, pos, tw, pw, sw, math.sqrt(d))
+    g = torch.randn_like(out)
+    g[:, 25:] = 0.0  # masked positions: no gradient
+    g[0, 3] = 0.0
+    out.backward(g)
+    t2, p2, s2 = [w.detach().clone().requires_grad_() for w in (tw, pw, sw)]
+    embedding_sum_reference(ids, ty, pos, t2, p2, s2, math.sqrt(d)).backward(g)
+    assert rel(tw.grad, t2.grad) < 1e-5 and rel(pw.grad, p2.grad) < 1e-5 and rel(sw.grad, s2.grad) < 1e-5
+
+
 def test_fused_mlp(cuda):
     from faster_distributed_training_amd.ops.mlp import fused_mlp
     X = torch.randn(64, 512, device=cuda, requires_grad=True)
