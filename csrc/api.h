@@ -102,4 +102,12 @@ void attn_fwd(uint64_t q, uint64_t k, uint64_t v, const std::vector<long>& strid
 void attn_bwd(uint64_t q, uint64_t k, uint64_t v, const std::vector<long>& strides, uint64_t o, uint64_t dout,
               uint64_t lse, uint64_t delta, uint64_t mask, uint64_t dq, uint64_t dk, uint64_t dv, int B, int L, int H,
               float fill, float p_drop, uint64_t seed, uint64_t stream);
+// ngd.hip
+void ngd_sumsq(uint64_t X, long per, int G, uint64_t out, uint64_t stream);
+void ngd_rescale(uint64_t X, uint64_t Y, long per, int G, uint64_t ip, uint64_t fp, uint64_t stream);
+void ngd_pre_eigh(uint64_t K, uint64_t L, uint64_t d, uint64_t rho, uint64_t Z, uint64_t ise, uint64_t drho, uint64_t zs,
+                  uint64_t dsum, int G, int R, float alpha, float eta, float N, float D, uint64_t stream);
+void ngd_post_eigh(uint64_t c, uint64_t U, uint64_t ise, uint64_t drho, uint64_t zs, uint64_t dsum, uint64_t trXX,
+                   uint64_t d, uint64_t rho, uint64_t A, uint64_t wc, int G, int R, float alpha, float eta, float N,
+                   float D, uint64_t stream);
 }  // namespace fdt

@@ -36,6 +36,10 @@ PYBIND11_MODULE(_fdt_native, m) {
   DEF(wgrad_reduce);
   DEF(pack_weights);
   DEF(jacobi_eigh);
+  DEF(ngd_pre_eigh);
+  DEF(ngd_sumsq);
+  DEF(ngd_rescale);
+  DEF(ngd_post_eigh);
   DEF(attn_fwd);
   DEF(attn_bwd);
   // optimizers

@@ -1,0 +1,215 @@
+// Online natural-gradient (NGD) preconditioner update -- the rank x rank "small math" of one
+// update step, fused (optim/ngd.py NGState._step; reference ngd_optimizer.py:205-324).
+//
+// Written with PyTorch ops this is ~70 launches per (shape group, axis) on [G,R] / [G,R,R]
+// tensors (R <= 80): thousands of tiny kernels per NGD update step whose launch latency,
+// not arithmetic, bounds the step.  Here it is two launches per (group, axis), one
+// workgroup per preconditioner g:
+//
+//   ngd_pre_eigh : (K = J J^T, L, d, rho)           -> Z (symmetric, to the eigensolver),
+//                                                      ise = e^-1/2, drho = d + rho, zs, sum d
+//   ngd_post_eigh: (eigenpairs of Z ascending, ...)  -> A = U^T diag(lp) diag(ise) (R x R),
+//                                                      wc, and d, rho updated in place
+// followed on the host side by W <- A (J + wc W) (one batched GEMM).  fp32 throughout,
+// same expressions as the PyTorch formulation (GPU test compares the two).
+#include "common.h"
+
+namespace fdt {
+
+constexpr int kNgdMaxR = 128;
+constexpr float kNgdEpsilon = 1.0e-10f;
+constexpr float kNgdDelta = 5.0e-4f;
+
+__device__ __forceinline__ float block_sum256(float v, float* red) {
+  v = wave_sum(v);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  __syncthreads();
+  if (lane == 0) red[w] = v;
+  __syncthreads();
+  return red[0] + red[1] + red[2] + red[3];
+}
+
+__device__ __forceinline__ float block_max256(float v, float* red) {
+  v = wave_max(v);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  __syncthreads();
+  if (lane == 0) red[w] = v;
+  __syncthreads();
+  return fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+}
+
+__global__ __launch_bounds__(256) void ngd_pre_eigh_kernel(const float* __restrict__ K, const float* __restrict__ L,
+                                                           const float* __restrict__ d, const float* __restrict__ rho,
+                                                           float* __restrict__ Z, float* __restrict__ ise_o,
+                                                           float* __restrict__ drho_o, float* __restrict__ zs_o,
+                                                           float* __restrict__ dsum_o, int R, float alpha, float eta,
+                                                           float N, float D) {
+  __shared__ float s_ise[kNgdMaxR], s_drho[kNgdMaxR], red[4];
+  const int g = blockIdx.x, tid = threadIdx.x;
+  const float* Kg = K + (long)g * R * R;
+  const float* Lg = L + (long)g * R * R;
+  const float* dg = d + (long)g * R;
+  const float rh = rho[g];
+  float ds = 0.f, tr = 0.f;
+  for (int i = tid; i < R; i += 256) { ds += dg[i]; tr += Kg[i * R + i]; }
+  const float dsum = block_sum256(ds, red);
+  const float trK = block_sum256(tr, red);
+  const float beta = rh * (1.f + alpha) + alpha * dsum / D;
+  const float zs = fmaxf(trK, 1.f);
+  for (int i = tid; i < R; i += 256) {
+    const float e = 1.f / (beta / dg[i] + 1.f);
+    const float is = rsqrtf(e);
+    s_ise[i] = is;
+    s_drho[i] = dg[i] + rh;
+    ise_o[(long)g * R + i] = is;
+    drho_o[(long)g * R + i] = dg[i] + rh;
+  }
+  if (tid == 0) { zs_o[g] = zs; dsum_o[g] = dsum; }
+  __syncthreads();
+  const float en = eta / N;
+  const float c1 = en * en / zs, c2 = en * (1.f - eta) / zs, c3 = (1.f - eta) * (1.f - eta) / zs;
+  float* Zg = Z + (long)g * R * R;
+  for (int e = tid; e < R * R; e += 256) {
+    const int i = e / R, j = e - i * R;
+    const float oo = s_ise[i] * s_ise[j];
+    // o1 + o1^T = ise_i ise_j (drho_j + drho_i)
+    float z = Kg[e] * (c1 * oo) + Lg[e] * (c2 * (s_ise[i] * (s_ise[j] * s_drho[j]) + s_ise[j] * (s_ise[i] * s_drho[i])));
+    if (i == j) z += c3 * s_drho[i] * s_drho[i];
+    Zg[e] = z;
+  }
+}
+
+// c: eigenvalues ascending [G][R]; U: eigenvectors as columns, ascending [G][R][R].
+__global__ __launch_bounds__(256) void ngd_post_eigh_kernel(const float* __restrict__ c, const float* __restrict__ U,
+                                                            const float* __restrict__ ise, const float* __restrict__ drho,
+                                                            const float* __restrict__ zs_in, const float* __restrict__ dsum_in,
+                                                            const float* __restrict__ trXX, float* __restrict__ d,
+                                                            float* __restrict__ rho, float* __restrict__ A,
+                                                            float* __restrict__ wc, int R, float alpha, float eta, float N,
+                                                            float D) {
+  __shared__ float s_sqc[kNgdMaxR], s_lp[kNgdMaxR], s_ise[kNgdMaxR], red[4];
+  const int g = blockIdx.x, tid = threadIdx.x;
+  const float rh = rho[g], zs = zs_in[g], dsum = dsum_in[g];
+  const float en = eta / N;
+  const float cfl = (rh * (1.f - eta)) * (rh * (1.f - eta)) / zs;
+  float part = 0.f, mx = 0.f;
+  for (int k = tid; k < R; k += 256) {
+    const float ck = fmaxf(c[(long)g * R + (R - 1 - k)], cfl);  // descending order
+    const float sq = sqrtf(ck) * sqrtf(zs);
+    s_sqc[k] = sq;
+    part += sq;
+    mx = fmaxf(mx, sq);
+    s_ise[k] = ise[(long)g * R + k];
+  }
+  const float sum_sqc = block_sum256(part, red);
+  const float max_sqc = block_max256(mx, red);
+  float rho1 = (en * trXX[g] + (1.f - eta) * (D * rh + dsum) - sum_sqc) / (D - (float)R);
+  const float floor = fmaxf(kNgdDelta * max_sqc, kNgdEpsilon);
+  float pd = 0.f;
+  for (int k = tid; k < R; k += 256) {
+    const float d1 = fmaxf(s_sqc[k] - rho1, floor);
+    d[(long)g * R + k] = d1;
+    pd += d1;
+  }
+  const float sum_d1 = block_sum256(pd, red);  // (its barriers also order the d writes)
+  rho1 = fmaxf(rho1, floor);
+  const float beta1 = rho1 * (1.f + alpha) + alpha * sum_d1 / D;
+  for (int k = tid; k < R; k += 256) {
+    const float d1 = d[(long)g * R + k];
+    const float e1 = 1.f / (beta1 / d1 + 1.f);
+    s_lp[k] = en * sqrtf(e1) / s_sqc[k];
+    wc[(long)g * R + k] = ((1.f - eta) / en) * drho[(long)g * R + k];
+  }
+  __syncthreads();
+  if (tid == 0) rho[g] = rho1;
+  // A[k][j] = U_desc[j][k] * lp[k] * ise[j],  U_desc[:, k] = U[:, R-1-k]
+  const float* Ug = U + (long)g * R * R;
+  float* Ag = A + (long)g * R * R;
+  for (int e = tid; e < R * R; e += 256) {
+    const int k = e / R, j = e - k * R;
+    Ag[e] = Ug[j * R + (R - 1 - k)] * s_lp[k] * s_ise[j];
+  }
+}
+
+// ---------------------------------------------------------------- norm-preserving rescale
+// The preconditioned direction keeps the Frobenius norm of the input per matrix g
+// (reference ngd_optimizer.py:151-168):  Y <- isnan(|Y|^2) ? X : Y * sqrt(|X|^2 / |Y|^2).
+// ngd_sumsq: out[g] += sum of squares of the g-th slab (float4 loads, block reduce, one
+// atomic per block; out zeroed by the caller) -- one launch instead of square + reduce.
+__global__ __launch_bounds__(256) void ngd_sumsq_kernel(const float* __restrict__ X, long per, int chunks,
+                                                        float* __restrict__ out) {
+  __shared__ float red[4];
+  const int g = blockIdx.x / chunks, ch = blockIdx.x - g * chunks;
+  const float* x = X + (long)g * per;
+  const long n4 = per / 4;
+  const long b0 = n4 * ch / chunks, b1 = n4 * (ch + 1) / chunks;
+  float acc = 0.f;
+  for (long i = b0 + threadIdx.x; i < b1; i += 256) {
+    const float4 v = reinterpret_cast<const float4*>(x)[i];
+    acc = fmaf(v.x, v.x, fmaf(v.y, v.y, fmaf(v.z, v.z, fmaf(v.w, v.w, acc))));
+  }
+  if (ch == chunks - 1)
+    for (long i = n4 * 4 + threadIdx.x; i < per; i += 256) acc = fmaf(x[i], x[i], acc);
+  acc = block_sum256(acc, red);
+  if (threadIdx.x == 0) atomicAdd(out + g, acc);
+}
+
+__global__ __launch_bounds__(256) void ngd_rescale_kernel(const float* __restrict__ X, float* __restrict__ Y, long per,
+                                                          int chunks, const float* __restrict__ ip,
+                                                          const float* __restrict__ fp) {
+  const int g = blockIdx.x / chunks, ch = blockIdx.x - g * chunks;
+  const float f = fp[g];
+  const bool bad = isnan(f);
+  const float sc = sqrtf(ip[g] / (f + 1e-30f));
+  const long b0 = per * ch / chunks, b1 = per * (ch + 1) / chunks;
+  const float* x = X + (long)g * per;
+  float* y = Y + (long)g * per;
+  for (long i = b0 + threadIdx.x; i < b1; i += 256) y[i] = bad ? x[i] : y[i] * sc;
+}
+
+static int ngd_chunks(long per) {
+  long c = per / (256 * 64);  // ~64 elements per thread
+  if (c < 1) c = 1;
+  if (c > 512) c = 512;
+  return (int)c;
+}
+
+void ngd_sumsq(uint64_t X, long per, int G, uint64_t out, uint64_t stream) {
+  if (G == 0 || per == 0) return;
+  FDT_CHECK(X % 16 == 0 && per % 4 == 0, "ngd_sumsq: 16-B aligned slabs");
+  const int ch = ngd_chunks(per);
+  ngd_sumsq_kernel<<<G * ch, 256, 0, as_stream(stream)>>>(P<const float>(X), per, ch, P<float>(out));
+  FDT_LAUNCH_CHECK();
+}
+
+void ngd_rescale(uint64_t X, uint64_t Y, long per, int G, uint64_t ip, uint64_t fp, uint64_t stream) {
+  if (G == 0 || per == 0) return;
+  const int ch = ngd_chunks(per);
+  ngd_rescale_kernel<<<G * ch, 256, 0, as_stream(stream)>>>(P<const float>(X), P<float>(Y), per, ch, P<const float>(ip),
+                                                           P<const float>(fp));
+  FDT_LAUNCH_CHECK();
+}
+
+void ngd_pre_eigh(uint64_t K, uint64_t L, uint64_t d, uint64_t rho, uint64_t Z, uint64_t ise, uint64_t drho, uint64_t zs,
+                  uint64_t dsum, int G, int R, float alpha, float eta, float N, float D, uint64_t stream) {
+  FDT_CHECK(R >= 1 && R <= kNgdMaxR, "ngd: rank out of range");
+  if (G == 0) return;
+  ngd_pre_eigh_kernel<<<G, 256, 0, as_stream(stream)>>>(P<const float>(K), P<const float>(L), P<const float>(d),
+                                                       P<const float>(rho), P<float>(Z), P<float>(ise), P<float>(drho),
+                                                       P<float>(zs), P<float>(dsum), R, alpha, eta, N, D);
+  FDT_LAUNCH_CHECK();
+}
+
+void ngd_post_eigh(uint64_t c, uint64_t U, uint64_t ise, uint64_t drho, uint64_t zs, uint64_t dsum, uint64_t trXX,
+                   uint64_t d, uint64_t rho, uint64_t A, uint64_t wc, int G, int R, float alpha, float eta, float N,
+                   float D, uint64_t stream) {
+  FDT_CHECK(R >= 1 && R <= kNgdMaxR, "ngd: rank out of range");
+  if (G == 0) return;
+  ngd_post_eigh_kernel<<<G, 256, 0, as_stream(stream)>>>(P<const float>(c), P<const float>(U), P<const float>(ise),
+                                                        P<const float>(drho), P<const float>(zs), P<const float>(dsum),
+                                                        P<const float>(trXX), P<float>(d), P<float>(rho), P<float>(A),
+                                                        P<float>(wc), R, alpha, eta, N, D);
+  FDT_LAUNCH_CHECK();
+}
+
+}  // namespace fdt

@@ -26,6 +26,7 @@ import os
 
 import torch
 
+from ..ops import _native
 from ..utils.flat import FlatParams
 from .flat_optim import SGD
 
@@ -56,6 +57,14 @@ def orthonormal_special(rank: int, dim: int, dtype=torch.float32, device=None) -
     eye = torch.diag(k)
     blocks = [torch.diag(k * first)] + [eye] * (ncols + 1)
     return torch.cat(blocks, dim=1)[:, :dim].contiguous()
+
+
+FUSED = os.environ.get("FDT_NGD_FUSED", "1") != "0"
+
+
+def _fused_small_math(X, R) -> bool:
+    return (FUSED and X.is_cuda and X.dtype == torch.float32 and R <= 128 and _native.enabled()
+            and hasattr(_native.native(), "ngd_pre_eigh"))
 
 
 def _native_eigh(device) -> bool:
@@ -128,6 +137,19 @@ class NGState:
         return (yield from self._precondition_scaled(X))
 
     def _precondition_scaled(self, X):
+        if _fused_small_math(X, 1) and X.is_contiguous() and X.numel() % (4 * X.shape[0]) == 0:
+            # HIP: |X|^2, |Y|^2 per matrix and the norm-preserving rescale + NaN guard in three
+            # launches (+ one fill) instead of ~10 (csrc/kernels/ngd.hip)
+            nat = _native.native()
+            G, per = X.shape[0], X.numel() // X.shape[0]
+            sums = torch.zeros(2, G, device=X.device, dtype=torch.float32)
+            ip, fp = sums[0], sums[1]
+            nat.ngd_sumsq(X.data_ptr(), per, G, ip.data_ptr(), _native.stream_ptr())
+            Y = yield from self._step(X, ip)
+            Y = Y.contiguous()
+            nat.ngd_sumsq(Y.data_ptr(), per, G, fp.data_ptr(), _native.stream_ptr())
+            nat.ngd_rescale(X.data_ptr(), Y.data_ptr(), per, G, ip.data_ptr(), fp.data_ptr(), _native.stream_ptr())
+            return Y
         ip = (X * X).sum(dim=(1, 2))
         Y = yield from self._step(X, ip)
         fp = (Y * Y).sum(dim=(1, 2))
@@ -152,6 +174,27 @@ class NGState:
         else:
             L = torch.bmm(H.transpose(1, 2), H)
         K = torch.bmm(J, J.transpose(1, 2))                      # [G,R,R]
+        if _fused_small_math(X, R):
+            # the rank x rank math around the eigensolver in two HIP launches (csrc/kernels/ngd.hip)
+            nat = _native.native()
+            G = X.shape[0]
+            sp = _native.stream_ptr()
+            Kc, Lc = K.contiguous(), L.contiguous()
+            Z = torch.empty(G, R, R, device=X.device, dtype=torch.float32)
+            ise, drho = torch.empty(G, R, device=X.device), torch.empty(G, R, device=X.device)
+            zs, dsum = torch.empty(G, device=X.device), torch.empty(G, device=X.device)
+            nat.ngd_pre_eigh(Kc.data_ptr(), Lc.data_ptr(), d.data_ptr(), rho.data_ptr(), Z.data_ptr(), ise.data_ptr(),
+                             drho.data_ptr(), zs.data_ptr(), dsum.data_ptr(), G, R, alpha, eta, float(N), float(D), sp)
+            c, U = yield Z                                        # eigh, ascending
+            A = torch.empty(G, R, R, device=X.device, dtype=torch.float32)
+            wc = torch.empty(G, R, device=X.device, dtype=torch.float32)
+            tr = trXX.contiguous()
+            nat.ngd_post_eigh(c.contiguous().data_ptr(), U.contiguous().data_ptr(), ise.data_ptr(), drho.data_ptr(),
+                              zs.data_ptr(), dsum.data_ptr(), tr.data_ptr(), d.data_ptr(), rho.data_ptr(), A.data_ptr(),
+                              wc.data_ptr(), G, R, alpha, eta, float(N), float(D), _native.stream_ptr())
+            B = torch.addcmul(J, wc.unsqueeze(2), W)              # J + wc W
+            torch.bmm(A, B, out=self.W)                           # W <- A B (in place)
+            return Xh
         dsum = d.sum(dim=1)                                       # [G]
         beta = rho * (1.0 + alpha) + alpha * dsum / D
         e = 1.0 / (beta.unsqueeze(1) / d + 1.0)

@@ -312,3 +312,88 @@ def test_ngd_graph_replay_matches_eager(cuda, monkeypatch):
     assert sum(1 for v in og._graphs.values() if not isinstance(v, str)) >= 2  # U and N graphs replayed
     assert rel(p_g, p_e) < 1e-6, rel(p_g, p_e)
     assert all(rel(a, b) < 1e-5 for a, b in zip(w_g, w_e))
+
+
+def test_ngd_fused_small_math_matches_torch(cuda, monkeypatch):
+    """The fused rank x rank update kernels (csrc/kernels/ngd.hip) vs the PyTorch formulation
+    of the same NGD step, both against the fp64 CPU path over 14 steps: the early Z matrices
+    have degenerate eigenspaces, so fp32 rounding differences rotate eigenvectors -- the
+    fused path must drift no more than the PyTorch fp32 path does."""
+    import torch.nn as nn
+    import faster_distributed_training_amd.optim.ngd as N
+    from faster_distributed_training_amd.utils.flat import FlatParams
+
+    def run(dev, fused=True):
+        monkeypatch.setattr(N, "FUSED", fused)
+        torch.manual_seed(0)
+        m = nn.Sequential(nn.Linear(40, 24), nn.Linear(24, 10, bias=False), nn.Linear(10, 7)).to(dev)
+        f = FlatParams(m)
+        o = N.NGD(f, lr=0.05, momentum=0.9, weight_decay=1e-4)
+        for s in range(14):
+            f.grad.copy_(torch.randn(f.numel, generator=torch.Generator().manual_seed(s)).to(dev))
+            o.step()
+        return f.data.cpu()
+
+    ref = run("cpu")
+    e_fused, e_torch = rel(run(cuda, True), ref), rel(run(cuda, False), ref)
+    assert e_fused < max(2.0 * e_torch, 1e-3), (e_fused, e_torch)
+
+
+def test_ngd_pre_post_kernels_vs_torch(cuda):
+    """ngd_pre_eigh / ngd_post_eigh against the PyTorch expressions of NGState._step."""
+    from faster_distributed_training_amd.ops import _native
+    nat = _native.native()
+    torch.manual_seed(5)
+    G, R, N, D, alpha, eta = 3, 7, 50.0, 20.0, 4.0, 0.1
+    J = torch.randn(G, R, int(D), device=cuda)
+    K = torch.bmm(J, J.transpose(1, 2))
+    L = torch.randn(G, R, R, device=cuda)
+    L = L + L.transpose(1, 2)
+    d = torch.rand(G, R, device=cuda) + 0.1
+    rho = torch.rand(G, device=cuda) + 0.05
+    trXX = torch.rand(G, device=cuda) * 100 + 10
+    # torch reference (ngd.py NGState._step)
+    dsum = d.sum(dim=1)
+    beta = rho * (1.0 + alpha) + alpha * dsum / D
+    e = 1.0 / (beta.unsqueeze(1) / d + 1.0)
+    ise = torch.rsqrt(e)
+    zs = torch.clamp(torch.diagonal(K, dim1=1, dim2=2).sum(1), min=1.0)
+    drho = d + rho.unsqueeze(1)
+    c1, c2, c3 = ((eta / N) ** 2) / zs, ((eta / N) * (1.0 - eta)) / zs, ((1.0 - eta) ** 2) / zs
+    oo = ise.unsqueeze(2) * ise.unsqueeze(1)
+    o1 = ise.unsqueeze(2) * (ise * drho).unsqueeze(1)
+    Zr = K * (c1.view(-1, 1, 1) * oo) + L * (c2.view(-1, 1, 1) * (o1 + o1.transpose(1, 2)))
+    Zr = Zr + torch.diag_embed(c3.unsqueeze(1) * drho * drho)
+    Z = torch.empty_like(Zr)
+    ise_k, drho_k = torch.empty_like(d), torch.empty_like(d)
+    zs_k, dsum_k = torch.empty_like(rho), torch.empty_like(rho)
+    sp = _native.stream_ptr()
+    nat.ngd_pre_eigh(K.data_ptr(), L.data_ptr(), d.data_ptr(), rho.data_ptr(), Z.data_ptr(), ise_k.data_ptr(),
+                     drho_k.data_ptr(), zs_k.data_ptr(), dsum_k.data_ptr(), G, R, alpha, eta, N, D, sp)
+    assert rel(Z, Zr) < 1e-5 and rel(ise_k, ise) < 1e-6 and rel(drho_k, drho) < 1e-6 and rel(zs_k, zs) < 1e-6
+    c, U = torch.linalg.eigh(Zr.double())
+    c, U = c.float().contiguous(), U.float().contiguous()
+    cf, Uf = c.flip(1), U.flip(2)
+    c_floor = ((rho * (1.0 - eta)) ** 2) / zs
+    cf = torch.maximum(cf, c_floor.unsqueeze(1))
+    sqc = torch.sqrt(cf) * torch.sqrt(zs).unsqueeze(1)
+    rho1 = ((eta / N) * trXX + (1.0 - eta) * (D * rho + dsum) - sqc.sum(1)) / (D - R)
+    floor = torch.clamp(1e-3 * 0.5 * sqc.max(dim=1).values, min=1e-10)
+    d1 = torch.maximum(sqc - rho1.unsqueeze(1), floor.unsqueeze(1))
+    rho1 = torch.maximum(rho1, floor)
+    beta1 = rho1 * (1.0 + alpha) + alpha * d1.sum(1) / D
+    e1 = 1.0 / (beta1.unsqueeze(1) / d1 + 1.0)
+    wc = ((1.0 - eta) / (eta / N)) * drho
+    lp = (eta / N) * torch.sqrt(e1) / sqc
+    A = Uf.transpose(1, 2) * (lp.unsqueeze(2) * ise.unsqueeze(1))
+    d_k, rho_k = d.clone(), rho.clone()
+    # (not empty_like(A): A inherits the transposed strides of Uf.transpose(1, 2))
+    A_k, wc_k = torch.empty(G, R, R, device=cuda), torch.empty_like(d)
+    nat.ngd_post_eigh(c.data_ptr(), U.data_ptr(), ise_k.data_ptr(), drho_k.data_ptr(), zs_k.data_ptr(),
+                      dsum_k.data_ptr(), trXX.data_ptr(), d_k.data_ptr(), rho_k.data_ptr(), A_k.data_ptr(),
+                      wc_k.data_ptr(), G, R, alpha, eta, N, D, sp)
+    torch.cuda.synchronize()
+    assert rel(d_k, d1) < 1e-5, (d_k, d1)
+    assert rel(rho_k, rho1) < 1e-5, (rho_k, rho1)
+    assert rel(wc_k, wc) < 1e-6
+    assert rel(A_k, A) < 1e-5
