@@ -104,6 +104,9 @@ void attn_bwd(uint64_t q, uint64_t k, uint64_t v, const std::vector<long>& strid
               float fill, float p_drop, uint64_t seed, uint64_t stream);
 // ngd.hip
 void ngd_sumsq(uint64_t X, long per, int G, uint64_t out, uint64_t stream);
+bool ngd_small_supported(int D, int R);
+void ngd_small_proj(uint64_t X, uint64_t Y, uint64_t W, int G, int A, int D, int B, int R, uint64_t sums, uint64_t J,
+                    uint64_t HH, uint64_t stream);
 void ngd_rescale(uint64_t X, uint64_t Y, long per, int G, uint64_t ip, uint64_t fp, uint64_t stream);
 void ngd_pre_eigh(uint64_t K, uint64_t L, uint64_t d, uint64_t rho, uint64_t Z, uint64_t ise, uint64_t drho, uint64_t zs,
                   uint64_t dsum, int G, int R, float alpha, float eta, float N, float D, uint64_t stream);

@@ -38,6 +38,8 @@ PYBIND11_MODULE(_fdt_native, m) {
   DEF(jacobi_eigh);
   DEF(ngd_pre_eigh);
   DEF(ngd_sumsq);
+  DEF(ngd_small_supported);
+  DEF(ngd_small_proj);
   DEF(ngd_rescale);
   DEF(ngd_post_eigh);
   DEF(attn_fwd);

@@ -167,6 +167,114 @@ __global__ __launch_bounds__(256) void ngd_rescale_kernel(const float* __restric
   for (long i = b0 + threadIdx.x; i < b1; i += 256) y[i] = bad ? x[i] : y[i] * sc;
 }
 
+// ---------------------------------------------------------------- tiny-dim axes (D <= 8)
+// The kh / kw axes of the 3x3 convs (D = 3, R = 2, N up to 2.4M rows per matrix) as batched
+// GEMMs are the worst shapes there are: H = X W^T has K = 3, and J = H^T X is a 2 x 3 output
+// with a 786K-long reduction that the library tiles as a handful of 16x16 workgroups (~250 us
+// each, measured).  It is one streaming pass: each thread owns rows, keeps W (R x D) in
+// registers, and produces in one read of X
+//   Xh = X - (X W^T) W  (written in X's own layout, so no transpose copies),
+//   |X|^2, |Xh|^2, and (update steps) J = H^T X, H^T H  -- block-reduced, one atomic each.
+// X is addressed in the parameter's canonical layout: element (g, a, d, b) of a
+// [G][A][D][B] tensor, row n = a * B + b (the transpose the GEMM path copies into).
+template <int D, int R>
+__global__ __launch_bounds__(256) void ngd_small_proj_kernel(const float* __restrict__ X, float* __restrict__ Y,
+                                                             const float* __restrict__ W, int A, int B, int chunks,
+                                                             float* __restrict__ sums, float* __restrict__ J,
+                                                             float* __restrict__ HH) {
+  constexpr int NV = 2 + R * D + R * R;
+  __shared__ float red[4][NV];
+  const int g = blockIdx.x / chunks, ch = blockIdx.x - g * chunks;
+  const int G = gridDim.x / chunks;
+  const int per = A * D * B, rows = A * B;
+  const float* x = X + (long)g * per;
+  float* y = Y + (long)g * per;
+  float w[R][D];
+#pragma unroll
+  for (int r = 0; r < R; ++r)
+#pragma unroll
+    for (int d = 0; d < D; ++d) w[r][d] = W[((long)g * R + r) * D + d];
+  float v[NV];
+#pragma unroll
+  for (int i = 0; i < NV; ++i) v[i] = 0.f;
+  const int r0 = (int)((long)rows * ch / chunks), r1 = (int)((long)rows * (ch + 1) / chunks);
+  for (int n = r0 + threadIdx.x; n < r1; n += 256) {
+    const int a = n / B, b = n - a * B;
+    const int base = a * D * B + b;
+    float xv[D], h[R];
+#pragma unroll
+    for (int d = 0; d < D; ++d) xv[d] = x[base + d * B];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      float s = 0.f;
+#pragma unroll
+      for (int d = 0; d < D; ++d) s = fmaf(w[r][d], xv[d], s);
+      h[r] = s;
+    }
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+      float o = xv[d];
+#pragma unroll
+      for (int r = 0; r < R; ++r) o = fmaf(-h[r], w[r][d], o);
+      y[base + d * B] = o;
+      v[0] = fmaf(xv[d], xv[d], v[0]);
+      v[1] = fmaf(o, o, v[1]);
+    }
+    if (J != nullptr) {
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+#pragma unroll
+        for (int d = 0; d < D; ++d) v[2 + r * D + d] = fmaf(h[r], xv[d], v[2 + r * D + d]);
+#pragma unroll
+        for (int s = 0; s < R; ++s) v[2 + R * D + r * R + s] = fmaf(h[r], h[s], v[2 + R * D + r * R + s]);
+      }
+    }
+  }
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int nv = J != nullptr ? NV : 2;
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    if (i < nv) {
+      const float s = wave_sum(v[i]);
+      if (lane == 0) red[wv][i] = s;
+    }
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < nv; i += 256) {
+    const float s = red[0][i] + red[1][i] + red[2][i] + red[3][i];
+    if (i < 2) atomicAdd(sums + (long)i * G + g, s);  // sums = [ip[G], fp[G]]
+    else if (i < 2 + R * D) atomicAdd(J + (long)g * R * D + (i - 2), s);
+    else atomicAdd(HH + (long)g * R * R + (i - 2 - R * D), s);
+  }
+}
+
+bool ngd_small_supported(int D, int R) {
+  return (D == 2 && R == 1) || (D == 3 && R == 2) || (D == 4 && R == 2) || (D == 5 && R == 3) ||
+         (D == 6 && R == 3) || (D == 7 && R == 4) || (D == 8 && R == 4);
+}
+
+void ngd_small_proj(uint64_t X, uint64_t Y, uint64_t W, int G, int A, int D, int B, int R, uint64_t sums, uint64_t J,
+                    uint64_t HH, uint64_t stream) {
+  FDT_CHECK(ngd_small_supported(D, R), "ngd_small_proj: unsupported (dim, rank)");
+  FDT_CHECK((long)A * D * B < (1L << 31), "ngd_small_proj: matrix too large");
+  FDT_CHECK((J == 0) == (HH == 0), "ngd_small_proj: J and HH together");
+  if (G == 0 || A == 0 || B == 0) return;
+  const long rows = (long)A * B;
+  long ch = rows / (256 * 16);  // ~16 rows per thread
+  if (ch < 1) ch = 1;
+  if (ch > 1024) ch = 1024;
+  const dim3 grid((unsigned)(G * ch));
+  hipStream_t s = as_stream(stream);
+#define FDT_NGD_SMALL(DD, RR)                                                                                      \
+  if (D == DD && R == RR)                                                                                         \
+    ngd_small_proj_kernel<DD, RR><<<grid, 256, 0, s>>>(P<const float>(X), P<float>(Y), P<const float>(W), A, B, \
+                                                       (int)ch, P<float>(sums), P<float>(J), P<float>(HH));
+  FDT_NGD_SMALL(2, 1) FDT_NGD_SMALL(3, 2) FDT_NGD_SMALL(4, 2) FDT_NGD_SMALL(5, 3) FDT_NGD_SMALL(6, 3)
+  FDT_NGD_SMALL(7, 4) FDT_NGD_SMALL(8, 4)
+#undef FDT_NGD_SMALL
+  FDT_LAUNCH_CHECK();
+}
+
 static int ngd_chunks(long per) {
   long c = per / (256 * 64);  // ~64 elements per thread
   if (c < 1) c = 1;

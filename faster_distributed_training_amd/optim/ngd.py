@@ -175,25 +175,7 @@ class NGState:
             L = torch.bmm(H.transpose(1, 2), H)
         K = torch.bmm(J, J.transpose(1, 2))                      # [G,R,R]
         if _fused_small_math(X, R):
-            # the rank x rank math around the eigensolver in two HIP launches (csrc/kernels/ngd.hip)
-            nat = _native.native()
-            G = X.shape[0]
-            sp = _native.stream_ptr()
-            Kc, Lc = K.contiguous(), L.contiguous()
-            Z = torch.empty(G, R, R, device=X.device, dtype=torch.float32)
-            ise, drho = torch.empty(G, R, device=X.device), torch.empty(G, R, device=X.device)
-            zs, dsum = torch.empty(G, device=X.device), torch.empty(G, device=X.device)
-            nat.ngd_pre_eigh(Kc.data_ptr(), Lc.data_ptr(), d.data_ptr(), rho.data_ptr(), Z.data_ptr(), ise.data_ptr(),
-                             drho.data_ptr(), zs.data_ptr(), dsum.data_ptr(), G, R, alpha, eta, float(N), float(D), sp)
-            c, U = yield Z                                        # eigh, ascending
-            A = torch.empty(G, R, R, device=X.device, dtype=torch.float32)
-            wc = torch.empty(G, R, device=X.device, dtype=torch.float32)
-            tr = trXX.contiguous()
-            nat.ngd_post_eigh(c.contiguous().data_ptr(), U.contiguous().data_ptr(), ise.data_ptr(), drho.data_ptr(),
-                              zs.data_ptr(), dsum.data_ptr(), tr.data_ptr(), d.data_ptr(), rho.data_ptr(), A.data_ptr(),
-                              wc.data_ptr(), G, R, alpha, eta, float(N), float(D), _native.stream_ptr())
-            B = torch.addcmul(J, wc.unsqueeze(2), W)              # J + wc W
-            torch.bmm(A, B, out=self.W)                           # W <- A B (in place)
+            yield from self._fused_update(J, K, L, trXX, N)
             return Xh
         dsum = d.sum(dim=1)                                       # [G]
         beta = rho * (1.0 + alpha) + alpha * dsum / D
@@ -230,6 +212,71 @@ class NGState:
         self.d.copy_(d1)
         self.rho.copy_(rho1)
         return Xh
+
+    def _fused_update(self, J, K, L, trXX, N):
+        """The rank x rank math around the eigensolver in two HIP launches
+        (csrc/kernels/ngd.hip), then W <- A (J + wc W) in place."""
+        nat = _native.native()
+        G, R, D = J.shape[0], self.rank, self.dim
+        dev = J.device
+        sp = _native.stream_ptr()
+        Kc, Lc = K.contiguous(), L.contiguous()
+        Z = torch.empty(G, R, R, device=dev, dtype=torch.float32)
+        ise, drho = torch.empty(G, R, device=dev), torch.empty(G, R, device=dev)
+        zs, dsum = torch.empty(G, device=dev), torch.empty(G, device=dev)
+        nat.ngd_pre_eigh(Kc.data_ptr(), Lc.data_ptr(), self.d.data_ptr(), self.rho.data_ptr(), Z.data_ptr(),
+                         ise.data_ptr(), drho.data_ptr(), zs.data_ptr(), dsum.data_ptr(), G, R, self.alpha, self.eta,
+                         float(N), float(D), sp)
+        c, U = yield Z                                            # eigh, ascending
+        A = torch.empty(G, R, R, device=dev, dtype=torch.float32)
+        wc = torch.empty(G, R, device=dev, dtype=torch.float32)
+        tr = trXX.contiguous()
+        nat.ngd_post_eigh(c.contiguous().data_ptr(), U.contiguous().data_ptr(), ise.data_ptr(), drho.data_ptr(),
+                          zs.data_ptr(), dsum.data_ptr(), tr.data_ptr(), self.d.data_ptr(), self.rho.data_ptr(),
+                          A.data_ptr(), wc.data_ptr(), G, R, self.alpha, self.eta, float(N), float(D),
+                          _native.stream_ptr())
+        B = torch.addcmul(J, wc.unsqueeze(2), self.W)             # J + wc W
+        torch.bmm(A, B, out=self.W)                               # W <- A B (in place)
+
+    # ------------------------------------------------- tiny-dim axes (HIP, no transposes)
+    def small_ok(self, G: torch.Tensor) -> bool:
+        """The kh / kw axes of 3x3 convs (dim <= 8): one streaming HIP pass per step instead of
+        transpose + 2-5 badly shaped batched GEMMs (csrc/kernels/ngd.hip ngd_small_proj)."""
+        return (_fused_small_math(G, self.rank) and hasattr(_native.native(), "ngd_small_proj")
+                and _native.native().ngd_small_supported(self.dim, self.rank))
+
+    def precondition_small_gen(self, G: torch.Tensor, A: int, B: int):
+        """G: [P, A, dim, B] in its own (contiguous) layout -> preconditioned, same layout."""
+        if self.t == 0:
+            self._init_default()
+            self.t = 1
+            for _ in range(3):
+                yield from self._small_step(G, A, B)
+            self.t = 0
+        return (yield from self._small_step(G, A, B))
+
+    def _small_step(self, G, A, B):
+        updating = self._updating()
+        self.t += 1
+        nat = _native.native()
+        P, R, D = G.shape[0], self.rank, self.dim
+        N = A * B
+        nj = P * R * D if updating else 0
+        buf = torch.zeros(2 * P + nj + (P * R * R if updating else 0), device=G.device, dtype=torch.float32)
+        sums = buf[:2 * P]
+        ip, fp = sums[:P], sums[P:]
+        J = buf[2 * P:2 * P + nj].view(P, R, D) if updating else None
+        HH = buf[2 * P + nj:].view(P, R, R) if updating else None
+        Y = torch.empty_like(G)
+        nat.ngd_small_proj(G.data_ptr(), Y.data_ptr(), self.W.data_ptr(), P, A, D, B, R, sums.data_ptr(),
+                           J.data_ptr() if updating else 0, HH.data_ptr() if updating else 0, _native.stream_ptr())
+        if updating:
+            L = torch.bmm(J, self.W.transpose(1, 2)) if N > D else HH
+            K = torch.bmm(J, J.transpose(1, 2))
+            yield from self._fused_update(J, K, L, ip, N)
+        nat.ngd_rescale(G.data_ptr(), Y.data_ptr(), G.numel() // P, P, ip.data_ptr(), fp.data_ptr(),
+                        _native.stream_ptr())
+        return Y
 
     def state_dict(self):
         return {"t": self.t, "W": self.W, "d": self.d, "rho": self.rho}
@@ -287,6 +334,12 @@ class _ShapeGroup:
     def precondition_gen(self, G: torch.Tensor):
         for ax, st in self.axes:
             a = ax + 1  # leading stack dim
+            if st.small_ok(G):
+                G = G.contiguous()
+                A = math.prod(self.shape[:ax])
+                B = math.prod(self.shape[ax + 1:])
+                G = (yield from st.precondition_small_gen(G, A, B)).view(G.shape)
+                continue
             X = G.transpose(-1, a).contiguous()
             shp = X.shape
             Y = yield from st.precondition_gen(X.view(shp[0], -1, shp[-1]))
@@ -391,9 +444,12 @@ class NGD(SGD):
             live = [(sg, slots) for sg, slots in self.groups if sg.axes]
             gens = [sg.precondition_gen(torch.stack([grad[s.offset:s.offset + s.numel].view(s.shape) for s in slots]))
                     for sg, slots in live]
+            dst, src = [], []
             for (sg, slots), out in zip(live, drive(gens)):
                 for i, s in enumerate(slots):
-                    grad[s.offset:s.offset + s.numel].view(s.shape).copy_(out[i])
+                    dst.append(grad[s.offset:s.offset + s.numel].view(s.shape))
+                    src.append(out[i])
+            torch._foreach_copy_(dst, src)  # multi-tensor launches, not one copy per parameter
         wd = g["weight_decay"]
         g["weight_decay"] = 0.0
         try:

@@ -339,6 +339,71 @@ def test_ngd_fused_small_math_matches_torch(cuda, monkeypatch):
     assert e_fused < max(2.0 * e_torch, 1e-3), (e_fused, e_torch)
 
 
+@pytest.mark.parametrize("D,R,A,B", [(3, 2, 70, 3), (3, 2, 5000, 1), (5, 3, 33, 7), (8, 4, 1, 900)])
+def test_ngd_small_proj_kernel_vs_torch(cuda, D, R, A, B):
+    """ngd_small_proj (one streaming pass over a tiny-dim axis, canonical layout) against
+    the GEMM formulation on the transposed copy: Xh, |X|^2, |Xh|^2, J = H^T X, H^T H."""
+    from faster_distributed_training_amd.ops import _native
+    nat = _native.native()
+    torch.manual_seed(D * 100 + B)
+    P = 3
+    X = torch.randn(P, A, D, B, device=cuda)
+    W = torch.randn(P, R, D, device=cuda) * 0.5
+    buf = torch.zeros(2 * P + P * R * D + P * R * R, device=cuda)
+    Y = torch.empty_like(X)
+    J = buf[2 * P:2 * P + P * R * D]
+    HH = buf[2 * P + P * R * D:]
+    nat.ngd_small_proj(X.data_ptr(), Y.data_ptr(), W.data_ptr(), P, A, D, B, R, buf.data_ptr(), J.data_ptr(),
+                       HH.data_ptr(), _native.stream_ptr())
+    Xt = X.double().transpose(2, 3).reshape(P, A * B, D)      # rows n = a * B + b
+    Wd = W.double()
+    H = torch.bmm(Xt, Wd.transpose(1, 2))
+    Xh = Xt - torch.bmm(H, Wd)
+    ref_Y = Xh.view(P, A, B, D).transpose(2, 3)
+    torch.cuda.synchronize()
+    assert rel(Y.double(), ref_Y) < 1e-5
+    assert rel(buf[:P].double(), (Xt * Xt).sum((1, 2))) < 1e-5
+    assert rel(buf[P:2 * P].double(), (Xh * Xh).sum((1, 2))) < 1e-5
+    assert rel(J.view(P, R, D).double(), torch.bmm(H.transpose(1, 2), Xt)) < 1e-4
+    assert rel(HH.view(P, R, R).double(), torch.bmm(H.transpose(1, 2), H)) < 1e-4
+    # non-update form: only the two sums, J / HH untouched
+    buf2 = torch.zeros(2 * P, device=cuda)
+    Y2 = torch.empty_like(X)
+    nat.ngd_small_proj(X.data_ptr(), Y2.data_ptr(), W.data_ptr(), P, A, D, B, R, buf2.data_ptr(), 0, 0,
+                       _native.stream_ptr())
+    torch.cuda.synchronize()
+    assert torch.equal(Y2, Y)
+    assert rel(buf2, buf[:2 * P]) < 1e-5
+
+
+def test_ngd_small_axes_match_gemm_path(cuda, monkeypatch):
+    """A conv model's NGD steps with the kh / kw axes on the streaming HIP pass vs the same
+    axes on transpose + batched GEMMs, both against the fp64 CPU path over 14 steps."""
+    import torch.nn as nn
+    import faster_distributed_training_amd.optim.ngd as N
+    from faster_distributed_training_amd.utils.flat import FlatParams
+    used = []
+    orig = N.NGState.small_ok
+
+    def run(dev, small=True):
+        monkeypatch.setattr(N.NGState, "small_ok",
+                            (lambda self, G: orig(self, G) and not used.append(1)) if small else (lambda self, G: False))
+        torch.manual_seed(0)
+        m = nn.Sequential(nn.Conv2d(4, 6, 3), nn.Conv2d(6, 6, 3), nn.Conv2d(6, 5, 3, bias=False),
+                          nn.Conv2d(5, 8, (1, 5))).to(dev)
+        f = FlatParams(m)
+        o = N.NGD(f, lr=0.05, momentum=0.9, weight_decay=1e-4)
+        for s in range(14):
+            f.grad.copy_(torch.randn(f.numel, generator=torch.Generator().manual_seed(s)).to(dev))
+            o.step()
+        return f.data.cpu()
+
+    ref = run("cpu")
+    e_small, e_gemm = rel(run(cuda, True), ref), rel(run(cuda, False), ref)
+    assert used, "small-dim path not taken"
+    assert e_small < max(2.0 * e_gemm, 1e-3), (e_small, e_gemm)
+
+
 def test_ngd_pre_post_kernels_vs_torch(cuda):
     """ngd_pre_eigh / ngd_post_eigh against the PyTorch expressions of NGState._step."""
     from faster_distributed_training_amd.ops import _native
