@@ -157,14 +157,30 @@ __global__ __launch_bounds__(256) void ngd_sumsq_kernel(const float* __restrict_
 __global__ __launch_bounds__(256) void ngd_rescale_kernel(const float* __restrict__ X, float* __restrict__ Y, long per,
                                                           int chunks, const float* __restrict__ ip,
                                                           const float* __restrict__ fp) {
+  // X is read only by the (block-uniform) NaN branch; float4 body + scalar tail
   const int g = blockIdx.x / chunks, ch = blockIdx.x - g * chunks;
   const float f = fp[g];
   const bool bad = isnan(f);
   const float sc = sqrtf(ip[g] / (f + 1e-30f));
-  const long b0 = per * ch / chunks, b1 = per * (ch + 1) / chunks;
   const float* x = X + (long)g * per;
   float* y = Y + (long)g * per;
-  for (long i = b0 + threadIdx.x; i < b1; i += 256) y[i] = bad ? x[i] : y[i] * sc;
+  const long n4 = per / 4;
+  const long b0 = n4 * ch / chunks, b1 = n4 * (ch + 1) / chunks;
+  float4* y4 = reinterpret_cast<float4*>(y);
+  if (bad) {
+    const float4* x4 = reinterpret_cast<const float4*>(x);
+    for (long i = b0 + threadIdx.x; i < b1; i += 256) y4[i] = x4[i];
+    if (ch == chunks - 1)
+      for (long i = n4 * 4 + threadIdx.x; i < per; i += 256) y[i] = x[i];
+    return;
+  }
+  for (long i = b0 + threadIdx.x; i < b1; i += 256) {
+    float4 v = y4[i];
+    v.x *= sc; v.y *= sc; v.z *= sc; v.w *= sc;
+    y4[i] = v;
+  }
+  if (ch == chunks - 1)
+    for (long i = n4 * 4 + threadIdx.x; i < per; i += 256) y[i] *= sc;
 }
 
 // ---------------------------------------------------------------- tiny-dim axes (D <= 8)
@@ -276,9 +292,11 @@ void ngd_small_proj(uint64_t X, uint64_t Y, uint64_t W, int G, int A, int D, int
 }
 
 static int ngd_chunks(long per) {
-  long c = per / (256 * 64);  // ~64 elements per thread
+  // ~8 float4 per thread, enough workgroups per matrix to fill the chip (the first version
+  // ran 64 scalar elements per thread on a few hundred workgroups: ~10% of HBM bandwidth)
+  long c = per / (256 * 4 * 8);
   if (c < 1) c = 1;
-  if (c > 512) c = 512;
+  if (c > 4096) c = 4096;
   return (int)c;
 }
 
@@ -292,6 +310,7 @@ void ngd_sumsq(uint64_t X, long per, int G, uint64_t out, uint64_t stream) {
 
 void ngd_rescale(uint64_t X, uint64_t Y, long per, int G, uint64_t ip, uint64_t fp, uint64_t stream) {
   if (G == 0 || per == 0) return;
+  FDT_CHECK(X % 16 == 0 && Y % 16 == 0 && per % 4 == 0, "ngd_rescale: 16-B aligned slabs");
   const int ch = ngd_chunks(per);
   ngd_rescale_kernel<<<G * ch, 256, 0, as_stream(stream)>>>(P<const float>(X), P<float>(Y), per, ch, P<const float>(ip),
                                                            P<const float>(fp));

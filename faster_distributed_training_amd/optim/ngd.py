@@ -108,6 +108,7 @@ class NGState:
         self.W = None
         self.d = None
         self.rho = None
+        self.last_ip = None  # per-matrix |X|^2 of the last call (HIP path), handed to the next axis
 
     # -------------------------------------------------------------- schedule
     def _updating(self):
@@ -126,31 +127,41 @@ class NGState:
         """X: [G, N, dim] -> preconditioned, same shape (Frobenius norm preserved)."""
         return drive([self.precondition_gen(X)])[0]
 
-    def precondition_gen(self, X: torch.Tensor):
-        """Generator form of ``precondition`` (yields Z, receives eigenpairs)."""
+    def precondition_gen(self, X: torch.Tensor, ip=None):
+        """Generator form of ``precondition`` (yields Z, receives eigenpairs).  ``ip``:
+        per-matrix |X|^2 when the caller already has it (HIP path); ``self.last_ip`` holds
+        it afterwards (None on the PyTorch path)."""
         if self.t == 0:
             self._init_default()
             self.t = 1
             for _ in range(3):
-                yield from self._precondition_scaled(X)
+                yield from self._precondition_scaled(X, ip)
+                ip = self.last_ip
             self.t = 0
-        return (yield from self._precondition_scaled(X))
+        return (yield from self._precondition_scaled(X, ip))
 
-    def _precondition_scaled(self, X):
+    def _precondition_scaled(self, X, ip_in=None):
         if _fused_small_math(X, 1) and X.is_contiguous() and X.numel() % (4 * X.shape[0]) == 0:
             # HIP: |X|^2, |Y|^2 per matrix and the norm-preserving rescale + NaN guard in three
-            # launches (+ one fill) instead of ~10 (csrc/kernels/ngd.hip)
+            # launches (+ one fill) instead of ~10 (csrc/kernels/ngd.hip).  |X|^2 is known
+            # when X is the previous axis' (norm-preserved) output: ip_in, no extra pass.
             nat = _native.native()
             G, per = X.shape[0], X.numel() // X.shape[0]
-            sums = torch.zeros(2, G, device=X.device, dtype=torch.float32)
-            ip, fp = sums[0], sums[1]
-            nat.ngd_sumsq(X.data_ptr(), per, G, ip.data_ptr(), _native.stream_ptr())
+            if ip_in is not None:
+                ip = ip_in
+                fp = torch.zeros(G, device=X.device, dtype=torch.float32)
+            else:
+                sums = torch.zeros(2, G, device=X.device, dtype=torch.float32)
+                ip, fp = sums[0], sums[1]
+                nat.ngd_sumsq(X.data_ptr(), per, G, ip.data_ptr(), _native.stream_ptr())
+            self.last_ip = ip
             Y = yield from self._step(X, ip)
             Y = Y.contiguous()
             nat.ngd_sumsq(Y.data_ptr(), per, G, fp.data_ptr(), _native.stream_ptr())
             nat.ngd_rescale(X.data_ptr(), Y.data_ptr(), per, G, ip.data_ptr(), fp.data_ptr(), _native.stream_ptr())
             return Y
         ip = (X * X).sum(dim=(1, 2))
+        self.last_ip = None
         Y = yield from self._step(X, ip)
         fp = (Y * Y).sum(dim=(1, 2))
         out = Y * torch.sqrt(ip / (fp + 1e-30)).view(-1, 1, 1)
@@ -243,7 +254,8 @@ class NGState:
         """The kh / kw axes of 3x3 convs (dim <= 8): one streaming HIP pass per step instead of
         transpose + 2-5 badly shaped batched GEMMs (csrc/kernels/ngd.hip ngd_small_proj)."""
         return (_fused_small_math(G, self.rank) and hasattr(_native.native(), "ngd_small_proj")
-                and _native.native().ngd_small_supported(self.dim, self.rank))
+                and _native.native().ngd_small_supported(self.dim, self.rank)
+                and (G.numel() // G.shape[0]) % 4 == 0)
 
     def precondition_small_gen(self, G: torch.Tensor, A: int, B: int):
         """G: [P, A, dim, B] in its own (contiguous) layout -> preconditioned, same layout."""
@@ -270,6 +282,7 @@ class NGState:
         Y = torch.empty_like(G)
         nat.ngd_small_proj(G.data_ptr(), Y.data_ptr(), self.W.data_ptr(), P, A, D, B, R, sums.data_ptr(),
                            J.data_ptr() if updating else 0, HH.data_ptr() if updating else 0, _native.stream_ptr())
+        self.last_ip = ip
         if updating:
             L = torch.bmm(J, self.W.transpose(1, 2)) if N > D else HH
             K = torch.bmm(J, J.transpose(1, 2))
@@ -332,6 +345,9 @@ class _ShapeGroup:
         return drive([self.precondition_gen(G)])[0]
 
     def precondition_gen(self, G: torch.Tensor):
+        # every axis preserves each matrix's Frobenius norm, so |G|^2 measured by the first
+        # (HIP) axis is handed on instead of re-reduced per axis
+        ip = None
         for ax, st in self.axes:
             a = ax + 1  # leading stack dim
             if st.small_ok(G):
@@ -339,11 +355,12 @@ class _ShapeGroup:
                 A = math.prod(self.shape[:ax])
                 B = math.prod(self.shape[ax + 1:])
                 G = (yield from st.precondition_small_gen(G, A, B)).view(G.shape)
-                continue
-            X = G.transpose(-1, a).contiguous()
-            shp = X.shape
-            Y = yield from st.precondition_gen(X.view(shp[0], -1, shp[-1]))
-            G = Y.view(shp).transpose(-1, a)
+            else:
+                X = G.transpose(-1, a).contiguous()
+                shp = X.shape
+                Y = yield from st.precondition_gen(X.view(shp[0], -1, shp[-1]), ip)
+                G = Y.view(shp).transpose(-1, a)
+            ip = st.last_ip
         return G
 
 

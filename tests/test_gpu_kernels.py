@@ -376,6 +376,30 @@ def test_ngd_small_proj_kernel_vs_torch(cuda, D, R, A, B):
     assert rel(buf2, buf[:2 * P]) < 1e-5
 
 
+@pytest.mark.parametrize("per", [4, 1000, 3 * 512 * 512 * 3])
+def test_ngd_sumsq_rescale_vs_torch(cuda, per):
+    """ngd_sumsq / ngd_rescale (float4 streaming, many workgroups per matrix) against the
+    PyTorch expressions, including the NaN guard (matrix 1 falls back to X)."""
+    from faster_distributed_training_amd.ops import _native
+    nat = _native.native()
+    G = 3
+    X = torch.randn(G, per, device=cuda)
+    Y = torch.randn(G, per, device=cuda)
+    Y[1, per // 2] = float("nan")
+    s = torch.zeros(2, G, device=cuda)
+    sp = _native.stream_ptr()
+    nat.ngd_sumsq(X.data_ptr(), per, G, s[0].data_ptr(), sp)
+    nat.ngd_sumsq(Y.data_ptr(), per, G, s[1].data_ptr(), sp)
+    ip, fp = (X.double() ** 2).sum(1), (Y.double() ** 2).sum(1)
+    ref = torch.where(torch.isnan(fp).view(-1, 1), X.double(), Y.double() * torch.sqrt(ip / (fp + 1e-30)).view(-1, 1))
+    nat.ngd_rescale(X.data_ptr(), Y.data_ptr(), per, G, s[0].data_ptr(), s[1].data_ptr(), sp)
+    torch.cuda.synchronize()
+    assert rel(s[0].double(), ip) < 1e-5
+    assert torch.isnan(s[1, 1]) and rel(s[1, [0, 2]].double(), fp[[0, 2]]) < 1e-5
+    assert torch.equal(Y[1], X[1])
+    assert rel(Y.double(), ref) < 1e-5
+
+
 def test_ngd_small_axes_match_gemm_path(cuda, monkeypatch):
     """A conv model's NGD steps with the kh / kw axes on the streaming HIP pass vs the same
     axes on transpose + batched GEMMs, both against the fp64 CPU path over 14 steps."""
