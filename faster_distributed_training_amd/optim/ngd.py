@@ -60,6 +60,8 @@ def orthonormal_special(rank: int, dim: int, dtype=torch.float32, device=None) -
 
 
 FUSED = os.environ.get("FDT_NGD_FUSED", "1") != "0"
+# one eigensolver launch per optimizer step for all update-step Z matrices (see Deferred)
+DEFER = os.environ.get("FDT_NGD_DEFER", "1") != "0"
 
 
 def _fused_small_math(X, R) -> bool:
@@ -73,27 +75,54 @@ def _native_eigh(device) -> bool:
     return E._use_native(torch.empty(1, 2, 2, device=device))
 
 
+class Deferred:
+    """A Z matrix whose eigenpairs only feed the preconditioner's NEXT step (the W / d / rho
+    update): the generator goes on without waiting, and ``drive`` solves every deferred Z of
+    the whole optimizer step in one eigensolver launch at the end, then calls ``fn(c, U)``."""
+    __slots__ = ("Z", "fn")
+
+    def __init__(self, Z, fn):
+        self.Z, self.fn = Z, fn
+
+
 def drive(gens):
     """Run preconditioner generators in lock-step: each yields a batch of Z matrices and
     receives ``(eigenvalues, eigenvectors)``; all Z pending at the same time are solved by
-    one ``eigh_many`` launch.  Returns the generators' return values."""
+    one ``eigh_many`` launch.  ``Deferred`` yields are collected and solved together after
+    all generators finished (one launch for all axes instead of one per axis level).
+    Returns the generators' return values."""
     from ..ops.eigh import eigh_many
     results = [None] * len(gens)
-    pending = {}
-    for i, g in enumerate(gens):
+    deferred = []
+
+    def advance(i, val, first=False):
+        g = gens[i]
         try:
-            pending[i] = next(g)
+            out = next(g) if first else g.send(val)
+            while isinstance(out, Deferred):
+                deferred.append(out)
+                out = g.send(None)
+            return out
         except StopIteration as e:
             results[i] = e.value
+            return None
+
+    pending = {}
+    for i in range(len(gens)):
+        z = advance(i, None, first=True)
+        if z is not None:
+            pending[i] = z
     while pending:
         idx = list(pending)
         outs = eigh_many([pending[i] for i in idx])
         pending = {}
         for i, o in zip(idx, outs):
-            try:
-                pending[i] = gens[i].send(o)
-            except StopIteration as e:
-                results[i] = e.value
+            z = advance(i, o)
+            if z is not None:
+                pending[i] = z
+    if deferred:
+        for d, (c, U) in zip(deferred, eigh_many([d.Z for d in deferred])):
+            d.fn(c, U)
     return results
 
 
@@ -109,6 +138,9 @@ class NGState:
         self.d = None
         self.rho = None
         self.last_ip = None  # per-matrix |X|^2 of the last call (HIP path), handed to the next axis
+        # HIP path: defer the eigensolve of an update to the end of the optimizer step (off
+        # only inside the initialisation iterations, where each one needs the previous W)
+        self.defer = True
 
     # -------------------------------------------------------------- schedule
     def _updating(self):
@@ -134,9 +166,13 @@ class NGState:
         if self.t == 0:
             self._init_default()
             self.t = 1
-            for _ in range(3):
-                yield from self._precondition_scaled(X, ip)
-                ip = self.last_ip
+            self.defer = False
+            try:
+                for _ in range(3):
+                    yield from self._precondition_scaled(X, ip)
+                    ip = self.last_ip
+            finally:
+                self.defer = True
             self.t = 0
         return (yield from self._precondition_scaled(X, ip))
 
@@ -238,7 +274,19 @@ class NGState:
         nat.ngd_pre_eigh(Kc.data_ptr(), Lc.data_ptr(), self.d.data_ptr(), self.rho.data_ptr(), Z.data_ptr(),
                          ise.data_ptr(), drho.data_ptr(), zs.data_ptr(), dsum.data_ptr(), G, R, self.alpha, self.eta,
                          float(N), float(D), sp)
+        post = (J, ise, drho, zs, dsum, trXX, N)
+        if self.defer and DEFER:
+            # the eigenpairs only shape this state's NEXT step: solved with every other
+            # axis' Z in one launch at the end of the optimizer step (``drive``)
+            yield Deferred(Z, lambda c, U: self._post_update(c, U, *post))
+            return
         c, U = yield Z                                            # eigh, ascending
+        self._post_update(c, U, *post)
+
+    def _post_update(self, c, U, J, ise, drho, zs, dsum, trXX, N):
+        nat = _native.native()
+        G, R, D = J.shape[0], self.rank, self.dim
+        dev = J.device
         A = torch.empty(G, R, R, device=dev, dtype=torch.float32)
         wc = torch.empty(G, R, device=dev, dtype=torch.float32)
         tr = trXX.contiguous()
@@ -262,8 +310,12 @@ class NGState:
         if self.t == 0:
             self._init_default()
             self.t = 1
-            for _ in range(3):
-                yield from self._small_step(G, A, B)
+            self.defer = False
+            try:
+                for _ in range(3):
+                    yield from self._small_step(G, A, B)
+            finally:
+                self.defer = True
             self.t = 0
         return (yield from self._small_step(G, A, B))
 

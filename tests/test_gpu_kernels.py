@@ -400,6 +400,36 @@ def test_ngd_sumsq_rescale_vs_torch(cuda, per):
     assert rel(Y.double(), ref) < 1e-5
 
 
+def test_ngd_deferred_eigh_matches_sync(cuda, monkeypatch):
+    """Update-step eigensolves deferred to one launch at the end of the optimizer step give
+    the same trajectory as solving each axis level before the next (they only feed the
+    next step's W); also counts the eigensolver launches of a steady update step."""
+    import torch.nn as nn
+    import faster_distributed_training_amd.optim.ngd as N
+    import faster_distributed_training_amd.ops.eigh as E
+    from faster_distributed_training_amd.utils.flat import FlatParams
+    calls = []
+    orig = E.eigh_many
+    monkeypatch.setattr(E, "eigh_many", lambda Zs, *a, **k: calls.append(len(Zs)) or orig(Zs, *a, **k))
+
+    def run(defer):
+        monkeypatch.setattr(N, "DEFER", defer)
+        torch.manual_seed(0)
+        m = nn.Sequential(nn.Conv2d(4, 8, 3), nn.Conv2d(8, 8, 3), nn.Linear(8, 12)).to(cuda)
+        f = FlatParams(m)
+        o = N.NGD(f, lr=0.05, momentum=0.9, weight_decay=1e-4)
+        for s in range(13):  # the last step (t = 12) is an update step
+            calls.clear()
+            f.grad.copy_(torch.randn(f.numel, generator=torch.Generator().manual_seed(s)).to(cuda))
+            o.step()
+        return f.data.clone(), list(calls)
+
+    (a, ca), (b, cb) = run(True), run(False)
+    assert ca == [sum(cb)], (ca, cb)  # one launch (all axes) vs one per axis level
+    assert len(cb) > 1
+    assert rel(a, b) < 1e-5
+
+
 def test_ngd_small_axes_match_gemm_path(cuda, monkeypatch):
     """A conv model's NGD steps with the kh / kw axes on the streaming HIP pass vs the same
     axes on transpose + batched GEMMs, both against the fp64 CPU path over 14 steps."""
