@@ -30,6 +30,7 @@ import torch.nn.functional as F
 from ..ops.attention import scaled_dot_product_attention
 from ..ops.embedding import embedding_sum
 from ..ops.layernorm import layer_norm_unbiased
+from ..ops.linear import linear
 from ..ops.mlp import fused_mlp
 
 
@@ -157,7 +158,8 @@ class PositionalWiseFFN(nn.Module):
         self.dropout = nn.Dropout(dropout)
 
     def forward(self, x):
-        return self.w_2(self.dropout(F.gelu(self.w_1(x))))
+        h = self.dropout(F.gelu(linear(x, self.w_1.weight, self.w_1.bias)))
+        return linear(h, self.w_2.weight, self.w_2.bias)
 
 
 class MultiheadAttention(nn.Module):
@@ -181,14 +183,14 @@ class MultiheadAttention(nn.Module):
         if query is key and key is value:
             w = torch.cat([l.weight for l in self.heads], 0)
             bias = torch.cat([l.bias for l in self.heads], 0)
-            qkv = F.linear(query, w, bias).view(b, L, 3, self.h, self.d_k)
+            qkv = linear(query, w, bias).view(b, L, 3, self.h, self.d_k)
             q, k, v = qkv.unbind(2)
         else:
             q, k, v = [l(t).view(b, -1, self.h, self.d_k) for l, t in zip(self.heads, (query, key, value))]
         p = self.dropout.p if self.training else 0.0
         x = scaled_dot_product_attention(q, k, v, mask, dropout_p=p,
                                          mask_value=(-1e-9 if self.faithful else None))
-        return self.output(x.reshape(b, L, self.h * self.d_k))
+        return linear(x.reshape(b, L, self.h * self.d_k), self.output.weight, self.output.bias)
 
 
 class LayerNorm(nn.Module):
