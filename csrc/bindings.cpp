@@ -63,6 +63,7 @@ PYBIND11_MODULE(_fdt_native, m) {
   DEF(embedding_bwd);
   DEF(bias_relu_fwd);
   DEF(relu_bwd_colsum);
+  DEF(colsum_bf16);
   // data
   DEF(augment);
   DEF(rng_advance);

@@ -62,6 +62,10 @@ struct Args {
   uint32_t drop_thr;  // drop iff hash < drop_thr (p * 2^32); 0 = no dropout
   float keep_scale;   // 1 / (1 - p)
   uint64_t seed;
+  // optional device word XORed into the seed at kernel start: a HIP-graph replay draws new
+  // dropout masks from a per-step seed written before the replay (the kernel argument is
+  // frozen at capture)
+  const uint64_t* seed_ptr;
 };
 
 __device__ __forceinline__ bool dropped(const Args& a, int bh, int q, int key) {
@@ -129,6 +133,7 @@ __device__ __forceinline__ float masked_score(float s, int st, const Args& a) {
 
 // ------------------------------------------------------------------------------ forward
 __global__ __launch_bounds__(256) void attn_fwd_kernel(Args a) {
+  if (a.seed_ptr != nullptr) a.seed ^= *a.seed_ptr;
   __shared__ __attribute__((aligned(16))) bf16 Ks[kTile * kRowLd];
   __shared__ __attribute__((aligned(16))) bf16 Vt[kD * kTLd];
   __shared__ int8_t ms[kTile];
@@ -247,6 +252,7 @@ __global__ __launch_bounds__(256) void attn_bwd_prep_kernel(Args a) {
 }
 
 __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(Args a) {
+  if (a.seed_ptr != nullptr) a.seed ^= *a.seed_ptr;
   __shared__ __attribute__((aligned(16))) bf16 Qs[kTile * kRowLd];
   __shared__ __attribute__((aligned(16))) bf16 Qt[kD * kTLd];
   __shared__ __attribute__((aligned(16))) bf16 Gs[kTile * kRowLd];  // dO rows
@@ -339,6 +345,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(Args a) {
 }
 
 __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(Args a) {
+  if (a.seed_ptr != nullptr) a.seed ^= *a.seed_ptr;
   __shared__ __attribute__((aligned(16))) bf16 Ks[kTile * kRowLd];
   __shared__ __attribute__((aligned(16))) bf16 Vs[kTile * kRowLd];
   __shared__ __attribute__((aligned(16))) bf16 Kt[kD * kTLd];
@@ -417,7 +424,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(Args a) {
 }
 
 static Args make_args(uint64_t q, uint64_t k, uint64_t v, const std::vector<long>& st, uint64_t mask, int B, int L,
-                      int H, float fill, float p_drop, uint64_t seed) {
+                      int H, float fill, float p_drop, uint64_t seed, uint64_t seed_ptr) {
   FDT_CHECK(st.size() == 9, "attention: 9 strides (q, k, v x batch, position, head)");
   FDT_CHECK(L >= 1 && L <= 4096 && B >= 1 && H >= 1, "attention: bad shape");
   FDT_CHECK(p_drop >= 0.f && p_drop < 1.f, "attention: dropout in [0, 1)");
@@ -437,15 +444,17 @@ static Args make_args(uint64_t q, uint64_t k, uint64_t v, const std::vector<long
   a.drop_thr = (uint32_t)fminf(p_drop * 4294967296.f, 4294967295.f);
   a.keep_scale = 1.f / (1.f - p_drop);
   a.seed = seed;
+  a.seed_ptr = P<const uint64_t>(seed_ptr);
   return a;
 }
 
 }  // namespace attn
 
 void attn_fwd(uint64_t q, uint64_t k, uint64_t v, const std::vector<long>& strides, uint64_t out, uint64_t lse,
-              uint64_t mask, int B, int L, int H, float fill, float p_drop, uint64_t seed, uint64_t stream) {
+              uint64_t mask, int B, int L, int H, float fill, float p_drop, uint64_t seed, uint64_t seed_ptr,
+              uint64_t stream) {
   using namespace attn;
-  Args a = make_args(q, k, v, strides, mask, B, L, H, fill, p_drop, seed);
+  Args a = make_args(q, k, v, strides, mask, B, L, H, fill, p_drop, seed, seed_ptr);
   a.out = P<bf16>(out);
   a.lse = P<float>(lse);
   hipLaunchKernelGGL(attn_fwd_kernel, dim3((L + kBlk - 1) / kBlk, H, B), dim3(256), 0, as_stream(stream), a);
@@ -454,9 +463,9 @@ void attn_fwd(uint64_t q, uint64_t k, uint64_t v, const std::vector<long>& strid
 
 void attn_bwd(uint64_t q, uint64_t k, uint64_t v, const std::vector<long>& strides, uint64_t o, uint64_t dout,
               uint64_t lse, uint64_t delta, uint64_t mask, uint64_t dq, uint64_t dk, uint64_t dv, int B, int L, int H,
-              float fill, float p_drop, uint64_t seed, uint64_t stream) {
+              float fill, float p_drop, uint64_t seed, uint64_t seed_ptr, uint64_t stream) {
   using namespace attn;
-  Args a = make_args(q, k, v, strides, mask, B, L, H, fill, p_drop, seed);
+  Args a = make_args(q, k, v, strides, mask, B, L, H, fill, p_drop, seed, seed_ptr);
   a.o = P<const bf16>(o);
   a.dout = P<const bf16>(dout);
   a.lse = P<float>(lse);

@@ -39,6 +39,56 @@ __global__ __launch_bounds__(256) void relu_bwd_colsum_kernel(const T* __restric
   }
 }
 
+// out[c] += sum_r x[r][c] for bf16 x [rows][cols] (cols % 8 == 0), fp32 out zeroed by the
+// caller: the bias gradient of a linear layer.  Lane = 8 adjacent columns (one 16-B load);
+// a 256-thread block covers (256 / lanes_per_row) rows x cols_blk columns of a row chunk,
+// folds its rows in registers + LDS, one atomic per column per block.
+__global__ __launch_bounds__(256) void colsum_bf16_kernel(const bf16* __restrict__ x, float* __restrict__ out,
+                                                          long rows, int cols, int rows_per_blk) {
+  __shared__ float red[256 * 8];
+  const int lanes = min(cols / 8 - blockIdx.x * 32, 32);  // column groups of this block
+  const int cg = threadIdx.x % 32, rl = threadIdx.x / 32;  // 32 column groups x 8 row lanes
+  const long r0 = (long)blockIdx.y * rows_per_blk;
+  const long r1 = min(rows, r0 + rows_per_blk);
+  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  const int c0 = (blockIdx.x * 32 + cg) * 8;
+  if (cg < lanes) {
+    for (long r = r0 + rl; r < r1; r += 8) {
+      const uint4 v = *reinterpret_cast<const uint4*>(x + r * cols + c0);
+      const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        acc[2 * j] += __uint_as_float(w[j] << 16);
+        acc[2 * j + 1] += __uint_as_float(w[j] & 0xffff0000u);
+      }
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) red[(rl * 32 + cg) * 8 + j] = acc[j];
+  __syncthreads();
+  // 256 threads fold the 8 row lanes of 32 x 8 columns
+  const int col = threadIdx.x;  // 0..255 = cg * 8 + j
+  if (col / 8 < lanes) {
+    float s = 0.f;
+#pragma unroll
+    for (int l = 0; l < 8; ++l) s += red[(l * 32 + col / 8) * 8 + (col % 8)];
+    atomicAdd(out + blockIdx.x * 256 + col, s);
+  }
+}
+
+void colsum_bf16(uint64_t x, uint64_t out, long rows, int cols, uint64_t stream) {
+  FDT_CHECK(cols % 8 == 0 && x % 16 == 0, "colsum_bf16: cols % 8 == 0, 16-B aligned rows");
+  if (rows == 0 || cols == 0) return;
+  const int cblk = (cols / 8 + 31) / 32;
+  // ~512 workgroups in total, >= 64 rows per block
+  long rpb = rows * cblk / 512;
+  if (rpb < 64) rpb = 64;
+  rpb = (rpb + 7) / 8 * 8;
+  dim3 grid((unsigned)cblk, (unsigned)((rows + rpb - 1) / rpb));
+  colsum_bf16_kernel<<<grid, 256, 0, as_stream(stream)>>>(P<const bf16>(x), P<float>(out), rows, cols, (int)rpb);
+  FDT_LAUNCH_CHECK();
+}
+
 #define DISPATCH_T(dt, ...)                                     \
   switch (dt) {                                                 \
     case kF32: { using T = float; __VA_ARGS__; break; }         \

@@ -54,7 +54,16 @@ class Transformer(nn.Module):
         self.n_layers = n_layers
         self.alpha = alpha
         self.faithful = faithful
+        # (perm, lam[B]) device tensors that replace the in-forward sampling (a HIP-graph
+        # runner samples outside the captured region and writes them before each replay)
+        self.mix_override = None
         self.init_params()
+
+    def sample_lam(self) -> float:
+        """The manifold-mixup coefficient (host sample, as the reference's ``.item()``)."""
+        if self.alpha > 0:
+            return float(torch.distributions.beta.Beta(self.alpha, self.alpha).sample())
+        return float(self.alpha)
 
     def forward(self, x, token_types, index, mask=None):
         """Returns ``(logits, perm_index, lam)`` like the reference (``transformer.py:84``).
@@ -71,12 +80,11 @@ class Transformer(nn.Module):
         x = self.dropout_post(x)
         b = x.size(0)
         mix = self.training or self.faithful
-        if mix and self.alpha > 0:
-            lam = float(torch.distributions.beta.Beta(self.alpha, self.alpha).sample())
-        elif mix:
-            lam = float(self.alpha)
-        else:
-            lam = 1.0
+        if mix and self.mix_override is not None:
+            from ..ops.mixup import mixup_interpolate
+            perm, lam_t = self.mix_override
+            return self.classifier(mixup_interpolate(x, perm, lam_t)), perm, lam_t
+        lam = self.sample_lam() if mix else 1.0
         if mix:
             perm = torch.randperm(b, device=x.device)
             from ..ops.mixup import mixup_interpolate

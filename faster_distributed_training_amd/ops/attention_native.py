@@ -13,6 +13,10 @@ from . import _native
 
 HEAD_DIM = 64
 
+# Set by a HIP-graph runner while it captures (train/graphs.py): a device uint64 re-drawn
+# before every replay and XORed into each call's (capture-time constant) dropout seed.
+DEVICE_SEED = None
+
 
 def _strides(*ts):
     out = []
@@ -37,18 +41,19 @@ class FlashAttention(torch.autograd.Function):
         out = torch.empty(B, L, H, D, device=q.device, dtype=torch.bfloat16)
         lse = torch.empty(B, H, L, device=q.device, dtype=torch.float32)
         seed = int(torch.randint(0, 2**62, (1,)).item()) if dropout_p > 0 else 0
+        sptr = DEVICE_SEED.data_ptr() if (DEVICE_SEED is not None and dropout_p > 0) else 0
         nat.attn_fwd(q.data_ptr(), k.data_ptr(), v.data_ptr(), _strides(q, k, v), out.data_ptr(), lse.data_ptr(),
                      0 if mask_u8 is None else mask_u8.data_ptr(), B, L, H, float(fill), float(dropout_p), seed,
-                     _native.stream_ptr())
+                     sptr, _native.stream_ptr())
         ctx.save_for_backward(q, k, v, out, lse, mask_u8)
-        ctx.cfg = (float(fill), float(dropout_p), seed)
+        ctx.cfg = (float(fill), float(dropout_p), seed, sptr)
         return out
 
     @staticmethod
     def backward(ctx, g):
         nat = _native.native()
         q, k, v, out, lse, mask_u8 = ctx.saved_tensors
-        fill, p, seed = ctx.cfg
+        fill, p, seed, sptr = ctx.cfg
         B, L, H, D = q.shape
         g = g.contiguous().to(torch.bfloat16)
         dq = torch.empty(B, L, H, D, device=q.device, dtype=torch.bfloat16)
@@ -57,7 +62,7 @@ class FlashAttention(torch.autograd.Function):
         delta = torch.empty(B, H, L, device=q.device, dtype=torch.float32)
         nat.attn_bwd(q.data_ptr(), k.data_ptr(), v.data_ptr(), _strides(q, k, v), out.data_ptr(), g.data_ptr(),
                      lse.data_ptr(), delta.data_ptr(), 0 if mask_u8 is None else mask_u8.data_ptr(),
-                     dq.data_ptr(), dk.data_ptr(), dv.data_ptr(), B, L, H, fill, p, seed, _native.stream_ptr())
+                     dq.data_ptr(), dk.data_ptr(), dv.data_ptr(), B, L, H, fill, p, seed, sptr, _native.stream_ptr())
         return dq, dk, dv, None, None, None
 
 

@@ -34,6 +34,8 @@ from . import checkpoint as ckpt
 from . import resilience
 from .metrics import DeviceMeter, JsonlLogger, PhaseProfiler, draw_graph, peak_memory_gb
 
+TR_GRAPHS = os.environ.get("FDT_TR_GRAPHS", "1") != "0"
+
 
 @dataclass
 class TransformerConfig:
@@ -116,6 +118,7 @@ class TransformerTrainer:
         self.global_step = 0
         self.skipped = torch.zeros((), device=self.device, dtype=torch.int32)
         self.profiler = PhaseProfiler(cfg.profile_steps, self.device.type == "cuda", self.logger)
+        self._graphs, self._graph_stream, self._graph_pool = {}, None, None
         if cfg.auto_resume and resilience.restore_last(self):
             print0(f"auto-resume: restored {self.last_path}, continuing at epoch {self.start_epoch}")
 
@@ -175,19 +178,30 @@ class TransformerTrainer:
                                                       steps_per_epoch=max(1, steps), cycle_momentum=True)
         return opt, sch
 
-    def _autocast(self):
+    def _autocast(self, cache=True):
         p = self.cfg.precision
         if p == "fp32":
             return torch.autocast(self.device.type, enabled=False)
         dt = torch.bfloat16 if p == "bf16" else torch.float16
-        return torch.autocast(self.device.type, dtype=dt, enabled=(self.device.type == "cuda" or p == "bf16"))
+        return torch.autocast(self.device.type, dtype=dt, enabled=(self.device.type == "cuda" or p == "bf16"),
+                              cache_enabled=cache)
 
-    def train_step(self, tokens, labels, types, masks):
-        cfg = self.cfg
+    # ------------------------------------------------------------ HIP graphs
+    # The transformer step is ~700 kernels, many of them short: the host, not the GPU,
+    # bounds it (measured: 4.1 ms of a 16.8 ms step idle between kernels).  Forward, loss
+    # and backward of one batch shape are captured once into a HIP graph and replayed;
+    # per-step randomness stays live: the manifold-mixup permutation and lambda are written
+    # into static device buffers before each replay, torch's dropout advances its philox
+    # offset per replay, and the attention kernels XOR a per-replay device seed into their
+    # dropout hash (ops/attention_native.py DEVICE_SEED).  Gradients accumulate into the
+    # flat gradient buffer (static; the optimizer zeroes it).  Single process, bf16 only.
+    def _graphs_on(self):
+        return (TR_GRAPHS and self.device.type == "cuda" and self.reducer is None and self.fsdp is None
+                and not self.scaler.enabled and self.cfg.profile_steps <= 0 and not self.cfg.faithful
+                and self.model.training)
+
+    def _fwd_bwd(self, tokens, labels, types, masks):
         prof = self.profiler
-        resilience.maybe_inject_fault(self.global_step, self.rank)
-        prof.begin_step()
-        prof.mark("forward")
         mask = masks.view(masks.shape[0], 1, 1, masks.shape[1])
         with self._autocast():
             logits, perm, lam = self.model(tokens, types, self.pos_index, mask)
@@ -195,6 +209,72 @@ class TransformerTrainer:
             loss = mixup_criterion(None, logits, labels, labels[perm], lam)
         prof.mark("backward")
         self.scaler.scale_loss(loss).backward()
+        return loss, logits, perm, lam
+
+    def _graph_fill(self, st, tokens, labels, types, masks):
+        st["tokens"].copy_(tokens, non_blocking=True)
+        st["types"].copy_(types, non_blocking=True)
+        st["masks"].copy_(masks, non_blocking=True)
+        st["labels"].copy_(labels, non_blocking=True)
+        torch.randperm(tokens.shape[0], device=self.device, out=st["perm"])
+        lam = self.model.sample_lam()
+        st["lam"].fill_(lam)
+        st["seed"].random_()
+        return lam
+
+    def _fwd_bwd_graphed(self, tokens, labels, types, masks):
+        from ..ops import attention_native as AN
+        from ..ops.mixup import mixup_cross_entropy
+        key = (tuple(tokens.shape), tuple(masks.shape), str(tokens.dtype))
+        ent = self._graphs.get(key, 0)
+        if isinstance(ent, int):
+            if self._graph_stream is None:
+                self._graph_stream = torch.cuda.Stream(device=self.device)
+                self._graph_pool = torch.cuda.graph_pool_handle()
+            if ent < 2:  # eager warm-up steps on a side stream (lazy library / allocator init)
+                self._graphs[key] = ent + 1
+                s = self._graph_stream
+                s.wait_stream(torch.cuda.current_stream())
+                with torch.cuda.stream(s):
+                    out = self._fwd_bwd(tokens, labels, types, masks)
+                torch.cuda.current_stream().wait_stream(s)
+                return out
+            B = tokens.shape[0]
+            st = dict(tokens=torch.empty_like(tokens), types=torch.empty_like(types), masks=torch.empty_like(masks),
+                      labels=torch.empty_like(labels),
+                      perm=torch.empty(B, dtype=torch.long, device=self.device),
+                      lam=torch.empty(B, dtype=torch.float32, device=self.device),
+                      seed=torch.zeros(1, dtype=torch.int64, device=self.device))
+            g = torch.cuda.CUDAGraph()
+            torch.cuda.synchronize()
+            AN.DEVICE_SEED = st["seed"]
+            self.model.mix_override = (st["perm"], st["lam"])
+            try:
+                with torch.cuda.graph(g, pool=self._graph_pool):
+                    mask = st["masks"].view(B, 1, 1, st["masks"].shape[1])
+                    with self._autocast(cache=False):  # no cast cache across a graph capture
+                        logits, perm, _ = self.model(st["tokens"], st["types"], self.pos_index, mask)
+                        loss = mixup_cross_entropy(logits, st["labels"], st["labels"][perm], st["lam"])
+                    loss.backward()
+            finally:
+                AN.DEVICE_SEED = None
+                self.model.mix_override = None
+            st.update(graph=g, loss=loss, logits=logits)
+            self._graphs[key] = ent = st
+        lam = self._graph_fill(ent, tokens, labels, types, masks)
+        ent["graph"].replay()
+        return ent["loss"], ent["logits"], ent["perm"], lam
+
+    def train_step(self, tokens, labels, types, masks):
+        cfg = self.cfg
+        prof = self.profiler
+        resilience.maybe_inject_fault(self.global_step, self.rank)
+        prof.begin_step()
+        prof.mark("forward")
+        if self._graphs_on():
+            loss, logits, perm, lam = self._fwd_bwd_graphed(tokens, labels, types, masks)
+        else:
+            loss, logits, perm, lam = self._fwd_bwd(tokens, labels, types, masks)
         prof.mark("grad_sync")
         if self.reducer is not None:
             self.reducer.finish()

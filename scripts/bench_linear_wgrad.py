@@ -65,6 +65,11 @@ def main():
         fn()
         torch.cuda.synchronize()
         err = ((out - ref).norm() / ref.norm()).item()
+        from faster_distributed_training_amd.ops.linear import bias_grad
+        t_bsum = timeit(lambda: g.sum(0, dtype=torch.float32))
+        t_bgemv = timeit(lambda: bias_grad(g))
+        print(f"  bias grad: column sum {t_bsum:.1f} us, GEMV {t_bgemv:.1f} us "
+              f"(rel diff {((bias_grad(g) - g.float().sum(0)).norm() / g.float().sum(0).norm()).item():.1e})")
         gf = 2.0 * M * fin * fout / 1e9
         print(f"in {fin:5d} out {fout:5d}: library {t_lib:7.1f} us ({gf / t_lib:6.1f} TF/s)  split-K bmm {t_sk:7.1f} us  "
               f"MFMA wgrad {t_wg:7.1f} us ({gf / t_wg:6.1f} TF/s, rel err {err:.1e})", flush=True)
