@@ -68,6 +68,7 @@ void embedding_bwd(uint64_t g, uint64_t ids, uint64_t types, uint64_t pos_ids, u
 // mlp.hip
 void bias_relu_fwd(uint64_t pre, uint64_t b, uint64_t act, long rows, int cols, int dt, uint64_t stream);
 void colsum_bf16(uint64_t x, uint64_t out, long rows, int cols, uint64_t stream);
+void slab_sum_acc(uint64_t src, uint64_t dst, int s, long ld, long n, uint64_t stream);
 void relu_bwd_colsum(uint64_t gact, uint64_t pre, uint64_t gpre, uint64_t gb, long rows, int cols, int dt,
                      uint64_t stream);
 // augment.hip
@@ -103,7 +104,14 @@ void attn_fwd(uint64_t q, uint64_t k, uint64_t v, const std::vector<long>& strid
               uint64_t stream);
 void attn_bwd(uint64_t q, uint64_t k, uint64_t v, const std::vector<long>& strides, uint64_t o, uint64_t dout,
               uint64_t lse, uint64_t delta, uint64_t mask, uint64_t dq, uint64_t dk, uint64_t dv, int B, int L, int H,
-              float fill, float p_drop, uint64_t seed, uint64_t seed_ptr, uint64_t stream);
+              float fill, float p_drop, uint64_t seed, uint64_t seed_ptr, long grad_ld, uint64_t stream);
+// dropout.hip
+void dropout_add_fwd(uint64_t y, uint64_t x, uint64_t out, long n, float p, uint64_t seed, uint64_t seed_ptr,
+                     uint64_t stream);
+void dropout_bwd(uint64_t g, uint64_t gy, long n, float p, uint64_t seed, uint64_t seed_ptr, uint64_t stream);
+void gelu_dropout_fwd(uint64_t a, uint64_t h, long n, float p, uint64_t seed, uint64_t seed_ptr, uint64_t stream);
+void gelu_dropout_bwd(uint64_t g, uint64_t a, uint64_t ga, long n, float p, uint64_t seed, uint64_t seed_ptr,
+                      uint64_t stream);
 // ngd.hip
 void ngd_sumsq(uint64_t X, long per, int G, uint64_t out, uint64_t stream);
 bool ngd_small_supported(int D, int R);

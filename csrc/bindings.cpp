@@ -64,6 +64,11 @@ PYBIND11_MODULE(_fdt_native, m) {
   DEF(bias_relu_fwd);
   DEF(relu_bwd_colsum);
   DEF(colsum_bf16);
+  DEF(slab_sum_acc);
+  DEF(dropout_add_fwd);
+  DEF(dropout_bwd);
+  DEF(gelu_dropout_fwd);
+  DEF(gelu_dropout_bwd);
   // data
   DEF(augment);
   DEF(rng_advance);

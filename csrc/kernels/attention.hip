@@ -52,6 +52,7 @@ struct Args {
   bf16* dq;
   bf16* dk;
   bf16* dv;
+  long gl;  // position stride of dq/dk/dv (H*D contiguous; 3*H*D = packed [B][L][3][H][D])
   const uint8_t* mask;  // [B][L] nonzero = keep; nullptr = no mask
   float* lse;           // [B][H][L] log2-domain log-sum-exp
   float* delta;         // [B][H][L]
@@ -329,7 +330,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(Args a) {
   }
 
   if (kv) {
-    const long off = (((long)b * a.L + key) * a.H + hd) * kD;
+    const long off = ((long)b * a.L + key) * a.gl + hd * kD;
 #pragma unroll
     for (int dt = 0; dt < 2; ++dt)
 #pragma unroll
@@ -412,7 +413,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(Args a) {
   }
 
   if (qv) {
-    bf16* dp = a.dq + (((long)b * a.L + q) * a.H + hd) * kD;
+    bf16* dp = a.dq + ((long)b * a.L + q) * a.gl + hd * kD;
 #pragma unroll
     for (int dt = 0; dt < 2; ++dt)
 #pragma unroll
@@ -463,9 +464,11 @@ void attn_fwd(uint64_t q, uint64_t k, uint64_t v, const std::vector<long>& strid
 
 void attn_bwd(uint64_t q, uint64_t k, uint64_t v, const std::vector<long>& strides, uint64_t o, uint64_t dout,
               uint64_t lse, uint64_t delta, uint64_t mask, uint64_t dq, uint64_t dk, uint64_t dv, int B, int L, int H,
-              float fill, float p_drop, uint64_t seed, uint64_t seed_ptr, uint64_t stream) {
+              float fill, float p_drop, uint64_t seed, uint64_t seed_ptr, long grad_ld, uint64_t stream) {
   using namespace attn;
   Args a = make_args(q, k, v, strides, mask, B, L, H, fill, p_drop, seed, seed_ptr);
+  FDT_CHECK(grad_ld == 0 || (grad_ld >= (long)H * kD && grad_ld % 8 == 0), "attention: bad gradient row stride");
+  a.gl = grad_ld == 0 ? (long)H * kD : grad_ld;
   a.o = P<const bf16>(o);
   a.dout = P<const bf16>(dout);
   a.lse = P<float>(lse);

@@ -5,6 +5,8 @@
 // per element (survey Q6); this is the whole of it in one launch.
 #include "common.h"
 
+#include <algorithm>
+
 namespace fdt {
 
 template <typename T>
@@ -86,6 +88,59 @@ void colsum_bf16(uint64_t x, uint64_t out, long rows, int cols, uint64_t stream)
   rpb = (rpb + 7) / 8 * 8;
   dim3 grid((unsigned)cblk, (unsigned)((rows + rpb - 1) / rpb));
   colsum_bf16_kernel<<<grid, 256, 0, as_stream(stream)>>>(P<const bf16>(x), P<float>(out), rows, cols, (int)rpb);
+  FDT_LAUNCH_CHECK();
+}
+
+// dst[i] += sum_j src[j * ld + i] for j < s (fp32): the split-K weight-gradient slabs (or
+// per-block LayerNorm partials) folded straight into the fp32 master gradient -- one pass
+// instead of a reduction kernel + a separate accumulate kernel.  Block = 64 float4 columns x
+// 4 slab lanes; grid.y splits the slab axis when the columns alone give too few workgroups
+// (LayerNorm: 512 slabs x 128 float4) -- those blocks combine with atomics.
+__global__ __launch_bounds__(256) void slab_sum_acc_kernel(const float* __restrict__ src, float* __restrict__ dst,
+                                                           int s, long ld4, long n4, int s_per_blk) {
+  __shared__ float4 red[4][64];
+  const int cl = threadIdx.x & 63, rl = threadIdx.x >> 6;
+  const long i = blockIdx.x * 64L + cl;
+  const int j0 = blockIdx.y * s_per_blk, j1 = min(s, j0 + s_per_blk);
+  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (i < n4)
+    for (int j = j0 + rl; j < j1; j += 4) {
+      const float4 v = reinterpret_cast<const float4*>(src)[(long)j * ld4 + i];
+      acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+    }
+  red[rl][cl] = acc;
+  __syncthreads();
+  if (rl == 0 && i < n4) {
+#pragma unroll
+    for (int r = 1; r < 4; ++r) {
+      acc.x += red[r][cl].x; acc.y += red[r][cl].y; acc.z += red[r][cl].z; acc.w += red[r][cl].w;
+    }
+    float4* d = reinterpret_cast<float4*>(dst) + i;
+    if (gridDim.y == 1) {
+      float4 o = *d;
+      o.x += acc.x; o.y += acc.y; o.z += acc.z; o.w += acc.w;
+      *d = o;
+    } else {
+      float* df = reinterpret_cast<float*>(d);
+      atomicAdd(df + 0, acc.x); atomicAdd(df + 1, acc.y); atomicAdd(df + 2, acc.z); atomicAdd(df + 3, acc.w);
+    }
+  }
+}
+
+void slab_sum_acc(uint64_t src, uint64_t dst, int s, long ld, long n, uint64_t stream) {
+  FDT_CHECK(n % 4 == 0 && ld % 4 == 0 && src % 16 == 0 && dst % 16 == 0 && s >= 1,
+            "slab_sum_acc: n, ld multiples of 4, 16-B aligned");
+  if (n == 0) return;
+  const long n4 = n / 4;
+  const long nbx = (n4 + 63) / 64;
+  int spb = s;
+  if (nbx < 512) {  // split the slab axis: ~512 workgroups, >= 16 slabs each
+    spb = (int)std::max<long>(16, ((long)s * nbx + 511) / 512);
+    spb = (spb + 3) / 4 * 4;
+    if (spb > s) spb = s;
+  }
+  dim3 grid((unsigned)nbx, (unsigned)((s + spb - 1) / spb));
+  slab_sum_acc_kernel<<<grid, 256, 0, as_stream(stream)>>>(P<const float>(src), P<float>(dst), s, ld / 4, n4, spb);
   FDT_LAUNCH_CHECK();
 }
 

@@ -27,7 +27,8 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
-from ..ops.attention import scaled_dot_product_attention
+from ..ops.dropout import dropout_add, gelu_dropout
+from ..ops.attention import packed_attention, scaled_dot_product_attention
 from ..ops.embedding import embedding_sum
 from ..ops.layernorm import layer_norm_unbiased
 from ..ops.linear import linear
@@ -166,7 +167,7 @@ class PositionalWiseFFN(nn.Module):
         self.dropout = nn.Dropout(dropout)
 
     def forward(self, x):
-        h = self.dropout(F.gelu(linear(x, self.w_1.weight, self.w_1.bias)))
+        h = gelu_dropout(linear(x, self.w_1.weight, self.w_1.bias), self.dropout.p, self.training)
         return linear(h, self.w_2.weight, self.w_2.bias)
 
 
@@ -192,9 +193,10 @@ class MultiheadAttention(nn.Module):
             w = torch.cat([l.weight for l in self.heads], 0)
             bias = torch.cat([l.bias for l in self.heads], 0)
             qkv = linear(query, w, bias).view(b, L, 3, self.h, self.d_k)
-            q, k, v = qkv.unbind(2)
-        else:
-            q, k, v = [l(t).view(b, -1, self.h, self.d_k) for l, t in zip(self.heads, (query, key, value))]
+            p = self.dropout.p if self.training else 0.0
+            x = packed_attention(qkv, mask, dropout_p=p, mask_value=(-1e-9 if self.faithful else None))
+            return linear(x.reshape(b, L, self.h * self.d_k), self.output.weight, self.output.bias)
+        q, k, v = [l(t).view(b, -1, self.h, self.d_k) for l, t in zip(self.heads, (query, key, value))]
         p = self.dropout.p if self.training else 0.0
         x = scaled_dot_product_attention(q, k, v, mask, dropout_p=p,
                                          mask_value=(-1e-9 if self.faithful else None))
@@ -224,7 +226,7 @@ class sublayerConnectionAttention(nn.Module):  # noqa: N801 (reference name)
     def forward(self, x, mask=None):
         y = self.layernorm(x)
         y = self.multiheads(y, y, y, mask)
-        return self.dropout(y) + x
+        return dropout_add(y, x, self.dropout.p, self.training)
 
 
 class sublayerConnectionFFN(nn.Module):  # noqa: N801 (reference name)
@@ -235,7 +237,7 @@ class sublayerConnectionFFN(nn.Module):  # noqa: N801 (reference name)
         self.dropout = nn.Dropout(p=dropout_connection)
 
     def forward(self, x):
-        return self.dropout(self.ffn(self.layernorm(x))) + x
+        return dropout_add(self.ffn(self.layernorm(x)), x, self.dropout.p, self.training)
 
 
 class Classifier(nn.Module):

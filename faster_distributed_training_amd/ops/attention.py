@@ -44,3 +44,15 @@ def scaled_dot_product_attention(q, k, v, mask=None, dropout_p=0.0, mask_value=N
         if an.supported(q, k, v):
             return an.attention_native(q, k, v, mask, dropout_p, mask_value)
     return attention_reference(q, k, v, mask, dropout_p, mask_value)
+
+
+def packed_attention(qkv, mask=None, dropout_p=0.0, mask_value=None):
+    """qkv: (B, L, 3, H, D), the fused Q/K/V projection output.  On MI355X the HIP kernels
+    read Q/K/V in place and write the packed gradient; otherwise unbind + the reference."""
+    if _native.use_native(qkv):
+        from . import attention_native as an
+        q, k, v = qkv.unbind(2)
+        if an.supported(q, k, v):
+            return an.attention_packed(qkv, mask, dropout_p, mask_value)
+    q, k, v = qkv.unbind(2)
+    return attention_reference(q, k, v, mask, dropout_p, mask_value)

@@ -34,9 +34,18 @@ def supported(q, k, v) -> bool:
 
 
 class FlashAttention(torch.autograd.Function):
+    """``packed`` (k = v = None): q is the fused projection output [B, L, 3, H, D] and the
+    backward writes dq/dk/dv straight into one [B, L, 3, H, D] gradient (the kernels take
+    its row stride) -- no stack/cat of three gradients (measured 77 us per layer at
+    bs 256 x L 128 as a separate copy kernel)."""
+
     @staticmethod
     def forward(ctx, q, k, v, mask_u8, dropout_p: float, fill: float):
         nat = _native.native()
+        packed = k is None
+        qkv = q
+        if packed:
+            q, k, v = qkv.unbind(2)
         B, L, H, D = q.shape
         out = torch.empty(B, L, H, D, device=q.device, dtype=torch.bfloat16)
         lse = torch.empty(B, H, L, device=q.device, dtype=torch.float32)
@@ -45,33 +54,52 @@ class FlashAttention(torch.autograd.Function):
         nat.attn_fwd(q.data_ptr(), k.data_ptr(), v.data_ptr(), _strides(q, k, v), out.data_ptr(), lse.data_ptr(),
                      0 if mask_u8 is None else mask_u8.data_ptr(), B, L, H, float(fill), float(dropout_p), seed,
                      sptr, _native.stream_ptr())
-        ctx.save_for_backward(q, k, v, out, lse, mask_u8)
-        ctx.cfg = (float(fill), float(dropout_p), seed, sptr)
+        ctx.save_for_backward(qkv if packed else q, None if packed else k, None if packed else v, out, lse, mask_u8)
+        ctx.cfg = (float(fill), float(dropout_p), seed, sptr, packed)
         return out
 
     @staticmethod
     def backward(ctx, g):
         nat = _native.native()
         q, k, v, out, lse, mask_u8 = ctx.saved_tensors
-        fill, p, seed, sptr = ctx.cfg
+        fill, p, seed, sptr, packed = ctx.cfg
+        if packed:
+            q, k, v = q.unbind(2)
         B, L, H, D = q.shape
         g = g.contiguous().to(torch.bfloat16)
-        dq = torch.empty(B, L, H, D, device=q.device, dtype=torch.bfloat16)
-        dk = torch.empty_like(dq)
-        dv = torch.empty_like(dq)
+        if packed:
+            dqkv = torch.empty(B, L, 3, H, D, device=q.device, dtype=torch.bfloat16)
+            dq, dk, dv = dqkv.unbind(2)
+        else:
+            dq = torch.empty(B, L, H, D, device=q.device, dtype=torch.bfloat16)
+            dk = torch.empty_like(dq)
+            dv = torch.empty_like(dq)
         delta = torch.empty(B, H, L, device=q.device, dtype=torch.float32)
         nat.attn_bwd(q.data_ptr(), k.data_ptr(), v.data_ptr(), _strides(q, k, v), out.data_ptr(), g.data_ptr(),
                      lse.data_ptr(), delta.data_ptr(), 0 if mask_u8 is None else mask_u8.data_ptr(),
-                     dq.data_ptr(), dk.data_ptr(), dv.data_ptr(), B, L, H, fill, p, seed, sptr, _native.stream_ptr())
+                     dq.data_ptr(), dk.data_ptr(), dv.data_ptr(), B, L, H, fill, p, seed, sptr,
+                     dq.stride(1) if packed else 0, _native.stream_ptr())
+        if packed:
+            return dqkv, None, None, None, None, None
         return dq, dk, dv, None, None, None
+
+
+def _mask_u8(mask):
+    if mask is None:
+        return None
+    m = mask if mask.dtype == torch.uint8 else (mask != 0).to(torch.uint8)
+    return m.contiguous()
+
+
+def attention_packed(qkv, mask=None, dropout_p=0.0, mask_value=None):
+    """qkv: (B, L, 3, H, 64) bf16 with contiguous head dim (the fused Q/K/V projection
+    output); gradient returned in the same packed layout."""
+    fill = float("-inf") if mask_value is None else float(mask_value)
+    return FlashAttention.apply(qkv, None, None, _mask_u8(mask), float(dropout_p), fill)
 
 
 def attention_native(q, k, v, mask=None, dropout_p=0.0, mask_value=None):
     """q, k, v: (B, L, H, 64) bf16; mask (B, L) with nonzero = keep; ``mask_value`` None =
     true masking, else the reference's fill value for masked scores."""
-    m = None
-    if mask is not None:
-        m = mask if mask.dtype == torch.uint8 else (mask != 0).to(torch.uint8)
-        m = m.contiguous()
     fill = float("-inf") if mask_value is None else float(mask_value)
-    return FlashAttention.apply(q, k, v, m, float(dropout_p), fill)
+    return FlashAttention.apply(q, k, v, _mask_u8(mask), float(dropout_p), fill)

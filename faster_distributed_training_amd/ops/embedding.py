@@ -36,6 +36,7 @@ class _EmbeddingNative(torch.autograd.Function):
                           pos_w.data_ptr(), seg_w.data_ptr(), out.data_ptr(), B, L, d, float(scale),
                           tok_w.shape[0], pos_w.shape[0], seg_w.shape[0], _native.stream_ptr())
         ctx.save_for_backward(ids32, ty32, pos32)
+        ctx.params = (tok_w, pos_w, seg_w)
         ctx.shapes = (tok_w.shape, pos_w.shape, seg_w.shape)
         ctx.scale = scale
         return out
@@ -47,12 +48,25 @@ class _EmbeddingNative(torch.autograd.Function):
         B, L = ids32.shape
         (vt, d), (vp, _), (vs, _) = ctx.shapes
         g = g.contiguous().float()
-        gt = torch.zeros(vt, d, device=g.device, dtype=torch.float32)
-        gp = torch.zeros(vp, d, device=g.device, dtype=torch.float32)
-        gs = torch.zeros(vs, d, device=g.device, dtype=torch.float32)
+        # the kernels accumulate atomically: with direct gradients (ops/linear.py) they add
+        # straight into the flat fp32 gradient views -- no zeroed 62 MB token-table scratch
+        # and no separate accumulate pass over it
+        from .linear import direct_target, mark_ready
+        tg = [direct_target(p) for p in ctx.params]
+        direct = all(t is not None for t in tg) and all(ctx.needs_input_grad[3:6])
+        if direct:
+            gt, gp, gs = tg
+        else:
+            gt = torch.zeros(vt, d, device=g.device, dtype=torch.float32)
+            gp = torch.zeros(vp, d, device=g.device, dtype=torch.float32)
+            gs = torch.zeros(vs, d, device=g.device, dtype=torch.float32)
         nat.embedding_bwd(g.data_ptr(), ids32.data_ptr(), ty32.data_ptr(), pos32.data_ptr(), gt.data_ptr(),
                           gp.data_ptr(), gs.data_ptr(), B, L, d, float(ctx.scale), vt, vp, vs,
                           _native.stream_ptr())
+        if direct:
+            for p in ctx.params:
+                mark_ready(p)
+            return None, None, None, None, None, None, None
         return None, None, None, gt, gp, gs, None
 
 

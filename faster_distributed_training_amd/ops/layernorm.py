@@ -40,6 +40,7 @@ class _LayerNormNative(torch.autograd.Function):
                           rstd.data_ptr(), rows, d, float(eps), DT[x2.dtype], DT[out_dtype], DT[a.dtype],
                           _native.stream_ptr())
         ctx.save_for_backward(x2, a, mean, rstd)
+        ctx.params = (a, b)
         ctx.shape = shape
         ctx.eps = eps
         return y.view(*shape[:-1], d)
@@ -58,6 +59,16 @@ class _LayerNormNative(torch.autograd.Function):
         nat.layernorm_bwd(gy2.data_ptr(), x2.data_ptr(), a.data_ptr(), mean.data_ptr(), rstd.data_ptr(),
                           gx.data_ptr(), part.data_ptr(), rows, d, nblk, DT[gy2.dtype], DT[x2.dtype],
                           DT[a.dtype], float(ctx.eps), _native.stream_ptr())
+        from .linear import direct_target, mark_ready, slab_sum_into
+        pa, pb = ctx.params
+        ta = direct_target(pa) if ctx.needs_input_grad[1] else None
+        tb = direct_target(pb) if ctx.needs_input_grad[2] else None
+        if ta is not None and tb is not None:  # partials folded straight into the fp32 grads
+            slab_sum_into(part[0], ta)
+            slab_sum_into(part[1], tb)
+            mark_ready(pa)
+            mark_ready(pb)
+            return gx.view(ctx.shape), None, None, None, None
         ga, gb = part.sum(1).unbind(0)
         return gx.view(ctx.shape), ga.to(a.dtype), gb.to(a.dtype), None, None
 

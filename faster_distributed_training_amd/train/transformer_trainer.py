@@ -35,6 +35,9 @@ from . import resilience
 from .metrics import DeviceMeter, JsonlLogger, PhaseProfiler, draw_graph, peak_memory_gb
 
 TR_GRAPHS = os.environ.get("FDT_TR_GRAPHS", "1") != "0"
+# linear / LayerNorm / embedding backward kernels accumulate straight into the flat fp32
+# gradient views (ops/linear.py direct gradients) instead of autograd's per-parameter add
+DIRECT_GRADS = os.environ.get("FDT_DIRECT_GRADS", "1") != "0"
 
 
 @dataclass
@@ -105,6 +108,9 @@ class TransformerTrainer:
             else:
                 from ..parallel.ddp import BucketReducer
                 self.reducer = BucketReducer(self.flat, self.model, bucket_mb=cfg.bucket_mb)
+        if self.fsdp is None and DIRECT_GRADS:
+            from ..ops.linear import enable_direct_grads
+            enable_direct_grads(self.model.parameters())
         seed_everything(cfg.seed, self.rank)
         self.space = self.fsdp.view if self.fsdp is not None else self.flat
         self._build_data()

@@ -1,0 +1,122 @@
+"""Transformer epilogue kernels vs fp32 PyTorch references: fused dropout + residual add,
+fused GELU + dropout (csrc/kernels/dropout.hip), packed-QKV attention gradients
+(attention.hip row-strided dQ/dK/dV), direct gradient accumulation into flat fp32 views
+(slab_sum_acc, colsum, LayerNorm partials, embedding scatter)."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+
+def test_dropout_add_matches_reference(cuda):
+    from faster_distributed_training_amd.ops.dropout import dropout_add
+    torch.manual_seed(0)
+    y = torch.randn(4096, 512, device=cuda, dtype=torch.bfloat16, requires_grad=True)
+    x = torch.randn(4096, 512, device=cuda, dtype=torch.float32, requires_grad=True)
+    # p = 0: exact residual add
+    out = dropout_add(y, x, 0.0)
+    torch.testing.assert_close(out, x + y.float(), rtol=0, atol=0)
+    # p = 0.1: kept elements scaled by 1/0.9, ~10 % dropped, backward regenerates the mask
+    p = 0.1
+    out = dropout_add(y, x, p)
+    d = (out - x).detach()
+    kept = d != 0
+    frac = 1 - kept.float().mean().item()
+    assert abs(frac - p) < 0.01, frac
+    torch.testing.assert_close(d[kept], (y.float() / (1 - p)).detach()[kept], rtol=1e-6, atol=1e-6)
+    g = torch.randn_like(x)
+    out.backward(g)
+    torch.testing.assert_close(x.grad, g)
+    ref = (g * kept / (1 - p)).to(torch.bfloat16)
+    torch.testing.assert_close(y.grad.float(), ref.float(), rtol=1e-2, atol=1e-2)
+    # a different host seed draws a different mask
+    out2 = dropout_add(y, x, p)
+    assert not torch.equal(out, out2)
+
+
+def test_gelu_dropout_matches_reference(cuda):
+    from faster_distributed_training_amd.ops.dropout import gelu_dropout
+    torch.manual_seed(1)
+    a = torch.randn(2048, 2048, device=cuda, dtype=torch.bfloat16, requires_grad=True)
+    af = a.detach().float().requires_grad_(True)
+    h = gelu_dropout(a, 0.0)
+    hr = F.gelu(af)
+    torch.testing.assert_close(h.float(), hr, rtol=1e-2, atol=1e-2)
+    g = torch.randn_like(h)
+    h.backward(g)
+    hr.backward(g.float())
+    torch.testing.assert_close(a.grad.float(), af.grad, rtol=2e-2, atol=2e-2)
+    a.grad = None
+    p = 0.25
+    h = gelu_dropout(a, p)
+    ref = F.gelu(a.detach().float()) / (1 - p)
+    kept = h != 0
+    frac = 1 - kept.float().mean().item()
+    assert abs(frac - p) < 0.01, frac
+    torch.testing.assert_close(h.float()[kept], ref[kept], rtol=1e-2, atol=1e-2)
+    h.backward(g)
+    af2 = a.detach().float().requires_grad_(True)
+    (F.gelu(af2) * kept / (1 - p)).backward(g.float())
+    # where gelu(a) rounds to 0 in bf16 the mask cannot be read back from h: skip those
+    amb = (F.gelu(a.detach().float()) / (1 - p)).to(torch.bfloat16) == 0
+    torch.testing.assert_close(a.grad.float()[~amb], af2.grad[~amb], rtol=2e-2, atol=2e-2)
+
+
+def test_packed_attention_grads_match_unpacked(cuda):
+    from faster_distributed_training_amd.ops import attention_native as AN
+    torch.manual_seed(2)
+    B, L, H, D = 4, 128, 8, 64
+    qkv = torch.randn(B, L, 3, H, D, device=cuda, dtype=torch.bfloat16, requires_grad=True)
+    mask = torch.ones(B, L, device=cuda, dtype=torch.uint8)
+    mask[1, 100:] = 0
+    out_p = AN.attention_packed(qkv, mask)
+    g = torch.randn_like(out_p)
+    out_p.backward(g)
+    q, k, v = (t.detach().clone().requires_grad_(True) for t in qkv.detach().unbind(2))
+    out_u = AN.attention_native(q, k, v, mask)
+    out_u.backward(g)
+    assert torch.equal(out_p, out_u)
+    assert torch.equal(qkv.grad, torch.stack([q.grad, k.grad, v.grad], 2))
+
+
+@pytest.mark.parametrize("s,shape", [(16, (1536, 512)), (512, (512,)), (7, (4, 36))])
+def test_slab_sum_acc(cuda, s, shape):
+    """Wide (split-K slabs, no atomics) and tall (LayerNorm partials, slab axis split over
+    workgroups + atomics) shapes."""
+    from faster_distributed_training_amd.ops.linear import slab_sum_into
+    src = torch.randn(s, *shape, device=cuda)
+    dst = torch.randn(*shape, device=cuda)
+    ref = dst + src.double().sum(0).float()
+    slab_sum_into(src, dst)
+    torch.testing.assert_close(dst, ref, rtol=1e-5, atol=1e-4)
+
+
+def test_direct_grads_match_autograd(cuda):
+    """Transformer forward+backward with flat gradients: kernels accumulating straight into
+    the fp32 views give the same gradients as autograd's per-parameter accumulation."""
+    from faster_distributed_training_amd.models.transformer import Transformer
+    from faster_distributed_training_amd.ops.linear import enable_direct_grads
+    from faster_distributed_training_amd.utils.flat import FlatParams
+
+    def run(direct):
+        torch.manual_seed(0)
+        m = Transformer(4, 1000, n_layers=2, h=8, d_model=512, d_ff=2048, d_hidden=256, maxlen=128,
+                        alpha=0.0).to(cuda)
+        flat = FlatParams(m, device=cuda)
+        enable_direct_grads(m.parameters(), direct)
+        m.eval()
+        torch.manual_seed(1)
+        tok = torch.randint(0, 1000, (64, 128), device=cuda)
+        types = torch.zeros_like(tok)
+        idx = torch.arange(128, device=cuda)
+        mask = torch.ones(64, 1, 1, 128, device=cuda)
+        for _ in range(2):  # two backwards: accumulation on top of an existing gradient
+            with torch.autocast("cuda", dtype=torch.bfloat16):
+                logits, _, _ = m(tok, types, idx, mask)
+            logits.float().square().mean().backward()
+        torch.cuda.synchronize()
+        return flat.grad.clone()
+
+    ga, gd = run(False), run(True)
+    assert ((ga - gd).norm() / ga.norm()).item() < 1e-3
