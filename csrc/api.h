@@ -67,7 +67,7 @@ void embedding_bwd(uint64_t g, uint64_t ids, uint64_t types, uint64_t pos_ids, u
                    int B, int L, int d, float scale, int vt, int vp, int vs, uint64_t stream);
 // mlp.hip
 void bias_relu_fwd(uint64_t pre, uint64_t b, uint64_t act, long rows, int cols, int dt, uint64_t stream);
-void colsum_bf16(uint64_t x, uint64_t out, long rows, int cols, uint64_t stream);
+void colsum_bf16(uint64_t x, uint64_t out, long rows, int cols, long ld, uint64_t stream);
 void slab_sum_acc(uint64_t src, uint64_t dst, int s, long ld, long n, uint64_t stream);
 void relu_bwd_colsum(uint64_t gact, uint64_t pre, uint64_t gpre, uint64_t gb, long rows, int cols, int dt,
                      uint64_t stream);

@@ -46,7 +46,7 @@ __global__ __launch_bounds__(256) void relu_bwd_colsum_kernel(const T* __restric
 // a 256-thread block covers (256 / lanes_per_row) rows x cols_blk columns of a row chunk,
 // folds its rows in registers + LDS, one atomic per column per block.
 __global__ __launch_bounds__(256) void colsum_bf16_kernel(const bf16* __restrict__ x, float* __restrict__ out,
-                                                          long rows, int cols, int rows_per_blk) {
+                                                          long rows, int cols, long ld, int rows_per_blk) {
   __shared__ float red[256 * 8];
   const int lanes = min(cols / 8 - blockIdx.x * 32, 32);  // column groups of this block
   const int cg = threadIdx.x % 32, rl = threadIdx.x / 32;  // 32 column groups x 8 row lanes
@@ -56,7 +56,7 @@ __global__ __launch_bounds__(256) void colsum_bf16_kernel(const bf16* __restrict
   const int c0 = (blockIdx.x * 32 + cg) * 8;
   if (cg < lanes) {
     for (long r = r0 + rl; r < r1; r += 8) {
-      const uint4 v = *reinterpret_cast<const uint4*>(x + r * cols + c0);
+      const uint4 v = *reinterpret_cast<const uint4*>(x + r * ld + c0);
       const uint32_t w[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
@@ -78,8 +78,9 @@ __global__ __launch_bounds__(256) void colsum_bf16_kernel(const bf16* __restrict
   }
 }
 
-void colsum_bf16(uint64_t x, uint64_t out, long rows, int cols, uint64_t stream) {
-  FDT_CHECK(cols % 8 == 0 && x % 16 == 0, "colsum_bf16: cols % 8 == 0, 16-B aligned rows");
+void colsum_bf16(uint64_t x, uint64_t out, long rows, int cols, long ld, uint64_t stream) {
+  if (ld == 0) ld = cols;
+  FDT_CHECK(cols % 8 == 0 && ld % 8 == 0 && ld >= cols && x % 16 == 0, "colsum_bf16: cols, ld % 8 == 0, 16-B aligned rows");
   if (rows == 0 || cols == 0) return;
   const int cblk = (cols / 8 + 31) / 32;
   // ~512 workgroups in total, >= 64 rows per block
@@ -87,7 +88,7 @@ void colsum_bf16(uint64_t x, uint64_t out, long rows, int cols, uint64_t stream)
   if (rpb < 64) rpb = 64;
   rpb = (rpb + 7) / 8 * 8;
   dim3 grid((unsigned)cblk, (unsigned)((rows + rpb - 1) / rpb));
-  colsum_bf16_kernel<<<grid, 256, 0, as_stream(stream)>>>(P<const bf16>(x), P<float>(out), rows, cols, (int)rpb);
+  colsum_bf16_kernel<<<grid, 256, 0, as_stream(stream)>>>(P<const bf16>(x), P<float>(out), rows, cols, ld, (int)rpb);
   FDT_LAUNCH_CHECK();
 }
 

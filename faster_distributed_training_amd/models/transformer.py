@@ -31,7 +31,7 @@ from ..ops.dropout import dropout_add, gelu_dropout
 from ..ops.attention import packed_attention, scaled_dot_product_attention
 from ..ops.embedding import embedding_sum
 from ..ops.layernorm import layer_norm_unbiased
-from ..ops.linear import linear
+from ..ops.linear import linear, linear_cat
 from ..ops.mlp import fused_mlp
 
 
@@ -190,9 +190,8 @@ class MultiheadAttention(nn.Module):
     def forward(self, query, key, value, mask=None):
         b, L, _ = query.shape
         if query is key and key is value:
-            w = torch.cat([l.weight for l in self.heads], 0)
-            bias = torch.cat([l.bias for l in self.heads], 0)
-            qkv = linear(query, w, bias).view(b, L, 3, self.h, self.d_k)
+            qkv = linear_cat(query, [l.weight for l in self.heads], [l.bias for l in self.heads])
+            qkv = qkv.view(b, L, 3, self.h, self.d_k)
             p = self.dropout.p if self.training else 0.0
             x = packed_attention(qkv, mask, dropout_p=p, mask_value=(-1e-9 if self.faithful else None))
             return linear(x.reshape(b, L, self.h * self.d_k), self.output.weight, self.output.bias)

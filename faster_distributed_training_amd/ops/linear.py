@@ -65,6 +65,23 @@ def direct_target(p):
     return g
 
 
+def enable_shadow_weights(flat) -> None:
+    """Point every parameter at its bf16 shadow in ``flat`` (utils/flat.py: rewritten by the
+    optimizer kernel each step), so bf16 compute reads it instead of casting the fp32 master
+    weight each forward (~50 cast kernels per transformer step)."""
+    if flat.shadow is None:
+        return
+    for s in flat.slots:
+        s.param._fdt_shadow = flat.shadow_view(s.param)
+
+
+def cast_weight(w: torch.Tensor, dt) -> torch.Tensor:
+    sh = getattr(w, "_fdt_shadow", None)
+    if sh is not None and dt == torch.bfloat16 and w.dtype == torch.float32:
+        return sh
+    return w.to(dt)
+
+
 def _native_ok(t) -> bool:
     from . import _native
     return _native.use_native(t) and hasattr(_native.native(), "slab_sum_acc")
@@ -103,9 +120,11 @@ def wgrad_into(gy: torch.Tensor, x: torch.Tensor, dst: torch.Tensor) -> None:
 def bias_grad_into(gy: torch.Tensor, dst: torch.Tensor) -> None:
     """dst += column sums of gy [M, out] (the colsum kernel accumulates atomically)."""
     from . import _native
-    if (gy.dtype == torch.bfloat16 and gy.is_contiguous() and gy.shape[1] % 8 == 0 and _native.use_native(gy)
-            and hasattr(_native.native(), "colsum_bf16") and dst.numel() == gy.shape[1]):
-        _native.native().colsum_bf16(gy.data_ptr(), dst.data_ptr(), gy.shape[0], gy.shape[1], _native.stream_ptr())
+    if (gy.dtype == torch.bfloat16 and gy.stride(1) == 1 and gy.stride(0) % 8 == 0 and gy.data_ptr() % 16 == 0
+            and gy.shape[1] % 8 == 0 and _native.use_native(gy) and hasattr(_native.native(), "colsum_bf16")
+            and dst.numel() == gy.shape[1]):
+        _native.native().colsum_bf16(gy.data_ptr(), dst.data_ptr(), gy.shape[0], gy.shape[1], gy.stride(0),
+                                     _native.stream_ptr())
     else:
         dst.add_(gy.sum(0, dtype=torch.float32).view_as(dst))
 
@@ -118,7 +137,7 @@ def bias_grad(gy: torch.Tensor) -> torch.Tensor:
     if (gy.dtype == torch.bfloat16 and gy.is_contiguous() and gy.shape[1] % 8 == 0 and _native.use_native(gy)
             and hasattr(_native.native(), "colsum_bf16")):
         out = torch.zeros(gy.shape[1], device=gy.device, dtype=torch.float32)
-        _native.native().colsum_bf16(gy.data_ptr(), out.data_ptr(), gy.shape[0], gy.shape[1], _native.stream_ptr())
+        _native.native().colsum_bf16(gy.data_ptr(), out.data_ptr(), gy.shape[0], gy.shape[1], 0, _native.stream_ptr())
         return out
     return gy.sum(0, dtype=torch.float32)
 
@@ -128,8 +147,8 @@ class _Linear(torch.autograd.Function):
     def forward(ctx, x, w, b, dt):
         xin_dtype = x.dtype
         xc = x.to(dt)
-        wc = w.to(dt)
-        y = F.linear(xc, wc, None if b is None else b.to(dt))
+        wc = cast_weight(w, dt)
+        y = F.linear(xc, wc, None if b is None else cast_weight(b, dt))
         ctx.save_for_backward(xc, wc)
         ctx.meta = (xin_dtype, w.dtype, None if b is None else b.dtype)
         ctx.params = (w, b)  # leaves whose gradient may be written in place (direct_target)
@@ -172,3 +191,86 @@ def linear(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor | None = No
         return F.linear(x, weight, bias)
     with torch.autocast("cuda", enabled=False):
         return _Linear.apply(x, weight, bias, dt)
+
+
+class _LinearCat(torch.autograd.Function):
+    """``F.linear(x, cat(ws), cat(bs))`` for row-stacked weights (the fused Q/K/V projection of
+    three ``nn.Linear``s): the weight gradient is one split-K product over the stacked rows
+    whose slabs are folded straight into each parameter's flat gradient (row-offset source,
+    slab stride = the stacked size), bias gradients by row-strided column sums -- no cat
+    backward split and no per-parameter accumulate kernels."""
+
+    @staticmethod
+    def forward(ctx, x, dt, n, *params):
+        ws, bs = params[:n], params[n:]
+        xc = x.to(dt)
+        wc = torch.cat([cast_weight(w, dt) for w in ws], 0)
+        bc = torch.cat([cast_weight(b, dt) for b in bs], 0) if bs else None
+        y = F.linear(xc, wc, bc)
+        ctx.save_for_backward(xc, wc)
+        ctx.params = (ws, bs)
+        ctx.xd = x.dtype
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        from . import _native
+        xc, wc = ctx.saved_tensors
+        ws, bs = ctx.params
+        n = len(ws)
+        g2 = gy.reshape(-1, gy.shape[-1]).to(wc.dtype)
+        x2 = xc.reshape(-1, xc.shape[-1])
+        dx = (g2 @ wc).view(xc.shape).to(ctx.xd) if ctx.needs_input_grad[0] else None
+        rows = [w.shape[0] for w in ws]
+        offs = [sum(rows[:i]) for i in range(n)]
+        gw = [None] * n
+        if any(ctx.needs_input_grad[3:3 + n]):
+            tg = [direct_target(w) for w in ws]
+            M, K, R = g2.shape[0], x2.shape[1], wc.shape[0]
+            s = _splits(M)
+            done = False
+            if all(t is not None for t in tg) and s > 1 and _native_ok(g2) and K % 4 == 0:
+                try:
+                    p = torch.bmm(g2.view(s, M // s, -1).transpose(1, 2), x2.view(s, M // s, -1),
+                                  out_dtype=torch.float32)
+                    for i in range(n):
+                        _native.native().slab_sum_acc(p.data_ptr() + offs[i] * K * 4, tg[i].data_ptr(), s, R * K,
+                                                      rows[i] * K, _native.stream_ptr())
+                    done = True
+                except (TypeError, RuntimeError):
+                    done = False
+            if done:
+                for w in ws:
+                    mark_ready(w)
+            else:
+                dw = wgrad(g2, x2)
+                for i, w in enumerate(ws):
+                    part = dw[offs[i]:offs[i] + rows[i]]
+                    if tg[i] is not None:
+                        tg[i].add_(part)
+                        mark_ready(w)
+                    else:
+                        gw[i] = part.to(w.dtype)
+        gb = [None] * len(bs)
+        for i, b in enumerate(bs):
+            if not ctx.needs_input_grad[3 + n + i]:
+                continue
+            cols = g2[:, offs[i]:offs[i] + rows[i]]
+            tgt = direct_target(b)
+            if tgt is not None:
+                bias_grad_into(cols, tgt)
+                mark_ready(b)
+            else:
+                gb[i] = bias_grad(cols.contiguous()).to(b.dtype)
+        return (dx, None, None, *gw, *gb)
+
+
+def linear_cat(x: torch.Tensor, weights, biases=None) -> torch.Tensor:
+    """``F.linear(x, cat(weights), cat(biases))`` with per-parameter gradients (see _LinearCat)."""
+    biases = list(biases) if biases is not None else []
+    if x.is_cuda:
+        dt = torch.get_autocast_dtype("cuda") if torch.is_autocast_enabled("cuda") else x.dtype
+        if dt in (torch.bfloat16, torch.float16) and x.numel() // x.shape[-1] >= 4096:
+            with torch.autocast("cuda", enabled=False):
+                return _LinearCat.apply(x, dt, len(weights), *weights, *biases)
+    return F.linear(x, torch.cat(list(weights), 0), torch.cat(biases, 0) if biases else None)

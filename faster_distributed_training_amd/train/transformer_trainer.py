@@ -38,6 +38,8 @@ TR_GRAPHS = os.environ.get("FDT_TR_GRAPHS", "1") != "0"
 # linear / LayerNorm / embedding backward kernels accumulate straight into the flat fp32
 # gradient views (ops/linear.py direct gradients) instead of autograd's per-parameter add
 DIRECT_GRADS = os.environ.get("FDT_DIRECT_GRADS", "1") != "0"
+# bf16 shadow weights kept by the optimizer kernels (utils/flat.py) for the linears
+SHADOW = os.environ.get("FDT_TR_SHADOW", "1") != "0"
 
 
 @dataclass
@@ -99,7 +101,12 @@ class TransformerTrainer:
         self.best_acc, self.start_epoch = ckpt.load_best_performance(self.ckpt_path, NUM_CLASSES, cfg.resume)
         if cfg.resume:
             ckpt.load_model_state(self.model, ckpt.load_checkpoint(self.ckpt_path)["net"])
-        self.flat = FlatParams(self.model, device=self.device)
+        shadow = (SHADOW and self.device.type == "cuda" and cfg.precision == "bf16"
+                  and not (cfg.distributed and cfg.fsdp))
+        self.flat = FlatParams(self.model, device=self.device, with_shadow=shadow)
+        if shadow:  # bf16 compute reads the optimizer-maintained bf16 copy (no per-step casts)
+            from ..ops.linear import enable_shadow_weights
+            enable_shadow_weights(self.flat)
         self.reducer = self.fsdp = None
         if cfg.distributed:
             if cfg.fsdp:

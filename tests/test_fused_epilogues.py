@@ -120,3 +120,32 @@ def test_direct_grads_match_autograd(cuda):
 
     ga, gd = run(False), run(True)
     assert ((ga - gd).norm() / ga.norm()).item() < 1e-3
+
+
+@pytest.mark.parametrize("direct", [False, True])
+def test_linear_cat_matches_reference(cuda, direct):
+    """Stacked Q/K/V projection: output and per-parameter gradients vs fp32 F.linear(cat)."""
+    from faster_distributed_training_amd.ops.linear import enable_direct_grads, linear_cat
+    torch.manual_seed(3)
+    ws = [torch.randn(512, 512, device=cuda) * 0.05 for _ in range(3)]
+    bs = [torch.randn(512, device=cuda) * 0.1 for _ in range(3)]
+    params = [t.clone().requires_grad_(True) for t in ws + bs]
+    if direct:  # pre-existing fp32 gradients that the kernels accumulate into
+        for p in params:
+            p.grad = torch.ones_like(p)
+        enable_direct_grads(params)
+    x = torch.randn(8192, 512, device=cuda)
+    g = torch.randn(8192, 1536, device=cuda)
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        y = linear_cat(x, params[:3], params[3:])
+    y.backward(g.to(y.dtype))
+    ref_p = [t.clone().requires_grad_(True) for t in ws + bs]
+    xr = x.to(torch.bfloat16).float()
+    yr = F.linear(xr, torch.cat([p.to(torch.bfloat16).float() for p in ref_p[:3]]),
+                  torch.cat([p.to(torch.bfloat16).float() for p in ref_p[3:]]))
+    yr.backward(g.to(torch.bfloat16).float())
+    torch.testing.assert_close(y.float(), yr, rtol=2e-2, atol=2e-2)
+    for p, r in zip(params, ref_p):
+        want = r.grad + (1.0 if direct else 0.0)
+        err = ((p.grad - want).norm() / want.norm()).item()
+        assert err < 1e-2, err

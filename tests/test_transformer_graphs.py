@@ -61,3 +61,29 @@ def test_attention_device_seed_redraws_dropout(cuda):
     assert torch.equal(a, b)
     assert not torch.equal(a, c)
     assert all(torch.isfinite(t.grad).all() for t in (q, k, v))
+
+
+def test_shadow_weights_match_casts(cuda, monkeypatch):
+    """bf16 shadow weights (rewritten by the optimizer kernel) give the same trajectory as
+    casting the fp32 master weights each forward (graphs off, dropout off)."""
+    import torch.nn as nn
+    import faster_distributed_training_amd.train.transformer_trainer as T
+
+    def run(shadow):
+        monkeypatch.setattr(T, "SHADOW", shadow)
+        torch.manual_seed(0)
+        tr = _trainer(False, monkeypatch)
+        assert (tr.flat.shadow is not None) == shadow
+        for mod in tr.model.modules():
+            if isinstance(mod, nn.Dropout):
+                mod.p = 0.0
+        tr.model.alpha = 0.0
+        it = iter(tr.train_loader)
+        losses = [float(tr.train_step(*next(it))) for _ in range(4)]
+        torch.cuda.synchronize()
+        return losses, tr.flat.data.clone()
+
+    lc, pc = run(False)
+    ls, ps = run(True)
+    assert max(abs(a - b) / max(abs(a), 1e-6) for a, b in zip(lc, ls)) < 1e-3, (lc, ls)
+    assert ((pc - ps).norm() / pc.norm()).item() < 1e-4
