@@ -452,24 +452,46 @@ __global__ __launch_bounds__(kBlk) void residual_act_bwd_kernel(const T* __restr
   long r_end = r_begin + rows_per_blk;
   if (r_end > M) r_end = M;
   float p0[8] = {0, 0, 0, 0, 0, 0, 0, 0}, p1[8] = {0, 0, 0, 0, 0, 0, 0, 0}, p2[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  for (long r = r_begin + rr; r < r_end; r += RPP) {
-    const long e = r * C + c0;
-    float gv[8], av[8], bv[8], ov[8];
-    Vec8<T>::load(g + e, gv);
-    uint32_t m = 0;
-    if (mask) m = mask[e >> 3];
-    else Vec8<T>::load(out + e, ov);
-    Vec8<T>::load(ya + e, av);
-    if (yb) Vec8<T>::load(yb + e, bv);
+  // Two rows per iteration: every load of both rows is issued before the first use, so each
+  // thread keeps 6-8 16-B loads in flight (one row per trip left the kernel at ~3 TB/s on the
+  // small per-GPU batches where each thread only walks ~16 rows).
+  auto row = [&](long e, const float* gv, const float* av, const float* bv, const float* ov, uint32_t m) {
+    float gp8[8];
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
       const float gp = mask ? ((m >> i) & 1u ? gv[i] : 0.f) : gv[i] * act_grad_from_out(ov[i], act, alpha);
-      gv[i] = gp;
+      gp8[i] = gp;
       p0[i] = fmaf(gp, av[i], p0[i]);
       p1[i] += gp;
       if (yb) p2[i] = fmaf(gp, bv[i], p2[i]);
     }
-    Vec8<T>::store(gpre + e, gv);
+    Vec8<T>::store(gpre + e, gp8);
+  };
+  long r = r_begin + rr;
+  for (; r + RPP < r_end; r += 2 * RPP) {
+    const long e0 = r * C + c0, e1 = e0 + (long)RPP * C;
+    float g0[8], a0[8], b0[8], o0[8], g1[8], a1[8], b1[8], o1[8];
+    uint32_t m0 = 0, m1 = 0;
+    Vec8<T>::load(g + e0, g0);
+    Vec8<T>::load(g + e1, g1);
+    Vec8<T>::load(ya + e0, a0);
+    Vec8<T>::load(ya + e1, a1);
+    if (yb) { Vec8<T>::load(yb + e0, b0); Vec8<T>::load(yb + e1, b1); }
+    if (mask) { m0 = mask[e0 >> 3]; m1 = mask[e1 >> 3]; }
+    else { Vec8<T>::load(out + e0, o0); Vec8<T>::load(out + e1, o1); }
+    row(e0, g0, a0, b0, o0, m0);
+    row(e1, g1, a1, b1, o1, m1);
+  }
+  if (r < r_end) {
+    const long e = r * C + c0;
+    float gv[8], av[8], bv[8], ov[8];
+    uint32_t m = 0;
+    Vec8<T>::load(g + e, gv);
+    Vec8<T>::load(ya + e, av);
+    if (yb) Vec8<T>::load(yb + e, bv);
+    if (mask) m = mask[e >> 3];
+    else Vec8<T>::load(out + e, ov);
+    row(e, gv, av, bv, ov, m);
   }
 #pragma unroll
   for (int i = 0; i < 8; ++i) { sm[tid * 24 + i] = p0[i]; sm[tid * 24 + 8 + i] = p1[i]; sm[tid * 24 + 16 + i] = p2[i]; }
@@ -665,9 +687,17 @@ void residual_act_bwd(uint64_t g, uint64_t out, uint64_t mask, uint64_t ya, uint
   FDT_CHECK(out != 0 || mask != 0, "residual_act_bwd needs the output or its mask");
   ChanGeom gg = chan_geom(C);
   // ~1024 blocks: more waves in flight for this 4-5 stream kernel than the stats default
-  long target = 1024 / (gg.gy > 0 ? gg.gy : 1);
+  static const long blocks = [] {
+    const char* s = std::getenv("FDT_RAB_BLOCKS");  // A/B knob for the block-count target
+    return s ? std::max(64L, std::atol(s)) : 1024L;
+  }();
+  static const long min_iters = [] {
+    const char* s = std::getenv("FDT_RAB_MINIT");  // min rows each thread walks (atomics amortisation)
+    return s ? std::max(1L, std::atol(s)) : 1L;
+  }();
+  long target = blocks / (gg.gy > 0 ? gg.gy : 1);
   long r = (M + target - 1) / target;
-  if (r < gg.RPP) r = gg.RPP;
+  if (r < gg.RPP * min_iters) r = gg.RPP * min_iters;
   r = (r + gg.RPP - 1) / gg.RPP * gg.RPP;
   dim3 grid((unsigned)((M + r - 1) / r), gg.gy);
   DISPATCH_T(dt, {
