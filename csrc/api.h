@@ -40,14 +40,14 @@ void grad_norm_finalize(uint64_t part, int nb, float max_norm, uint64_t out, uin
 void sgd_step(uint64_t p, uint64_t g, uint64_t buf, uint64_t shadow, long n, float lr, float momentum, float dampening,
               float wd, int nesterov, int first, uint64_t gsc, uint64_t found_inf, int zero_grad, uint64_t stream);
 void madgrad_step(uint64_t p, uint64_t g, uint64_t gss, uint64_t s, uint64_t x0, uint64_t shadow, long n, float lr,
-                  float momentum, float wd, float eps, int decouple, long k, uint64_t gsc, uint64_t found_inf,
-                  int zero_grad, uint64_t stream);
+                  float momentum, float wd, float eps, int decouple, long k, uint64_t kskip, uint64_t gsc,
+                  uint64_t found_inf, int zero_grad, uint64_t stream);
 void mirror_madgrad_step(uint64_t p, uint64_t g, uint64_t gss, uint64_t z, uint64_t shadow, long n, float lr,
-                         float momentum, float wd, float eps, int decouple, long k, uint64_t gsc, uint64_t found_inf,
-                         int zero_grad, uint64_t stream);
+                         float momentum, float wd, float eps, int decouple, long k, uint64_t kskip, uint64_t gsc,
+                         uint64_t found_inf, int zero_grad, uint64_t stream);
 void adam_step(uint64_t p, uint64_t g, uint64_t m, uint64_t v, uint64_t shadow, long n, float lr, float b1, float b2,
-               float eps, float wd, int adamw, long step, uint64_t gsc, uint64_t found_inf, int zero_grad,
-               uint64_t stream);
+               float eps, float wd, int adamw, long step, uint64_t kskip, uint64_t gsc, uint64_t found_inf,
+               int zero_grad, uint64_t stream);
 void cast_bf16(uint64_t x, uint64_t y, long n, uint64_t stream);
 // mixup.hip
 void mixup_fwd(uint64_t x, uint64_t perm, uint64_t lam, uint64_t out, int b, long inner, int dt, uint64_t stream);
@@ -74,7 +74,7 @@ void relu_bwd_colsum(uint64_t gact, uint64_t pre, uint64_t gpre, uint64_t gb, lo
 // augment.hip
 void augment(uint64_t src, uint64_t idx, uint64_t labels_src, uint64_t labels_out, uint64_t out, int B, int H, int W,
              int C, int Cout, int pad, int do_flip, uint64_t rng, float m0, float m1, float m2, float s0, float s1,
-             float s2, int nchw, int dt_out, uint64_t stream);
+             float s2, int nchw, int pad_norm, int dt_out, uint64_t stream);
 void rng_advance(uint64_t rng, uint64_t stream);
 // conv_igemm.hip
 void conv_igemm(uint64_t x, uint64_t x2, uint64_t ps, uint64_t pt, uint64_t pg, uint64_t w, uint64_t out, uint64_t part,

@@ -8,6 +8,13 @@
 // kernels) or NCHW.  Per-sample random parameters come from a counter-based hash of
 // (seed, counter, sample) read from device memory, so the kernel is graph-replayable
 // and needs no host RNG.
+//
+// Transform order (the reference permutes crop / flip / normalise once per run,
+// resnet50_test.py:304-309): flip commutes with both other transforms in distribution
+// (a mirrored uniform crop offset is again uniform), so the only observable difference is
+// whether normalisation runs before the zero-padded crop: then padding is 0 in normalised
+// space (pad_norm = 1) instead of raw 0 -> -mean/std (pad_norm = 0, torchvision's
+// crop -> flip -> normalise order).
 #include "common.h"
 
 namespace fdt {
@@ -18,7 +25,7 @@ __global__ __launch_bounds__(256) void augment_kernel(const uint8_t* __restrict_
                                                       TO* __restrict__ out, int B, int H, int W, int C, int Cout,
                                                       int pad, int do_flip, const long long* __restrict__ rng,
                                                       float m0, float m1, float m2, float is0, float is1, float is2,
-                                                      int nchw) {
+                                                      int nchw, int pad_norm) {
   const long total = (long)B * H * W;
   const uint64_t seed = rng ? (uint64_t)rng[0] : 0ull, ctr = rng ? (uint64_t)rng[1] : 0ull;
   for (long p = (long)blockIdx.x * blockDim.x + threadIdx.x; p < total; p += (long)gridDim.x * blockDim.x) {
@@ -40,8 +47,8 @@ __global__ __launch_bounds__(256) void augment_kernel(const uint8_t* __restrict_
     for (int c = 0; c < Cout; ++c) {
       float v = 0.f;
       if (c < C) {
-        float raw = inside ? (float)px[c] * (1.f / 255.f) : 0.f;
-        v = (raw - mean[c < 3 ? c : 2]) * istd[c < 3 ? c : 2];
+        const float raw = inside ? (float)px[c] * (1.f / 255.f) : 0.f;
+        v = (inside || !pad_norm) ? (raw - mean[c < 3 ? c : 2]) * istd[c < 3 ? c : 2] : 0.f;
       }
       long o = nchw ? (((long)b * Cout + c) * H + y) * W + x : p * Cout + c;
       out[o] = from_f<TO>(v);
@@ -51,7 +58,7 @@ __global__ __launch_bounds__(256) void augment_kernel(const uint8_t* __restrict_
 
 void augment(uint64_t src, uint64_t idx, uint64_t labels_src, uint64_t labels_out, uint64_t out, int B, int H, int W,
              int C, int Cout, int pad, int do_flip, uint64_t rng, float m0, float m1, float m2, float s0, float s1,
-             float s2, int nchw, int dt_out, uint64_t stream) {
+             float s2, int nchw, int pad_norm, int dt_out, uint64_t stream) {
   FDT_CHECK(C <= 3 && Cout >= C, "augment: C <= 3 and Cout >= C");
   long total = (long)B * H * W;
   if (total == 0) return;
@@ -61,12 +68,12 @@ void augment(uint64_t src, uint64_t idx, uint64_t labels_src, uint64_t labels_ou
     augment_kernel<bf16><<<g, 256, 0, as_stream(stream)>>>(P<const uint8_t>(src), P<const int>(idx),
                                                           P<const int>(labels_src), P<int>(labels_out), P<bf16>(out), B,
                                                           H, W, C, Cout, pad, do_flip, P<const long long>(rng), m0, m1,
-                                                          m2, 1.f / s0, 1.f / s1, 1.f / s2, nchw);
+                                                          m2, 1.f / s0, 1.f / s1, 1.f / s2, nchw, pad_norm);
   } else if (dt_out == kF32) {
     augment_kernel<float><<<g, 256, 0, as_stream(stream)>>>(P<const uint8_t>(src), P<const int>(idx),
                                                            P<const int>(labels_src), P<int>(labels_out), P<float>(out),
                                                            B, H, W, C, Cout, pad, do_flip, P<const long long>(rng), m0,
-                                                           m1, m2, 1.f / s0, 1.f / s1, 1.f / s2, nchw);
+                                                           m1, m2, 1.f / s0, 1.f / s1, 1.f / s2, nchw, pad_norm);
   } else {
     throw std::runtime_error("augment: output dtype must be f32 or bf16");
   }

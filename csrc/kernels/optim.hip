@@ -32,6 +32,16 @@ __device__ __forceinline__ void skip_zero(float* __restrict__ g, long n, int zer
 }
 __device__ __forceinline__ float gscale(const float* p) { return p ? *p : 1.f; }
 
+// Step counters of MADGRAD / MirrorMADGRAD / Adam count APPLIED steps only (torch's
+// GradScaler skips optimizer.step() on an overflow, so the reference never advances them on
+// a skipped step).  The host passes the number of step() calls k; the device counter
+// kskip holds the number of skipped ones: a skipped step bumps it (one thread; no other
+// block reads it in a skipped step), an applied step uses k - kskip.
+__device__ __forceinline__ void count_skip(int* kskip) {
+  if (kskip && blockIdx.x == 0 && threadIdx.x == 0) *kskip += 1;
+}
+__device__ __forceinline__ long applied_k(long k, const int* kskip) { return kskip ? k - (long)*kskip : k; }
+
 __device__ __forceinline__ void store_shadow(bf16* sh, long i, float4 v) {
   uint2 u;
   u.x = pack_bf16x2(v.x, v.y);
@@ -128,13 +138,13 @@ __global__ __launch_bounds__(kOB) void sgd_kernel(float* __restrict__ p, float* 
 __global__ __launch_bounds__(kOB) void madgrad_kernel(float* __restrict__ p, float* __restrict__ g, float* __restrict__ gss,
                                                       float* __restrict__ s, float* __restrict__ x0,
                                                       bf16* __restrict__ shadow, long n4, float lr, float momentum,
-                                                      float wd, float eps, int decouple, long k,
+                                                      float wd, float eps, int decouple, long k, int* __restrict__ kskip,
                                                       const float* __restrict__ gsc, const int* __restrict__ found_inf,
                                                       int zero_grad) {
-  if (skip_step(found_inf)) { skip_zero(g, n4 * 4, zero_grad); return; }
+  if (skip_step(found_inf)) { count_skip(kskip); skip_zero(g, n4 * 4, zero_grad); return; }
   const float c = gscale(gsc);
   const float lr_e = lr + eps;
-  const float lamb = lr_e * sqrtf((float)(k + 1));
+  const float lamb = lr_e * sqrtf((float)(applied_k(k, kskip) + 1));
   const float ck = 1.f - momentum;
   for (long i = (long)blockIdx.x * kOB + threadIdx.x; i < n4 * 4; i += (long)gridDim.x * kOB) {
     float pv = p[i], gv = g[i] * c;
@@ -163,12 +173,12 @@ __global__ __launch_bounds__(kOB) void mirror_madgrad_kernel(float* __restrict__
                                                              float* __restrict__ gss, float* __restrict__ z,
                                                              bf16* __restrict__ shadow, long n, float lr, float momentum,
                                                              float wd, float eps, int decouple, long k,
-                                                             const float* __restrict__ gsc,
+                                                             int* __restrict__ kskip, const float* __restrict__ gsc,
                                                              const int* __restrict__ found_inf, int zero_grad) {
-  if (skip_step(found_inf)) { skip_zero(g, n, zero_grad); return; }
+  if (skip_step(found_inf)) { count_skip(kskip); skip_zero(g, n, zero_grad); return; }
   const float c = gscale(gsc);
   const float lr_e = lr + eps;
-  const float lamb = lr_e * sqrtf((float)(k + 1));
+  const float lamb = lr_e * sqrtf((float)(applied_k(k, kskip) + 1));
   const float ck = 1.f - momentum;
   for (long i = (long)blockIdx.x * kOB + threadIdx.x; i < n; i += (long)gridDim.x * kOB) {
     float pv = p[i], gv = g[i] * c;
@@ -191,11 +201,12 @@ __global__ __launch_bounds__(kOB) void mirror_madgrad_kernel(float* __restrict__
 __global__ __launch_bounds__(kOB) void adam_kernel(float* __restrict__ p, float* __restrict__ g, float* __restrict__ m,
                                                    float* __restrict__ v, bf16* __restrict__ shadow, long n, float lr,
                                                    float b1, float b2, float eps, float wd, int adamw, long step,
-                                                   const float* __restrict__ gsc, const int* __restrict__ found_inf,
-                                                   int zero_grad) {
-  if (skip_step(found_inf)) { skip_zero(g, n, zero_grad); return; }
+                                                   int* __restrict__ kskip, const float* __restrict__ gsc,
+                                                   const int* __restrict__ found_inf, int zero_grad) {
+  if (skip_step(found_inf)) { count_skip(kskip); skip_zero(g, n, zero_grad); return; }
   const float c = gscale(gsc);
-  const float bc1 = 1.f - powf(b1, (float)step), bc2 = 1.f - powf(b2, (float)step);
+  const float st = (float)applied_k(step, kskip);
+  const float bc1 = 1.f - powf(b1, st), bc2 = 1.f - powf(b2, st);
   for (long i = (long)blockIdx.x * kOB + threadIdx.x; i < n; i += (long)gridDim.x * kOB) {
     float pv = p[i], gv = g[i] * c;
     if (wd != 0.f) {
@@ -244,33 +255,33 @@ void sgd_step(uint64_t p, uint64_t g, uint64_t buf, uint64_t shadow, long n, flo
 }
 
 void madgrad_step(uint64_t p, uint64_t g, uint64_t gss, uint64_t s, uint64_t x0, uint64_t shadow, long n, float lr,
-                  float momentum, float wd, float eps, int decouple, long k, uint64_t gsc, uint64_t found_inf,
-                  int zero_grad, uint64_t stream) {
+                  float momentum, float wd, float eps, int decouple, long k, uint64_t kskip, uint64_t gsc,
+                  uint64_t found_inf, int zero_grad, uint64_t stream) {
   FDT_CHECK(n % 4 == 0, "flat buffer must be padded to a multiple of 4");
   FDT_CHECK(momentum == 0.f || x0 != 0, "x0 buffer required with momentum");
   madgrad_kernel<<<opt_grid(n / 4), kOB, 0, as_stream(stream)>>>(P<float>(p), P<float>(g), P<float>(gss), P<float>(s),
                                                                   P<float>(x0), P<bf16>(shadow), n / 4, lr, momentum, wd,
-                                                                  eps, decouple, k, P<const float>(gsc),
+                                                                  eps, decouple, k, P<int>(kskip), P<const float>(gsc),
                                                                   P<const int>(found_inf), zero_grad);
   FDT_LAUNCH_CHECK();
 }
 
 void mirror_madgrad_step(uint64_t p, uint64_t g, uint64_t gss, uint64_t z, uint64_t shadow, long n, float lr,
-                         float momentum, float wd, float eps, int decouple, long k, uint64_t gsc, uint64_t found_inf,
-                         int zero_grad, uint64_t stream) {
+                         float momentum, float wd, float eps, int decouple, long k, uint64_t kskip, uint64_t gsc,
+                         uint64_t found_inf, int zero_grad, uint64_t stream) {
   mirror_madgrad_kernel<<<opt_grid(n), kOB, 0, as_stream(stream)>>>(P<float>(p), P<float>(g), P<float>(gss), P<float>(z),
                                                                      P<bf16>(shadow), n, lr, momentum, wd, eps, decouple,
-                                                                     k, P<const float>(gsc), P<const int>(found_inf),
-                                                                     zero_grad);
+                                                                     k, P<int>(kskip), P<const float>(gsc),
+                                                                     P<const int>(found_inf), zero_grad);
   FDT_LAUNCH_CHECK();
 }
 
 void adam_step(uint64_t p, uint64_t g, uint64_t m, uint64_t v, uint64_t shadow, long n, float lr, float b1, float b2,
-               float eps, float wd, int adamw, long step, uint64_t gsc, uint64_t found_inf, int zero_grad,
-               uint64_t stream) {
+               float eps, float wd, int adamw, long step, uint64_t kskip, uint64_t gsc, uint64_t found_inf,
+               int zero_grad, uint64_t stream) {
   adam_kernel<<<opt_grid(n), kOB, 0, as_stream(stream)>>>(P<float>(p), P<float>(g), P<float>(m), P<float>(v),
                                                            P<bf16>(shadow), n, lr, b1, b2, eps, wd, adamw, step,
-                                                           P<const float>(gsc), P<const int>(found_inf), zero_grad);
+                                                           P<int>(kskip), P<const float>(gsc), P<const int>(found_inf), zero_grad);
   FDT_LAUNCH_CHECK();
 }
 

@@ -137,11 +137,37 @@ def synthetic_cifar(n=50000, num_classes=10, seed=0, hw=32):
 
 
 # ------------------------------------------------------------------ CPU transforms
+TRANSFORMS = ("crop", "flip", "normalize")
+
+
+def augment_order(seed: int | None = None, faithful: bool = False):
+    """Order of the train transforms.  The reference draws a random permutation of
+    (RandomCrop, RandomHorizontalFlip, Normalize) once per run with
+    ``np.random.choice(range(3), 3, replace=False)`` (resnet50_test.py:304-309, survey Q13);
+    ``faithful`` reproduces that draw from a seeded generator, the default is the fixed
+    torchvision order crop -> flip -> normalise."""
+    if not faithful:
+        return TRANSFORMS
+    perm = np.random.RandomState(seed).choice(range(3), 3, replace=False)
+    return tuple(TRANSFORMS[i] for i in perm)
+
+
+def pad_normalized(order) -> bool:
+    """True when normalisation precedes the zero-padded crop (padding is then 0 in
+    normalised space); flip commutes with both in distribution (csrc/kernels/augment.hip)."""
+    return order.index("normalize") < order.index("crop")
+
+
 def augment_cpu(imgs_u8: torch.Tensor, gen: torch.Generator | None = None, pad=4, flip=True, train=True,
-                out_dtype=torch.float32, channels_last=False):
+                out_dtype=torch.float32, channels_last=False, order=TRANSFORMS):
     """Reference-semantics batch transform on CPU: uint8 NHWC -> normalised NCHW float."""
     x = imgs_u8.permute(0, 3, 1, 2).float() / 255.0
     B, C, H, W = x.shape
+    mean = torch.tensor(CIFAR_MEAN).view(1, 3, 1, 1)
+    std = torch.tensor(CIFAR_STD).view(1, 3, 1, 1)
+    norm_first = train and pad > 0 and pad_normalized(order)
+    if norm_first:
+        x = (x - mean) / std
     if train and pad > 0:
         xp = torch.nn.functional.pad(x, (pad, pad, pad, pad))
         dy = torch.randint(0, 2 * pad + 1, (B,), generator=gen)
@@ -153,9 +179,9 @@ def augment_cpu(imgs_u8: torch.Tensor, gen: torch.Generator | None = None, pad=4
     if train and flip:
         f = torch.rand(B, generator=gen) < 0.5
         x = torch.where(f.view(B, 1, 1, 1), x.flip(3), x)
-    mean = torch.tensor(CIFAR_MEAN).view(1, 3, 1, 1)
-    std = torch.tensor(CIFAR_STD).view(1, 3, 1, 1)
-    x = ((x - mean) / std).to(out_dtype)
+    if not norm_first:
+        x = (x - mean) / std
+    x = x.to(out_dtype)
     if channels_last:
         x = x.contiguous(memory_format=torch.channels_last)
     return x
@@ -170,7 +196,8 @@ class DeviceCIFARLoader:
     shared permutation (DistributedSampler semantics)."""
 
     def __init__(self, data_u8, targets, batch_size, device, train=True, rank=0, world_size=1, seed=0,
-                 drop_last=True, shuffle=True, out_dtype=torch.bfloat16, pad=4, flip=True, augment=True):
+                 drop_last=True, shuffle=True, out_dtype=torch.bfloat16, pad=4, flip=True, augment=True,
+                 order=TRANSFORMS):
         self.device = torch.device(device)
         self.train = train
         self.bs = batch_size
@@ -180,11 +207,13 @@ class DeviceCIFARLoader:
         self.shuffle = shuffle
         self.out_dtype = out_dtype
         self.pad, self.flip, self.augment = pad, flip, augment
+        self.order = tuple(order)
         self.n = len(targets)
         self.images = torch.as_tensor(np.ascontiguousarray(data_u8)).to(self.device)
         self.labels = torch.as_tensor(np.asarray(targets)).to(torch.int32).to(self.device)
         self.epoch = 0
-        self.rng = torch.tensor([seed, 0], dtype=torch.int64, device=self.device)
+        # per-rank stream of crop / flip draws (the kernel hashes (seed, step, sample))
+        self.rng = torch.tensor([seed + 7919 * rank, 0], dtype=torch.int64, device=self.device)
         self._gpu = self.device.type == "cuda" and _native.enabled()
         self._cpu_gen = torch.Generator().manual_seed(seed + 7919 * rank)
 
@@ -221,13 +250,13 @@ class DeviceCIFARLoader:
             train = self.train and self.augment
             nat.augment(self.images.data_ptr(), idx.data_ptr(), self.labels.data_ptr(), lab.data_ptr(),
                         out.data_ptr(), B, 32, 32, 3, cp, self.pad if train else 0, int(train and self.flip),
-                        self.rng.data_ptr(), *CIFAR_MEAN, *CIFAR_STD, 0,
+                        self.rng.data_ptr(), *CIFAR_MEAN, *CIFAR_STD, 0, int(pad_normalized(self.order)),
                         1 if self.out_dtype == torch.bfloat16 else 0, _native.stream_ptr())
             nat.rng_advance(self.rng.data_ptr(), _native.stream_ptr())
             return out[..., :3].permute(0, 3, 1, 2), lab.long()
         imgs = self.images[idx.long()].cpu()
         x = augment_cpu(imgs, self._cpu_gen, pad=self.pad, flip=self.flip, train=self.train and self.augment,
-                        out_dtype=torch.float32)
+                        out_dtype=torch.float32, order=self.order)
         return x.to(self.device), self.labels[idx.long()].long()
 
     def __iter__(self):

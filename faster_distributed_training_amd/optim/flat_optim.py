@@ -40,7 +40,12 @@ class FlatOptimizer(torch.optim.Optimizer):
         self.flat = flat
         super().__init__(flat.params, defaults)
         self.zero_grad_in_step = zero_grad_in_step
-        self.k = 0  # completed steps
+        self.k = 0  # step() calls
+        # steps skipped on the device (non-finite / fp16 overflow): the kernels bump it and
+        # use k - kskip as their step count, like torch's GradScaler which never calls
+        # optimizer.step() on a skipped step (so MADGRAD's lamb / Adam's bias correction
+        # only advance on applied steps) -- no host sync
+        self.kskip = torch.zeros(1, device=flat.device, dtype=torch.int32)
         self._native = flat.data.is_cuda and _native.enabled()
 
     @property
@@ -73,7 +78,8 @@ class FlatOptimizer(torch.optim.Optimizer):
         groups = [{k: v for k, v in g.items() if k != "params"} for g in self.param_groups]
         flat = {k: (v.detach().clone() if torch.is_tensor(v) else v)
                 for k, v in self.state.get("__flat__", {}).items()}
-        return {"flat_state": flat, "param_groups": groups, "k": self.k, "numel": self.flat.numel}
+        return {"flat_state": flat, "param_groups": groups, "k": self.k, "kskip": self.kskip.detach().clone().cpu(),
+                "numel": self.flat.numel}
 
     def load_state_dict(self, sd):
         if "flat_state" not in sd:  # a plain torch.optim state dict: hyper-parameters only
@@ -88,9 +94,17 @@ class FlatOptimizer(torch.optim.Optimizer):
         for k, v in sd["flat_state"].items():
             st[k] = v.to(self.flat.device) if torch.is_tensor(v) else v
         self.k = int(sd.get("k", 0))
+        if "kskip" in sd:
+            self.kskip.copy_(sd["kskip"].to(self.kskip.device))
+
+    @property
+    def applied_k(self) -> int:
+        """Applied steps so far (host view; syncs -- CPU path / tests only)."""
+        return self.k - int(self.kskip.item())
 
     def _cpu_common(self, grad_scale, found_inf):
         if found_inf is not None and bool(found_inf.item() != 0):
+            self.kskip += 1
             if self.zero_grad_in_step:  # a skipped step still clears the gradient
                 self.flat.grad.zero_()
             return None
@@ -155,15 +169,15 @@ class MADGRAD(FlatOptimizer):
             _native.native().madgrad_step(
                 self.flat.data.data_ptr(), self.flat.grad.data_ptr(), gss.data_ptr(), s.data_ptr(), _p(x0),
                 _p(self.flat.shadow), self.flat.numel, float(g["lr"]), float(g["momentum"]), float(g["weight_decay"]),
-                float(g["eps"]), int(g["decouple_decay"]), self.k, _p(grad_scale), _p(found_inf),
-                int(self.zero_grad_in_step), _sp())
+                float(g["eps"]), int(g["decouple_decay"]), self.k, self.kskip.data_ptr(), _p(grad_scale),
+                _p(found_inf), int(self.zero_grad_in_step), _sp())
             return
         gr = self._cpu_common(grad_scale, found_inf)
         if gr is None:
             return
         p = self.flat.data
         eps, lr = g["eps"], g["lr"] + g["eps"]
-        lamb = lr * math.sqrt(self.k + 1)
+        lamb = lr * math.sqrt(self.applied_k + 1)
         ck = 1 - g["momentum"]
         if g["weight_decay"] != 0 and not g["decouple_decay"]:
             gr = gr + g["weight_decay"] * p
@@ -197,15 +211,15 @@ class MirrorMADGRAD(FlatOptimizer):
             _native.native().mirror_madgrad_step(
                 self.flat.data.data_ptr(), self.flat.grad.data_ptr(), gss.data_ptr(), z.data_ptr(),
                 _p(self.flat.shadow), self.flat.numel, float(g["lr"]), float(g["momentum"]), float(g["weight_decay"]),
-                float(g["eps"]), int(g["decouple_decay"]), self.k, _p(grad_scale), _p(found_inf),
-                int(self.zero_grad_in_step), _sp())
+                float(g["eps"]), int(g["decouple_decay"]), self.k, self.kskip.data_ptr(), _p(grad_scale),
+                _p(found_inf), int(self.zero_grad_in_step), _sp())
             return
         gr = self._cpu_common(grad_scale, found_inf)
         if gr is None:
             return
         p = self.flat.data
         eps, lr = g["eps"], g["lr"] + g["eps"]
-        lamb = lr * math.sqrt(self.k + 1)
+        lamb = lr * math.sqrt(self.applied_k + 1)
         ck = 1 - g["momentum"]
         if g["weight_decay"] != 0 and not g["decouple_decay"]:
             gr = gr + g["weight_decay"] * p
@@ -228,16 +242,17 @@ class Adam(FlatOptimizer):
         m = self._state_buf("exp_avg")
         v = self._state_buf("exp_avg_sq")
         b1, b2 = g["betas"]
-        step = self.k + 1
         if self._native:
             _native.native().adam_step(
                 self.flat.data.data_ptr(), self.flat.grad.data_ptr(), m.data_ptr(), v.data_ptr(), _p(self.flat.shadow),
                 self.flat.numel, float(g["lr"]), float(b1), float(b2), float(g["eps"]), float(g["weight_decay"]),
-                int(g["adamw"]), step, _p(grad_scale), _p(found_inf), int(self.zero_grad_in_step), _sp())
+                int(g["adamw"]), self.k + 1, self.kskip.data_ptr(), _p(grad_scale), _p(found_inf),
+                int(self.zero_grad_in_step), _sp())
             return
         gr = self._cpu_common(grad_scale, found_inf)
         if gr is None:
             return
+        step = self.applied_k + 1
         p = self.flat.data
         if g["weight_decay"] != 0:
             if g["adamw"]:

@@ -158,18 +158,8 @@ class BucketReducer:
     @torch.no_grad()
     def sync_buffers(self, src: int = 0):
         """X3: broadcast BatchNorm running statistics (DDP's broadcast_buffers)."""
-        if self.module is None:
-            return
-        bufs = [b for b in self.module.buffers() if b.dtype.is_floating_point]
-        if not bufs:
-            return
-        flat = torch.cat([b.reshape(-1) for b in bufs])
-        dist.broadcast(flat, src, group=self.pg)
-        off = 0
-        for b in bufs:
-            n = b.numel()
-            b.copy_(flat[off:off + n].view_as(b))
-            off += n
+        from .dist import broadcast_buffers
+        broadcast_buffers(self.module, src, self.pg)
 
     def remove(self):
         for h in self._hooks:

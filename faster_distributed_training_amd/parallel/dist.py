@@ -102,6 +102,36 @@ def barrier():
             dist.barrier()
 
 
+@torch.no_grad()
+def broadcast_buffers(module, src: int = 0, group=None):
+    """Broadcast the floating-point buffers of ``module`` (BatchNorm running statistics)
+    from ``src`` in ONE collective (DDP ``broadcast_buffers``, X3)."""
+    if module is None or not is_dist():
+        return
+    bufs = [b for b in module.buffers() if b.dtype.is_floating_point]
+    if not bufs:
+        return
+    flat = torch.cat([b.reshape(-1) for b in bufs])
+    dist.broadcast(flat, src, group=group)
+    off = 0
+    for b in bufs:
+        n = b.numel()
+        b.copy_(flat[off:off + n].view_as(b))
+        off += n
+
+
+def broadcast_scalar(value: float, src: int = 0, device=None) -> float:
+    """``value`` as seen by rank ``src`` (collective decisions such as "save a new best
+    checkpoint" must be taken identically on every rank)."""
+    if not is_dist():
+        return float(value)
+    if device is None:
+        device = torch.device("cuda", torch.cuda.current_device()) if dist.get_backend() == "nccl" else "cpu"
+    t = torch.tensor([float(value)], dtype=torch.float64, device=device)
+    dist.broadcast(t, src)
+    return float(t.item())
+
+
 def all_reduce_metrics(*tensors: torch.Tensor, op=dist.ReduceOp.SUM):
     """Metric all-reduce (X7): one collective for all metric scalars (the reference
     issues one per scalar).  Tensors are reduced in place."""

@@ -8,6 +8,11 @@ GradScaler's inf skip, resnet50_test.py:541-548, 664-690).
   best accuracy, global step, and every RNG stream (python, numpy, torch CPU / device, the
   device data loader's counter RNG) so a resumed run continues the same random sequence.
   Loads use ``weights_only=True``; numpy/python RNG states are stored as tensors/ints.
+* per-rank state lives in ``*_last.rank{r}.pth`` next to the main file (every rank writes
+  its own): the RNG streams (seeded per rank, so restoring rank 0's on every rank would make
+  all ranks draw the same mixup / augmentation / dropout randomness) and, when the optimizer
+  state is sharded (FSDP / sharded NGD), that rank's optimizer shard.  A resume must use the
+  same world size (checked).
 * ``--auto_resume``: at start-up a trainer restores ``*_last.pth`` if present and continues
   with the next epoch -- combined with ``torchrun --max-restarts N`` (run_distributed.sh)
   a crashed or killed rank restarts the job from the last completed epoch.
@@ -77,17 +82,49 @@ def _set_rng_state(trainer, st):
         ld._cpu_gen.set_state(st["loader_cpu_gen"])
 
 
+def rank_path(path: str, rank: int) -> str:
+    root, ext = os.path.splitext(path)
+    return f"{root}.rank{rank}{ext}"
+
+
+def _sharded(trainer) -> bool:
+    return getattr(trainer, "fsdp", None) is not None or bool(getattr(trainer.optimizer, "sharded", False))
+
+
+def _optimizer_state(trainer):
+    st = {"optimizer": trainer.optimizer.state_dict()}
+    ngd = getattr(trainer.optimizer, "ngd_state_dict", None)
+    if ngd is not None:
+        st["ngd"] = ngd()
+    return st
+
+
+def _load_optimizer_state(trainer, ck):
+    trainer.optimizer.load_state_dict(ck["optimizer"])
+    if "ngd" in ck and hasattr(trainer.optimizer, "load_ngd_state_dict"):
+        trainer.optimizer.load_ngd_state_dict(ck["ngd"])
+
+
 def save_last(trainer, epoch: int):
-    """Full training state after ``epoch`` completed (rank 0 writes, all ranks barrier)."""
-    extra = {"optimizer": trainer.optimizer.state_dict(), "global_step": int(trainer.global_step),
-             "best_acc": float(trainer.best_acc), "rng": _rng_state(trainer), "last": True}
+    """Full training state after ``epoch`` completed: every rank writes its rank file, rank 0
+    the main file, then all ranks barrier."""
+    rank, world = int(getattr(trainer, "rank", 0)), int(getattr(trainer, "world", 1))
+    mine = {"rng": _rng_state(trainer), "rank": rank, "world": world}
+    sharded = _sharded(trainer)
+    if sharded:
+        mine.update(_optimizer_state(trainer))
+    path = rank_path(trainer.last_path, rank)
+    os.makedirs(os.path.dirname(os.path.abspath(path)) or ".", exist_ok=True)
+    torch.save(mine, path + ".tmp")
+    os.replace(path + ".tmp", path)
+    extra = {"global_step": int(trainer.global_step), "best_acc": float(trainer.best_acc), "world": world,
+             "sharded_optimizer": sharded, "last": True}
+    if not sharded:
+        extra.update(_optimizer_state(trainer))
     if getattr(trainer, "scheduler", None) is not None:
         extra["scheduler"] = trainer.scheduler.state_dict()
     if getattr(trainer, "scaler", None) is not None:
         extra["scaler"] = trainer.scaler.state_dict()
-    ngd = getattr(trainer.optimizer, "ngd_state_dict", None)
-    if ngd is not None:
-        extra["ngd"] = ngd()
     meta = getattr(trainer, "meta", None)
     if meta is not None:
         extra["meta"] = {k: v.detach().cpu() for k, v in meta.state_dict().items()}
@@ -102,12 +139,23 @@ def restore_last(trainer) -> bool:
     if not os.path.isfile(path):
         return False
     ck = ckpt.load_checkpoint(path)
+    rank, world = int(getattr(trainer, "rank", 0)), int(getattr(trainer, "world", 1))
+    if int(ck.get("world", world)) != world:
+        raise RuntimeError(f"{path} was written by {ck['world']} ranks; resume with the same world size "
+                           f"(this run has {world})")
+    rp = rank_path(path, rank)
+    mine = ckpt.load_checkpoint(rp) if os.path.isfile(rp) else None
+    if ck.get("sharded_optimizer", False) != _sharded(trainer):
+        raise RuntimeError(f"{path}: optimizer sharding differs from this run's (--fsdp / sharded NGD)")
     ckpt.load_model_state(trainer.model, ck["net"])
     if hasattr(trainer.flat, "refresh_shadow"):
         trainer.flat.refresh_shadow()
-    trainer.optimizer.load_state_dict(ck["optimizer"])
-    if "ngd" in ck and hasattr(trainer.optimizer, "load_ngd_state_dict"):
-        trainer.optimizer.load_ngd_state_dict(ck["ngd"])
+    if ck.get("sharded_optimizer", False):
+        if mine is None:
+            raise FileNotFoundError(f"missing per-rank optimizer shard {rp}")
+        _load_optimizer_state(trainer, mine)
+    else:
+        _load_optimizer_state(trainer, ck)
     if "scheduler" in ck and getattr(trainer, "scheduler", None) is not None:
         trainer.scheduler.load_state_dict(ck["scheduler"])
     if "scaler" in ck and getattr(trainer, "scaler", None) is not None:
@@ -117,6 +165,7 @@ def restore_last(trainer) -> bool:
     trainer.global_step = int(ck.get("global_step", 0))
     trainer.best_acc = max(float(trainer.best_acc), float(ck.get("best_acc", 0.0)))
     trainer.start_epoch = int(ck["epoch"]) + 1
-    if "rng" in ck:
-        _set_rng_state(trainer, ck["rng"])
+    rng = mine["rng"] if mine is not None else ck.get("rng")  # (older files: rank 0's only)
+    if rng is not None:
+        _set_rng_state(trainer, rng)
     return True

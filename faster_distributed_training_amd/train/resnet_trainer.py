@@ -19,7 +19,7 @@ import numpy as np
 import torch
 import torch.nn as nn
 
-from ..data.cifar import CLASSES, CIFAR10, DeviceCIFARLoader, synthetic_cifar
+from ..data.cifar import CLASSES, CIFAR10, DeviceCIFARLoader, augment_order, synthetic_cifar
 from ..models import resnet as resnet_models
 from ..ops.mixup import MetaMixup, mixup_criterion, mixup_criterion_meta, mixup_data
 from ..optim.flat_optim import MADGRAD, SGD, Adam, DeviceGradScaler, GradClipper, MirrorMADGRAD
@@ -201,8 +201,11 @@ class ResNetTrainer:
         if sub:
             tr = (tr[0][::sub], tr[1][::sub])
             te = (te[0][::sub], te[1][::sub])
+        # Q13: the reference permutes the train transforms once per run; --faithful draws that
+        # permutation from the run seed, the default is crop -> flip -> normalise
+        self.augment_order = augment_order(cfg.seed, faithful=cfg.faithful)
         self.train_loader = DeviceCIFARLoader(tr[0], tr[1], cfg.bs, self.device, train=True, rank=self.rank,
-                                              world_size=self.world, seed=cfg.seed)
+                                              world_size=self.world, seed=cfg.seed, order=self.augment_order)
         # eval: every rank evaluates the full test set like the reference (no sharding)
         self.test_loader = DeviceCIFARLoader(te[0], te[1], cfg.bs, self.device, train=False, shuffle=False,
                                              drop_last=False)
@@ -220,6 +223,11 @@ class ResNetTrainer:
         prof = self.profiler
         resilience.maybe_inject_fault(self.global_step, self.rank)
         prof.begin_step()
+        if cfg.faithful and self.world > 1:
+            # X3: reference DDP (broadcast_buffers=True) re-broadcasts rank 0's BatchNorm
+            # running statistics at every forward (resnet50_test.py:716); by default they
+            # are synchronised once per epoch and before every evaluation instead
+            self._sync_buffers()
         prof.mark("mixup")
         if self.meta is not None:
             x, ya, yb, lam = self.meta(x, y)
@@ -263,12 +271,16 @@ class ResNetTrainer:
         self.global_step += 1
         return loss
 
+    def _sync_buffers(self):
+        """Rank 0's BatchNorm running statistics to every rank (one collective)."""
+        if self.world > 1 and (self.fsdp is not None or (self.reducer is not None and self.reducer.broadcast_buffers)):
+            pdist.broadcast_buffers(self.model)
+
     def train_epoch(self, epoch):
         self.model.train()
         self.meter.reset()
         self.train_loader.set_epoch(epoch)  # Q10 fix
-        if self.reducer is not None and self.reducer.broadcast_buffers:
-            self.reducer.sync_buffers()
+        self._sync_buffers()
         if self.device.type == "cuda":
             torch.cuda.synchronize()
             torch.cuda.reset_peak_memory_stats()
@@ -297,6 +309,10 @@ class ResNetTrainer:
 
     @torch.no_grad()
     def test(self, epoch):
+        # every rank evaluates with rank 0's running statistics (reference DDP broadcasts
+        # buffers at every forward), so the accuracy -- and the collective "new best ->
+        # save" decision below -- is the same on every rank
+        self._sync_buffers()
         self.model.eval()
         correct = torch.zeros((), device=self.device)
         total = torch.zeros((), device=self.device)
@@ -309,6 +325,7 @@ class ResNetTrainer:
             correct += (out.argmax(1) == y).sum()
             total += y.numel()
         acc = 100.0 * float(correct) / max(float(total), 1.0)
+        acc = pdist.broadcast_scalar(acc)  # one decision for all ranks (save_checkpoint is collective)
         self.testing_acc.append(acc)
         print0(f"test epoch {epoch}: acc {acc:.2f}% loss {float(loss_sum) / max(float(total), 1):.4f}")
         if acc > self.best_acc:

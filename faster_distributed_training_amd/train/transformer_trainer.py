@@ -362,6 +362,7 @@ class TransformerTrainer:
             correct += (logits.argmax(1) == labels).sum()
             total += labels.numel()
         acc = 100.0 * float(correct) / max(float(total), 1.0)
+        acc = pdist.broadcast_scalar(acc)  # one decision for all ranks (save_checkpoint is collective)
         self.testing_acc.append(acc)
         print0(f"test epoch {epoch}: acc {acc:.2f}%")
         if acc > self.best_acc:

@@ -116,3 +116,56 @@ def _trainer_worker(rank, world, tmp):
 
 def test_resnet_trainer_ddp_two_ranks(tmp_path):
     run_world(_trainer_worker, world=2, args=(str(tmp_path),))
+
+
+def _eval_decision_worker(rank, world, tmp):
+    """the "new best -> save" decision is collective (save_checkpoint barriers).
+    Give each rank a different test set so local accuracies differ: every rank must still
+    take rank 0's decision (no hang, same best_acc everywhere)."""
+    from faster_distributed_training_amd.data.cifar import DeviceCIFARLoader, synthetic_cifar
+    from faster_distributed_training_amd.train.resnet_trainer import ResNetConfig, ResNetTrainer
+    os.chdir(tmp)
+    cfg = ResNetConfig(arch="resnet18", bs=8, synthetic=True, epoch=1, steps_per_epoch=1, eval=True, plot=False,
+                       distributed=True, optimizer="sgd", checkpoint_dir=os.path.join(tmp, "ck"),
+                       extra={"subset_stride": 100})
+    tr = ResNetTrainer(cfg)
+    data, tg = synthetic_cifar(16, seed=50 + rank)
+    tr.test_loader = DeviceCIFARLoader(data, tg, 8, tr.device, train=False, shuffle=False, drop_last=False)
+    tr.best_acc = -1.0
+    acc = tr.test(0)
+    accs = [None] * world
+    dist.all_gather_object(accs, (acc, tr.best_acc))
+    assert all(a == accs[0] for a in accs), accs
+    assert os.path.isfile(tr.ckpt_path)
+
+
+def test_eval_save_decision_is_collective(tmp_path):
+    run_world(_eval_decision_worker, world=2, args=(str(tmp_path),))
+
+
+def _resume_rank_state_worker(rank, world, tmp):
+    """per-rank RNG streams and (FSDP) per-rank optimizer shards survive
+    save_last / auto-resume; rank 0's are not broadcast over the others."""
+    from faster_distributed_training_amd.train import resilience
+    from faster_distributed_training_amd.train.resnet_trainer import ResNetConfig, ResNetTrainer
+    os.chdir(tmp)
+    base = dict(arch="resnet18", bs=4, synthetic=True, epoch=1, steps_per_epoch=2, eval=False, plot=False,
+                distributed=True, optimizer="madgrad", fsdp=True, checkpoint_dir=os.path.join(tmp, "ck"),
+                extra={"subset_stride": 100})
+    a = ResNetTrainer(ResNetConfig(save_last=True, **base)).fit()
+    rng_after = torch.get_rng_state()
+    opt_after = {k: v.clone() for k, v in a.optimizer.state_dict()["flat_state"].items() if torch.is_tensor(v)}
+    assert os.path.isfile(resilience.rank_path(a.last_path, rank))
+    torch.manual_seed(999)
+    b = ResNetTrainer(ResNetConfig(auto_resume=True, **base))
+    assert b.start_epoch == 1
+    assert torch.equal(torch.get_rng_state(), rng_after)  # this rank's own stream
+    opt_b = b.optimizer.state_dict()["flat_state"]
+    assert all(torch.equal(opt_b[k], v) for k, v in opt_after.items())
+    states = [None] * world
+    dist.all_gather_object(states, torch.get_rng_state())
+    assert not torch.equal(states[0], states[1])
+
+
+def test_auto_resume_restores_each_ranks_state(tmp_path):
+    run_world(_resume_rank_state_worker, world=2, args=(str(tmp_path),))

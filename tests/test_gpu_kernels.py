@@ -2,6 +2,7 @@
 import math
 
 import pytest
+import numpy as np
 import torch
 import torch.nn.functional as F
 
@@ -215,6 +216,26 @@ def test_augment_matches_cpu(cuda):
     # on the interior is hard to check exactly; check statistics + range instead
     assert xa.shape == (64, 3, 32, 32)
     assert torch.isfinite(xa).all()
+
+
+@pytest.mark.parametrize("order", [("crop", "flip", "normalize"), ("normalize", "crop", "flip")])
+def test_augment_padding_follows_transform_order(cuda, order):
+    """Faithful transform permutation (Q13): normalising before the padded crop pads with 0
+    in normalised space, otherwise with raw 0 (= -mean/std)."""
+    from faster_distributed_training_amd.data.cifar import CIFAR_MEAN, CIFAR_STD, DeviceCIFARLoader
+    data = np.full((256, 32, 32, 3), 128, dtype=np.uint8)
+    tg = np.zeros(256, dtype=np.int64)
+    ld = DeviceCIFARLoader(data, tg, 256, cuda, train=True, shuffle=False, out_dtype=torch.float32, order=order)
+    x, _ = next(iter(ld))
+    x = x.cpu()
+    for c in range(3):
+        inside = (128 / 255 - CIFAR_MEAN[c]) / CIFAR_STD[c]
+        pad = 0.0 if order[0] == "normalize" else -CIFAR_MEAN[c] / CIFAR_STD[c]
+        v = x[:, c]
+        is_in = (v - inside).abs() < 1e-5
+        is_pad = (v - pad).abs() < 1e-5
+        assert bool((is_in | is_pad).all())
+        assert 0 < int(is_pad.sum()) < v.numel() // 4  # some crops reach into the padding
 
 
 @pytest.mark.parametrize("n,G", [(2, 5), (5, 3), (32, 4), (64, 2), (80, 8), (1, 2), (127, 1)])

@@ -132,3 +132,44 @@ def test_checkpoint_loads_into_flat_model(tmp_path):
     p0 = next(m.parameters())
     assert p0.data_ptr() == flat.data[flat.slot_of(p0).offset:].data_ptr()
     assert torch.equal(p0, next(src.parameters()))
+
+
+def test_faithful_augment_order_and_padding():
+    """Q13: --faithful draws the transform permutation once from the run seed; only the
+    position of Normalize relative to the padded crop is observable (padding value)."""
+    from faster_distributed_training_amd.data import cifar as C
+    assert C.augment_order(1, faithful=False) == ("crop", "flip", "normalize")
+    orders = {C.augment_order(s, faithful=True) for s in range(40)}
+    assert len(orders) == 6 and C.augment_order(5, True) == C.augment_order(5, True)
+    imgs = torch.full((16, 32, 32, 3), 128, dtype=torch.uint8)
+    for order in (("crop", "flip", "normalize"), ("normalize", "flip", "crop")):
+        x = C.augment_cpu(imgs, torch.Generator().manual_seed(0), train=True, order=order)
+        pad = 0.0 if C.pad_normalized(order) else -C.CIFAR_MEAN[0] / C.CIFAR_STD[0]
+        inside = (128 / 255 - C.CIFAR_MEAN[0]) / C.CIFAR_STD[0]
+        v = x[:, 0]
+        assert bool((((v - pad).abs() < 1e-5) | ((v - inside).abs() < 1e-5)).all())
+
+
+def test_skipped_steps_do_not_advance_madgrad_counter():
+    """a step skipped on non-finite gradients must not advance MADGRAD's k
+    (torch GradScaler never calls optimizer.step() on it)."""
+    from faster_distributed_training_amd.optim.flat_optim import MADGRAD
+    from faster_distributed_training_amd.utils.flat import FlatParams
+
+    def run(skip):
+        torch.manual_seed(0)
+        m = torch.nn.Linear(4, 3)
+        flat = FlatParams(m)
+        opt = MADGRAD(flat, lr=0.1)
+        for i in range(3):
+            torch.manual_seed(10 + i)
+            m(torch.randn(5, 4)).square().sum().backward()
+            opt.step(found_inf=torch.zeros(1, dtype=torch.int32))
+            if skip and i == 0:
+                flat.grad.fill_(float("inf"))
+                opt.step(found_inf=torch.ones(1, dtype=torch.int32))
+        return flat.data.clone(), opt
+    a, _ = run(False)
+    b, ob = run(True)
+    assert ob.k == 4 and ob.applied_k == 3
+    assert torch.equal(a, b)
