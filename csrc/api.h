@@ -78,11 +78,11 @@ void augment(uint64_t src, uint64_t idx, uint64_t labels_src, uint64_t labels_ou
 void rng_advance(uint64_t rng, uint64_t stream);
 // conv_igemm.hip
 void conv_igemm(uint64_t x, uint64_t x2, uint64_t ps, uint64_t pt, uint64_t pg, uint64_t w, uint64_t out, uint64_t part,
-                uint64_t ex, uint64_t es, uint64_t et, long Nb, int Hi, int Wi, int Cx, int Ho, int Wo, int S,
-                const std::vector<int>& dh, const std::vector<int>& dw, const std::vector<int>& wt, int Cout, int ldw,
-                int Hout, int Wout, int OS, int oy, int ox, int pro, int pro_act, float pro_alpha, int epi, int epi_act,
-                float epi_alpha, int BM, int BN, int BK, int nsplit, uint64_t slab, uint64_t cnt,
-                const std::vector<uint64_t>& fin_p, const std::vector<double>& fin_s, uint64_t stream);
+                uint64_t ex, uint64_t es, uint64_t et, uint64_t jmask, uint64_t jyb, uint64_t jout, long Nb, int Hi,
+                int Wi, int Cx, int Ho, int Wo, int S, const std::vector<int>& dh, const std::vector<int>& dw,
+                const std::vector<int>& wt, int Cout, int ldw, int Hout, int Wout, int OS, int oy, int ox, int pro,
+                int pro_act, float pro_alpha, int epi, int epi_act, float epi_alpha, int BM, int BN, int BK, int nsplit,
+                uint64_t slab, uint64_t cnt, uint64_t stream);
 int conv_num_row_blocks(long M, int BM);
 std::vector<long> conv_splitk_workspace(long M, int Cout, int BM, int BN, int nsplit);
 // conv_wgrad.hip

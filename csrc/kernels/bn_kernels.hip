@@ -687,17 +687,10 @@ void residual_act_bwd(uint64_t g, uint64_t out, uint64_t mask, uint64_t ya, uint
   FDT_CHECK(out != 0 || mask != 0, "residual_act_bwd needs the output or its mask");
   ChanGeom gg = chan_geom(C);
   // ~1024 blocks: more waves in flight for this 4-5 stream kernel than the stats default
-  static const long blocks = [] {
-    const char* s = std::getenv("FDT_RAB_BLOCKS");  // A/B knob for the block-count target
-    return s ? std::max(64L, std::atol(s)) : 1024L;
-  }();
-  static const long min_iters = [] {
-    const char* s = std::getenv("FDT_RAB_MINIT");  // min rows each thread walks (atomics amortisation)
-    return s ? std::max(1L, std::atol(s)) : 1L;
-  }();
-  long target = blocks / (gg.gy > 0 ? gg.gy : 1);
+  constexpr long kBlocks = 1024;
+  long target = kBlocks / (gg.gy > 0 ? gg.gy : 1);
   long r = (M + target - 1) / target;
-  if (r < gg.RPP * min_iters) r = gg.RPP * min_iters;
+  if (r < gg.RPP) r = gg.RPP;
   r = (r + gg.RPP - 1) / gg.RPP * gg.RPP;
   dim3 grid((unsigned)((M + r - 1) / r), gg.gy);
   DISPATCH_T(dt, {

@@ -1,5 +1,5 @@
 // Per-channel batch-norm finalisation math shared by the standalone finalize kernel
-// (bn_kernels.hip) and the conv epilogue's fused last-arriver finalize (conv_igemm.hip),
+// (bn_kernels.hip) and any kernel that finalises statistics in its own epilogue,
 // so both produce bit-identical (s, t) for the same fp64 sums.
 //
 // mode 0: FusedConvBN (unbiased var, s = 1/(sqrt(var)+eps), no affine)   resnet.py:75-100

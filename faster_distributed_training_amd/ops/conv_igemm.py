@@ -23,17 +23,8 @@ import torch
 
 from . import _native
 
-PRO_NONE, PRO_AFFINE_ACT, PRO_FOLD, PRO_NONE_GLDS = 0, 1, 2, 3
-# FDT_GLDS=1: prologue-free convolutions staged by LDS-DMA (buffer_load ... lds, one tile in
-# flight) instead of the register pipeline (two tiles in flight + ds_write).  Measured on
-# MI355X, ResNet-50 bs 1024: per-shape fwd/dgrad 3-10 % slower, step 28.9 -> 31.8 ms, so
-# the register pipeline stays the default; numerics are covered by the same GPU tests.
-GLDS = os.environ.get("FDT_GLDS", "0") == "1"
-
-
-def _launch_pro(pro):
-    return PRO_NONE_GLDS if (GLDS and pro == PRO_NONE) else pro
-EPI_STATS, EPI_ACTBWD, EPI_STORE, EPI_ADD = 0, 1, 2, 3
+PRO_NONE, PRO_AFFINE_ACT, PRO_FOLD = 0, 1, 2
+EPI_STATS, EPI_ACTBWD, EPI_STORE, EPI_ADD, EPI_JOINBWD = 0, 1, 2, 3, 4
 
 
 def _sp():
@@ -197,12 +188,10 @@ def stat_slots(nq: int, C: int, device) -> torch.Tensor:
     return torch.zeros(STAT_SLOTS, nq, C, device=device, dtype=torch.float32)
 
 
-def conv_fwd(x, wf, shp: ConvShape, s=None, t=None, act=0, alpha=1.0, tile=None, part=None, nsplit=None, fin=None):
+def conv_fwd(x, wf, shp: ConvShape, s=None, t=None, act=0, alpha=1.0, tile=None, part=None, nsplit=None):
     """y = conv(act(x*s+t)) (or conv(x) when s is None and act == 0); returns
     (y [N,Ho,Wo,Cout] bf16, part [STAT_SLOTS,2,Cout] fp32 slots whose row sum is
-    (sum y, sum y^2)).  ``part``: a zeroed slot buffer to accumulate into.
-    ``fin`` = (pointer list, scalar list): the epilogue's last arriver per channel tile also
-    finalises the batch-norm statistics (bn_math.h) and re-zeroes ``part``."""
+    (sum y, sum y^2)).  ``part``: a zeroed slot buffer to accumulate into."""
     nat = _native.native()
     N, H, W, C = x.shape
     assert C == shp.cxp and x.dtype == torch.bfloat16 and x.is_contiguous()
@@ -224,21 +213,25 @@ def conv_fwd(x, wf, shp: ConvShape, s=None, t=None, act=0, alpha=1.0, tile=None,
     if pro == PRO_AFFINE_ACT and s is None:
         s = torch.ones(C, device=x.device, dtype=torch.float32)
         t = torch.zeros(C, device=x.device, dtype=torch.float32)
-    nat.conv_igemm(x.data_ptr(), 0, _p(s), _p(t), 0, wf.data_ptr(), y.data_ptr(), part.data_ptr(), 0, 0, 0,
+    nat.conv_igemm(x.data_ptr(), 0, _p(s), _p(t), 0, wf.data_ptr(), y.data_ptr(), part.data_ptr(), 0, 0, 0, 0, 0, 0,
                    N, H, W, C, Ho, Wo, shp.stride, list(dh), list(dw), list(wt), shp.cout, shp.ntaps * shp.cxp,
-                   Ho, Wo, 1, 0, 0, _launch_pro(pro), int(act), float(alpha), EPI_STATS, 0, 1.0, bm, bn, bk, ns, slab_p, cnt_p,
-                   fin[0] if fin else [], fin[1] if fin else [], _sp())
+                   Ho, Wo, 1, 0, 0, pro, int(act), float(alpha), EPI_STATS, 0, 1.0, bm, bn, bk, ns, slab_p, cnt_p, _sp())
     return y, part
 
 
 def conv_dgrad(g, y, al, be, wd, shp: ConvShape, x_shape, epi=EPI_STORE, out=None, ex=None, es=None, et=None,
-               act=0, alpha=1.0, tile=None, part=None, nsplit=None, gs=None):
+               act=0, alpha=1.0, tile=None, part=None, nsplit=None, gs=None, jmask=None, jyb=None, jout=None):
     """Data gradient of y = conv(a): dA = conv^T(g*gs + al + be*y)  (gs None: 1).
 
     epi: EPI_STORE -> write dA; EPI_ADD -> out += dA; EPI_ACTBWD -> through the lazy
     input a = act(ex*es + et): out = dA*act'(.)*es, returns statistics slots
     [STAT_SLOTS, 2, Cin] whose row sum is (sum g_pre*ex, sum g_pre) (``part``: a zeroed
-    slot buffer to accumulate into; every parity class of a strided conv adds to it)."""
+    slot buffer to accumulate into; every parity class of a strided conv adds to it);
+    EPI_JOINBWD -> out (the gradient of a residual block's output, this dgrad completes it)
+    becomes g_pre = (out + dA) * act'(join) with act' from ``jmask`` (ReLU bit mask) or
+    ``jout`` (the join output, CELU), and ``part`` [STAT_SLOTS, 3, Cin] receives
+    (sum g_pre*ex, sum g_pre, sum g_pre*jyb) -- ex / jyb = the block's residual / shortcut
+    branch outputs (jyb None: identity shortcut)."""
     nat = _native.native()
     N, Hy, Wy, Cy = g.shape
     assert Cy == shp.cout and g.is_contiguous() and (y is None or y.is_contiguous())
@@ -248,10 +241,12 @@ def conv_dgrad(g, y, al, be, wd, shp: ConvShape, x_shape, epi=EPI_STORE, out=Non
         out = torch.empty(N, Hx, Wx, shp.cin, device=g.device, dtype=torch.bfloat16)
     if epi == EPI_ACTBWD and part is None:
         part = stat_slots(2, shp.cin, g.device)
+    if epi == EPI_JOINBWD:
+        assert shp.stride == 1 and ex is not None and part is not None and (jmask is not None or jout is not None)
     ent = None
     if tile is None:
         pro = PRO_FOLD if al is not None else PRO_NONE
-        e = EPI_STORE if epi == EPI_ADD else epi
+        e = EPI_STORE if epi in (EPI_ADD, EPI_JOINBWD) else epi
         ent = tuned(f"dgrad{pro}{e}", N, Hx, shp) or tuned("dgrad", N, Hx, shp)
         tile = tuple(ent["tile"]) if ent else None
     if nsplit is not None:
@@ -268,12 +263,11 @@ def conv_dgrad(g, y, al, be, wd, shp: ConvShape, x_shape, epi=EPI_STORE, out=Non
         pro = PRO_FOLD if al is not None else PRO_NONE  # al None: g is already folded
         assert gs is None or pro == PRO_FOLD, "gs needs the fold prologue (al/be)"
         nat.conv_igemm(g.data_ptr(), _p(y) if pro == PRO_FOLD else 0, _p(al), _p(be), _p(gs), wd.data_ptr(),
-                       out.data_ptr(),
-                       _p(part) if epi == EPI_ACTBWD else 0, _p(ex), _p(es), _p(et), N, Hy, Wy, Cy, Ha, Wa, 1,
+                       out.data_ptr(), _p(part) if epi in (EPI_ACTBWD, EPI_JOINBWD) else 0, _p(ex), _p(es), _p(et),
+                       _p(jmask), _p(jyb), _p(jout), N, Hy, Wy, Cy, Ha, Wa, 1,
                        list(dh), list(dw), list(wt), shp.cin, shp.ntaps * shp.cout, Hx, Wx, shp.stride, py, px,
-                       _launch_pro(pro), 0, 1.0, epi, int(act),
-                       float(alpha), bm, bn, bk, ns, slab_p, cnt_p, [], [], _sp())
-    return out, (part if epi == EPI_ACTBWD else None)
+                       pro, 0, 1.0, epi, int(act), float(alpha), bm, bn, bk, ns, slab_p, cnt_p, _sp())
+    return out, (part if epi in (EPI_ACTBWD, EPI_JOINBWD) else None)
 
 
 def wgrad_split(M: int, tiles: int, want: int = 512, min_px: int = 1024) -> int:

@@ -67,48 +67,10 @@ def register_grad_ready_hook(param, fn, deferrable=False):
 # on every replay (communication keeps overlapping backward).
 _RECORDER = None
 
-# Optional (FDT_WGRAD_STREAM=1): weight gradients on a side stream, concurrent with the
-# data-gradient chain (the critical path).  Measured on MI355X (ResNet-50, graphs on):
-# bs 1024 29.2 -> 29.2 ms, bs 128 6.09 -> 6.53 ms -- co-running conv kernels slow each
-# other down (kernel-time sum +18 %) by as much as the overlap saves, so it is off.
-WGRAD_STREAM = os.environ.get("FDT_WGRAD_STREAM", "0") == "1"
-_SIDE_STREAMS: dict = {}
-_GS = None  # the _GradStreams of the backward in progress
-
-
-class _GradStreams:
-    """Fork/join bookkeeping of the weight-gradient side stream for one backward.  Tensors
-    the side stream reads are kept alive until the next join, so the caching allocator
-    cannot hand their memory to main-stream work that might run before the side reads."""
-
-    def __init__(self, main, side):
-        self.main, self.side, self.keep = main, side, []
-        self.pending = False
-
-    def fork(self, *tensors):
-        self.side.wait_stream(self.main)
-        self.keep.extend(t for t in tensors if t is not None)
-        self.pending = True
-
-    def join(self):
-        if self.pending:
-            self.main.wait_stream(self.side)
-            self.keep.clear()
-            self.pending = False
-
-
-def _side_stream(dev):
-    st = _SIDE_STREAMS.get(dev)
-    if st is None:
-        st = _SIDE_STREAMS[dev] = torch.cuda.Stream(device=dev)
-    return st
-
-
 def grad_ready(param):
     hooks = _GRAD_READY_HOOKS.get(id(param), ())
     if not hooks:
         return
-    gs = _GS
     rec = _RECORDER
     acts = []
     for fn, deferrable in hooks:
@@ -117,13 +79,9 @@ def grad_ready(param):
             if a is not None:
                 acts.append(a)
         else:
-            if gs is not None:
-                gs.join()  # a generic hook may read the gradient on the main stream
             fn(param)
     if not acts:
         return
-    if gs is not None:
-        gs.join()  # every gradient of the bucket is complete on the main stream
     if rec is not None:
         rec.cut(acts)
     else:
@@ -250,15 +208,6 @@ def slots(nq, C, dev):
     return ws[: ci.STAT_SLOTS * nq * C].view(ci.STAT_SLOTS, nq, C)
 
 
-# FDT_FUSED_FINALIZE=1: the conv epilogue's last arriver per channel tile finalises the BN
-# statistics instead of a separate finalize launch.  Measured on MI355X (ResNet-50): 29.2 ->
-# 39.8 ms/step at bs 1024, 6.09 -> 7.47 ms at bs 128 -- every workgroup must drain its
-# memory-side atomics and round-trip a ticket before it can retire, which costs far more
-# than the launch it saves.  Kept as an option (tested), off by default.
-FUSED_FINALIZE = os.environ.get("FDT_FUSED_FINALIZE", "0") == "1"
-_FIN_TICKETS: dict = {}
-
-
 def _bn_fin_params(u: Unit, training):
     bn = u.bn
     mode = u.mode(training)
@@ -272,31 +221,13 @@ def _bn_fin_params(u: Unit, training):
     return mode, 0.0, None, None, None, None, None
 
 
-def fused_fin(u: Unit, M, training, dev):
-    """Buffers (s, t, save_mean, save_aux) + the conv epilogue's fused-finalize arguments
-    (``conv_fwd(fin=...)``); None when the fusion is disabled."""
-    if not FUSED_FINALIZE:
-        return None, None
-    C = u.shp.cout
-    out = (_f32(C, dev), _f32(C, dev), _f32(C, dev), _f32(C, dev))
-    mode, mom, rm, rv, nbt, gamma, beta = _bn_fin_params(u, training)
-    tk = _FIN_TICKETS.get(dev)
-    if tk is None:
-        tk = _FIN_TICKETS[dev] = torch.zeros(4096, device=dev, dtype=torch.int32)
-    ptrs = [tk.data_ptr(), _p(gamma), _p(beta), _p(rm), _p(rv), _p(nbt)] + [b.data_ptr() for b in out]
-    return out, (ptrs, [float(mode), float(u.eps), float(mom), float(M)])
-
-
 def conv_bn_fwd(x, u: Unit, s, t, act, training, dev):
     """One unit's conv + batch statistics -> (y, (s, t, save_mean, save_aux), M)."""
     Ho, Wo = ci.out_hw(x.shape[1], x.shape[2], u.shp)
     M = x.shape[0] * Ho * Wo
-    bufs, fin = fused_fin(u, M, training, dev)
     y, part = ci.conv_fwd(x, u.wf, u.shp, s, t, act[0] if act else 0, act[1] if act else 1.0,
-                          part=slots(2, u.shp.cout, dev), fin=fin)
-    if bufs is None:
-        bufs = finalize_stats(part, u, M, training, dev)
-    return y, bufs, M
+                          part=slots(2, u.shp.cout, dev))
+    return y, finalize_stats(part, u, M, training, dev), M
 
 
 def finalize_stats(part, u: Unit, M, training, dev):
@@ -362,13 +293,7 @@ def bwd_finalize(part, nq, ua, sta, ub=None, stb=None, training=True, dev=None):
 def wgrad_into(u: Unit, g, y, al, be, x, xs, xt, act, gs=None):
     if u.w.grad is None:
         u.w.grad = torch.zeros_like(u.w)
-    st = _GS
-    if st is None:
-        ci.conv_wgrad(g, y, al, be, x, u.shp, u.w.grad, xs, xt, act[0], act[1], accumulate=True, gs=gs)
-    else:
-        st.fork(g, y, al, be, x, xs, xt, gs)
-        with torch.cuda.stream(st.side):
-            ci.conv_wgrad(g, y, al, be, x, u.shp, u.w.grad, xs, xt, act[0], act[1], accumulate=True, gs=gs)
+    ci.conv_wgrad(g, y, al, be, x, u.shp, u.w.grad, xs, xt, act[0], act[1], accumulate=True, gs=gs)
     grad_ready(u.w)
 
 
@@ -435,40 +360,55 @@ class ResNetBodyFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, g_out):
-        global _GS
-        if WGRAD_STREAM and g_out.is_cuda:
-            _GS = _GradStreams(torch.cuda.current_stream(), _side_stream(g_out.device))
-        try:
-            return ResNetBodyFn._backward(ctx, g_out)
-        finally:
-            if _GS is not None:
-                _GS.join()
-                _GS = None
-
-    @staticmethod
-    def _backward(ctx, g_out):
+        """Blocks in reverse order.  The gradient of a block's output arrives ALREADY through
+        that block's join backward (g_pre = g*act'(out), plus its 3 statistics rows in the
+        slot workspace): the next block's last dgrad -- the one that completes the gradient
+        of its input -- ran the join backward in its epilogue (EPI_JOINBWD).  Only the last
+        block (its gradient comes from the pooling) runs the standalone join kernel.
+        Within a block the shortcut dgrad goes first (a full-coverage store of the input
+        gradient; a strided shortcut writes its zero parity classes too) so the final writer
+        is always the stride-1 first unit."""
         nat = _native.native()
         plan, training = ctx.plan, ctx.training
         g = g_out.contiguous()
         dev = g.device
-        for b, (x_in, ys, sc, out, mask) in zip(reversed(plan.blocks), reversed(ctx.recs)):
+        recs = ctx.recs
+        nblk = len(plan.blocks)
+        joined = False  # g is already g_pre of the current block (stats in the slots)
+        for bi in range(nblk - 1, -1, -1):
+            b = plan.blocks[bi]
+            x_in, ys, sc, out, mask = recs[bi]
             y3, s3 = ys[-1][0], ys[-1][1]
             C = y3.shape[-1]
             M = _rows(y3)
             part = slots(3, C, dev)
-            # ONE gradient g_pre = g*act'(z) for both branches: each consumer folds in its own
-            # BN scale (gs = s3 / s_shortcut) in its prologue; for an identity block g_pre is
-            # also the x_in gradient the first unit's dgrad accumulates into
-            gpre = torch.empty_like(y3)
-            nat.residual_act_bwd(g.data_ptr(), 0 if mask is not None else out.data_ptr(), _p(mask), y3.data_ptr(),
-                                 _p(sc[0] if sc else None), gpre.data_ptr(), part.data_ptr(), M, C, b.join[0],
-                                 float(b.join[1]), 1, _sp())
+            if joined:
+                gpre = g
+            else:
+                # ONE gradient g_pre = g*act'(z) for both branches: each consumer folds in its
+                # own BN scale (gs = s3 / s_shortcut) in its prologue
+                gpre = torch.empty_like(y3)
+                nat.residual_act_bwd(g.data_ptr(), 0 if mask is not None else out.data_ptr(), _p(mask),
+                                     y3.data_ptr(), _p(sc[0] if sc else None), gpre.data_ptr(), part.data_ptr(), M, C,
+                                     b.join[0], float(b.join[1]), 1, _sp())
             ul = b.units[-1]
             (al, be), coef_sc = bwd_finalize(part, 3, ul, (ys[-1][3], ys[-1][4], ys[-1][5]),
                                              b.shortcut, (sc[3], sc[4], sc[5]) if sc else None, training, dev)
-            g_cur, gs_cur = gpre, s3
             assert sc is not None or len(b.units) > 1, "identity block needs >1 unit (g_pre aliasing)"
-            g_x = None if sc is not None else gpre
+            if sc is not None:
+                u = b.shortcut
+                als, bes = coef_sc
+                g_x, _ = ci.conv_dgrad(gpre, sc[0], als, bes, u.wd, u.shp, tuple(x_in.shape), epi=ci.EPI_STORE,
+                                       gs=sc[1])
+                wgrad_into(u, gpre, sc[0], als, bes, x_in, None, None, (ACT_NONE, 1.0), gs=sc[1])
+            else:
+                g_x = gpre  # identity: the x_in gradient accumulates onto g_pre in place
+            # the block whose output is x_in: its join backward runs in the epilogue of the
+            # dgrad that completes g_x (unit 0's, below) when that dgrad is dense (a strided
+            # unit 0 -- BasicBlock downsampling -- writes parity classes: standalone join)
+            prev = plan.blocks[bi - 1] if (bi > 0 and b.units[0].shp.stride == 1) else None
+            prec = recs[bi - 1] if bi > 0 else None
+            g_cur, gs_cur = gpre, s3
             # residual chain, last unit first; (al, be) = BN-backward correction of unit i
             for i in range(len(b.units) - 1, -1, -1):
                 u = b.units[i]
@@ -499,20 +439,18 @@ class ResNetBodyFn(torch.autograd.Function):
                                                training=training, dev=dev)
                     g_cur, gs_cur = g_prev, None
                 else:
-                    if g_x is None:
-                        g_x, _ = ci.conv_dgrad(g_cur, y, al, be, u.wd, u.shp, tuple(x_in.shape), epi=ci.EPI_STORE,
-                                               gs=gs_cur)
+                    if prev is not None:
+                        _, pys, psc, pout, pmask = prec
+                        ci.conv_dgrad(g_cur, y, al, be, u.wd, u.shp, tuple(x_in.shape), epi=ci.EPI_JOINBWD, out=g_x,
+                                      gs=gs_cur, ex=pys[-1][0], part=slots(3, x_in.shape[-1], dev), act=prev.join[0],
+                                      alpha=prev.join[1], jmask=pmask, jyb=psc[0] if psc else None,
+                                      jout=None if pmask is not None else pout)
                     else:
                         ci.conv_dgrad(g_cur, y, al, be, u.wd, u.shp, tuple(x_in.shape), epi=ci.EPI_ADD, out=g_x,
                                       gs=gs_cur)
                     wgrad_into(u, g_cur, y, al, be, x_in, None, None, (ACT_NONE, 1.0), gs=gs_cur)
-            if sc is not None:
-                u = b.shortcut
-                ysc = sc[0]
-                al, be = coef_sc
-                ci.conv_dgrad(gpre, ysc, al, be, u.wd, u.shp, tuple(x_in.shape), epi=ci.EPI_ADD, out=g_x, gs=sc[1])
-                wgrad_into(u, gpre, ysc, al, be, x_in, None, None, (ACT_NONE, 1.0), gs=sc[1])
             g = g_x
+            joined = prev is not None
         # stem: act backward + statistics -> wgrad on the input image
         x_img, y0, s0, t0, sm0, sa0 = ctx.stem_rec
         st = plan.stem

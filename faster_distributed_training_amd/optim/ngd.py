@@ -32,10 +32,6 @@ from .flat_optim import SGD
 
 EPSILON = 1.0e-10
 DELTA = 5.0e-4
-# FDT_NGD_GRAPHS=1: replay the NGD step as a captured HIP graph.  Measured on MI355X
-# (ResNet-50 bs 1024, NGD + meta-mixup): 47.0 -> 47.4 ms/step -- the step is bound by the
-# GPU time of its ~2,500 small kernels, not by host dispatch -- so it is off by default.
-GRAPHS = os.environ.get("FDT_NGD_GRAPHS", "0") == "1"
 
 
 def default_rank(dim: int, rank: int = -1) -> int:
@@ -446,57 +442,8 @@ class NGD(SGD):
                          self.flat.device), slots)
             for shape, slots in by_shape.items()]
 
-    # ------------------------------------------------------------ HIP graphs
-    # The NGD step is ~60 small tensor ops per (shape group, axis) -- thousands of launches
-    # whose host-side dispatch, not GPU work, bounds the step.  It is free of host syncs and
-    # its shapes are static, so after the eager first (initialisation) step it is captured
-    # into a HIP graph per configuration (update / non-update step of the reference's
-    # schedule, hyper-parameters, first-momentum flag) and replayed: one launch per step.
-    def _states(self):
-        return [st for sg, _ in (self.groups or []) for _, st in sg.axes]
-
-    def _graph_key(self, grad_scale):
-        sts = self._states()
-        if not sts or any(st.t == 0 or st.W is None for st in sts):
-            return None  # initialisation step(s) run eagerly
-        upd = {st._updating() for st in sts}
-        if len(upd) != 1:
-            return None
-        g = self.group
-        first = int(self.state.get("__flat__", {}).get("initialized", 0) == 0) if g["momentum"] != 0 else 0
-        return (upd.pop(), float(g["lr"]), float(g["momentum"]), float(g["dampening"]), float(g["weight_decay"]),
-                bool(g["nesterov"]), bool(g["ngd"]), first,
-                grad_scale.data_ptr() if grad_scale is not None else 0)
-
     @torch.no_grad()
     def _step(self, grad_scale, found_inf, d_override=None):
-        use_graph = (GRAPHS and found_inf is None and d_override is None and self.flat.data.is_cuda
-                     and self.group["ngd"] and self.groups is not None and _native_eigh(self.flat.data.device))
-        key = self._graph_key(grad_scale) if use_graph else None
-        if key is None:
-            return self._step_eager(grad_scale, found_inf, d_override)
-        graphs = self.__dict__.setdefault("_graphs", {})
-        ent = graphs.get(key)
-        if ent is None:  # first time for this configuration: eager (warms caches / tables)
-            graphs[key] = "seen"
-            return self._step_eager(grad_scale, None)
-        if ent == "seen":
-            if getattr(self, "_pool", None) is None:
-                self._pool = torch.cuda.graph_pool_handle()
-            graph = torch.cuda.CUDAGraph()
-            torch.cuda.synchronize()
-            with torch.cuda.graph(graph, pool=self._pool):
-                self._step_eager(grad_scale, None)  # advances every state's t once (host)
-            graph.replay()
-            graphs[key] = graph
-            return None
-        ent.replay()
-        for st in self._states():
-            st.t += 1
-        return None
-
-    @torch.no_grad()
-    def _step_eager(self, grad_scale, found_inf, d_override=None):
         g = self.group
         if found_inf is not None and bool(found_inf.item() != 0):
             if self.zero_grad_in_step:  # GradScaler skip (fp16 mode only); still clear the gradient

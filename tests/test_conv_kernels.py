@@ -226,51 +226,73 @@ def test_fold_gradient_scale(cuda, case):
         assert rel(outw, refw) < 5e-3, ns
 
 
-@pytest.mark.parametrize("case", [(4, 8, 64, 128, 1, 1, 0), (2, 16, 128, 128, 3, 2, 1), (2, 4, 512, 512, 3, 1, 1)])
-@pytest.mark.parametrize("mode", [0, 1])
-def test_conv_fused_finalize(cuda, case, mode):
-    """The conv epilogue's last-arriver batch-norm finalize (fin=...) equals the standalone
-    finalize kernel on the same slot sums, re-zeroes the slots and resets its tickets (mode 0:
-    FusedConvBN; mode 1: BatchNorm2d with running statistics); with and without split-K."""
+@pytest.mark.parametrize("case", [(4, 8, 64, 256, 1, 1, 0), (3, 5, 128, 64, 1, 1, 0), (2, 4, 512, 1024, 1, 1, 0)])
+@pytest.mark.parametrize("join", ["relu_mask", "relu_mask_shortcut", "celu_out"])
+@pytest.mark.parametrize("ns", [1, 3])
+def test_conv_dgrad_join_backward(cuda, case, join, ns):
+    """EPI_JOINBWD: the dgrad that completes a block-output gradient also runs that block's
+    residual-join backward: g_pre = (prev + dA) * act'(out) stored in place, slots
+    (sum g_pre*y_res, sum g_pre, sum g_pre*y_sc)."""
     from faster_distributed_training_amd.ops import _native
     nat = _native.native()
     N, H, Cin, Cout, k, stride, pad = case
-    torch.manual_seed(4)
+    torch.manual_seed(5)
     shp = ci.ConvShape(Cin, Cout, k, stride, pad)
-    x = padc(make((N, H, H, Cin), cuda), shp.cxp)
     w = torch.randn(Cout, Cin, k, k, device=cuda) / (Cin * k * k) ** 0.5
-    wf, _ = ci.alloc_packed(shp, cuda, dgrad=False)
-    ci.pack_weights([(w, wf, None, shp)])
-    Ho, Wo = ci.out_hw(H, H, shp)
-    M = N * Ho * Wo
-    tickets = torch.zeros(64, device=cuda, dtype=torch.int32)
-    gamma = torch.rand(Cout, device=cuda) + 0.5
-    beta = torch.randn(Cout, device=cuda)
-    for tile, ns in [(None, None), ((64, 64, 64), 3), ((128, 128, 64), 1)]:
-        if tile and Cout % tile[1]:
-            continue
-        rm_a, rv_a = torch.zeros(Cout, device=cuda), torch.ones(Cout, device=cuda)
-        rm_b, rv_b = rm_a.clone(), rv_a.clone()
-        nbt_a = torch.zeros(1, device=cuda, dtype=torch.int64)
-        nbt_b = nbt_a.clone()
-        # reference: plain conv + standalone finalize kernel
-        y, part = ci.conv_fwd(x, wf, shp, tile=tile, nsplit=ns)
-        ref = [torch.empty(Cout, device=cuda) for _ in range(4)]
-        g_b = (gamma, beta, rm_a, rv_a, nbt_a) if mode == 1 else (None,) * 5
-        nat.stats_finalize(part.data_ptr(), part.shape[0], Cout, float(M), mode, 1e-3, 0.1,
-                           *[0 if t is None else t.data_ptr() for t in g_b], *[r.data_ptr() for r in ref], 1,
-                           _native.stream_ptr())
-        # fused
-        outs = [torch.empty(Cout, device=cuda) for _ in range(4)]
-        g_f = (gamma, beta, rm_b, rv_b, nbt_b) if mode == 1 else (None,) * 5
-        ptrs = [tickets.data_ptr()] + [0 if t is None else t.data_ptr() for t in g_f] + [o.data_ptr() for o in outs]
-        part2 = ci.stat_slots(2, Cout, cuda)
-        y2, _ = ci.conv_fwd(x, wf, shp, tile=tile, nsplit=ns, part=part2, fin=(ptrs, [float(mode), 1e-3, 0.1, float(M)]))
-        torch.cuda.synchronize()
-        assert torch.equal(y, y2)
-        for a, b in zip(ref, outs):
-            assert rel(b, a) < 1e-5, (tile, ns)
-        assert torch.count_nonzero(part2).item() == 0, "slots not re-zeroed"
-        assert torch.count_nonzero(tickets).item() == 0, "tickets not reset"
-        if mode == 1:
-            assert rel(rm_b, rm_a) < 1e-5 and rel(rv_b, rv_a) < 1e-5 and nbt_b.item() == 1
+    wf, wd = ci.alloc_packed(shp, cuda)
+    ci.pack_weights([(w, wf, wd, shp)])
+    g = make((N, H, H, Cout), cuda)
+    y = make((N, H, H, Cout), cuda)
+    al = torch.randn(Cout, device=cuda) * 0.1
+    be = torch.randn(Cout, device=cuda) * 0.1
+    gt = (g.float() + al + be * y.float()).to(BF).float()
+    xs = (N, H, H, Cin)
+    dA = nhwc(torch.nn.grad.conv2d_input((N, Cin, H, H), w.to(BF).float(), nchw(gt), stride=1, padding=pad))
+    prev = make(xs, cuda)
+    ya = make(xs, cuda)
+    yb = make(xs, cuda) if join == "relu_mask_shortcut" else None
+    out_join = make(xs, cuda)
+    if join == "celu_out":
+        act, alpha = 2, 0.075
+        out_join = F.celu(out_join.float(), alpha).to(BF)
+        o = out_join.float()
+        dact = torch.where(o > 0, torch.ones_like(o), o / alpha + 1)
+        mask = None
+    else:
+        act, alpha = 1, 1.0
+        dact = (out_join.float() > 0).float()
+        mask = torch.empty(out_join.numel() // 8, device=cuda, dtype=torch.uint8)
+        # the forward join kernel's mask: residual_act_fwd with y_a = out, s = 1, t = 0, x = 0
+        one, zero = torch.ones(Cin, device=cuda), torch.zeros(Cin, device=cuda)
+        tmp = torch.empty_like(out_join)
+        nat.residual_act_fwd(out_join.data_ptr(), one.data_ptr(), zero.data_ptr(), 0, 0, 0,
+                             torch.zeros_like(out_join).data_ptr(), tmp.data_ptr(), mask.data_ptr(),
+                             N * H * H, Cin, 1, 1.0, 1, _native.stream_ptr())
+    gp = (prev.float() + dA) * dact
+    part = ci.stat_slots(3, Cin, cuda)
+    out = prev.clone()
+    ci.conv_dgrad(g, y, al, be, wd, shp, xs, epi=ci.EPI_JOINBWD, out=out, ex=ya, part=part, act=act, alpha=alpha,
+                  jmask=mask, jyb=yb, jout=None if mask is not None else out_join, nsplit=ns)
+    assert rel(out, gp) < 1e-2
+    ps = part.sum(0)
+    assert rel(ps[0], (gp * ya.float()).reshape(-1, Cin).sum(0)) < 1e-2
+    assert rel(ps[1], gp.reshape(-1, Cin).sum(0)) < 1e-2
+    if yb is not None:
+        assert rel(ps[2], (gp * yb.float()).reshape(-1, Cin).sum(0)) < 1e-2
+    else:
+        assert torch.count_nonzero(ps[2]).item() == 0
+
+
+def test_strided_dgrad_store_writes_every_parity_class(cuda):
+    """A 1x1 stride-2 dgrad with EPI_STORE must write zeros in the parity classes it has no
+    taps for (the engine's shortcut dgrad is the first writer of the block-input gradient)."""
+    shp = ci.ConvShape(64, 256, 1, 2, 0)
+    w = torch.randn(256, 64, 1, 1, device=cuda) / 8
+    wf, wd = ci.alloc_packed(shp, cuda)
+    ci.pack_weights([(w, wf, wd, shp)])
+    g = make((2, 4, 4, 256), cuda)
+    xs = (2, 8, 8, 64)
+    out = torch.full(xs, float("nan"), device=cuda, dtype=BF)
+    ci.conv_dgrad(g, None, None, None, wd, shp, xs, epi=ci.EPI_STORE, out=out)
+    ref = nhwc(torch.nn.grad.conv2d_input((2, 64, 8, 8), w.to(BF).float(), nchw(g), stride=2, padding=0))
+    assert torch.isfinite(out.float()).all() and rel(out, ref) < 1e-2
