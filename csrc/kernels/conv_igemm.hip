@@ -187,19 +187,6 @@ __global__ __launch_bounds__(256) void igemm_kernel(const ConvArgs a) {
   const __amdgpu_buffer_rsrc_t rw_d = __builtin_amdgcn_make_buffer_rsrc(
       (void*)a.w, (short)0, (int)(a.w_bytes), 0x00020000);
 
-  if constexpr (HASPRO) {
-    for (int i = tid; i < a.Cx; i += 256) {
-      pst[i] = a.ps[i];
-      pst[a.Cx + i] = a.pt[i];
-      if constexpr (PRO == kProFold) pst[2 * a.Cx + i] = a.pg ? a.pg[i] : 1.f;
-    }
-  }
-  if (tid < 12) {
-    const int dh = a.dh[tid], dw = a.dw[tid];
-    tapt[tid] = dh * a.Wi + dw;
-    tapw[tid] = (int)(uint8_t)a.dh[tid] | ((int)(uint8_t)a.dw[tid] << 8) | ((int)(uint8_t)a.wt[tid] << 16);
-  }
-
   // ---- per-thread activation rows (fixed across K tiles): pixel index of tap (0,0)
   const int cc = tid % CPR;  // this thread's 16-B chunk column inside a K tile
   int pixb[NXL], ohs[NXL], ows[NXL];
@@ -222,7 +209,6 @@ __global__ __launch_bounds__(256) void igemm_kernel(const ConvArgs a) {
       pixb[j] = (n * a.Hi + ohs[j]) * a.Wi + ows[j];
     }
   }
-  __syncthreads();
 
   // one register stage = the global loads of one K tile (staged to LDS after the MFMAs
   // of the previous tile).  Two stages alternate so that the loads of tile k+2 are in
@@ -361,13 +347,43 @@ __global__ __launch_bounds__(256) void igemm_kernel(const ConvArgs a) {
   const int nk = min(nkt - kb, a.kps);
 
   {
-  // prologue: tile 0 -> LDS buf 0; tile 1 pending in B; tile 2 in flight in A
+  // prologue: tile 0 -> LDS buf 0; tile 1 pending in B; tile 2 in flight in A.
+  // 1x1 convolutions address their operands without the LDS tap table, so their first two
+  // K tiles are requested BEFORE the LDS setup (prologue parameters, tap table) and its
+  // barrier: the workgroup pays one memory latency at start-up instead of two (these
+  // memory-bound layers run many short workgroups).
   Stage SA, SB;
+  if constexpr (PURE) {
+    if (nk > 0) {
+      load_tile(SA, kb, true);
+      __builtin_amdgcn_sched_barrier(0);  // issue order SA, SB, SA' pinned (exact vmcnt counting)
+      load_tile(SB, kb + 1, nk > 1);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+  if constexpr (HASPRO) {
+    for (int i = tid; i < a.Cx; i += 256) {
+      pst[i] = a.ps[i];
+      pst[a.Cx + i] = a.pt[i];
+      if constexpr (PRO == kProFold) pst[2 * a.Cx + i] = a.pg ? a.pg[i] : 1.f;
+    }
+  }
+  if (tid < 12) {
+    const int dh = a.dh[tid], dw = a.dw[tid];
+    tapt[tid] = dh * a.Wi + dw;
+    tapw[tid] = (int)(uint8_t)a.dh[tid] | ((int)(uint8_t)a.dw[tid] << 8) | ((int)(uint8_t)a.wt[tid] << 16);
+  }
+
+  __syncthreads();
+  if constexpr (!PURE) {
+    if (nk > 0) {
+      load_tile(SA, kb, true);
+      __builtin_amdgcn_sched_barrier(0);
+      load_tile(SB, kb + 1, nk > 1);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
   if (nk > 0) {
-    load_tile(SA, kb, true);
-    __builtin_amdgcn_sched_barrier(0);  // issue order SA, SB, SA' pinned (exact vmcnt counting)
-    load_tile(SB, kb + 1, nk > 1);
-    __builtin_amdgcn_sched_barrier(0);
     store_tile(SA, 0);
     load_tile(SA, kb + 2, nk > 2);
     __builtin_amdgcn_sched_barrier(0);

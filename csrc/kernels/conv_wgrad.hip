@@ -410,11 +410,13 @@ __device__ __forceinline__ void pack_block(const PackEntry& E, int b, bf16* img)
   }
   __syncthreads();
   // forward layout wf[co][t][ci] (Cxp-padded rows): ci fastest
-  for (int e = tid; e < nco * T * kPackT; e += 256) {
-    const int cl = e % kPackT, r = e / kPackT;  // r = col * T + t
-    if (cl < nci_v) {
-      const int col = r / T, t = r - col * T;
-      E.wf[((long)(co0 + col) * T + t) * E.Cxp + ci0 + cl] = img[r * kPackLd + cl];
+  if (E.wf != nullptr) {
+    for (int e = tid; e < nco * T * kPackT; e += 256) {
+      const int cl = e % kPackT, r = e / kPackT;  // r = col * T + t
+      if (cl < nci_v) {
+        const int col = r / T, t = r - col * T;
+        E.wf[((long)(co0 + col) * T + t) * E.Cxp + ci0 + cl] = img[r * kPackLd + cl];
+      }
     }
   }
   // dgrad layout wd[ci][t][co]: co fastest

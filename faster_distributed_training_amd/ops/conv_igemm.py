@@ -326,13 +326,14 @@ def conv_wgrad(g, y, al, be, x, shp: ConvShape, out, xs=None, xt=None, act=0, al
 
 
 def pack_weights(entries):
-    """entries: iterable of (w fp32 OIHW, wf bf16, wd bf16 or None, ConvShape); one launch."""
+    """entries: iterable of (w fp32 OIHW, wf bf16 or None, wd bf16 or None, ConvShape); one
+    launch (a None layout is skipped)."""
     nat = _native.native()
     src, wf, wd, co, ci, cx, nt = [], [], [], [], [], [], []
     for w, f, d, shp in entries:
         assert w.is_contiguous() and w.dtype == torch.float32
         src.append(w.data_ptr())
-        wf.append(f.data_ptr())
+        wf.append(_p(f))
         wd.append(_p(d))
         co.append(shp.cout)
         ci.append(shp.cin)

@@ -1,70 +1,102 @@
-"""Fully-sharded data parallel over the flat parameter buffer (survey P6, X5).
+"""Fully-sharded data parallel (ZeRO-3): parameters sharded at rest, gathered per wrap unit.
 
-The reference wraps the Transformer in torch-1.11 FSDP with CPU offload
-(``transformer_test.py:387-392``): one flat parameter (auto-wrap never triggers at
-29.3M params), all-gather of the full parameter for forward/backward, reduce-scatter of
-the gradient, and — because NGD then sees a flat 1-D CPU shard — NGD preconditions the
-wrong thing (survey Q17).
+Reference: ``transformer_test.py:387-392`` wraps the Transformer in torch-1.11 FSDP with
+``size_based_auto_wrap_policy`` and ``CPUOffload(offload_params=True)`` (survey P6, X5; at
+29.3M parameters the policy never fires, so the reference has ONE unit and NGD sees a flat
+1-D CPU shard -- survey Q17).  BASELINE.json config 5 asks for ResNet-50 FSDP full-shard.
 
-MI355X design (``FlatShardedDP``):
+MI355X design (``FullyShardedDP``):
 
-* the flat buffer is partitioned into ``world`` contiguous runs of WHOLE parameters
-  (balanced by element count); rank r owns run r: its gradients after reduction, its
-  optimizer state (MADGRAD/NGD/...), and its update;
-* after backward one ``reduce_scatter_tensor`` (RCCL) delivers each rank the averaged
-  gradient of its run (runs padded to equal length in a staging buffer so the
-  collective is a single equal-chunk call); after the optimizer step one
-  ``all_gather_into_tensor`` rebuilds the full parameters on every rank;
-* NGD sees whole, correctly shaped parameters (Q17 fixed);
-* gradient-norm clipping reduces the per-shard sum of squares across ranks (device
-  scalar all-reduce, no host sync);
-* with 288 GB of HBM per MI355X the full parameter copy stays resident between steps
-  (ResNet-50: 94 MB): the communication schedule is FSDP's (reduce-scatter +
-  all-gather = the same bytes as one all-reduce), optimizer state and gradient
-  ownership are sharded 1/world; ``offload_optimizer=True`` keeps the owned optimizer
-  state in pinned host memory (the reference's CPUOffload analogue).
+* **wrap units**: ResNet: stem, conv2_x .. conv5_x, fc; Transformer: the embeddings, every
+  attention / FFN sublayer, pooler + classifier (``default_units``); or a size-based policy
+  (``min_params``), like the reference's ``size_based_auto_wrap_policy``.  Parameters
+  outside every unit form a root unit that stays gathered.
+* **at rest** each rank keeps only its shard of every unit: the fp32 master copy, its
+  gradient and the optimizer state over it (``self.space``: a FlatParams-like object the
+  fused optimizers and the gradient clipper run on).  Full unit parameters exist only while
+  the unit is in use: the storage behind the parameter views is resized to 0 in between.
+* **layout**: a unit's full buffer is ``world`` equal chunks, chunk r = rank r's shard, so
+  one ``all_gather_into_tensor`` rebuilds it and one ``reduce_scatter_tensor`` of the unit's
+  gradient buffer delivers every rank its averaged shard (RCCL, no packing).  Shard mode
+  ``flat`` cuts the unit's parameters evenly (elementwise optimizers); mode ``param`` gives
+  every rank whole parameters (NGD preconditions along parameter axes -- Q17: it sees
+  correctly shaped tensors, never a flat shard).
+* **schedule**: forward: a unit waits for its all-gather and immediately launches the
+  next unit's (prefetch), runs, then frees its parameters; backward (entered through a hook
+  on the unit's output gradient): gather again + prefetch the previous unit, gradients
+  accumulate into a unit gradient buffer, and when the unit's last gradient is final
+  (post-accumulate hooks) its reduce-scatter is launched asynchronously while backward
+  continues; ``finish_backward`` only waits.  The optimizer then updates the shards; the
+  next forward gathers the new values -- no post-step all-gather.
+* **offload**: ``offload=True`` keeps shards (and optimizer state) in pinned host memory
+  like the reference's ``CPUOffload``: gathers copy the shard H2D first, gradients come back
+  D2H after the reduce-scatter, and the optimizer runs on the host.
+* the fused ResNet engine (one autograd node for the whole body) drives the units itself at
+  stage boundaries through ``EngineUnits`` (``ops/resnet_fused.py``).
+
+Memory: with 288 GB per MI355X this is a capability, not a necessity, for these models;
+``peak_full_bytes`` reports the largest amount of gathered parameter storage alive at once.
 """
 from __future__ import annotations
 
+import contextlib
+
 import torch
 import torch.distributed as dist
+import torch.nn as nn
 
-from ..utils.flat import ALIGN, FlatParams
-
-
-def partition_slots(slots, world):
-    """Contiguous partition of the flat slot list into ``world`` runs of whole
-    parameters with balanced element counts (boundary placed nearest to
-    total*r/world).  Runs may be empty when one parameter dominates."""
-    sizes = [s.numel for s in slots]
-    total = sum(sizes)
-    cuts, acc, j = [0], 0, 0
-    for r in range(1, world):
-        target = total * r / world
-        while j < len(slots) and acc + sizes[j] / 2 < target:
-            acc += sizes[j]
-            j += 1
-        cuts.append(max(j, cuts[-1]))
-    cuts.append(len(slots))
-    return [(cuts[i], cuts[i + 1]) for i in range(world)]
+from ..utils.flat import ALIGN, Slot, partition_runs
 
 
-class ShardView:
-    """FlatParams-compatible view of one rank's run (what the optimizer updates)."""
+def _al(n):
+    return (n + ALIGN - 1) // ALIGN * ALIGN
 
-    def __init__(self, flat: FlatParams, lo: int, hi: int, slots):
-        self.parent = flat
-        self.lo, self.hi = lo, hi
-        self.numel = hi - lo
-        self.data = flat.data[lo:hi]
-        self.grad = flat.grad[lo:hi]
-        self.shadow = flat.shadow[lo:hi] if flat.shadow is not None else None
-        self.device = flat.device
-        self.slots = []
-        from ..utils.flat import Slot
-        for s in slots:
-            self.slots.append(Slot(s.name, s.param, s.offset - lo, s.numel, s.shape))
-        self._by_param = {id(s.param): s for s in self.slots}
+
+def default_units(model: nn.Module):
+    """Wrap units for the models of this package (name, module) in forward order."""
+    names = dict(model.named_children())
+    if all(k in names for k in ("conv1", "conv2_x", "conv3_x", "conv4_x", "conv5_x", "fc")):
+        return [(k, names[k]) for k in ("conv1", "conv2_x", "conv3_x", "conv4_x", "conv5_x", "fc")]
+    if "sublayer_attention" in names and "sublayer_ffn" in names:
+        units = [("input_embeddings", model.input_embeddings)]
+        for i, (a, f) in enumerate(zip(model.sublayer_attention, model.sublayer_ffn)):
+            units += [(f"sublayer_attention.{i}", a), (f"sublayer_ffn.{i}", f)]
+        units += [("pooler", model.pooler), ("classifier", model.classifier)]
+        return units
+    return size_based_units(model, 10**6)
+
+
+def size_based_units(model: nn.Module, min_params: int):
+    """Reference-style size-based auto wrap: a maximal submodule with >= min_params
+    parameters becomes a unit (recursively, children first)."""
+    out = []
+
+    def visit(prefix, mod):
+        n = sum(p.numel() for p in mod.parameters())
+        big_children = False
+        for name, ch in mod.named_children():
+            if sum(p.numel() for p in ch.parameters()) >= min_params:
+                big_children = True
+        if big_children:
+            for name, ch in mod.named_children():
+                visit(f"{prefix}{name}.", ch)
+        elif n >= min_params and prefix:
+            out.append((prefix[:-1], mod))
+
+    visit("", model)
+    return out
+
+
+class SpaceView:
+    """The rank's shard space seen by the optimizer / clipper (FlatParams interface)."""
+
+    def __init__(self, data, grad, slots, device):
+        self.data, self.grad = data, grad
+        self.numel = data.numel()
+        self.slots = slots
+        self.shadow = None
+        self.device = device
+        self._by_param = {id(s.param): s for s in slots}
 
     @property
     def params(self):
@@ -74,74 +106,343 @@ class ShardView:
         return self._by_param[id(p)]
 
     def zero_grad(self):
-        self.parent.zero_grad()
+        self.grad.zero_()
 
     def refresh_shadow(self):
-        if self.shadow is not None:
-            self.shadow.copy_(self.data)
+        pass
 
 
-class FlatShardedDP:
-    def __init__(self, flat: FlatParams, module=None, process_group=None, broadcast_init=True):
-        self.flat = flat
-        self.module = module
+class Unit:
+    def __init__(self, fs, idx, name, params, mode, root=False):
+        self.fs, self.idx, self.name, self.root = fs, idx, name, root
+        self.params = params  # [(qualified name, Parameter)]
+        ws, rank = fs.ws, fs.rank
+        sizes = [_al(p.numel()) for _, p in params]
+        if mode == "param":
+            runs = partition_runs(sizes, ws)
+            self.chunk = max(ALIGN, max(sum(sizes[a:b]) for a, b in runs))
+            self.pos = {}
+            for r, (a, b) in enumerate(runs):
+                off = r * self.chunk
+                for i in range(a, b):
+                    self.pos[i] = off
+                    off += sizes[i]
+            mine = runs[rank]
+            self.owned = [(i, self.pos[i] - rank * self.chunk) for i in range(mine[0], mine[1])]
+        else:
+            total = sum(sizes)
+            self.chunk = _al(-(-total // ws))
+            self.pos, off = {}, 0
+            for i, s in enumerate(sizes):
+                self.pos[i] = off
+                off += s
+            lo, hi = rank * self.chunk, (rank + 1) * self.chunk
+            # whole parameters inside this rank's chunk (NGD-usable; flat mode is for
+            # elementwise optimizers, the slots only name the parameters)
+            self.owned = [(i, self.pos[i] - lo) for i in range(len(params))
+                          if self.pos[i] >= lo and self.pos[i] + params[i][1].numel() <= hi]
+        self.numel = ws * self.chunk
+        dev = fs.device
+        self.full = torch.zeros(self.numel, device=dev, dtype=torch.float32)
+        self.gfull = torch.zeros(self.numel, device=dev, dtype=torch.float32)
+        self.views = []
+        with torch.no_grad():
+            for i, (n, p) in enumerate(params):
+                v = self.full[self.pos[i]:self.pos[i] + p.numel()].view(p.shape)
+                v.copy_(p.data)
+                self.views.append(v)
+                p.data = v
+        self.gathered = True
+        self.grads_live = False
+        self.work = None      # pending all-gather
+        self.rs_work = None   # pending reduce-scatter
+        self.pending = 0      # gradients still to arrive in this backward
+        self.bwd_started = False
+
+    # ------------------------------------------------------------ storage
+    def _bytes(self):
+        return self.numel * 4
+
+    def _alloc(self, t):
+        st = t.untyped_storage()
+        if st.size() == 0:
+            st.resize_(self._bytes())
+
+    def _free(self, t):
+        st = t.untyped_storage()
+        if st.size() != 0:
+            st.resize_(0)
+
+    # ------------------------------------------------------------ gather / reshard
+    def gather(self, wait=True):
+        fs = self.fs
+        if not self.gathered and self.work is None:
+            self._alloc(self.full)
+            fs._account()
+            src = fs.shard_chunk(self)
+            self.work = dist.all_gather_into_tensor(self.full, src, group=fs.pg, async_op=True)
+        if wait and self.work is not None:
+            self.work.wait()
+            self.work = None
+            self.gathered = True
+
+    def reshard(self):
+        if self.root or not self.gathered or self.work is not None:
+            return
+        self._free(self.full)
+        self.gathered = False
+
+    # ------------------------------------------------------------ backward
+    def begin_backward(self):
+        if self.bwd_started:
+            return
+        self.bwd_started = True
+        self.gather(wait=True)
+        self._alloc(self.gfull)
+        self.gfull.zero_()
+        for i, (n, p) in enumerate(self.params):
+            p.grad = self.gfull[self.pos[i]:self.pos[i] + p.numel()].view(p.shape)
+        self.grads_live = True
+        self.pending = sum(1 for _, p in self.params if p.requires_grad)
+        self.fs._account()
+
+    def grad_ready(self):
+        self.pending -= 1
+        if self.pending == 0:
+            self.reduce()
+
+    def reduce(self):
+        """Launch the reduce-scatter of this unit's gradient (async), release buffers."""
+        fs = self.fs
+        if not self.grads_live or self.rs_work is not None:
+            return
+        op = dist.ReduceOp.AVG if fs.use_avg else dist.ReduceOp.SUM
+        self.rs_work = dist.reduce_scatter_tensor(fs.grad_chunk(self), self.gfull, op=op, group=fs.pg,
+                                                  async_op=True)
+        for _, p in self.params:
+            p.grad = None
+        self.grads_live = False
+        if not self.root:
+            self.reshard()
+
+    def finish(self):
+        if self.grads_live:
+            self.reduce()
+        if self.rs_work is not None:
+            self.rs_work.wait()
+            self.rs_work = None
+            self._free(self.gfull)
+        self.bwd_started = False
+
+
+class FullyShardedDP:
+    sharded_optimizer = True
+
+    def __init__(self, model: nn.Module, device=None, units=None, mode="flat", offload=False, process_group=None,
+                 prefetch=True, engine_units=()):
+        """units: [(name, module)] (None: ``default_units``); mode: 'flat' | 'param' (NGD);
+        engine_units: names of units whose forward/backward an engine drives explicitly
+        (no module hooks installed on them)."""
+        self.model = model
         self.pg = process_group
         self.ws = dist.get_world_size(process_group)
         self.rank = dist.get_rank(process_group)
+        self.device = torch.device(device) if device is not None else next(model.parameters()).device
         self.use_avg = dist.get_backend(process_group) == "nccl"
-        runs = partition_slots(flat.slots, self.ws)
-        self.ranges = []
-        for a, b in runs:
-            if a == b:
-                lo = hi = flat.numel
-            else:
-                lo = flat.slots[a].offset
-                last = flat.slots[b - 1]
-                hi = min((last.offset + last.numel + ALIGN - 1) // ALIGN * ALIGN, flat.numel)
-            self.ranges.append((lo, hi))
-        # slots are contiguous and 64-aligned, so consecutive non-empty runs already tile
-        # the buffer; the trailing padding goes to the last non-empty run
-        last_nonempty = max(r for r in range(self.ws) if self.ranges[r][0] < flat.numel)
-        self.ranges[last_nonempty] = (self.ranges[last_nonempty][0], flat.numel)
-        self.chunk = max(hi - lo for lo, hi in self.ranges)
-        self.chunk = (self.chunk + ALIGN - 1) // ALIGN * ALIGN
-        self.stage = torch.zeros(self.ws * self.chunk, device=flat.device, dtype=torch.float32)
-        self.local = torch.zeros(self.chunk, device=flat.device, dtype=torch.float32)
-        lo, hi = self.ranges[self.rank]
-        a, b = runs[self.rank]
-        self.view = ShardView(flat, lo, hi, flat.slots[a:b])
-        if broadcast_init:
-            dist.broadcast(flat.data, 0, group=self.pg)
-            flat.refresh_shadow()
+        self.offload = offload
+        self.prefetch = prefetch
+        self.mode = mode
+        # identical initial parameters on every rank (rank 0's), before sharding
+        with torch.no_grad():
+            for p in model.parameters():
+                dist.broadcast(p.data, 0, group=self.pg)
+        unit_list = list(units) if units is not None else default_units(model)
+        owner = {}
+        for ui, (name, mod) in enumerate(unit_list):
+            for pn, p in mod.named_parameters():
+                if p.requires_grad and id(p) not in owner:
+                    owner[id(p)] = (ui, f"{name}.{pn}")
+        root_params = [(n, p) for n, p in model.named_parameters() if p.requires_grad and id(p) not in owner]
+        self.units = []
+        for ui, (name, mod) in enumerate(unit_list):
+            ps = [(f"{name}.{pn}", p) for pn, p in mod.named_parameters() if p.requires_grad
+                  and owner.get(id(p), (None,))[0] == ui]
+            if ps:
+                self.units.append(Unit(self, len(self.units), name, ps, mode))
+        if root_params:
+            self.units.append(Unit(self, len(self.units), "<root>", root_params, mode, root=True))
+        self.by_name = {u.name: u for u in self.units}
+        # shard storage: the units' chunks concatenated
+        total = sum(u.chunk for u in self.units)
+        sdev = torch.device("cpu") if offload else self.device
+        self.shard_data = torch.zeros(total, device=sdev, dtype=torch.float32, pin_memory=offload and
+                                      torch.cuda.is_available())
+        self.shard_grad = torch.zeros_like(self.shard_data)
+        if offload:
+            self.shard_grad = self.shard_grad.pin_memory() if torch.cuda.is_available() else self.shard_grad
+            self.stage_data = torch.empty(max(u.chunk for u in self.units), device=self.device)
+            self.stage_grad = torch.empty(total, device=self.device)
+            self.copy_stream = torch.cuda.Stream(self.device) if self.device.type == "cuda" else None
+        off = 0
+        slots = []
+        for u in self.units:
+            u.shard_off = off
+            lo = self.rank * u.chunk
+            self.shard_data[off:off + u.chunk].copy_(u.full[lo:lo + u.chunk])
+            for i, rel in u.owned:
+                n, p = u.params[i]
+                slots.append(Slot(n, p, off + rel, p.numel(), p.shape))
+            off += u.chunk
+        self.space = SpaceView(self.shard_data, self.shard_grad, slots, sdev)
+        self.view = self.space  # (trainer interface shared with the sharded-optimizer DP)
+        self.peak_full_bytes = 0
+        self.order = [u for u in self.units if not u.root]
+        self.engine_units = set(engine_units)
+        self._hooks = []
+        self._install_hooks()
+        for u in self.units:
+            u.reshard()
+        self._account()
 
-    def _pack(self, src: torch.Tensor):
-        for r, (lo, hi) in enumerate(self.ranges):
-            if hi > lo:
-                self.stage[r * self.chunk:r * self.chunk + (hi - lo)].copy_(src[lo:hi])
+    # ------------------------------------------------------------ shard views
+    def shard_chunk(self, u):
+        c = self.shard_data[u.shard_off:u.shard_off + u.chunk]
+        if self.offload:
+            st = self.stage_data[:u.chunk]
+            st.copy_(c, non_blocking=True)
+            return st
+        return c
 
-    def _unpack(self, dst: torch.Tensor):
-        for r, (lo, hi) in enumerate(self.ranges):
-            if hi > lo:
-                dst[lo:hi].copy_(self.stage[r * self.chunk:r * self.chunk + (hi - lo)])
+    def grad_chunk(self, u):
+        if self.offload:
+            return self.stage_grad[u.shard_off:u.shard_off + u.chunk]
+        return self.shard_grad[u.shard_off:u.shard_off + u.chunk]
 
+    def _account(self):
+        b = sum(u._bytes() for u in self.units if u.full.untyped_storage().size() != 0)
+        b += sum(u._bytes() for u in self.units if u.gfull.untyped_storage().size() != 0)
+        self.peak_full_bytes = max(self.peak_full_bytes, b)
+
+    def resident_param_bytes(self):
+        return sum(u._bytes() for u in self.units if u.full.untyped_storage().size() != 0)
+
+    # ------------------------------------------------------------ unit API (hooks / engine)
+    def _next(self, u, step):
+        i = self.order.index(u) if u in self.order else -1
+        j = i + step
+        return self.order[j] if 0 <= j < len(self.order) else None
+
+    def pre_forward(self, name):
+        u = self.by_name[name]
+        for r in self.units:
+            if r.root:
+                r.gather(wait=True)
+        u.gather(wait=True)
+        if self.prefetch:
+            nxt = self._next(u, +1)
+            if nxt is not None:
+                nxt.gather(wait=False)
+
+    def post_forward(self, name, keep=False):
+        u = self.by_name[name]
+        if not keep and u is not self.order[-1]:
+            u.reshard()
+
+    def pre_backward(self, name):
+        u = self.by_name[name]
+        u.begin_backward()
+        if self.prefetch:
+            prv = self._next(u, -1)
+            if prv is not None and not prv.bwd_started:
+                prv.gather(wait=False)
+
+    def post_backward(self, name):
+        self.by_name[name].reduce()
+
+    # ------------------------------------------------------------ module hooks
+    def _install_hooks(self):
+        mods = dict(self.model.named_modules())
+        for u in self.units:
+            for _, p in u.params:
+                self._hooks.append(p.register_post_accumulate_grad_hook(self._make_acc_hook(u)))
+            if u.root or u.name in self.engine_units:
+                continue
+            m = mods[u.name]
+            self._hooks.append(m.register_forward_pre_hook(self._make_pre(u)))
+            self._hooks.append(m.register_forward_hook(self._make_post(u)))
+
+    def _make_acc_hook(self, u):
+        def hook(p):
+            if u.name in self.engine_units:
+                return  # the engine calls post_backward at the stage boundary
+            if not u.bwd_started:
+                u.begin_backward()  # a parameter whose unit output hook did not fire
+            u.grad_ready()
+        return hook
+
+    def _make_pre(self, u):
+        def pre(mod, args):
+            self.pre_forward(u.name)
+        return pre
+
+    def _make_post(self, u):
+        def post(mod, args, out):
+            if torch.is_grad_enabled():
+                fired = [False]
+
+                def on_grad(g):
+                    if not fired[0]:
+                        fired[0] = True
+                        self.pre_backward(u.name)
+                    return g
+                for t in (out if isinstance(out, (tuple, list)) else (out,)):
+                    if isinstance(t, torch.Tensor) and t.requires_grad:
+                        t.register_hook(on_grad)
+            self.post_forward(u.name)
+            return out
+        return post
+
+    # ------------------------------------------------------------ step boundary
     def finish_backward(self):
-        """Reduce-scatter: rank r receives the averaged gradient of run r."""
-        self._pack(self.flat.grad)
-        op = dist.ReduceOp.AVG if self.use_avg else dist.ReduceOp.SUM
-        dist.reduce_scatter_tensor(self.local, self.stage, op=op, group=self.pg)
+        """Complete every unit's gradient reduce-scatter (launch what is left, e.g. units
+        whose parameters got no gradient), land the averaged shard gradients."""
+        for u in self.units:
+            if u.bwd_started or u.grads_live:
+                u.finish()
+            else:  # unused this step: contributes zeros (every rank must join the collective)
+                u.begin_backward()
+                u.finish()
+        if self.offload:
+            self.shard_grad.copy_(self.stage_grad, non_blocking=False)
         if not self.use_avg:
-            self.local.div_(self.ws)
-        lo, hi = self.ranges[self.rank]
-        self.flat.grad[lo:hi].copy_(self.local[:hi - lo])
+            self.shard_grad.div_(self.ws)
+        for u in self.units:
+            if not u.root:
+                u.reshard()
 
     def after_step(self):
-        """All-gather the updated runs into every rank's full parameter buffer."""
-        lo, hi = self.ranges[self.rank]
-        self.local.zero_()
-        self.local[:hi - lo].copy_(self.flat.data[lo:hi])
-        dist.all_gather_into_tensor(self.stage, self.local, group=self.pg)
-        with torch.no_grad():
-            self._unpack(self.flat.data)
-        self.flat.refresh_shadow()
-        # gradients outside the owned run were consumed by the reduce-scatter
-        self.flat.grad.zero_()
+        """Nothing to all-gather: the next forward gathers the updated shards."""
+
+    def sync_buffers(self, src: int = 0):
+        from .dist import broadcast_buffers
+        broadcast_buffers(self.model, src, self.pg)
+
+    @contextlib.contextmanager
+    def summon_full_params(self):
+        """All units gathered (checkpointing / state_dict); resharded on exit."""
+        for u in self.units:
+            u.gather(wait=True)
+        try:
+            yield
+        finally:
+            for u in self.units:
+                u.reshard()
+
+    def full_state_dict(self):
+        with self.summon_full_params():
+            return {k: v.detach().clone().cpu() for k, v in self.model.state_dict().items()}
+
+    def remove(self):
+        for h in self._hooks:
+            h.remove()
+        self._hooks = []

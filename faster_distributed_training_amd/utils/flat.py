@@ -36,8 +36,33 @@ class Slot:
     shape: torch.Size
 
 
+def _aligned(n: int) -> int:
+    return (n + ALIGN - 1) // ALIGN * ALIGN
+
+
+def partition_runs(sizes, world):
+    """Contiguous partition of a list of sizes into ``world`` runs with balanced totals
+    (each boundary placed nearest to total*r/world).  Returns [(first, last+1)] per run;
+    runs may be empty when one item dominates."""
+    total = sum(sizes)
+    cuts, acc, j = [0], 0, 0
+    for r in range(1, world):
+        target = total * r / world
+        while j < len(sizes) and acc + sizes[j] / 2 < target:
+            acc += sizes[j]
+            j += 1
+        cuts.append(max(j, cuts[-1]))
+    cuts.append(len(sizes))
+    return [(cuts[i], cuts[i + 1]) for i in range(world)]
+
+
 class FlatParams:
-    def __init__(self, module_or_params, device=None, reverse=True, with_shadow=False, names=None):
+    """``partition=W``: the slots are split into W contiguous runs of whole parameters
+    (balanced) and run r is placed at offset r*chunk (chunk = the longest run, aligned), so
+    the buffers are W equal chunks: reduce-scatter / all-gather need no packing (the
+    sharded-optimizer data parallel of ``parallel/zero.py``)."""
+
+    def __init__(self, module_or_params, device=None, reverse=True, with_shadow=False, names=None, partition=0):
         if isinstance(module_or_params, nn.Module):
             named = [(n, p) for n, p in module_or_params.named_parameters() if p.requires_grad]
         else:
@@ -46,12 +71,25 @@ class FlatParams:
         if reverse:
             named = named[::-1]
         self.slots: list[Slot] = []
-        off = 0
-        for n, p in named:
-            k = p.numel()
-            self.slots.append(Slot(n, p, off, k, p.shape))
-            off += (k + ALIGN - 1) // ALIGN * ALIGN
-        self.numel = off
+        self.runs = None
+        self.chunk = 0
+        if partition and partition > 1:
+            self.runs = partition_runs([_aligned(p.numel()) for _, p in named], partition)
+            self.chunk = max(sum(_aligned(named[i][1].numel()) for i in range(a, b)) for a, b in self.runs)
+            self.chunk = max(self.chunk, ALIGN)
+            for r, (a, b) in enumerate(self.runs):
+                off = r * self.chunk
+                for n, p in named[a:b]:
+                    self.slots.append(Slot(n, p, off, p.numel(), p.shape))
+                    off += _aligned(p.numel())
+            self.numel = partition * self.chunk
+        else:
+            off = 0
+            for n, p in named:
+                k = p.numel()
+                self.slots.append(Slot(n, p, off, k, p.shape))
+                off += _aligned(k)
+            self.numel = off
         dev = device if device is not None else (named[0][1].device if named else torch.device("cpu"))
         self.device = torch.device(dev)
         self.data = torch.zeros(self.numel, device=self.device, dtype=torch.float32)
