@@ -343,7 +343,7 @@ def pack_weights(entries):
         nat.pack_weights(src, wf, wd, co, ci, cx, nt, _sp())
 
 
-def alloc_packed(shp: ConvShape, device, dgrad=True):
-    wf = torch.empty(shp.cout, shp.ntaps, shp.cxp, device=device, dtype=torch.bfloat16)
+def alloc_packed(shp: ConvShape, device, dgrad=True, fwd=True):
+    wf = torch.empty(shp.cout, shp.ntaps, shp.cxp, device=device, dtype=torch.bfloat16) if fwd else None
     wd = torch.empty(shp.cin, shp.ntaps, shp.cout, device=device, dtype=torch.bfloat16) if dgrad else None
     return wf, wd

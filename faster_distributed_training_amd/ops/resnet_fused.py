@@ -130,9 +130,11 @@ class Unit:
 
     def ensure_packed_buffers(self, dev, need_dgrad):
         need_wd = need_dgrad and self.shp.cin >= 8
-        if self.wf is None or self.wf.device != dev or (need_wd and self.wd is None):
-            # (an eval / no-grad forward packs no dgrad layout; a later train step needs it)
+        if self.wf is None or self.wf.device != dev:
             self.wf, self.wd = ci.alloc_packed(self.shp, dev, dgrad=need_wd)
+        elif need_wd and self.wd is None:
+            # (an eval / no-grad forward packs no dgrad layout; a later train step needs it)
+            self.wd = ci.alloc_packed(self.shp, dev, dgrad=True, fwd=False)[1]
 
 
 def _act_of(m):
@@ -175,13 +177,20 @@ class Block:
         self.join = (ACT_RELU, 1.0) if isinstance(blk, BottleNeck) else (ACT_CELU, 0.075)
 
 
+STAGES = ("conv2_x", "conv3_x", "conv4_x", "conv5_x")
+
+
 class Plan:
     def __init__(self, model):
         stem_seq = model.conv1
         self.stem = Unit(stem_seq[0], None, _act_of(stem_seq[1]))
-        self.blocks = [Block(b) for stage in (model.conv2_x, model.conv3_x, model.conv4_x, model.conv5_x)
-                       for b in stage]
+        self.blocks, self.stage_of = [], []
+        for name in STAGES:
+            for b in getattr(model, name):
+                self.blocks.append(Block(b))
+                self.stage_of.append(name)
         self.units = [self.stem] + [u for b in self.blocks for u in (b.units + ([b.shortcut] if b.shortcut else []))]
+        self.fsdp = None  # parallel/fsdp.py FullyShardedDP driving the stages as wrap units
 
     def pack(self, dev, need_dgrad=True):
         ents = []
@@ -189,6 +198,39 @@ class Plan:
             u.ensure_packed_buffers(dev, need_dgrad and u is not self.stem)
             ents.append((u.w.detach(), u.wf, u.wd, u.shp))
         ci.pack_weights(ents)
+
+    # ---- FSDP: units are gathered stage by stage, so weights are packed per stage (the
+    # forward layout before the stage's forward, the dgrad layout before its backward) and
+    # the packed copies are released with the gathered parameters
+    def stage_units(self, name):
+        if name == "conv1":
+            return [self.stem]
+        return [u for b, st in zip(self.blocks, self.stage_of) if st == name
+                for u in (b.units + ([b.shortcut] if b.shortcut else []))]
+
+    def pack_stage(self, name, dev, fwd: bool):
+        ents = []
+        for u in self.stage_units(name):
+            need_wd = (not fwd) and u is not self.stem
+            u.ensure_packed_buffers(dev, need_wd)
+            _restore(u.wf if fwd else u.wd)
+            if fwd or need_wd:
+                ents.append((u.w.detach(), u.wf if fwd else None, None if fwd else u.wd, u.shp))
+        ci.pack_weights(ents)
+
+    def release_stage(self, name, fwd: bool):
+        for u in self.stage_units(name):
+            _release(u.wf if fwd else u.wd)
+
+
+def _release(t):
+    if t is not None and t.untyped_storage().size() != 0:
+        t.untyped_storage().resize_(0)
+
+
+def _restore(t):
+    if t is not None and t.untyped_storage().size() == 0:
+        t.untyped_storage().resize_(t.numel() * t.element_size())
 
 
 # ------------------------------------------------------------------ kernels glue
@@ -307,7 +349,12 @@ class ResNetBodyFn(torch.autograd.Function):
     def forward(ctx, x_nhwc, plan: Plan, training: bool, need_grad: bool):
         nat = _native.native()
         dev = x_nhwc.device
-        plan.pack(dev, need_dgrad=need_grad)
+        fs = plan.fsdp
+        if fs is None:
+            plan.pack(dev, need_dgrad=need_grad)
+        else:
+            fs.pre_forward("conv1")
+            plan.pack_stage("conv1", dev, fwd=True)
         recs = []
         # stem: conv -> FCBN stats -> materialised CELU output
         st = plan.stem
@@ -316,7 +363,14 @@ class ResNetBodyFn(torch.autograd.Function):
         nat.act_affine_fwd(y0.data_ptr(), s0.data_ptr(), t0.data_ptr(), h.data_ptr(), M0, st.shp.cout,
                            st.act_out[0], float(st.act_out[1]), 1, 1, _sp())
         stem_rec = (x_nhwc, y0, s0, t0, sm0, sa0)
-        for b in plan.blocks:
+        cur = "conv1"
+        for bi, b in enumerate(plan.blocks):
+            if fs is not None and plan.stage_of[bi] != cur:
+                plan.release_stage(cur, fwd=True)
+                fs.post_forward(cur)
+                cur = plan.stage_of[bi]
+                fs.pre_forward(cur)
+                plan.pack_stage(cur, dev, fwd=True)
             x_in = h
             ys = []
             raw, s, t, act = x_in, None, None, (ACT_NONE, 1.0)
@@ -353,6 +407,9 @@ class ResNetBodyFn(torch.autograd.Function):
             if need_grad:
                 recs.append((x_in, ys, sc, out, mask))
             h = out
+        if fs is not None:
+            plan.release_stage(cur, fwd=True)
+            fs.post_forward(cur)
         if need_grad:
             ctx.plan, ctx.training = plan, training
             ctx.recs, ctx.stem_rec = recs, stem_rec
@@ -375,8 +432,17 @@ class ResNetBodyFn(torch.autograd.Function):
         recs = ctx.recs
         nblk = len(plan.blocks)
         joined = False  # g is already g_pre of the current block (stats in the slots)
+        fs = plan.fsdp
+        cur = None
         for bi in range(nblk - 1, -1, -1):
             b = plan.blocks[bi]
+            if fs is not None and plan.stage_of[bi] != cur:
+                if cur is not None:
+                    plan.release_stage(cur, fwd=False)
+                    fs.post_backward(cur)
+                cur = plan.stage_of[bi]
+                fs.pre_backward(cur)
+                plan.pack_stage(cur, dev, fwd=False)
             x_in, ys, sc, out, mask = recs[bi]
             y3, s3 = ys[-1][0], ys[-1][1]
             C = y3.shape[-1]
@@ -451,6 +517,10 @@ class ResNetBodyFn(torch.autograd.Function):
                     wgrad_into(u, g_cur, y, al, be, x_in, None, None, (ACT_NONE, 1.0), gs=gs_cur)
             g = g_x
             joined = prev is not None
+        if fs is not None and cur is not None:
+            plan.release_stage(cur, fwd=False)
+            fs.post_backward(cur)
+            fs.pre_backward("conv1")
         # stem: act backward + statistics -> wgrad on the input image
         x_img, y0, s0, t0, sm0, sa0 = ctx.stem_rec
         st = plan.stem
@@ -462,6 +532,8 @@ class ResNetBodyFn(torch.autograd.Function):
                            part.data_ptr(), M0, C0, st.act_out[0], float(st.act_out[1]), 1, _sp())
         (al, be), _ = bwd_finalize(part, 2, st, (sm0, sa0, M0), training=training, dev=dev)
         wgrad_into(st, gy0, y0, al, be, x_img, None, None, (ACT_NONE, 1.0))
+        if fs is not None:
+            fs.post_backward("conv1")
         if not getattr(ctx, "keep", False):
             ctx.recs = ctx.stem_rec = None
         return None, None, None, None
@@ -484,7 +556,9 @@ def resnet_engine_forward(model, x):
     plan = getattr(model, "_plan", None)
     if plan is None:
         plan = model._plan = Plan(model)
-    plan.use_graphs = bool(getattr(model, "graph_engine", False))
+    plan.fsdp = getattr(model, "_fsdp", None)
+    # collectives run between the stages under FSDP: no whole-body graph capture
+    plan.use_graphs = bool(getattr(model, "graph_engine", False)) and plan.fsdp is None
     xin = to_engine_input(x, plan.stem.shp.cxp)
     need_grad = torch.is_grad_enabled() and any(p.requires_grad for p in model.parameters())
     if need_grad:

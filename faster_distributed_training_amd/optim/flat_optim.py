@@ -38,7 +38,9 @@ def _p(t):
 class FlatOptimizer(torch.optim.Optimizer):
     def __init__(self, flat: FlatParams, defaults: dict, zero_grad_in_step: bool = True):
         self.flat = flat
-        super().__init__(flat.params, defaults)
+        # the update runs over the flat buffer; torch.optim.Optimizer only needs a parameter
+        # list for its param_groups bookkeeping (a flat FSDP shard may hold no whole one)
+        super().__init__(flat.params or [torch.nn.Parameter(torch.zeros(0))], defaults)
         self.zero_grad_in_step = zero_grad_in_step
         self.k = 0  # step() calls
         # steps skipped on the device (non-finite / fp16 overflow): the kernels bump it and
@@ -317,7 +319,10 @@ class GradClipper:
     def _sharded_finalize(self, sumsq, max_norm):
         import torch.distributed as dist
         t = sumsq.reshape(1).float()
+        if not t.is_cuda and dist.get_backend(self.pg) == "nccl":  # host-offloaded shard on RCCL
+            t = t.cuda()
         dist.all_reduce(t, group=self.pg)
+        t = t.to(self.out.device)
         norm = t.sqrt()
         coef = (max_norm / (norm + 1e-6)).clamp(max=1.0) if max_norm > 0 else torch.ones_like(norm)
         self.out[0:1].copy_(norm)

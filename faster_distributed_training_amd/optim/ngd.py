@@ -438,7 +438,7 @@ class NGD(SGD):
         for s in self.flat.slots:
             by_shape.setdefault(tuple(s.shape), []).append(s)
         self.groups = [
-            (_ShapeGroup(shape, slots, g["alpha"], g["rank"], g["update_period"], g["eta"], torch.float32,
+            (_ShapeGroup(shape, slots, g["alpha"], g["rank"], g["update_period"], g["eta"], self.flat.data.dtype,
                          self.flat.device), slots)
             for shape, slots in by_shape.items()]
 

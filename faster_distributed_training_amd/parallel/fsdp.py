@@ -31,8 +31,9 @@ MI355X design (``FullyShardedDP``):
 * **offload**: ``offload=True`` keeps shards (and optimizer state) in pinned host memory
   like the reference's ``CPUOffload``: gathers copy the shard H2D first, gradients come back
   D2H after the reduce-scatter, and the optimizer runs on the host.
-* the fused ResNet engine (one autograd node for the whole body) drives the units itself at
-  stage boundaries through ``EngineUnits`` (``ops/resnet_fused.py``).
+* the fused ResNet engine (one autograd node for the whole body) drives its units itself at
+  stage boundaries (``pre_forward`` / ``post_forward`` / ``pre_backward`` / ``post_backward``,
+  ``ops/resnet_fused.py``) and packs / releases its bf16 weight layouts per stage.
 
 Memory: with 288 GB per MI355X this is a capability, not a necessity, for these models;
 ``peak_full_bytes`` reports the largest amount of gathered parameter storage alive at once.
@@ -193,11 +194,12 @@ class Unit:
         self.gathered = False
 
     # ------------------------------------------------------------ backward
-    def begin_backward(self):
+    def begin_backward(self, gather=True):
         if self.bwd_started:
             return
         self.bwd_started = True
-        self.gather(wait=True)
+        if gather:
+            self.gather(wait=True)
         self._alloc(self.gfull)
         self.gfull.zero_()
         for i, (n, p) in enumerate(self.params):
@@ -280,7 +282,7 @@ class FullyShardedDP:
         self.shard_grad = torch.zeros_like(self.shard_data)
         if offload:
             self.shard_grad = self.shard_grad.pin_memory() if torch.cuda.is_available() else self.shard_grad
-            self.stage_data = torch.empty(max(u.chunk for u in self.units), device=self.device)
+            self.stage_data = torch.empty(total, device=self.device)
             self.stage_grad = torch.empty(total, device=self.device)
             self.copy_stream = torch.cuda.Stream(self.device) if self.device.type == "cuda" else None
         off = 0
@@ -302,13 +304,15 @@ class FullyShardedDP:
         self._install_hooks()
         for u in self.units:
             u.reshard()
+            u._free(u.gfull)
         self._account()
+        model._fsdp_sharded = self  # checkpoint I/O gathers through summon_full_params
 
     # ------------------------------------------------------------ shard views
     def shard_chunk(self, u):
         c = self.shard_data[u.shard_off:u.shard_off + u.chunk]
         if self.offload:
-            st = self.stage_data[:u.chunk]
+            st = self.stage_data[u.shard_off:u.shard_off + u.chunk]
             st.copy_(c, non_blocking=True)
             return st
         return c
@@ -345,8 +349,9 @@ class FullyShardedDP:
 
     def post_forward(self, name, keep=False):
         u = self.by_name[name]
-        if not keep and u is not self.order[-1]:
-            u.reshard()
+        if keep or (torch.is_grad_enabled() and u is self.order[-1]):
+            return  # the backward starts with this unit
+        u.reshard()
 
     def pre_backward(self, name):
         u = self.by_name[name]
@@ -376,7 +381,13 @@ class FullyShardedDP:
             if u.name in self.engine_units:
                 return  # the engine calls post_backward at the stage boundary
             if not u.bwd_started:
-                u.begin_backward()  # a parameter whose unit output hook did not fire
+                # a gradient that arrived before the unit's output hook (root unit, or an
+                # output without grad): start the unit's backward, keep what was accumulated
+                g = p.grad
+                u.begin_backward()
+                if g is not None:
+                    with torch.no_grad():
+                        p.grad.add_(g)
             u.grad_ready()
         return hook
 
@@ -410,7 +421,7 @@ class FullyShardedDP:
             if u.bwd_started or u.grads_live:
                 u.finish()
             else:  # unused this step: contributes zeros (every rank must join the collective)
-                u.begin_backward()
+                u.begin_backward(gather=False)
                 u.finish()
         if self.offload:
             self.shard_grad.copy_(self.stage_grad, non_blocking=False)
@@ -421,7 +432,13 @@ class FullyShardedDP:
                 u.reshard()
 
     def after_step(self):
-        """Nothing to all-gather: the next forward gathers the updated shards."""
+        """Nothing to all-gather: the next forward gathers the updated shards (any copy still
+        gathered -- the root unit -- is marked stale)."""
+        for u in self.units:
+            if u.root:
+                u.gathered = False
+            else:
+                u.reshard()
 
     def sync_buffers(self, src: int = 0):
         from .dist import broadcast_buffers
@@ -437,6 +454,16 @@ class FullyShardedDP:
         finally:
             for u in self.units:
                 u.reshard()
+
+    def load_full_state_dict(self, sd, strict=True):
+        """Load a full (reference-schema) state_dict: every rank keeps its shard of it."""
+        with self.summon_full_params():
+            res = self.model.load_state_dict(sd, strict=strict)
+            with torch.no_grad():
+                for u in self.units:
+                    lo = self.rank * u.chunk
+                    self.shard_data[u.shard_off:u.shard_off + u.chunk].copy_(u.full[lo:lo + u.chunk])
+        return res
 
     def full_state_dict(self):
         with self.summon_full_params():

@@ -73,7 +73,7 @@ class ShardedOptimizerDP:
         self.lo, self.hi = self.rank * c, (self.rank + 1) * c
         a, b = flat.runs[self.rank]
         self.view = ShardView(flat, self.lo, self.hi, flat.slots[a:b])
-        self.local = torch.empty(c, device=flat.device, dtype=torch.float32)
+        self.local = torch.empty(c, device=flat.device, dtype=flat.data.dtype)
         if broadcast_init:
             dist.broadcast(flat.data, 0, group=self.pg)
             flat.refresh_shadow()

@@ -28,11 +28,23 @@ def _compact(sd):
     return {k: (v.detach().clone().cpu() if isinstance(v, torch.Tensor) else v) for k, v in sd.items()}
 
 
+def _sharded(model):
+    """The FullyShardedDP (parallel/fsdp.py) owning ``model``'s parameters, if any."""
+    return getattr(model, "_fsdp_sharded", None)
+
+
 def model_state(model, module_prefix=False):
-    sd = model.state_dict()
+    """Full state_dict (compact CPU copies).  Under FSDP this gathers every unit: it is a
+    collective and must run on every rank."""
+    fs = _sharded(model)
+    if fs is not None:
+        with fs.summon_full_params():
+            sd = _compact(model.state_dict())
+    else:
+        sd = _compact(model.state_dict())
     if module_prefix:
         sd = {"module." + k: v for k, v in sd.items()}
-    return _compact(sd)
+    return sd
 
 
 def strip_prefix(sd, prefix="module."):
@@ -42,9 +54,10 @@ def strip_prefix(sd, prefix="module."):
 
 
 def save_checkpoint(path, model, acc, epoch, module_prefix=False, extra=None):
+    net = model_state(model, module_prefix) if (is_rank0() or _sharded(model) is not None) else None
     if is_rank0():
         os.makedirs(os.path.dirname(os.path.abspath(path)) or ".", exist_ok=True)
-        state = {"net": model_state(model, module_prefix), "acc": float(acc), "epoch": int(epoch)}
+        state = {"net": net, "acc": float(acc), "epoch": int(epoch)}
         if extra:
             state.update(extra)
         tmp = path + ".tmp"
@@ -61,6 +74,9 @@ def load_model_state(model, sd, strict=True):
     """Load a reference-schema state_dict (with or without ``module.``) in place
     (copies into the existing, possibly flat-buffer-backed, parameters)."""
     sd = strip_prefix(sd)
+    fs = _sharded(model)
+    if fs is not None:
+        return fs.load_full_state_dict(sd, strict=strict)
     missing, unexpected = model.load_state_dict(sd, strict=strict)
     return missing, unexpected
 

@@ -22,6 +22,7 @@ import torch.nn as nn
 from ..data.cifar import CLASSES, CIFAR10, DeviceCIFARLoader, augment_order, synthetic_cifar
 from ..models import resnet as resnet_models
 from ..ops.mixup import MetaMixup, mixup_criterion, mixup_criterion_meta, mixup_data
+from ..ops.resnet_fused import STAGES
 from ..optim.flat_optim import MADGRAD, SGD, Adam, DeviceGradScaler, GradClipper, MirrorMADGRAD
 from ..optim.ngd import NGD
 from ..parallel import dist as pdist
@@ -58,6 +59,8 @@ class ResNetConfig:
     first_bucket_mb: float = 1.0
     comm_dtype: str = "fp32"
     fsdp: bool = False
+    fsdp_offload: bool = False         # FSDP shards + optimizer state in pinned host memory (CPUOffload)
+    shard_ngd: bool = True             # distributed NGD: each rank owns + preconditions 1/world of the params
     scheduler: str = "auto"
     resume: bool = False
     checkpoint_dir: str = "./checkpoint"
@@ -101,23 +104,42 @@ class ResNetTrainer:
         self.meta = None
         if cfg.meta_learning:
             self.meta = MetaMixup(cfg.bs, device=self.device, learnable=cfg.learnable_meta)
-        params_owner = self.model if not (self.meta and cfg.learnable_meta) else nn.ModuleList([self.model, self.meta])
-        self.flat = FlatParams(params_owner, device=self.device)
-        self.reducer = None
-        self.fsdp = None
-        if cfg.distributed:
-            if cfg.fsdp:
-                from ..parallel.fsdp import FlatShardedDP
-                self.fsdp = FlatShardedDP(self.flat, self.model)
-            else:
+        learnable = bool(self.meta and cfg.learnable_meta)
+        params_owner = self.model if not learnable else nn.ModuleList([self.model, self.meta])
+        ngd_opt = cfg.optimizer == "ngd" or (cfg.optimizer == "auto" and cfg.ngd)
+        self.reducer = self.fsdp = self.zero = None
+        if cfg.distributed and cfg.fsdp:
+            # ZeRO-3: parameters sharded at rest, gathered per stage (parallel/fsdp.py); NGD
+            # needs whole parameters per rank ("param" shard mode, survey Q17)
+            if learnable:
+                raise ValueError("--fsdp does not shard the learnable meta-mixup parameters")
+            from ..parallel.fsdp import FullyShardedDP
+            engine = self.model.use_fast_path(torch.empty(1, device=self.device))
+            self.model.graph_engine = False
+            self.fsdp = FullyShardedDP(self.model, self.device, mode="param" if ngd_opt else "flat",
+                                       offload=cfg.fsdp_offload,
+                                       engine_units=("conv1",) + STAGES if engine else ())
+            if engine:
+                self.model._fsdp = self.fsdp
+            self.flat = self.fsdp.space
+        elif cfg.distributed and ngd_opt and cfg.shard_ngd:
+            # ZeRO-2 for NGD: each rank preconditions + updates only the parameters it owns
+            # (parallel/zero.py) instead of every rank repeating the whole NGD step
+            from ..parallel.zero import ShardedOptimizerDP
+            self.flat = FlatParams(params_owner, device=self.device, partition=self.world)
+            self.zero = ShardedOptimizerDP(self.flat, self.model)
+        else:
+            self.flat = FlatParams(params_owner, device=self.device)
+            if cfg.distributed:
                 from ..parallel.ddp import BucketReducer
                 cdt = {"fp32": None, "bf16": torch.bfloat16}[cfg.comm_dtype]
                 self.reducer = BucketReducer(self.flat, self.model, bucket_mb=cfg.bucket_mb,
                                              first_bucket_mb=cfg.first_bucket_mb, comm_dtype=cdt)
+        self.sharder = self.fsdp if self.fsdp is not None else self.zero
         seed_everything(cfg.seed, self.rank)  # per-rank data/mixup randomness
-        self.space = self.fsdp.view if self.fsdp is not None else self.flat
+        self.space = self.sharder.view if self.sharder is not None else self.flat
         self.optimizer, self.scheduler = self._build_optimizer()
-        self.clipper = GradClipper(self.space, sharded=self.fsdp is not None)
+        self.clipper = GradClipper(self.space, sharded=self.sharder is not None)
         self.scaler = DeviceGradScaler(self.device, enabled=(cfg.precision == "fp16"))
         self._build_data()
         self.meter = DeviceMeter(self.device)
@@ -246,8 +268,8 @@ class ResNetTrainer:
         prof.mark("grad_sync")
         if self.reducer is not None:
             self.reducer.finish()
-        if self.fsdp is not None:
-            self.fsdp.finish_backward()
+        if self.sharder is not None:
+            self.sharder.finish_backward()
         prof.mark("optimizer")
         fp16 = self.scaler.enabled
         # device-side non-finite check (same kernel as the norm): the optimizer kernels skip
@@ -256,7 +278,7 @@ class ResNetTrainer:
         check = fp16 or guard
         self.clipper(cfg.clip, inv_scale=self.scaler.inv_scale(), check_inf=check)
         found = self.clipper.found_inf if check else None
-        if fp16 or (check and self.fsdp is not None):
+        if fp16 or (check and self.sharder is not None):
             # fp16 / sharded gradients: every rank must take the same decision
             self.scaler.sync_found_inf(self.clipper.found_inf)
         self.optimizer.step(grad_scale=self.clipper.coef, found_inf=found)
@@ -264,8 +286,8 @@ class ResNetTrainer:
             self.scaler.update(found)
         if guard:
             self.skipped += found.reshape(())
-        if self.fsdp is not None:
-            self.fsdp.after_step()
+        if self.sharder is not None:
+            self.sharder.after_step()
         self.meter.update(loss, out.detach(), ya, yb, lam.detach() if isinstance(lam, torch.Tensor) else lam)
         prof.end_step()
         self.global_step += 1
@@ -273,7 +295,7 @@ class ResNetTrainer:
 
     def _sync_buffers(self):
         """Rank 0's BatchNorm running statistics to every rank (one collective)."""
-        if self.world > 1 and (self.fsdp is not None or (self.reducer is not None and self.reducer.broadcast_buffers)):
+        if self.world > 1 and (self.sharder is not None or (self.reducer is not None and self.reducer.broadcast_buffers)):
             pdist.broadcast_buffers(self.model)
 
     def train_epoch(self, epoch):

@@ -59,6 +59,8 @@ class TransformerConfig:
     seed: int = 123456
     faithful: bool = False
     fsdp: bool = False
+    fsdp_offload: bool = False       # FSDP shards + optimizer state in pinned host memory (reference CPUOffload)
+    shard_ngd: bool = True           # distributed NGD: each rank owns + preconditions 1/world of the params
     bucket_mb: float = 8.0
     resume: bool = False
     checkpoint_dir: str = "./checkpoint"
@@ -103,26 +105,38 @@ class TransformerTrainer:
             ckpt.load_model_state(self.model, ckpt.load_checkpoint(self.ckpt_path)["net"])
         shadow = (SHADOW and self.device.type == "cuda" and cfg.precision == "bf16"
                   and not (cfg.distributed and cfg.fsdp))
-        self.flat = FlatParams(self.model, device=self.device, with_shadow=shadow)
-        if shadow:  # bf16 compute reads the optimizer-maintained bf16 copy (no per-step casts)
-            from ..ops.linear import enable_shadow_weights
-            enable_shadow_weights(self.flat)
-        self.reducer = self.fsdp = None
-        if cfg.distributed:
-            if cfg.fsdp:
-                from ..parallel.fsdp import FlatShardedDP
-                self.fsdp = FlatShardedDP(self.flat, self.model)
-            else:
+        ngd_opt = cfg.optimizer == "ngd" or (cfg.optimizer == "auto" and cfg.ngd)
+        self.reducer = self.fsdp = self.zero = None
+        if cfg.distributed and cfg.fsdp:
+            # ZeRO-3 (parallel/fsdp.py): parameters sharded at rest, one wrap unit per
+            # embedding / attention / FFN sublayer / head, gathered with prefetch and
+            # reduce-scattered from gradient hooks; NGD sees whole parameters (Q17)
+            from ..parallel.fsdp import FullyShardedDP
+            self.fsdp = FullyShardedDP(self.model, self.device, mode="param" if ngd_opt else "flat",
+                                       offload=cfg.fsdp_offload)
+            self.flat = self.fsdp.space
+        else:
+            part = self.world if (cfg.distributed and ngd_opt and cfg.shard_ngd) else 0
+            self.flat = FlatParams(self.model, device=self.device, with_shadow=shadow, partition=part)
+            if shadow:  # bf16 compute reads the optimizer-maintained bf16 copy (no per-step casts)
+                from ..ops.linear import enable_shadow_weights
+                enable_shadow_weights(self.flat)
+            if part:
+                # ZeRO-2 for NGD: every rank preconditions only the parameters it owns
+                from ..parallel.zero import ShardedOptimizerDP
+                self.zero = ShardedOptimizerDP(self.flat, self.model)
+            elif cfg.distributed:
                 from ..parallel.ddp import BucketReducer
                 self.reducer = BucketReducer(self.flat, self.model, bucket_mb=cfg.bucket_mb)
+        self.sharder = self.fsdp if self.fsdp is not None else self.zero
         if self.fsdp is None and DIRECT_GRADS:
             from ..ops.linear import enable_direct_grads
             enable_direct_grads(self.model.parameters())
         seed_everything(cfg.seed, self.rank)
-        self.space = self.fsdp.view if self.fsdp is not None else self.flat
+        self.space = self.sharder.view if self.sharder is not None else self.flat
         self._build_data()
         self.optimizer, self.scheduler = self._build_optimizer()
-        self.clipper = GradClipper(self.space, sharded=self.fsdp is not None)
+        self.clipper = GradClipper(self.space, sharded=self.sharder is not None)
         self.scaler = DeviceGradScaler(self.device, enabled=(cfg.precision == "fp16"))
         self.meter = DeviceMeter(self.device)
         self.logger = JsonlLogger(cfg.log_path)
@@ -291,23 +305,23 @@ class TransformerTrainer:
         prof.mark("grad_sync")
         if self.reducer is not None:
             self.reducer.finish()
-        if self.fsdp is not None:
-            self.fsdp.finish_backward()
+        if self.sharder is not None:
+            self.sharder.finish_backward()
         prof.mark("optimizer")
         fp16 = self.scaler.enabled
         guard = cfg.nonfinite_guard and not isinstance(self.optimizer, NGD)  # NGD: host check, fp16 only
         check = fp16 or guard
         self.clipper(cfg.clip, inv_scale=self.scaler.inv_scale(), check_inf=check)
         found = self.clipper.found_inf if check else None
-        if fp16 or (check and self.fsdp is not None):
+        if fp16 or (check and self.sharder is not None):
             self.scaler.sync_found_inf(self.clipper.found_inf)
         self.optimizer.step(grad_scale=self.clipper.coef, found_inf=found)
         if fp16:
             self.scaler.update(found)
         if guard:
             self.skipped += found.reshape(())
-        if self.fsdp is not None:
-            self.fsdp.after_step()
+        if self.sharder is not None:
+            self.sharder.after_step()
         if not cfg.faithful and self.scheduler is not None and isinstance(
                 self.scheduler, torch.optim.lr_scheduler.OneCycleLR):
             if self.scheduler.last_epoch + 1 < self.scheduler.total_steps:

@@ -62,7 +62,8 @@ class FlatParams:
     the buffers are W equal chunks: reduce-scatter / all-gather need no packing (the
     sharded-optimizer data parallel of ``parallel/zero.py``)."""
 
-    def __init__(self, module_or_params, device=None, reverse=True, with_shadow=False, names=None, partition=0):
+    def __init__(self, module_or_params, device=None, reverse=True, with_shadow=False, names=None, partition=0,
+                 dtype=torch.float32):
         if isinstance(module_or_params, nn.Module):
             named = [(n, p) for n, p in module_or_params.named_parameters() if p.requires_grad]
         else:
@@ -92,13 +93,14 @@ class FlatParams:
             self.numel = off
         dev = device if device is not None else (named[0][1].device if named else torch.device("cpu"))
         self.device = torch.device(dev)
-        self.data = torch.zeros(self.numel, device=self.device, dtype=torch.float32)
-        self.grad = torch.zeros(self.numel, device=self.device, dtype=torch.float32)
+        # (dtype: fp32 master weights; fp64 for CPU golden tests)
+        self.data = torch.zeros(self.numel, device=self.device, dtype=dtype)
+        self.grad = torch.zeros(self.numel, device=self.device, dtype=dtype)
         self.shadow = torch.zeros(self.numel, device=self.device, dtype=torch.bfloat16) if with_shadow else None
         with torch.no_grad():
             for s in self.slots:
                 v = self.data[s.offset:s.offset + s.numel].view(s.shape)
-                v.copy_(s.param.data.to(self.device, torch.float32))
+                v.copy_(s.param.data.to(self.device, dtype))
                 s.param.data = v
                 s.param.grad = self.grad[s.offset:s.offset + s.numel].view(s.shape)
         self.refresh_shadow()

@@ -15,7 +15,7 @@ def free_port() -> int:
         return s.getsockname()[1]
 
 
-def _entry(rank, world, port, fn, args, errq, native=False):
+def _entry(rank, world, port, fn, args, errq, native=False, backend="gloo"):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     os.environ["RANK"] = str(rank)
@@ -24,7 +24,13 @@ def _entry(rank, world, port, fn, args, errq, native=False):
     os.environ["FDT_NATIVE"] = "1" if native else "0"
     try:
         import torch.distributed as dist
-        dist.init_process_group("gloo", rank=rank, world_size=world)
+        if backend == "nccl":  # RCCL: one process per device; bind it before the group exists
+            import torch
+            os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+            torch.cuda.set_device(rank)
+            dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", rank))
+        else:
+            dist.init_process_group("gloo", rank=rank, world_size=world)
         try:
             fn(rank, world, *args)
         finally:
@@ -34,13 +40,15 @@ def _entry(rank, world, port, fn, args, errq, native=False):
         sys.exit(1)
 
 
-def run_world(fn, world=2, args=(), timeout=240, native=False):
+def run_world(fn, world=2, args=(), timeout=240, native=False, backend="gloo"):
     """Spawn ``world`` ranks (gloo).  native=True keeps the HIP fast path on (GPU tests:
-    every rank shares cuda:0 -- gloo, unlike RCCL, allows several ranks per device)."""
+    every rank shares cuda:0 -- gloo, unlike RCCL, allows several ranks per device);
+    backend="nccl" runs RCCL (one rank per GPU: world 1 on the single-GPU test box)."""
     ctx = mp.get_context("spawn")
     errq = ctx.SimpleQueue()
     port = free_port()
-    procs = [ctx.Process(target=_entry, args=(r, world, port, fn, args, errq, native)) for r in range(world)]
+    procs = [ctx.Process(target=_entry, args=(r, world, port, fn, args, errq, native, backend))
+             for r in range(world)]
     for p in procs:
         p.start()
     for p in procs:

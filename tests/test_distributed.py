@@ -51,13 +51,15 @@ def test_bucket_reducer_averages_gradients(world):
     run_world(_ddp_worker, world=world, args=(0.0005,))
 
 
-def _fsdp_worker(rank, world):
+def _zero_worker(rank, world):
+    """ZeRO-2 (parallel/zero.py): per-rank optimizer over whole owned parameters, reduce-
+    scatter of gradients, all-gather of parameters == single-process training."""
     from faster_distributed_training_amd.optim.flat_optim import SGD, GradClipper
-    from faster_distributed_training_amd.parallel.fsdp import FlatShardedDP
+    from faster_distributed_training_amd.parallel.zero import ShardedOptimizerDP
     from faster_distributed_training_amd.utils.flat import FlatParams
     m = _model(seed=rank)
-    flat = FlatParams(m)
-    fs = FlatShardedDP(flat, m)
+    flat = FlatParams(m, partition=world)
+    fs = ShardedOptimizerDP(flat, m)
     opt = SGD(fs.view, lr=0.1, momentum=0.9)
     clip = GradClipper(fs.view, sharded=True)
     ref = _model(seed=0)
@@ -79,8 +81,143 @@ def _fsdp_worker(rank, world):
 
 
 @pytest.mark.parametrize("world", [2, 3])
-def test_flat_sharded_dp_matches_single_process(world):
-    run_world(_fsdp_worker, world=world)
+def test_sharded_optimizer_dp_matches_single_process(world):
+    run_world(_zero_worker, world=world)
+
+
+def _ngd_model(seed=0):
+    torch.manual_seed(seed)
+    return nn.Sequential(nn.Linear(12, 20), nn.Tanh(), nn.Linear(20, 16), nn.Tanh(), nn.Linear(16, 5))
+
+
+def _sharded_ngd_worker(rank, world, steps):
+    """Sharded NGD: each rank preconditions + updates only the parameters it
+    owns; over ``steps`` steps (init schedule, every-step updates for the first 10 calls, then
+    every update_period-th) the result equals single-process NGD on the averaged gradient,
+    and each rank holds preconditioner state only for its own parameters.  fp64: NGD's
+    eigen-normalisation of near-degenerate early Fisher estimates amplifies 1-ulp
+    differences of the gradient summation order (single-process, summing the same three
+    gradients in another order: fp32 2e-4 after one step; fp64 3e-7 after three steps,
+    then bounded at ~4e-6 over 20), so the check is fp64 with a 2e-5 bound -- a sharding
+    error (a parameter preconditioned on the wrong gradient / axis) is O(1e-2)."""
+    from faster_distributed_training_amd.optim.ngd import NGD
+    from faster_distributed_training_amd.parallel.zero import ShardedOptimizerDP
+    from faster_distributed_training_amd.utils.flat import FlatParams
+    m = _ngd_model(seed=rank).double()
+    flat = FlatParams(m, partition=world, dtype=torch.float64)
+    fs = ShardedOptimizerDP(flat, m)
+    opt = NGD(fs.view, lr=0.05, momentum=0.9, weight_decay=1e-4)
+    ref = _ngd_model(seed=0).double()
+    rflat = FlatParams(ref, dtype=torch.float64)
+    ropt = NGD(rflat, lr=0.05, momentum=0.9, weight_decay=1e-4)
+    for step in range(steps):
+        g = torch.Generator().manual_seed(500 + step)
+        xs = [torch.randn(6, 12, generator=g, dtype=torch.float64) for _ in range(world)]
+        ys = [torch.randint(0, 5, (6,), generator=g) for _ in range(world)]
+        F.cross_entropy(m(xs[rank]), ys[rank]).backward()
+        fs.finish_backward()
+        opt.step()
+        fs.after_step()
+        (sum(F.cross_entropy(ref(xs[r]), ys[r]) for r in range(world)) / world).backward()
+        ropt.step()
+        for p, q in zip(m.parameters(), ref.parameters()):
+            assert torch.allclose(p, q, atol=2e-5, rtol=0), (step, (p - q).abs().max())
+    mine = sum(len(sg.axes) for sg, _ in opt.groups)
+    total = sum(len(sg.axes) for sg, _ in ropt.groups)
+    counts = [None] * world
+    dist.all_gather_object(counts, mine)
+    assert sum(counts) == total and max(counts) < total, counts
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_ngd_matches_single_process(world):
+    run_world(_sharded_ngd_worker, world=world, args=(20,))
+
+
+def _units_model(seed=0):
+    torch.manual_seed(seed)
+    dims = [10, 32, 48, 40, 48, 32, 40, 24, 4]
+    layers = []
+    for a, b in zip(dims[:-1], dims[1:]):
+        layers += [nn.Linear(a, b), nn.ReLU()]
+    return nn.Sequential(*layers[:-1])
+
+
+def _fsdp_worker(rank, world, mode, offload):
+    """FSDP full-shard (ZeRO-3, parallel/fsdp.py): parameters sharded at rest and gathered
+    per unit (prefetch), per-unit reduce-scatter from gradient hooks == single-process
+    training; between steps only 1/world of the parameters is resident."""
+    from faster_distributed_training_amd.optim.flat_optim import MADGRAD, GradClipper
+    from faster_distributed_training_amd.parallel.fsdp import FullyShardedDP
+    m = _units_model(seed=rank)
+    units = [(str(i), m[i]) for i in range(0, len(m), 2)]
+    fs = FullyShardedDP(m, torch.device("cpu"), units=units, mode=mode, offload=offload)
+    full_bytes = sum(p.numel() for p in _units_model().parameters()) * 4
+    assert fs.resident_param_bytes() == 0
+    assert fs.space.numel * world >= sum(p.numel() for p in _units_model().parameters())
+    opt = MADGRAD(fs.space, lr=0.01, momentum=0.9)
+    clip = GradClipper(fs.space, sharded=True)
+    ref = _units_model(seed=0)
+    from faster_distributed_training_amd.utils.flat import FlatParams
+    rflat = FlatParams(ref)
+    ropt = MADGRAD(rflat, lr=0.01, momentum=0.9)
+    rclip = GradClipper(rflat)
+    for step in range(4):
+        x, y = _batch(rank + 10 * step)
+        F.cross_entropy(m(x), y).backward()
+        fs.finish_backward()
+        clip(1.0)
+        opt.step(grad_scale=clip.coef)
+        fs.after_step()
+        assert fs.resident_param_bytes() == 0  # resharded at rest
+        loss = sum(F.cross_entropy(ref(_batch(r + 10 * step)[0]), _batch(r + 10 * step)[1]) for r in range(world))
+        (loss / world).backward()
+        rclip(1.0)
+        ropt.step(grad_scale=rclip.coef)
+    sd = fs.full_state_dict()
+    for k, v in ref.state_dict().items():
+        assert torch.allclose(sd[k], v, atol=1e-5), (k, (sd[k] - v).abs().max())
+    # per-unit schedule: at no point are all units' parameters + gradients materialised
+    assert fs.peak_full_bytes < 0.6 * sum(2 * u._bytes() for u in fs.units), (fs.peak_full_bytes, full_bytes)
+
+
+@pytest.mark.parametrize("world,mode,offload", [(2, "flat", False), (3, "flat", False), (2, "param", False),
+                                                (3, "param", True)])
+def test_fsdp_full_shard_matches_single_process(world, mode, offload):
+    run_world(_fsdp_worker, world=world, args=(mode, offload))
+
+
+def _fsdp_ngd_worker(rank, world):
+    """FSDP + NGD (the reference's distributed transformer run, transformer_test.py:216-217,
+    387-392): with whole-parameter shards NGD preconditions correctly shaped parameters (Q17)
+    and matches single-process NGD."""
+    from faster_distributed_training_amd.optim.ngd import NGD
+    from faster_distributed_training_amd.parallel.fsdp import FullyShardedDP
+    from faster_distributed_training_amd.utils.flat import FlatParams
+    m = _ngd_model(seed=rank)
+    fs = FullyShardedDP(m, torch.device("cpu"), units=[("0", m[0]), ("2", m[2]), ("4", m[4])], mode="param")
+    opt = NGD(fs.space, lr=0.05, momentum=0.9)
+    ref = _ngd_model(seed=0)
+    ropt = NGD(FlatParams(ref), lr=0.05, momentum=0.9)
+    for step in range(12):
+        g = torch.Generator().manual_seed(900 + step)
+        xs = [torch.randn(6, 12, generator=g) for _ in range(world)]
+        ys = [torch.randint(0, 5, (6,), generator=g) for _ in range(world)]
+        F.cross_entropy(m(xs[rank]), ys[rank]).backward()
+        fs.finish_backward()
+        opt.step()
+        fs.after_step()
+        (sum(F.cross_entropy(ref(xs[r]), ys[r]) for r in range(world)) / world).backward()
+        ropt.step()
+    sd = fs.full_state_dict()
+    for k, v in ref.state_dict().items():
+        assert torch.allclose(sd[k], v, atol=2e-5, rtol=1e-4), (k, (sd[k] - v).abs().max())
+    for s in opt.flat.slots:  # whole, correctly shaped parameters only
+        assert tuple(s.shape) == tuple(s.param.shape) and s.numel == s.param.numel()
+
+
+def test_fsdp_ngd_whole_parameter_shards(tmp_path):
+    run_world(_fsdp_ngd_worker, world=2)
 
 
 def _metrics_ckpt_worker(rank, world, path):
@@ -169,3 +306,36 @@ def _resume_rank_state_worker(rank, world, tmp):
 
 def test_auto_resume_restores_each_ranks_state(tmp_path):
     run_world(_resume_rank_state_worker, world=2, args=(str(tmp_path),))
+
+
+def _trainer_fsdp_vs_ddp_worker(rank, world, tmp, model):
+    """Trainer level: --fsdp (full shard, per-unit schedule) ends with the same parameters as
+    DDP on the same data (both average the per-rank gradients).  fp32 compute: under bf16
+    autocast a 1e-7 fp32 difference of the reduction order flips bf16 roundings, which
+    MADGRAD's normalised updates turn into ~1e-3 parameter differences after two steps."""
+    os.chdir(tmp)
+    if model == "resnet":
+        from faster_distributed_training_amd.train.resnet_trainer import ResNetConfig as C, ResNetTrainer as T
+        base = dict(arch="resnet18", bs=4, synthetic=True, epoch=1, steps_per_epoch=2, eval=False, plot=False,
+                    distributed=True, optimizer="madgrad", precision="fp32", extra={"subset_stride": 100})
+    else:
+        from faster_distributed_training_amd.train.transformer_trainer import TransformerConfig as C
+        from faster_distributed_training_amd.train.transformer_trainer import TransformerTrainer as T
+        base = dict(batch_size=4, epoch=1, synthetic=True, eval=False, plot=False, steps_per_epoch=2, n_layers=2,
+                    d_model=64, heads=4, d_ff=128, d_hidden=128, length_buckets=(32,), distributed=True,
+                    optimizer="mirror_madgrad", precision="fp32",
+                    extra={"subset_stride": 200, "scheduler": "multistep"})
+    a = T(C(**base)).fit()
+    sd_a = {k: v.clone() for k, v in a.model.state_dict().items()}
+    b = T(C(fsdp=True, **base))
+    assert b.fsdp is not None and b.fsdp.resident_param_bytes() == 0
+    b.fit()
+    sd_b = b.fsdp.full_state_dict()
+    for k, v in sd_a.items():
+        if v.dtype.is_floating_point:
+            assert torch.allclose(sd_b[k], v, atol=1e-4, rtol=1e-4), (k, (sd_b[k] - v).abs().max())
+
+
+@pytest.mark.parametrize("model", ["resnet", "transformer"])
+def test_trainer_fsdp_matches_ddp(tmp_path, model):
+    run_world(_trainer_fsdp_vs_ddp_worker, world=2, args=(str(tmp_path), model), timeout=600)

@@ -100,3 +100,132 @@ def _graph_worker(rank, world):
 
 def test_ddp_engine_hip_graphs_two_ranks(cuda):
     run_world(_graph_worker, world=2, native=True, timeout=400)
+
+
+def _fsdp_engine_worker(rank, world):
+    """FSDP full-shard driving the fused ResNet engine stage by stage (gather + per-stage
+    weight packing before each stage's forward and backward, reduce-scatter at each stage
+    boundary): every rank's shard gradient equals its chunk of the average of the per-rank
+    gradients of an unsharded engine model; nothing is gathered between steps."""
+    import torch.distributed as dist
+    from faster_distributed_training_amd.models import resnet as R
+    from faster_distributed_training_amd.ops.resnet_fused import STAGES
+    from faster_distributed_training_amd.parallel.fsdp import FullyShardedDP
+    from faster_distributed_training_amd.utils.flat import FlatParams
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    torch.manual_seed(0)
+    ref = R.resnet50(10).to(dev)
+    ref.fast_path = True
+    torch.manual_seed(rank)
+    m = R.resnet50(10).to(dev)
+    m.fast_path = True
+    fs = FullyShardedDP(m, dev, engine_units=("conv1",) + STAGES)  # broadcasts rank 0's weights
+    m._fsdp = fs
+    ref.load_state_dict(fs.full_state_dict())
+    rflat = FlatParams(ref, device=dev)
+    x, y = _batch(rank)
+    for it in range(2):
+        rflat.grad.zero_()
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            out = m(x.to(dev))
+            rout = ref(x.to(dev))
+        F.cross_entropy(out.float(), y.to(dev)).backward()
+        F.cross_entropy(rout.float(), y.to(dev)).backward()
+        fs.finish_backward()
+        g = rflat.grad.clone()
+        dist.all_reduce(g)
+        g /= world
+        rslots = {s.name: s for s in rflat.slots}
+        for u in fs.units:
+            full = torch.zeros(u.numel, device=dev)
+            for i, (n, p) in enumerate(u.params):
+                s = rslots[n]
+                full[u.pos[i]:u.pos[i] + p.numel()] = g[s.offset:s.offset + s.numel]
+            mine = full[rank * u.chunk:(rank + 1) * u.chunk]
+            got = fs.shard_grad[u.shard_off:u.shard_off + u.chunk]
+            err = ((got - mine).norm() / (mine.norm() + 1e-12)).item()
+            assert err < 2e-2, (it, u.name, err)
+        fs.space.grad.zero_()
+        fs.after_step()
+        assert fs.resident_param_bytes() == 0
+    assert fs.peak_full_bytes < 0.75 * sum(2 * u._bytes() for u in fs.units)
+
+
+def test_fsdp_engine_two_ranks_one_gpu(cuda):
+    run_world(_fsdp_engine_worker, world=2, native=True, timeout=400)
+
+
+def _rccl_worker(rank, world):
+    """The RCCL (backend nccl) code paths at world size 1 on the single-GPU box: AVG bucket
+    all-reduces launched from the engine's hooks and between captured HIP-graph segments,
+    the bf16 wire format, barrier(device_ids), the sharded-optimizer reduce-scatter /
+    all-gather and FSDP's per-unit collectives -- same gradients as no communication."""
+    import torch.distributed as dist
+    from faster_distributed_training_amd.models import resnet as R
+    from faster_distributed_training_amd.optim.flat_optim import SGD
+    from faster_distributed_training_amd.parallel import dist as pdist
+    from faster_distributed_training_amd.parallel.ddp import BucketReducer
+    from faster_distributed_training_amd.parallel.fsdp import FullyShardedDP
+    from faster_distributed_training_amd.parallel.zero import ShardedOptimizerDP
+    from faster_distributed_training_amd.utils.flat import FlatParams
+    assert dist.get_backend() == "nccl"
+    dev = torch.device("cuda", 0)
+    x, y = _batch(0)
+    x, y = x.to(dev), y.to(dev)
+
+    def grads(model, flat):
+        flat.grad.zero_()
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            out = model(x)
+        F.cross_entropy(out.float(), y).backward()
+
+    torch.manual_seed(0)
+    base = R.resnet18(10).to(dev)
+    base.fast_path = True
+    bflat = FlatParams(base, device=dev)
+    grads(base, bflat)
+    g0 = bflat.grad.clone()
+    for cdt, graphs in ((None, False), (torch.bfloat16, False), (None, True)):
+        torch.manual_seed(0)
+        m = R.resnet18(10).to(dev)
+        m.fast_path = True
+        m.graph_engine = graphs
+        flat = FlatParams(m, device=dev)
+        red = BucketReducer(flat, m, bucket_mb=1.0, first_bucket_mb=0.25, comm_dtype=cdt)
+        assert red.use_avg  # ReduceOp.AVG on RCCL
+        for it in range(3 if graphs else 1):
+            grads(m, flat)
+            assert all(w is not None for w in red.works)
+            red.finish()
+        err = ((flat.grad - g0).norm() / g0.norm()).item()
+        assert err < (1e-2 if cdt is not None else 5e-3), (cdt, graphs, err)
+        red.remove()
+    pdist.barrier()  # dist.barrier(device_ids=[...]) on RCCL
+    # sharded optimizer (ZeRO-2) and FSDP full-shard over RCCL
+    torch.manual_seed(0)
+    m = R.resnet18(10).to(dev)
+    m.fast_path = True
+    flat = FlatParams(m, device=dev, partition=1)
+    zero = ShardedOptimizerDP(flat, m)
+    grads(m, flat)
+    zero.finish_backward()
+    assert ((flat.grad - g0).norm() / g0.norm()).item() < 5e-3
+    opt = SGD(zero.view, lr=0.1)
+    opt.step()
+    zero.after_step()
+    torch.manual_seed(0)
+    m2 = R.resnet18(10).to(dev)
+    m2.fast_path = True
+    from faster_distributed_training_amd.ops.resnet_fused import STAGES
+    fs = FullyShardedDP(m2, dev, engine_units=("conv1",) + STAGES)
+    m2._fsdp = fs
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        out = m2(x)
+    F.cross_entropy(out.float(), y).backward()
+    fs.finish_backward()
+    assert torch.isfinite(fs.shard_grad).all() and fs.resident_param_bytes() == 0
+
+
+def test_rccl_world1_code_paths(cuda):
+    run_world(_rccl_worker, world=1, native=True, backend="nccl", timeout=400)
