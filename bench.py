@@ -47,6 +47,7 @@ def parse():
     ap.add_argument("--no-native", action="store_true", help="ablation: plain PyTorch ops (w/o tricks)")
     ap.add_argument("--profile-steps", type=int, default=0)
     ap.add_argument("--no-graphs", action="store_true", help="ablation: launch the engine's kernels eagerly")
+    ap.add_argument("--deterministic", action="store_true", help="bitwise-repeatable engine reductions (cost probe)")
     ap.add_argument("--model", default="resnet50", choices=["resnet50", "transformer"],
                     help="transformer: secondary benchmark (BASELINE.json config 4, AG-News-shaped)")
     ap.add_argument("--seq-bucket", type=int, default=128, help="transformer: padded sequence length")
@@ -74,7 +75,8 @@ def main():
                        distributed=n > 1, ngd=args.ngd, meta_learning=args.meta_learning,
                        optimizer="ngd" if args.ngd else args.optimizer, fsdp=args.fsdp,
                        precision=args.precision, bucket_mb=args.bucket_mb, comm_dtype=args.comm_dtype,
-                       fast_path=False if args.no_native else None, graphs=not args.no_graphs)
+                       fast_path=False if args.no_native else None, graphs=not args.no_graphs,
+                       deterministic=args.deterministic)
     tr = ResNetTrainer(cfg)
     dev = tr.device
     cuda = dev.type == "cuda"
@@ -133,7 +135,7 @@ def main():
         "config": {"model": f"{args.arch} (CIFAR stem, 10 classes)", "global_batch": gb, "seq_len": None,
                    "image_size": 32, "parallelism": f"{'fsdp' if args.fsdp else 'dp'}{n}",
                    "optimizer": "ngd" if args.ngd else args.optimizer, "mixup": "meta" if args.meta_learning else "input",
-                   "native_kernels": native, "hip_graphs": graphs},
+                   "native_kernels": native, "hip_graphs": graphs, "deterministic": args.deterministic},
         "epoch_time_s": round(50000.0 / value, 3),
         "peak_mem_gb": round(torch.cuda.max_memory_allocated() / 2**30, 2) if cuda else None,
     }

@@ -15,8 +15,8 @@ void channel_stats_partial(uint64_t y, uint64_t part, long M, int C, int dt, uin
 void stats_finalize(uint64_t part, int nb, int C, double count, int mode, float eps, float momentum, uint64_t gamma,
                     uint64_t beta, uint64_t run_mean, uint64_t run_var, uint64_t nbt, uint64_t out_s, uint64_t out_t,
                     uint64_t save_mean, uint64_t save_aux, int zero_after, uint64_t stream);
-void act_bwd_reduce(uint64_t g, uint64_t x, uint64_t s, uint64_t t, uint64_t gx, uint64_t part, long M, int C, int act,
-                    float alpha, int dt, uint64_t stream);
+void act_bwd_reduce(uint64_t g, uint64_t x, uint64_t s, uint64_t t, uint64_t gx, uint64_t part, int part_rows, long M,
+                    int C, int act, float alpha, int dt, uint64_t stream);
 void reduce_partials(uint64_t part, int nb, int nq, int C, uint64_t out, int zero_after, uint64_t stream);
 int partials_compact(uint64_t part, int nb, int W, int R, uint64_t out, uint64_t stream);
 void stats_bwd_coef(uint64_t gs, uint64_t gt, int C, double count, int mode, float eps, uint64_t save_mean,
@@ -32,7 +32,10 @@ void affine_fold(uint64_t gy, uint64_t y, uint64_t alpha, uint64_t beta, uint64_
 void residual_act_fwd(uint64_t ya, uint64_t sa, uint64_t ta, uint64_t yb, uint64_t sb, uint64_t tb, uint64_t xid,
                       uint64_t out, uint64_t mask, long M, int C, int act, float alpha, int dt, uint64_t stream);
 void residual_act_bwd(uint64_t g, uint64_t out, uint64_t mask, uint64_t ya, uint64_t yb, uint64_t gpre, uint64_t part,
-                      long M, int C, int act, float alpha, int dt, uint64_t stream);
+                      int part_rows, long M, int C, int act, float alpha, int dt, uint64_t stream);
+// deterministic mode (common.h): no-wrap statistics slots, ordered split-K sums
+void set_deterministic_mode(bool on);
+bool deterministic_mode();
 // optim.hip
 void grad_sumsq(uint64_t g, long n, uint64_t inv_scale, int unscale, uint64_t part, int nb, uint64_t found_inf,
                 uint64_t stream);
@@ -78,7 +81,7 @@ void augment(uint64_t src, uint64_t idx, uint64_t labels_src, uint64_t labels_ou
 void rng_advance(uint64_t rng, uint64_t stream);
 // conv_igemm.hip
 void conv_igemm(uint64_t x, uint64_t x2, uint64_t ps, uint64_t pt, uint64_t pg, uint64_t w, uint64_t out, uint64_t part,
-                uint64_t ex, uint64_t es, uint64_t et, uint64_t jmask, uint64_t jyb, uint64_t jout, long Nb, int Hi,
+                int part_rows, uint64_t ex, uint64_t es, uint64_t et, uint64_t jmask, uint64_t jyb, uint64_t jout, long Nb, int Hi,
                 int Wi, int Cx, int Ho, int Wo, int S, const std::vector<int>& dh, const std::vector<int>& dw,
                 const std::vector<int>& wt, int Cout, int ldw, int Hout, int Wout, int OS, int oy, int ox, int pro,
                 int pro_act, float pro_alpha, int epi, int epi_act, float epi_alpha, int BM, int BN, int BK, int nsplit,

@@ -28,6 +28,8 @@ PYBIND11_MODULE(_fdt_native, m) {
   DEF(affine_fold);
   DEF(residual_act_fwd);
   DEF(residual_act_bwd);
+  DEF(set_deterministic_mode);
+  DEF(deterministic_mode);
   // implicit-GEMM convolution engine
   DEF(conv_igemm);
   DEF(conv_num_row_blocks);

@@ -166,8 +166,9 @@ __global__ __launch_bounds__(64 * kRedWaves) void stats_finalize_kernel(float* _
 template <typename T>
 __global__ __launch_bounds__(kBlk) void act_bwd_reduce_kernel(const T* __restrict__ g, const T* __restrict__ x,
                                                               const float* __restrict__ s, const float* __restrict__ t,
-                                                              T* __restrict__ gx, float* __restrict__ part, long M, int C,
-                                                              int TPR, int RPP, long rows_per_blk, int act, float alpha) {
+                                                              T* __restrict__ gx, float* __restrict__ part,
+                                                              unsigned slot_mask, long M, int C, int TPR, int RPP,
+                                                              long rows_per_blk, int act, float alpha) {
   __shared__ float sm[kBlk * 16];
   const int tid = threadIdx.x;
   const int gi = tid % TPR, rr = tid / TPR;
@@ -201,7 +202,7 @@ __global__ __launch_bounds__(kBlk) void act_bwd_reduce_kernel(const T* __restric
     float acc = 0.f;
     for (int q = 0; q < RPP; ++q) acc += sm[(q * TPR + gg) * 16 + i];
     int c = (blockIdx.y * TPR + gg) * 8 + (i & 7);
-    atomicAdd(&part[((long)(blockIdx.x & (kStatSlots - 1)) * 2 + (i >> 3)) * C + c], acc);
+    atomicAdd(&part[((long)(blockIdx.x & slot_mask) * 2 + (i >> 3)) * C + c], acc);
   }
 }
 
@@ -441,9 +442,9 @@ template <typename T>
 __global__ __launch_bounds__(kBlk) void residual_act_bwd_kernel(const T* __restrict__ g, const T* __restrict__ out,
                                                                 const uint8_t* __restrict__ mask,
                                                                 const T* __restrict__ ya, const T* __restrict__ yb,
-                                                                T* __restrict__ gpre, float* __restrict__ part, long M,
-                                                                int C, int TPR, int RPP, long rows_per_blk, int act,
-                                                                float alpha) {
+                                                                T* __restrict__ gpre, float* __restrict__ part,
+                                                                unsigned slot_mask, long M, int C, int TPR, int RPP,
+                                                                long rows_per_blk, int act, float alpha) {
   __shared__ float sm[kBlk * 24];
   const int tid = threadIdx.x;
   const int gi = tid % TPR, rr = tid / TPR;
@@ -501,7 +502,7 @@ __global__ __launch_bounds__(kBlk) void residual_act_bwd_kernel(const T* __restr
     float acc = 0.f;
     for (int q = 0; q < RPP; ++q) acc += sm[(q * TPR + gg) * 24 + i];
     int c = (blockIdx.y * TPR + gg) * 8 + (i & 7);
-    atomicAdd(&part[((long)(blockIdx.x & (kStatSlots - 1)) * 3 + (i >> 3)) * C + c], acc);
+    atomicAdd(&part[((long)(blockIdx.x & slot_mask) * 3 + (i >> 3)) * C + c], acc);
   }
 }
 
@@ -576,15 +577,26 @@ void stats_finalize(uint64_t part, int nb, int C, double count, int mode, float 
   FDT_LAUNCH_CHECK();
 }
 
-void act_bwd_reduce(uint64_t g, uint64_t x, uint64_t s, uint64_t t, uint64_t gx, uint64_t part, long M, int C, int act,
-                    float alpha, int dt, uint64_t stream) {
+void set_deterministic_mode(bool on) { set_deterministic(on); }
+bool deterministic_mode() { return deterministic(); }
+
+// deterministic mode: at most `rows` blocks along the slot axis (one slot row per block)
+static long cap_rows_per_block(long M, long r, const ChanGeom& g, int rows) {
+  if (!deterministic() || (M + r - 1) / r <= rows) return r;
+  r = (M + rows - 1) / rows;
+  return (r + g.RPP - 1) / g.RPP * g.RPP;
+}
+
+void act_bwd_reduce(uint64_t g, uint64_t x, uint64_t s, uint64_t t, uint64_t gx, uint64_t part, int part_rows, long M,
+                    int C, int act, float alpha, int dt, uint64_t stream) {
   ChanGeom gg = chan_geom(C);
-  long r = rows_per_block(M, gg);
+  long r = cap_rows_per_block(M, rows_per_block(M, gg), gg, part_rows);
   dim3 grid((unsigned)((M + r - 1) / r), gg.gy);
+  const unsigned mask = stat_slot_mask(part_rows, grid.x);
   DISPATCH_T(dt, {
     act_bwd_reduce_kernel<T><<<grid, kBlk, 0, as_stream(stream)>>>(P<const T>(g), P<const T>(x), P<const float>(s),
-                                                                  P<const float>(t), P<T>(gx), P<float>(part), M, C,
-                                                                  gg.TPR, gg.RPP, r, act, alpha);
+                                                                  P<const float>(t), P<T>(gx), P<float>(part), mask, M,
+                                                                  C, gg.TPR, gg.RPP, r, act, alpha);
   });
   FDT_LAUNCH_CHECK();
 }
@@ -683,7 +695,7 @@ void residual_act_fwd(uint64_t ya, uint64_t sa, uint64_t ta, uint64_t yb, uint64
 }
 
 void residual_act_bwd(uint64_t g, uint64_t out, uint64_t mask, uint64_t ya, uint64_t yb, uint64_t gpre, uint64_t part,
-                      long M, int C, int act, float alpha, int dt, uint64_t stream) {
+                      int part_rows, long M, int C, int act, float alpha, int dt, uint64_t stream) {
   FDT_CHECK(out != 0 || mask != 0, "residual_act_bwd needs the output or its mask");
   ChanGeom gg = chan_geom(C);
   // ~1024 blocks: more waves in flight for this 4-5 stream kernel than the stats default
@@ -692,11 +704,13 @@ void residual_act_bwd(uint64_t g, uint64_t out, uint64_t mask, uint64_t ya, uint
   long r = (M + target - 1) / target;
   if (r < gg.RPP) r = gg.RPP;
   r = (r + gg.RPP - 1) / gg.RPP * gg.RPP;
+  r = cap_rows_per_block(M, r, gg, part_rows);
   dim3 grid((unsigned)((M + r - 1) / r), gg.gy);
+  const unsigned smask = stat_slot_mask(part_rows, grid.x);
   DISPATCH_T(dt, {
     residual_act_bwd_kernel<T><<<grid, kBlk, 0, as_stream(stream)>>>(
         P<const T>(g), P<const T>(out), P<const uint8_t>(mask), P<const T>(ya), P<const T>(yb), P<T>(gpre), P<float>(part),
-        M, C, gg.TPR, gg.RPP, r, act, alpha);
+        smask, M, C, gg.TPR, gg.RPP, r, act, alpha);
   });
   FDT_LAUNCH_CHECK();
 }

@@ -108,6 +108,25 @@ template <> struct Vec8<float> {
 // re-zeroes them.  Replaces per-workgroup slabs + a compaction pass.
 constexpr int kStatSlots = 64;
 
+// Deterministic mode (--deterministic): every statistics producer writes slot = its block
+// index WITHOUT wrapping (the Python side sizes the slot buffer to >= the block count), so
+// each slot address has exactly one writer and the fp32 atomic add onto a zeroed slot is
+// exact; the fp64 finalize then sums the rows in a fixed order.  Split-K reducers sum every
+// split's partials in split order.  Result: bitwise-repeatable steps.
+inline int& deterministic_flag() {
+  static int f = 0;
+  return f;
+}
+inline void set_deterministic(bool on) { deterministic_flag() = on ? 1 : 0; }
+inline bool deterministic() { return deterministic_flag() != 0; }
+// slot index mask for a launch whose slot buffer holds `rows` rows (nblocks: the launch's
+// block count along the slot axis)
+inline unsigned stat_slot_mask(int rows, long nblocks) {
+  if (!deterministic()) return (unsigned)(kStatSlots - 1);
+  FDT_CHECK(nblocks <= rows, "deterministic mode: statistics slot buffer smaller than the block count");
+  return 0xFFFFFFFFu;
+}
+
 // ---------------------------------------------------------------- wave reductions
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll

@@ -70,7 +70,9 @@ struct ConvArgs {
   const float* pg;   // FOLD: per-channel scale of g (nullptr = 1): g*pg + alpha + beta*y    [Cx]
   const bf16* w;     // packed weights [Cout][ldw], k-index = wt[tap]*Cx + ci
   bf16* out;         // [Nb][Hout][Wout][Cout]
-  float* part;       // statistics slots [kStatSlots][2][Cout], fp32 atomics (zeroed by the consumer)
+  float* part;       // statistics slots [slots][NQ][Cout], fp32 atomics (zeroed by the consumer)
+  unsigned slot_mask;  // slot = row block & slot_mask (deterministic mode: no wrap, one writer per slot)
+  int det;             // deterministic mode: the split-K reducer sums every split in split order
   const bf16* ex;    // ACTBWD: producer raw output x (shape of out); JOINBWD: residual-branch y
   const float* es;   // ACTBWD: producer scale s [Cout]
   const float* et;   // ACTBWD: producer shift t [Cout]
@@ -441,8 +443,17 @@ __global__ __launch_bounds__(256) void igemm_kernel(const ConvArgs a) {
     const int last = flag[0];
     __syncthreads();  // red is reused by the epilogue
     if (!last) return;
+    if (a.det) {
+      // fixed summation order whichever split arrived last (its own slab was written too)
+#pragma unroll
+      for (int i = 0; i < TN; ++i)
+#pragma unroll
+        for (int j = 0; j < TM; ++j)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+    }
     for (int sp = 0; sp < a.nsplit; ++sp) {
-      if (sp == split) continue;
+      if (sp == split && !a.det) continue;
       const float4* other = slab + (long)sp * NR4 * 256 + tid;
 #pragma unroll
       for (int i = 0; i < TN; ++i)
@@ -605,7 +616,7 @@ __global__ __launch_bounds__(256) void igemm_kernel(const ConvArgs a) {
       for (int e = tid; e < NQ * BN; e += 256) {
         const float t = red[e] + red[NQ * BN + e] + red[2 * NQ * BN + e] + red[3 * NQ * BN + e];
         const int q = e / BN, cc2 = e - q * BN;
-        atomicAdd(&a.part[((long)(bm & (kStatSlots - 1)) * NQ + q) * a.Cout + n0 + cc2], t);
+        atomicAdd(&a.part[((long)(bm & a.slot_mask) * NQ + q) * a.Cout + n0 + cc2], t);
       }
     }
   }
@@ -656,7 +667,7 @@ static void launch_tile(const ConvArgs& a, int BM, int BN, int BK, bool pure, hi
 
 // Python-facing launcher.  taps: list of (dh, dw, wt) triples encoded as int8 arrays.
 void conv_igemm(uint64_t x, uint64_t x2, uint64_t ps, uint64_t pt, uint64_t pg, uint64_t w, uint64_t out, uint64_t part,
-                uint64_t ex, uint64_t es, uint64_t et, uint64_t jmask, uint64_t jyb, uint64_t jout, long Nb, int Hi,
+                int part_rows, uint64_t ex, uint64_t es, uint64_t et, uint64_t jmask, uint64_t jyb, uint64_t jout, long Nb, int Hi,
                 int Wi, int Cx, int Ho, int Wo, int S,
                 const std::vector<int>& dh, const std::vector<int>& dw, const std::vector<int>& wt, int Cout, int ldw,
                 int Hout, int Wout, int OS, int oy, int ox, int pro, int pro_act, float pro_alpha, int epi, int epi_act,
@@ -706,6 +717,8 @@ void conv_igemm(uint64_t x, uint64_t x2, uint64_t ps, uint64_t pt, uint64_t pg, 
             "conv operand exceeds the 2 GiB buffer-descriptor range");
   a.nbm = (int)((a.M + BM - 1) / BM);
   a.nbn = Cout / BN;
+  a.det = deterministic() ? 1 : 0;
+  a.slot_mask = part ? stat_slot_mask(part_rows, a.nbm) : 0u;
   {
     const int nkt = (a.K + BK - 1) / BK;
     if (nsplit < 1 || nkt <= 1) nsplit = 1;

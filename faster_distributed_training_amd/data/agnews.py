@@ -171,11 +171,17 @@ def _round_up(L, buckets):
 class TextBatchLoader:
     """Batches of ``(input_ids [B,L], labels [B], token_type_ids [B,L], attention_mask [B,L])``
     with DistributedSampler semantics (seeded shared permutation, rank-strided shard,
-    ``set_epoch``, ``drop_last``).  The packed token store is uploaded to the device once;
-    each batch is one gather + pad."""
+    ``set_epoch``, ``drop_last``).
+
+    ``resident`` (default): the packed token store is uploaded to the device once and a
+    batch is one device gather + pad; only the batch's sample indices and lengths cross
+    the bus.  ``resident=False`` (corpora larger than wanted in HBM, e.g. a real CSV of
+    any size): the host gathers + pads the token ids and stages them.  On a GPU every
+    per-batch transfer goes through the pinned ring + copy stream of ``prefetch.py``
+    (staged one batch ahead, no pageable copy, no host sync)."""
 
     def __init__(self, store: TokenStore, batch_size: int, device, rank=0, world_size=1, shuffle=True,
-                 drop_last=True, seed=0, length_buckets=(64, 128, 256, 512)):
+                 drop_last=True, seed=0, length_buckets=(64, 128, 256, 512), resident=True, pinned=None):
         self.store = store
         self.bs = batch_size
         self.device = torch.device(device)
@@ -183,10 +189,22 @@ class TextBatchLoader:
         self.shuffle, self.drop_last, self.seed = shuffle, drop_last, seed
         self.buckets = sorted(length_buckets) if length_buckets else None
         self.epoch = 0
-        self.tokens = torch.from_numpy(store.tokens.astype(np.int64)).to(self.device)
-        self.offsets = torch.from_numpy(store.offsets).to(self.device)
-        self.lengths = torch.from_numpy(store.lengths)
-        self.labels = torch.from_numpy(store.labels).to(self.device)
+        self.resident = resident
+        if pinned is None:
+            pinned = self.device.type == "cuda"
+        self.stager = None
+        if pinned:
+            from .prefetch import PinnedStager
+            lmax = int(store.lengths.max()) if len(store) else 1
+            if self.buckets:
+                lmax = _round_up(lmax, self.buckets)
+            per = 2 * 8 * batch_size + 512 if resident else (4 * batch_size * lmax + 3 * 4 * batch_size + 1024)
+            self.stager = PinnedStager(self.device, per, 3)
+        if resident:
+            self.tokens = torch.from_numpy(store.tokens.astype(np.int64)).to(self.device)
+            self.offsets = torch.from_numpy(store.offsets).to(self.device)
+            self.labels = torch.from_numpy(store.labels).to(self.device)
+        self._types = {}
 
     def set_epoch(self, e):
         self.epoch = e
@@ -204,22 +222,54 @@ class TextBatchLoader:
         per = len(self.store) // self.world if self.drop_last else -(-len(self.store) // self.world)
         return per // self.bs if self.drop_last else -(-per // self.bs)
 
-    def batch(self, idx: torch.Tensor):
-        lens = self.lengths[idx]
+    # ---- host half: what crosses the bus for one batch
+    def _host(self, idx: np.ndarray):
+        lens = self.store.lengths[idx]
         L = _round_up(int(lens.max()), self.buckets)
-        B = idx.numel()
-        dev_idx = idx.to(self.device)
-        start = self.offsets[dev_idx]
-        ln = lens.to(self.device).clamp(max=L)
+        ln = np.minimum(lens, L).astype(np.int64)
+        if self.resident:
+            return [idx.astype(np.int64), ln], L
+        B = idx.size
+        starts = self.store.offsets[idx]
+        pos = np.arange(L)
+        valid = pos[None, :] < ln[:, None]
+        gat = np.minimum(starts[:, None] + pos[None, :], max(len(self.store.tokens) - 1, 0))
+        ids = np.where(valid, self.store.tokens[gat], PAD_ID).astype(np.int32)
+        return [ids.reshape(B, L), self.store.labels[idx].astype(np.int32), ln], L
+
+    # ---- device half: build the batch from the transferred tensors
+    def _device(self, arrs, L):
         pos = torch.arange(L, device=self.device)
-        valid = pos.unsqueeze(0) < ln.unsqueeze(1)
-        gather = (start.unsqueeze(1) + pos.unsqueeze(0)).clamp(max=self.tokens.numel() - 1)
-        ids = torch.where(valid, self.tokens[gather], torch.zeros((), dtype=torch.long, device=self.device))
-        mask = valid.to(torch.long)
-        types = torch.zeros(B, L, dtype=torch.long, device=self.device)
-        return ids, self.labels[dev_idx], types, mask
+        if self.resident:
+            dev_idx, ln = arrs
+            start = self.offsets[dev_idx]
+            valid = pos.unsqueeze(0) < ln.unsqueeze(1)
+            gather = (start.unsqueeze(1) + pos.unsqueeze(0)).clamp(max=self.tokens.numel() - 1)
+            ids = torch.where(valid, self.tokens[gather], torch.zeros((), dtype=torch.long, device=self.device))
+            labels = self.labels[dev_idx]
+        else:
+            ids32, lab32, ln = arrs
+            valid = pos.unsqueeze(0) < ln.unsqueeze(1)
+            ids = ids32.long()
+            labels = lab32.long()
+        B = ids.shape[0]
+        types = self._types.get((B, L))
+        if types is None:
+            types = self._types[(B, L)] = torch.zeros(B, L, dtype=torch.long, device=self.device)
+        return ids, labels, types, valid.to(torch.long)
+
+    def batch(self, idx):
+        """One batch from sample indices (host tensor/array), without staging (CPU path)."""
+        arrs, L = self._host(np.asarray(idx, dtype=np.int64))
+        return self._device([torch.from_numpy(a).to(self.device) for a in arrs], L)
 
     def __iter__(self):
-        idx = self._indices()
-        for b in range(len(self)):
-            yield self.batch(idx[b * self.bs:(b + 1) * self.bs])
+        idx = self._indices().numpy()
+        nb = len(self)
+        if self.stager is None:
+            for b in range(nb):
+                yield self.batch(idx[b * self.bs:(b + 1) * self.bs])
+            return
+        from .prefetch import StagedIterator
+        yield from StagedIterator(self.stager, nb, lambda b: self._host(idx[b * self.bs:(b + 1) * self.bs]),
+                                  self._device)

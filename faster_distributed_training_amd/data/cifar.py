@@ -10,8 +10,11 @@ ONCE to HBM; a batch is a slice of a per-epoch permutation (DistributedSampler
 semantics: identical seeded permutation on every rank, rank-strided shard,
 ``set_epoch``, ``drop_last``); one HIP kernel (``csrc/kernels/augment.hip``) gathers,
 crops, flips, normalises and writes channels-last bf16 directly in the layout the conv
-engine consumes.  No worker processes, no pinned-memory thread, no per-sample Python.
-The CPU path (tests, CPU training) implements the same transform with torch ops.
+engine consumes.  No worker processes, no per-sample Python.  ``resident=False`` (image
+sets larger than wanted in HBM) keeps the images on the host: each batch is gathered in
+numpy and staged through the pinned ring + copy stream of ``prefetch.py`` one batch
+ahead (the reference's pin_memory + non_blocking path), then augmented by the same
+kernel.  The CPU path (tests, CPU training) implements the same transform with torch ops.
 
 Fixed vs the reference: the transform order is deterministic crop -> flip -> normalise
 (the reference permutes it randomly once per run, survey Q13); the sampler epoch is
@@ -197,7 +200,7 @@ class DeviceCIFARLoader:
 
     def __init__(self, data_u8, targets, batch_size, device, train=True, rank=0, world_size=1, seed=0,
                  drop_last=True, shuffle=True, out_dtype=torch.bfloat16, pad=4, flip=True, augment=True,
-                 order=TRANSFORMS):
+                 order=TRANSFORMS, resident=True):
         self.device = torch.device(device)
         self.train = train
         self.bs = batch_size
@@ -209,12 +212,22 @@ class DeviceCIFARLoader:
         self.pad, self.flip, self.augment = pad, flip, augment
         self.order = tuple(order)
         self.n = len(targets)
-        self.images = torch.as_tensor(np.ascontiguousarray(data_u8)).to(self.device)
-        self.labels = torch.as_tensor(np.asarray(targets)).to(torch.int32).to(self.device)
+        self._gpu = self.device.type == "cuda" and _native.enabled()
+        self.resident = resident or not self._gpu
+        self.stager = None
+        if self.resident:
+            self.images = torch.as_tensor(np.ascontiguousarray(data_u8)).to(self.device)
+            self.labels = torch.as_tensor(np.asarray(targets)).to(torch.int32).to(self.device)
+        else:
+            from .prefetch import PinnedStager
+            self.host_images = np.ascontiguousarray(data_u8)
+            self.host_labels = np.asarray(targets).astype(np.int32)
+            per = batch_size * int(np.prod(self.host_images.shape[1:])) + 4 * batch_size + 512
+            self.stager = PinnedStager(self.device, per, 3)
+            self._iota = torch.arange(batch_size, dtype=torch.int32, device=self.device)
         self.epoch = 0
         # per-rank stream of crop / flip draws (the kernel hashes (seed, step, sample))
         self.rng = torch.tensor([seed + 7919 * rank, 0], dtype=torch.int64, device=self.device)
-        self._gpu = self.device.type == "cuda" and _native.enabled()
         self._cpu_gen = torch.Generator().manual_seed(seed + 7919 * rank)
 
     def set_epoch(self, epoch: int):
@@ -238,17 +251,20 @@ class DeviceCIFARLoader:
         per_rank = self.n // self.world if self.drop_last else -(-self.n // self.world)
         return per_rank // self.bs if self.drop_last else -(-per_rank // self.bs)
 
-    def batch(self, idx: torch.Tensor):
-        """Augment one batch given sample indices (device int32)."""
+    def batch(self, idx: torch.Tensor, images=None, labels=None):
+        """Augment one batch given sample indices (device int32) into ``images`` /
+        ``labels`` (default: the resident set)."""
         B = idx.numel()
         if self._gpu:
             nat = _native.native()
+            images = self.images if images is None else images
+            labels = self.labels if labels is None else labels
             # NHWC with channels zero-padded to 8: the conv engine's stem operand layout
             cp = 8
             out = torch.empty(B, 32, 32, cp, device=self.device, dtype=self.out_dtype)
             lab = torch.empty(B, device=self.device, dtype=torch.int32)
             train = self.train and self.augment
-            nat.augment(self.images.data_ptr(), idx.data_ptr(), self.labels.data_ptr(), lab.data_ptr(),
+            nat.augment(images.data_ptr(), idx.data_ptr(), labels.data_ptr(), lab.data_ptr(),
                         out.data_ptr(), B, 32, 32, 3, cp, self.pad if train else 0, int(train and self.flip),
                         self.rng.data_ptr(), *CIFAR_MEAN, *CIFAR_STD, 0, int(pad_normalized(self.order)),
                         1 if self.out_dtype == torch.bfloat16 else 0, _native.stream_ptr())
@@ -259,10 +275,27 @@ class DeviceCIFARLoader:
                         out_dtype=torch.float32, order=self.order)
         return x.to(self.device), self.labels[idx.long()].long()
 
+    def _host(self, shard, b):
+        sel = shard[b * self.bs:(b + 1) * self.bs]
+        return [np.take(self.host_images, sel, axis=0), self.host_labels[sel]], None
+
+    def _device(self, arrs, _meta):
+        imgs, labs = arrs
+        return self.batch(self._iota[:imgs.shape[0]], images=imgs, labels=labs)
+
     def __iter__(self):
         shard = self._indices()
         nb = len(self)
-        idx_all = shard.to(torch.int32).to(self.device)
+        if not self.resident:
+            from .prefetch import StagedIterator
+            sh = shard.numpy()
+            yield from StagedIterator(self.stager, nb, lambda b: self._host(sh, b), self._device)
+            return
+        # one index upload per epoch, from pinned memory on the compute stream (no host sync)
+        idx_cpu = shard.to(torch.int32)
+        if self.device.type == "cuda":
+            idx_cpu = idx_cpu.pin_memory()
+        idx_all = idx_cpu.to(self.device, non_blocking=True)
         for b in range(nb):
             idx = idx_all[b * self.bs:(b + 1) * self.bs]
             if idx.numel() == 0:

@@ -75,3 +75,26 @@ def stream_ptr(device: torch.device | None = None) -> int:
 
 def ptr(t: torch.Tensor | None) -> int:
     return 0 if t is None else t.data_ptr()
+
+
+# ---------------------------------------------------------------- deterministic mode
+_DET = False
+
+
+def set_deterministic(on: bool = True) -> None:
+    """Bitwise-repeatable engine steps (``--deterministic``; SURVEY section 5 race detection).
+
+    The ResNet engine's per-channel statistics producers write one slot row per workgroup
+    (no wrapping onto shared rows, so no two fp32 atomics meet on an address), the split-K
+    conv reducer sums partials in split order, and 1x1 weight gradients go through the
+    ordered slab reduction instead of fp32 atomics.  Costs a little time (larger slot
+    buffers; see profiles/deterministic_cost.json)."""
+    global _DET
+    _DET = bool(on)
+    m = load()
+    if m is not None:
+        m.set_deterministic_mode(_DET)
+
+
+def deterministic() -> bool:
+    return _DET

@@ -182,10 +182,21 @@ def out_hw(h, w, shp: ConvShape):
 STAT_SLOTS = 64  # csrc/kernels/common.h kStatSlots
 
 
-def stat_slots(nq: int, C: int, device) -> torch.Tensor:
-    """A fresh zeroed statistics-slot buffer [STAT_SLOTS, nq, C] (the engine instead reuses
-    one persistent workspace that its finalize kernels re-zero)."""
-    return torch.zeros(STAT_SLOTS, nq, C, device=device, dtype=torch.float32)
+def slot_rows(M: int | None = None) -> int:
+    """Statistics slot rows for a producer over M output rows: STAT_SLOTS (rows shared by
+    workgroups, block index mod 64), or in deterministic mode one row per workgroup
+    (conv row blocks are >= 64 rows; the BN-backward kernels cap their grid to the rows)."""
+    if not _native.deterministic():
+        return STAT_SLOTS
+    assert M is not None, "deterministic mode sizes the slots by the producer's row count"
+    need = max(STAT_SLOTS, -(-int(M) // 64))
+    return 1 << (need - 1).bit_length()
+
+
+def stat_slots(nq: int, C: int, device, M: int | None = None) -> torch.Tensor:
+    """A fresh zeroed statistics-slot buffer [slot_rows(M), nq, C] (the engine instead
+    reuses one persistent workspace that its finalize kernels re-zero)."""
+    return torch.zeros(slot_rows(M), nq, C, device=device, dtype=torch.float32)
 
 
 def conv_fwd(x, wf, shp: ConvShape, s=None, t=None, act=0, alpha=1.0, tile=None, part=None, nsplit=None):
@@ -208,12 +219,13 @@ def conv_fwd(x, wf, shp: ConvShape, s=None, t=None, act=0, alpha=1.0, tile=None,
     ns, slab_p, cnt_p = _splitk_args(ent, M, shp.cout, shp.ntaps * C, bm, bn, bk, x.device)
     y = torch.empty(N, Ho, Wo, shp.cout, device=x.device, dtype=torch.bfloat16)
     if part is None:
-        part = stat_slots(2, shp.cout, x.device)
+        part = stat_slots(2, shp.cout, x.device, M)
     dh, dw, wt = taps_fwd(shp.k, shp.pad)
     if pro == PRO_AFFINE_ACT and s is None:
         s = torch.ones(C, device=x.device, dtype=torch.float32)
         t = torch.zeros(C, device=x.device, dtype=torch.float32)
-    nat.conv_igemm(x.data_ptr(), 0, _p(s), _p(t), 0, wf.data_ptr(), y.data_ptr(), part.data_ptr(), 0, 0, 0, 0, 0, 0,
+    nat.conv_igemm(x.data_ptr(), 0, _p(s), _p(t), 0, wf.data_ptr(), y.data_ptr(), part.data_ptr(), part.shape[0],
+                   0, 0, 0, 0, 0, 0,
                    N, H, W, C, Ho, Wo, shp.stride, list(dh), list(dw), list(wt), shp.cout, shp.ntaps * shp.cxp,
                    Ho, Wo, 1, 0, 0, pro, int(act), float(alpha), EPI_STATS, 0, 1.0, bm, bn, bk, ns, slab_p, cnt_p, _sp())
     return y, part
@@ -240,7 +252,7 @@ def conv_dgrad(g, y, al, be, wd, shp: ConvShape, x_shape, epi=EPI_STORE, out=Non
     if out is None:
         out = torch.empty(N, Hx, Wx, shp.cin, device=g.device, dtype=torch.bfloat16)
     if epi == EPI_ACTBWD and part is None:
-        part = stat_slots(2, shp.cin, g.device)
+        part = stat_slots(2, shp.cin, g.device, Nx * Hx * Wx)
     if epi == EPI_JOINBWD:
         assert shp.stride == 1 and ex is not None and part is not None and (jmask is not None or jout is not None)
     ent = None
@@ -263,7 +275,8 @@ def conv_dgrad(g, y, al, be, wd, shp: ConvShape, x_shape, epi=EPI_STORE, out=Non
         pro = PRO_FOLD if al is not None else PRO_NONE  # al None: g is already folded
         assert gs is None or pro == PRO_FOLD, "gs needs the fold prologue (al/be)"
         nat.conv_igemm(g.data_ptr(), _p(y) if pro == PRO_FOLD else 0, _p(al), _p(be), _p(gs), wd.data_ptr(),
-                       out.data_ptr(), _p(part) if epi in (EPI_ACTBWD, EPI_JOINBWD) else 0, _p(ex), _p(es), _p(et),
+                       out.data_ptr(), _p(part) if epi in (EPI_ACTBWD, EPI_JOINBWD) else 0,
+                       part.shape[0] if part is not None else 0, _p(ex), _p(es), _p(et),
                        _p(jmask), _p(jyb), _p(jout), N, Hy, Wy, Cy, Ha, Wa, 1,
                        list(dh), list(dw), list(wt), shp.cin, shp.ntaps * shp.cout, Hx, Wx, shp.stride, py, px,
                        pro, 0, 1.0, epi, int(act), float(alpha), bm, bn, bk, ns, slab_p, cnt_p, _sp())
@@ -303,8 +316,9 @@ def conv_wgrad(g, y, al, be, x, shp: ConvShape, out, xs=None, xt=None, act=0, al
     tiles = (shp.cout // bm) * (-(-ldw // bn))
     ns = nsplit or wgrad_split(M, tiles)
     # 1x1 without channel padding: the slab row layout IS OIHW -> every split adds into
-    # `out` with fp32 atomics (no slab, no reduce launch)
-    direct = shp.ntaps == 1 and shp.cxp == shp.cin and out.is_contiguous()
+    # `out` with fp32 atomics (no slab, no reduce launch); deterministic mode keeps the
+    # ordered slab reduction
+    direct = shp.ntaps == 1 and shp.cxp == shp.cin and out.is_contiguous() and not _native.deterministic()
     if direct:
         if not accumulate:
             out.zero_()

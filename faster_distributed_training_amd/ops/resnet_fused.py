@@ -237,17 +237,21 @@ def _restore(t):
 _SLOTS: dict = {}
 
 
-def slots(nq, C, dev):
-    """The persistent statistics-slot workspace viewed as [STAT_SLOTS, nq, C].  Producers
-    (conv epilogues, BN-backward reductions) add into it with fp32 atomics; the consuming
-    finalize / reduce kernel sums it in fp64 and re-zeroes it, so the next producer needs
-    no memset.  One workspace suffices: every producer is consumed before the next one."""
-    need = ci.STAT_SLOTS * 3 * 2048
+def slots(nq, C, dev, M):
+    """The persistent statistics-slot workspace viewed as [rows, nq, C] for a producer over
+    M output rows (rows = 64, or one per workgroup in deterministic mode: ci.slot_rows).
+    Producers (conv epilogues, BN-backward reductions) add into it with fp32 atomics; the
+    consuming finalize / reduce kernel sums it in fp64 and re-zeroes it, so the next
+    producer needs no memset.  One workspace suffices: every producer is consumed before
+    the next one (and a view only ever covers rows its finalize re-zeroes)."""
+    rows = ci.slot_rows(M)
+    n = max(ci.STAT_SLOTS * 3 * 2048, rows * nq * C)
     ws = _SLOTS.get(dev)
-    if ws is None or ws.numel() < max(need, ci.STAT_SLOTS * nq * C):
-        ws = torch.zeros(max(need, ci.STAT_SLOTS * nq * C), device=dev, dtype=torch.float32)
+    if ws is None or ws.numel() < n:
+        # (allocation happens in the eager warm-up step, before any graph capture)
+        ws = torch.zeros(n, device=dev, dtype=torch.float32)
         _SLOTS[dev] = ws
-    return ws[: ci.STAT_SLOTS * nq * C].view(ci.STAT_SLOTS, nq, C)
+    return ws[: rows * nq * C].view(rows, nq, C)
 
 
 def _bn_fin_params(u: Unit, training):
@@ -268,7 +272,7 @@ def conv_bn_fwd(x, u: Unit, s, t, act, training, dev):
     Ho, Wo = ci.out_hw(x.shape[1], x.shape[2], u.shp)
     M = x.shape[0] * Ho * Wo
     y, part = ci.conv_fwd(x, u.wf, u.shp, s, t, act[0] if act else 0, act[1] if act else 1.0,
-                          part=slots(2, u.shp.cout, dev))
+                          part=slots(2, u.shp.cout, dev, M))
     return y, finalize_stats(part, u, M, training, dev), M
 
 
@@ -447,7 +451,7 @@ class ResNetBodyFn(torch.autograd.Function):
             y3, s3 = ys[-1][0], ys[-1][1]
             C = y3.shape[-1]
             M = _rows(y3)
-            part = slots(3, C, dev)
+            part = slots(3, C, dev, M)
             if joined:
                 gpre = g
             else:
@@ -455,7 +459,8 @@ class ResNetBodyFn(torch.autograd.Function):
                 # own BN scale (gs = s3 / s_shortcut) in its prologue
                 gpre = torch.empty_like(y3)
                 nat.residual_act_bwd(g.data_ptr(), 0 if mask is not None else out.data_ptr(), _p(mask),
-                                     y3.data_ptr(), _p(sc[0] if sc else None), gpre.data_ptr(), part.data_ptr(), M, C,
+                                     y3.data_ptr(), _p(sc[0] if sc else None), gpre.data_ptr(), part.data_ptr(),
+                                     part.shape[0], M, C,
                                      b.join[0], float(b.join[1]), 1, _sp())
             ul = b.units[-1]
             (al, be), coef_sc = bwd_finalize(part, 3, ul, (ys[-1][3], ys[-1][4], ys[-1][5]),
@@ -482,7 +487,7 @@ class ResNetBodyFn(torch.autograd.Function):
                 if i > 0:
                     yp, sp_, tp = ys[i - 1][0], ys[i - 1][1], ys[i - 1][2]
                     actp = b.units[i - 1].act_out
-                    pp = slots(2, u.shp.cin, dev)
+                    pp = slots(2, u.shp.cin, dev, _rows(yp))
                     if MATERIALIZE_3X3 and u.shp.k > 1:
                         # fold the BN-backward correction into the gradient once (3x3: the
                         # dgrad operand is re-read 9x, the wgrad operand once per column block)
@@ -508,7 +513,7 @@ class ResNetBodyFn(torch.autograd.Function):
                     if prev is not None:
                         _, pys, psc, pout, pmask = prec
                         ci.conv_dgrad(g_cur, y, al, be, u.wd, u.shp, tuple(x_in.shape), epi=ci.EPI_JOINBWD, out=g_x,
-                                      gs=gs_cur, ex=pys[-1][0], part=slots(3, x_in.shape[-1], dev), act=prev.join[0],
+                                      gs=gs_cur, ex=pys[-1][0], part=slots(3, x_in.shape[-1], dev, _rows(x_in)), act=prev.join[0],
                                       alpha=prev.join[1], jmask=pmask, jyb=psc[0] if psc else None,
                                       jout=None if pmask is not None else pout)
                     else:
@@ -526,10 +531,10 @@ class ResNetBodyFn(torch.autograd.Function):
         st = plan.stem
         M0 = _rows(y0)
         C0 = st.shp.cout
-        part = slots(2, C0, dev)
+        part = slots(2, C0, dev, M0)
         gy0 = torch.empty_like(y0)
         nat.act_bwd_reduce(g.data_ptr(), y0.data_ptr(), s0.data_ptr(), t0.data_ptr(), gy0.data_ptr(),
-                           part.data_ptr(), M0, C0, st.act_out[0], float(st.act_out[1]), 1, _sp())
+                           part.data_ptr(), part.shape[0], M0, C0, st.act_out[0], float(st.act_out[1]), 1, _sp())
         (al, be), _ = bwd_finalize(part, 2, st, (sm0, sa0, M0), training=training, dev=dev)
         wgrad_into(st, gy0, y0, al, be, x_img, None, None, (ACT_NONE, 1.0))
         if fs is not None:

@@ -36,7 +36,10 @@ MI355X design (``FullyShardedDP``):
   ``ops/resnet_fused.py``) and packs / releases its bf16 weight layouts per stage.
 
 Memory: with 288 GB per MI355X this is a capability, not a necessity, for these models;
-``peak_full_bytes`` reports the largest amount of gathered parameter storage alive at once.
+``peak_full_bytes`` reports the largest amount of gathered parameter + unit-gradient storage
+alive at once.  The schedule bounds it by max_i(2 b_i + b_(i-1) + b_(i+1)) + 2 b_root (unit
+i gathered with its gradient buffer, unit i-1 prefetched, unit i+1's reduce-scatter in
+flight; b = a unit's full fp32 bytes).
 """
 from __future__ import annotations
 
@@ -221,6 +224,14 @@ class Unit:
         op = dist.ReduceOp.AVG if fs.use_avg else dist.ReduceOp.SUM
         self.rs_work = dist.reduce_scatter_tensor(fs.grad_chunk(self), self.gfull, op=op, group=fs.pg,
                                                   async_op=True)
+        # at most two unit gradient buffers alive: the previously launched reduce-scatter
+        # is ordered before further compute (a stream wait on RCCL) and its buffer released
+        prev = fs.last_rs
+        if prev is not None and prev is not self and prev.rs_work is not None:
+            prev.rs_work.wait()
+            prev.rs_work = None
+            prev._free(prev.gfull)
+        fs.last_rs = self
         for _, p in self.params:
             p.grad = None
         self.grads_live = False
@@ -298,6 +309,7 @@ class FullyShardedDP:
         self.space = SpaceView(self.shard_data, self.shard_grad, slots, sdev)
         self.view = self.space  # (trainer interface shared with the sharded-optimizer DP)
         self.peak_full_bytes = 0
+        self.last_rs = None  # unit whose reduce-scatter was launched last
         self.order = [u for u in self.units if not u.root]
         self.engine_units = set(engine_units)
         self._hooks = []
@@ -423,6 +435,7 @@ class FullyShardedDP:
             else:  # unused this step: contributes zeros (every rank must join the collective)
                 u.begin_backward(gather=False)
                 u.finish()
+        self.last_rs = None
         if self.offload:
             self.shard_grad.copy_(self.stage_grad, non_blocking=False)
         if not self.use_avg:

@@ -75,6 +75,7 @@ class ResNetConfig:
     save_last: bool = False            # write the rolling full-state *_last.pth every epoch
     nonfinite_guard: bool = True       # skip (on device) optimizer steps whose gradients are not finite
     profile_steps: int = 0             # per-phase device timing (+ roctx ranges) of the first K steps
+    deterministic: bool = False        # bitwise-repeatable engine steps (ops/_native.set_deterministic)
     extra: dict = field(default_factory=dict)
 
 
@@ -95,6 +96,9 @@ class ResNetTrainer:
             self.rank, self.world = pdist.rank(), pdist.world()
             cfg.distributed = self.world > 1
         self.device = default_device()
+        if cfg.deterministic:
+            from ..ops import _native
+            _native.set_deterministic(True)
         seed_everything(cfg.seed)  # identical init on every rank
         self.model = build_model(cfg, self.device)
         self.best_acc, self.start_epoch = ckpt.load_best_performance(self.ckpt_path, cfg.num_classes, cfg.resume)

@@ -74,7 +74,7 @@ class FlatParams:
         self.slots: list[Slot] = []
         self.runs = None
         self.chunk = 0
-        if partition and partition > 1:
+        if partition and partition >= 1:  # (partition=1: one run, the world-size-1 case)
             self.runs = partition_runs([_aligned(p.numel()) for _, p in named], partition)
             self.chunk = max(sum(_aligned(named[i][1].numel()) for i in range(a, b)) for a, b in self.runs)
             self.chunk = max(self.chunk, ALIGN)

@@ -57,6 +57,8 @@ def parse(argv=None):
     p.add_argument("--no_nonfinite_guard", action="store_true", help="do not skip steps with non-finite gradients")
     p.add_argument("--profile_steps", default=0, type=int, help="per-phase device timing + roctx ranges of K steps")
     p.add_argument("--no_graphs", action="store_true", help="launch the engine's kernels eagerly (no HIP graphs)")
+    p.add_argument("--deterministic", action="store_true",
+                   help="bitwise-repeatable engine steps: ordered statistics/split-K reductions, no shared fp32 atomics")
     return p.parse_args(argv)
 
 
@@ -79,7 +81,8 @@ def config_from_args(a):
                         checkpoint_dir=a.checkpoint_dir, steps_per_epoch=a.steps, eval=not a.no_eval,
                         log_path=a.log, plot=not a.no_plot, workers=a.workers, auto_resume=a.auto_resume,
                         save_last=a.save_last, nonfinite_guard=not a.no_nonfinite_guard,
-                        profile_steps=a.profile_steps, graphs=not a.no_graphs, extra=extra)
+                        profile_steps=a.profile_steps, graphs=not a.no_graphs,
+                        deterministic=a.deterministic, extra=extra)
 
 
 def main(argv=None):

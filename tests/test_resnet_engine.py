@@ -23,11 +23,20 @@ def _pair(arch, cuda):
     return m_ref, m_eng
 
 
-@pytest.mark.parametrize("arch", ["resnet18", "resnet50"])
-def test_engine_train_step_matches_reference(cuda, arch):
+@pytest.mark.parametrize("arch,det", [("resnet18", False), ("resnet50", False), ("resnet50", True)])
+def test_engine_train_step_matches_reference(cuda, arch, det):
     """bf16 engine vs the fp32 reference: logits within 2x the error of the reference run
     under bf16 autocast; every parameter gradient closely aligned; BN running statistics
-    updated identically."""
+    updated identically.  det: the deterministic-mode reductions (--deterministic)."""
+    from faster_distributed_training_amd.ops import _native
+    _native.set_deterministic(det)
+    try:
+        _train_step_vs_reference(cuda, arch)
+    finally:
+        _native.set_deterministic(False)
+
+
+def _train_step_vs_reference(cuda, arch):
     m_ref, m_eng = _pair(arch, cuda)
     torch.backends.cudnn.allow_tf32 = False
     torch.manual_seed(1)
