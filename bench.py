@@ -50,7 +50,9 @@ def parse():
     ap.add_argument("--deterministic", action="store_true", help="bitwise-repeatable engine reductions (cost probe)")
     ap.add_argument("--model", default="resnet50", choices=["resnet50", "transformer"],
                     help="transformer: secondary benchmark (BASELINE.json config 4, AG-News-shaped)")
-    ap.add_argument("--seq-bucket", type=int, default=128, help="transformer: padded sequence length")
+    ap.add_argument("--seq-buckets", default="128,256",
+                    help="transformer: padded-length buckets (a batch pads to the smallest bucket >= its longest "
+                         "sample; the largest bucket must cover the longest sample, so nothing is truncated)")
     return ap.parse_args()
 
 
@@ -147,8 +149,9 @@ def main():
 
 def bench_transformer(args):
     """Transformer text classifier (6 layers, d 512, vocab 30522), AG-News-shaped synthetic
-    batches padded to one length bucket, global batch 256 (reference: 64 x 4 GPUs),
-    NGD optimizer (run_distributed.sh:3), bf16."""
+    batches padded to a length bucket (never truncated: the reference pads to the longest
+    sample), global batch 256 (reference: 64 x 4 GPUs), NGD optimizer (run_distributed.sh:3),
+    bf16."""
     import torch
     import torch.distributed as dist
 
@@ -157,10 +160,13 @@ def bench_transformer(args):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     gb = 256 if args.global_batch == 1024 else args.global_batch
     assert gb % world == 0
+    buckets = tuple(sorted(int(b) for b in args.seq_buckets.split(",")))
     cfg = TransformerConfig(batch_size=gb // world, synthetic=True, eval=False, plot=False, distributed=world > 1,
-                            ngd=True, precision=args.precision, length_buckets=(args.seq_bucket,),
+                            ngd=True, precision=args.precision, length_buckets=buckets,
                             bucket_mb=args.bucket_mb, fsdp=args.fsdp, epoch=1)
     tr = TransformerTrainer(cfg)
+    longest = int(tr.train_loader.store.lengths.max())
+    assert longest <= buckets[-1], f"largest bucket {buckets[-1]} would truncate samples of length {longest}"
     dev = tr.device
     cuda = dev.type == "cuda"
     it = iter(tr.train_loader)
@@ -191,7 +197,8 @@ def bench_transformer(args):
            "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True, "scaling": "strong",
            "vs_baseline": round(value / 66.0, 2), "dtype": args.precision,
            "data": "synthetic (AG-News-shaped token batches), random-init weights",
-           "config": {"model": "transformer 6x512 (vocab 30522)", "global_batch": gb, "seq_len": args.seq_bucket,
+           "config": {"model": "transformer 6x512 (vocab 30522)", "global_batch": gb, "seq_len": list(buckets),
+                      "truncation": "none (pad to the smallest bucket >= the batch's longest sample)",
                       "parallelism": f"{'fsdp' if args.fsdp else 'dp'}{world}", "optimizer": "ngd"},
            "peak_mem_gb": round(torch.cuda.max_memory_allocated() / 2**30, 2) if cuda else None}
     if tr.rank == 0:

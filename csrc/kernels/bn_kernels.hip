@@ -264,46 +264,6 @@ __global__ __launch_bounds__(256) void partials_compact_kernel(const float* __re
 //    beta = -(g_s - mean g_t) gamma inv^3 / N,    alpha = -beta*mean - g_t s / N
 //    g_gamma = (g_s - mean g_t) inv,  g_beta = g_t
 // mode 2 (BatchNorm2d eval, running stats): beta = alpha = 0, g_gamma/g_beta as above
-struct CoefArgs {
-  int mode;
-  float eps;
-  double count;
-  const float* save_mean;
-  const float* save_aux;
-  const float* gamma;
-  float* alpha;
-  float* beta;
-  float* ggamma;
-  float* gbeta;
-};
-
-__device__ __forceinline__ void bwd_coef_one(const CoefArgs& a, int c, double g_s, double g_t) {
-  const double mean = a.save_mean[c], aux = a.save_aux[c];
-  const double count = a.count;
-  if (a.mode == 0) {
-    const double sd = aux;
-    const double s = 1.0 / (sd + (double)a.eps);
-    const double b = sd > 0.0 ? -(g_s - mean * g_t) * s * s / ((count - 1.0) * sd) : 0.0;
-    a.beta[c] = (float)b;
-    a.alpha[c] = (float)(-b * mean - g_t * s / count);
-  } else {
-    const double inv = aux;
-    const double g = a.gamma ? (double)a.gamma[c] : 1.0;
-    const double s = g * inv;
-    if (a.mode == 1) {
-      const double b = -(g_s - mean * g_t) * g * inv * inv * inv / count;
-      a.beta[c] = (float)b;
-      a.alpha[c] = (float)(-b * mean - g_t * s / count);
-    } else {
-      a.beta[c] = 0.f;
-      a.alpha[c] = 0.f;
-    }
-    // accumulate (+=) into the parameter gradients (flat gradient views)
-    if (a.ggamma) a.ggamma[c] += (float)((g_s - mean * g_t) * inv);
-    if (a.gbeta) a.gbeta[c] += (float)g_t;
-  }
-}
-
 __global__ void stats_bwd_coef_kernel(const float* __restrict__ gs, const float* __restrict__ gt, int C, CoefArgs a) {
   int c = blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= C) return;
@@ -569,7 +529,7 @@ void channel_stats_partial(uint64_t y, uint64_t part, long M, int C, int dt, uin
 void stats_finalize(uint64_t part, int nb, int C, double count, int mode, float eps, float momentum, uint64_t gamma,
                     uint64_t beta, uint64_t run_mean, uint64_t run_var, uint64_t nbt, uint64_t out_s, uint64_t out_t,
                     uint64_t save_mean, uint64_t save_aux, int zero_after, uint64_t stream) {
-  FinArgs f{nullptr, mode, eps, momentum, count, P<const float>(gamma), P<const float>(beta), P<float>(run_mean),
+  FinArgs f{mode, eps, momentum, count, P<const float>(gamma), P<const float>(beta), P<float>(run_mean),
             P<float>(run_var), P<long long>(nbt), P<float>(out_s), P<float>(out_t), P<float>(save_mean),
             P<float>(save_aux)};
   stats_finalize_kernel<<<(C + 63) / 64, 64 * kRedWaves, 0, as_stream(stream)>>>(P<float>(part), part ? nb : 0, C,

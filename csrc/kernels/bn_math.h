@@ -13,7 +13,6 @@
 namespace fdt {
 
 struct FinArgs {
-  int* cnt;  // fused form: per-channel-tile arrival tickets (zero between launches); nullptr = not fused
   int mode;
   float eps;
   float momentum;
@@ -65,6 +64,48 @@ __device__ __forceinline__ void bn_finalize_channel(const FinArgs& f, int c, dou
     f.out_t[c] = (float)(b - mean * g * inv);
     f.save_mean[c] = (float)mean;
     f.save_aux[c] = (float)inv;
+  }
+}
+
+// BN-backward coefficients from the per-channel reductions (g_s, g_t) of dL/dy; see the mode
+// table above stats_bwd_coef_kernel (bn_kernels.hip).
+struct CoefArgs {
+  int mode;
+  float eps;
+  double count;
+  const float* save_mean;
+  const float* save_aux;
+  const float* gamma;
+  float* alpha;
+  float* beta;
+  float* ggamma;
+  float* gbeta;
+};
+
+__device__ __forceinline__ void bwd_coef_one(const CoefArgs& a, int c, double g_s, double g_t) {
+  const double mean = a.save_mean[c], aux = a.save_aux[c];
+  const double count = a.count;
+  if (a.mode == 0) {
+    const double sd = aux;
+    const double s = 1.0 / (sd + (double)a.eps);
+    const double b = sd > 0.0 ? -(g_s - mean * g_t) * s * s / ((count - 1.0) * sd) : 0.0;
+    a.beta[c] = (float)b;
+    a.alpha[c] = (float)(-b * mean - g_t * s / count);
+  } else {
+    const double inv = aux;
+    const double g = a.gamma ? (double)a.gamma[c] : 1.0;
+    const double s = g * inv;
+    if (a.mode == 1) {
+      const double b = -(g_s - mean * g_t) * g * inv * inv * inv / count;
+      a.beta[c] = (float)b;
+      a.alpha[c] = (float)(-b * mean - g_t * s / count);
+    } else {
+      a.beta[c] = 0.f;
+      a.alpha[c] = 0.f;
+    }
+    // accumulate (+=) into the parameter gradients (flat gradient views)
+    if (a.ggamma) a.ggamma[c] += (float)((g_s - mean * g_t) * inv);
+    if (a.gbeta) a.gbeta[c] += (float)g_t;
   }
 }
 

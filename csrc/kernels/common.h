@@ -103,8 +103,8 @@ template <> struct Vec8<float> {
 };
 
 // Per-channel statistics producers (conv epilogues, BN-backward reductions) add their
-// per-workgroup partial sums with fp32 atomics into kStatSlots rows (row = block index mod
-// kStatSlots, spreading contention); the fp64 finalize/reduce kernel sums the rows and
+// per-workgroup partial sums with fp32 atomics into at most kStatSlots rows (row = block index
+// mod rows, spreading contention); the fp64 finalize/reduce kernel sums the rows and
 // re-zeroes them.  Replaces per-workgroup slabs + a compaction pass.
 constexpr int kStatSlots = 64;
 
@@ -122,7 +122,11 @@ inline bool deterministic() { return deterministic_flag() != 0; }
 // slot index mask for a launch whose slot buffer holds `rows` rows (nblocks: the launch's
 // block count along the slot axis)
 inline unsigned stat_slot_mask(int rows, long nblocks) {
-  if (!deterministic()) return (unsigned)(kStatSlots - 1);
+  if (!deterministic()) {
+    // rows: a power of two <= kStatSlots (fewer for small grids: less for the finalize to read)
+    FDT_CHECK(rows >= 1 && rows <= kStatSlots && (rows & (rows - 1)) == 0, "statistics slot rows");
+    return (unsigned)(rows - 1);
+  }
   FDT_CHECK(nblocks <= rows, "deterministic mode: statistics slot buffer smaller than the block count");
   return 0xFFFFFFFFu;
 }

@@ -1,669 +1,8 @@
-// Implicit-GEMM convolution for the NHWC ResNet engine on MI355X (gfx950 / CDNA4).
-//
-// One kernel template covers every forward convolution and every data-gradient
-// (dgrad) convolution of the network:
-//
-//   C^T[ch][px] = sum_k  W[ch][k] * X[px][k],   k = (tap, ci),  px = output pixel
-//
-// The weight tile is the MFMA "A" operand (rows = output channels) and the activation
-// tile the "B" operand (columns = pixels), so an accumulator lane holds 4-channel runs
-// of ONE pixel: after a permlane32 swap every lane owns 8 consecutive channels of one
-// NHWC row and the epilogue reads/writes 16 B per lane (T21).  mfma_f32_32x32x16_bf16,
-// 4 waves (2 x 2) per 256-thread workgroup, BK = 64-element K tiles double-buffered in
-// LDS with register-staged prefetch (loads for tile k+1 are issued before the MFMAs of
-// tile k, the prologue math and LDS write happen after them, one barrier per tile),
-// XOR-swizzled LDS rows (conflict-free ds_read_b128 for the fragment reads), XCD-aware
-// workgroup remap so tiles sharing activation rows sit on one L2.  The epilogue transposes
-// the accumulators through LDS so every global access is a full row segment.
-//
-// Fusion (the reason this is not a library call):
-//  * prologue on the activation operand, applied while staging to LDS:
-//      PRO_AFFINE_ACT  x -> act(x*s[c] + t[c])   (the producer's lazy batch-norm)
-//      PRO_FOLD        g -> g*gs[c] + alpha[c] + beta[c]*y  (batch-norm backward correction;
-//                      gs lets the residual join store one un-scaled gradient for both branches)
-//    zero padding is applied AFTER the transform (the conv pads the normalised input);
-//  * epilogue:
-//      EPI_STATS   y (bf16) + per-block per-channel (sum y, sum y^2) slabs -> BN stats
-//      EPI_ACTBWD  dgrad through the producer's lazy act(x*s+t): gx = g*act'(z)*s and
-//                  per-channel (sum g_pre*x, sum g_pre) slabs
-//      EPI_STORE / EPI_ADD  plain bf16 store / accumulate into an existing gradient.
-//      EPI_JOINBWD  accumulate into the existing gradient of a residual-block output AND
-//                  run that block's join backward on it: g_pre = g*act'(out) (ReLU bit
-//                  mask or the stored CELU output), stored in place, plus the per-channel
-//                  (sum g_pre*y_res, sum g_pre, sum g_pre*y_shortcut) slot reductions that
-//                  the block's BN backward needs.  This is the dgrad that completes the
-//                  gradient (the first 1x1 of the next block), so the standalone join pass
-//                  (a full read of g + write of g_pre) disappears.
-//
-// Split-K (small-M layers: the 8x8 / 4x4 stages at the per-GPU batch of an 8-GPU run
-// have only 32-512 output tiles but K up to 4608): nsplit workgroups share one output tile,
-// each reducing a contiguous range of K tiles; all but the last to finish write their fp32
-// accumulators to a slab (in register order: [tile][split][reg/4][thread] float4, so the
-// reducer's thread t reads exactly its own registers' counterparts, coalesced), publish
-// with an agent-scope release + ticket; the last arriver acquires, adds the other slabs
-// and runs the normal fused epilogue.  Counters are reset by the last arriver.
-//
-// Strided convolutions: forward uses the input stride S; the dgrad of a stride-2
-// convolution is split by output parity into 4 dense classes (each its own tap table and
-// output row map: hi = ho*OS + oy), so no MFMA work is spent on structural zeros.
-//
-// Reference semantics being accelerated: resnet.py:72-113 (FusedConvBN forward and its
-// hand-derived backward), resnet.py:201-227 (strided conv + BatchNorm2d blocks).
-#include "common.h"
-#include "bn_math.h"
-#include <vector>
+// Host launcher of the implicit-GEMM convolution kernels (kernel: conv_igemm_impl.h; the
+// (prologue, epilogue, activation) instantiations: conv_igemm_inst_*.hip).
+#include "conv_igemm_impl.h"
 
 namespace fdt {
-namespace conv {
-
-typedef short bf16x8_t __attribute__((ext_vector_type(8)));
-typedef float f32x16 __attribute__((ext_vector_type(16)));
-
-enum Pro : int { kProNone = 0, kProAffineAct = 1, kProFold = 2 };
-enum Epi : int { kEpiStats = 0, kEpiActBwd = 1, kEpiStore = 2, kEpiAdd = 3, kEpiJoinBwd = 4 };
-
-struct ConvArgs {
-  const bf16* x;     // activation operand [Nb][Hi][Wi][Cx]   (PRO_FOLD: the gradient G)
-  const bf16* x2;    // PRO_FOLD: the producer output Y (same shape as x)
-  const float* ps;   // prologue per-channel scale: s (AFFINE_ACT) or alpha (FOLD)   [Cx]
-  const float* pt;   // prologue per-channel shift: t (AFFINE_ACT) or beta  (FOLD)   [Cx]
-  const float* pg;   // FOLD: per-channel scale of g (nullptr = 1): g*pg + alpha + beta*y    [Cx]
-  const bf16* w;     // packed weights [Cout][ldw], k-index = wt[tap]*Cx + ci
-  bf16* out;         // [Nb][Hout][Wout][Cout]
-  float* part;       // statistics slots [slots][NQ][Cout], fp32 atomics (zeroed by the consumer)
-  unsigned slot_mask;  // slot = row block & slot_mask (deterministic mode: no wrap, one writer per slot)
-  int det;             // deterministic mode: the split-K reducer sums every split in split order
-  const bf16* ex;    // ACTBWD: producer raw output x (shape of out); JOINBWD: residual-branch y
-  const float* es;   // ACTBWD: producer scale s [Cout]
-  const float* et;   // ACTBWD: producer shift t [Cout]
-  const uint8_t* jmask;  // JOINBWD: ReLU join bit mask (bit i of byte e/8 = out[e] > 0), or nullptr
-  const bf16* jyb;       // JOINBWD: shortcut-branch y (nullptr: identity shortcut)
-  const bf16* jout;      // JOINBWD: join output (CELU joins; read when jmask is nullptr)
-  long M;            // Nb*Ho*Wo GEMM rows
-  int Hi, Wi, Cx, log2Cx;
-  int Ho, Wo, S;
-  int ntaps, K, Cout, ldw;
-  int Hout, Wout, OS, oy, ox;
-  int pro_act;
-  float pro_alpha;
-  int epi_act;
-  float epi_alpha;
-  int nbm, nbn;
-  int nsplit, kps;   // split-K: workgroups per output tile, K tiles per split
-  float* slab;       // split-K partials [tiles][nsplit][TN*TM*4][256] float4
-  int* cnt;          // split-K tickets [tiles], zero between launches
-  int8_t dh[12], dw[12], wt[12];
-  long Nb_HiWi_Cx_bytes;  // bytes of the activation operand(s)
-  long w_bytes;           // bytes of the packed weights
-};
-
-__device__ __forceinline__ uint32_t pk_bf16(float lo, float hi) { return pack_bf16x2(lo, hi); }
-
-template <int CPR>
-__device__ __forceinline__ int swz(int row) {
-  // conflict-free ds_read_b128 of one 16-B chunk from 32 consecutive rows (see file header)
-  if constexpr (CPR == 8) return (row >> 1) & 7;
-  else return (row >> 2) & 3;
-}
-
-__device__ __forceinline__ int xcd_remap(int bid, int nblk) {
-  const int q = nblk >> 3, r = nblk & 7, xcd = bid & 7;
-  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
-}
-
-__device__ __forceinline__ void swap32(float& a, float& b) {
-  auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(a), __float_as_uint(b), false, false);
-  a = __uint_as_float(r[0]);
-  b = __uint_as_float(r[1]);
-}
-
-// Activation helpers specialised at compile time (ACT: 0 none, 1 ReLU, 2 CELU(alpha)).
-template <int ACT>
-__device__ __forceinline__ float actf(float z, float alpha, float inv_alpha) {
-  if constexpr (ACT == kActRelu) return fmaxf(z, 0.f);
-  else if constexpr (ACT == kActCelu) return z > 0.f ? z : alpha * (__expf(z * inv_alpha) - 1.f);
-  else return z;
-}
-template <int ACT>
-__device__ __forceinline__ float actg(float z, float inv_alpha) {
-  if constexpr (ACT == kActRelu) return z > 0.f ? 1.f : 0.f;
-  else if constexpr (ACT == kActCelu) return z > 0.f ? 1.f : __expf(z * inv_alpha);
-  else return 1.f;
-}
-// act'(z) from the activation OUTPUT o = act(z) (CELU: exp(z/alpha) = o/alpha + 1 for z <= 0)
-template <int ACT>
-__device__ __forceinline__ float actg_out(float o, float inv_alpha) {
-  if constexpr (ACT == kActRelu) return o > 0.f ? 1.f : 0.f;
-  else if constexpr (ACT == kActCelu) return o > 0.f ? 1.f : fmaf(o, inv_alpha, 1.f);
-  else return 1.f;
-}
-
-__device__ __forceinline__ uint4 ld_buf16(__amdgpu_buffer_rsrc_t r, uint32_t byte_off) {
-  auto v = __builtin_amdgcn_raw_buffer_load_b128(r, byte_off, 0, 0);
-  return *reinterpret_cast<uint4*>(&v);
-}
-
-constexpr uint32_t kOOB = 0xFFFFFFF0u;  // byte offset past any buffer: the load returns zeros
-
-template <int BM, int BN, int BK, int PRO, int EPI, bool PURE, int ACT>
-__global__ __launch_bounds__(256) void igemm_kernel(const ConvArgs a) {
-  constexpr int CPR = BK / 8;        // 16-B chunks per LDS row
-  constexpr int RPR = 256 / CPR;     // rows covered by one load round
-  constexpr int NXL = BM / RPR;      // activation chunks per thread per tile
-  constexpr int NWL = BN / RPR;      // weight chunks per thread per tile
-  constexpr int TM = BM / 64, TN = BN / 64;
-  constexpr int XT = BM * BK, WT = BN * BK;
-  static_assert(NXL >= 1 && NWL >= 1, "tile too small for 256 threads");
-
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int nkt = (a.K + BK - 1) / BK;
-  constexpr bool HASPRO = PRO == kProAffineAct || PRO == kProFold;
-  constexpr int NPRM = PRO == kProFold ? 3 : (HASPRO ? 2 : 0);
-  constexpr int NQ = EPI == kEpiJoinBwd ? 3 : 2;                       // statistics rows
-  // LDS: [prologue params | per-wave statistics | tap tables | K tiles, reused as the
-  // epilogue's staging area] (the header size must match lds_bytes() on the host)
-  float* pst = reinterpret_cast<float*>(smem);                         // [2|3][Cx] (PRO != none)
-  float* red = pst + NPRM * a.Cx;                                      // [4 waves][NQ][BN]
-  int* tapt = reinterpret_cast<int*>(red + 4 * NQ * BN);               // [12]: tap pixel offset
-  int* tapw = tapt + 12;                                               // [12]: dh | dw<<8 | wt<<16
-  const int hdr = ((NPRM * a.Cx + 4 * NQ * BN + 24) * 4 + 15) & ~15;
-  bf16* tiles = reinterpret_cast<bf16*>(smem + hdr);                   // [nbuf][WT + XT]
-
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int wn = wid & 1, wm = wid >> 1;
-  // a tile's splits are consecutive ids -> the same XCD after the remap
-  const int rid = xcd_remap(blockIdx.x, a.nbm * a.nbn * a.nsplit);
-  const int id = rid / a.nsplit, split = rid - id * a.nsplit;
-  const int bn = id % a.nbn, bm = id / a.nbn;
-  const long m0 = (long)bm * BM;
-  const int n0 = bn * BN;
-  const float inv_alpha = ACT == kActCelu ? 1.f / (PRO == kProAffineAct ? a.pro_alpha : a.epi_alpha) : 1.f;
-  static_assert(!(PRO == kProAffineAct && EPI == kEpiJoinBwd), "one activation per instantiation");
-
-  // buffer descriptors (wave-uniform, built from kernel arguments): 32-bit offsets and
-  // hardware bounds checking -> zero padding / K tails need no branches
-  const __amdgpu_buffer_rsrc_t rx_d = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)a.x, (short)0, (int)(a.Nb_HiWi_Cx_bytes), 0x00020000);
-  const __amdgpu_buffer_rsrc_t ry_d = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)(PRO == kProFold ? a.x2 : a.x), (short)0, (int)(a.Nb_HiWi_Cx_bytes), 0x00020000);
-  const __amdgpu_buffer_rsrc_t rw_d = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)a.w, (short)0, (int)(a.w_bytes), 0x00020000);
-
-  // ---- per-thread activation rows (fixed across K tiles): pixel index of tap (0,0)
-  const int cc = tid % CPR;  // this thread's 16-B chunk column inside a K tile
-  int pixb[NXL], ohs[NXL], ows[NXL];
-  bool rv[NXL];
-#pragma unroll
-  for (int j = 0; j < NXL; ++j) {
-    const long m = m0 + tid / CPR + j * RPR;
-    rv[j] = m < a.M;
-    if constexpr (PURE) {
-      pixb[j] = (int)m;
-      ohs[j] = ows[j] = 0;
-    } else {
-      const int hw = a.Ho * a.Wo;
-      const int mi = rv[j] ? (int)m : 0;
-      const int n = mi / hw;
-      const int rem = mi - n * hw;
-      const int oh = rem / a.Wo, ow = rem - (rem / a.Wo) * a.Wo;
-      ohs[j] = oh * a.S;
-      ows[j] = ow * a.S;
-      pixb[j] = (n * a.Hi + ohs[j]) * a.Wi + ows[j];
-    }
-  }
-
-  // one register stage = the global loads of one K tile (staged to LDS after the MFMAs
-  // of the previous tile).  Two stages alternate so that the loads of tile k+2 are in
-  // flight during the MFMAs of tiles k and k+1.
-  struct Stage {
-    uint4 rx[NXL], rx2[PRO == kProFold ? NXL : 1], rw[NWL];
-    bool xv[NXL];
-    int kci;
-  };
-
-  // Loads are issued unconditionally (a K tile past this split's range, or past K, reads
-  // the OOB offset and returns zeros): no branch around a load, so hipcc's waitcnt pass
-  // can count the two in-flight stages exactly (vmcnt(N), not vmcnt(0)) -- a branch-guarded
-  // prefetch degenerates to a full-latency wait every K tile.
-  auto load_tile = [&](Stage& S, int kt, bool live) {
-    const int k = kt * BK + cc * 8;
-    const int tap = k >> a.log2Cx;
-    const int ci = k & (a.Cx - 1);
-    S.kci = ci;
-    const bool tok = live && tap < a.ntaps;
-    int dh = 0, dw = 0, wt = 0, toff = 0;
-    if constexpr (!PURE) {
-      const int tq = tap < 12 ? tap : 11;  // branch-free LDS lookup (masked by tok below)
-      const int e = tapw[tq];
-      dh = (int)(int8_t)(e & 0xff);
-      dw = (int)(int8_t)((e >> 8) & 0xff);
-      wt = (e >> 16) & 0xff;
-      toff = tapt[tq];
-    }
-#pragma unroll
-    for (int j = 0; j < NXL; ++j) {
-      bool v = rv[j] & tok;  // bitwise: no short-circuit branch around the load
-      if constexpr (!PURE)
-        v = v & ((unsigned)(ohs[j] + dh) < (unsigned)a.Hi) & ((unsigned)(ows[j] + dw) < (unsigned)a.Wi);
-      S.xv[j] = v;
-      const uint32_t off = v ? (((uint32_t)(pixb[j] + toff) << a.log2Cx) + ci) * 2u : kOOB;
-      S.rx[j] = ld_buf16(rx_d, off);
-      if constexpr (PRO == kProFold) S.rx2[j] = ld_buf16(ry_d, off);
-    }
-    const uint32_t wk = (uint32_t)((PURE ? 0 : wt) * a.Cx + ci);
-#pragma unroll
-    for (int j = 0; j < NWL; ++j) {
-      const int row = tid / CPR + j * RPR;
-      S.rw[j] = ld_buf16(rw_d, tok ? ((uint32_t)(n0 + row) * (uint32_t)a.ldw + wk) * 2u : kOOB);
-    }
-  };
-
-  auto store_tile = [&](const Stage& S, int buf) {
-    bf16* Wl = tiles + buf * (WT + XT);
-    bf16* Xl = Wl + WT;
-#pragma unroll
-    for (int j = 0; j < NWL; ++j) {
-      const int row = tid / CPR + j * RPR;
-      *reinterpret_cast<uint4*>(Wl + row * BK + 8 * (cc ^ swz<CPR>(row))) = S.rw[j];
-    }
-    float sv[8], tv[8], gv[8];
-    if constexpr (PRO == kProFold) {
-      const float4* gp = reinterpret_cast<const float4*>(pst + 2 * a.Cx + S.kci);
-      float4 g0 = gp[0], g1 = gp[1];
-      gv[0] = g0.x; gv[1] = g0.y; gv[2] = g0.z; gv[3] = g0.w; gv[4] = g1.x; gv[5] = g1.y; gv[6] = g1.z; gv[7] = g1.w;
-    }
-    if constexpr (HASPRO) {
-      const float4* sp = reinterpret_cast<const float4*>(pst + S.kci);
-      const float4* tp = reinterpret_cast<const float4*>(pst + a.Cx + S.kci);
-      float4 s0 = sp[0], s1 = sp[1], t0 = tp[0], t1 = tp[1];
-      sv[0] = s0.x; sv[1] = s0.y; sv[2] = s0.z; sv[3] = s0.w; sv[4] = s1.x; sv[5] = s1.y; sv[6] = s1.z; sv[7] = s1.w;
-      tv[0] = t0.x; tv[1] = t0.y; tv[2] = t0.z; tv[3] = t0.w; tv[4] = t1.x; tv[5] = t1.y; tv[6] = t1.z; tv[7] = t1.w;
-    }
-#pragma unroll
-    for (int j = 0; j < NXL; ++j) {
-      const int row = tid / CPR + j * RPR;
-      uint4 o = S.rx[j];
-      if constexpr (PRO == kProAffineAct) {
-        // act(x*s+t), then zero where the conv pads (select, no branch)
-        float v[8];
-        const uint32_t u[4] = {o.x, o.y, o.z, o.w};
-#pragma unroll
-        for (int q = 0; q < 4; ++q) { v[2 * q] = bf16_lo(u[q]); v[2 * q + 1] = bf16_hi(u[q]); }
-#pragma unroll
-        for (int q = 0; q < 8; ++q) v[q] = actf<ACT>(fmaf(v[q], sv[q], tv[q]), a.pro_alpha, inv_alpha);
-        o = make_uint4(pk_bf16(v[0], v[1]), pk_bf16(v[2], v[3]), pk_bf16(v[4], v[5]), pk_bf16(v[6], v[7]));
-        if (!S.xv[j]) o = make_uint4(0, 0, 0, 0);
-      } else if constexpr (PRO == kProFold) {
-        // g + alpha + beta*y (padding: g = y = 0 from the bounds-checked load -> masked)
-        float g[8], y[8];
-        const uint32_t u[4] = {o.x, o.y, o.z, o.w};
-        const uint32_t uy[4] = {S.rx2[j].x, S.rx2[j].y, S.rx2[j].z, S.rx2[j].w};
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          g[2 * q] = bf16_lo(u[q]); g[2 * q + 1] = bf16_hi(u[q]);
-          y[2 * q] = bf16_lo(uy[q]); y[2 * q + 1] = bf16_hi(uy[q]);
-        }
-#pragma unroll
-        for (int q = 0; q < 8; ++q) g[q] = fmaf(g[q], gv[q], fmaf(tv[q], y[q], sv[q]));
-        o = make_uint4(pk_bf16(g[0], g[1]), pk_bf16(g[2], g[3]), pk_bf16(g[4], g[5]), pk_bf16(g[6], g[7]));
-        if (!S.xv[j]) o = make_uint4(0, 0, 0, 0);
-      }
-      *reinterpret_cast<uint4*>(Xl + row * BK + 8 * (cc ^ swz<CPR>(row))) = o;
-    }
-  };
-
-  f32x16 acc[TN][TM];
-#pragma unroll
-  for (int i = 0; i < TN; ++i)
-#pragma unroll
-    for (int j = 0; j < TM; ++j)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
-
-  auto compute = [&](int buf) {
-    const bf16* Wl = tiles + buf * (WT + XT);
-    const bf16* Xl = Wl + WT;
-#pragma unroll
-    for (int ks = 0; ks < BK / 16; ++ks) {
-      const int ch = ks * 2 + (lane >> 5);
-      bf16x8_t wf[TN], xf[TM];
-#pragma unroll
-      for (int i = 0; i < TN; ++i) {
-        const int row = wn * (BN / 2) + i * 32 + (lane & 31);
-        wf[i] = *reinterpret_cast<const bf16x8_t*>(Wl + row * BK + 8 * (ch ^ swz<CPR>(row)));
-      }
-#pragma unroll
-      for (int j = 0; j < TM; ++j) {
-        const int row = wm * (BM / 2) + j * 32 + (lane & 31);
-        xf[j] = *reinterpret_cast<const bf16x8_t*>(Xl + row * BK + 8 * (ch ^ swz<CPR>(row)));
-      }
-#pragma unroll
-      for (int i = 0; i < TN; ++i)
-#pragma unroll
-        for (int j = 0; j < TM; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wf[i], xf[j], acc[i][j], 0, 0, 0);
-    }
-  };
-
-  // this split's K tiles [kb, kb + nk)
-  const int kb = split * a.kps;
-  const int nk = min(nkt - kb, a.kps);
-
-  {
-  // prologue: tile 0 -> LDS buf 0; tile 1 pending in B; tile 2 in flight in A.
-  // 1x1 convolutions address their operands without the LDS tap table, so their first two
-  // K tiles are requested BEFORE the LDS setup (prologue parameters, tap table) and its
-  // barrier: the workgroup pays one memory latency at start-up instead of two (these
-  // memory-bound layers run many short workgroups).
-  Stage SA, SB;
-  if constexpr (PURE) {
-    if (nk > 0) {
-      load_tile(SA, kb, true);
-      __builtin_amdgcn_sched_barrier(0);  // issue order SA, SB, SA' pinned (exact vmcnt counting)
-      load_tile(SB, kb + 1, nk > 1);
-      __builtin_amdgcn_sched_barrier(0);
-    }
-  }
-  if constexpr (HASPRO) {
-    for (int i = tid; i < a.Cx; i += 256) {
-      pst[i] = a.ps[i];
-      pst[a.Cx + i] = a.pt[i];
-      if constexpr (PRO == kProFold) pst[2 * a.Cx + i] = a.pg ? a.pg[i] : 1.f;
-    }
-  }
-  if (tid < 12) {
-    const int dh = a.dh[tid], dw = a.dw[tid];
-    tapt[tid] = dh * a.Wi + dw;
-    tapw[tid] = (int)(uint8_t)a.dh[tid] | ((int)(uint8_t)a.dw[tid] << 8) | ((int)(uint8_t)a.wt[tid] << 16);
-  }
-
-  __syncthreads();
-  if constexpr (!PURE) {
-    if (nk > 0) {
-      load_tile(SA, kb, true);
-      __builtin_amdgcn_sched_barrier(0);
-      load_tile(SB, kb + 1, nk > 1);
-      __builtin_amdgcn_sched_barrier(0);
-    }
-  }
-  if (nk > 0) {
-    store_tile(SA, 0);
-    load_tile(SA, kb + 2, nk > 2);
-    __builtin_amdgcn_sched_barrier(0);
-    __syncthreads();
-  }
-  for (int kt = 0; kt < nk; kt += 2) {
-    // even tile kt in buf 0; SB holds kt+1, SA holds kt+2 (in flight)
-    compute(0);
-    if (kt + 1 >= nk) break;
-    store_tile(SB, 1);
-    __syncthreads();
-    load_tile(SB, kb + kt + 3, kt + 3 < nk);
-    __builtin_amdgcn_sched_barrier(0);  // keep the prefetch issued ahead of the MFMAs
-    // odd tile kt+1 in buf 1; SA holds kt+2, SB holds kt+3 (in flight)
-    compute(1);
-    if (kt + 2 >= nk) break;
-    store_tile(SA, 0);
-    __syncthreads();
-    load_tile(SA, kb + kt + 4, kt + 4 < nk);
-    __builtin_amdgcn_sched_barrier(0);
-  }
-  }
-
-  // ------------------------------------------------------------------ split-K combine
-  if (a.nsplit > 1) {
-    constexpr int NR4 = TN * TM * 4;  // float4 registers per thread
-    float4* slab = reinterpret_cast<float4*>(a.slab) + (long)id * a.nsplit * NR4 * 256;
-    {
-      float4* mine = slab + (long)split * NR4 * 256 + tid;
-#pragma unroll
-      for (int i = 0; i < TN; ++i)
-#pragma unroll
-        for (int j = 0; j < TM; ++j)
-#pragma unroll
-          for (int q = 0; q < 4; ++q)
-            mine[((i * TM + j) * 4 + q) * 256] =
-                make_float4(acc[i][j][4 * q], acc[i][j][4 * q + 1], acc[i][j][4 * q + 2], acc[i][j][4 * q + 3]);
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    int* flag = reinterpret_cast<int*>(red);
-    if (tid == 0) {
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      const int t = __hip_atomic_fetch_add(&a.cnt[id], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      const int last = t == a.nsplit - 1;
-      if (last) {
-        __hip_atomic_store(&a.cnt[id], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      }
-      flag[0] = last;
-    }
-    __syncthreads();
-    const int last = flag[0];
-    __syncthreads();  // red is reused by the epilogue
-    if (!last) return;
-    if (a.det) {
-      // fixed summation order whichever split arrived last (its own slab was written too)
-#pragma unroll
-      for (int i = 0; i < TN; ++i)
-#pragma unroll
-        for (int j = 0; j < TM; ++j)
-#pragma unroll
-          for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
-    }
-    for (int sp = 0; sp < a.nsplit; ++sp) {
-      if (sp == split && !a.det) continue;
-      const float4* other = slab + (long)sp * NR4 * 256 + tid;
-#pragma unroll
-      for (int i = 0; i < TN; ++i)
-#pragma unroll
-        for (int j = 0; j < TM; ++j)
-#pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            const float4 v = other[((i * TM + j) * 4 + q) * 256];
-            acc[i][j][4 * q] += v.x;
-            acc[i][j][4 * q + 1] += v.y;
-            acc[i][j][4 * q + 2] += v.z;
-            acc[i][j][4 * q + 3] += v.w;
-          }
-    }
-  }
-
-  // ------------------------------------------------------------------ epilogue
-  // The accumulators are transposed through LDS before touching memory: a lane's MFMA
-  // result is 8 channels of ONE pixel, so a direct store / load covers 32 pixels x 32 B per
-  // wave instruction (32 partial cache lines).  Staged as fp32 rows [64 pixels][BN] (one
-  // pass per 32-pixel block j), each thread then owns 8 channels of whole rows and every
-  // wave instruction moves full contiguous 128-256 B row segments; per-channel statistics
-  // reduce over a thread's rows, then across the lanes sharing its channels (shuffles),
-  // then across the 4 waves in LDS.  Rows padded by 4 floats: conflict-free ds_write_b128
-  // of the accumulator layout and ds_read_b128 of the row layout.
-  {
-    constexpr int SW = BN + 4;     // staged row stride (floats)
-    constexpr int CG = BN / 8;     // 8-channel groups per row
-    constexpr int RPS = 256 / CG;  // rows per sweep
-    constexpr int NSW = 64 / RPS;  // sweeps per 64-row pass
-    constexpr bool STATS = EPI == kEpiStats || EPI == kEpiActBwd || EPI == kEpiJoinBwd;
-    const int h = lane >> 5;
-    float* stg = reinterpret_cast<float*>(smem + hdr);
-    const int cg = tid % CG, rs = tid / CG;
-    const int c = n0 + cg * 8;  // this thread's 8 output channels
-    const bool dense = a.OS == 1 && a.oy == 0 && a.ox == 0 && a.Hout == a.Ho && a.Wout == a.Wo;
-    float sv[8], tv[8];
-    if constexpr (EPI == kEpiActBwd) {
-      const float4* sp = reinterpret_cast<const float4*>(a.es + c);
-      const float4* tp = reinterpret_cast<const float4*>(a.et + c);
-      const float4 s0 = sp[0], s1 = sp[1], t0 = tp[0], t1 = tp[1];
-      sv[0] = s0.x; sv[1] = s0.y; sv[2] = s0.z; sv[3] = s0.w; sv[4] = s1.x; sv[5] = s1.y; sv[6] = s1.z; sv[7] = s1.w;
-      tv[0] = t0.x; tv[1] = t0.y; tv[2] = t0.z; tv[3] = t0.w; tv[4] = t1.x; tv[5] = t1.y; tv[6] = t1.z; tv[7] = t1.w;
-    }
-    float q0[8], q1[8], q2[8];
-#pragma unroll
-    for (int k = 0; k < 8; ++k) { q0[k] = 0.f; q1[k] = 0.f; q2[k] = 0.f; }
-    __syncthreads();  // every wave is done with the K tiles (and the split-K flag)
-#pragma unroll
-    for (int j = 0; j < TM; ++j) {
-      // ---- stage accumulator block j: local row = wm*32 + pixel, 8 channels per (i, p)
-#pragma unroll
-      for (int i = 0; i < TN; ++i) {
-#pragma unroll
-        for (int p = 0; p < 2; ++p) {
-          const int g = 2 * p;
-          float v[8];
-#pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            float lo = acc[i][j][4 * g + q], hi = acc[i][j][4 * g + 4 + q];
-            swap32(lo, hi);
-            v[q] = lo;
-            v[4 + q] = hi;
-          }
-          float* dst = stg + (wm * 32 + (lane & 31)) * SW + wn * (BN / 2) + i * 32 + 16 * p + 8 * h;
-          *reinterpret_cast<float4*>(dst) = make_float4(v[0], v[1], v[2], v[3]);
-          *reinterpret_cast<float4*>(dst + 4) = make_float4(v[4], v[5], v[6], v[7]);
-        }
-      }
-      __syncthreads();
-      // ---- rows of this pass: 8 channels x NSW rows per thread
-#pragma unroll
-      for (int sw = 0; sw < NSW; ++sw) {
-        const int lr = rs + sw * RPS;
-        const long m = m0 + (lr >> 5) * (BM / 2) + j * 32 + (lr & 31);
-        if (m < a.M) {
-          uint32_t orow;
-          if (dense) {
-            orow = (uint32_t)m;
-          } else {
-            const int mi = (int)m, hw = a.Ho * a.Wo;
-            const int n = mi / hw, rem = mi - n * hw;
-            const int oh = rem / a.Wo, ow = rem - oh * a.Wo;
-            orow = (uint32_t)((n * a.Hout + oh * a.OS + a.oy) * a.Wout + ow * a.OS + a.ox);
-          }
-          const uint32_t e = orow * (uint32_t)a.Cout + c;
-          const float4 va = *reinterpret_cast<const float4*>(stg + lr * SW + cg * 8);
-          const float4 vb = *reinterpret_cast<const float4*>(stg + lr * SW + cg * 8 + 4);
-          float v[8] = {va.x, va.y, va.z, va.w, vb.x, vb.y, vb.z, vb.w};
-          if constexpr (EPI == kEpiStats) {
-#pragma unroll
-            for (int k = 0; k < 8; ++k) { q0[k] += v[k]; q1[k] = fmaf(v[k], v[k], q1[k]); }
-            Vec8<bf16>::store(a.out + e, v);
-          } else if constexpr (EPI == kEpiActBwd) {
-            float x8[8];
-            Vec8<bf16>::load(a.ex + e, x8);
-#pragma unroll
-            for (int k = 0; k < 8; ++k) {
-              const float gp = v[k] * actg<ACT>(fmaf(x8[k], sv[k], tv[k]), inv_alpha);
-              v[k] = gp * sv[k];
-              q0[k] = fmaf(gp, x8[k], q0[k]);
-              q1[k] += gp;
-            }
-            Vec8<bf16>::store(a.out + e, v);
-          } else if constexpr (EPI == kEpiJoinBwd) {
-            float e8[8], ya[8], yb[8], o8[8];
-            Vec8<bf16>::load(a.out + e, e8);
-            Vec8<bf16>::load(a.ex + e, ya);
-            const bool hb = a.jyb != nullptr;
-            if (hb) Vec8<bf16>::load(a.jyb + e, yb);
-            uint32_t mk = 0;
-            if constexpr (ACT == kActRelu) mk = a.jmask[e >> 3];
-            else Vec8<bf16>::load(a.jout + e, o8);
-#pragma unroll
-            for (int k = 0; k < 8; ++k) {
-              const float gv = v[k] + e8[k];
-              float gp;
-              if constexpr (ACT == kActRelu) gp = ((mk >> k) & 1u) ? gv : 0.f;
-              else gp = gv * actg_out<ACT>(o8[k], inv_alpha);
-              v[k] = gp;
-              q0[k] = fmaf(gp, ya[k], q0[k]);
-              q1[k] += gp;
-              if (hb) q2[k] = fmaf(gp, yb[k], q2[k]);
-            }
-            Vec8<bf16>::store(a.out + e, v);
-          } else if constexpr (EPI == kEpiAdd) {
-            float e8[8];
-            Vec8<bf16>::load(a.out + e, e8);
-#pragma unroll
-            for (int k = 0; k < 8; ++k) v[k] += e8[k];
-            Vec8<bf16>::store(a.out + e, v);
-          } else {
-            Vec8<bf16>::store(a.out + e, v);
-          }
-        }
-      }
-      if (j + 1 < TM) __syncthreads();  // the next pass overwrites the staging rows
-    }
-    if constexpr (STATS) {
-      // lanes l, l + CG, l + 2CG, ... of a wave hold the same channels
-#pragma unroll
-      for (int o = CG; o < 64; o <<= 1) {
-#pragma unroll
-        for (int k = 0; k < 8; ++k) {
-          q0[k] += __shfl_xor(q0[k], o, 64);
-          q1[k] += __shfl_xor(q1[k], o, 64);
-          if constexpr (NQ == 3) q2[k] += __shfl_xor(q2[k], o, 64);
-        }
-      }
-      if (lane < CG) {
-        float* rw = red + wid * NQ * BN + cg * 8;
-#pragma unroll
-        for (int k = 0; k < 8; ++k) {
-          rw[k] = q0[k];
-          rw[BN + k] = q1[k];
-          if constexpr (NQ == 3) rw[2 * BN + k] = q2[k];
-        }
-      }
-      __syncthreads();
-      for (int e = tid; e < NQ * BN; e += 256) {
-        const float t = red[e] + red[NQ * BN + e] + red[2 * NQ * BN + e] + red[3 * NQ * BN + e];
-        const int q = e / BN, cc2 = e - q * BN;
-        atomicAdd(&a.part[((long)(bm & a.slot_mask) * NQ + q) * a.Cout + n0 + cc2], t);
-      }
-    }
-  }
-}
-
-// ---------------------------------------------------------------------- host side
-struct Cfg {
-  int BM, BN;
-};
-
-template <int BM, int BN, int BK, int PRO, int EPI, bool PURE, int ACT>
-static void launch_one(const ConvArgs& a, size_t lds, hipStream_t st) {
-  auto kern = igemm_kernel<BM, BN, BK, PRO, EPI, PURE, ACT>;
-  static size_t attr_set = 64 * 1024;  // default dynamic-LDS limit; raise only when needed
-  if (lds > attr_set) {
-    FDT_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
-                                      (int)lds));
-    attr_set = lds;
-  }
-  hipLaunchKernelGGL(kern, dim3(a.nbm * a.nbn * a.nsplit), dim3(256), lds, st, a);
-  FDT_LAUNCH_CHECK();
-}
-
-template <int BM, int BN, int BK, int PRO, int EPI, int ACT>
-static void launch_pure(const ConvArgs& a, bool pure, size_t lds, hipStream_t st) {
-  if (pure) launch_one<BM, BN, BK, PRO, EPI, true, ACT>(a, lds, st);
-  else launch_one<BM, BN, BK, PRO, EPI, false, ACT>(a, lds, st);
-}
-
-template <int PRO, int EPI, int ACT>
-static void launch_tile(const ConvArgs& a, int BM, int BN, int BK, bool pure, hipStream_t st) {
-  const int nkt = (a.K + BK - 1) / BK;
-  const size_t nbuf = nkt > 1 ? 2 : 1;
-  // header (must match the kernel's hdr) + max(K tiles, epilogue staging [64][BN + 4] fp32)
-  const int nprm = PRO == kProFold ? 3 : ((PRO == kProAffineAct) ? 2 : 0);
-  const size_t hdr = (((size_t)nprm * a.Cx + 4 * (EPI == kEpiJoinBwd ? 3 : 2) * BN + 24) * 4 + 15) & ~(size_t)15;
-  const size_t tiles = nbuf * (BM + BN) * BK * 2, stage = (size_t)64 * (BN + 4) * 4;
-  size_t lds = hdr + (tiles > stage ? tiles : stage);
-#define FDT_T(BM_, BN_, BK_) \
-  if (BM == BM_ && BN == BN_ && BK == BK_) { launch_pure<BM_, BN_, BK_, PRO, EPI, ACT>(a, pure, lds, st); return; }
-  FDT_T(128, 128, 64) FDT_T(128, 64, 64) FDT_T(64, 128, 64) FDT_T(64, 64, 64) FDT_T(256, 64, 64)
-  FDT_T(128, 128, 32) FDT_T(128, 64, 32) FDT_T(64, 128, 32) FDT_T(64, 64, 32) FDT_T(256, 128, 32)
-#undef FDT_T
-  FDT_CHECK(false, "unsupported conv tile");
-}
-
-}  // namespace conv
 
 // Python-facing launcher.  taps: list of (dh, dw, wt) triples encoded as int8 arrays.
 void conv_igemm(uint64_t x, uint64_t x2, uint64_t ps, uint64_t pt, uint64_t pg, uint64_t w, uint64_t out, uint64_t part,
@@ -733,26 +72,9 @@ void conv_igemm(uint64_t x, uint64_t x2, uint64_t ps, uint64_t pt, uint64_t pg, 
   hipStream_t st = as_stream(stream);
   if (a.M == 0) return;
   const int act = pro == kProAffineAct ? pro_act : ((epi == kEpiActBwd || epi == kEpiJoinBwd) ? epi_act : 0);
-#define FDT_CONV_CASE(P_, E_, A_) \
-  if (pro == P_ && epi == E_ && act == A_) { launch_tile<P_, E_, A_>(a, BM, BN, BK, pure, st); return; }
-  FDT_CONV_CASE(kProNone, kEpiStats, kActNone)
-  FDT_CONV_CASE(kProAffineAct, kEpiStats, kActRelu)
-  FDT_CONV_CASE(kProAffineAct, kEpiStats, kActCelu)
-  FDT_CONV_CASE(kProAffineAct, kEpiStats, kActNone)
-  FDT_CONV_CASE(kProFold, kEpiActBwd, kActRelu)
-  FDT_CONV_CASE(kProFold, kEpiActBwd, kActCelu)
-  FDT_CONV_CASE(kProFold, kEpiActBwd, kActNone)
-  FDT_CONV_CASE(kProFold, kEpiStore, kActNone)
-  FDT_CONV_CASE(kProFold, kEpiAdd, kActNone)
-  // dgrad on a pre-folded gradient (the engine materialises g + alpha + beta*y once for 3x3)
-  FDT_CONV_CASE(kProNone, kEpiActBwd, kActRelu)
-  FDT_CONV_CASE(kProNone, kEpiActBwd, kActCelu)
-  FDT_CONV_CASE(kProNone, kEpiStore, kActNone)
-  FDT_CONV_CASE(kProNone, kEpiAdd, kActNone)
-  // the dgrad that completes a residual block's output gradient + that block's join backward
-  FDT_CONV_CASE(kProFold, kEpiJoinBwd, kActRelu)
-  FDT_CONV_CASE(kProFold, kEpiJoinBwd, kActCelu)
-#undef FDT_CONV_CASE
+  if (launch_cases_fwd(pro, epi, act, a, BM, BN, BK, pure, st) || launch_cases_fold(pro, epi, act, a, BM, BN, BK, pure, st) ||
+      launch_cases_join(pro, epi, act, a, BM, BN, BK, pure, st) || launch_cases_plain(pro, epi, act, a, BM, BN, BK, pure, st))
+    return;
   FDT_CHECK(false, "unsupported (prologue, epilogue) combination");
 }
 

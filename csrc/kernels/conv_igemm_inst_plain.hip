@@ -1,0 +1,19 @@
+// Instantiations of the implicit-GEMM conv kernel: dgrad on a pre-folded gradient (3x3 convs).
+#include "conv_igemm_impl.h"
+
+namespace fdt {
+namespace conv {
+
+bool launch_cases_plain(int pro, int epi, int act, const ConvArgs& a, int BM, int BN, int BK, bool pure, hipStream_t st) {
+#define FDT_CONV_CASE(P_, E_, A_) \
+  if (pro == P_ && epi == E_ && act == A_) { launch_tile<P_, E_, A_>(a, BM, BN, BK, pure, st); return true; }
+  FDT_CONV_CASE(kProNone, kEpiActBwd, kActRelu)
+  FDT_CONV_CASE(kProNone, kEpiActBwd, kActCelu)
+  FDT_CONV_CASE(kProNone, kEpiStore, kActNone)
+  FDT_CONV_CASE(kProNone, kEpiAdd, kActNone)
+#undef FDT_CONV_CASE
+  return false;
+}
+
+}  // namespace conv
+}  // namespace fdt

@@ -181,13 +181,29 @@ def out_hw(h, w, shp: ConvShape):
 
 STAT_SLOTS = 64  # csrc/kernels/common.h kStatSlots
 
+def _finalize_standalone(nat, kind, part, nq, C, fptr, fval):
+    """The statistics consumer launched right after its producer conv: kind 1 = forward
+    batch-norm finalize, kind 2 = BN-backward coefficients.  (Folding it into the conv as a
+    last-arriver epilogue was measured slower: README, performance notes.)"""
+    if kind == 1:  # fptr: gamma beta rm rv nbt s t sm sa ; fval: mode eps momentum count
+        nat.stats_finalize(part.data_ptr(), part.shape[0], C, float(fval[3]), int(fval[0]), float(fval[1]),
+                           float(fval[2]), *fptr[:9], 1, _sp())
+    else:  # per unit: fptr sm sa gamma alpha beta gg gb ; fval mode eps count
+        a = [int(fval[0]), float(fval[1]), float(fval[2]), *fptr[0:7]]
+        b = [int(fval[3]), float(fval[4]), float(fval[5]), *fptr[7:14]]
+        nat.stats_bwd_finalize(part.data_ptr(), part.shape[0], nq, C, *a, *b, _sp())
+
 
 def slot_rows(M: int | None = None) -> int:
-    """Statistics slot rows for a producer over M output rows: STAT_SLOTS (rows shared by
-    workgroups, block index mod 64), or in deterministic mode one row per workgroup
-    (conv row blocks are >= 64 rows; the BN-backward kernels cap their grid to the rows)."""
+    """Statistics slot rows for a producer over M output rows: rows shared by workgroups
+    (block index mod rows) -- STAT_SLOTS, or fewer for small M (a conv has at most M/64 row
+    blocks, and fewer rows are less for the finalize to read) -- or in deterministic mode
+    one row per workgroup (the BN-backward kernels cap their grid to the rows)."""
     if not _native.deterministic():
-        return STAT_SLOTS
+        if M is None:
+            return STAT_SLOTS
+        need = min(STAT_SLOTS, max(1, -(-int(M) // 64)))
+        return 1 << (need - 1).bit_length()
     assert M is not None, "deterministic mode sizes the slots by the producer's row count"
     need = max(STAT_SLOTS, -(-int(M) // 64))
     return 1 << (need - 1).bit_length()
@@ -199,10 +215,14 @@ def stat_slots(nq: int, C: int, device, M: int | None = None) -> torch.Tensor:
     return torch.zeros(slot_rows(M), nq, C, device=device, dtype=torch.float32)
 
 
-def conv_fwd(x, wf, shp: ConvShape, s=None, t=None, act=0, alpha=1.0, tile=None, part=None, nsplit=None):
+def conv_fwd(x, wf, shp: ConvShape, s=None, t=None, act=0, alpha=1.0, tile=None, part=None, nsplit=None,
+             fin=None):
     """y = conv(act(x*s+t)) (or conv(x) when s is None and act == 0); returns
     (y [N,Ho,Wo,Cout] bf16, part [STAT_SLOTS,2,Cout] fp32 slots whose row sum is
-    (sum y, sum y^2)).  ``part``: a zeroed slot buffer to accumulate into."""
+    (sum y, sum y^2)).  ``part``: a zeroed slot buffer to accumulate into.
+    ``fin`` = (fptr, fval): then finalise the batch-norm statistics (stats_finalize
+    arguments: gamma beta run_mean run_var nbt s t save_mean save_aux / mode eps momentum
+    count) and re-zero the slots."""
     nat = _native.native()
     N, H, W, C = x.shape
     assert C == shp.cxp and x.dtype == torch.bfloat16 and x.is_contiguous()
@@ -228,11 +248,14 @@ def conv_fwd(x, wf, shp: ConvShape, s=None, t=None, act=0, alpha=1.0, tile=None,
                    0, 0, 0, 0, 0, 0,
                    N, H, W, C, Ho, Wo, shp.stride, list(dh), list(dw), list(wt), shp.cout, shp.ntaps * shp.cxp,
                    Ho, Wo, 1, 0, 0, pro, int(act), float(alpha), EPI_STATS, 0, 1.0, bm, bn, bk, ns, slab_p, cnt_p, _sp())
+    if fin is not None:
+        _finalize_standalone(nat, 1, part, 2, shp.cout, fin[0], fin[1])
     return y, part
 
 
 def conv_dgrad(g, y, al, be, wd, shp: ConvShape, x_shape, epi=EPI_STORE, out=None, ex=None, es=None, et=None,
-               act=0, alpha=1.0, tile=None, part=None, nsplit=None, gs=None, jmask=None, jyb=None, jout=None):
+               act=0, alpha=1.0, tile=None, part=None, nsplit=None, gs=None, jmask=None, jyb=None, jout=None,
+               coef=None):
     """Data gradient of y = conv(a): dA = conv^T(g*gs + al + be*y)  (gs None: 1).
 
     epi: EPI_STORE -> write dA; EPI_ADD -> out += dA; EPI_ACTBWD -> through the lazy
@@ -243,7 +266,10 @@ def conv_dgrad(g, y, al, be, wd, shp: ConvShape, x_shape, epi=EPI_STORE, out=Non
     becomes g_pre = (out + dA) * act'(join) with act' from ``jmask`` (ReLU bit mask) or
     ``jout`` (the join output, CELU), and ``part`` [STAT_SLOTS, 3, Cin] receives
     (sum g_pre*ex, sum g_pre, sum g_pre*jyb) -- ex / jyb = the block's residual / shortcut
-    branch outputs (jyb None: identity shortcut)."""
+    branch outputs (jyb None: identity shortcut).
+    ``coef`` = (fptr, fval) with EPI_ACTBWD / EPI_JOINBWD: then turn the statistics into the
+    producer units' BN-backward coefficients (stats_bwd_finalize arguments, units A and B:
+    save_mean save_aux gamma alpha beta ggamma gbeta / mode eps count)."""
     nat = _native.native()
     N, Hy, Wy, Cy = g.shape
     assert Cy == shp.cout and g.is_contiguous() and (y is None or y.is_contiguous())
@@ -264,6 +290,7 @@ def conv_dgrad(g, y, al, be, wd, shp: ConvShape, x_shape, epi=EPI_STORE, out=Non
     if nsplit is not None:
         ent = {"nsplit": nsplit}
     classes = dgrad_classes(shp.k, shp.stride, shp.pad)
+    assert coef is None or epi in (EPI_ACTBWD, EPI_JOINBWD)
     for (py, px, dh, dw, wt) in classes:
         Ha = (Hx - py + shp.stride - 1) // shp.stride
         Wa = (Wx - px + shp.stride - 1) // shp.stride
@@ -280,6 +307,8 @@ def conv_dgrad(g, y, al, be, wd, shp: ConvShape, x_shape, epi=EPI_STORE, out=Non
                        _p(jmask), _p(jyb), _p(jout), N, Hy, Wy, Cy, Ha, Wa, 1,
                        list(dh), list(dw), list(wt), shp.cin, shp.ntaps * shp.cout, Hx, Wx, shp.stride, py, px,
                        pro, 0, 1.0, epi, int(act), float(alpha), bm, bn, bk, ns, slab_p, cnt_p, _sp())
+    if coef is not None:
+        _finalize_standalone(nat, 2, part, 3 if epi == EPI_JOINBWD else 2, shp.cin, coef[0], coef[1])
     return out, (part if epi in (EPI_ACTBWD, EPI_JOINBWD) else None)
 
 

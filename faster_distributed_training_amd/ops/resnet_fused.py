@@ -35,6 +35,7 @@ import torch.nn as nn
 
 from . import _native
 from . import conv_igemm as ci
+from ..parallel import graphs as _graphs
 
 ACT_NONE, ACT_RELU, ACT_CELU = 0, 1, 2
 # materialise the normalised input / folded gradient of 3x3 convs once (see forward/backward)
@@ -62,16 +63,14 @@ def register_grad_ready_hook(param, fn, deferrable=False):
     return _Handle()
 
 
-# While a backward is being captured into HIP graphs, deferrable hooks return their GPU
-# action; the recorder cuts the graph there so the action runs between two graph segments
-# on every replay (communication keeps overlapping backward).
-_RECORDER = None
-
+# While a backward is being captured into HIP graphs (parallel/graphs.py recording),
+# deferrable hooks return their GPU action; the recorder cuts the graph there so the action
+# runs between two graph segments on every replay (communication keeps overlapping backward).
 def grad_ready(param):
     hooks = _GRAD_READY_HOOKS.get(id(param), ())
     if not hooks:
         return
-    rec = _RECORDER
+    rec = _graphs.active()
     acts = []
     for fn, deferrable in hooks:
         if deferrable:
@@ -268,24 +267,24 @@ def _bn_fin_params(u: Unit, training):
 
 
 def conv_bn_fwd(x, u: Unit, s, t, act, training, dev):
-    """One unit's conv + batch statistics -> (y, (s, t, save_mean, save_aux), M)."""
+    """One unit's conv + batch statistics -> (y, (s, t, save_mean, save_aux), M).  The
+    statistics are finalised inside the conv launch when its grid is small (ci.conv_fwd)."""
     Ho, Wo = ci.out_hw(x.shape[1], x.shape[2], u.shp)
     M = x.shape[0] * Ho * Wo
-    y, part = ci.conv_fwd(x, u.wf, u.shp, s, t, act[0] if act else 0, act[1] if act else 1.0,
-                          part=slots(2, u.shp.cout, dev, M))
-    return y, finalize_stats(part, u, M, training, dev), M
+    st, fin = _fin_args(u, M, training, dev)
+    y, _ = ci.conv_fwd(x, u.wf, u.shp, s, t, act[0] if act else 0, act[1] if act else 1.0,
+                       part=slots(2, u.shp.cout, dev, M), fin=fin)
+    return y, st, M
 
 
-def finalize_stats(part, u: Unit, M, training, dev):
-    nat = _native.native()
+def _fin_args(u: Unit, M, training, dev):
+    """Outputs (s, t, save_mean, save_aux) and the finalisation arguments of one unit's
+    statistics (eval-mode BN reads none of them but still re-zeroes the slots)."""
     C = u.shp.cout
     s, t, sm, sa = _f32(C, dev), _f32(C, dev), _f32(C, dev), _f32(C, dev)
     mode, mom, rm, rv, nbt, gamma, beta = _bn_fin_params(u, training)
-    # eval-mode BN reads no statistics but still re-zeroes the slots the conv filled
-    nat.stats_finalize(part.data_ptr(), part.shape[0], C, float(M), mode, float(u.eps), float(mom), _p(gamma),
-                       _p(beta), _p(rm), _p(rv), _p(nbt), s.data_ptr(), t.data_ptr(), sm.data_ptr(), sa.data_ptr(), 1,
-                       _sp())
-    return s, t, sm, sa
+    fptr = [_p(gamma), _p(beta), _p(rm), _p(rv), _p(nbt), s.data_ptr(), t.data_ptr(), sm.data_ptr(), sa.data_ptr()]
+    return (s, t, sm, sa), (fptr, [float(mode), float(u.eps), float(mom), float(M)])
 
 
 def reduce_parts(part, nq, C, dev):
@@ -316,23 +315,35 @@ def _coef_args(u: Unit, sm, sa, M, training, dev):
 _NO_UNIT = [0, 0.0, 1.0, 0, 0, 0, 0, 0, 0, 0]
 
 
-def bwd_finalize(part, nq, ua, sta, ub=None, stb=None, training=True, dev=None):
-    """Statistics slots [S, nq, C] of dL/dy reductions -> BN-backward corrections.
-
-    Unit ``ua`` takes (g_s, g_t) = rows (0, 1); with nq == 3 unit ``ub`` (the block's
-    shortcut) takes rows (2, 1).  ``st*`` = (save_mean, save_aux, M).  One launch; the slots
-    are re-zeroed.  Returns ((alpha_a, beta_a), (alpha_b, beta_b) or None)."""
-    nat = _native.native()
+def coef_args(ua, sta, ub=None, stb=None, training=True, dev=None):
+    """BN-backward coefficient arguments of unit ``ua`` (rows (0, 1) of the dL/dy slots) and,
+    with nq == 3, of the block's shortcut unit ``ub`` (rows (2, 1)); ``st*`` = (save_mean,
+    save_aux, M).  Returns ((fptr, fval) for ci.conv_dgrad(coef=...) / the standalone
+    kernel, (alpha_a, beta_a), (alpha_b, beta_b) or None)."""
     aa, ra = _coef_args(ua, sta[0], sta[1], sta[2], training, dev)
     if ub is not None:
         ab, rb = _coef_args(ub, stb[0], stb[1], stb[2], training, dev)
     else:
         ab, rb = _NO_UNIT, None
-    nat.stats_bwd_finalize(part.data_ptr(), part.shape[0], nq, ua.shp.cout, *aa, *ab, _sp())
-    for u in (ua, ub):
+    fptr = list(aa[3:]) + list(ab[3:])
+    fval = [float(aa[0]), float(aa[1]), float(aa[2]), float(ab[0]), float(ab[1]), float(ab[2])]
+    return (fptr, fval), ra, rb
+
+
+def coef_ready(*units):
+    for u in units:
         if u is not None and u.bn is not None:
             grad_ready(u.bn.weight)
             grad_ready(u.bn.bias)
+
+
+def bwd_finalize(part, nq, ua, sta, ub=None, stb=None, training=True, dev=None):
+    """Statistics slots [S, nq, C] of dL/dy reductions -> BN-backward corrections in one
+    standalone launch (the slots are re-zeroed).  Returns ((alpha_a, beta_a), (alpha_b,
+    beta_b) or None)."""
+    (fptr, fval), ra, rb = coef_args(ua, sta, ub, stb, training, dev)
+    ci._finalize_standalone(_native.native(), 2, part, nq, ua.shp.cout, fptr, fval)
+    coef_ready(ua, ub)
     return ra, rb
 
 
@@ -435,7 +446,8 @@ class ResNetBodyFn(torch.autograd.Function):
         dev = g.device
         recs = ctx.recs
         nblk = len(plan.blocks)
-        joined = False  # g is already g_pre of the current block (stats in the slots)
+        joined = False  # g is already g_pre of the current block (its BN-backward coefficients
+        joined_coef = None  # computed with the dgrad that completed it: joined_coef)
         fs = plan.fsdp
         cur = None
         for bi in range(nblk - 1, -1, -1):
@@ -463,8 +475,11 @@ class ResNetBodyFn(torch.autograd.Function):
                                      part.shape[0], M, C,
                                      b.join[0], float(b.join[1]), 1, _sp())
             ul = b.units[-1]
-            (al, be), coef_sc = bwd_finalize(part, 3, ul, (ys[-1][3], ys[-1][4], ys[-1][5]),
-                                             b.shortcut, (sc[3], sc[4], sc[5]) if sc else None, training, dev)
+            if joined:
+                (al, be), coef_sc = joined_coef  # finalised with the completing dgrad (below)
+            else:
+                (al, be), coef_sc = bwd_finalize(part, 3, ul, (ys[-1][3], ys[-1][4], ys[-1][5]),
+                                                 b.shortcut, (sc[3], sc[4], sc[5]) if sc else None, training, dev)
             assert sc is not None or len(b.units) > 1, "identity block needs >1 unit (g_pre aliasing)"
             if sc is not None:
                 u = b.shortcut
@@ -488,6 +503,9 @@ class ResNetBodyFn(torch.autograd.Function):
                     yp, sp_, tp = ys[i - 1][0], ys[i - 1][1], ys[i - 1][2]
                     actp = b.units[i - 1].act_out
                     pp = slots(2, u.shp.cin, dev, _rows(yp))
+                    up = b.units[i - 1]
+                    cf, (al_p, be_p), _ = coef_args(up, (ys[i - 1][3], ys[i - 1][4], ys[i - 1][5]),
+                                                    training=training, dev=dev)
                     if MATERIALIZE_3X3 and u.shp.k > 1:
                         # fold the BN-backward correction into the gradient once (3x3: the
                         # dgrad operand is re-read 9x, the wgrad operand once per column block)
@@ -496,26 +514,30 @@ class ResNetBodyFn(torch.autograd.Function):
                                         gf.data_ptr(), _rows(gf), gf.shape[-1], 1, _sp())
                         g_prev, _ = ci.conv_dgrad(gf, None, None, None, u.wd, u.shp, tuple(yp.shape),
                                                   epi=ci.EPI_ACTBWD, ex=yp, es=sp_, et=tp, act=actp[0],
-                                                  alpha=actp[1], part=pp)
+                                                  alpha=actp[1], part=pp, coef=cf)
                         wgrad_into(u, gf, None, None, None, a_in if a_in is not None else yp,
                                    None if a_in is not None else sp_, None if a_in is not None else tp,
                                    (ACT_NONE, 1.0) if a_in is not None else actp)
                     else:
                         g_prev, _ = ci.conv_dgrad(g_cur, y, al, be, u.wd, u.shp, tuple(yp.shape),
                                                   epi=ci.EPI_ACTBWD, ex=yp, es=sp_, et=tp, act=actp[0],
-                                                  alpha=actp[1], part=pp, gs=gs_cur)
+                                                  alpha=actp[1], part=pp, gs=gs_cur, coef=cf)
                         wgrad_into(u, g_cur, y, al, be, yp, sp_, tp, actp, gs=gs_cur)
-                    up = b.units[i - 1]
-                    (al, be), _ = bwd_finalize(pp, 2, up, (ys[i - 1][3], ys[i - 1][4], ys[i - 1][5]),
-                                               training=training, dev=dev)
+                    coef_ready(up)
+                    al, be = al_p, be_p
                     g_cur, gs_cur = g_prev, None
                 else:
                     if prev is not None:
                         _, pys, psc, pout, pmask = prec
+                        pul = prev.units[-1]
+                        cf, ra, rb = coef_args(pul, (pys[-1][3], pys[-1][4], pys[-1][5]), prev.shortcut,
+                                               (psc[3], psc[4], psc[5]) if psc else None, training, dev)
                         ci.conv_dgrad(g_cur, y, al, be, u.wd, u.shp, tuple(x_in.shape), epi=ci.EPI_JOINBWD, out=g_x,
-                                      gs=gs_cur, ex=pys[-1][0], part=slots(3, x_in.shape[-1], dev, _rows(x_in)), act=prev.join[0],
-                                      alpha=prev.join[1], jmask=pmask, jyb=psc[0] if psc else None,
-                                      jout=None if pmask is not None else pout)
+                                      gs=gs_cur, ex=pys[-1][0], part=slots(3, x_in.shape[-1], dev, _rows(x_in)),
+                                      act=prev.join[0], alpha=prev.join[1], jmask=pmask,
+                                      jyb=psc[0] if psc else None, jout=None if pmask is not None else pout, coef=cf)
+                        coef_ready(pul, prev.shortcut)
+                        joined_coef = (ra, rb)
                     else:
                         ci.conv_dgrad(g_cur, y, al, be, u.wd, u.shp, tuple(x_in.shape), epi=ci.EPI_ADD, out=g_x,
                                       gs=gs_cur)
@@ -581,29 +603,6 @@ class _NoCtx:
     pass
 
 
-class _Recorder:
-    """Backward capture split into graph segments at deferred hook actions."""
-
-    def __init__(self, pool):
-        self.pool = pool
-        self.segments = []  # [(CUDAGraph, [actions to run after it])]
-        self.cur = None
-
-    def begin(self):
-        self.cur = torch.cuda.CUDAGraph()
-        self.cur.capture_begin(pool=self.pool, capture_error_mode="thread_local")
-
-    def cut(self, actions):
-        self.cur.capture_end()
-        self.segments.append((self.cur, list(actions)))
-        self.begin()
-
-    def end(self):
-        self.cur.capture_end()
-        self.segments.append((self.cur, []))
-        self.cur = None
-
-
 class _GraphState:
     """HIP graphs of one (batch shape, train/eval) configuration of the body.
 
@@ -664,7 +663,6 @@ class _BodyWithDummy(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, g):
-        global _RECORDER
         st = ctx.gstate
         if st is None:
             ResNetBodyFn.backward(ctx.inner, g)
@@ -674,22 +672,18 @@ class _BodyWithDummy(torch.autograd.Function):
             side = torch.cuda.Stream()
             side.wait_stream(torch.cuda.current_stream())
             torch.cuda.synchronize()
-            rec = _Recorder(st.pool)
-            with torch.cuda.stream(side):
-                _RECORDER = rec
+            rec = _graphs.Recorder(st.pool)
+            with torch.cuda.stream(side), _graphs.recording(rec):
+                rec.begin()
                 try:
-                    rec.begin()
                     ResNetBodyFn.backward(st.inner, st.g)
-                    rec.end()
                 finally:
-                    _RECORDER = None
+                    rec.end()
             torch.cuda.current_stream().wait_stream(side)
+            st.rec = rec
             st.segments = rec.segments
             st.stage = "ready"
         else:
             st.g.copy_(g)
-        for graph, acts in st.segments:
-            graph.replay()
-            for a in acts:
-                a()
+        st.rec.replay()
         return None, None, None, None

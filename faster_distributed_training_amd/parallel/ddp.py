@@ -11,9 +11,10 @@ X2-X4) with a reducer designed around the flat gradient buffer (``utils/flat.py`
   RCCL on ROCm), so communication overlaps the rest of backward;
 * ``finish()`` (call after ``backward``) launches any bucket left (unused params) and
   makes the compute stream wait on RCCL — no host blocking on GPU;
-* with the ResNet engine running its backward as captured HIP graphs, the engine cuts the
-  graph where a bucket completes and launches that bucket's all-reduce between segments
-  (``_hook(p, defer=True)``), so overlap survives graph replay;
+* with the backward captured as HIP graphs (the ResNet engine's, or any autograd backward
+  under ``parallel/graphs.SegmentedStep``), the capture is cut where a bucket completes and
+  that bucket's all-reduce is launched between the replayed segments, so overlap survives
+  graph replay;
 * averaging uses ``ReduceOp.AVG`` on RCCL (no extra scaling pass), ``SUM`` + scale on
   gloo; optional bf16 wire format halves bytes on xGMI.
 
@@ -32,6 +33,7 @@ import torch.distributed as dist
 
 from ..ops import _native
 from ..utils.flat import FlatParams
+from . import graphs
 
 
 def plan_buckets_py(sizes, first_cap, cap):
@@ -107,14 +109,21 @@ class BucketReducer:
     # ------------------------------------------------------------------ hooks
     def _hook(self, p, defer=False):
         """Gradient of ``p`` is final.  ``defer`` (the engine is capturing its backward into
-        HIP graphs): do the bookkeeping, return the launch as a callable instead."""
+        HIP graphs): do the bookkeeping, return the launch as a callable instead.  Under any
+        other graph recording (parallel/graphs.py, e.g. an autograd backward being captured)
+        the capture is cut here and the launch runs between the replayed segments."""
         if not self.enabled:
             return None
         b = self.bucket_of[id(p)]
         self.pending[b] -= 1
         if self.pending[b] == 0:
+            act = lambda: self._launch(b)  # noqa: E731
             if defer:
-                return lambda: self._launch(b)
+                return act
+            rec = graphs.active()
+            if rec is not None:
+                rec.cut([act])
+                return None
             self._launch(b)
         return None
 

@@ -28,6 +28,7 @@ from ..ops.mixup import mixup_criterion
 from ..optim.flat_optim import SGD, Adam, DeviceGradScaler, GradClipper, MirrorMADGRAD, MADGRAD
 from ..optim.ngd import NGD
 from ..parallel import dist as pdist
+from ..parallel.graphs import SegmentedStep
 from ..utils.env import default_device, print0, seed_everything
 from ..utils.flat import FlatParams
 from . import checkpoint as ckpt
@@ -221,9 +222,12 @@ class TransformerTrainer:
     # into static device buffers before each replay, torch's dropout advances its philox
     # offset per replay, and the attention kernels XOR a per-replay device seed into their
     # dropout hash (ops/attention_native.py DEVICE_SEED).  Gradients accumulate into the
-    # flat gradient buffer (static; the optimizer zeroes it).  Single process, bf16 only.
+    # flat gradient buffer (static; the optimizer zeroes it).  Under DDP the capture is cut
+    # where a gradient bucket completes (parallel/graphs.SegmentedStep) and the replay
+    # launches each bucket's all-reduce between segments; the sharded optimizer (ZeRO-2 NGD)
+    # communicates after the replay.  bf16 only; not with FSDP (collectives inside forward).
     def _graphs_on(self):
-        return (TR_GRAPHS and self.device.type == "cuda" and self.reducer is None and self.fsdp is None
+        return (TR_GRAPHS and self.device.type == "cuda" and self.fsdp is None
                 and not self.scaler.enabled and self.cfg.profile_steps <= 0 and not self.cfg.faithful
                 and self.model.training)
 
@@ -272,24 +276,35 @@ class TransformerTrainer:
                       perm=torch.empty(B, dtype=torch.long, device=self.device),
                       lam=torch.empty(B, dtype=torch.float32, device=self.device),
                       seed=torch.zeros(1, dtype=torch.int64, device=self.device))
-            g = torch.cuda.CUDAGraph()
+            def body():
+                mask = st["masks"].view(B, 1, 1, st["masks"].shape[1])
+                with self._autocast(cache=False):  # no cast cache across a graph capture
+                    logits, perm, _ = self.model(st["tokens"], st["types"], self.pos_index, mask)
+                    loss = mixup_cross_entropy(logits, st["labels"], st["labels"][perm], st["lam"])
+                loss.backward()
+                return loss, logits
+
             torch.cuda.synchronize()
             AN.DEVICE_SEED = st["seed"]
             self.model.mix_override = (st["perm"], st["lam"])
             try:
-                with torch.cuda.graph(g, pool=self._graph_pool):
-                    mask = st["masks"].view(B, 1, 1, st["masks"].shape[1])
-                    with self._autocast(cache=False):  # no cast cache across a graph capture
-                        logits, perm, _ = self.model(st["tokens"], st["types"], self.pos_index, mask)
-                        loss = mixup_cross_entropy(logits, st["labels"], st["labels"][perm], st["lam"])
-                    loss.backward()
+                if self.reducer is not None:
+                    # segments cut at bucket boundaries; all-reduces launched between them
+                    step = SegmentedStep(self.device, self._graph_pool)
+                    loss, logits = step.capture(body)
+                    st.update(replay=step.replay, segments=step.num_segments)
+                else:
+                    g = torch.cuda.CUDAGraph()
+                    with torch.cuda.graph(g, pool=self._graph_pool):
+                        loss, logits = body()
+                    st.update(replay=g.replay, segments=1)
             finally:
                 AN.DEVICE_SEED = None
                 self.model.mix_override = None
-            st.update(graph=g, loss=loss, logits=logits)
+            st.update(loss=loss, logits=logits)
             self._graphs[key] = ent = st
         lam = self._graph_fill(ent, tokens, labels, types, masks)
-        ent["graph"].replay()
+        ent["replay"]()
         return ent["loss"], ent["logits"], ent["perm"], lam
 
     def train_step(self, tokens, labels, types, masks):

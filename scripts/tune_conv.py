@@ -23,7 +23,8 @@ from faster_distributed_training_amd.ops import conv_igemm as ci
 from bench_conv import SHAPES, timeit
 
 FWD_TILES = [(128, 128, 64), (128, 64, 64), (64, 128, 64), (64, 64, 64), (256, 64, 64),
-             (128, 128, 32), (128, 64, 32), (64, 128, 32), (64, 64, 32), (256, 128, 32)]
+             (128, 128, 32), (128, 64, 32), (64, 128, 32), (64, 64, 32), (256, 128, 32),
+             (64, 64, 128), (128, 64, 128), (64, 128, 128)]
 WG_TILES = [(128, 128, 32), (64, 128, 32), (128, 64, 32), (64, 64, 32),
             (128, 128, 64), (64, 128, 64), (128, 64, 64), (64, 64, 64)]
 

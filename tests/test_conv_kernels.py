@@ -74,7 +74,8 @@ def test_conv_fwd(cuda, case, mode):
         act, alpha = (1, 1.0) if mode == "relu" else (2, 0.075)
         a = act_ref(x.float() * s + t, act, alpha).to(BF).float()[..., :Cin]
     for tile, ns in [(None, None), ((64, 64, 64), 1), ((64, 64, 64), 3), ((128, 64, 32), None),
-                     ((128, 128, 64), 2), ((256, 128, 32), None), ((256, 64, 64), 1)]:
+                     ((128, 128, 64), 2), ((256, 128, 32), None), ((256, 64, 64), 1), ((64, 64, 128), 1),
+                     ((64, 64, 128), 3), ((128, 64, 128), 2), ((64, 128, 128), None)]:
         if tile and Cout % tile[1]:
             continue
         y, part = ci.conv_fwd(x, wf, shp, s, t, act, alpha, tile=tile, nsplit=ns)
@@ -113,7 +114,10 @@ def test_conv_dgrad(cuda, case, epi):
     ref = nhwc(torch.nn.grad.conv2d_input((N, Cin, H, H), w.to(BF).float(), nchw(gt), stride=stride, padding=pad))
     xs = (N, H, H, Cin)
     if epi == "store":
-        for tile, ns in [(None, None), ((64, 64, 32), 1), ((64, 64, 32), 4), ((128, 64, 64), 2)]:
+        for tile, ns in [(None, None), ((64, 64, 32), 1), ((64, 64, 32), 4), ((128, 64, 64), 2),
+                         ((64, 64, 128), 2), ((64, 128, 128), 1)]:
+            if tile and Cin % tile[1]:
+                continue
             out, _ = ci.conv_dgrad(g, y, al, be, wd, shp, xs, epi=ci.EPI_STORE, tile=tile, nsplit=ns)
             assert rel(out, ref) < 1e-2, (tile, ns)
     elif epi == "add":

@@ -13,7 +13,7 @@ def test_slot_rows_sizing():
     assert ci.slot_rows() == ci.STAT_SLOTS
     _native.set_deterministic(True)
     try:
-        assert ci.slot_rows(128) == ci.STAT_SLOTS  # at least the shared-slot count
+        assert ci.slot_rows(128) == ci.STAT_SLOTS  # at least the shared-slot count (det mode)
         assert ci.slot_rows(64 * 100) == 128       # one row per 64-row block, power of two
         assert ci.slot_rows(1024 * 32 * 32) == 16384
         with pytest.raises(AssertionError):
