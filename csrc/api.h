@@ -61,8 +61,8 @@ void mixup_ce_fwd(uint64_t logits, uint64_t ya, uint64_t yb, uint64_t lam, uint6
 // layernorm.hip
 void layernorm_fwd(uint64_t x, uint64_t a, uint64_t b, uint64_t y, uint64_t mean, uint64_t rstd, long rows, int d,
                    float eps, int dt_x, int dt_y, int dt_w, uint64_t stream);
-void layernorm_bwd(uint64_t gy, uint64_t x, uint64_t a, uint64_t mean, uint64_t rstd, uint64_t gx, uint64_t part,
-                   long rows, int d, int nblk, int dt_g, int dt_x, int dt_w, float eps, uint64_t stream);
+void layernorm_bwd(uint64_t gy, uint64_t x, uint64_t a, uint64_t mean, uint64_t rstd, uint64_t gx, uint64_t gres,
+                   uint64_t part, long rows, int d, int nblk, int dt_g, int dt_x, int dt_w, float eps, uint64_t stream);
 // embedding.hip
 void embedding_fwd(uint64_t ids, uint64_t types, uint64_t pos_ids, uint64_t tok, uint64_t pos, uint64_t seg,
                    uint64_t out, int B, int L, int d, float scale, int vt, int vp, int vs, uint64_t stream);

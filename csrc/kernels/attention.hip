@@ -13,8 +13,9 @@
 // MFMA mapping (mfma_f32_32x32x16_bf16; C[row][col]: col = lane & 31, row = (r&3) + 8(r>>2)
 // + 4(lane>>5)): every product is oriented so that the accumulator of the first GEMM is
 // already the B operand of the next one (its k index = the accumulator's row index, in the
-// permuted order row(j) = 16s + 8(j>>2) + 4h + (j&3)); the other operand is read from a
-// transposed LDS image in that same permuted order (two 8-byte reads per lane).
+// permuted order row(j) = 16s + 8(j>>2) + 4h + (j&3)); the other operand is read in that
+// same permuted order from the row image itself with the gfx950 transposing LDS read
+// (ds_read_b64_tr_b16, two per fragment) -- no transposed copy is staged.
 //   forward     S^T = K Q^T (query on the lane -> row max / sum are in-register plus one
 //               lane^32 exchange), online softmax, O^T += V^T P^T.          grid (L/128, H, B)
 //   bwd dK,dV   S = Q K^T, dP = dO V^T (key on the lane), dV^T += dO^T P, dK^T += Q^T dS:
@@ -37,7 +38,6 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 constexpr int kD = 64;
 constexpr int kRowLd = kD + 8;  // [row][d] images: 144-B rows -> ds_read_b128 of 16 rows hits 64 distinct banks
-constexpr int kTLd = 64 + 4;    // [d][row] images: 136-B rows -> ds_read_b64 of 32 rows hits 64 distinct banks
 constexpr int kBlk = 128;       // queries (fwd, dq) / keys (dkdv) per workgroup: 4 waves x 32
 constexpr int kTile = 64;       // keys (fwd, dq) / queries (dkdv) staged per loop iteration
 
@@ -69,22 +69,32 @@ struct Args {
   const uint64_t* seed_ptr;
 };
 
+// keep-mask hash of (bh, q, key) under the per-call seed: 32-bit murmur3 finaliser (two
+// 32-bit multiplies; the 64-bit mix it replaces cost ~3x the VALU work per score element)
 __device__ __forceinline__ bool dropped(const Args& a, int bh, int q, int key) {
-  uint64_t x = (((uint64_t)bh * (uint64_t)a.L + (uint64_t)q) * (uint64_t)a.L + (uint64_t)key) ^ a.seed;
-  x ^= x >> 33;
-  x *= 0xff51afd7ed558ccdull;
-  x ^= x >> 33;
-  x *= 0xc4ceb9fe1a85ec53ull;
-  x ^= x >> 33;
-  return (uint32_t)x < a.drop_thr;
+  uint32_t x = (((uint32_t)bh * (uint32_t)a.L + (uint32_t)q) * (uint32_t)a.L + (uint32_t)key) ^ (uint32_t)a.seed;
+  x += (uint32_t)(a.seed >> 32);
+  x ^= x >> 16;
+  x *= 0x85ebca6bu;
+  x ^= x >> 13;
+  x *= 0xc2b2ae35u;
+  x ^= x >> 16;
+  return x < a.drop_thr;
 }
 
 __device__ __forceinline__ bf16x8_t ld8(const bf16* p) { return *reinterpret_cast<const bf16x8_t*>(p); }
 
-// two 8-byte reads (k elements j = 0..3 and 4..7 of the permuted order) of a transposed image
-__device__ __forceinline__ bf16x8_t ld4x2(const bf16* p) {
-  const bf16x4_t lo = *reinterpret_cast<const bf16x4_t*>(p);
-  const bf16x4_t hi = *reinterpret_cast<const bf16x4_t*>(p + 8);
+typedef __attribute__((address_space(3))) bf16x4_t lds_bf16x4;
+
+// Transposed MFMA fragment straight from a ROW image [row][kRowLd] (gfx950 ds_read_b64_tr_b16,
+// no transposed LDS copy): lane l gets column c0 + (l & 31) and the k elements = rows
+// R..R+3 (lo) and R+8..R+11 (hi), R = r0 + 4h -- the permuted order of the accumulator rows.
+// In each 16-lane group lane 4q+p supplies row R+q, columns 16g + 4p..4p+3 (g = (l >> 4) & 1).
+__device__ __forceinline__ bf16x8_t ldtr(const bf16* img, int r0, int c0, int lane) {
+  const int q = (lane & 15) >> 2, p = lane & 3, g = (lane >> 4) & 1, h = lane >> 5;
+  const bf16* p0 = img + (r0 + 4 * h + q) * kRowLd + c0 + 16 * g + 4 * p;
+  const bf16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_bf16x4*)(p0));
+  const bf16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_bf16x4*)(p0 + 8 * kRowLd));
   return __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
 }
 
@@ -100,25 +110,16 @@ __device__ __forceinline__ f32x16 mfma(bf16x8_t a, bf16x8_t b, f32x16 c) {
 
 __device__ __forceinline__ int crow(int r, int h) { return (r & 3) + 8 * (r >> 2) + 4 * h; }
 
-// rows [r0, r0 + 64) of a strided [L][64] matrix -> row image [64][kRowLd] and/or
-// transposed image [64][kTLd]; rows past L are zero.
-__device__ __forceinline__ void stage(bf16* rows, bf16* trans, const bf16* src, long ld, int r0, int L, int tid) {
+// rows [r0, r0 + 64) of a strided [L][64] matrix -> row image [64][kRowLd] (16-B stores;
+// transposed operands are read from it with ldtr); rows past L are zero.
+__device__ __forceinline__ void stage(bf16* rows, const bf16* src, long ld, int r0, int L, int tid) {
 #pragma unroll
   for (int it = 0; it < 2; ++it) {
     const int c = tid + it * 256;
     const int row = c >> 3, ch = c & 7;
     uint4 v = make_uint4(0, 0, 0, 0);
     if (r0 + row < L) v = *reinterpret_cast<const uint4*>(src + (long)(r0 + row) * ld + ch * 8);
-    if (rows) *reinterpret_cast<uint4*>(rows + row * kRowLd + ch * 8) = v;
-    if (trans) {
-      const uint32_t u[4] = {v.x, v.y, v.z, v.w};
-      uint16_t* t = reinterpret_cast<uint16_t*>(trans) + (ch * 8) * kTLd + row;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        t[(2 * e) * kTLd] = (uint16_t)(u[e] & 0xffffu);
-        t[(2 * e + 1) * kTLd] = (uint16_t)(u[e] >> 16);
-      }
-    }
+    *reinterpret_cast<uint4*>(rows + row * kRowLd + ch * 8) = v;
   }
 }
 
@@ -136,7 +137,7 @@ __device__ __forceinline__ float masked_score(float s, int st, const Args& a) {
 __global__ __launch_bounds__(256) void attn_fwd_kernel(Args a) {
   if (a.seed_ptr != nullptr) a.seed ^= *a.seed_ptr;
   __shared__ __attribute__((aligned(16))) bf16 Ks[kTile * kRowLd];
-  __shared__ __attribute__((aligned(16))) bf16 Vt[kD * kTLd];
+  __shared__ __attribute__((aligned(16))) bf16 Vs[kTile * kRowLd];
   __shared__ int8_t ms[kTile];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5, l32 = lane & 31;
   const int b = blockIdx.z, hd = blockIdx.y, bh = b * a.H + hd;
@@ -156,8 +157,8 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(Args a) {
   float m = -INFINITY, l = 0.f;
 
   for (int k0 = 0; k0 < a.L; k0 += kTile) {
-    stage(Ks, nullptr, kp, a.kl, k0, a.L, tid);
-    stage(nullptr, Vt, vp, a.vl, k0, a.L, tid);
+    stage(Ks, kp, a.kl, k0, a.L, tid);
+    stage(Vs, vp, a.vl, k0, a.L, tid);
     if (tid < kTile) ms[tid] = key_state(a, b, k0 + tid);
     __syncthreads();
     float x[2][16];
@@ -207,9 +208,8 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(Args a) {
 #pragma unroll
       for (int hs = 0; hs < 2; ++hs) {
         const bf16x8_t pb = pack8(&x[t][8 * hs]);
-        const int kof = 32 * t + 16 * hs + 4 * h;
 #pragma unroll
-        for (int dt = 0; dt < 2; ++dt) oacc[dt] = mfma(ld4x2(Vt + (32 * dt + l32) * kTLd + kof), pb, oacc[dt]);
+        for (int dt = 0; dt < 2; ++dt) oacc[dt] = mfma(ldtr(Vs, 32 * t + 16 * hs, 32 * dt, lane), pb, oacc[dt]);
       }
     __syncthreads();
   }
@@ -255,10 +255,9 @@ __global__ __launch_bounds__(256) void attn_bwd_prep_kernel(Args a) {
 __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(Args a) {
   if (a.seed_ptr != nullptr) a.seed ^= *a.seed_ptr;
   __shared__ __attribute__((aligned(16))) bf16 Qs[kTile * kRowLd];
-  __shared__ __attribute__((aligned(16))) bf16 Qt[kD * kTLd];
   __shared__ __attribute__((aligned(16))) bf16 Gs[kTile * kRowLd];  // dO rows
-  __shared__ __attribute__((aligned(16))) bf16 Gt[kD * kTLd];       // dO transposed
-  __shared__ float lse_s[kTile], del_s[kTile];
+  __shared__ __attribute__((aligned(16))) float lse_s[kTile];
+  __shared__ __attribute__((aligned(16))) float del_s[kTile];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5, l32 = lane & 31;
   const int b = blockIdx.z, hd = blockIdx.y, bh = b * a.H + hd;
   const int key = blockIdx.x * kBlk + w * 32 + l32;
@@ -285,8 +284,8 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(Args a) {
     for (int r = 0; r < 16; ++r) { dk[dt][r] = 0.f; dv[dt][r] = 0.f; }
 
   for (int q0 = 0; q0 < a.L; q0 += kTile) {
-    stage(Qs, Qt, qbase, a.ql, q0, a.L, tid);
-    stage(Gs, Gt, gbase, gl, q0, a.L, tid);
+    stage(Qs, qbase, a.ql, q0, a.L, tid);
+    stage(Gs, gbase, gl, q0, a.L, tid);
     if (tid < kTile) {
       const int qq = q0 + tid;
       lse_s[tid] = qq < a.L ? a.lse[(long)bh * a.L + qq] : INFINITY;
@@ -303,26 +302,32 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(Args a) {
         S = mfma(ld8(Qs + (32 * qt + l32) * kRowLd + 16 * ks + 8 * h), kf[ks], S);
         dP = mfma(ld8(Gs + (32 * qt + l32) * kRowLd + 16 * ks + 8 * h), vf[ks], dP);
       }
-      float p[16], ds[16];
+      float p[16], ds[16], lv[16], dv16[16];
+#pragma unroll
+      for (int g4 = 0; g4 < 4; ++g4) {  // rows crow(4 g4 + j, h) = 32 qt + 8 g4 + 4h + j: one float4
+        const float4 l4 = *reinterpret_cast<const float4*>(lse_s + 32 * qt + 8 * g4 + 4 * h);
+        const float4 d4 = *reinterpret_cast<const float4*>(del_s + 32 * qt + 8 * g4 + 4 * h);
+        lv[4 * g4] = l4.x; lv[4 * g4 + 1] = l4.y; lv[4 * g4 + 2] = l4.z; lv[4 * g4 + 3] = l4.w;
+        dv16[4 * g4] = d4.x; dv16[4 * g4 + 1] = d4.y; dv16[4 * g4 + 2] = d4.z; dv16[4 * g4 + 3] = d4.w;
+      }
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int qr = 32 * qt + crow(r, h);
-        const float lse2 = lse_s[qr];
+        const float lse2 = lv[r];
         const float pv = lse2 == -INFINITY ? 0.f : exp2f(masked_score(S[r], st, a) - lse2);
         float z = 1.f;
         if (a.drop_thr) z = dropped(a, bh, q0 + qr, key) ? 0.f : a.keep_scale;
         p[r] = pv * z;
-        ds[r] = st > 0 ? pv * (dP[r] * z - del_s[qr]) : 0.f;
+        ds[r] = st > 0 ? pv * (dP[r] * z - dv16[r]) : 0.f;
       }
 #pragma unroll
       for (int hs = 0; hs < 2; ++hs) {
         const bf16x8_t pb = pack8(&p[8 * hs]);
         const bf16x8_t sb = pack8(&ds[8 * hs]);
-        const int qof = 32 * qt + 16 * hs + 4 * h;
 #pragma unroll
         for (int dt = 0; dt < 2; ++dt) {
-          dv[dt] = mfma(ld4x2(Gt + (32 * dt + l32) * kTLd + qof), pb, dv[dt]);
-          dk[dt] = mfma(ld4x2(Qt + (32 * dt + l32) * kTLd + qof), sb, dk[dt]);
+          dv[dt] = mfma(ldtr(Gs, 32 * qt + 16 * hs, 32 * dt, lane), pb, dv[dt]);
+          dk[dt] = mfma(ldtr(Qs, 32 * qt + 16 * hs, 32 * dt, lane), sb, dk[dt]);
         }
       }
     }
@@ -349,7 +354,6 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(Args a) {
   if (a.seed_ptr != nullptr) a.seed ^= *a.seed_ptr;
   __shared__ __attribute__((aligned(16))) bf16 Ks[kTile * kRowLd];
   __shared__ __attribute__((aligned(16))) bf16 Vs[kTile * kRowLd];
-  __shared__ __attribute__((aligned(16))) bf16 Kt[kD * kTLd];
   __shared__ int8_t ms[kTile];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5, l32 = lane & 31;
   const int b = blockIdx.z, hd = blockIdx.y, bh = b * a.H + hd;
@@ -377,8 +381,8 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(Args a) {
     for (int r = 0; r < 16; ++r) dq[dt][r] = 0.f;
 
   for (int k0 = 0; k0 < a.L; k0 += kTile) {
-    stage(Ks, Kt, kp, a.kl, k0, a.L, tid);
-    stage(Vs, nullptr, vp, a.vl, k0, a.L, tid);
+    stage(Ks, kp, a.kl, k0, a.L, tid);
+    stage(Vs, vp, a.vl, k0, a.L, tid);
     if (tid < kTile) ms[tid] = key_state(a, b, k0 + tid);
     __syncthreads();
 #pragma unroll
@@ -404,9 +408,8 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(Args a) {
 #pragma unroll
       for (int hs = 0; hs < 2; ++hs) {
         const bf16x8_t sb = pack8(&ds[8 * hs]);
-        const int kof = 32 * t + 16 * hs + 4 * h;
 #pragma unroll
-        for (int dt = 0; dt < 2; ++dt) dq[dt] = mfma(ld4x2(Kt + (32 * dt + l32) * kTLd + kof), sb, dq[dt]);
+        for (int dt = 0; dt < 2; ++dt) dq[dt] = mfma(ldtr(Ks, 32 * t + 16 * hs, 32 * dt, lane), sb, dq[dt]);
       }
     }
     __syncthreads();

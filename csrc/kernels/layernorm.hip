@@ -65,6 +65,7 @@ __global__ __launch_bounds__(64 * kLnWaves) void layernorm_bwd_kernel(const TG* 
                                                                       const TW* __restrict__ a,
                                                                       const float* __restrict__ mean_in,
                                                                       const float* __restrict__ rstd_in, TX* __restrict__ gx,
+                                                                      const TX* __restrict__ gres,
                                                                       float* __restrict__ part, long rows, int d,
                                                                       long rows_per_blk, float eps_unused) {
   extern __shared__ float lds[];  // [kLnWaves][2][d]
@@ -96,6 +97,11 @@ __global__ __launch_bounds__(64 * kLnWaves) void layernorm_bwd_kernel(const TG* 
     const float sd = fmaxf(1.f / r - eps_unused, 1e-30f);
     const float c2 = r * r * s2 / ((float)(d - 1) * sd);
     _Pragma("unroll") for (int k = 0; k < E; ++k) gv[k] = r * (av[k] * gv[k] - s1 * inv_d) - c2 * xv[k];
+    if (gres != nullptr) {  // + the residual (skip-path) gradient of x: no separate add pass
+      float rv[E];
+      ln_load<E>(gres + row * d, d, lane, rv);
+      _Pragma("unroll") for (int k = 0; k < E; ++k) gv[k] += rv[k];
+    }
     ln_store<E>(gx + row * d, d, lane, gv);
   }
   _Pragma("unroll") for (int k = 0; k < E; ++k) {
@@ -150,8 +156,8 @@ void layernorm_fwd(uint64_t x, uint64_t a, uint64_t b, uint64_t y, uint64_t mean
 }
 
 // part: [2][nblk][d] fp32 (dgamma partials, dbeta partials); caller sums over nblk.
-void layernorm_bwd(uint64_t gy, uint64_t x, uint64_t a, uint64_t mean, uint64_t rstd, uint64_t gx, uint64_t part,
-                   long rows, int d, int nblk, int dt_g, int dt_x, int dt_w, float eps, uint64_t stream) {
+void layernorm_bwd(uint64_t gy, uint64_t x, uint64_t a, uint64_t mean, uint64_t rstd, uint64_t gx, uint64_t gres,
+                   uint64_t part, long rows, int d, int nblk, int dt_g, int dt_x, int dt_w, float eps, uint64_t stream) {
   FDT_CHECK(d % 64 == 0 && d / 64 <= kMaxE, "layernorm: unsupported d");
   FDT_CHECK(dt_w == kF32, "layernorm weights must be fp32");
   if (rows == 0) return;
@@ -163,7 +169,7 @@ void layernorm_bwd(uint64_t gy, uint64_t x, uint64_t a, uint64_t mean, uint64_t 
       DISPATCH_E(d / 64, {
         layernorm_bwd_kernel<E, TG, T, float><<<nblk, 64 * kLnWaves, lds, as_stream(stream)>>>(
             P<const TG>(gy), P<const T>(x), P<const float>(a), P<const float>(mean), P<const float>(rstd), P<T>(gx),
-            P<float>(part), rows, d, rpb, eps);
+            P<const T>(gres), P<float>(part), rows, d, rpb, eps);
       });
     });
   });

@@ -30,7 +30,7 @@ import torch.nn.functional as F
 from ..ops.dropout import dropout_add, gelu_dropout
 from ..ops.attention import packed_attention, scaled_dot_product_attention
 from ..ops.embedding import embedding_sum
-from ..ops.layernorm import layer_norm_unbiased
+from ..ops.layernorm import ResidualGrad, layer_norm_unbiased
 from ..ops.linear import linear, linear_cat
 from ..ops.mlp import fused_mlp
 
@@ -211,8 +211,8 @@ class LayerNorm(nn.Module):
         self.b_2 = nn.Parameter(torch.zeros(features))
         self.eps = eps
 
-    def forward(self, x):
-        return layer_norm_unbiased(x, self.a_2, self.b_2, self.eps)
+    def forward(self, x, res=None):
+        return layer_norm_unbiased(x, self.a_2, self.b_2, self.eps, res=res)
 
 
 class sublayerConnectionAttention(nn.Module):  # noqa: N801 (reference name)
@@ -223,9 +223,10 @@ class sublayerConnectionAttention(nn.Module):  # noqa: N801 (reference name)
         self.dropout = nn.Dropout(p=dropout_connection)
 
     def forward(self, x, mask=None):
-        y = self.layernorm(x)
+        res = ResidualGrad()  # skip gradient handed to the LayerNorm backward (no add pass)
+        y = self.layernorm(x, res)
         y = self.multiheads(y, y, y, mask)
-        return dropout_add(y, x, self.dropout.p, self.training)
+        return dropout_add(y, x, self.dropout.p, self.training, res)
 
 
 class sublayerConnectionFFN(nn.Module):  # noqa: N801 (reference name)
@@ -236,7 +237,8 @@ class sublayerConnectionFFN(nn.Module):  # noqa: N801 (reference name)
         self.dropout = nn.Dropout(p=dropout_connection)
 
     def forward(self, x):
-        return dropout_add(self.ffn(self.layernorm(x)), x, self.dropout.p, self.training)
+        res = ResidualGrad()
+        return dropout_add(self.ffn(self.layernorm(x, res)), x, self.dropout.p, self.training, res)
 
 
 class Classifier(nn.Module):

@@ -29,12 +29,13 @@ def _seed(p):
 
 class _DropoutAdd(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, y, x, p):
+    def forward(ctx, y, x, p, res=None):
         out = torch.empty_like(x)
         seed, sptr = _seed(p)
         _native.native().dropout_add_fwd(y.data_ptr(), x.data_ptr(), out.data_ptr(), y.numel(), float(p), seed, sptr,
                                          _native.stream_ptr())
         ctx.cfg = (float(p), seed, sptr, y.dtype)
+        ctx.res = res
         return out
 
     @staticmethod
@@ -45,7 +46,10 @@ class _DropoutAdd(torch.autograd.Function):
             g = g.float()
         gy = torch.empty(g.shape, device=g.device, dtype=torch.bfloat16)
         _native.native().dropout_bwd(g.data_ptr(), gy.data_ptr(), g.numel(), p, seed, sptr, _native.stream_ptr())
-        return gy.to(ydt), g, None
+        if ctx.res is not None:  # the sublayer's LayerNorm backward adds the skip gradient
+            ctx.res.g = g
+            return gy.to(ydt), None, None, None
+        return gy.to(ydt), g, None, None
 
 
 class _GeluDropout(torch.autograd.Function):
@@ -75,11 +79,13 @@ def _ok(t) -> bool:
             and _native.use_native(t) and hasattr(_native.native(), "dropout_add_fwd"))
 
 
-def dropout_add(y: torch.Tensor, x: torch.Tensor, p: float, training: bool = True) -> torch.Tensor:
-    """``x + dropout(y, p)``."""
+def dropout_add(y: torch.Tensor, x: torch.Tensor, p: float, training: bool = True, res=None) -> torch.Tensor:
+    """``x + dropout(y, p)``.  ``res``: the ops/layernorm.ResidualGrad of the LayerNorm that
+    consumed x (armed by its native forward): x's skip gradient is handed to that LayerNorm's
+    backward instead of being summed by autograd."""
     p = float(p) if training else 0.0
     if _ok(y) and _ok(x) and y.dtype == torch.bfloat16 and x.dtype == torch.float32 and y.shape == x.shape:
-        return _DropoutAdd.apply(y, x, p)
+        return _DropoutAdd.apply(y, x, p, res if (res is not None and res.armed) else None)
     return F.dropout(y, p, training) + x
 
 

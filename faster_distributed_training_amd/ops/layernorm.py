@@ -23,9 +23,23 @@ def layer_norm_reference(x, a, b, eps=1e-6):
     return a * (x - mean) / (std + eps) + b
 
 
+class ResidualGrad:
+    """Hand-off of a residual block's skip-path gradient (``x + f(LN(x))``, the transformer
+    sublayers): ``dropout_add``'s backward parks dL/d(out) here instead of returning it as
+    x's gradient, and the LayerNorm backward adds it to its own dL/dx inside the kernel --
+    autograd never sees two gradients for x, so no separate fp32 add pass over the residual
+    stream.  ``armed`` is set by the native LayerNorm forward (only then may the skip
+    gradient be parked)."""
+    __slots__ = ("armed", "g")
+
+    def __init__(self):
+        self.armed = False
+        self.g = None
+
+
 class _LayerNormNative(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, a, b, eps, out_dtype):
+    def forward(ctx, x, a, b, eps, out_dtype, res=None):
         nat = _native.native()
         shape = x.shape
         d = shape[-1]
@@ -43,6 +57,9 @@ class _LayerNormNative(torch.autograd.Function):
         ctx.params = (a, b)
         ctx.shape = shape
         ctx.eps = eps
+        ctx.res = res
+        if res is not None:
+            res.armed = True
         return y.view(*shape[:-1], d)
 
     @staticmethod
@@ -56,9 +73,14 @@ class _LayerNormNative(torch.autograd.Function):
         gx = torch.empty_like(x2)
         nblk = max(1, min(512, (rows + 31) // 32))
         part = torch.empty(2, nblk, d, device=x2.device, dtype=torch.float32)
+        gres = None
+        if ctx.res is not None and ctx.res.g is not None:
+            gres = ctx.res.g.reshape(rows, d)
+            assert gres.dtype == x2.dtype and gres.is_contiguous()
+            ctx.res.g = None
         nat.layernorm_bwd(gy2.data_ptr(), x2.data_ptr(), a.data_ptr(), mean.data_ptr(), rstd.data_ptr(),
-                          gx.data_ptr(), part.data_ptr(), rows, d, nblk, DT[gy2.dtype], DT[x2.dtype],
-                          DT[a.dtype], float(ctx.eps), _native.stream_ptr())
+                          gx.data_ptr(), 0 if gres is None else gres.data_ptr(), part.data_ptr(), rows, d, nblk,
+                          DT[gy2.dtype], DT[x2.dtype], DT[a.dtype], float(ctx.eps), _native.stream_ptr())
         from .linear import direct_target, mark_ready, slab_sum_into
         pa, pb = ctx.params
         ta = direct_target(pa) if ctx.needs_input_grad[1] else None
@@ -68,14 +90,15 @@ class _LayerNormNative(torch.autograd.Function):
             slab_sum_into(part[1], tb)
             mark_ready(pa)
             mark_ready(pb)
-            return gx.view(ctx.shape), None, None, None, None
+            return gx.view(ctx.shape), None, None, None, None, None
         ga, gb = part.sum(1).unbind(0)
-        return gx.view(ctx.shape), ga.to(a.dtype), gb.to(a.dtype), None, None
+        return gx.view(ctx.shape), ga.to(a.dtype), gb.to(a.dtype), None, None, None
 
 
-def layer_norm_unbiased(x, a, b, eps=1e-6):
+def layer_norm_unbiased(x, a, b, eps=1e-6, res: ResidualGrad | None = None):
+    """``res``: the residual block's skip-gradient hand-off (see ResidualGrad)."""
     if (_native.use_native(x) and x.shape[-1] % 64 == 0 and 64 <= x.shape[-1] <= 2048
             and x.dtype in DT and a.dtype == torch.float32):
         out_dtype = torch.get_autocast_dtype("cuda") if torch.is_autocast_enabled("cuda") else x.dtype
-        return _LayerNormNative.apply(x, a, b, eps, out_dtype)
+        return _LayerNormNative.apply(x, a, b, eps, out_dtype, res)
     return layer_norm_reference(x, a, b, eps)

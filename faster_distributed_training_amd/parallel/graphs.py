@@ -10,7 +10,8 @@ of kernels (the transformer at 32 samples/GPU is host-bound without graphs).
 
 Used by the fused ResNet engine (ops/resnet_fused.py: backward captured inside its
 autograd node) and by ``SegmentedStep`` (any forward + autograd backward, e.g. the
-transformer trainer under DDP).  Reference: DDP's bucketed overlap
+transformer trainer under DDP; its backward capture starts in the loss's backward node so
+that it runs on autograd's device thread like the hooks that cut it).  Reference: DDP's bucketed overlap
 (``resnet50_test.py:716``, ``transformer_test.py:241-271``).
 """
 from __future__ import annotations
@@ -29,11 +30,10 @@ def active():
 class Recorder:
     """Capture split into graph segments at deferred hook actions.
 
-    ``mode``: the stream-capture mode.  "thread_local" when every begin / cut / end happens
-    on one thread (the engine's backward); "global" when the capture starts on the main
-    thread and is cut from autograd's device thread (``SegmentedStep``).  A cut always
-    ends and restarts the capture on the stream it began on, after joining the caller's
-    current stream if autograd runs the hook on another (forked, captured) stream."""
+    Begin, cuts and end must all happen on ONE thread (HIP rejects ending a capture from
+    another thread): autograd's device thread, where backward nodes and gradient hooks run.
+    A cut ends and restarts the capture on the stream it began on, after joining the
+    caller's current stream if autograd runs the hook on another (forked, captured) one."""
 
     def __init__(self, pool, mode="thread_local"):
         self.pool = pool
@@ -95,37 +95,70 @@ class recording:
         _ACTIVE = None
 
 
+class _BackwardCaptureStart(torch.autograd.Function):
+    """Identity on the loss.  Its backward is the first node autograd runs, on its device
+    thread: the backward capture begins there (HIP refuses to end or cut a capture from a
+    thread other than the one that began it, and the bucket hooks cut from that thread);
+    the capture ends in autograd's final callback, on that same thread."""
+
+    @staticmethod
+    def forward(ctx, x, rec):
+        ctx.rec = rec
+        return x.view_as(x)
+
+    @staticmethod
+    def backward(ctx, g):
+        rec = ctx.rec
+        rec.begin()
+        torch.autograd.Variable._execution_engine.queue_callback(rec.end)
+        return g, None
+
+
 class SegmentedStep:
-    """forward + backward of one static batch shape as segmented HIP graphs.
+    """forward + backward of one static batch shape as HIP graphs: the forward (and loss)
+    as one graph captured on the calling thread, the backward as segments cut where a DDP
+    bucket completes, captured on autograd's device thread.
 
-    ``capture(fn)`` runs ``fn()`` (forward, loss, ``loss.backward()``; its tensors must be
-    static: inputs copied into buffers the caller owns) under capture on a side stream and
-    returns fn's outputs (graph-owned static tensors, refreshed by every replay);
-    ``replay()`` re-runs it, launching the bucket all-reduces between segments."""
+    ``capture(fwd)`` runs ``fwd()`` -> (loss, *outputs) under capture (its tensors must be
+    static: inputs copied into buffers the caller owns), then ``loss.backward()``; returns
+    (loss, *outputs) as graph-owned static tensors refreshed by every replay.  ``replay()``
+    re-runs it, launching each bucket's all-reduce between the backward segments."""
 
-    def __init__(self, device, pool=None):
+    def __init__(self, device, pool=None, stream=None):
+        """``stream``: capture on this stream -- pass the side stream the eager warm-up steps
+        ran on: autograd runs a parameter's gradient accumulation on the stream its
+        accumulator was created on, and a cut must not leave work forked onto another
+        stream unjoined."""
         self.device = torch.device(device)
         self.pool = pool if pool is not None else torch.cuda.graph_pool_handle()
+        self.stream = stream
+        self.fwd = None
         self.rec = None
+        self.one = None
 
-    def capture(self, fn):
-        side = torch.cuda.Stream(device=self.device)
+    def capture(self, fwd):
+        side = self.stream if self.stream is not None else torch.cuda.Stream(device=self.device)
         side.wait_stream(torch.cuda.current_stream(self.device))
         torch.cuda.synchronize(self.device)
-        rec = Recorder(self.pool, mode="global")
-        with torch.cuda.stream(side), recording(rec):
-            rec.begin()
-            try:
-                out = fn()
-            finally:
-                rec.end()
+        rec = Recorder(self.pool)
+        self.one = torch.ones((), device=self.device)  # static seed gradient of the loss
+        with torch.cuda.stream(side):
+            self.fwd = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(self.fwd, pool=self.pool, stream=side, capture_error_mode="thread_local"):
+                out = fwd()
+                loss = _BackwardCaptureStart.apply(out[0], rec)
+            assert loss.dim() == 0 and loss.dtype == torch.float32, "SegmentedStep: scalar fp32 loss"
+            with recording(rec):
+                loss.backward(self.one)
         torch.cuda.current_stream(self.device).wait_stream(side)
+        assert rec.cur is None and rec.segments, "backward capture did not complete"
         self.rec = rec
         return out
 
     @property
     def num_segments(self):
-        return len(self.rec.segments) if self.rec else 0
+        return 1 + (len(self.rec.segments) if self.rec else 0)
 
     def replay(self):
+        self.fwd.replay()
         self.rec.replay()

@@ -276,12 +276,11 @@ class TransformerTrainer:
                       perm=torch.empty(B, dtype=torch.long, device=self.device),
                       lam=torch.empty(B, dtype=torch.float32, device=self.device),
                       seed=torch.zeros(1, dtype=torch.int64, device=self.device))
-            def body():
+            def fwd():
                 mask = st["masks"].view(B, 1, 1, st["masks"].shape[1])
                 with self._autocast(cache=False):  # no cast cache across a graph capture
                     logits, perm, _ = self.model(st["tokens"], st["types"], self.pos_index, mask)
                     loss = mixup_cross_entropy(logits, st["labels"], st["labels"][perm], st["lam"])
-                loss.backward()
                 return loss, logits
 
             torch.cuda.synchronize()
@@ -290,13 +289,14 @@ class TransformerTrainer:
             try:
                 if self.reducer is not None:
                     # segments cut at bucket boundaries; all-reduces launched between them
-                    step = SegmentedStep(self.device, self._graph_pool)
-                    loss, logits = step.capture(body)
+                    step = SegmentedStep(self.device, self._graph_pool, stream=self._graph_stream)
+                    loss, logits = step.capture(fwd)
                     st.update(replay=step.replay, segments=step.num_segments)
                 else:
                     g = torch.cuda.CUDAGraph()
                     with torch.cuda.graph(g, pool=self._graph_pool):
-                        loss, logits = body()
+                        loss, logits = fwd()
+                        loss.backward()
                     st.update(replay=g.replay, segments=1)
             finally:
                 AN.DEVICE_SEED = None

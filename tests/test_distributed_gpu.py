@@ -275,16 +275,14 @@ def _segmented_worker(rank, world):
     sx, sy = xs[0].clone(), ys[0].clone()
 
     def body():
-        loss = F.cross_entropy(m(sx), sy)
-        loss.backward()
-        return loss
+        return (F.cross_entropy(m(sx), sy),)
 
     eager(xs[0], ys[0])  # warm-up on the side stream's allocator
     step = SegmentedStep(dev)
     flat.grad.zero_()
     step.capture(body)
     red.finish()  # (the capture launched nothing; reset the bucket state)
-    assert step.num_segments == len(red.buckets) + 1, (step.num_segments, len(red.buckets))
+    assert step.num_segments == len(red.buckets) + 2, (step.num_segments, len(red.buckets))  # fwd + cuts + tail
     for x, y, w in zip(xs, ys, want):
         sx.copy_(x)
         sy.copy_(y)
