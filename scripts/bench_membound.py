@@ -5,6 +5,7 @@ epilogue traffic, per tile config, with effective HBM bandwidth on the MINIMAL b
     python scripts/bench_membound.py [--batch 1024] [--reps 20]
 
 ops: fwd   = conv(act(x*s+t)) + BN statistics epilogue (block's expanding 1x1)
+     store = plain conv, no prologue / statistics (the store-path ceiling)
      join  = dgrad of the block's first 1x1 + the previous block's residual-join backward
      add   = dgrad + accumulate (EPI_ADD)
      actb  = dgrad through the producer's lazy BN + act (EPI_ACTBWD)
@@ -44,7 +45,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--batch", type=int, default=1024)
     ap.add_argument("--reps", type=int, default=20)
-    ap.add_argument("--ops", default="fwd,join,add,actb")
+    ap.add_argument("--ops", default="fwd,store,join,add,actb")
     ap.add_argument("--shape", default=None, help="H,Cin,Cout: only this shape")
     ap.add_argument("--tile", default=None, help="BM,BN,BK: only this tile")
     a = ap.parse_args()
@@ -84,6 +85,12 @@ def main():
                 n_out = Cin
                 fn = lambda tile: ci.conv_dgrad(g, y, al, be, wd, shp, (N, H, H, Cin), epi=ci.EPI_JOINBWD, out=out,
                                                 ex=ya, part=part3, act=1, alpha=1.0, jmask=mask, tile=tile)
+            elif op == "store":
+                # plain 1x1 (dgrad form, no prologue / statistics): reads [M, Cout], writes [M, Cin]
+                nbytes = M * Cout * 2 + M * Cin * 2
+                n_out = Cin
+                fn = lambda tile: ci.conv_dgrad(g, None, None, None, wd, shp, (N, H, H, Cin), epi=ci.EPI_STORE,
+                                                tile=tile)
             elif op == "add":
                 nbytes = M * Cout * 2 * 2 + M * Cin * 2 * 2
                 n_out = Cin
