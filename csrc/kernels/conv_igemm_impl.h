@@ -163,8 +163,17 @@ __device__ __forceinline__ float4 ld_buf16_sc1(__amdgpu_buffer_rsrc_t r, uint32_
 
 constexpr uint32_t kOOB = 0xFFFFFFF0u;  // byte offset past any buffer: the load returns zeros
 
+// Occupancy floor per instantiation: the 128x128x32 tiles whose prologue / epilogue fit in
+// 128 registers without spilling (no fold prologue, no epilogue loads beyond one tensor:
+// measured with -Rpass-analysis=kernel-resource-usage) are held to 4 waves per SIMD instead
+// of the compiler's 2 (136 VGPRs + 64 AGPRs) -- these are the memory-bound 1x1 / plain-dgrad
+// layers, where twice the workgroups in flight hide load and store latency.
+template <int BM, int BN, int BK, int PRO, bool PURE>
+constexpr int kMinWavesPerEU =
+    (BM == 128 && BN == 128 && BK == 32 && (PRO == kProNone || (PRO == kProAffineAct && PURE))) ? 4 : 1;
+
 template <int BM, int BN, int BK, int PRO, int EPI, bool PURE, int ACT>
-__global__ __launch_bounds__(256) void igemm_kernel(const ConvArgs a) {
+__global__ __launch_bounds__(256, (kMinWavesPerEU<BM, BN, BK, PRO, PURE>)) void igemm_kernel(const ConvArgs a) {
   constexpr int CPR = BK / 8;        // 16-B chunks per LDS row
   constexpr int RPR = 256 / CPR;     // rows covered by one load round
   constexpr int NXL = BM / RPR;      // activation chunks per thread per tile
