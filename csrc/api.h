@@ -118,6 +118,10 @@ void gelu_dropout_bwd(uint64_t g, uint64_t a, uint64_t ga, long n, float p, uint
 // ngd.hip
 void ngd_sumsq(uint64_t X, long per, int G, uint64_t out, uint64_t stream);
 bool ngd_small_supported(int D, int R);
+bool ngd_proj_supported(int D, int R);
+void ngd_proj(uint64_t X, uint64_t Y, uint64_t W, uint64_t Hbuf, int G, int A, int D, int B, int R, uint64_t ip,
+              uint64_t fp, uint64_t J, uint64_t HH, uint64_t stream);
+long ngd_proj_hbuf_numel(int G, int A, int D, int B, int R);
 void ngd_small_proj(uint64_t X, uint64_t Y, uint64_t W, int G, int A, int D, int B, int R, uint64_t sums, uint64_t J,
                     uint64_t HH, uint64_t stream);
 void ngd_rescale(uint64_t X, uint64_t Y, long per, int G, uint64_t ip, uint64_t fp, uint64_t stream);

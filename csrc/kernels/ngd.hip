@@ -291,6 +291,315 @@ void ngd_small_proj(uint64_t X, uint64_t Y, uint64_t W, int G, int A, int D, int
   FDT_LAUNCH_CHECK();
 }
 
+// ---------------------------------------------------------------- general axes (D >= 9)
+// One axis of a stacked parameter in its OWN layout [G][A][D][B] (row n = a B + b, the D
+// elements of a row strided by B): what the PyTorch formulation does as transpose copy ->
+// H = X W^T (batched GEMM) -> Xh = X - H W (batched GEMM) -> |X|^2, |Xh|^2 reductions, and
+// on update steps J = H^T X and H^T H (two more batched GEMMs) -- six or more launches with
+// a full read or write of X each, the GEMMs at [N x D] x [D x R<=80] shapes that the library
+// tiles poorly (profiles/ngd_step_bench.txt) -- is one kernel here.  A workgroup owns 64 rows
+// of one matrix g:
+//   phase 1  H[64][R] = X_tile W^T over 32-wide d chunks staged in LDS (fp32 FMA, each
+//            thread a 4-row x 5-rank register block, float4 LDS reads), |X|^2 on the way;
+//            H^T H of the tile (update steps, when the caller needs it) -> atomics;
+//   phase 2  per d chunk again (second read of X: L2): Y = X - H W (4 rows x 2 d per
+//            thread, W staged transposed so both operands are float4 reads), J += H^T X
+//            (update steps) -> atomics, Y staged through LDS so the store is coalesced in
+//            the tensor's own layout, |Y|^2 on the way.
+// The norm-preserving rescale of Y (and its NaN guard) stays ngd_rescale: it needs |Y|^2 of
+// the whole matrix.  fp32 throughout (the NGD golden tests compare against fp64).
+constexpr int kPN = 64;      // rows per workgroup
+constexpr int kPD = 32;      // d per staged chunk
+constexpr int kPR = 80;      // max rank
+constexpr int kXs = kPD + 4;  // [row][d] stride (float4-aligned)
+constexpr int kWr = kPD + 4;  // W as [r][d] (phase 1)
+constexpr int kWd = kPR + 4;  // W as [d][r] (phase 2); also the H stride
+
+__device__ __forceinline__ void proj_stage_x(float* Xs, const float* x, long n0, long N, int dend, int D, int B,
+                                             int d0, int tid, float* sq) {
+  if (B > 1) {  // thread: row tid & 63 (consecutive b -> coalesced), d (tid >> 6) + 4 i
+    const long n = n0 + (tid & 63);
+    const int row = tid & 63;
+    const bool rv = n < N;
+    const long a = rv ? n / B : 0, b = rv ? n - a * B : 0;
+    const float* xr = x + a * (long)D * B + b;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int dd = (tid >> 6) + 4 * i, d = d0 + dd;
+      float v = 0.f;
+      if (rv && d < dend) v = xr[(long)d * B];
+      Xs[row * kXs + dd] = v;
+      if (sq) *sq = fmaf(v, v, *sq);
+    }
+  } else {  // rows contiguous in d: thread d tid & 31, rows (tid >> 5) + 8 i
+    const int dd = tid & 31, d = d0 + dd;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int row = (tid >> 5) + 8 * i;
+      const long n = n0 + row;
+      float v = 0.f;
+      if (n < N && d < dend) v = x[n * D + d];
+      Xs[row * kXs + dd] = v;
+      if (sq) *sq = fmaf(v, v, *sq);
+    }
+  }
+}
+
+__device__ __forceinline__ void proj_store_y(const float* Ys, float* y, long n0, long N, int dend, int D, int B,
+                                             int d0, int tid, float* sq) {
+  if (B > 1) {
+    const long n = n0 + (tid & 63);
+    const int row = tid & 63;
+    if (n >= N) return;
+    const long a = n / B, b = n - a * B;
+    float* yr = y + a * (long)D * B + b;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int dd = (tid >> 6) + 4 * i, d = d0 + dd;
+      if (d < dend) {
+        const float v = Ys[row * kXs + dd];
+        yr[(long)d * B] = v;
+        *sq = fmaf(v, v, *sq);
+      }
+    }
+  } else {
+    const int dd = tid & 31, d = d0 + dd;
+    if (d >= dend) return;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int row = (tid >> 5) + 8 * i;
+      const long n = n0 + row;
+      if (n < N) {
+        const float v = Ys[row * kXs + dd];
+        y[n * D + d] = v;
+        *sq = fmaf(v, v, *sq);
+      }
+    }
+  }
+}
+
+// Split over d as well as rows: a [N x D] matrix with few rows and a long D (ResNet's
+// [2048, 512] axis 0: 8 row tiles; the transformer embedding's 30522-long axis) would
+// otherwise run as a handful of workgroups walking D serially.  Kernel 1 accumulates
+// partial H of one (row tile, d range) into Hbuf [G][N][R] (atomics when D is split);
+// kernel 2 reloads the tile's H and produces Y, J and |Y|^2 over its own d range.
+struct ProjArgs {
+  const float* X;
+  float* Y;
+  const float* W;
+  float* H;  // [G][N][R]
+  float *ip, *fp, *J, *HH;
+  int A, D, B, R;
+  int tiles, ds, dlen;  // row tiles, d splits, d per split (multiple of kPD)
+};
+
+__global__ __launch_bounds__(256) void ngd_proj_h_kernel(ProjArgs p) {
+  __shared__ __attribute__((aligned(16))) float Xs[kPN * kXs];
+  __shared__ __attribute__((aligned(16))) float Ws[kPR * kWr];
+  __shared__ float red[4];
+  const int tid = threadIdx.x;
+  const int per_g = p.tiles * p.ds;
+  const int g = blockIdx.x / per_g, rem = blockIdx.x - g * per_g;
+  const int tile = rem / p.ds, sp = rem - tile * p.ds;
+  const int D = p.D, R = p.R;
+  const long N = (long)p.A * p.B;
+  const long n0 = (long)tile * kPN;
+  const float* x = p.X + g * N * D;
+  const float* w = p.W + (long)g * R * D;
+  const int dbeg = sp * p.dlen, dend = min(D, dbeg + p.dlen);
+  const int tr = tid >> 4, tc = tid & 15;
+  float sx = 0.f;
+  float acc[4][5];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 5; ++j) acc[i][j] = 0.f;
+  for (int d0 = dbeg; d0 < dend; d0 += kPD) {
+    proj_stage_x(Xs, x, n0, N, dend, D, p.B, d0, tid, p.ip ? &sx : nullptr);
+#pragma unroll
+    for (int i = 0; i < 10; ++i) {  // W chunk as [r][d]
+      const int r = (tid >> 5) + 8 * i, dd = tid & 31, d = d0 + dd;
+      Ws[r * kWr + dd] = (r < R && d < dend) ? w[(long)r * D + d] : 0.f;
+    }
+    __syncthreads();
+#pragma unroll 2
+    for (int dq = 0; dq < kPD; dq += 4) {
+      float4 xv[4], wv[5];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) xv[i] = *reinterpret_cast<const float4*>(Xs + (4 * tr + i) * kXs + dq);
+#pragma unroll
+      for (int j = 0; j < 5; ++j) wv[j] = *reinterpret_cast<const float4*>(Ws + (tc + 16 * j) * kWr + dq);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 5; ++j) {
+          acc[i][j] = fmaf(xv[i].x, wv[j].x, acc[i][j]);
+          acc[i][j] = fmaf(xv[i].y, wv[j].y, acc[i][j]);
+          acc[i][j] = fmaf(xv[i].z, wv[j].z, acc[i][j]);
+          acc[i][j] = fmaf(xv[i].w, wv[j].w, acc[i][j]);
+        }
+    }
+    __syncthreads();
+  }
+  float* h = p.H + g * N * R;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const long n = n0 + 4 * tr + i;
+    if (n >= N) continue;
+#pragma unroll
+    for (int j = 0; j < 5; ++j) {
+      const int r = tc + 16 * j;
+      if (r >= R) continue;
+      if (p.ds == 1) h[n * R + r] = acc[i][j];
+      else atomicAdd(h + n * R + r, acc[i][j]);
+    }
+  }
+  if (p.ip != nullptr) {
+    sx = block_sum256(sx, red);
+    if (tid == 0) atomicAdd(p.ip + g, sx);
+  }
+}
+
+__global__ __launch_bounds__(256) void ngd_proj_y_kernel(ProjArgs p) {
+  __shared__ __attribute__((aligned(16))) float Xs[kPN * kXs];
+  __shared__ __attribute__((aligned(16))) float Ws[kPD * kWd];
+  __shared__ __attribute__((aligned(16))) float Hs[kPN * kWd];
+  __shared__ float red[4];
+  const int tid = threadIdx.x;
+  const int per_g = p.tiles * p.ds;
+  const int g = blockIdx.x / per_g, rem = blockIdx.x - g * per_g;
+  const int tile = rem / p.ds, sp = rem - tile * p.ds;
+  const int D = p.D, R = p.R;
+  const long N = (long)p.A * p.B;
+  const long n0 = (long)tile * kPN;
+  const float* x = p.X + g * N * D;
+  float* y = p.Y + g * N * D;
+  const float* w = p.W + (long)g * R * D;
+  const float* h = p.H + g * N * R;
+  const int dbeg = sp * p.dlen, dend = min(D, dbeg + p.dlen);
+  const int tr = tid >> 4, tc = tid & 15;
+  for (int e = tid; e < kPN * kPR; e += 256) {  // H rows of the tile, zero past N / R
+    const int row = e / kPR, r = e - row * kPR;
+    const long n = n0 + row;
+    Hs[row * kWd + r] = (n < N && r < R) ? h[n * R + r] : 0.f;
+  }
+  __syncthreads();
+  if (p.HH != nullptr && sp == 0) {
+    for (int e = tid; e < R * R; e += 256) {
+      const int r = e / R, q = e - r * R;
+      float s = 0.f;
+#pragma unroll 8
+      for (int n = 0; n < kPN; ++n) s = fmaf(Hs[n * kWd + r], Hs[n * kWd + q], s);
+      atomicAdd(p.HH + (long)g * R * R + e, s);
+    }
+  }
+  float sy = 0.f;
+  for (int d0 = dbeg; d0 < dend; d0 += kPD) {
+    proj_stage_x(Xs, x, n0, N, dend, D, p.B, d0, tid, nullptr);
+#pragma unroll
+    for (int i = 0; i < 10; ++i) {  // W chunk as [d][r]
+      const int r = (tid >> 5) + 8 * i, dd = tid & 31, d = d0 + dd;
+      Ws[dd * kWd + r] = (r < R && d < dend) ? w[(long)r * D + d] : 0.f;
+    }
+    __syncthreads();
+    float yv[4][2];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int k = 0; k < 2; ++k) yv[i][k] = Xs[(4 * tr + i) * kXs + tc + 16 * k];
+    for (int r0 = 0; r0 < R; r0 += 4) {  // H / W columns past R are zero
+      float4 hv[4], wv[2];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) hv[i] = *reinterpret_cast<const float4*>(Hs + (4 * tr + i) * kWd + r0);
+#pragma unroll
+      for (int k = 0; k < 2; ++k) wv[k] = *reinterpret_cast<const float4*>(Ws + (tc + 16 * k) * kWd + r0);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+          float v = yv[i][k];
+          v = fmaf(-hv[i].x, wv[k].x, v);
+          v = fmaf(-hv[i].y, wv[k].y, v);
+          v = fmaf(-hv[i].z, wv[k].z, v);
+          v = fmaf(-hv[i].w, wv[k].w, v);
+          yv[i][k] = v;
+        }
+    }
+    if (p.J != nullptr) {  // J[r][d] += sum_n H[n][r] X[n][d]: thread d = tid & 31, r = (tid >> 5) + 8 j
+      const int dd = tid & 31, d = d0 + dd;
+      float ja[10];
+#pragma unroll
+      for (int j = 0; j < 10; ++j) ja[j] = 0.f;
+      for (int n = 0; n < kPN; ++n) {
+        const float xv = Xs[n * kXs + dd];
+#pragma unroll
+        for (int j = 0; j < 10; ++j) ja[j] = fmaf(Hs[n * kWd + (tid >> 5) + 8 * j], xv, ja[j]);
+      }
+      if (d < dend) {
+#pragma unroll
+        for (int j = 0; j < 10; ++j) {
+          const int r = (tid >> 5) + 8 * j;
+          if (r < R) atomicAdd(p.J + ((long)g * R + r) * D + d, ja[j]);
+        }
+      }
+    }
+    __syncthreads();  // every read of Xs done: stage Y through it
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int k = 0; k < 2; ++k) Xs[(4 * tr + i) * kXs + tc + 16 * k] = yv[i][k];
+    __syncthreads();
+    proj_store_y(Xs, y, n0, N, dend, D, p.B, d0, tid, &sy);
+    __syncthreads();
+  }
+  sy = block_sum256(sy, red);
+  if (tid == 0) atomicAdd(p.fp + g, sy);
+}
+
+bool ngd_proj_supported(int D, int R) { return D >= 9 && R >= 1 && R <= kPR; }
+
+static void proj_split(int G, long N, int D, int& tiles, int& ds, int& dlen) {
+  tiles = (int)((N + kPN - 1) / kPN);
+  const int chunks = (D + kPD - 1) / kPD;
+  // enough workgroups to cover the chip ~4 deep; at least 2 d chunks per workgroup
+  long want = (2048 + (long)G * tiles - 1) / ((long)G * tiles);
+  long cap = (chunks + 1) / 2;
+  ds = (int)(want < 1 ? 1 : (want > cap ? (cap < 1 ? 1 : cap) : want));
+  const int cps = (chunks + ds - 1) / ds;
+  dlen = cps * kPD;
+  ds = (D + dlen - 1) / dlen;
+}
+
+long ngd_proj_hbuf_numel(int G, int A, int D, int B, int R) { return (long)G * A * B * R; }
+
+void ngd_proj(uint64_t X, uint64_t Y, uint64_t W, uint64_t Hbuf, int G, int A, int D, int B, int R, uint64_t ip,
+              uint64_t fp, uint64_t J, uint64_t HH, uint64_t stream) {
+  FDT_CHECK(ngd_proj_supported(D, R), "ngd_proj: needs D >= 9 and rank <= 80");
+  FDT_CHECK(fp != 0 && Hbuf != 0, "ngd_proj: |Y|^2 output and the H buffer are required");
+  if (G == 0 || A == 0 || B == 0) return;
+  const long N = (long)A * B;
+  ProjArgs p{};
+  p.X = P<const float>(X);
+  p.Y = P<float>(Y);
+  p.W = P<const float>(W);
+  p.H = P<float>(Hbuf);
+  p.ip = P<float>(ip);
+  p.fp = P<float>(fp);
+  p.J = P<float>(J);
+  p.HH = P<float>(HH);
+  p.A = A; p.D = D; p.B = B; p.R = R;
+  proj_split(G, N, D, p.tiles, p.ds, p.dlen);
+  const long grid = (long)G * p.tiles * p.ds;
+  FDT_CHECK(grid < (1L << 31), "ngd_proj: grid too large");
+  hipStream_t st = as_stream(stream);
+  // split d: H accumulated with atomics, so zero it first (the caller's buffer is reused)
+  if (p.ds > 1) FDT_HIP_CHECK(hipMemsetAsync(p.H, 0, sizeof(float) * (size_t)G * N * R, st));
+  ngd_proj_h_kernel<<<(unsigned)grid, 256, 0, st>>>(p);
+  FDT_LAUNCH_CHECK();
+  ngd_proj_y_kernel<<<(unsigned)grid, 256, 0, st>>>(p);
+  FDT_LAUNCH_CHECK();
+}
+
 static int ngd_chunks(long per) {
   // ~8 float4 per thread, enough workgroups per matrix to fill the chip (the first version
   // ran 64 scalar elements per thread on a few hundred workgroups: ~10% of HBM bandwidth)

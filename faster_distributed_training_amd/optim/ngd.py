@@ -339,6 +339,60 @@ class NGState:
                         _native.stream_ptr())
         return Y
 
+    # ------------------------------------------------ general axes (HIP, no transposes)
+    def proj_ok(self, G: torch.Tensor) -> bool:
+        """Every other axis (dim >= 9, rank <= 80): one fused HIP pass per step in the
+        parameter's own layout (csrc/kernels/ngd.hip ngd_proj: H = X W^T, X - H W, |X|^2,
+        |Xh|^2 and, on update steps, J = H^T X and H^T H) instead of a transpose copy plus
+        2-4 batched library GEMMs and two reductions."""
+        return (_fused_small_math(G, self.rank) and hasattr(_native.native(), "ngd_proj")
+                and _native.native().ngd_proj_supported(self.dim, self.rank)
+                and (G.numel() // G.shape[0]) % 4 == 0)
+
+    def precondition_proj_gen(self, G: torch.Tensor, A: int, B: int, ip=None):
+        """G: [P, A, dim, B] contiguous -> preconditioned, same layout.  ``ip``: per-matrix
+        |G|^2 when the previous axis already has it."""
+        if self.t == 0:
+            self._init_default()
+            self.t = 1
+            self.defer = False
+            try:
+                for _ in range(3):
+                    yield from self._proj_step(G, A, B, ip)
+                    ip = self.last_ip
+            finally:
+                self.defer = True
+            self.t = 0
+        return (yield from self._proj_step(G, A, B, ip))
+
+    def _proj_step(self, G, A, B, ip_in):
+        updating = self._updating()
+        self.t += 1
+        nat = _native.native()
+        P, R, D = G.shape[0], self.rank, self.dim
+        N = A * B
+        need_hh = updating and N <= D  # L = H^T H (else J W^T, a [R, D] x [D, R] product)
+        nj = P * R * D if updating else 0
+        nh = P * R * R if need_hh else 0
+        buf = torch.zeros(2 * P + nj + nh, device=G.device, dtype=torch.float32)
+        ip = ip_in if ip_in is not None else buf[:P]
+        fp = buf[P:2 * P]
+        J = buf[2 * P:2 * P + nj].view(P, R, D) if updating else None
+        HH = buf[2 * P + nj:].view(P, R, R) if need_hh else None
+        Y = torch.empty_like(G)
+        Hb = torch.empty(nat.ngd_proj_hbuf_numel(P, A, D, B, R), device=G.device, dtype=torch.float32)
+        sp = _native.stream_ptr()
+        nat.ngd_proj(G.data_ptr(), Y.data_ptr(), self.W.data_ptr(), Hb.data_ptr(), P, A, D, B, R,
+                     0 if ip_in is not None else ip.data_ptr(), fp.data_ptr(),
+                     J.data_ptr() if updating else 0, HH.data_ptr() if need_hh else 0, sp)
+        self.last_ip = ip
+        if updating:
+            L = HH if need_hh else torch.bmm(J, self.W.transpose(1, 2))
+            K = torch.bmm(J, J.transpose(1, 2))
+            yield from self._fused_update(J, K, L, ip, N)
+        nat.ngd_rescale(G.data_ptr(), Y.data_ptr(), G.numel() // P, P, ip.data_ptr(), fp.data_ptr(), sp)
+        return Y
+
     def state_dict(self):
         return {"t": self.t, "W": self.W, "d": self.d, "rho": self.rho}
 
@@ -403,6 +457,11 @@ class _ShapeGroup:
                 A = math.prod(self.shape[:ax])
                 B = math.prod(self.shape[ax + 1:])
                 G = (yield from st.precondition_small_gen(G, A, B)).view(G.shape)
+            elif st.proj_ok(G):
+                G = G.contiguous()
+                A = math.prod(self.shape[:ax])
+                B = math.prod(self.shape[ax + 1:])
+                G = (yield from st.precondition_proj_gen(G, A, B, ip)).view(G.shape)
             else:
                 X = G.transpose(-1, a).contiguous()
                 shp = X.shape
@@ -472,6 +531,12 @@ class NGD(SGD):
             super()._step(None, None)
         finally:
             g["weight_decay"] = wd
+
+    def _states(self):
+        """Every batched per-axis preconditioner state (empty before the first step)."""
+        if self.groups is None:
+            return []
+        return [st for sg, _ in self.groups for _, st in sg.axes]
 
     def ngd_state_dict(self):
         if self.groups is None:

@@ -108,3 +108,4 @@ def test_transformer_attention_uses_native_kernel(cuda):
     finally:
         an.FlashAttention.apply = orig
     assert len(calls) == 2
+
