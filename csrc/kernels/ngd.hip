@@ -315,33 +315,49 @@ constexpr int kXs = kPD + 4;  // [row][d] stride (float4-aligned)
 constexpr int kWr = kPD + 4;  // W as [r][d] (phase 1)
 constexpr int kWd = kPR + 4;  // W as [d][r] (phase 2); also the H stride
 
-__device__ __forceinline__ void proj_stage_x(float* Xs, const float* x, long n0, long N, int dend, int D, int B,
-                                             int d0, int tid, float* sq) {
-  if (B > 1) {  // thread: row tid & 63 (consecutive b -> coalesced), d (tid >> 6) + 4 i
+// X chunk [kPN rows][kPD d] of one row tile: global -> 8 registers per thread (issued a chunk
+// ahead, so the loads are in flight during the previous chunk's FMAs), then -> LDS.
+//   B > 1: thread -> row tid & 63 (consecutive b: coalesced), d (tid >> 6) + 4 i
+//   B = 1: thread -> d tid & 31 (rows contiguous in d), rows (tid >> 5) + 8 i
+__device__ __forceinline__ void proj_load_x(float (&v)[8], const float* x, long n0, long N, int dend, int D, int B,
+                                            int d0, int tid) {
+  if (B > 1) {
     const long n = n0 + (tid & 63);
-    const int row = tid & 63;
     const bool rv = n < N;
     const long a = rv ? n / B : 0, b = rv ? n - a * B : 0;
     const float* xr = x + a * (long)D * B + b;
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
-      const int dd = (tid >> 6) + 4 * i, d = d0 + dd;
-      float v = 0.f;
-      if (rv && d < dend) v = xr[(long)d * B];
-      Xs[row * kXs + dd] = v;
-      if (sq) *sq = fmaf(v, v, *sq);
+      const int d = d0 + (tid >> 6) + 4 * i;
+      v[i] = (rv && d < dend) ? xr[(long)d * B] : 0.f;
     }
-  } else {  // rows contiguous in d: thread d tid & 31, rows (tid >> 5) + 8 i
-    const int dd = tid & 31, d = d0 + dd;
+  } else {
+    const int d = d0 + (tid & 31);
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
-      const int row = (tid >> 5) + 8 * i;
-      const long n = n0 + row;
-      float v = 0.f;
-      if (n < N && d < dend) v = x[n * D + d];
-      Xs[row * kXs + dd] = v;
-      if (sq) *sq = fmaf(v, v, *sq);
+      const long n = n0 + (tid >> 5) + 8 * i;
+      v[i] = (n < N && d < dend) ? x[n * D + d] : 0.f;
     }
+  }
+}
+
+__device__ __forceinline__ void proj_put_x(float* Xs, const float (&v)[8], int B, int tid, float* sq) {
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int row = B > 1 ? (tid & 63) : (tid >> 5) + 8 * i;
+    const int dd = B > 1 ? (tid >> 6) + 4 * i : (tid & 31);
+    Xs[row * kXs + dd] = v[i];
+    if (sq) *sq = fmaf(v[i], v[i], *sq);
+  }
+}
+
+// W chunk [80 r][kPD d]: thread -> d tid & 31, r (tid >> 5) + 8 i
+__device__ __forceinline__ void proj_load_w(float (&v)[10], const float* w, int R, int D, int dend, int d0, int tid) {
+  const int d = d0 + (tid & 31);
+#pragma unroll
+  for (int i = 0; i < 10; ++i) {
+    const int r = (tid >> 5) + 8 * i;
+    v[i] = (r < R && d < dend) ? w[(long)r * D + d] : 0.f;
   }
 }
 
@@ -414,12 +430,19 @@ __global__ __launch_bounds__(256) void ngd_proj_h_kernel(ProjArgs p) {
   for (int i = 0; i < 4; ++i)
 #pragma unroll
     for (int j = 0; j < 5; ++j) acc[i][j] = 0.f;
+  float xv8[8], wv10[10];
+  if (dbeg < dend) {
+    proj_load_x(xv8, x, n0, N, dend, D, p.B, dbeg, tid);
+    proj_load_w(wv10, w, R, D, dend, dbeg, tid);
+  }
   for (int d0 = dbeg; d0 < dend; d0 += kPD) {
-    proj_stage_x(Xs, x, n0, N, dend, D, p.B, d0, tid, p.ip ? &sx : nullptr);
+    proj_put_x(Xs, xv8, p.B, tid, p.ip ? &sx : nullptr);
 #pragma unroll
-    for (int i = 0; i < 10; ++i) {  // W chunk as [r][d]
-      const int r = (tid >> 5) + 8 * i, dd = tid & 31, d = d0 + dd;
-      Ws[r * kWr + dd] = (r < R && d < dend) ? w[(long)r * D + d] : 0.f;
+    for (int i = 0; i < 10; ++i) Ws[((tid >> 5) + 8 * i) * kWr + (tid & 31)] = wv10[i];  // W chunk as [r][d]
+    __syncthreads();
+    if (d0 + kPD < dend) {  // next chunk's loads in flight during this chunk's FMAs
+      proj_load_x(xv8, x, n0, N, dend, D, p.B, d0 + kPD, tid);
+      proj_load_w(wv10, w, R, D, dend, d0 + kPD, tid);
     }
     __syncthreads();
 #pragma unroll 2
@@ -460,7 +483,7 @@ __global__ __launch_bounds__(256) void ngd_proj_h_kernel(ProjArgs p) {
   }
 }
 
-__global__ __launch_bounds__(256) void ngd_proj_y_kernel(ProjArgs p) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void ngd_proj_y_kernel(ProjArgs p) {
   __shared__ __attribute__((aligned(16))) float Xs[kPN * kXs];
   __shared__ __attribute__((aligned(16))) float Ws[kPD * kWd];
   __shared__ __attribute__((aligned(16))) float Hs[kPN * kWd];
@@ -494,19 +517,26 @@ __global__ __launch_bounds__(256) void ngd_proj_y_kernel(ProjArgs p) {
     }
   }
   float sy = 0.f;
+  float xv8[8], wv10[10];
+  if (dbeg < dend) {
+    proj_load_x(xv8, x, n0, N, dend, D, p.B, dbeg, tid);
+    proj_load_w(wv10, w, R, D, dend, dbeg, tid);
+  }
   for (int d0 = dbeg; d0 < dend; d0 += kPD) {
-    proj_stage_x(Xs, x, n0, N, dend, D, p.B, d0, tid, nullptr);
+    proj_put_x(Xs, xv8, p.B, tid, nullptr);
 #pragma unroll
-    for (int i = 0; i < 10; ++i) {  // W chunk as [d][r]
-      const int r = (tid >> 5) + 8 * i, dd = tid & 31, d = d0 + dd;
-      Ws[dd * kWd + r] = (r < R && d < dend) ? w[(long)r * D + d] : 0.f;
-    }
+    for (int i = 0; i < 10; ++i) Ws[(tid & 31) * kWd + (tid >> 5) + 8 * i] = wv10[i];  // W chunk as [d][r]
     __syncthreads();
+    if (d0 + kPD < dend) {
+      proj_load_x(xv8, x, n0, N, dend, D, p.B, d0 + kPD, tid);
+      proj_load_w(wv10, w, R, D, dend, d0 + kPD, tid);
+    }
     float yv[4][2];
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
       for (int k = 0; k < 2; ++k) yv[i][k] = Xs[(4 * tr + i) * kXs + tc + 16 * k];
+#pragma unroll 2
     for (int r0 = 0; r0 < R; r0 += 4) {  // H / W columns past R are zero
       float4 hv[4], wv[2];
 #pragma unroll
@@ -530,6 +560,7 @@ __global__ __launch_bounds__(256) void ngd_proj_y_kernel(ProjArgs p) {
       float ja[10];
 #pragma unroll
       for (int j = 0; j < 10; ++j) ja[j] = 0.f;
+#pragma unroll 4
       for (int n = 0; n < kPN; ++n) {
         const float xv = Xs[n * kXs + dd];
 #pragma unroll

@@ -501,14 +501,9 @@ class NGD(SGD):
                          self.flat.device), slots)
             for shape, slots in by_shape.items()]
 
-    @torch.no_grad()
-    def _step(self, grad_scale, found_inf, d_override=None):
+    def _precondition(self, grad, grad_scale):
+        """grad <- NGD-preconditioned (grad * scale + wd * p), in place."""
         g = self.group
-        if found_inf is not None and bool(found_inf.item() != 0):
-            if self.zero_grad_in_step:  # GradScaler skip (fp16 mode only); still clear the gradient
-                self.flat.grad.zero_()
-            return
-        grad = self.flat.grad
         if grad_scale is not None:
             grad.mul_(grad_scale)
         if g["weight_decay"] != 0:
@@ -525,6 +520,15 @@ class NGD(SGD):
                     dst.append(grad[s.offset:s.offset + s.numel].view(s.shape))
                     src.append(out[i])
             torch._foreach_copy_(dst, src)  # multi-tensor launches, not one copy per parameter
+
+    @torch.no_grad()
+    def _step(self, grad_scale, found_inf, d_override=None):
+        g = self.group
+        if found_inf is not None and bool(found_inf.item() != 0):
+            if self.zero_grad_in_step:  # GradScaler skip (fp16 mode only); still clear the gradient
+                self.flat.grad.zero_()
+            return
+        self._precondition(self.flat.grad, grad_scale)
         wd = g["weight_decay"]
         g["weight_decay"] = 0.0
         try:

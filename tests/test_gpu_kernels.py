@@ -577,3 +577,4 @@ def test_ngd_proj_axes_match_gemm_path(cuda, monkeypatch):
     e_proj, e_gemm = rel(run(cuda, True), ref), rel(run(cuda, False), ref)
     assert used, "fused projection path not taken"
     assert e_proj < max(2.0 * e_gemm, 1e-3), (e_proj, e_gemm)
+
