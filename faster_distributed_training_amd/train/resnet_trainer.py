@@ -130,7 +130,7 @@ class ResNetTrainer:
             # ZeRO-2 for NGD: each rank preconditions + updates only the parameters it owns
             # (parallel/zero.py) instead of every rank repeating the whole NGD step
             from ..parallel.zero import ShardedOptimizerDP
-            self.flat = FlatParams(params_owner, device=self.device, partition=self.world)
+            self.flat = FlatParams(params_owner, device=self.device, partition=self.world, balance="ngd")
             self.zero = ShardedOptimizerDP(self.flat, self.model)
         else:
             self.flat = FlatParams(params_owner, device=self.device)

@@ -118,7 +118,7 @@ class TransformerTrainer:
             self.flat = self.fsdp.space
         else:
             part = self.world if (cfg.distributed and ngd_opt and cfg.shard_ngd) else 0
-            self.flat = FlatParams(self.model, device=self.device, with_shadow=shadow, partition=part)
+            self.flat = FlatParams(self.model, device=self.device, with_shadow=shadow, partition=part, balance="ngd")
             if shadow:  # bf16 compute reads the optimizer-maintained bf16 copy (no per-step casts)
                 from ..ops.linear import enable_shadow_weights
                 enable_shadow_weights(self.flat)

@@ -21,6 +21,8 @@ from __future__ import annotations
 
 from dataclasses import dataclass
 
+import math
+
 import torch
 import torch.nn as nn
 
@@ -56,14 +58,54 @@ def partition_runs(sizes, world):
     return [(cuts[i], cuts[i + 1]) for i in range(world)]
 
 
+# NGD cost of a parameter in element-equivalents: each preconditioned axis (dim > 1) costs a
+# fixed ~25 us of launches and small-matrix math whatever its size (measured: ResNet-50 NGD
+# with an element-balanced 8-way split ran 1.7 ms on the rank holding the stem + stage 1
+# -- dozens of small tensors -- and 0.3-0.5 ms on the others, scripts/bench_ngd.py --world)
+NGD_AXIS_COST = 200_000
+
+
+def ngd_cost(shape) -> int:
+    n = 1
+    for d in shape:
+        n *= d
+    return n + NGD_AXIS_COST * sum(1 for d in shape if d > 1)
+
+
+def ngd_balanced_order(shapes, world, slack=1.15):
+    """Order of parameters (indices into ``shapes``) such that cutting it into ``world``
+    contiguous runs balances the NGD cost per rank while every run stays within
+    ``slack`` x the even share of elements (the flat chunk, hence the reduce-scatter /
+    all-gather size, is the largest run).  Greedy: largest cost first onto the cheapest
+    rank with element room.  Returns (order, runs)."""
+    sizes = [_aligned(math.prod(sh)) for sh in shapes]
+    cap = max(max(sizes, default=0), int(slack * sum(sizes) / max(world, 1)) + ALIGN)
+    cost, elems = [0] * world, [0] * world
+    members = [[] for _ in range(world)]
+    for i in sorted(range(len(shapes)), key=lambda i: -ngd_cost(shapes[i])):
+        fits = [r for r in range(world) if elems[r] + sizes[i] <= cap]
+        r = min(fits, key=lambda r: (cost[r], elems[r])) if fits else min(range(world), key=lambda r: elems[r])
+        members[r].append(i)
+        cost[r] += ngd_cost(shapes[i])
+        elems[r] += sizes[i]
+    order, runs = [], []
+    for r in range(world):
+        a = len(order)
+        order += sorted(members[r])  # keep model order inside a run
+        runs.append((a, len(order)))
+    return order, runs
+
+
 class FlatParams:
     """``partition=W``: the slots are split into W contiguous runs of whole parameters
     (balanced) and run r is placed at offset r*chunk (chunk = the longest run, aligned), so
     the buffers are W equal chunks: reduce-scatter / all-gather need no packing (the
-    sharded-optimizer data parallel of ``parallel/zero.py``)."""
+    sharded-optimizer data parallel of ``parallel/zero.py``).  ``balance="ngd"``: runs
+    balance the NGD preconditioning cost (``ngd_balanced_order``; parameters are regrouped,
+    not kept in model order) instead of the element count alone."""
 
     def __init__(self, module_or_params, device=None, reverse=True, with_shadow=False, names=None, partition=0,
-                 dtype=torch.float32):
+                 dtype=torch.float32, balance="numel"):
         if isinstance(module_or_params, nn.Module):
             named = [(n, p) for n, p in module_or_params.named_parameters() if p.requires_grad]
         else:
@@ -75,7 +117,11 @@ class FlatParams:
         self.runs = None
         self.chunk = 0
         if partition and partition >= 1:  # (partition=1: one run, the world-size-1 case)
-            self.runs = partition_runs([_aligned(p.numel()) for _, p in named], partition)
+            if balance == "ngd" and partition > 1:
+                order, self.runs = ngd_balanced_order([tuple(p.shape) for _, p in named], partition)
+                named = [named[i] for i in order]
+            else:
+                self.runs = partition_runs([_aligned(p.numel()) for _, p in named], partition)
             self.chunk = max(sum(_aligned(named[i][1].numel()) for i in range(a, b)) for a, b in self.runs)
             self.chunk = max(self.chunk, ALIGN)
             for r, (a, b) in enumerate(self.runs):

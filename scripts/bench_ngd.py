@@ -17,6 +17,9 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--model", default="resnet50")
     ap.add_argument("--steps", type=int, default=24)
+    ap.add_argument("--world", type=int, default=1,
+                    help="simulate the ZeRO-2 sharded NGD of this many ranks: time each rank's shard optimizer")
+    ap.add_argument("--balance", default="ngd", choices=["ngd", "numel"])
     a = ap.parse_args()
     from faster_distributed_training_amd.optim.ngd import NGD
     from faster_distributed_training_amd.utils.flat import FlatParams
@@ -28,6 +31,18 @@ def main():
         from faster_distributed_training_amd.models.transformer import Transformer
         m = Transformer(4, 30522)
     m = m.to(dev)
+    if a.world > 1:
+        from faster_distributed_training_amd.parallel.zero import ShardView
+        full = FlatParams(m, device=dev, partition=a.world, balance=a.balance)
+        per = []
+        for r, (lo_s, hi_s) in enumerate(full.runs):
+            v = ShardView(full, r * full.chunk, (r + 1) * full.chunk, full.slots[lo_s:hi_s])
+            per.append((r, time_steps(NGD(v, lr=0.01, momentum=0.9, weight_decay=1e-4), v, a.steps, dev)))
+        for r, t in per:
+            print(f"{a.model}: world {a.world} rank {r}: " + ", ".join(f"{k} median {v:.2f} ms" for k, v in t.items()))
+        worst = {k: max(t[k] for _, t in per) for k in per[0][1]}
+        print(f"{a.model}: world {a.world} ({a.balance}-balanced) slowest rank: " + ", ".join(f"{k} {v:.2f} ms" for k, v in worst.items()))
+        return
     f = FlatParams(m, device=dev)
     o = NGD(f, lr=0.01, momentum=0.9, weight_decay=1e-4)
     g = torch.Generator(device=dev).manual_seed(0)
@@ -49,6 +64,22 @@ def main():
             v.sort()
             print(f"{a.model}: {'update' if k else 'non-update'} steps: median {v[len(v) // 2]:.2f} ms "
                   f"(min {v[0]:.2f}, n={len(v)}), {n_axes} batched axis states")
+
+
+def time_steps(o, f, steps, dev):
+    g = torch.Generator(device=dev).manual_seed(0)
+    times = {True: [], False: []}
+    for s in range(steps):
+        f.grad.normal_(generator=g)
+        sts = o._states()
+        upd = bool(sts) and sts[0]._updating()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        o.step()
+        torch.cuda.synchronize()
+        if s >= 12:
+            times[upd].append((time.perf_counter() - t0) * 1e3)
+    return {("update" if k else "non-update"): sorted(v)[len(v) // 2] for k, v in times.items() if v}
 
 
 if __name__ == "__main__":

@@ -14,3 +14,5 @@ timeout -k 10 300 python bench.py --model transformer --steps 20 --warmup 12 > "
 grep '"value"' "$OUT/bench_tr.log" | cut -c1-200
 timeout -k 10 300 python bench.py --ngd --meta_learning --steps 20 --warmup 15 > "$OUT/bench_ngd_meta.log" 2>&1 || { tail "$OUT/bench_ngd_meta.log"; exit 1; }
 grep '"value"' "$OUT/bench_ngd_meta.log" | cut -c1-200
+timeout -k 10 300 python scripts/bench_ngd.py --model resnet50 --steps 32 --world 8 --balance ngd > "$OUT/bench_ngd_w8.log" 2>&1 && timeout -k 10 300 python scripts/bench_ngd.py --model resnet50 --steps 32 --world 8 --balance numel >> "$OUT/bench_ngd_w8.log" 2>&1 || { tail "$OUT/bench_ngd_w8.log"; exit 1; }
+grep world "$OUT/bench_ngd_w8.log"

@@ -104,7 +104,7 @@ def _sharded_ngd_worker(rank, world, steps):
     from faster_distributed_training_amd.parallel.zero import ShardedOptimizerDP
     from faster_distributed_training_amd.utils.flat import FlatParams
     m = _ngd_model(seed=rank).double()
-    flat = FlatParams(m, partition=world, dtype=torch.float64)
+    flat = FlatParams(m, partition=world, dtype=torch.float64, balance="ngd")
     fs = ShardedOptimizerDP(flat, m)
     opt = NGD(fs.view, lr=0.05, momentum=0.9, weight_decay=1e-4)
     ref = _ngd_model(seed=0).double()
