@@ -317,11 +317,24 @@ constexpr int kWd = kPR + 4;  // W as [d][r] (phase 2); also the H stride
 
 // X chunk [kPN rows][kPD d] of one row tile: global -> 8 registers per thread (issued a chunk
 // ahead, so the loads are in flight during the previous chunk's FMAs), then -> LDS.
+//   VEC (B = 1, D % 4 == 0): rows contiguous in d, float4 loads: thread -> row (q >> 3),
+//                            d 4 (q & 7) for q = tid + 256 i, i < 2
 //   B > 1: thread -> row tid & 63 (consecutive b: coalesced), d (tid >> 6) + 4 i
-//   B = 1: thread -> d tid & 31 (rows contiguous in d), rows (tid >> 5) + 8 i
+//   B = 1: thread -> d tid & 31, rows (tid >> 5) + 8 i
+template <bool VEC>
 __device__ __forceinline__ void proj_load_x(float (&v)[8], const float* x, long n0, long N, int dend, int D, int B,
                                             int d0, int tid) {
-  if (B > 1) {
+  if (VEC) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int q = tid + 256 * i;
+      const long n = n0 + (q >> 3);
+      const int d = d0 + 4 * (q & 7);
+      const float4 t = (n < N && d < dend) ? *reinterpret_cast<const float4*>(x + n * D + d)
+                                           : make_float4(0.f, 0.f, 0.f, 0.f);
+      v[4 * i] = t.x; v[4 * i + 1] = t.y; v[4 * i + 2] = t.z; v[4 * i + 3] = t.w;
+    }
+  } else if (B > 1) {
     const long n = n0 + (tid & 63);
     const bool rv = n < N;
     const long a = rv ? n / B : 0, b = rv ? n - a * B : 0;
@@ -341,23 +354,75 @@ __device__ __forceinline__ void proj_load_x(float (&v)[8], const float* x, long 
   }
 }
 
+template <bool VEC>
 __device__ __forceinline__ void proj_put_x(float* Xs, const float (&v)[8], int B, int tid, float* sq) {
+  if (VEC) {
 #pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    const int row = B > 1 ? (tid & 63) : (tid >> 5) + 8 * i;
-    const int dd = B > 1 ? (tid >> 6) + 4 * i : (tid & 31);
-    Xs[row * kXs + dd] = v[i];
-    if (sq) *sq = fmaf(v[i], v[i], *sq);
+    for (int i = 0; i < 2; ++i) {
+      const int q = tid + 256 * i;
+      *reinterpret_cast<float4*>(Xs + (q >> 3) * kXs + 4 * (q & 7)) =
+          make_float4(v[4 * i], v[4 * i + 1], v[4 * i + 2], v[4 * i + 3]);
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int row = B > 1 ? (tid & 63) : (tid >> 5) + 8 * i;
+      const int dd = B > 1 ? (tid >> 6) + 4 * i : (tid & 31);
+      Xs[row * kXs + dd] = v[i];
+    }
+  }
+  if (sq) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) *sq = fmaf(v[i], v[i], *sq);
   }
 }
 
-// W chunk [80 r][kPD d]: thread -> d tid & 31, r (tid >> 5) + 8 i
-__device__ __forceinline__ void proj_load_w(float (&v)[10], const float* w, int R, int D, int dend, int d0, int tid) {
-  const int d = d0 + (tid & 31);
+// W chunk [80 r][kPD d]: VEC -> float4 (r = q >> 3, d 4 (q & 7), q = tid + 256 i < 640);
+// else thread -> d tid & 31, r (tid >> 5) + 8 i
+template <bool VEC>
+__device__ __forceinline__ void proj_load_w(float (&v)[12], const float* w, int R, int D, int dend, int d0, int tid) {
+  if (VEC) {
 #pragma unroll
-  for (int i = 0; i < 10; ++i) {
-    const int r = (tid >> 5) + 8 * i;
-    v[i] = (r < R && d < dend) ? w[(long)r * D + d] : 0.f;
+    for (int i = 0; i < 3; ++i) {
+      const int q = tid + 256 * i;
+      const int r = q >> 3, d = d0 + 4 * (q & 7);
+      const float4 t = (q < kPR * 8 && r < R && d < dend) ? *reinterpret_cast<const float4*>(w + (long)r * D + d)
+                                                          : make_float4(0.f, 0.f, 0.f, 0.f);
+      v[4 * i] = t.x; v[4 * i + 1] = t.y; v[4 * i + 2] = t.z; v[4 * i + 3] = t.w;
+    }
+  } else {
+    const int d = d0 + (tid & 31);
+#pragma unroll
+    for (int i = 0; i < 10; ++i) {
+      const int r = (tid >> 5) + 8 * i;
+      v[i] = (r < R && d < dend) ? w[(long)r * D + d] : 0.f;
+    }
+  }
+}
+
+// W chunk into LDS as [r][d] (stride kWr) or [d][r] (stride kWd)
+template <bool VEC, bool RD>
+__device__ __forceinline__ void proj_put_w(float* Ws, const float (&v)[12], int tid) {
+  if (VEC) {
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      const int q = tid + 256 * i;
+      if (q >= kPR * 8) continue;
+      const int r = q >> 3, c = 4 * (q & 7);
+      if (RD) {
+        *reinterpret_cast<float4*>(Ws + r * kWr + c) = make_float4(v[4 * i], v[4 * i + 1], v[4 * i + 2], v[4 * i + 3]);
+      } else {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) Ws[(c + j) * kWd + r] = v[4 * i + j];
+      }
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < 10; ++i) {
+      const int r = (tid >> 5) + 8 * i, dd = tid & 31;
+      if (RD) Ws[r * kWr + dd] = v[i];
+      else Ws[dd * kWd + r] = v[i];
+    }
   }
 }
 
@@ -409,6 +474,7 @@ struct ProjArgs {
   int tiles, ds, dlen;  // row tiles, d splits, d per split (multiple of kPD)
 };
 
+template <bool VEC>
 __global__ __launch_bounds__(256) void ngd_proj_h_kernel(ProjArgs p) {
   __shared__ __attribute__((aligned(16))) float Xs[kPN * kXs];
   __shared__ __attribute__((aligned(16))) float Ws[kPR * kWr];
@@ -430,19 +496,18 @@ __global__ __launch_bounds__(256) void ngd_proj_h_kernel(ProjArgs p) {
   for (int i = 0; i < 4; ++i)
 #pragma unroll
     for (int j = 0; j < 5; ++j) acc[i][j] = 0.f;
-  float xv8[8], wv10[10];
+  float xv8[8], wv12[12];
   if (dbeg < dend) {
-    proj_load_x(xv8, x, n0, N, dend, D, p.B, dbeg, tid);
-    proj_load_w(wv10, w, R, D, dend, dbeg, tid);
+    proj_load_x<VEC>(xv8, x, n0, N, dend, D, p.B, dbeg, tid);
+    proj_load_w<VEC>(wv12, w, R, D, dend, dbeg, tid);
   }
   for (int d0 = dbeg; d0 < dend; d0 += kPD) {
-    proj_put_x(Xs, xv8, p.B, tid, p.ip ? &sx : nullptr);
-#pragma unroll
-    for (int i = 0; i < 10; ++i) Ws[((tid >> 5) + 8 * i) * kWr + (tid & 31)] = wv10[i];  // W chunk as [r][d]
+    proj_put_x<VEC>(Xs, xv8, p.B, tid, p.ip ? &sx : nullptr);
+    proj_put_w<VEC, true>(Ws, wv12, tid);  // W chunk as [r][d]
     __syncthreads();
     if (d0 + kPD < dend) {  // next chunk's loads in flight during this chunk's FMAs
-      proj_load_x(xv8, x, n0, N, dend, D, p.B, d0 + kPD, tid);
-      proj_load_w(wv10, w, R, D, dend, d0 + kPD, tid);
+      proj_load_x<VEC>(xv8, x, n0, N, dend, D, p.B, d0 + kPD, tid);
+      proj_load_w<VEC>(wv12, w, R, D, dend, d0 + kPD, tid);
     }
     __syncthreads();
 #pragma unroll 2
@@ -483,6 +548,7 @@ __global__ __launch_bounds__(256) void ngd_proj_h_kernel(ProjArgs p) {
   }
 }
 
+template <bool VEC>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void ngd_proj_y_kernel(ProjArgs p) {
   __shared__ __attribute__((aligned(16))) float Xs[kPN * kXs];
   __shared__ __attribute__((aligned(16))) float Ws[kPD * kWd];
@@ -501,10 +567,22 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void n
   const float* h = p.H + g * N * R;
   const int dbeg = sp * p.dlen, dend = min(D, dbeg + p.dlen);
   const int tr = tid >> 4, tc = tid & 15;
-  for (int e = tid; e < kPN * kPR; e += 256) {  // H rows of the tile, zero past N / R
-    const int row = e / kPR, r = e - row * kPR;
-    const long n = n0 + row;
-    Hs[row * kWd + r] = (n < N && r < R) ? h[n * R + r] : 0.f;
+  if ((R & 3) == 0) {  // the tile's H rows are one contiguous [rows][R] block: float4 loads
+    const long nrows = N - n0 < kPN ? N - n0 : kPN;
+    const int q4 = R >> 2;
+    for (int e = tid; e < kPN * (kPR / 4); e += 256) {
+      const int row = e / (kPR / 4), c = 4 * (e - row * (kPR / 4));
+      float4 t = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (row < nrows && c < R) t = reinterpret_cast<const float4*>(h + (n0 + row) * R)[c >> 2];
+      *reinterpret_cast<float4*>(Hs + row * kWd + c) = t;
+    }
+    (void)q4;
+  } else {
+    for (int e = tid; e < kPN * kPR; e += 256) {  // H rows of the tile, zero past N / R
+      const int row = e / kPR, r = e - row * kPR;
+      const long n = n0 + row;
+      Hs[row * kWd + r] = (n < N && r < R) ? h[n * R + r] : 0.f;
+    }
   }
   __syncthreads();
   if (p.HH != nullptr && sp == 0) {
@@ -517,19 +595,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void n
     }
   }
   float sy = 0.f;
-  float xv8[8], wv10[10];
+  float xv8[8], wv12[12];
   if (dbeg < dend) {
-    proj_load_x(xv8, x, n0, N, dend, D, p.B, dbeg, tid);
-    proj_load_w(wv10, w, R, D, dend, dbeg, tid);
+    proj_load_x<VEC>(xv8, x, n0, N, dend, D, p.B, dbeg, tid);
+    proj_load_w<VEC>(wv12, w, R, D, dend, dbeg, tid);
   }
   for (int d0 = dbeg; d0 < dend; d0 += kPD) {
-    proj_put_x(Xs, xv8, p.B, tid, nullptr);
-#pragma unroll
-    for (int i = 0; i < 10; ++i) Ws[(tid & 31) * kWd + (tid >> 5) + 8 * i] = wv10[i];  // W chunk as [d][r]
+    proj_put_x<VEC>(Xs, xv8, p.B, tid, nullptr);
+    proj_put_w<VEC, false>(Ws, wv12, tid);  // W chunk as [d][r]
     __syncthreads();
     if (d0 + kPD < dend) {
-      proj_load_x(xv8, x, n0, N, dend, D, p.B, d0 + kPD, tid);
-      proj_load_w(wv10, w, R, D, dend, d0 + kPD, tid);
+      proj_load_x<VEC>(xv8, x, n0, N, dend, D, p.B, d0 + kPD, tid);
+      proj_load_w<VEC>(wv12, w, R, D, dend, d0 + kPD, tid);
     }
     float yv[4][2];
 #pragma unroll
@@ -574,14 +651,30 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void n
         }
       }
     }
-    __syncthreads();  // every read of Xs done: stage Y through it
+    if (VEC) {  // rows contiguous in d: store Y from registers (16 lanes = 64 contiguous bytes)
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+      for (int i = 0; i < 4; ++i) {
+        const long n = n0 + 4 * tr + i;
 #pragma unroll
-      for (int k = 0; k < 2; ++k) Xs[(4 * tr + i) * kXs + tc + 16 * k] = yv[i][k];
-    __syncthreads();
-    proj_store_y(Xs, y, n0, N, dend, D, p.B, d0, tid, &sy);
-    __syncthreads();
+        for (int k = 0; k < 2; ++k) {
+          const int d = d0 + tc + 16 * k;
+          if (n < N && d < dend) {
+            y[n * D + d] = yv[i][k];
+            sy = fmaf(yv[i][k], yv[i][k], sy);
+          }
+        }
+      }
+      __syncthreads();  // Xs / Ws reads done before the next chunk is staged
+    } else {
+      __syncthreads();  // every read of Xs done: stage Y through it (coalesced strided store)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int k = 0; k < 2; ++k) Xs[(4 * tr + i) * kXs + tc + 16 * k] = yv[i][k];
+      __syncthreads();
+      proj_store_y(Xs, y, n0, N, dend, D, p.B, d0, tid, &sy);
+      __syncthreads();
+    }
   }
   sy = block_sum256(sy, red);
   if (tid == 0) atomicAdd(p.fp + g, sy);
@@ -625,9 +718,13 @@ void ngd_proj(uint64_t X, uint64_t Y, uint64_t W, uint64_t Hbuf, int G, int A, i
   hipStream_t st = as_stream(stream);
   // split d: H accumulated with atomics, so zero it first (the caller's buffer is reused)
   if (p.ds > 1) FDT_HIP_CHECK(hipMemsetAsync(p.H, 0, sizeof(float) * (size_t)G * N * R, st));
-  ngd_proj_h_kernel<<<(unsigned)grid, 256, 0, st>>>(p);
+  // float4 path: rows contiguous in d (the last axis) and 16-B aligned rows / matrices
+  const bool vec = B == 1 && D % 4 == 0 && X % 16 == 0 && Y % 16 == 0 && W % 16 == 0;
+  if (vec) ngd_proj_h_kernel<true><<<(unsigned)grid, 256, 0, st>>>(p);
+  else ngd_proj_h_kernel<false><<<(unsigned)grid, 256, 0, st>>>(p);
   FDT_LAUNCH_CHECK();
-  ngd_proj_y_kernel<<<(unsigned)grid, 256, 0, st>>>(p);
+  if (vec) ngd_proj_y_kernel<true><<<(unsigned)grid, 256, 0, st>>>(p);
+  else ngd_proj_y_kernel<false><<<(unsigned)grid, 256, 0, st>>>(p);
   FDT_LAUNCH_CHECK();
 }
 
