@@ -539,7 +539,7 @@ __global__ __launch_bounds__(256) void ngd_proj_h_kernel(ProjArgs p) {
       const int r = tc + 16 * j;
       if (r >= R) continue;
       if (p.ds == 1) h[n * R + r] = acc[i][j];
-      else atomicAdd(h + n * R + r, acc[i][j]);
+      else p.H[((long)(sp + 1) * (gridDim.x / per_g) + g) * N * R + n * R + r] = acc[i][j];  // slab sp
     }
   }
   if (p.ip != nullptr) {
@@ -694,7 +694,23 @@ static void proj_split(int G, long N, int D, int& tiles, int& ds, int& dlen) {
   ds = (D + dlen - 1) / dlen;
 }
 
-long ngd_proj_hbuf_numel(int G, int A, int D, int B, int R) { return (long)G * A * B * R; }
+// split d: every (tile, d range) workgroup writes its partial H to slab [sp][G][N][R] (after
+// the final [G][N][R] block) and this pass sums the slabs in a fixed order -- no atomics
+// (deterministic) and no zero fill; ~9.8M same-address atomics made the 239-way split of
+// the transformer embedding's 30522-long axis the slowest NGD kernel
+__global__ __launch_bounds__(256) void ngd_proj_hsum_kernel(float* __restrict__ H, long n, int ds) {
+  for (long e = (long)blockIdx.x * 256 + threadIdx.x; e < n; e += (long)gridDim.x * 256) {
+    float s = 0.f;
+    for (int k = 1; k <= ds; ++k) s += H[(long)k * n + e];
+    H[e] = s;
+  }
+}
+
+long ngd_proj_hbuf_numel(int G, int A, int D, int B, int R) {
+  int tiles, ds, dlen;
+  proj_split(G, (long)A * B, D, tiles, ds, dlen);
+  return (long)G * A * B * R * (ds > 1 ? ds + 1 : 1);
+}
 
 void ngd_proj(uint64_t X, uint64_t Y, uint64_t W, uint64_t Hbuf, int G, int A, int D, int B, int R, uint64_t ip,
               uint64_t fp, uint64_t J, uint64_t HH, uint64_t stream) {
@@ -716,13 +732,18 @@ void ngd_proj(uint64_t X, uint64_t Y, uint64_t W, uint64_t Hbuf, int G, int A, i
   const long grid = (long)G * p.tiles * p.ds;
   FDT_CHECK(grid < (1L << 31), "ngd_proj: grid too large");
   hipStream_t st = as_stream(stream);
-  // split d: H accumulated with atomics, so zero it first (the caller's buffer is reused)
-  if (p.ds > 1) FDT_HIP_CHECK(hipMemsetAsync(p.H, 0, sizeof(float) * (size_t)G * N * R, st));
+  const long hn = (long)G * N * R;
   // float4 path: rows contiguous in d (the last axis) and 16-B aligned rows / matrices
   const bool vec = B == 1 && D % 4 == 0 && X % 16 == 0 && Y % 16 == 0 && W % 16 == 0;
   if (vec) ngd_proj_h_kernel<true><<<(unsigned)grid, 256, 0, st>>>(p);
   else ngd_proj_h_kernel<false><<<(unsigned)grid, 256, 0, st>>>(p);
   FDT_LAUNCH_CHECK();
+  if (p.ds > 1) {
+    long nb = (hn + 255) / 256;
+    if (nb > 4096) nb = 4096;
+    ngd_proj_hsum_kernel<<<(unsigned)nb, 256, 0, st>>>(p.H, hn, p.ds);
+    FDT_LAUNCH_CHECK();
+  }
   if (vec) ngd_proj_y_kernel<true><<<(unsigned)grid, 256, 0, st>>>(p);
   else ngd_proj_y_kernel<false><<<(unsigned)grid, 256, 0, st>>>(p);
   FDT_LAUNCH_CHECK();
