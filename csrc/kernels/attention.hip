@@ -71,8 +71,9 @@ struct Args {
 
 // keep-mask hash of (bh, q, key) under the per-call seed: 32-bit murmur3 finaliser (two
 // 32-bit multiplies; the 64-bit mix it replaces cost ~3x the VALU work per score element)
-__device__ __forceinline__ bool dropped(const Args& a, int bh, int q, int key) {
-  uint32_t x = (((uint32_t)bh * (uint32_t)a.L + (uint32_t)q) * (uint32_t)a.L + (uint32_t)key) ^ (uint32_t)a.seed;
+// (lin = (bh L + q) L + key: the callers form it with adds from per-lane / per-tile bases)
+__device__ __forceinline__ bool dropped_lin(const Args& a, uint32_t lin) {
+  uint32_t x = lin ^ (uint32_t)a.seed;
   x += (uint32_t)(a.seed >> 32);
   x ^= x >> 16;
   x *= 0x85ebca6bu;
@@ -81,6 +82,10 @@ __device__ __forceinline__ bool dropped(const Args& a, int bh, int q, int key) {
   x ^= x >> 16;
   return x < a.drop_thr;
 }
+
+// raw v_exp_f32 (exp2f adds a compare / select / ldexp per call for denormal results, which
+// probabilities below 2^-126 do not need); exp2(-inf) = 0
+__device__ __forceinline__ float fexp2(float x) { return __builtin_amdgcn_exp2f(x); }
 
 __device__ __forceinline__ bf16x8_t ld8(const bf16* p) { return *reinterpret_cast<const bf16x8_t*>(p); }
 
@@ -129,16 +134,23 @@ __device__ __forceinline__ int8_t key_state(const Args& a, int b, int key) {
   return a.mask ? (int8_t)(a.mask[(long)b * a.L + key] != 0) : (int8_t)1;
 }
 
-__device__ __forceinline__ float masked_score(float s, int st, const Args& a) {
-  return st > 0 ? s * a.c2 : (st == 0 ? a.fill2 : -INFINITY);
+// key state -> (score multiplier, addend, dS factor): the masked log2-domain score is one
+// FMA, x = s * mul + add, and dS is zeroed by a multiply instead of per-element selects
+__device__ __forceinline__ float4 key_coef(const Args& a, int st) {
+  return st > 0 ? make_float4(a.c2, 0.f, 1.f, 0.f)
+                : make_float4(0.f, st == 0 ? a.fill2 : -INFINITY, 0.f, 0.f);
 }
 
+// log-sum-exp of a fully masked row is -inf: +inf makes exp2(x - lse) = 0 without a select
+__device__ __forceinline__ float lse_safe(float l) { return l == -INFINITY ? INFINITY : l; }
+
 // ------------------------------------------------------------------------------ forward
+template <bool DROP>
 __global__ __launch_bounds__(256) void attn_fwd_kernel(Args a) {
   if (a.seed_ptr != nullptr) a.seed ^= *a.seed_ptr;
   __shared__ __attribute__((aligned(16))) bf16 Ks[kTile * kRowLd];
   __shared__ __attribute__((aligned(16))) bf16 Vs[kTile * kRowLd];
-  __shared__ int8_t ms[kTile];
+  __shared__ __attribute__((aligned(16))) float2 km[kTile];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5, l32 = lane & 31;
   const int b = blockIdx.z, hd = blockIdx.y, bh = b * a.H + hd;
   const int q = blockIdx.x * kBlk + w * 32 + l32;
@@ -155,11 +167,15 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(Args a) {
 #pragma unroll
     for (int r = 0; r < 16; ++r) oacc[dt][r] = 0.f;
   float m = -INFINITY, l = 0.f;
+  const uint32_t qlin = ((uint32_t)bh * (uint32_t)a.L + (uint32_t)q) * (uint32_t)a.L;
 
   for (int k0 = 0; k0 < a.L; k0 += kTile) {
     stage(Ks, kp, a.kl, k0, a.L, tid);
     stage(Vs, vp, a.vl, k0, a.L, tid);
-    if (tid < kTile) ms[tid] = key_state(a, b, k0 + tid);
+    if (tid < kTile) {
+      const float4 c = key_coef(a, key_state(a, b, k0 + tid));
+      km[tid] = make_float2(c.x, c.y);
+    }
     __syncthreads();
     float x[2][16];
     float mb = -INFINITY;
@@ -172,20 +188,21 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(Args a) {
       for (int ks = 0; ks < 4; ++ks) s = mfma(ld8(Ks + (32 * t + l32) * kRowLd + 16 * ks + 8 * h), qf[ks], s);
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        x[t][r] = masked_score(s[r], ms[32 * t + crow(r, h)], a);
+        const float2 c = km[32 * t + crow(r, h)];
+        x[t][r] = fmaf(s[r], c.x, c.y);
         mb = fmaxf(mb, x[t][r]);
       }
     }
     mb = fmaxf(mb, __shfl_xor(mb, 32));
     const float mn = fmaxf(m, mb);
     const float mu = mn == -INFINITY ? 0.f : mn;
-    const float alpha = exp2f(m - mu);
+    const float alpha = fexp2(m - mu);
     float ls = 0.f;
 #pragma unroll
     for (int t = 0; t < 2; ++t)
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const float p = exp2f(x[t][r] - mu);
+        const float p = fexp2(x[t][r] - mu);
         ls += p;
         x[t][r] = p;
       }
@@ -196,12 +213,12 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(Args a) {
     for (int dt = 0; dt < 2; ++dt)
 #pragma unroll
       for (int r = 0; r < 16; ++r) oacc[dt][r] *= alpha;
-    if (a.drop_thr) {
+    if (DROP) {
 #pragma unroll
       for (int t = 0; t < 2; ++t)
 #pragma unroll
         for (int r = 0; r < 16; ++r)
-          x[t][r] = dropped(a, bh, q, k0 + 32 * t + crow(r, h)) ? 0.f : x[t][r] * a.keep_scale;
+          x[t][r] = dropped_lin(a, qlin + (uint32_t)(k0 + 32 * t + crow(r, h))) ? 0.f : x[t][r] * a.keep_scale;
     }
 #pragma unroll
     for (int t = 0; t < 2; ++t)
@@ -252,7 +269,10 @@ __global__ __launch_bounds__(256) void attn_bwd_prep_kernel(Args a) {
   a.delta[((long)b * a.H + hd) * a.L + qpos] = acc;
 }
 
-__global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(Args a) {
+// 2 waves / SIMD: without the floor the dropout variant is allocated 183 VGPRs + 96 AGPRs and
+// runs one wave per SIMD
+template <bool DROP>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void attn_bwd_dkdv_kernel(Args a) {
   if (a.seed_ptr != nullptr) a.seed ^= *a.seed_ptr;
   __shared__ __attribute__((aligned(16))) bf16 Qs[kTile * kRowLd];
   __shared__ __attribute__((aligned(16))) bf16 Gs[kTile * kRowLd];  // dO rows
@@ -273,7 +293,12 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(Args a) {
       vf[s] = ld8(vp + 16 * s + 8 * h);
     }
   }
-  const int st = key_state(a, b, key);
+  const float4 kc4 = key_coef(a, key_state(a, b, key));
+  const float smul = kc4.x, sadd = kc4.y, dsm = kc4.z;
+  // dropout index (bh L + q) L + key for q = q0 + 32 qt + 4h + (r & 3) + 8 (r >> 2): per-tile
+  // base + lo[r & 3] + hi[r >> 2] (adds, no per-element 32-bit multiplies)
+  const uint32_t Lu = (uint32_t)a.L;
+  const uint32_t lo[4] = {0u, Lu, 2u * Lu, 3u * Lu}, hi[4] = {0u, 8u * Lu, 16u * Lu, 24u * Lu};
   const bf16* qbase = a.q + b * a.qb + hd * a.qh;
   const long gl = (long)a.H * kD;  // row stride of the contiguous tensors
   const bf16* gbase = a.dout + (long)b * a.L * gl + hd * kD;
@@ -288,7 +313,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(Args a) {
     stage(Gs, gbase, gl, q0, a.L, tid);
     if (tid < kTile) {
       const int qq = q0 + tid;
-      lse_s[tid] = qq < a.L ? a.lse[(long)bh * a.L + qq] : INFINITY;
+      lse_s[tid] = qq < a.L ? lse_safe(a.lse[(long)bh * a.L + qq]) : INFINITY;
       del_s[tid] = qq < a.L ? a.delta[(long)bh * a.L + qq] : 0.f;
     }
     __syncthreads();
@@ -303,6 +328,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(Args a) {
         dP = mfma(ld8(Gs + (32 * qt + l32) * kRowLd + 16 * ks + 8 * h), vf[ks], dP);
       }
       float p[16], ds[16], lv[16], dv16[16];
+      const uint32_t tlin = ((uint32_t)bh * Lu + (uint32_t)(q0 + 32 * qt + 4 * h)) * Lu + (uint32_t)key;
 #pragma unroll
       for (int g4 = 0; g4 < 4; ++g4) {  // rows crow(4 g4 + j, h) = 32 qt + 8 g4 + 4h + j: one float4
         const float4 l4 = *reinterpret_cast<const float4*>(lse_s + 32 * qt + 8 * g4 + 4 * h);
@@ -312,13 +338,11 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(Args a) {
       }
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const int qr = 32 * qt + crow(r, h);
-        const float lse2 = lv[r];
-        const float pv = lse2 == -INFINITY ? 0.f : exp2f(masked_score(S[r], st, a) - lse2);
+        const float pv = fexp2(fmaf(S[r], smul, sadd) - lv[r]);
         float z = 1.f;
-        if (a.drop_thr) z = dropped(a, bh, q0 + qr, key) ? 0.f : a.keep_scale;
+        if (DROP) z = dropped_lin(a, tlin + lo[r & 3] + hi[r >> 2]) ? 0.f : a.keep_scale;
         p[r] = pv * z;
-        ds[r] = st > 0 ? pv * (dP[r] * z - dv16[r]) : 0.f;
+        ds[r] = dsm * pv * (dP[r] * z - dv16[r]);
       }
 #pragma unroll
       for (int hs = 0; hs < 2; ++hs) {
@@ -350,11 +374,12 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(Args a) {
   }
 }
 
+template <bool DROP>
 __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(Args a) {
   if (a.seed_ptr != nullptr) a.seed ^= *a.seed_ptr;
   __shared__ __attribute__((aligned(16))) bf16 Ks[kTile * kRowLd];
   __shared__ __attribute__((aligned(16))) bf16 Vs[kTile * kRowLd];
-  __shared__ int8_t ms[kTile];
+  __shared__ __attribute__((aligned(16))) float4 km[kTile];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5, l32 = lane & 31;
   const int b = blockIdx.z, hd = blockIdx.y, bh = b * a.H + hd;
   const int q = blockIdx.x * kBlk + w * 32 + l32;
@@ -370,7 +395,8 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(Args a) {
       gf[s] = ld8(gp + 16 * s + 8 * h);
     }
   }
-  const float lse2 = qv ? a.lse[(long)bh * a.L + q] : INFINITY;
+  const float lse2 = qv ? lse_safe(a.lse[(long)bh * a.L + q]) : INFINITY;
+  const uint32_t qlin = ((uint32_t)bh * (uint32_t)a.L + (uint32_t)q) * (uint32_t)a.L;
   const float dl = qv ? a.delta[(long)bh * a.L + q] : 0.f;
   const bf16* kp = a.k + b * a.kb + hd * a.kh;
   const bf16* vp = a.v + b * a.vb + hd * a.vh;
@@ -383,7 +409,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(Args a) {
   for (int k0 = 0; k0 < a.L; k0 += kTile) {
     stage(Ks, kp, a.kl, k0, a.L, tid);
     stage(Vs, vp, a.vl, k0, a.L, tid);
-    if (tid < kTile) ms[tid] = key_state(a, b, k0 + tid);
+    if (tid < kTile) km[tid] = key_coef(a, key_state(a, b, k0 + tid));
     __syncthreads();
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
@@ -399,11 +425,11 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(Args a) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int kr = 32 * t + crow(r, h);
-        const int st = ms[kr];
-        const float pv = lse2 == -INFINITY ? 0.f : exp2f(masked_score(S[r], st, a) - lse2);
+        const float4 c = km[kr];
+        const float pv = fexp2(fmaf(S[r], c.x, c.y) - lse2);
         float z = 1.f;
-        if (a.drop_thr) z = dropped(a, bh, q, k0 + kr) ? 0.f : a.keep_scale;
-        ds[r] = st > 0 ? pv * (dP[r] * z - dl) : 0.f;
+        if (DROP) z = dropped_lin(a, qlin + (uint32_t)(k0 + kr)) ? 0.f : a.keep_scale;
+        ds[r] = c.z * pv * (dP[r] * z - dl);
       }
 #pragma unroll
       for (int hs = 0; hs < 2; ++hs) {
@@ -461,7 +487,9 @@ void attn_fwd(uint64_t q, uint64_t k, uint64_t v, const std::vector<long>& strid
   Args a = make_args(q, k, v, strides, mask, B, L, H, fill, p_drop, seed, seed_ptr);
   a.out = P<bf16>(out);
   a.lse = P<float>(lse);
-  hipLaunchKernelGGL(attn_fwd_kernel, dim3((L + kBlk - 1) / kBlk, H, B), dim3(256), 0, as_stream(stream), a);
+  const dim3 grid((L + kBlk - 1) / kBlk, H, B);
+  if (a.drop_thr) hipLaunchKernelGGL(attn_fwd_kernel<true>, grid, dim3(256), 0, as_stream(stream), a);
+  else hipLaunchKernelGGL(attn_fwd_kernel<false>, grid, dim3(256), 0, as_stream(stream), a);
   FDT_LAUNCH_CHECK();
 }
 
@@ -484,9 +512,11 @@ void attn_bwd(uint64_t q, uint64_t k, uint64_t v, const std::vector<long>& strid
   hipLaunchKernelGGL(attn_bwd_prep_kernel, dim3((unsigned)((rows + 255) / 256)), dim3(256), 0, st, a);
   FDT_LAUNCH_CHECK();
   const dim3 grid((L + kBlk - 1) / kBlk, H, B);
-  hipLaunchKernelGGL(attn_bwd_dkdv_kernel, grid, dim3(256), 0, st, a);
+  if (a.drop_thr) hipLaunchKernelGGL(attn_bwd_dkdv_kernel<true>, grid, dim3(256), 0, st, a);
+  else hipLaunchKernelGGL(attn_bwd_dkdv_kernel<false>, grid, dim3(256), 0, st, a);
   FDT_LAUNCH_CHECK();
-  hipLaunchKernelGGL(attn_bwd_dq_kernel, grid, dim3(256), 0, st, a);
+  if (a.drop_thr) hipLaunchKernelGGL(attn_bwd_dq_kernel<true>, grid, dim3(256), 0, st, a);
+  else hipLaunchKernelGGL(attn_bwd_dq_kernel<false>, grid, dim3(256), 0, st, a);
   FDT_LAUNCH_CHECK();
 }
 
