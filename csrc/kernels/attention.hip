@@ -146,7 +146,7 @@ __device__ __forceinline__ float lse_safe(float l) { return l == -INFINITY ? INF
 
 // ------------------------------------------------------------------------------ forward
 template <bool DROP>
-__global__ __launch_bounds__(256) void attn_fwd_kernel(Args a) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void attn_fwd_kernel(Args a) {
   if (a.seed_ptr != nullptr) a.seed ^= *a.seed_ptr;
   __shared__ __attribute__((aligned(16))) bf16 Ks[kTile * kRowLd];
   __shared__ __attribute__((aligned(16))) bf16 Vs[kTile * kRowLd];
@@ -375,7 +375,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void a
 }
 
 template <bool DROP>
-__global__ __launch_bounds__(256) void attn_bwd_dq_kernel(Args a) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void attn_bwd_dq_kernel(Args a) {
   if (a.seed_ptr != nullptr) a.seed ^= *a.seed_ptr;
   __shared__ __attribute__((aligned(16))) bf16 Ks[kTile * kRowLd];
   __shared__ __attribute__((aligned(16))) bf16 Vs[kTile * kRowLd];

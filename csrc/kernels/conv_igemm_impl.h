@@ -167,10 +167,14 @@ constexpr uint32_t kOOB = 0xFFFFFFF0u;  // byte offset past any buffer: the load
 // 128 registers without spilling (no fold prologue, no epilogue loads beyond one tensor:
 // measured with -Rpass-analysis=kernel-resource-usage) are held to 4 waves per SIMD instead
 // of the compiler's 2 (136 VGPRs + 64 AGPRs) -- these are the memory-bound 1x1 / plain-dgrad
-// layers, where twice the workgroups in flight hide load and store latency.
+// layers, where twice the workgroups in flight hide load and store latency.  The other 128x128
+// tiles (fold prologue at BK = 32, any prologue but the fold at BK = 64) are held to 3 waves
+// (168 registers: spill-free except <= 8-34 VGPRs on a few non-PURE variants, measured the
+// same way); the fold-prologue BK = 64 tiles would spill 120+ and keep the compiler's 2.
 template <int BM, int BN, int BK, int PRO, bool PURE>
 constexpr int kMinWavesPerEU =
-    (BM == 128 && BN == 128 && BK == 32 && (PRO == kProNone || (PRO == kProAffineAct && PURE))) ? 4 : 1;
+    (BM == 128 && BN == 128 && BK == 32 && (PRO == kProNone || (PRO == kProAffineAct && PURE))) ? 4
+    : (BM == 128 && BN == 128 && (BK == 32 || PRO != 2)) ? 3 : 1;
 
 template <int BM, int BN, int BK, int PRO, int EPI, bool PURE, int ACT>
 __global__ __launch_bounds__(256, (kMinWavesPerEU<BM, BN, BK, PRO, PURE>)) void igemm_kernel(const ConvArgs a) {
