@@ -81,12 +81,20 @@ class Deferred:
         self.Z, self.fn = Z, fn
 
 
-def drive(gens):
+def drive(gens, side=None):
     """Run preconditioner generators in lock-step: each yields a batch of Z matrices and
     receives ``(eigenvalues, eigenvectors)``; all Z pending at the same time are solved by
     one ``eigh_many`` launch.  ``Deferred`` yields are collected and solved together after
     all generators finished (one launch for all axes instead of one per axis level).
-    Returns the generators' return values."""
+    Returns the generators' return values.
+
+    ``side`` (a HIP stream): the deferred solve and the state updates it feeds run there,
+    concurrently with whatever the caller's stream does next (the next training step): the
+    eigensolver occupies one workgroup per matrix -- 16-60 of the 256 CUs -- for ~1 ms, and
+    its results are only read by the next optimizer step.  ``drive`` then also returns
+    ``(done_event, keepalive)``: the caller's stream must wait on the event before the state
+    is read again, and ``keepalive`` (the deferred inputs, made on the caller's stream) must
+    outlive that wait."""
     from ..ops.eigh import eigh_many
     results = [None] * len(gens)
     deferred = []
@@ -116,6 +124,16 @@ def drive(gens):
             z = advance(i, o)
             if z is not None:
                 pending[i] = z
+    if side is not None:
+        if not deferred:
+            return results, None
+        side.wait_stream(torch.cuda.current_stream(side.device))
+        with torch.cuda.stream(side):
+            for d, (c, U) in zip(deferred, eigh_many([d.Z for d in deferred])):
+                d.fn(c, U)
+            done = torch.cuda.Event()
+            done.record(side)
+        return results, (done, deferred)
     if deferred:
         for d, (c, U) in zip(deferred, eigh_many([d.Z for d in deferred])):
             d.fn(c, U)
@@ -479,7 +497,7 @@ class NGD(SGD):
     the flat grad -> fused SGD momentum/nesterov update (wd already applied)."""
 
     def __init__(self, flat: FlatParams, lr=1e-4, momentum=0, dampening=0, weight_decay=0, nesterov=False,
-                 ngd=True, alpha=4, rank=-1, update_period=4, eta=0.1, **kw):
+                 ngd=True, alpha=4, rank=-1, update_period=4, eta=0.1, overlap_eigh=True, **kw):
         if lr < 0.0:
             raise ValueError(f"Invalid learning rate: {lr}")
         if momentum < 0.0:
@@ -490,6 +508,10 @@ class NGD(SGD):
                          nesterov=nesterov, **kw)
         self.group.update(ngd=ngd, alpha=alpha, rank=rank, update_period=update_period, eta=eta)
         self.groups = None
+        # deferred eigensolves on a side stream, overlapping the next step (see drive)
+        self.overlap_eigh = overlap_eigh
+        self._side = None
+        self._pending = None
 
     def _build_groups(self):
         g = self.group
@@ -501,8 +523,25 @@ class NGD(SGD):
                          self.flat.device), slots)
             for shape, slots in by_shape.items()]
 
+    def _side_stream(self, grad):
+        """Stream for the deferred eigensolve + state update (see ``drive``): CUDA only."""
+        if not (self.overlap_eigh and grad.is_cuda):
+            return None
+        if self._side is None:
+            self._side = torch.cuda.Stream(device=grad.device)
+        return self._side
+
+    def sync_state(self):
+        """Order the caller's stream after the previous step's deferred state update (the
+        next preconditioning step, checkpointing and tests read W / d / rho)."""
+        if self._pending is not None:
+            done, _keep = self._pending
+            torch.cuda.current_stream().wait_event(done)
+            self._pending = None
+
     def _precondition(self, grad, grad_scale):
         """grad <- NGD-preconditioned (grad * scale + wd * p), in place."""
+        self.sync_state()
         g = self.group
         if grad_scale is not None:
             grad.mul_(grad_scale)
@@ -514,8 +553,13 @@ class NGD(SGD):
             live = [(sg, slots) for sg, slots in self.groups if sg.axes]
             gens = [sg.precondition_gen(torch.stack([grad[s.offset:s.offset + s.numel].view(s.shape) for s in slots]))
                     for sg, slots in live]
+            side = self._side_stream(grad)
+            if side is not None:
+                outs, self._pending = drive(gens, side)
+            else:
+                outs = drive(gens)
             dst, src = [], []
-            for (sg, slots), out in zip(live, drive(gens)):
+            for (sg, slots), out in zip(live, outs):
                 for i, s in enumerate(slots):
                     dst.append(grad[s.offset:s.offset + s.numel].view(s.shape))
                     src.append(out[i])
@@ -538,17 +582,20 @@ class NGD(SGD):
 
     def _states(self):
         """Every batched per-axis preconditioner state (empty before the first step)."""
+        self.sync_state()
         if self.groups is None:
             return []
         return [st for sg, _ in self.groups for _, st in sg.axes]
 
     def ngd_state_dict(self):
+        self.sync_state()
         if self.groups is None:
             return []
         return [[st.state_dict() for _, st in sg.axes] for sg, _ in self.groups]
 
     def load_ngd_state_dict(self, sd):
         """Restore per-axis preconditioner states saved by ``ngd_state_dict`` (same model)."""
+        self.sync_state()
         if not sd:
             return
         if self.groups is None:
