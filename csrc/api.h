@@ -121,9 +121,10 @@ bool ngd_small_supported(int D, int R);
 bool ngd_proj_supported(int D, int R);
 void ngd_proj(uint64_t X, uint64_t Y, uint64_t W, uint64_t Hbuf, int G, int A, int D, int B, int R, uint64_t ip,
               uint64_t fp, uint64_t J, uint64_t HH, uint64_t stream);
-long ngd_proj_hbuf_numel(int G, int A, int D, int B, int R);
+long ngd_proj_hbuf_numel(int G, int A, int D, int B, int R, bool need_ip, bool need_j, bool need_hh);
 void ngd_small_proj(uint64_t X, uint64_t Y, uint64_t W, int G, int A, int D, int B, int R, uint64_t sums, uint64_t J,
-                    uint64_t HH, uint64_t stream);
+                    uint64_t HH, uint64_t part, uint64_t stream);
+long ngd_small_part_numel(int G, int A, int D, int B, int R);
 void ngd_rescale(uint64_t X, uint64_t Y, long per, int G, uint64_t ip, uint64_t fp, uint64_t stream);
 void ngd_pre_eigh(uint64_t K, uint64_t L, uint64_t d, uint64_t rho, uint64_t Z, uint64_t ise, uint64_t drho, uint64_t zs,
                   uint64_t dsum, int G, int R, float alpha, float eta, float N, float D, uint64_t stream);

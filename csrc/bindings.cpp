@@ -42,6 +42,7 @@ PYBIND11_MODULE(_fdt_native, m) {
   DEF(ngd_sumsq);
   DEF(ngd_small_supported);
   DEF(ngd_small_proj);
+  DEF(ngd_small_part_numel);
   DEF(ngd_proj_supported);
   DEF(ngd_proj);
   DEF(ngd_proj_hbuf_numel);

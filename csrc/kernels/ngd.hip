@@ -190,18 +190,17 @@ __global__ __launch_bounds__(256) void ngd_rescale_kernel(const float* __restric
 // each, measured).  It is one streaming pass: each thread owns rows, keeps W (R x D) in
 // registers, and produces in one read of X
 //   Xh = X - (X W^T) W  (written in X's own layout, so no transpose copies),
-//   |X|^2, |Xh|^2, and (update steps) J = H^T X, H^T H  -- block-reduced, one atomic each.
+//   |X|^2, |Xh|^2, and (update steps) J = H^T X, H^T H  -- block-reduced into per-workgroup
+//   partial slots, summed in workgroup order by ngd_small_sums_kernel (bitwise repeatable).
 // X is addressed in the parameter's canonical layout: element (g, a, d, b) of a
 // [G][A][D][B] tensor, row n = a * B + b (the transpose the GEMM path copies into).
 template <int D, int R>
 __global__ __launch_bounds__(256) void ngd_small_proj_kernel(const float* __restrict__ X, float* __restrict__ Y,
                                                              const float* __restrict__ W, int A, int B, int chunks,
-                                                             float* __restrict__ sums, float* __restrict__ J,
-                                                             float* __restrict__ HH) {
+                                                             float* __restrict__ part, bool upd) {
   constexpr int NV = 2 + R * D + R * R;
   __shared__ float red[4][NV];
   const int g = blockIdx.x / chunks, ch = blockIdx.x - g * chunks;
-  const int G = gridDim.x / chunks;
   const int per = A * D * B, rows = A * B;
   const float* x = X + (long)g * per;
   float* y = Y + (long)g * per;
@@ -236,7 +235,7 @@ __global__ __launch_bounds__(256) void ngd_small_proj_kernel(const float* __rest
       v[0] = fmaf(xv[d], xv[d], v[0]);
       v[1] = fmaf(o, o, v[1]);
     }
-    if (J != nullptr) {
+    if (upd) {
 #pragma unroll
       for (int r = 0; r < R; ++r) {
 #pragma unroll
@@ -247,7 +246,7 @@ __global__ __launch_bounds__(256) void ngd_small_proj_kernel(const float* __rest
     }
   }
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const int nv = J != nullptr ? NV : 2;
+  const int nv = upd ? NV : 2;
 #pragma unroll
   for (int i = 0; i < NV; ++i) {
     if (i < nv) {
@@ -256,11 +255,23 @@ __global__ __launch_bounds__(256) void ngd_small_proj_kernel(const float* __rest
     }
   }
   __syncthreads();
+  // per-workgroup partials, summed in a fixed order by ngd_small_sums_kernel (no atomics)
+  float* out = part + ((long)g * chunks + ch) * NV;
+  for (int i = threadIdx.x; i < nv; i += 256) out[i] = red[0][i] + red[1][i] + red[2][i] + red[3][i];
+}
+
+// sums[0][g] = |X|^2, sums[1][g] = |Y|^2, J[g], HH[g] from the partials of the g-th matrix's
+// workgroups, in workgroup order
+__global__ __launch_bounds__(256) void ngd_small_sums_kernel(const float* __restrict__ part, int chunks, int nv, int NV,
+                                                             int RD, float* __restrict__ sums, float* __restrict__ J,
+                                                             float* __restrict__ HH) {
+  const int g = blockIdx.x, G = gridDim.x;
   for (int i = threadIdx.x; i < nv; i += 256) {
-    const float s = red[0][i] + red[1][i] + red[2][i] + red[3][i];
-    if (i < 2) atomicAdd(sums + (long)i * G + g, s);  // sums = [ip[G], fp[G]]
-    else if (i < 2 + R * D) atomicAdd(J + (long)g * R * D + (i - 2), s);
-    else atomicAdd(HH + (long)g * R * R + (i - 2 - R * D), s);
+    float s = 0.f;
+    for (int c = 0; c < chunks; ++c) s += part[((long)g * chunks + c) * NV + i];
+    if (i < 2) sums[(long)i * G + g] = s;
+    else if (i < 2 + RD) J[(long)g * RD + (i - 2)] = s;
+    else HH[(long)g * (NV - 2 - RD) + (i - 2 - RD)] = s;
   }
 }
 
@@ -269,25 +280,39 @@ bool ngd_small_supported(int D, int R) {
          (D == 6 && R == 3) || (D == 7 && R == 4) || (D == 8 && R == 4);
 }
 
-void ngd_small_proj(uint64_t X, uint64_t Y, uint64_t W, int G, int A, int D, int B, int R, uint64_t sums, uint64_t J,
-                    uint64_t HH, uint64_t stream) {
-  FDT_CHECK(ngd_small_supported(D, R), "ngd_small_proj: unsupported (dim, rank)");
-  FDT_CHECK((long)A * D * B < (1L << 31), "ngd_small_proj: matrix too large");
-  FDT_CHECK((J == 0) == (HH == 0), "ngd_small_proj: J and HH together");
-  if (G == 0 || A == 0 || B == 0) return;
-  const long rows = (long)A * B;
+static long small_chunks(long rows) {
   long ch = rows / (256 * 16);  // ~16 rows per thread
   if (ch < 1) ch = 1;
   if (ch > 1024) ch = 1024;
+  return ch;
+}
+
+long ngd_small_part_numel(int G, int A, int D, int B, int R) {
+  return (long)G * small_chunks((long)A * B) * (2 + R * D + R * R);
+}
+
+void ngd_small_proj(uint64_t X, uint64_t Y, uint64_t W, int G, int A, int D, int B, int R, uint64_t sums, uint64_t J,
+                    uint64_t HH, uint64_t part, uint64_t stream) {
+  FDT_CHECK(ngd_small_supported(D, R), "ngd_small_proj: unsupported (dim, rank)");
+  FDT_CHECK((long)A * D * B < (1L << 31), "ngd_small_proj: matrix too large");
+  FDT_CHECK((J == 0) == (HH == 0), "ngd_small_proj: J and HH together");
+  FDT_CHECK(part != 0, "ngd_small_proj: partial-sum buffer required");
+  if (G == 0 || A == 0 || B == 0) return;
+  const long ch = small_chunks((long)A * B);
   const dim3 grid((unsigned)(G * ch));
+  const bool upd = J != 0;
   hipStream_t s = as_stream(stream);
 #define FDT_NGD_SMALL(DD, RR)                                                                                      \
   if (D == DD && R == RR)                                                                                         \
     ngd_small_proj_kernel<DD, RR><<<grid, 256, 0, s>>>(P<const float>(X), P<float>(Y), P<const float>(W), A, B, \
-                                                       (int)ch, P<float>(sums), P<float>(J), P<float>(HH));
+                                                       (int)ch, P<float>(part), upd);
   FDT_NGD_SMALL(2, 1) FDT_NGD_SMALL(3, 2) FDT_NGD_SMALL(4, 2) FDT_NGD_SMALL(5, 3) FDT_NGD_SMALL(6, 3)
   FDT_NGD_SMALL(7, 4) FDT_NGD_SMALL(8, 4)
 #undef FDT_NGD_SMALL
+  FDT_LAUNCH_CHECK();
+  const int NV = 2 + R * D + R * R;
+  ngd_small_sums_kernel<<<G, 256, 0, s>>>(P<const float>(part), (int)ch, upd ? NV : 2, NV, R * D, P<float>(sums),
+                                          P<float>(J), P<float>(HH));
   FDT_LAUNCH_CHECK();
 }
 
@@ -464,12 +489,19 @@ __device__ __forceinline__ void proj_store_y(const float* Ys, float* y, long n0,
 // otherwise run as a handful of workgroups walking D serially.  Kernel 1 accumulates
 // partial H of one (row tile, d range) into Hbuf [G][N][R] (atomics when D is split);
 // kernel 2 reloads the tile's H and produces Y, J and |Y|^2 over its own d range.
+// Every reduction across workgroups goes through per-workgroup partial slots summed in a
+// fixed order afterwards (ngd_proj_sums_kernel / ngd_slab_sum_kernel): no atomics, so the
+// projection is bitwise repeatable (NGD's early near-degenerate eigenproblems turn atomic-
+// order noise into O(1) run-to-run differences).
 struct ProjArgs {
   const float* X;
   float* Y;
   const float* W;
-  float* H;  // [G][N][R]
-  float *ip, *fp, *J, *HH;
+  float* H;    // [G][N][R] (+ ds slabs of partial H when d is split)
+  float* ipp;  // [G][tiles * ds] partial |X|^2 (nullptr: not wanted)
+  float* fpp;  // [G][tiles * ds] partial |Y|^2
+  float* Jp;   // [tiles][G][R][D] partial J (nullptr: not an update step)
+  float* HHp;  // [tiles][G][R][R] partial H^T H (nullptr: not wanted)
   int A, D, B, R;
   int tiles, ds, dlen;  // row tiles, d splits, d per split (multiple of kPD)
 };
@@ -502,7 +534,7 @@ __global__ __launch_bounds__(256) void ngd_proj_h_kernel(ProjArgs p) {
     proj_load_w<VEC>(wv12, w, R, D, dend, dbeg, tid);
   }
   for (int d0 = dbeg; d0 < dend; d0 += kPD) {
-    proj_put_x<VEC>(Xs, xv8, p.B, tid, p.ip ? &sx : nullptr);
+    proj_put_x<VEC>(Xs, xv8, p.B, tid, p.ipp ? &sx : nullptr);
     proj_put_w<VEC, true>(Ws, wv12, tid);  // W chunk as [r][d]
     __syncthreads();
     if (d0 + kPD < dend) {  // next chunk's loads in flight during this chunk's FMAs
@@ -539,12 +571,12 @@ __global__ __launch_bounds__(256) void ngd_proj_h_kernel(ProjArgs p) {
       const int r = tc + 16 * j;
       if (r >= R) continue;
       if (p.ds == 1) h[n * R + r] = acc[i][j];
-      else p.H[((long)(sp + 1) * (gridDim.x / per_g) + g) * N * R + n * R + r] = acc[i][j];  // slab sp
+      else p.H[((long)sp * (gridDim.x / per_g) + g) * N * R + n * R + r] = acc[i][j];  // slab sp
     }
   }
-  if (p.ip != nullptr) {
+  if (p.ipp != nullptr) {
     sx = block_sum256(sx, red);
-    if (tid == 0) atomicAdd(p.ip + g, sx);
+    if (tid == 0) p.ipp[(long)g * per_g + rem] = sx;
   }
 }
 
@@ -585,13 +617,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void n
     }
   }
   __syncthreads();
-  if (p.HH != nullptr && sp == 0) {
+  if (p.HHp != nullptr && sp == 0) {
+    const int G = gridDim.x / per_g;
     for (int e = tid; e < R * R; e += 256) {
       const int r = e / R, q = e - r * R;
       float s = 0.f;
 #pragma unroll 8
       for (int n = 0; n < kPN; ++n) s = fmaf(Hs[n * kWd + r], Hs[n * kWd + q], s);
-      atomicAdd(p.HH + (long)g * R * R + e, s);
+      p.HHp[((long)tile * G + g) * R * R + e] = s;
     }
   }
   float sy = 0.f;
@@ -632,7 +665,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void n
           yv[i][k] = v;
         }
     }
-    if (p.J != nullptr) {  // J[r][d] += sum_n H[n][r] X[n][d]: thread d = tid & 31, r = (tid >> 5) + 8 j
+    if (p.Jp != nullptr) {  // J[r][d] += sum_n H[n][r] X[n][d]: thread d = tid & 31, r = (tid >> 5) + 8 j
       const int dd = tid & 31, d = d0 + dd;
       float ja[10];
 #pragma unroll
@@ -647,7 +680,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void n
 #pragma unroll
         for (int j = 0; j < 10; ++j) {
           const int r = (tid >> 5) + 8 * j;
-          if (r < R) atomicAdd(p.J + ((long)g * R + r) * D + d, ja[j]);
+          if (r < R) p.Jp[(((long)tile * (gridDim.x / per_g) + g) * R + r) * D + d] = ja[j];
         }
       }
     }
@@ -677,7 +710,28 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void n
     }
   }
   sy = block_sum256(sy, red);
-  if (tid == 0) atomicAdd(p.fp + g, sy);
+  if (tid == 0) p.fpp[(long)g * per_g + rem] = sy;
+}
+
+// fixed-order sums of the per-workgroup partials: out[g] = sum_k part[g][k] (one block per g)
+__global__ __launch_bounds__(256) void ngd_proj_sums_kernel(const float* __restrict__ part, float* __restrict__ out,
+                                                            int nk) {
+  __shared__ float red[4];
+  const int g = blockIdx.x;
+  float s = 0.f;
+  for (int k = threadIdx.x; k < nk; k += 256) s += part[(long)g * nk + k];
+  s = block_sum256(s, red);
+  if (threadIdx.x == 0) out[g] = s;
+}
+
+// dst[e] = sum_{k < ns} src[k n + e], k in order
+__global__ __launch_bounds__(256) void ngd_slab_sum_kernel(const float* __restrict__ src, float* __restrict__ dst,
+                                                           long n, int ns) {
+  for (long e = (long)blockIdx.x * 256 + threadIdx.x; e < n; e += (long)gridDim.x * 256) {
+    float s = 0.f;
+    for (int k = 0; k < ns; ++k) s += src[(long)k * n + e];
+    dst[e] = s;
+  }
 }
 
 bool ngd_proj_supported(int D, int R) { return D >= 9 && R >= 1 && R <= kPR; }
@@ -694,41 +748,60 @@ static void proj_split(int G, long N, int D, int& tiles, int& ds, int& dlen) {
   ds = (D + dlen - 1) / dlen;
 }
 
-// split d: every (tile, d range) workgroup writes its partial H to slab [sp][G][N][R] (after
-// the final [G][N][R] block) and this pass sums the slabs in a fixed order -- no atomics
-// (deterministic) and no zero fill; ~9.8M same-address atomics made the 239-way split of
-// the transformer embedding's 30522-long axis the slowest NGD kernel
-__global__ __launch_bounds__(256) void ngd_proj_hsum_kernel(float* __restrict__ H, long n, int ds) {
-  for (long e = (long)blockIdx.x * 256 + threadIdx.x; e < n; e += (long)gridDim.x * 256) {
-    float s = 0.f;
-    for (int k = 1; k <= ds; ++k) s += H[(long)k * n + e];
-    H[e] = s;
-  }
+// scratch layout of one ngd_proj call (floats): final H [G][N][R], then (d split) ds slabs
+// of partial H, the partial |X|^2 and |Y|^2 slots [G][tiles * ds], and on update steps the
+// partial J [tiles][G][R][D] and H^T H [tiles][G][R][R] slabs.  Every slot is written
+// exactly once per call, so the buffer needs no zero fill.
+struct ProjLayout {
+  long h, hslab, ipp, fpp, jp, hhp, total;
+};
+
+static ProjLayout proj_layout(int G, long N, int D, int R, int tiles, int ds, bool need_ip, bool need_j,
+                              bool need_hh) {
+  ProjLayout L{};
+  const long hn = (long)G * N * R, nwg = (long)G * tiles * ds;
+  long o = 0;
+  L.h = o; o += hn;
+  L.hslab = o; o += ds > 1 ? ds * hn : 0;
+  L.ipp = o; o += need_ip ? nwg : 0;
+  L.fpp = o; o += nwg;
+  L.jp = o; o += need_j ? (long)tiles * G * R * D : 0;
+  L.hhp = o; o += need_hh ? (long)tiles * G * R * R : 0;
+  L.total = o;
+  return L;
 }
 
-long ngd_proj_hbuf_numel(int G, int A, int D, int B, int R) {
+long ngd_proj_hbuf_numel(int G, int A, int D, int B, int R, bool need_ip, bool need_j, bool need_hh) {
   int tiles, ds, dlen;
   proj_split(G, (long)A * B, D, tiles, ds, dlen);
-  return (long)G * A * B * R * (ds > 1 ? ds + 1 : 1);
+  return proj_layout(G, (long)A * B, D, R, tiles, ds, need_ip, need_j, need_hh).total;
+}
+
+static int slab_blocks(long n) {
+  long nb = (n + 255) / 256;
+  return (int)(nb > 4096 ? 4096 : (nb < 1 ? 1 : nb));
 }
 
 void ngd_proj(uint64_t X, uint64_t Y, uint64_t W, uint64_t Hbuf, int G, int A, int D, int B, int R, uint64_t ip,
               uint64_t fp, uint64_t J, uint64_t HH, uint64_t stream) {
   FDT_CHECK(ngd_proj_supported(D, R), "ngd_proj: needs D >= 9 and rank <= 80");
-  FDT_CHECK(fp != 0 && Hbuf != 0, "ngd_proj: |Y|^2 output and the H buffer are required");
+  FDT_CHECK(fp != 0 && Hbuf != 0, "ngd_proj: |Y|^2 output and the scratch buffer are required");
   if (G == 0 || A == 0 || B == 0) return;
   const long N = (long)A * B;
   ProjArgs p{};
   p.X = P<const float>(X);
   p.Y = P<float>(Y);
   p.W = P<const float>(W);
-  p.H = P<float>(Hbuf);
-  p.ip = P<float>(ip);
-  p.fp = P<float>(fp);
-  p.J = P<float>(J);
-  p.HH = P<float>(HH);
   p.A = A; p.D = D; p.B = B; p.R = R;
   proj_split(G, N, D, p.tiles, p.ds, p.dlen);
+  const ProjLayout L = proj_layout(G, N, D, R, p.tiles, p.ds, ip != 0, J != 0, HH != 0);
+  float* sc = P<float>(Hbuf);
+  // kernel 1 writes partial H into the slabs when d is split (summed into sc + L.h below)
+  p.H = p.ds > 1 ? sc + L.hslab : sc + L.h;
+  p.ipp = ip ? sc + L.ipp : nullptr;
+  p.fpp = sc + L.fpp;
+  p.Jp = J ? sc + L.jp : nullptr;
+  p.HHp = HH ? sc + L.hhp : nullptr;
   const long grid = (long)G * p.tiles * p.ds;
   FDT_CHECK(grid < (1L << 31), "ngd_proj: grid too large");
   hipStream_t st = as_stream(stream);
@@ -739,14 +812,30 @@ void ngd_proj(uint64_t X, uint64_t Y, uint64_t W, uint64_t Hbuf, int G, int A, i
   else ngd_proj_h_kernel<false><<<(unsigned)grid, 256, 0, st>>>(p);
   FDT_LAUNCH_CHECK();
   if (p.ds > 1) {
-    long nb = (hn + 255) / 256;
-    if (nb > 4096) nb = 4096;
-    ngd_proj_hsum_kernel<<<(unsigned)nb, 256, 0, st>>>(p.H, hn, p.ds);
+    ngd_slab_sum_kernel<<<slab_blocks(hn), 256, 0, st>>>(sc + L.hslab, sc + L.h, hn, p.ds);
     FDT_LAUNCH_CHECK();
+    p.H = sc + L.h;
   }
   if (vec) ngd_proj_y_kernel<true><<<(unsigned)grid, 256, 0, st>>>(p);
   else ngd_proj_y_kernel<false><<<(unsigned)grid, 256, 0, st>>>(p);
   FDT_LAUNCH_CHECK();
+  const int nwg = p.tiles * p.ds;
+  if (ip) {
+    ngd_proj_sums_kernel<<<G, 256, 0, st>>>(p.ipp, P<float>(ip), nwg);
+    FDT_LAUNCH_CHECK();
+  }
+  ngd_proj_sums_kernel<<<G, 256, 0, st>>>(p.fpp, P<float>(fp), nwg);
+  FDT_LAUNCH_CHECK();
+  if (J) {
+    const long jn = (long)G * R * D;
+    ngd_slab_sum_kernel<<<slab_blocks(jn), 256, 0, st>>>(p.Jp, P<float>(J), jn, p.tiles);
+    FDT_LAUNCH_CHECK();
+  }
+  if (HH) {
+    const long hhn = (long)G * R * R;
+    ngd_slab_sum_kernel<<<slab_blocks(hhn), 256, 0, st>>>(p.HHp, P<float>(HH), hhn, p.tiles);
+    FDT_LAUNCH_CHECK();
+  }
 }
 
 static int ngd_chunks(long per) {

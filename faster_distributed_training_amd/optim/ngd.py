@@ -346,8 +346,10 @@ class NGState:
         J = buf[2 * P:2 * P + nj].view(P, R, D) if updating else None
         HH = buf[2 * P + nj:].view(P, R, R) if updating else None
         Y = torch.empty_like(G)
+        part = torch.empty(nat.ngd_small_part_numel(P, A, D, B, R), device=G.device, dtype=torch.float32)
         nat.ngd_small_proj(G.data_ptr(), Y.data_ptr(), self.W.data_ptr(), P, A, D, B, R, sums.data_ptr(),
-                           J.data_ptr() if updating else 0, HH.data_ptr() if updating else 0, _native.stream_ptr())
+                           J.data_ptr() if updating else 0, HH.data_ptr() if updating else 0, part.data_ptr(),
+                           _native.stream_ptr())
         self.last_ip = ip
         if updating:
             L = torch.bmm(J, self.W.transpose(1, 2)) if N > D else HH
@@ -398,7 +400,8 @@ class NGState:
         J = buf[2 * P:2 * P + nj].view(P, R, D) if updating else None
         HH = buf[2 * P + nj:].view(P, R, R) if need_hh else None
         Y = torch.empty_like(G)
-        Hb = torch.empty(nat.ngd_proj_hbuf_numel(P, A, D, B, R), device=G.device, dtype=torch.float32)
+        Hb = torch.empty(nat.ngd_proj_hbuf_numel(P, A, D, B, R, ip_in is None, updating, need_hh), device=G.device,
+                         dtype=torch.float32)
         sp = _native.stream_ptr()
         nat.ngd_proj(G.data_ptr(), Y.data_ptr(), self.W.data_ptr(), Hb.data_ptr(), P, A, D, B, R,
                      0 if ip_in is not None else ip.data_ptr(), fp.data_ptr(),
