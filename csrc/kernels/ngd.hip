@@ -713,24 +713,33 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void n
   if (tid == 0) p.fpp[(long)g * per_g + rem] = sy;
 }
 
-// fixed-order sums of the per-workgroup partials: out[g] = sum_k part[g][k] (one block per g)
-__global__ __launch_bounds__(256) void ngd_proj_sums_kernel(const float* __restrict__ part, float* __restrict__ out,
-                                                            int nk) {
+// fixed-order sums of the per-workgroup partials, one block per (g, quantity): block b < G
+// sums |Y|^2 of matrix b, block G + b (when ipp is given) |X|^2
+__global__ __launch_bounds__(256) void ngd_proj_sums_kernel(const float* __restrict__ fpp, float* __restrict__ fp,
+                                                            const float* __restrict__ ipp, float* __restrict__ ip,
+                                                            int G, int nk) {
   __shared__ float red[4];
-  const int g = blockIdx.x;
+  const bool second = (int)blockIdx.x >= G;
+  const int g = second ? blockIdx.x - G : blockIdx.x;
+  const float* part = second ? ipp : fpp;
   float s = 0.f;
   for (int k = threadIdx.x; k < nk; k += 256) s += part[(long)g * nk + k];
   s = block_sum256(s, red);
-  if (threadIdx.x == 0) out[g] = s;
+  if (threadIdx.x == 0) (second ? ip : fp)[g] = s;
 }
 
-// dst[e] = sum_{k < ns} src[k n + e], k in order
+// dst[e] = sum_{k < ns} src[k n + e], k in order; a second (src2, dst2, n2) slab set in the
+// same launch (J and H^T H of an update step) follows the first in the index space
 __global__ __launch_bounds__(256) void ngd_slab_sum_kernel(const float* __restrict__ src, float* __restrict__ dst,
-                                                           long n, int ns) {
-  for (long e = (long)blockIdx.x * 256 + threadIdx.x; e < n; e += (long)gridDim.x * 256) {
+                                                           long n, int ns, const float* __restrict__ src2,
+                                                           float* __restrict__ dst2, long n2) {
+  for (long e = (long)blockIdx.x * 256 + threadIdx.x; e < n + n2; e += (long)gridDim.x * 256) {
+    const bool two = e >= n;
+    const float* s_ = two ? src2 : src;
+    const long m = two ? n2 : n, i = two ? e - n : e;
     float s = 0.f;
-    for (int k = 0; k < ns; ++k) s += src[(long)k * n + e];
-    dst[e] = s;
+    for (int k = 0; k < ns; ++k) s += s_[(long)k * m + i];
+    (two ? dst2 : dst)[i] = s;
   }
 }
 
@@ -786,6 +795,7 @@ void ngd_proj(uint64_t X, uint64_t Y, uint64_t W, uint64_t Hbuf, int G, int A, i
               uint64_t fp, uint64_t J, uint64_t HH, uint64_t stream) {
   FDT_CHECK(ngd_proj_supported(D, R), "ngd_proj: needs D >= 9 and rank <= 80");
   FDT_CHECK(fp != 0 && Hbuf != 0, "ngd_proj: |Y|^2 output and the scratch buffer are required");
+  FDT_CHECK(HH == 0 || J != 0, "ngd_proj: H^T H only on update steps (with J)");
   if (G == 0 || A == 0 || B == 0) return;
   const long N = (long)A * B;
   ProjArgs p{};
@@ -812,7 +822,7 @@ void ngd_proj(uint64_t X, uint64_t Y, uint64_t W, uint64_t Hbuf, int G, int A, i
   else ngd_proj_h_kernel<false><<<(unsigned)grid, 256, 0, st>>>(p);
   FDT_LAUNCH_CHECK();
   if (p.ds > 1) {
-    ngd_slab_sum_kernel<<<slab_blocks(hn), 256, 0, st>>>(sc + L.hslab, sc + L.h, hn, p.ds);
+    ngd_slab_sum_kernel<<<slab_blocks(hn), 256, 0, st>>>(sc + L.hslab, sc + L.h, hn, p.ds, nullptr, nullptr, 0);
     FDT_LAUNCH_CHECK();
     p.H = sc + L.h;
   }
@@ -820,20 +830,12 @@ void ngd_proj(uint64_t X, uint64_t Y, uint64_t W, uint64_t Hbuf, int G, int A, i
   else ngd_proj_y_kernel<false><<<(unsigned)grid, 256, 0, st>>>(p);
   FDT_LAUNCH_CHECK();
   const int nwg = p.tiles * p.ds;
-  if (ip) {
-    ngd_proj_sums_kernel<<<G, 256, 0, st>>>(p.ipp, P<float>(ip), nwg);
-    FDT_LAUNCH_CHECK();
-  }
-  ngd_proj_sums_kernel<<<G, 256, 0, st>>>(p.fpp, P<float>(fp), nwg);
+  ngd_proj_sums_kernel<<<ip ? 2 * G : G, 256, 0, st>>>(p.fpp, P<float>(fp), p.ipp, P<float>(ip), G, nwg);
   FDT_LAUNCH_CHECK();
-  if (J) {
-    const long jn = (long)G * R * D;
-    ngd_slab_sum_kernel<<<slab_blocks(jn), 256, 0, st>>>(p.Jp, P<float>(J), jn, p.tiles);
-    FDT_LAUNCH_CHECK();
-  }
-  if (HH) {
-    const long hhn = (long)G * R * R;
-    ngd_slab_sum_kernel<<<slab_blocks(hhn), 256, 0, st>>>(p.HHp, P<float>(HH), hhn, p.tiles);
+  if (J) {  // J (and H^T H) slab sums in one launch
+    const long jn = (long)G * R * D, hhn = HH ? (long)G * R * R : 0;
+    ngd_slab_sum_kernel<<<slab_blocks(jn + hhn), 256, 0, st>>>(p.Jp, P<float>(J), jn, p.tiles, p.HHp, P<float>(HH),
+                                                               hhn);
     FDT_LAUNCH_CHECK();
   }
 }
