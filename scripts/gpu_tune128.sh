@@ -1,0 +1,14 @@
+#!/usr/bin/env bash
+# Re-tune the batch-128 conv tile table after the occupancy-floor change, then A/B the bench.
+set -o pipefail
+cd "$(dirname "$0")/.."
+export TMPDIR=/tmp
+OUT=gpurun_out/${1:-tune128}
+mkdir -p "$OUT"
+timeout -k 10 840 python -u scripts/tune_conv.py --batches 128 --out "$OUT/tuned.json" > "$OUT/tune.log" 2>&1 || { echo tune failed; tail -5 "$OUT/tune.log"; exit 1; }
+tail -2 "$OUT/tune.log"
+timeout -k 10 300 python bench.py --steps 30 --warmup 5 --global-batch 128 > "$OUT/bench128_old.log" 2>&1 || exit 1
+cp "$OUT/tuned.json" faster_distributed_training_amd/ops/conv_tuned.json
+timeout -k 10 300 python bench.py --steps 30 --warmup 5 --global-batch 128 > "$OUT/bench128_new.log" 2>&1 || exit 1
+timeout -k 10 300 python bench.py --steps 20 --warmup 5 > "$OUT/bench1024_new.log" 2>&1 || exit 1
+grep -h '"value"' "$OUT"/bench*.log | python3 -c "import sys,json; [print(json.loads(l)['config']['global_batch'], json.loads(l)['ms_per_step']) for l in sys.stdin]"
