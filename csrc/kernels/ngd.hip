@@ -580,7 +580,12 @@ __global__ __launch_bounds__(256) void ngd_proj_h_kernel(ProjArgs p) {
   }
 }
 
-template <bool VEC>
+// STR (strided axis, B > 1): a thread owns one row and 8 consecutive d (lanes = rows =
+// consecutive b), so Y goes out as coalesced stores straight from registers and each H
+// float4 feeds 32 FMAs (W reads are wave-uniform broadcasts); the [4 rows x 2 d] mapping
+// needed an LDS round trip and two extra barriers per chunk for the strided store and sat
+// at ~0.63 of its wave cycles waiting (profiles/pmc/ngd_proj_counters.md).
+template <bool VEC, bool STR>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void ngd_proj_y_kernel(ProjArgs p) {
   __shared__ __attribute__((aligned(16))) float Xs[kPN * kXs];
   __shared__ __attribute__((aligned(16))) float Ws[kPD * kWd];
@@ -642,6 +647,28 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void n
       proj_load_w<VEC>(wv12, w, R, D, dend, d0 + kPD, tid);
     }
     float yv[4][2];
+    float ys[8];
+    if (STR) {
+      const int row = tid & 63, dq = tid >> 6;
+      const float4 a0 = *reinterpret_cast<const float4*>(Xs + row * kXs + 8 * dq);
+      const float4 a1 = *reinterpret_cast<const float4*>(Xs + row * kXs + 8 * dq + 4);
+      ys[0] = a0.x; ys[1] = a0.y; ys[2] = a0.z; ys[3] = a0.w;
+      ys[4] = a1.x; ys[5] = a1.y; ys[6] = a1.z; ys[7] = a1.w;
+#pragma unroll 2
+      for (int r0 = 0; r0 < R; r0 += 4) {
+        const float4 hv = *reinterpret_cast<const float4*>(Hs + row * kWd + r0);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          const float4 wk = *reinterpret_cast<const float4*>(Ws + (8 * dq + k) * kWd + r0);
+          float v = ys[k];
+          v = fmaf(-hv.x, wk.x, v);
+          v = fmaf(-hv.y, wk.y, v);
+          v = fmaf(-hv.z, wk.z, v);
+          v = fmaf(-hv.w, wk.w, v);
+          ys[k] = v;
+        }
+      }
+    } else {
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -665,6 +692,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void n
           yv[i][k] = v;
         }
     }
+    }
     if (p.Jp != nullptr) {  // J[r][d] += sum_n H[n][r] X[n][d]: thread d = tid & 31, r = (tid >> 5) + 8 j
       const int dd = tid & 31, d = d0 + dd;
       float ja[10];
@@ -684,7 +712,23 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void n
         }
       }
     }
-    if (VEC) {  // rows contiguous in d: store Y from registers (16 lanes = 64 contiguous bytes)
+    if (STR) {  // lanes = consecutive rows (b): one coalesced store per d
+      const int row = tid & 63, dq = tid >> 6;
+      const long n = n0 + row;
+      if (n < N) {
+        const long a = n / p.B, b = n - a * p.B;
+        float* yr = y + a * (long)D * p.B + b;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          const int d = d0 + 8 * dq + k;
+          if (d < dend) {
+            yr[(long)d * p.B] = ys[k];
+            sy = fmaf(ys[k], ys[k], sy);
+          }
+        }
+      }
+      __syncthreads();  // Xs / Ws reads done before the next chunk is staged
+    } else if (VEC) {  // rows contiguous in d: store Y from registers (16 lanes = 64 contiguous bytes)
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const long n = n0 + 4 * tr + i;
@@ -826,8 +870,9 @@ void ngd_proj(uint64_t X, uint64_t Y, uint64_t W, uint64_t Hbuf, int G, int A, i
     FDT_LAUNCH_CHECK();
     p.H = sc + L.h;
   }
-  if (vec) ngd_proj_y_kernel<true><<<(unsigned)grid, 256, 0, st>>>(p);
-  else ngd_proj_y_kernel<false><<<(unsigned)grid, 256, 0, st>>>(p);
+  if (vec) ngd_proj_y_kernel<true, false><<<(unsigned)grid, 256, 0, st>>>(p);
+  else if (B > 1) ngd_proj_y_kernel<false, true><<<(unsigned)grid, 256, 0, st>>>(p);
+  else ngd_proj_y_kernel<false, false><<<(unsigned)grid, 256, 0, st>>>(p);
   FDT_LAUNCH_CHECK();
   const int nwg = p.tiles * p.ds;
   ngd_proj_sums_kernel<<<ip ? 2 * G : G, 256, 0, st>>>(p.fpp, P<float>(fp), p.ipp, P<float>(ip), G, nwg);
