@@ -227,7 +227,10 @@ class TransformerTrainer:
     # launches each bucket's all-reduce between segments; the sharded optimizer (ZeRO-2 NGD)
     # communicates after the replay.  bf16 only; not with FSDP (collectives inside forward).
     def _graphs_on(self):
-        return (TR_GRAPHS and self.device.type == "cuda" and self.fsdp is None
+        # (the --no-native ablation is plain eager PyTorch: no capture either -- captured, the
+        # torch-op transformer step faulted with an illegal address on replay, measured)
+        from ..ops import _native
+        return (TR_GRAPHS and self.device.type == "cuda" and self.fsdp is None and _native.enabled()
                 and not self.scaler.enabled and self.cfg.profile_steps <= 0 and not self.cfg.faithful
                 and self.model.training)
 
