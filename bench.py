@@ -141,10 +141,25 @@ def main():
         "epoch_time_s": round(50000.0 / value, 3),
         "peak_mem_gb": round(torch.cuda.max_memory_allocated() / 2**30, 2) if cuda else None,
     }
+    _sharding_fields(tr, rec)
     if tr.rank == 0:
         print(json.dumps(rec), flush=True)
     if dist.is_initialized():
         dist.destroy_process_group()
+
+
+def _sharding_fields(tr, rec):
+    """Record which data-parallel path actually ran (FSDP units / ZeRO-2 / bucket reducer)."""
+    cfg = rec["config"]
+    if tr.fsdp is not None:
+        cfg["fsdp_units"] = len(tr.fsdp.units)
+        cfg["fsdp_peak_full_bytes"] = int(tr.fsdp.peak_full_bytes)
+        cfg["fsdp_shard_numel"] = int(tr.fsdp.space.numel)
+        cfg["fsdp_graphs"] = bool(getattr(tr.fsdp, "graphs", False))
+    elif tr.zero is not None:
+        cfg["zero2_shard_numel"] = int(tr.zero.view.numel)
+    elif tr.reducer is not None:
+        cfg["ddp_buckets"] = len(tr.reducer.buckets)
 
 
 def bench_transformer(args):
@@ -201,6 +216,7 @@ def bench_transformer(args):
                       "truncation": "none (pad to the smallest bucket >= the batch's longest sample)",
                       "parallelism": f"{'fsdp' if args.fsdp else 'dp'}{world}", "optimizer": "ngd"},
            "peak_mem_gb": round(torch.cuda.max_memory_allocated() / 2**30, 2) if cuda else None}
+    _sharding_fields(tr, rec)
     if tr.rank == 0:
         print(json.dumps(rec), flush=True)
     if dist.is_initialized():

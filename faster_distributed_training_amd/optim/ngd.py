@@ -418,10 +418,19 @@ class NGState:
         return {"t": self.t, "W": self.W, "d": self.d, "rho": self.rho}
 
     def load_state_dict(self, sd):
-        self.t = int(sd["t"])
         def mv(v):
             return v.to(self.device) if isinstance(v, torch.Tensor) else v
-        self.W, self.d, self.rho = mv(sd["W"]), mv(sd["d"]), mv(sd["rho"])
+        W, d, rho = mv(sd["W"]), mv(sd["d"]), mv(sd["rho"])
+        if isinstance(W, torch.Tensor):
+            # the HIP kernels index W / d / rho by (G, rank, dim): a state saved for other
+            # parameters (e.g. another rank's ZeRO-2 shard) must not be loaded
+            want = {"W": (self.G, self.rank, self.dim), "d": (self.G, self.rank), "rho": (self.G,)}
+            for k, v in (("W", W), ("d", d), ("rho", rho)):
+                if not isinstance(v, torch.Tensor) or tuple(v.shape) != want[k]:
+                    got = tuple(v.shape) if isinstance(v, torch.Tensor) else type(v).__name__
+                    raise ValueError(f"NGD state {k}: shape {got}, expected {want[k]}")
+        self.t = int(sd["t"])
+        self.W, self.d, self.rho = W, d, rho
         if isinstance(self.W, torch.Tensor):  # own (contiguous) buffers: updated in place later
             self.W, self.d, self.rho = self.W.clone(), self.d.clone(), self.rho.clone()
 

@@ -82,13 +82,32 @@ def _set_rng_state(trainer, st):
         ld._cpu_gen.set_state(st["loader_cpu_gen"])
 
 
-def rank_path(path: str, rank: int) -> str:
+def rank_path(path: str, rank: int, epoch: int | None = None) -> str:
+    """Per-rank file of the save after ``epoch`` (epoch-tagged: a crash between the rank
+    files and the main file leaves the previous save's rank files intact)."""
     root, ext = os.path.splitext(path)
-    return f"{root}.rank{rank}{ext}"
+    tag = "" if epoch is None else f".e{int(epoch)}"
+    return f"{root}.rank{rank}{tag}{ext}"
 
 
 def _sharded(trainer) -> bool:
-    return getattr(trainer, "fsdp", None) is not None or bool(getattr(trainer.optimizer, "sharded", False))
+    """Optimizer state differs per rank: FSDP shards, ZeRO-2 sharded NGD (``trainer.zero``),
+    or any other sharder the trainer holds."""
+    return (getattr(trainer, "sharder", None) is not None or getattr(trainer, "fsdp", None) is not None
+            or getattr(trainer, "zero", None) is not None
+            or bool(getattr(getattr(trainer, "optimizer", None), "sharded", False)))
+
+
+def _drop_stale_rank_files(path: str, rank: int, keep_epoch: int):
+    root, ext = os.path.splitext(path)
+    d = os.path.dirname(os.path.abspath(path))
+    prefix = os.path.basename(f"{root}.rank{rank}.e")
+    for f in os.listdir(d):
+        if f.startswith(prefix) and f.endswith(ext) and f != os.path.basename(rank_path(path, rank, keep_epoch)):
+            try:
+                os.remove(os.path.join(d, f))
+            except OSError:
+                pass
 
 
 def _optimizer_state(trainer):
@@ -108,16 +127,19 @@ def _load_optimizer_state(trainer, ck):
 def save_last(trainer, epoch: int):
     """Full training state after ``epoch`` completed: every rank writes its rank file, rank 0
     the main file, then all ranks barrier."""
+    from ..parallel.dist import barrier
     rank, world = int(getattr(trainer, "rank", 0)), int(getattr(trainer, "world", 1))
-    mine = {"rng": _rng_state(trainer), "rank": rank, "world": world}
+    step = int(trainer.global_step)
+    mine = {"rng": _rng_state(trainer), "rank": rank, "world": world, "epoch": int(epoch), "global_step": step}
     sharded = _sharded(trainer)
     if sharded:
         mine.update(_optimizer_state(trainer))
-    path = rank_path(trainer.last_path, rank)
+    path = rank_path(trainer.last_path, rank, epoch)
     os.makedirs(os.path.dirname(os.path.abspath(path)) or ".", exist_ok=True)
     torch.save(mine, path + ".tmp")
     os.replace(path + ".tmp", path)
-    extra = {"global_step": int(trainer.global_step), "best_acc": float(trainer.best_acc), "world": world,
+    barrier()  # every rank file of this save exists before the main file names it
+    extra = {"global_step": step, "best_acc": float(trainer.best_acc), "world": world,
              "sharded_optimizer": sharded, "last": True}
     if not sharded:
         extra.update(_optimizer_state(trainer))
@@ -130,6 +152,7 @@ def save_last(trainer, epoch: int):
         extra["meta"] = {k: v.detach().cpu() for k, v in meta.state_dict().items()}
     acc = trainer.testing_acc[-1] if getattr(trainer, "testing_acc", None) else 0.0
     ckpt.save_checkpoint(trainer.last_path, trainer.model, acc, epoch, module_prefix=False, extra=extra)
+    _drop_stale_rank_files(trainer.last_path, rank, epoch)  # (after the main file's commit + barrier)
 
 
 def restore_last(trainer) -> bool:
@@ -143,8 +166,12 @@ def restore_last(trainer) -> bool:
     if int(ck.get("world", world)) != world:
         raise RuntimeError(f"{path} was written by {ck['world']} ranks; resume with the same world size "
                            f"(this run has {world})")
-    rp = rank_path(path, rank)
+    rp = rank_path(path, rank, int(ck["epoch"]))
     mine = ckpt.load_checkpoint(rp) if os.path.isfile(rp) else None
+    if mine is not None and (int(mine.get("epoch", -1)) != int(ck["epoch"])
+                             or int(mine.get("global_step", -1)) != int(ck.get("global_step", 0))):
+        raise RuntimeError(f"{rp} (epoch {mine.get('epoch')}, step {mine.get('global_step')}) does not belong to "
+                           f"{path} (epoch {ck['epoch']}, step {ck.get('global_step')})")
     if ck.get("sharded_optimizer", False) != _sharded(trainer):
         raise RuntimeError(f"{path}: optimizer sharding differs from this run's (--fsdp / sharded NGD)")
     ckpt.load_model_state(trainer.model, ck["net"])

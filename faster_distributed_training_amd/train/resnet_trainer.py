@@ -90,8 +90,9 @@ class ResNetTrainer:
     def __init__(self, cfg: ResNetConfig):
         self.cfg = cfg
         self.rank, self.world = 0, 1
-        if cfg.distributed or int(os.environ.get("WORLD_SIZE", "1")) > 1:
-            if not pdist.is_dist():
+        if cfg.distributed or cfg.fsdp or int(os.environ.get("WORLD_SIZE", "1")) > 1:
+            # (--fsdp always runs the sharded path, over a world-1 group on one GPU)
+            if not torch.distributed.is_initialized():
                 pdist.setup_norank()
             self.rank, self.world = pdist.rank(), pdist.world()
             cfg.distributed = self.world > 1
@@ -112,7 +113,7 @@ class ResNetTrainer:
         params_owner = self.model if not learnable else nn.ModuleList([self.model, self.meta])
         ngd_opt = cfg.optimizer == "ngd" or (cfg.optimizer == "auto" and cfg.ngd)
         self.reducer = self.fsdp = self.zero = None
-        if cfg.distributed and cfg.fsdp:
+        if cfg.fsdp:
             # ZeRO-3: parameters sharded at rest, gathered per stage (parallel/fsdp.py); NGD
             # needs whole parameters per rank ("param" shard mode, survey Q17)
             if learnable:

@@ -89,8 +89,9 @@ class TransformerTrainer:
     def __init__(self, cfg: TransformerConfig):
         self.cfg = cfg
         self.rank, self.world = 0, 1
-        if cfg.distributed or int(os.environ.get("WORLD_SIZE", "1")) > 1:
-            if not pdist.is_dist():
+        if cfg.distributed or cfg.fsdp or int(os.environ.get("WORLD_SIZE", "1")) > 1:
+            # (--fsdp always runs the sharded path, over a world-1 group on one GPU)
+            if not torch.distributed.is_initialized():
                 pdist.setup_norank()
             self.rank, self.world = pdist.rank(), pdist.world()
             cfg.distributed = self.world > 1
@@ -105,10 +106,10 @@ class TransformerTrainer:
         if cfg.resume:
             ckpt.load_model_state(self.model, ckpt.load_checkpoint(self.ckpt_path)["net"])
         shadow = (SHADOW and self.device.type == "cuda" and cfg.precision == "bf16"
-                  and not (cfg.distributed and cfg.fsdp))
+                  and not cfg.fsdp)
         ngd_opt = cfg.optimizer == "ngd" or (cfg.optimizer == "auto" and cfg.ngd)
         self.reducer = self.fsdp = self.zero = None
-        if cfg.distributed and cfg.fsdp:
+        if cfg.fsdp:
             # ZeRO-3 (parallel/fsdp.py): parameters sharded at rest, one wrap unit per
             # embedding / attention / FFN sublayer / head, gathered with prefetch and
             # reduce-scattered from gradient hooks; NGD sees whole parameters (Q17)

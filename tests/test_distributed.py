@@ -280,32 +280,58 @@ def test_eval_save_decision_is_collective(tmp_path):
     run_world(_eval_decision_worker, world=2, args=(str(tmp_path),))
 
 
-def _resume_rank_state_worker(rank, world, tmp):
-    """per-rank RNG streams and (FSDP) per-rank optimizer shards survive
-    save_last / auto-resume; rank 0's are not broadcast over the others."""
+def _resume_rank_state_worker(rank, world, tmp, mode):
+    """per-rank RNG streams and per-rank optimizer shards (FSDP, and ZeRO-2
+    sharded NGD: momentum over the rank's run + NGD axis states of its own parameters)
+    survive save_last / auto-resume; rank 0's are not broadcast over the others."""
     from faster_distributed_training_amd.train import resilience
     from faster_distributed_training_amd.train.resnet_trainer import ResNetConfig, ResNetTrainer
     os.chdir(tmp)
     base = dict(arch="resnet18", bs=4, synthetic=True, epoch=1, steps_per_epoch=2, eval=False, plot=False,
-                distributed=True, optimizer="madgrad", fsdp=True, checkpoint_dir=os.path.join(tmp, "ck"),
-                extra={"subset_stride": 100})
+                distributed=True, checkpoint_dir=os.path.join(tmp, "ck"), extra={"subset_stride": 100})
+    if mode == "fsdp":
+        base.update(optimizer="madgrad", fsdp=True)
+    else:
+        base.update(optimizer="ngd", ngd=True)
     a = ResNetTrainer(ResNetConfig(save_last=True, **base)).fit()
+    assert resilience._sharded(a)
     rng_after = torch.get_rng_state()
     opt_after = {k: v.clone() for k, v in a.optimizer.state_dict()["flat_state"].items() if torch.is_tensor(v)}
-    assert os.path.isfile(resilience.rank_path(a.last_path, rank))
+    ngd_after = a.optimizer.ngd_state_dict() if mode == "zero" else None
+    assert os.path.isfile(resilience.rank_path(a.last_path, rank, 0))
     torch.manual_seed(999)
     b = ResNetTrainer(ResNetConfig(auto_resume=True, **base))
     assert b.start_epoch == 1
     assert torch.equal(torch.get_rng_state(), rng_after)  # this rank's own stream
     opt_b = b.optimizer.state_dict()["flat_state"]
-    assert all(torch.equal(opt_b[k], v) for k, v in opt_after.items())
+    assert opt_after and all(torch.equal(opt_b[k], v) for k, v in opt_after.items())
+    if ngd_after is not None:
+        ngd_b = b.optimizer.ngd_state_dict()
+        assert len(ngd_b) == len(ngd_after) > 0
+        for ga, gb in zip(ngd_after, ngd_b):
+            for sa, sb in zip(ga, gb):
+                assert sa["t"] == sb["t"] and torch.equal(sa["W"].cpu(), sb["W"].cpu())
     states = [None] * world
     dist.all_gather_object(states, torch.get_rng_state())
     assert not torch.equal(states[0], states[1])
+    # a rank file from another save (the crash-between-writes case) is refused
+    if rank == 1:
+        import shutil
+        shutil.copy(resilience.rank_path(a.last_path, 0, 0), resilience.rank_path(a.last_path, 1, 0))
+        raw = torch.load(resilience.rank_path(a.last_path, 1, 0), weights_only=True)
+        raw["global_step"] = -5
+        torch.save(raw, resilience.rank_path(a.last_path, 1, 0))
+        try:
+            resilience.restore_last(b)
+        except RuntimeError as e:
+            assert "does not belong" in str(e)
+        else:
+            raise AssertionError("mismatched rank file accepted")
 
 
-def test_auto_resume_restores_each_ranks_state(tmp_path):
-    run_world(_resume_rank_state_worker, world=2, args=(str(tmp_path),))
+@pytest.mark.parametrize("mode", ["fsdp", "zero"])
+def test_auto_resume_restores_each_ranks_state(tmp_path, mode):
+    run_world(_resume_rank_state_worker, world=2, args=(str(tmp_path), mode))
 
 
 def _trainer_fsdp_vs_ddp_worker(rank, world, tmp, model):
