@@ -270,10 +270,17 @@ class FullyShardedDP:
             for p in model.parameters():
                 dist.broadcast(p.data, 0, group=self.pg)
         unit_list = list(units) if units is not None else default_units(model)
+        # a parameter used by several units (tied weights, overlapping user units) would be
+        # read by a later unit after its owner resharded it: such parameters go to the root
+        # unit, which stays gathered
+        seen = {}
+        for ui, (name, mod) in enumerate(unit_list):
+            for p in mod.parameters():
+                seen.setdefault(id(p), set()).add(ui)
         owner = {}
         for ui, (name, mod) in enumerate(unit_list):
             for pn, p in mod.named_parameters():
-                if p.requires_grad and id(p) not in owner:
+                if p.requires_grad and id(p) not in owner and len(seen[id(p)]) == 1:
                     owner[id(p)] = (ui, f"{name}.{pn}")
         root_params = [(n, p) for n, p in model.named_parameters() if p.requires_grad and id(p) not in owner]
         self.units = []

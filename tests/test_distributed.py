@@ -187,6 +187,49 @@ def test_fsdp_full_shard_matches_single_process(world, mode, offload):
     run_world(_fsdp_worker, world=world, args=(mode, offload))
 
 
+class _Tied(nn.Module):
+    def __init__(self, seed):
+        super().__init__()
+        torch.manual_seed(seed)
+        self.a, self.b, self.c, self.d = nn.Linear(10, 16), nn.Linear(16, 16), nn.Linear(16, 16), nn.Linear(16, 4)
+        self.c.weight = self.b.weight  # tied across two wrap units
+
+    def forward(self, x):
+        return self.d(torch.tanh(self.c(torch.tanh(self.b(torch.tanh(self.a(x)))))))
+
+
+def _fsdp_tied_worker(rank, world):
+    """a parameter shared by two wrap units lives in the always-gathered root
+    unit (the later unit would otherwise read it after its owner resharded it)."""
+    from faster_distributed_training_amd.optim.flat_optim import SGD
+    from faster_distributed_training_amd.parallel.fsdp import FullyShardedDP
+    m = _Tied(rank)
+    fs = FullyShardedDP(m, torch.device("cpu"), units=[(n, getattr(m, n)) for n in "abcd"], mode="flat")
+    root = [u for u in fs.units if u.root]
+    assert len(root) == 1 and any(p is m.b.weight for _, p in root[0].params)
+    assert all(p is not m.b.weight for u in fs.units if not u.root for _, p in u.params)
+    opt = SGD(fs.space, lr=0.1, momentum=0.9)
+    ref = _Tied(0)
+    ropt = torch.optim.SGD(ref.parameters(), lr=0.1, momentum=0.9)
+    for step in range(3):
+        x, y = _batch(rank + 10 * step)
+        F.cross_entropy(m(x), y).backward()
+        fs.finish_backward()
+        opt.step()
+        fs.after_step()
+        ropt.zero_grad()
+        (sum(F.cross_entropy(ref(_batch(r + 10 * step)[0]), _batch(r + 10 * step)[1])
+             for r in range(world)) / world).backward()
+        ropt.step()
+    sd = fs.full_state_dict()
+    for k, v in ref.state_dict().items():
+        assert torch.allclose(sd[k], v, atol=1e-5), (k, (sd[k] - v).abs().max())
+
+
+def test_fsdp_tied_parameter_goes_to_root():
+    run_world(_fsdp_tied_worker, world=2)
+
+
 def _fsdp_ngd_worker(rank, world):
     """FSDP + NGD (the reference's distributed transformer run, transformer_test.py:216-217,
     387-392): with whole-parameter shards NGD preconditions correctly shaped parameters (Q17)
