@@ -40,10 +40,25 @@ def load():
         spec = importlib.util.spec_from_file_location("_fdt_native", path)
         m = importlib.util.module_from_spec(spec)
         spec.loader.exec_module(m)
-        _mod = m
     except Exception as e:  # pragma: no cover - depends on build state
         _err = f"failed to load {path}: {e}"
+        return None
+    # provenance: the binary must have been built from the csrc/ next to it
+    from ._provenance import source_hash
+    want = source_hash()
+    got = m.source_hash() if hasattr(m, "source_hash") else None
+    if want is not None and got != want and os.environ.get("FDT_ALLOW_STALE_NATIVE", "0") != "1":
+        _err = (f"{path} is stale: built from sources with hash {got}, the tree has {want} "
+                f"(run `python build_native.py`)")
+        return None
+    _mod = m
     return _mod
+
+
+def built_from() -> str | None:
+    """Hash of the sources the loaded extension was built from (None if not loaded)."""
+    m = load()
+    return m.source_hash() if m is not None else None
 
 
 def enabled() -> bool:
