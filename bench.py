@@ -41,6 +41,8 @@ def parse():
     ap.add_argument("--ngd", action="store_true")
     ap.add_argument("--meta_learning", action="store_true")
     ap.add_argument("--fsdp", action="store_true")
+    ap.add_argument("--sharded-ngd", action="store_true",
+                    help="with --ngd at N=1: run the sharded-NGD data-parallel path over a world-1 group")
     ap.add_argument("--precision", default="bf16")
     ap.add_argument("--bucket-mb", type=float, default=8.0)
     ap.add_argument("--comm-dtype", default="fp32")
@@ -78,7 +80,7 @@ def main():
                        optimizer="ngd" if args.ngd else args.optimizer, fsdp=args.fsdp,
                        precision=args.precision, bucket_mb=args.bucket_mb, comm_dtype=args.comm_dtype,
                        fast_path=False if args.no_native else None, graphs=not args.no_graphs,
-                       deterministic=args.deterministic)
+                       deterministic=args.deterministic, force_sharded=args.sharded_ngd)
     tr = ResNetTrainer(cfg)
     dev = tr.device
     cuda = dev.type == "cuda"
@@ -157,7 +159,9 @@ def _sharding_fields(tr, rec):
         cfg["fsdp_shard_numel"] = int(tr.fsdp.space.numel)
         cfg["fsdp_graphs"] = bool(getattr(tr.fsdp, "graphs", False))
     elif tr.zero is not None:
-        cfg["zero2_shard_numel"] = int(tr.zero.view.numel)
+        cfg["optimizer_sharding"] = "ngd-owner-shards (bucketed all-reduce overlapped with backward + all-gather)"
+        cfg["owner_shard_numel"] = int(tr.zero.view.numel)
+        cfg["ddp_buckets"] = len(tr.zero.buckets)
     elif tr.reducer is not None:
         cfg["ddp_buckets"] = len(tr.reducer.buckets)
 

@@ -76,6 +76,7 @@ class ResNetConfig:
     nonfinite_guard: bool = True       # skip (on device) optimizer steps whose gradients are not finite
     profile_steps: int = 0             # per-phase device timing (+ roctx ranges) of the first K steps
     deterministic: bool = False        # bitwise-repeatable engine steps (ops/_native.set_deterministic)
+    force_sharded: bool = False        # sharded-NGD path even at world size 1 (bench / tests)
     extra: dict = field(default_factory=dict)
 
 
@@ -90,7 +91,7 @@ class ResNetTrainer:
     def __init__(self, cfg: ResNetConfig):
         self.cfg = cfg
         self.rank, self.world = 0, 1
-        if cfg.distributed or cfg.fsdp or int(os.environ.get("WORLD_SIZE", "1")) > 1:
+        if cfg.distributed or cfg.fsdp or cfg.force_sharded or int(os.environ.get("WORLD_SIZE", "1")) > 1:
             # (--fsdp always runs the sharded path, over a world-1 group on one GPU)
             if not torch.distributed.is_initialized():
                 pdist.setup_norank()
@@ -127,12 +128,14 @@ class ResNetTrainer:
             if engine:
                 self.model._fsdp = self.fsdp
             self.flat = self.fsdp.space
-        elif cfg.distributed and ngd_opt and cfg.shard_ngd:
+        elif (cfg.distributed or cfg.force_sharded) and ngd_opt and cfg.shard_ngd:
             # ZeRO-2 for NGD: each rank preconditions + updates only the parameters it owns
             # (parallel/zero.py) instead of every rank repeating the whole NGD step
             from ..parallel.zero import ShardedOptimizerDP
             self.flat = FlatParams(params_owner, device=self.device, partition=self.world, balance="ngd")
-            self.zero = ShardedOptimizerDP(self.flat, self.model)
+            cdt = {"fp32": None, "bf16": torch.bfloat16}[cfg.comm_dtype]
+            self.zero = ShardedOptimizerDP(self.flat, self.model, bucket_mb=cfg.bucket_mb,
+                                           first_bucket_mb=cfg.first_bucket_mb, comm_dtype=cdt)
         else:
             self.flat = FlatParams(params_owner, device=self.device)
             if cfg.distributed:

@@ -126,7 +126,7 @@ class TransformerTrainer:
             if part:
                 # ZeRO-2 for NGD: every rank preconditions only the parameters it owns
                 from ..parallel.zero import ShardedOptimizerDP
-                self.zero = ShardedOptimizerDP(self.flat, self.model)
+                self.zero = ShardedOptimizerDP(self.flat, self.model, bucket_mb=cfg.bucket_mb)
             elif cfg.distributed:
                 from ..parallel.ddp import BucketReducer
                 self.reducer = BucketReducer(self.flat, self.model, bucket_mb=cfg.bucket_mb)
@@ -225,8 +225,8 @@ class TransformerTrainer:
     # dropout hash (ops/attention_native.py DEVICE_SEED).  Gradients accumulate into the
     # flat gradient buffer (static; the optimizer zeroes it).  Under DDP the capture is cut
     # where a gradient bucket completes (parallel/graphs.SegmentedStep) and the replay
-    # launches each bucket's all-reduce between segments; the sharded optimizer (ZeRO-2 NGD)
-    # communicates after the replay.  bf16 only; not with FSDP (collectives inside forward).
+    # launches each bucket's all-reduce between segments (also under the sharded NGD
+    # optimizer, whose gradient all-reduce is the same bucket reducer).  bf16 only; not with FSDP (collectives inside forward).
     def _graphs_on(self):
         # (the --no-native ablation is plain eager PyTorch: no capture either -- captured, the
         # torch-op transformer step faulted with an illegal address on replay, measured)
@@ -291,7 +291,7 @@ class TransformerTrainer:
             AN.DEVICE_SEED = st["seed"]
             self.model.mix_override = (st["perm"], st["lam"])
             try:
-                if self.reducer is not None:
+                if self.reducer is not None or self.zero is not None:
                     # segments cut at bucket boundaries; all-reduces launched between them
                     step = SegmentedStep(self.device, self._graph_pool, stream=self._graph_stream)
                     loss, logits = step.capture(fwd)
