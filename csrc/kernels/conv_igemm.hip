@@ -4,15 +4,23 @@
 
 namespace fdt {
 
-// Python-facing launcher.  taps: list of (dh, dw, wt) triples encoded as int8 arrays.
-void conv_igemm(uint64_t x, uint64_t x2, uint64_t ps, uint64_t pt, uint64_t pg, uint64_t w, uint64_t out, uint64_t part,
-                int part_rows, uint64_t ex, uint64_t es, uint64_t et, uint64_t jmask, uint64_t jyb, uint64_t jout, long Nb, int Hi,
-                int Wi, int Cx, int Ho, int Wo, int S,
-                const std::vector<int>& dh, const std::vector<int>& dw, const std::vector<int>& wt, int Cout, int ldw,
-                int Hout, int Wout, int OS, int oy, int ox, int pro, int pro_act, float pro_alpha, int epi, int epi_act,
-                float epi_alpha, int BM, int BN, int BK, int nsplit, uint64_t slab, uint64_t cnt, uint64_t stream) {
+// Python-facing launchers.  taps: list of (dh, dw, wt) triples encoded as int8 arrays.
+static void conv_igemm_impl(uint64_t x, uint64_t x2, uint64_t ps, uint64_t pt, uint64_t pg, uint64_t w, uint64_t out,
+                            uint64_t part, int part_rows, uint64_t ex, uint64_t es, uint64_t et, uint64_t jmask,
+                            uint64_t jyb, uint64_t jout, long Nb, int Hi, int Wi, int Cx, int Ho, int Wo, int S,
+                            const std::vector<int>& dh, const std::vector<int>& dw, const std::vector<int>& wt, int Cout,
+                            int ldw, int Hout, int Wout, int OS, int oy, int ox, int pro, int pro_act, float pro_alpha,
+                            int epi, int epi_act, float epi_alpha, int BM, int BN, int BK, int nsplit, uint64_t slab,
+                            uint64_t cnt, uint64_t pt2, uint64_t pout, uint64_t pmask, uint64_t stream) {
   using namespace conv;
   ConvArgs a{};
+  a.pt2 = P<const float>(pt2);
+  a.pout = P<bf16>(pout);
+  a.pmask = P<uint8_t>(pmask);
+  if (pro == kProJoin) {
+    FDT_CHECK(x2 != 0 && pout != 0 && ps != 0 && pt != 0 && (pg == 0 || pt2 != 0), "join prologue: y, r, s, t, out");
+    FDT_CHECK(dh.size() == 1 && S == 1 && Hi == Ho && Wi == Wo, "join prologue: 1x1 stride-1 convolution only");
+  }
   a.x = P<const bf16>(x);
   a.x2 = P<const bf16>(x2);
   a.ps = P<const float>(ps);
@@ -71,11 +79,35 @@ void conv_igemm(uint64_t x, uint64_t x2, uint64_t ps, uint64_t pt, uint64_t pg, 
   const bool pure = a.ntaps == 1 && dh[0] == 0 && dw[0] == 0 && wt[0] == 0 && S == 1 && Hi == Ho && Wi == Wo;
   hipStream_t st = as_stream(stream);
   if (a.M == 0) return;
-  const int act = pro == kProAffineAct ? pro_act : ((epi == kEpiActBwd || epi == kEpiJoinBwd) ? epi_act : 0);
+  const int act = (pro == kProAffineAct || pro == kProJoin) ? pro_act : ((epi == kEpiActBwd || epi == kEpiJoinBwd) ? epi_act : 0);
   if (launch_cases_fwd(pro, epi, act, a, BM, BN, BK, pure, st) || launch_cases_fold(pro, epi, act, a, BM, BN, BK, pure, st) ||
       launch_cases_join(pro, epi, act, a, BM, BN, BK, pure, st) || launch_cases_plain(pro, epi, act, a, BM, BN, BK, pure, st))
     return;
   FDT_CHECK(false, "unsupported (prologue, epilogue) combination");
+}
+
+void conv_igemm(uint64_t x, uint64_t x2, uint64_t ps, uint64_t pt, uint64_t pg, uint64_t w, uint64_t out, uint64_t part,
+                int part_rows, uint64_t ex, uint64_t es, uint64_t et, uint64_t jmask, uint64_t jyb, uint64_t jout, long Nb, int Hi,
+                int Wi, int Cx, int Ho, int Wo, int S,
+                const std::vector<int>& dh, const std::vector<int>& dw, const std::vector<int>& wt, int Cout, int ldw,
+                int Hout, int Wout, int OS, int oy, int ox, int pro, int pro_act, float pro_alpha, int epi, int epi_act,
+                float epi_alpha, int BM, int BN, int BK, int nsplit, uint64_t slab, uint64_t cnt, uint64_t stream) {
+  FDT_CHECK(pro != conv::kProJoin, "the join prologue goes through conv_igemm_join");
+  conv_igemm_impl(x, x2, ps, pt, pg, w, out, part, part_rows, ex, es, et, jmask, jyb, jout, Nb, Hi, Wi, Cx, Ho, Wo, S, dh,
+                  dw, wt, Cout, ldw, Hout, Wout, OS, oy, ox, pro, pro_act, pro_alpha, epi, epi_act, epi_alpha, BM, BN, BK,
+                  nsplit, slab, cnt, 0, 0, 0, stream);
+}
+
+// Forward 1x1 convolution whose operand is the previous residual block's join (PRO_JOIN):
+// y (its BN'd residual branch), r (shortcut: identity or BN'd by s2/t2), join output + ReLU
+// mask stored on the way.
+void conv_igemm_join(uint64_t y, uint64_t r, uint64_t s, uint64_t t, uint64_t s2, uint64_t t2, uint64_t w, uint64_t out,
+                     uint64_t part, int part_rows, uint64_t jout, uint64_t jmask, long Nb, int H, int W, int Cx, int Cout,
+                     int ldw, int BM, int BN, int BK, int nsplit, uint64_t slab, uint64_t cnt, uint64_t stream) {
+  const std::vector<int> z{0};
+  conv_igemm_impl(y, r, s, t, s2, w, out, part, part_rows, 0, 0, 0, 0, 0, 0, Nb, H, W, Cx, H, W, 1, z, z, z, Cout, ldw, H,
+                  W, 1, 0, 0, conv::kProJoin, kActRelu, 1.f, conv::kEpiStats, 0, 1.f, BM, BN, BK, nsplit, slab, cnt, t2,
+                  jout, jmask, stream);
 }
 
 int conv_num_row_blocks(long M, int BM) { return (int)((M + BM - 1) / BM); }

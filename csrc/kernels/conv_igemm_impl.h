@@ -21,6 +21,13 @@
 //      PRO_AFFINE_ACT  x -> act(x*s[c] + t[c])   (the producer's lazy batch-norm)
 //      PRO_FOLD        g -> g*gs[c] + alpha[c] + beta[c]*y  (batch-norm backward correction;
 //                      gs lets the residual join store one un-scaled gradient for both branches)
+//      PRO_JOIN        (y, r) -> relu(y*s[c] + t[c] + r*s2[c] + t2[c])  -- the previous residual
+//                      block's join (its BN'd residual branch + BN'd / identity shortcut), computed
+//                      while staging the first 1x1 conv of the next block; the workgroups of the
+//                      first output-channel tile also store the joined rows (the block output the
+//                      identity shortcut and the backward need) and their ReLU bit mask, so the
+//                      standalone join pass (read y, r; write out) and this conv's re-read of
+//                      `out` become one pass
 //    zero padding is applied AFTER the transform (the conv pads the normalised input);
 //  * epilogue:
 //      EPI_STATS   y (bf16) + per-block per-channel (sum y, sum y^2) slabs -> BN stats
@@ -61,15 +68,19 @@ namespace conv {
 typedef short bf16x8_t __attribute__((ext_vector_type(8)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
-enum Pro : int { kProNone = 0, kProAffineAct = 1, kProFold = 2 };
+enum Pro : int { kProNone = 0, kProAffineAct = 1, kProFold = 2, kProJoin = 3 };
 enum Epi : int { kEpiStats = 0, kEpiActBwd = 1, kEpiStore = 2, kEpiAdd = 3, kEpiJoinBwd = 4 };
 
 struct ConvArgs {
   const bf16* x;     // activation operand [Nb][Hi][Wi][Cx]   (PRO_FOLD: the gradient G)
-  const bf16* x2;    // PRO_FOLD: the producer output Y (same shape as x)
+  const bf16* x2;    // PRO_FOLD: the producer output Y (same shape as x); PRO_JOIN: the shortcut operand r
   const float* ps;   // prologue per-channel scale: s (AFFINE_ACT) or alpha (FOLD)   [Cx]
   const float* pt;   // prologue per-channel shift: t (AFFINE_ACT) or beta  (FOLD)   [Cx]
   const float* pg;   // FOLD: per-channel scale of g (nullptr = 1): g*pg + alpha + beta*y    [Cx]
+                     // JOIN: shortcut scale s2 (nullptr: identity shortcut, r used as is)
+  const float* pt2;  // JOIN: shortcut shift t2 [Cx]
+  bf16* pout;        // JOIN: the joined block output [M][Cx] (stored by the n0 == 0 workgroups)
+  uint8_t* pmask;    // JOIN: its ReLU bit mask (bit i of byte e/8 = out[e] > 0), or nullptr
   const bf16* w;     // packed weights [Cout][ldw], k-index = wt[tap]*Cx + ci
   bf16* out;         // [Nb][Hout][Wout][Cout]
   float* part;       // statistics slots [rows][NQ][Cout], fp32 atomics (zeroed by the consumer)
@@ -174,7 +185,7 @@ constexpr uint32_t kOOB = 0xFFFFFFF0u;  // byte offset past any buffer: the load
 template <int BM, int BN, int BK, int PRO, bool PURE>
 constexpr int kMinWavesPerEU =
     (BM == 128 && BN == 128 && BK == 32 && (PRO == kProNone || (PRO == kProAffineAct && PURE))) ? 4
-    : (BM == 128 && BN == 128 && (BK == 32 || PRO != 2)) ? 3 : 1;
+    : (BM == 128 && BN == 128 && (BK == 32 || (PRO != 2 && PRO != 3))) ? 3 : 1;
 
 template <int BM, int BN, int BK, int PRO, int EPI, bool PURE, int ACT>
 __global__ __launch_bounds__(256, (kMinWavesPerEU<BM, BN, BK, PRO, PURE>)) void igemm_kernel(const ConvArgs a) {
@@ -188,8 +199,10 @@ __global__ __launch_bounds__(256, (kMinWavesPerEU<BM, BN, BK, PRO, PURE>)) void 
 
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int nkt = (a.K + BK - 1) / BK;
-  constexpr bool HASPRO = PRO == kProAffineAct || PRO == kProFold;
-  constexpr int NPRM = PRO == kProFold ? 3 : (HASPRO ? 2 : 0);
+  constexpr bool HASPRO = PRO == kProAffineAct || PRO == kProFold || PRO == kProJoin;
+  constexpr bool TWOX = PRO == kProFold || PRO == kProJoin;  // two activation operands
+  constexpr int NPRM = PRO == kProJoin ? 4 : (PRO == kProFold ? 3 : (HASPRO ? 2 : 0));
+  static_assert(PRO != kProJoin || PURE, "the join prologue is for 1x1 stride-1 convolutions");
   constexpr int NQ = EPI == kEpiJoinBwd ? 3 : 2;                       // statistics rows
   // LDS: [prologue params | per-wave statistics | tap tables | K tiles, reused as the
   // epilogue's staging area] (the header size must match lds_bytes() on the host)
@@ -216,7 +229,7 @@ __global__ __launch_bounds__(256, (kMinWavesPerEU<BM, BN, BK, PRO, PURE>)) void 
   const __amdgpu_buffer_rsrc_t rx_d = __builtin_amdgcn_make_buffer_rsrc(
       (void*)a.x, (short)0, (int)(a.Nb_HiWi_Cx_bytes), 0x00020000);
   const __amdgpu_buffer_rsrc_t ry_d = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)(PRO == kProFold ? a.x2 : a.x), (short)0, (int)(a.Nb_HiWi_Cx_bytes), 0x00020000);
+      (void*)(TWOX ? a.x2 : a.x), (short)0, (int)(a.Nb_HiWi_Cx_bytes), 0x00020000);
   const __amdgpu_buffer_rsrc_t rw_d = __builtin_amdgcn_make_buffer_rsrc(
       (void*)a.w, (short)0, (int)(a.w_bytes), 0x00020000);
 
@@ -247,7 +260,7 @@ __global__ __launch_bounds__(256, (kMinWavesPerEU<BM, BN, BK, PRO, PURE>)) void 
   // of the previous tile).  Two stages alternate so that the loads of tile k+2 are in
   // flight during the MFMAs of tiles k and k+1.
   struct Stage {
-    uint4 rx[NXL], rx2[PRO == kProFold ? NXL : 1], rw[NWL];
+    uint4 rx[NXL], rx2[TWOX ? NXL : 1], rw[NWL];
     bool xv[NXL];
     int kci;
   };
@@ -279,7 +292,7 @@ __global__ __launch_bounds__(256, (kMinWavesPerEU<BM, BN, BK, PRO, PURE>)) void 
       S.xv[j] = v;
       const uint32_t off = v ? (((uint32_t)(pixb[j] + toff) << a.log2Cx) + ci) * 2u : kOOB;
       S.rx[j] = ld_buf16(rx_d, off);
-      if constexpr (PRO == kProFold) S.rx2[j] = ld_buf16(ry_d, off);
+      if constexpr (TWOX) S.rx2[j] = ld_buf16(ry_d, off);
     }
     const uint32_t wk = (uint32_t)((PURE ? 0 : wt) * a.Cx + ci);
 #pragma unroll
@@ -324,6 +337,35 @@ __global__ __launch_bounds__(256, (kMinWavesPerEU<BM, BN, BK, PRO, PURE>)) void 
         for (int q = 0; q < 8; ++q) v[q] = actf<ACT>(fmaf(v[q], sv[q], tv[q]), a.pro_alpha, inv_alpha);
         o = make_uint4(pk_bf16(v[0], v[1]), pk_bf16(v[2], v[3]), pk_bf16(v[4], v[5]), pk_bf16(v[6], v[7]));
         if (!S.xv[j]) o = make_uint4(0, 0, 0, 0);
+      } else if constexpr (PRO == kProJoin) {
+        // relu(y*s + t + r*s2 + t2): the previous block's output, rounded to bf16 exactly as
+        // the standalone join stores it; the first column tile also materialises it
+        float v[8], r[8];
+        const uint32_t u[4] = {o.x, o.y, o.z, o.w};
+        const uint32_t ur[4] = {S.rx2[j].x, S.rx2[j].y, S.rx2[j].z, S.rx2[j].w};
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          v[2 * q] = bf16_lo(u[q]); v[2 * q + 1] = bf16_hi(u[q]);
+          r[2 * q] = bf16_lo(ur[q]); r[2 * q + 1] = bf16_hi(ur[q]);
+        }
+        const float4* s2p = reinterpret_cast<const float4*>(pst + 2 * a.Cx + S.kci);
+        const float4* t2p = reinterpret_cast<const float4*>(pst + 3 * a.Cx + S.kci);
+        const float4 a0 = s2p[0], a1 = s2p[1], b0 = t2p[0], b1 = t2p[1];
+        const float s2v[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
+        const float t2v[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
+        uint32_t mk = 0;
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+          v[q] = actf<ACT>(fmaf(v[q], sv[q], tv[q]) + fmaf(r[q], s2v[q], t2v[q]), a.pro_alpha, inv_alpha);
+          mk |= (v[q] > 0.f ? 1u : 0u) << q;
+        }
+        o = make_uint4(pk_bf16(v[0], v[1]), pk_bf16(v[2], v[3]), pk_bf16(v[4], v[5]), pk_bf16(v[6], v[7]));
+        if (!S.xv[j]) o = make_uint4(0, 0, 0, 0);
+        if (n0 == 0 && S.xv[j]) {
+          const long e = ((long)pixb[j] << a.log2Cx) + S.kci;
+          *reinterpret_cast<uint4*>(a.pout + e) = o;
+          if (a.pmask) a.pmask[e >> 3] = (uint8_t)mk;
+        }
       } else if constexpr (PRO == kProFold) {
         // g + alpha + beta*y (padding: g = y = 0 from the bounds-checked load -> masked)
         float g[8], y[8];
@@ -399,6 +441,10 @@ __global__ __launch_bounds__(256, (kMinWavesPerEU<BM, BN, BK, PRO, PURE>)) void 
       pst[i] = a.ps[i];
       pst[a.Cx + i] = a.pt[i];
       if constexpr (PRO == kProFold) pst[2 * a.Cx + i] = a.pg ? a.pg[i] : 1.f;
+      if constexpr (PRO == kProJoin) {
+        pst[2 * a.Cx + i] = a.pg ? a.pg[i] : 1.f;
+        pst[3 * a.Cx + i] = a.pg ? a.pt2[i] : 0.f;
+      }
     }
   }
   if (tid < 12) {
@@ -670,8 +716,13 @@ static void launch_one(const ConvArgs& a, size_t lds, hipStream_t st) {
 
 template <int BM, int BN, int BK, int PRO, int EPI, int ACT>
 static void launch_pure(const ConvArgs& a, bool pure, size_t lds, hipStream_t st) {
-  if (pure) launch_one<BM, BN, BK, PRO, EPI, true, ACT>(a, lds, st);
-  else launch_one<BM, BN, BK, PRO, EPI, false, ACT>(a, lds, st);
+  if constexpr (PRO == kProJoin) {
+    FDT_CHECK(pure, "the join prologue needs a 1x1 stride-1 convolution");
+    launch_one<BM, BN, BK, PRO, EPI, true, ACT>(a, lds, st);
+  } else {
+    if (pure) launch_one<BM, BN, BK, PRO, EPI, true, ACT>(a, lds, st);
+    else launch_one<BM, BN, BK, PRO, EPI, false, ACT>(a, lds, st);
+  }
 }
 
 template <int PRO, int EPI, int ACT>
@@ -679,7 +730,7 @@ static void launch_tile(const ConvArgs& a, int BM, int BN, int BK, bool pure, hi
   const int nkt = (a.K + BK - 1) / BK;
   const size_t nbuf = nkt > 1 ? 2 : 1;
   // header (must match the kernel's hdr) + max(K tiles, epilogue staging [64][BN + 4] fp32)
-  const int nprm = PRO == kProFold ? 3 : ((PRO == kProAffineAct) ? 2 : 0);
+  const int nprm = PRO == kProJoin ? 4 : (PRO == kProFold ? 3 : ((PRO == kProAffineAct) ? 2 : 0));
   const size_t hdr = (((size_t)nprm * a.Cx + 4 * (EPI == kEpiJoinBwd ? 3 : 2) * BN + 24) * 4 + 15) & ~(size_t)15;
   const size_t tiles = nbuf * (BM + BN) * BK * 2, stage = (size_t)64 * (BN + 4) * 4;
   size_t lds = hdr + (tiles > stage ? tiles : stage);

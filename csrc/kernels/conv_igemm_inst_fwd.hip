@@ -11,6 +11,7 @@ bool launch_cases_fwd(int pro, int epi, int act, const ConvArgs& a, int BM, int 
   FDT_CONV_CASE(kProAffineAct, kEpiStats, kActRelu)
   FDT_CONV_CASE(kProAffineAct, kEpiStats, kActCelu)
   FDT_CONV_CASE(kProAffineAct, kEpiStats, kActNone)
+  FDT_CONV_CASE(kProJoin, kEpiStats, kActRelu)
 #undef FDT_CONV_CASE
   return false;
 }

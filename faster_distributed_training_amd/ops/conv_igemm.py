@@ -23,7 +23,7 @@ import torch
 
 from . import _native
 
-PRO_NONE, PRO_AFFINE_ACT, PRO_FOLD = 0, 1, 2
+PRO_NONE, PRO_AFFINE_ACT, PRO_FOLD, PRO_JOIN = 0, 1, 2, 3
 EPI_STATS, EPI_ACTBWD, EPI_STORE, EPI_ADD, EPI_JOINBWD = 0, 1, 2, 3, 4
 
 
@@ -251,6 +251,42 @@ def conv_fwd(x, wf, shp: ConvShape, s=None, t=None, act=0, alpha=1.0, tile=None,
     if fin is not None:
         _finalize_standalone(nat, 1, part, 2, shp.cout, fin[0], fin[1])
     return y, part
+
+
+def conv_fwd_join(y, r, s, t, s2, t2, wf, shp: ConvShape, jout, jmask=None, tile=None, part=None, nsplit=None,
+                  fin=None):
+    """1x1 stride-1 forward conv of a residual block's joined output, computed on the fly:
+    the operand is a = relu(y*s + t + (r*s2 + t2 if s2 is not None else r)) -- the previous
+    block's join (BN'd residual branch y + BN'd or identity shortcut r).  ``jout`` receives
+    ``a`` (bf16, the block output the next join and the backward read) and ``jmask`` its
+    ReLU bit mask (None: not stored), written once by the first output-channel tile; the
+    standalone join kernel and this conv's re-read of ``a`` become one pass.  Returns
+    (conv output, statistics slots) like ``conv_fwd``."""
+    nat = _native.native()
+    N, H, W, C = y.shape
+    assert shp.k == 1 and shp.stride == 1 and shp.pad == 0 and C == shp.cin == shp.cxp
+    for tt in (y, r, jout):
+        assert tt.dtype == torch.bfloat16 and tt.is_contiguous() and tuple(tt.shape) == (N, H, W, C)
+    assert (s2 is None) == (t2 is None)
+    assert jmask is None or (jmask.dtype == torch.uint8 and jmask.numel() * 8 >= y.numel())
+    M = N * H * W
+    ent = None
+    if tile is None:
+        ent = tuned("fwd3", N, H, shp) or tuned("fwd0", N, H, shp) or tuned("fwd", N, H, shp)
+        tile = tuple(ent["tile"]) if ent else None
+    bm, bn, bk = _tile3(tile, M, shp.cout)
+    if nsplit is not None:
+        ent = {"nsplit": nsplit}
+    ns, slab_p, cnt_p = _splitk_args(ent, M, shp.cout, C, bm, bn, bk, y.device)
+    out = torch.empty(N, H, W, shp.cout, device=y.device, dtype=torch.bfloat16)
+    if part is None:
+        part = stat_slots(2, shp.cout, y.device, M)
+    nat.conv_igemm_join(y.data_ptr(), r.data_ptr(), s.data_ptr(), t.data_ptr(), _p(s2), _p(t2), wf.data_ptr(),
+                        out.data_ptr(), part.data_ptr(), part.shape[0], jout.data_ptr(), _p(jmask), N, H, W, C,
+                        shp.cout, shp.ntaps * shp.cxp, bm, bn, bk, ns, slab_p, cnt_p, _sp())
+    if fin is not None:
+        _finalize_standalone(nat, 1, part, 2, shp.cout, fin[0], fin[1])
+    return out, part
 
 
 def conv_dgrad(g, y, al, be, wd, shp: ConvShape, x_shape, epi=EPI_STORE, out=None, ex=None, es=None, et=None,

@@ -40,6 +40,9 @@ from ..parallel import graphs as _graphs
 ACT_NONE, ACT_RELU, ACT_CELU = 0, 1, 2
 # materialise the normalised input / folded gradient of 3x3 convs once (see forward/backward)
 MATERIALIZE_3X3 = os.environ.get("FDT_MATERIALIZE_3X3", "1") != "0"
+# run a block's ReLU join inside the next block's first 1x1 conv (PRO_JOIN prologue) instead
+# of a standalone pass (see ResNetBodyFn.forward)
+JOIN_FOLD = os.environ.get("FDT_JOIN_FOLD", "1") != "0"
 MODE_FCBN, MODE_BN_TRAIN, MODE_BN_EVAL = 0, 1, 2
 BF16 = torch.bfloat16
 
@@ -277,6 +280,28 @@ def conv_bn_fwd(x, u: Unit, s, t, act, training, dev):
     return y, st, M
 
 
+def conv_bn_fwd_join(pj, u: Unit, training, dev):
+    """``conv_bn_fwd`` of a block's first (1x1) unit whose input is the PREVIOUS block's
+    join, computed in the conv's operand staging (ci.conv_fwd_join); the join output (this
+    block's x_in) and its ReLU mask are stored on the way.  pj = (y, s, t, r, s2, t2, out, mask)."""
+    y, s, t, r, s2, t2, out, mask = pj
+    M = y.numel() // y.shape[-1]
+    st, fin = _fin_args(u, M, training, dev)
+    yo, _ = ci.conv_fwd_join(y, r, s, t, s2, t2, u.wf, u.shp, out, mask, part=slots(2, u.shp.cout, dev, M), fin=fin)
+    return yo, st, M
+
+
+def _join_foldable(b_next) -> bool:
+    """Fold a join into the next block's first conv only where that conv has ONE output-channel
+    tile (Cout <= 64): each joined row is then produced once and the fused kernel streams at
+    HBM rate (ResNet-50 stage 1 at batch 1024: 365 us vs 137 us conv + 355 us join pass).
+    With several column tiles every tile re-reads both join operands and re-runs the join
+    arithmetic (measured 1.5-2x slower than conv + join pass at stages 2-4)."""
+    u = b_next.units[0]
+    return (JOIN_FOLD and u.shp.k == 1 and u.shp.stride == 1 and u.shp.pad == 0 and u.shp.cin == u.shp.cxp
+            and u.shp.cin >= 8 and u.shp.cout <= 64)
+
+
 def _fin_args(u: Unit, M, training, dev):
     """Outputs (s, t, save_mean, save_aux) and the finalisation arguments of one unit's
     statistics (eval-mode BN reads none of them but still re-zeroes the slots)."""
@@ -379,6 +404,7 @@ class ResNetBodyFn(torch.autograd.Function):
                            st.act_out[0], float(st.act_out[1]), 1, 1, _sp())
         stem_rec = (x_nhwc, y0, s0, t0, sm0, sa0)
         cur = "conv1"
+        pending = None  # previous block's join, run inside this block's first conv
         for bi, b in enumerate(plan.blocks):
             if fs is not None and plan.stage_of[bi] != cur:
                 plan.release_stage(cur, fwd=True)
@@ -389,9 +415,13 @@ class ResNetBodyFn(torch.autograd.Function):
             x_in = h
             ys = []
             raw, s, t, act = x_in, None, None, (ACT_NONE, 1.0)
-            for u in b.units:
+            for ui, u in enumerate(b.units):
                 a_in = None
-                if MATERIALIZE_3X3 and u.shp.k > 1 and s is not None:
+                if ui == 0 and pending is not None:
+                    # writes x_in (= the previous block's output) while staging it
+                    y, (su, tu, smu, sau), M = conv_bn_fwd_join(pending, u, training, dev)
+                    pending = None
+                elif MATERIALIZE_3X3 and u.shp.k > 1 and s is not None:
                     # 3x3: normalise + activate the input ONCE instead of in every one of the
                     # 9 im2col re-reads of the conv's operand staging
                     a_in = torch.empty_like(raw)
@@ -415,10 +445,16 @@ class ResNetBodyFn(torch.autograd.Function):
             mask = None
             if need_grad and b.join[0] == ACT_RELU:
                 mask = torch.empty(out.numel() // 8, device=dev, dtype=torch.uint8)
-            nat.residual_act_fwd(y3.data_ptr(), s3.data_ptr(), t3.data_ptr(), _p(sc[0] if sc else None),
-                                 _p(sc[1] if sc else None), _p(sc[2] if sc else None),
-                                 0 if sc else x_in.data_ptr(), out.data_ptr(), _p(mask), _rows(y3), C, b.join[0],
-                                 float(b.join[1]), 1, _sp())
+            nxt = plan.blocks[bi + 1] if bi + 1 < len(plan.blocks) else None
+            if nxt is not None and b.join[0] == ACT_RELU and _join_foldable(nxt):
+                # the next block's first 1x1 conv computes this join while staging its operand
+                # and stores `out` + mask (one pass instead of join pass + operand re-read)
+                pending = (y3, s3, t3, sc[0] if sc else x_in, sc[1] if sc else None, sc[2] if sc else None, out, mask)
+            else:
+                nat.residual_act_fwd(y3.data_ptr(), s3.data_ptr(), t3.data_ptr(), _p(sc[0] if sc else None),
+                                     _p(sc[1] if sc else None), _p(sc[2] if sc else None),
+                                     0 if sc else x_in.data_ptr(), out.data_ptr(), _p(mask), _rows(y3), C, b.join[0],
+                                     float(b.join[1]), 1, _sp())
             if need_grad:
                 recs.append((x_in, ys, sc, out, mask))
             h = out

@@ -6,15 +6,23 @@ Dispatches of the timing pass and of each counter pass are matched by
 dropped instead of shifting the alignment.  Columns (per step = totals / --steps):
 
   ms      kernel time (timing pass, no counters attached)
-  rdGB    2 x FETCH_SIZE  (gfx950 FETCH_SIZE counts half the bytes of a 16-B/lane stream,
-          MI355X_MICROARCH.md "HBM"); memory-side, Infinity-Cache hits included
-  wrGB    WRITE_SIZE
+  rdGB    FETCH_SIZE x the calibrated bytes per FETCH_SIZE byte of a 16-B/lane stream
+          (profiles/pmc/calibration.json, tools/pmc_calib.hip: 2.0 on gfx950 for coalesced
+          16-, 8- and 4-B/lane streams alike -- FETCH_SIZE tallies a 128-B request at 64 B); a
+          row whose traffic would then exceed the achievable 6.3 TB/s cannot be made of full
+          128-B requests and is reported at factor 1 instead (marked "n": 64-B requests,
+          tallied at their size -- the lower bound of its bytes); memory-side, Infinity-Cache
+          hits included
+  wrGB    WRITE_SIZE x its calibrated factor
   TB/s    (rdGB + wrGB) / ms
-  TF/s    SQ_VALU_MFMA_BUSY_CYCLES x 1024 FLOP (= 32 busy cycles per 32x32x16 bf16 MFMA of
-          32*32*16*2 FLOP) / ms
-  mfma%   MFMA busy cycles / (GRBM_GUI_ACTIVE/8 cycles x 1024 SIMDs)
+  TF/s    SQ_VALU_MFMA_BUSY_CYCLES x the calibrated FLOP per busy cycle (1024 for
+          32x32x16 bf16: 32 busy cycles per 32768-FLOP MFMA, measured by the MFMA loop) / ms
+  mfma%   MFMA busy cycles / (kernel time x 2.4 GHz x 1024 SIMDs): the fraction of the
+          peak-clock MFMA rate (GRBM_GUI_ACTIVE / 8 reads high on dispatches shorter than
+          ~0.3 ms, so it is not used as the cycle base)
   ldsc%   SQ_LDS_BANK_CONFLICT / SQ_LDS_IDX_ACTIVE
   roof%   max(bytes / 6.3 TB/s, FLOP / 2.5 PF) / measured time
+  GHz     GRBM_GUI_ACTIVE / 8 / kernel time, shown only for dispatches >= 0.3 ms
 
     python scripts/pmc_table.py gpurun_out/pmc_x_1024 --steps 4 [--out profiles/x.md]
 """
@@ -24,11 +32,27 @@ import argparse
 import collections
 import csv
 import glob
+import json
 import os
 import re
 
 HBM = 6.3e12
 MFMA = 2.5e15
+PEAK_GHZ = 2.4
+CALIB = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "profiles", "pmc",
+                     "calibration.json")
+
+
+def calibration():
+    """(read factor of full-line streams, read factor of 64-B requests, write factor, FLOP per
+    MFMA busy cycle)."""
+    f16, fn, fw, fl = 2.0, 1.0, 1.0, 1024.0
+    if os.path.exists(CALIB):
+        c = json.load(open(CALIB))
+        f16 = c.get("read16", {}).get("read_factor") or f16
+        fw = c.get("write16", {}).get("write_factor") or fw
+        fl = c.get("mfma", {}).get("flop_per_busy_cycle") or fl
+    return f16, fn, fw, fl
 
 
 def _short(name: str) -> str:
@@ -101,19 +125,26 @@ def main():
     S = a.steps
     rows = []
     tot_t = sum(g["t"] for g in agg.values()) / S
+    f16, fnar, fw, fpc = calibration()
     for (name, grid), g in agg.items():
         t = g["t"] / S
-        rd = 2 * g["FETCH_SIZE"] * 1024 / S
-        wr = g["WRITE_SIZE"] * 1024 / S
-        flop = g["SQ_VALU_MFMA_BUSY_CYCLES"] * 1024 / S
-        cyc = g["GRBM_GUI_ACTIVE"] / 8 / S
-        mf = g["SQ_VALU_MFMA_BUSY_CYCLES"] / S / (cyc * 1024) if cyc else 0.0
+        wr = fw * g["WRITE_SIZE"] * 1024 / S
+        rd = f16 * g["FETCH_SIZE"] * 1024 / S
+        narrow = t > 0 and (rd + wr) / t > HBM
+        if narrow:
+            rd = fnar * g["FETCH_SIZE"] * 1024 / S
+        flop = g["SQ_VALU_MFMA_BUSY_CYCLES"] * fpc / S
+        mf = g["SQ_VALU_MFMA_BUSY_CYCLES"] / S / (t * PEAK_GHZ * 1e9 * 1024) if t else 0.0
+        per_call = t / max(g["calls"] / S, 1e-9)
+        ghz = g["GRBM_GUI_ACTIVE"] / 8 / S / t * 1e-9 if (t and per_call >= 3e-4) else None
         ldsc = g["SQ_LDS_BANK_CONFLICT"] / g["SQ_LDS_IDX_ACTIVE"] if g["SQ_LDS_IDX_ACTIVE"] else 0.0
         roof = max((rd + wr) / HBM, flop / MFMA)
-        rows.append((t, name, grid, g["calls"] / S, rd, wr, flop, mf, ldsc, roof, cyc / t * 1e-9 if t and cyc else 0))
+        rows.append((t, name + (" n" if narrow else ""), grid, g["calls"] / S, rd, wr, flop, mf, ldsc, roof, ghz))
     rows.sort(reverse=True)
     lines = [f"# per-kernel roofline ({a.dir}, {S} steps)", "",
-             f"total kernel time {tot_t * 1e3:.3f} ms/step; rdGB = 2 x FETCH_SIZE; roof% = max(bytes/6.3TB/s, FLOP/2.5PF)/time",
+             f"total kernel time {tot_t * 1e3:.3f} ms/step; rdGB = FETCH_SIZE x {f16:.2f} (calibrated 16-B stream; "
+             f"'n' rows: x {fnar:.2f}, 64-B requests); TF/s = MFMA busy x {fpc:.0f}; mfma% at {PEAK_GHZ} GHz; "
+             "roof% = max(bytes/6.3TB/s, FLOP/2.5PF)/time",
              "",
              "| ms/step | calls | kernel | grid | rdGB | wrGB | TB/s | TF/s | mfma% | ldsc% | roof% | GHz |",
              "|---:|---:|---|---:|---:|---:|---:|---:|---:|---:|---:|---:|"]
@@ -123,7 +154,7 @@ def main():
     for t, name, grid, calls, rd, wr, flop, mf, ldsc, roof, ghz in rows[: a.top]:
         lines.append(f"| {t * 1e3:.3f} | {calls:.1f} | `{name}` | {grid} | {rd / 1e9:.3f} | {wr / 1e9:.3f} | "
                      f"{(rd + wr) / t / 1e12:.2f} | {flop / t / 1e12:.0f} | {mf * 100:.1f} | {ldsc * 100:.1f} | "
-                     f"{roof / t * 100:.0f} | {ghz:.2f} |")
+                     f"{roof / t * 100:.0f} | {'—' if ghz is None else f'{ghz:.2f}'} |")
     lines += ["", f"sum of per-kernel roofline bounds {sum_roof * 1e3:.3f} ms/step vs measured {tot_t * 1e3:.3f} ms/step "
               f"({sum_roof / tot_t * 100:.0f} % of roofline overall)"]
     txt = "\n".join(lines)

@@ -87,6 +87,45 @@ def test_conv_fwd(cuda, case, mode):
         assert rel(ps[1], (yf * yf).sum(0)) < 2e-3
 
 
+@pytest.mark.parametrize("case", [(4, 8, 256, 64), (2, 8, 512, 128), (3, 5, 256, 256), (2, 4, 1024, 512)])
+@pytest.mark.parametrize("proj", [False, True])
+def test_conv_fwd_join_prologue(cuda, case, proj):
+    """PRO_JOIN: the 1x1 conv of relu(y*s + t + (r*s2 + t2 | r)) -- the previous residual
+    block's join -- plus the stored join output and its ReLU bit mask, against fp32 PyTorch
+    (the join rounded to bf16 like the standalone kernel stores it)."""
+    N, H, C, Cout = case
+    torch.manual_seed(3)
+    shp = ci.ConvShape(C, Cout, 1, 1, 0)
+    y, r = make((N, H, H, C), cuda), make((N, H, H, C), cuda)
+    s = torch.rand(C, device=cuda) + 0.5
+    t = torch.randn(C, device=cuda) * 0.3
+    s2 = torch.rand(C, device=cuda) + 0.5 if proj else None
+    t2 = torch.randn(C, device=cuda) * 0.3 if proj else None
+    w = torch.randn(Cout, C, 1, 1, device=cuda) / C ** 0.5
+    wf, _ = ci.alloc_packed(shp, cuda, dgrad=False)
+    ci.pack_weights([(w, wf, None, shp)])
+    sc = r.float() * s2 + t2 if proj else r.float()
+    joined = torch.relu(y.float() * s + t + sc)
+    a = joined.to(BF).float()
+    ref = nhwc(F.conv2d(nchw(a), w.to(BF).float()))
+    want_mask = (joined.reshape(-1, 8) > 0).to(torch.int32)
+    want_mask = (want_mask << torch.arange(8, device=cuda, dtype=torch.int32)).sum(1).to(torch.uint8)
+    for tile, ns in [(None, None), ((64, 64, 64), 1), ((128, 64, 32), 3), ((128, 128, 32), None),
+                     ((64, 128, 128), 2), ((64, 64, 128), 1)]:
+        if tile and Cout % tile[1]:
+            continue
+        jout = torch.full_like(y, float("nan"))
+        jmask = torch.zeros(y.numel() // 8, device=cuda, dtype=torch.uint8)
+        out, part = ci.conv_fwd_join(y, r, s, t, s2, t2, wf, shp, jout, jmask, tile=tile, nsplit=ns)
+        assert rel(out, ref) < 1e-2, (tile, rel(out, ref))
+        # (fma vs separate roundings of y*s + t: at most one bf16 ulp apart)
+        assert ((jout.float() - a).abs() <= a.abs() * 2 ** -7 + 1e-6).all(), (tile, (jout.float() - a).abs().max())
+        assert (jmask != want_mask).float().mean().item() < 1e-3, tile
+        ps = part.sum(0)
+        yf = ref.reshape(-1, Cout)
+        assert rel(ps[0], yf.sum(0)) < 2e-3 and rel(ps[1], (yf * yf).sum(0)) < 2e-3
+
+
 DGRAD_CASES = [
     (4, 8, 64, 128, 1, 1, 0),
     (2, 8, 64, 64, 3, 1, 1),

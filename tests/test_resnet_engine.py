@@ -54,26 +54,21 @@ def _train_step_vs_reference(cuda, arch):
     F.cross_entropy(out_e.float(), y).backward()
     F.cross_entropy(out_rb.float(), y).backward()
 
-    def cos(a, b):
-        return F.cosine_similarity(a.flatten().float(), b.flatten().float(), dim=0).item()
-
-    # Gradients of parameters sitting behind batch normalisation are small residuals of
-    # large cancelling terms (e.g. the stem weight after 50 normalised layers, BN betas):
-    # bf16 loses them in the reference's own autocast run as well.  Hence: the whole
-    # gradient vector must agree closely, and each parameter at least as well as the
-    # reference's bf16 autocast gradient does (with a noise margin).
-    ge = torch.cat([p.grad.flatten().float() for p in m_eng.parameters()])
-    gr = torch.cat([p.grad.flatten().float() for p in m_ref.parameters()])
-    gb = torch.cat([p.grad.flatten().float() for p in m_rb.parameters()])
-    assert cos(ge, gr) > min(0.98, cos(gb, gr) - 0.05), (cos(ge, gr), cos(gb, gr))
-    good = 0
+    # Every parameter's gradient -- conv weights, BN affines, the fc weight and bias -- must be
+    # within 2x the relative error of the reference model's own bf16-autocast gradient (plus a
+    # small absolute floor for parameters whose autocast gradient happens to be near exact).
+    # Gradients behind many normalised layers (the stem weight, BN betas) are small residuals
+    # of large cancelling terms, so their bf16 errors are large in both runs; the bound is
+    # relative to what bf16 itself loses on each parameter.
+    worst = []
     for (n, pr), (_, pe), (_, pb) in zip(m_ref.named_parameters(), m_eng.named_parameters(),
                                          m_rb.named_parameters()):
         assert pe.grad is not None, n
-        c_e, c_b = cos(pe.grad, pr.grad), cos(pb.grad, pr.grad)
-        assert c_e > min(0.95, c_b - 0.3), (n, c_e, c_b)
-        good += c_e > min(0.97, c_b - 0.05)
-    assert good >= 0.9 * len(list(m_ref.parameters())), good
+        e_e, e_b = rel(pe.grad, pr.grad), rel(pb.grad, pr.grad)
+        worst.append((e_e / max(e_b, 1e-6), n, e_e, e_b))
+        assert e_e <= max(2.0 * e_b, 5e-3), (n, e_e, e_b)
+    worst.sort(reverse=True)
+    print("worst engine/autocast gradient error ratios:", [(n, round(r, 2)) for r, n, _, _ in worst[:5]])
     for (n, br), (_, be) in zip(m_ref.named_buffers(), m_eng.named_buffers()):
         if br.dtype.is_floating_point:
             assert rel(be, br) < 2e-2, n
