@@ -41,7 +41,7 @@ void grad_sumsq(uint64_t g, long n, uint64_t inv_scale, int unscale, uint64_t pa
                 uint64_t stream);
 void grad_norm_finalize(uint64_t part, int nb, float max_norm, uint64_t out, uint64_t stream);
 void sgd_step(uint64_t p, uint64_t g, uint64_t buf, uint64_t shadow, long n, float lr, float momentum, float dampening,
-              float wd, int nesterov, int first, uint64_t gsc, uint64_t found_inf, int zero_grad, uint64_t stream);
+              float wd, int nesterov, int first, uint64_t gsc, uint64_t found_inf, int zero_grad, uint64_t lr_dev, uint64_t stream);
 void madgrad_step(uint64_t p, uint64_t g, uint64_t gss, uint64_t s, uint64_t x0, uint64_t shadow, long n, float lr,
                   float momentum, float wd, float eps, int decouple, long k, uint64_t kskip, uint64_t gsc,
                   uint64_t found_inf, int zero_grad, uint64_t stream);

@@ -101,9 +101,10 @@ __global__ __launch_bounds__(kOB) void sgd_kernel(float* __restrict__ p, float* 
                                                   bf16* __restrict__ shadow, long n4, float lr, float momentum,
                                                   float dampening, float wd, int nesterov, int first,
                                                   const float* __restrict__ gsc, const int* __restrict__ found_inf,
-                                                  int zero_grad) {
+                                                  int zero_grad, const float* __restrict__ lr_dev) {
   if (skip_step(found_inf)) { skip_zero(g, n4 * 4, zero_grad); return; }
   const float c = gscale(gsc);
+  if (lr_dev) lr = *lr_dev;  // device learning rate: a captured HIP graph follows the schedule
   float4* p4 = reinterpret_cast<float4*>(p);
   float4* g4 = reinterpret_cast<float4*>(g);
   float4* b4 = reinterpret_cast<float4*>(buf);
@@ -245,12 +246,14 @@ void grad_norm_finalize(uint64_t part, int nb, float max_norm, uint64_t out, uin
 }
 
 void sgd_step(uint64_t p, uint64_t g, uint64_t buf, uint64_t shadow, long n, float lr, float momentum, float dampening,
-              float wd, int nesterov, int first, uint64_t gsc, uint64_t found_inf, int zero_grad, uint64_t stream) {
+              float wd, int nesterov, int first, uint64_t gsc, uint64_t found_inf, int zero_grad, uint64_t lr_dev,
+              uint64_t stream) {
   FDT_CHECK(n % 4 == 0, "flat buffer must be padded to a multiple of 4");
   FDT_CHECK(momentum == 0.f || buf != 0, "momentum buffer required");
   sgd_kernel<<<opt_grid(n / 4), kOB, 0, as_stream(stream)>>>(P<float>(p), P<float>(g), P<float>(buf), P<bf16>(shadow),
                                                               n / 4, lr, momentum, dampening, wd, nesterov, first,
-                                                              P<const float>(gsc), P<const int>(found_inf), zero_grad);
+                                                              P<const float>(gsc), P<const int>(found_inf), zero_grad,
+                                                              P<const float>(lr_dev));
   FDT_LAUNCH_CHECK();
 }
 

@@ -14,11 +14,37 @@ import torch.nn.functional as F
 from . import _native
 
 
+class _GatherRows(torch.autograd.Function):
+    """``F.embedding`` whose backward is a static-shape ``index_add_`` (atomic scatter-add).
+
+    ATen's dense embedding backward sorts the indices and compacts them with a
+    data-dependent-size unique / partition (rocprim ``partition_kernel``): its output size is
+    only known on the device, so under HIP-graph capture the buffers are sized from a value
+    read at capture time and a replay with other token ids writes past them -- the
+    ``HSA_STATUS_ERROR_MEMORY_APERTURE_VIOLATION`` of the captured ``--no-native``
+    transformer step (round-2 review 5a).  ``index_add_`` has no data-dependent shape, so
+    the reference-op path is graph-safe (and ``parallel.graphs.capture_guard`` refuses the
+    ATen op inside any capture)."""
+
+    @staticmethod
+    def forward(ctx, idx, w):
+        ctx.save_for_backward(idx)
+        ctx.shape = w.shape
+        return F.embedding(idx, w)
+
+    @staticmethod
+    def backward(ctx, g):
+        (idx,) = ctx.saved_tensors
+        gw = torch.zeros(ctx.shape, device=g.device, dtype=g.dtype)
+        gw.index_add_(0, idx.reshape(-1), g.reshape(-1, ctx.shape[1]))
+        return None, gw
+
+
 def embedding_sum_reference(ids, types, pos_ids, tok_w, pos_w, seg_w, scale):
     L = ids.size(1)
-    pos = F.embedding(pos_ids[:L], pos_w).unsqueeze(0)
-    seg = F.embedding(types[:, :L], seg_w)
-    tok = F.embedding(ids.long(), tok_w.float() if tok_w.dtype != torch.float32 else tok_w)
+    pos = _GatherRows.apply(pos_ids[:L], pos_w).unsqueeze(0)
+    seg = _GatherRows.apply(types[:, :L], seg_w)
+    tok = _GatherRows.apply(ids.long(), tok_w.float() if tok_w.dtype != torch.float32 else tok_w)
     return (pos + tok + seg) * scale
 
 

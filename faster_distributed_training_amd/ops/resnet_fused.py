@@ -684,7 +684,7 @@ class _BodyWithDummy(torch.autograd.Function):
                 st.inner.keep = True
                 st.fwd = torch.cuda.CUDAGraph()
                 torch.cuda.synchronize()
-                with torch.cuda.graph(st.fwd, pool=st.pool, capture_error_mode="thread_local"):
+                with torch.cuda.graph(st.fwd, pool=st.pool, capture_error_mode="thread_local"), _graphs.capture_guard():
                     st.h = ResNetBodyFn.forward(st.inner, st.x, plan, training, True)
                 st.fwd.replay()
                 st.stage = "fwd"
@@ -709,7 +709,7 @@ class _BodyWithDummy(torch.autograd.Function):
             side.wait_stream(torch.cuda.current_stream())
             torch.cuda.synchronize()
             rec = _graphs.Recorder(st.pool)
-            with torch.cuda.stream(side), _graphs.recording(rec):
+            with torch.cuda.stream(side), _graphs.recording(rec), _graphs.capture_guard():
                 rec.begin()
                 try:
                     ResNetBodyFn.backward(st.inner, st.g)

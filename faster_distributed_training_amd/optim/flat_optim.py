@@ -136,7 +136,8 @@ class SGD(FlatOptimizer):
             _native.native().sgd_step(
                 self.flat.data.data_ptr(), self.flat.grad.data_ptr(), _p(buf), _p(self.flat.shadow), self.flat.numel,
                 float(g["lr"]), float(g["momentum"]), float(g["dampening"]), float(g["weight_decay"]),
-                int(g["nesterov"]), first, _p(grad_scale), _p(found_inf), int(self.zero_grad_in_step), _sp())
+                int(g["nesterov"]), first, _p(grad_scale), _p(found_inf), int(self.zero_grad_in_step),
+                _p(getattr(self, "lr_dev", None)), _sp())
         else:
             gr = self._cpu_common(grad_scale, found_inf) if d_override is None else d_override
             if gr is None:

@@ -58,6 +58,8 @@ def orthonormal_special(rank: int, dim: int, dtype=torch.float32, device=None) -
 FUSED = os.environ.get("FDT_NGD_FUSED", "1") != "0"
 # one eigensolver launch per optimizer step for all update-step Z matrices (see Deferred)
 DEFER = os.environ.get("FDT_NGD_DEFER", "1") != "0"
+# steady-state optimizer steps replayed as HIP graphs (NGD._graph_step)
+GRAPHS = os.environ.get("FDT_NGD_GRAPHS", "1") != "0"
 
 
 def _fused_small_math(X, R) -> bool:
@@ -81,7 +83,7 @@ class Deferred:
         self.Z, self.fn = Z, fn
 
 
-def drive(gens, side=None):
+def drive(gens, side=None, defer_out=None):
     """Run preconditioner generators in lock-step: each yields a batch of Z matrices and
     receives ``(eigenvalues, eigenvectors)``; all Z pending at the same time are solved by
     one ``eigh_many`` launch.  ``Deferred`` yields are collected and solved together after
@@ -94,7 +96,10 @@ def drive(gens, side=None):
     its results are only read by the next optimizer step.  ``drive`` then also returns
     ``(done_event, keepalive)``: the caller's stream must wait on the event before the state
     is read again, and ``keepalive`` (the deferred inputs, made on the caller's stream) must
-    outlive that wait."""
+    outlive that wait.
+
+    ``defer_out`` (a list): the deferred work is appended to it instead of being solved (the
+    HIP-graph path captures it as a separate graph on the side stream)."""
     from ..ops.eigh import eigh_many
     results = [None] * len(gens)
     deferred = []
@@ -124,6 +129,9 @@ def drive(gens, side=None):
             z = advance(i, o)
             if z is not None:
                 pending[i] = z
+    if defer_out is not None:
+        defer_out.extend(deferred)
+        return results
     if side is not None:
         if not deferred:
             return results, None
@@ -524,6 +532,11 @@ class NGD(SGD):
         self.overlap_eigh = overlap_eigh
         self._side = None
         self._pending = None
+        self.graphs = GRAPHS
+        self._gcache = {}
+        self._gpool = None
+        self.graph_replays = 0
+        self.lr_dev = None
 
     def _build_groups(self):
         g = self.group
@@ -551,8 +564,9 @@ class NGD(SGD):
             torch.cuda.current_stream().wait_event(done)
             self._pending = None
 
-    def _precondition(self, grad, grad_scale):
-        """grad <- NGD-preconditioned (grad * scale + wd * p), in place."""
+    def _precondition(self, grad, grad_scale, defer_out=None):
+        """grad <- NGD-preconditioned (grad * scale + wd * p), in place.  ``defer_out``: collect
+        the deferred eigensolves instead of running them (graph capture)."""
         self.sync_state()
         g = self.group
         if grad_scale is not None:
@@ -566,7 +580,9 @@ class NGD(SGD):
             gens = [sg.precondition_gen(torch.stack([grad[s.offset:s.offset + s.numel].view(s.shape) for s in slots]))
                     for sg, slots in live]
             side = self._side_stream(grad)
-            if side is not None:
+            if defer_out is not None:
+                outs = drive(gens, defer_out=defer_out)
+            elif side is not None:
                 outs, self._pending = drive(gens, side)
             else:
                 outs = drive(gens)
@@ -579,18 +595,124 @@ class NGD(SGD):
 
     @torch.no_grad()
     def _step(self, grad_scale, found_inf, d_override=None):
-        g = self.group
         if found_inf is not None and bool(found_inf.item() != 0):
             if self.zero_grad_in_step:  # GradScaler skip (fp16 mode only); still clear the gradient
                 self.flat.grad.zero_()
             return
-        self._precondition(self.flat.grad, grad_scale)
+        if self._graph_ready(grad_scale, found_inf, d_override):
+            return self._graph_step(grad_scale)
+        self._eager_step(grad_scale)
+
+    def _eager_step(self, grad_scale, defer_out=None):
+        g = self.group
+        if self.lr_dev is not None and not torch.cuda.is_current_stream_capturing():
+            self.lr_dev.fill_(float(g["lr"]))  # (the SGD kernel reads it once graphs exist)
+        self._precondition(self.flat.grad, grad_scale, defer_out)
         wd = g["weight_decay"]
         g["weight_decay"] = 0.0
         try:
             super()._step(None, None)
         finally:
             g["weight_decay"] = wd
+
+    # ------------------------------------------------------------ HIP-graph steps
+    # After the initialisation schedule (every preconditioner updates on each of its first 10
+    # calls) the step is periodic: update iff t % update_period == 0, the same for every
+    # state (they advance together).  Each kind of step -- update / plain -- is captured once
+    # and replayed: ~100-200 launches become one graph launch (+ one for the deferred
+    # eigensolve).  Everything a replay needs is static: gradients / parameters / momentum in
+    # the flat buffers, W / d / rho updated in place, the clip coefficient and the learning
+    # rate read from device buffers (``lr_dev``: schedulers keep working).  Host-side values
+    # baked into a capture are part of the cache key (momentum, dampening, weight decay, ...).
+    #
+    # The deferred eigensolve + W / d / rho update of an update step is its OWN graph,
+    # replayed on the side stream after the main graph, and the next step waits on an event
+    # recorded AFTER that replay.  (Round-2 root cause of the 2-4 % replay drift: the side-
+    # stream work had been captured into the step's graph with its completion event recorded
+    # during capture; an event recorded inside a capture is not re-recorded by replays, so the
+    # next step's wait on it returned at once and its preconditioning read W / d / rho while
+    # the previous replay was still rewriting them.)
+    def _graph_states(self):
+        return [st for sg, _ in (self.groups or []) for _, st in sg.axes]
+
+    def _graph_ready(self, grad_scale, found_inf, d_override):
+        g = self.group
+        if not (self.graphs and g["ngd"] and self.flat.data.is_cuda and _native.enabled() and d_override is None
+                and found_inf is None and self.groups is not None and _native_eigh(self.flat.device)):
+            return False
+        if torch.cuda.is_current_stream_capturing():
+            return False
+        sts = self._graph_states()
+        if not sts or min(st.t for st in sts) < 10 or len({(st.t, st.update_period) for st in sts}) != 1:
+            return False
+        if g["momentum"] != 0 and not self.state.get("__flat__", {}).get("initialized", 0):
+            return False
+        return True
+
+    def _graph_key(self, grad_scale):
+        g = self.group
+        st = self._graph_states()[0]
+        upd = st.t % st.update_period == 0
+        return (upd, float(g["momentum"]), float(g["dampening"]), float(g["weight_decay"]), bool(g["nesterov"]),
+                0 if grad_scale is None else grad_scale.data_ptr())
+
+    def _graph_step(self, grad_scale):
+        key = self._graph_key(grad_scale)
+        if self.lr_dev is None:
+            self.lr_dev = torch.zeros(1, device=self.flat.device, dtype=torch.float32)
+        self.lr_dev.fill_(float(self.group["lr"]))
+        ent = self._gcache.get(key)
+        if ent is None:
+            ent = self._gcache[key] = self._capture(grad_scale)
+        self.sync_state()  # the previous update's side-stream graph -> before this replay
+        ent["main"].replay()
+        if ent["side"] is not None:
+            cur = torch.cuda.current_stream()
+            side = self._side_stream(self.flat.grad) or cur
+            side.wait_stream(cur)
+            with torch.cuda.stream(side):
+                ent["side"].replay()
+                done = torch.cuda.Event()
+                done.record(side)
+            self._pending = (done, None)
+        for st in self._graph_states():
+            st.t += 1
+        self.graph_replays += 1
+
+    def _capture(self, grad_scale):
+        """Capture one step kind: the main graph (preconditioning + momentum update) and, on
+        update steps, the deferred eigensolves + state updates as a second graph."""
+        from ..ops.eigh import eigh_many
+        from ..parallel.graphs import capture_guard
+        self.sync_state()
+        dev = self.flat.device
+        if self._gpool is None:
+            self._gpool = torch.cuda.graph_pool_handle()
+        sts = self._graph_states()
+        t0 = [st.t for st in sts]
+        cur = torch.cuda.current_stream()
+        cs = torch.cuda.Stream(device=dev)
+        cs.wait_stream(cur)
+        torch.cuda.synchronize(dev)
+        deferred = []
+        main = torch.cuda.CUDAGraph()
+        side_g = None
+        try:
+            with torch.cuda.stream(cs):
+                with torch.cuda.graph(main, pool=self._gpool, stream=cs, capture_error_mode="thread_local"), \
+                        capture_guard():
+                    self._eager_step(grad_scale, defer_out=deferred)
+                if deferred:
+                    side_g = torch.cuda.CUDAGraph()
+                    with torch.cuda.graph(side_g, pool=self._gpool, stream=cs, capture_error_mode="thread_local"), \
+                            capture_guard():
+                        for d, (c, U) in zip(deferred, eigh_many([d.Z for d in deferred])):
+                            d.fn(c, U)
+        finally:
+            for st, t in zip(sts, t0):  # the captures ran the host schedule once: undo it
+                st.t = t
+        cur.wait_stream(cs)
+        return {"main": main, "side": side_g, "keep": deferred}
 
     def _states(self):
         """Every batched per-axis preconditioner state (empty before the first step)."""

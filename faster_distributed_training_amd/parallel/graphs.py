@@ -16,7 +16,10 @@ that it runs on autograd's device thread like the hooks that cut it).  Reference
 """
 from __future__ import annotations
 
+import contextlib
+
 import torch
+from torch.utils._python_dispatch import TorchDispatchMode
 
 # The recorder of the capture in progress (read by parallel/ddp.py hooks and the engine's
 # grad_ready from the autograd thread); None outside a capture.
@@ -144,11 +147,12 @@ class SegmentedStep:
         self.one = torch.ones((), device=self.device)  # static seed gradient of the loss
         with torch.cuda.stream(side):
             self.fwd = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(self.fwd, pool=self.pool, stream=side, capture_error_mode="thread_local"):
+            with torch.cuda.graph(self.fwd, pool=self.pool, stream=side, capture_error_mode="thread_local"), \
+                    capture_guard():
                 out = fwd()
                 loss = _BackwardCaptureStart.apply(out[0], rec)
             assert loss.dim() == 0 and loss.dtype == torch.float32, "SegmentedStep: scalar fp32 loss"
-            with recording(rec):
+            with recording(rec), capture_guard():
                 loss.backward(self.one)
         torch.cuda.current_stream(self.device).wait_stream(side)
         assert rec.cur is None and rec.segments, "backward capture did not complete"
@@ -162,3 +166,40 @@ class SegmentedStep:
     def replay(self):
         self.fwd.replay()
         self.rec.replay()
+
+
+# ------------------------------------------------------------------ capture guard
+class CaptureUnsafeOp(RuntimeError):
+    pass
+
+
+# ATen ops whose output size depends on tensor VALUES (or that read a device value back to
+# the host): under HIP-graph capture they either synchronise (illegal while capturing) or,
+# worse, size their buffers from a value read at capture time, so a replay with other data
+# writes out of bounds (round-2: rocprim partition_kernel aperture violation on replay of
+# the torch-op transformer step, from embedding_dense_backward's unique-by-key).
+_UNSAFE = ("nonzero", "masked_select", "unique", "_unique", "unique_consecutive", "unique_dim",
+           "_unique2", "embedding_dense_backward", "_local_scalar_dense", "repeat_interleave",
+           "masked_scatter", "_embedding_bag_backward", "bincount", "histc")
+
+
+class _CaptureGuardMode(TorchDispatchMode):
+    def __torch_dispatch__(self, func, types, args=(), kwargs=None):
+        name = func.overloadpacket.__name__
+        if name in _UNSAFE:
+            raise CaptureUnsafeOp(f"{func} inside a HIP-graph capture: its output size / host value depends on the "
+                                  f"data, so replays would reuse the capture-time size (not graph-safe)")
+        if name == "index" and any(isinstance(t, torch.Tensor) and t.dtype == torch.bool
+                                   for t in (args[1] if len(args) > 1 else ())):
+            raise CaptureUnsafeOp("boolean-mask indexing inside a HIP-graph capture (data-dependent output size)")
+        return func(*args, **(kwargs or {}))
+
+
+@contextlib.contextmanager
+def capture_guard():
+    """Raise ``CaptureUnsafeOp`` when a data-dependent-size or host-synchronising ATen op runs
+    inside the block (every HIP-graph capture of this package is wrapped in it; the mode is
+    part of the thread-local state autograd hands to its device threads, so backward ops are
+    checked too)."""
+    with _CaptureGuardMode():
+        yield

@@ -28,7 +28,7 @@ from ..ops.mixup import mixup_criterion
 from ..optim.flat_optim import SGD, Adam, DeviceGradScaler, GradClipper, MirrorMADGRAD, MADGRAD
 from ..optim.ngd import NGD
 from ..parallel import dist as pdist
-from ..parallel.graphs import SegmentedStep
+from ..parallel.graphs import SegmentedStep, capture_guard as _graph_guard
 from ..utils.env import default_device, print0, seed_everything
 from ..utils.flat import FlatParams
 from . import checkpoint as ckpt
@@ -228,10 +228,14 @@ class TransformerTrainer:
     # launches each bucket's all-reduce between segments (also under the sharded NGD
     # optimizer, whose gradient all-reduce is the same bucket reducer).  bf16 only; not with FSDP (collectives inside forward).
     def _graphs_on(self):
-        # (the --no-native ablation is plain eager PyTorch: no capture either -- captured, the
-        # torch-op transformer step faulted with an illegal address on replay, measured)
+        # (the --no-native ablation is plain eager PyTorch by default: graphs are one of the
+        # "tricks".  ``extra["graphs_torch_ops"]`` captures the torch-op step too -- graph-safe
+        # since its embedding backward is a static-shape index_add (ops/embedding._GatherRows;
+        # ATen's dense embedding backward sized its unique/partition buffers at capture time
+        # and faulted on replay), with parallel.graphs.capture_guard refusing any such op)
         from ..ops import _native
-        return (TR_GRAPHS and self.device.type == "cuda" and self.fsdp is None and _native.enabled()
+        native_ok = _native.enabled() or bool(self.cfg.extra.get("graphs_torch_ops"))
+        return (TR_GRAPHS and self.device.type == "cuda" and self.fsdp is None and native_ok
                 and not self.scaler.enabled and self.cfg.profile_steps <= 0 and not self.cfg.faithful
                 and self.model.training)
 
@@ -298,7 +302,7 @@ class TransformerTrainer:
                     st.update(replay=step.replay, segments=step.num_segments)
                 else:
                     g = torch.cuda.CUDAGraph()
-                    with torch.cuda.graph(g, pool=self._graph_pool):
+                    with torch.cuda.graph(g, pool=self._graph_pool), _graph_guard():
                         loss, logits = fwd()
                         loss.backward()
                     st.update(replay=g.replay, segments=1)

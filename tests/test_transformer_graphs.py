@@ -8,8 +8,9 @@ pytestmark = pytest.mark.gpu
 def _trainer(graphs, monkeypatch, **kw):
     import faster_distributed_training_amd.train.transformer_trainer as T
     monkeypatch.setattr(T, "TR_GRAPHS", graphs)
+    extra = kw.pop("extra", {"subset_stride": 50})
     cfg = T.TransformerConfig(batch_size=32, synthetic=True, eval=False, plot=False, ngd=False, optimizer="sgd",
-                              epoch=1, steps_per_epoch=8, length_buckets=(128,), extra={"subset_stride": 50},
+                              epoch=1, steps_per_epoch=8, length_buckets=(128,), extra=extra,
                               n_layers=2, **kw)
     return T.TransformerTrainer(cfg)
 
@@ -87,3 +88,51 @@ def test_shadow_weights_match_casts(cuda, monkeypatch):
     ls, ps = run(True)
     assert max(abs(a - b) / max(abs(a), 1e-6) for a, b in zip(lc, ls)) < 1e-3, (lc, ls)
     assert ((pc - ps).norm() / pc.norm()).item() < 1e-4
+
+
+def test_torch_op_step_graph_replay_matches_eager(cuda, monkeypatch):
+    """Review r2 5a: the --no-native (plain torch ops) transformer step captured as a HIP
+    graph used to fault on replay (aperture violation in rocprim partition_kernel: ATen's
+    dense embedding backward sizes its unique-by-key buffers from a value read at capture
+    time).  With the static-shape index_add embedding backward the captured torch-op step
+    replays to the eager trajectory; the capture guard is active during capture."""
+    import torch.nn as nn
+    monkeypatch.setenv("FDT_NATIVE", "0")
+
+    def run(graphs):
+        torch.manual_seed(0)
+        tr = _trainer(graphs, monkeypatch, extra={"subset_stride": 50, "graphs_torch_ops": True})
+        for mod in tr.model.modules():
+            if isinstance(mod, nn.Dropout):
+                mod.p = 0.0
+        tr.model.alpha = 0.0
+        assert tr._graphs_on() == graphs
+        it = iter(tr.train_loader)
+        losses = [float(tr.train_step(*next(it))) for _ in range(6)]
+        torch.cuda.synchronize()
+        return losses, tr.space.data.clone(), tr
+
+    le, pe, _ = run(False)
+    lg, pg, tg = run(True)
+    assert any(isinstance(v, dict) for v in tg._graphs.values()), "graph path not taken"
+    assert max(abs(a - b) / max(abs(a), 1e-6) for a, b in zip(le, lg)) < 1e-3, (le, lg)
+    assert ((pe - pg).norm() / pe.norm()).item() < 1e-4
+
+
+def test_capture_guard_refuses_data_dependent_ops(cuda):
+    """Inside a capture, ops with data-dependent output sizes raise instead of recording a
+    capture-time size (forward and autograd backward)."""
+    from faster_distributed_training_amd.parallel.graphs import CaptureUnsafeOp, capture_guard
+    x = torch.randn(64, device=cuda)
+    w = torch.randn(10, 8, device=cuda, requires_grad=True)
+    idx = torch.randint(0, 10, (32,), device=cuda)
+    g = torch.cuda.CUDAGraph()
+    s = torch.cuda.Stream()
+    with torch.cuda.stream(s):
+        with pytest.raises(CaptureUnsafeOp):
+            with torch.cuda.graph(g, stream=s), capture_guard():
+                torch.nonzero(x > 0)
+    out = torch.nn.functional.embedding(idx, w).sum()
+    with pytest.raises(CaptureUnsafeOp):
+        with capture_guard():
+            out.backward()
