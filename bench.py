@@ -157,7 +157,7 @@ def _sharding_fields(tr, rec):
         cfg["fsdp_units"] = len(tr.fsdp.units)
         cfg["fsdp_peak_full_bytes"] = int(tr.fsdp.peak_full_bytes)
         cfg["fsdp_shard_numel"] = int(tr.fsdp.space.numel)
-        cfg["fsdp_graphs"] = bool(getattr(tr.fsdp, "graphs", False))
+        cfg["fsdp_static_graphs"] = bool(tr.fsdp.static)
     elif tr.zero is not None:
         cfg["optimizer_sharding"] = "ngd-owner-shards (bucketed all-reduce overlapped with backward + all-gather)"
         cfg["owner_shard_numel"] = int(tr.zero.view.numel)

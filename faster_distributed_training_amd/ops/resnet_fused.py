@@ -221,6 +221,8 @@ class Plan:
         ci.pack_weights(ents)
 
     def release_stage(self, name, fwd: bool):
+        if self.fsdp is not None and self.fsdp.static:
+            return  # static FSDP (graphs): packed layouts keep their addresses
         for u in self.stage_units(name):
             _release(u.wf if fwd else u.wd)
 
@@ -620,8 +622,9 @@ def resnet_engine_forward(model, x):
     if plan is None:
         plan = model._plan = Plan(model)
     plan.fsdp = getattr(model, "_fsdp", None)
-    # collectives run between the stages under FSDP: no whole-body graph capture
-    plan.use_graphs = bool(getattr(model, "graph_engine", False)) and plan.fsdp is None
+    # FSDP: graph segments between the stages only in static mode (persistent buffers; the
+    # collectives run as actions between segments); eager otherwise
+    plan.use_graphs = bool(getattr(model, "graph_engine", False)) and (plan.fsdp is None or plan.fsdp.static)
     xin = to_engine_input(x, plan.stem.shp.cxp)
     need_grad = torch.is_grad_enabled() and any(p.requires_grad for p in model.parameters())
     if need_grad:
@@ -682,10 +685,21 @@ class _BodyWithDummy(torch.autograd.Function):
                 st.x = xin.clone()
                 st.inner = _NoCtx()
                 st.inner.keep = True
-                st.fwd = torch.cuda.CUDAGraph()
+                # forward as graph segments: one, or (static FSDP) one per stage with each
+                # unit's all-gather wait / next-unit prefetch as actions between them
+                cur = torch.cuda.current_stream()
+                side = torch.cuda.Stream()
+                side.wait_stream(cur)
                 torch.cuda.synchronize()
-                with torch.cuda.graph(st.fwd, pool=st.pool, capture_error_mode="thread_local"), _graphs.capture_guard():
-                    st.h = ResNetBodyFn.forward(st.inner, st.x, plan, training, True)
+                rec = _graphs.Recorder(st.pool)
+                with torch.cuda.stream(side), _graphs.recording(rec), _graphs.capture_guard():
+                    rec.begin()
+                    try:
+                        st.h = ResNetBodyFn.forward(st.inner, st.x, plan, training, True)
+                    finally:
+                        rec.end()
+                cur.wait_stream(side)
+                st.fwd = rec
                 st.fwd.replay()
                 st.stage = "fwd"
             else:

@@ -34,6 +34,15 @@ MI355X design (``FullyShardedDP``):
 * the fused ResNet engine (one autograd node for the whole body) drives its units itself at
   stage boundaries (``pre_forward`` / ``post_forward`` / ``pre_backward`` / ``post_backward``,
   ``ops/resnet_fused.py``) and packs / releases its bf16 weight layouts per stage.
+* **static mode** (``static=True``, the engine's HIP-graph path): every unit keeps its
+  gathered-parameter and gradient buffers for the whole run (fixed addresses, so the body can
+  be captured as graphs) -- FSDP's SHARD_GRAD_OP schedule: parameters are gathered once per
+  step in forward (next unit prefetched) and reused by backward, gradients are reduce-
+  scattered per unit from backward, the optimizer state and master weights stay sharded.
+  While a capture is recording, each collective becomes an action between two graph
+  segments (``parallel/graphs.Recorder.cut``): a replay waits for unit i's all-gather and
+  launches unit i+1's before replaying stage i, and launches unit i's reduce-scatter right
+  after stage i's backward segment -- communication keeps overlapping compute.
 
 Memory: with 288 GB per MI355X this is a capability, not a necessity, for these models;
 ``peak_full_bytes`` reports the largest amount of gathered parameter + unit-gradient storage
@@ -173,6 +182,8 @@ class Unit:
             st.resize_(self._bytes())
 
     def _free(self, t):
+        if self.fs.static:
+            return  # static mode: buffers keep their addresses (captured graphs read them)
         st = t.untyped_storage()
         if st.size() != 0:
             st.resize_(0)
@@ -191,7 +202,7 @@ class Unit:
             self.gathered = True
 
     def reshard(self):
-        if self.root or not self.gathered or self.work is not None:
+        if self.root or not self.gathered or self.work is not None or self.fs.static:
             return
         self._free(self.full)
         self.gathered = False
@@ -220,6 +231,13 @@ class Unit:
         """Launch the reduce-scatter of this unit's gradient (async), release buffers."""
         fs = self.fs
         if not self.grads_live or self.rs_work is not None:
+            return
+        if fs.static:
+            # gradient views stay bound to the persistent buffer; only the collective
+            op = dist.ReduceOp.AVG if fs.use_avg else dist.ReduceOp.SUM
+            self.rs_work = dist.reduce_scatter_tensor(fs.grad_chunk(self), self.gfull, op=op, group=fs.pg,
+                                                      async_op=True)
+            self.grads_live = False
             return
         op = dist.ReduceOp.AVG if fs.use_avg else dist.ReduceOp.SUM
         self.rs_work = dist.reduce_scatter_tensor(fs.grad_chunk(self), self.gfull, op=op, group=fs.pg,
@@ -252,11 +270,13 @@ class FullyShardedDP:
     sharded_optimizer = True
 
     def __init__(self, model: nn.Module, device=None, units=None, mode="flat", offload=False, process_group=None,
-                 prefetch=True, engine_units=()):
+                 prefetch=True, engine_units=(), static=False):
         """units: [(name, module)] (None: ``default_units``); mode: 'flat' | 'param' (NGD);
         engine_units: names of units whose forward/backward an engine drives explicitly
-        (no module hooks installed on them)."""
+        (no module hooks installed on them); static: persistent buffers, HIP-graph capture
+        (see the module docstring)."""
         self.model = model
+        self.static = bool(static)
         self.pg = process_group
         self.ws = dist.get_world_size(process_group)
         self.rank = dist.get_rank(process_group)
@@ -355,7 +375,23 @@ class FullyShardedDP:
         j = i + step
         return self.order[j] if 0 <= j < len(self.order) else None
 
+    def _deferred(self, fn):
+        """Run ``fn`` now, or -- while a HIP-graph capture is recording (static mode) -- as an
+        action between two graph segments on every replay."""
+        from . import graphs
+        rec = graphs.active()
+        if rec is not None:
+            assert self.static, "graph capture of FSDP needs static=True"
+            rec.cut([fn])
+        else:
+            fn()
+
     def pre_forward(self, name):
+        if self.static and name in self.engine_units:
+            return self._deferred(lambda: self._pre_forward_now(name))
+        self._pre_forward_now(name)
+
+    def _pre_forward_now(self, name):
         u = self.by_name[name]
         for r in self.units:
             if r.root:
@@ -374,6 +410,12 @@ class FullyShardedDP:
 
     def pre_backward(self, name):
         u = self.by_name[name]
+        if self.static:
+            # parameters are still gathered from this step's forward (engine units: always --
+            # while capturing, the forward's gathers are deferred actions, so the host flag
+            # cannot tell); the gradient buffer is zeroed in stream order (a captured memset)
+            u.begin_backward(gather=(not u.gathered) and name not in self.engine_units)
+            return
         u.begin_backward()
         if self.prefetch:
             prv = self._next(u, -1)
@@ -381,7 +423,17 @@ class FullyShardedDP:
                 prv.gather(wait=False)
 
     def post_backward(self, name):
-        self.by_name[name].reduce()
+        u = self.by_name[name]
+        if self.static and name in self.engine_units:
+            from . import graphs
+            if graphs.active() is not None:
+                u.grads_live = False  # (host state of the capture; the action relaunches it)
+
+                def act(u=u):
+                    u.grads_live = True
+                    u.reduce()
+                return self._deferred(act)
+        u.reduce()
 
     # ------------------------------------------------------------ module hooks
     def _install_hooks(self):
@@ -437,7 +489,7 @@ class FullyShardedDP:
         """Complete every unit's gradient reduce-scatter (launch what is left, e.g. units
         whose parameters got no gradient), land the averaged shard gradients."""
         for u in self.units:
-            if u.bwd_started or u.grads_live:
+            if u.bwd_started or u.grads_live or u.rs_work is not None:
                 u.finish()
             else:  # unused this step: contributes zeros (every rank must join the collective)
                 u.begin_backward(gather=False)
@@ -453,9 +505,9 @@ class FullyShardedDP:
 
     def after_step(self):
         """Nothing to all-gather: the next forward gathers the updated shards (any copy still
-        gathered -- the root unit -- is marked stale)."""
+        gathered -- the root unit, every unit in static mode -- is marked stale)."""
         for u in self.units:
-            if u.root:
+            if u.root or self.static:
                 u.gathered = False
             else:
                 u.reshard()

@@ -121,9 +121,13 @@ class ResNetTrainer:
                 raise ValueError("--fsdp does not shard the learnable meta-mixup parameters")
             from ..parallel.fsdp import FullyShardedDP
             engine = self.model.use_fast_path(torch.empty(1, device=self.device))
-            self.model.graph_engine = False
+            # HIP graphs under FSDP: static mode (persistent unit buffers, SHARD_GRAD_OP-style
+            # schedule, collectives between graph segments); eager FSDP is the full ZeRO-3
+            # reshard-after-forward schedule
+            static = bool(engine and cfg.graphs and not cfg.fsdp_offload and cfg.extra.get("fsdp_static", True))
+            self.model.graph_engine = static
             self.fsdp = FullyShardedDP(self.model, self.device, mode="param" if ngd_opt else "flat",
-                                       offload=cfg.fsdp_offload,
+                                       offload=cfg.fsdp_offload, static=static,
                                        engine_units=("conv1",) + STAGES if engine else ())
             if engine:
                 self.model._fsdp = self.fsdp

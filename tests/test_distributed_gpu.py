@@ -157,6 +157,65 @@ def _fsdp_engine_worker(rank, world):
     assert fs.peak_full_bytes <= _fsdp_peak_bound(fs) < sum(2 * u._bytes() for u in fs.units)
 
 
+def _fsdp_static_graph_worker(rank, world):
+    """FSDP static mode (the engine's HIP-graph path): the body is captured as
+    graph segments cut at the stage boundaries, each unit's all-gather wait / prefetch and
+    reduce-scatter running as actions between them; over eager warm-up, capture and replays
+    every rank's shard gradient equals its chunk of the averaged unsharded gradient."""
+    import torch.distributed as dist
+    from faster_distributed_training_amd.models import resnet as R
+    from faster_distributed_training_amd.ops.resnet_fused import STAGES
+    from faster_distributed_training_amd.parallel.fsdp import FullyShardedDP
+    from faster_distributed_training_amd.ops import _native
+    from faster_distributed_training_amd.utils.flat import FlatParams
+    _native.set_deterministic(True)
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    torch.manual_seed(0)
+    ref = R.resnet50(10).to(dev)
+    ref.fast_path = True
+    torch.manual_seed(rank)
+    m = R.resnet50(10).to(dev)
+    m.fast_path = True
+    m.graph_engine = True
+    fs = FullyShardedDP(m, dev, engine_units=("conv1",) + STAGES, static=True)
+    m._fsdp = fs
+    ref.load_state_dict(fs.full_state_dict())
+    rflat = FlatParams(ref, device=dev)
+    for it in range(4):  # eager warm-up, capture (+ replay), replay, replay
+        x, y = _batch(rank + 10 * it)
+        rflat.grad.zero_()
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            out = m(x.to(dev))
+            rout = ref(x.to(dev))
+        F.cross_entropy(out.float(), y.to(dev)).backward()
+        F.cross_entropy(rout.float(), y.to(dev)).backward()
+        fs.finish_backward()
+        g = rflat.grad.clone()
+        dist.all_reduce(g)
+        g /= world
+        rslots = {s.name: s for s in rflat.slots}
+        for u in fs.units:
+            full = torch.zeros(u.numel, device=dev)
+            for i, (n, p) in enumerate(u.params):
+                s = rslots[n]
+                full[u.pos[i]:u.pos[i] + p.numel()] = g[s.offset:s.offset + s.numel]
+            mine = full[rank * u.chunk:(rank + 1) * u.chunk]
+            got = fs.shard_grad[u.shard_off:u.shard_off + u.chunk]
+            err = ((got - mine).norm() / (mine.norm() + 1e-12)).item()
+            assert err < 1e-5, (it, u.name, err)
+        fs.space.grad.zero_()
+        fs.after_step()
+    st = list(m._plan._graphs.values())[0]
+    assert st.stage == "ready"
+    assert len(st.fwd.segments) >= len(STAGES) + 1  # cut before every stage's forward
+    assert sum(len(a) for _, a in st.rec.segments) >= len(STAGES)  # reduce-scatters between segments
+
+
+def test_fsdp_static_graphs_two_ranks_one_gpu(cuda):
+    run_world(_fsdp_static_graph_worker, world=2, native=True, timeout=400)
+
+
 def _fsdp_peak_bound(fs):
     """Schedule bound: unit i gathered + its gradient buffer, unit i-1 prefetched, unit
     i+1's reduce-scatter in flight, plus the (always gathered) root unit."""
