@@ -41,6 +41,8 @@ def parse():
     ap.add_argument("--ngd", action="store_true")
     ap.add_argument("--meta_learning", action="store_true")
     ap.add_argument("--fsdp", action="store_true")
+    ap.add_argument("--fsdp-param-dtype", default="bf16", choices=["bf16", "fp32"],
+                    help="--fsdp: parameter all-gather wire / compute-copy precision (masters stay fp32)")
     ap.add_argument("--sharded-ngd", action="store_true",
                     help="with --ngd at N=1: run the sharded-NGD data-parallel path over a world-1 group")
     ap.add_argument("--precision", default="bf16")
@@ -80,7 +82,8 @@ def main():
                        optimizer="ngd" if args.ngd else args.optimizer, fsdp=args.fsdp,
                        precision=args.precision, bucket_mb=args.bucket_mb, comm_dtype=args.comm_dtype,
                        fast_path=False if args.no_native else None, graphs=not args.no_graphs,
-                       deterministic=args.deterministic, force_sharded=args.sharded_ngd)
+                       deterministic=args.deterministic, force_sharded=args.sharded_ngd,
+                       fsdp_param_dtype=args.fsdp_param_dtype)
     tr = ResNetTrainer(cfg)
     dev = tr.device
     cuda = dev.type == "cuda"
@@ -151,13 +154,19 @@ def main():
 
 
 def _sharding_fields(tr, rec):
-    """Record which data-parallel path actually ran (FSDP units / ZeRO-2 / bucket reducer)."""
+    """Record which data-parallel path actually ran (FSDP units / ZeRO-2 / bucket reducer) and
+    whether the NGD step ran as HIP-graph replays."""
+    import torch
     cfg = rec["config"]
+    if hasattr(tr.optimizer, "graph_replays"):
+        cfg["ngd_graph_replays"] = int(tr.optimizer.graph_replays)
+        cfg["ngd_graph_kinds"] = len(tr.optimizer._gcache)
     if tr.fsdp is not None:
         cfg["fsdp_units"] = len(tr.fsdp.units)
         cfg["fsdp_peak_full_bytes"] = int(tr.fsdp.peak_full_bytes)
         cfg["fsdp_shard_numel"] = int(tr.fsdp.space.numel)
         cfg["fsdp_static_graphs"] = bool(tr.fsdp.static)
+        cfg["fsdp_param_dtype"] = str(tr.fsdp.param_dtype or torch.float32).replace("torch.", "")
     elif tr.zero is not None:
         cfg["optimizer_sharding"] = "ngd-owner-shards (bucketed all-reduce overlapped with backward + all-gather)"
         cfg["owner_shard_numel"] = int(tr.zero.view.numel)
@@ -182,7 +191,7 @@ def bench_transformer(args):
     buckets = tuple(sorted(int(b) for b in args.seq_buckets.split(",")))
     cfg = TransformerConfig(batch_size=gb // world, synthetic=True, eval=False, plot=False, distributed=world > 1,
                             ngd=True, precision=args.precision, length_buckets=buckets,
-                            bucket_mb=args.bucket_mb, fsdp=args.fsdp, epoch=1)
+                            bucket_mb=args.bucket_mb, fsdp=args.fsdp, epoch=1, fsdp_param_dtype=args.fsdp_param_dtype)
     tr = TransformerTrainer(cfg)
     longest = int(tr.train_loader.store.lengths.max())
     assert longest <= buckets[-1], f"largest bucket {buckets[-1]} would truncate samples of length {longest}"

@@ -157,6 +157,12 @@ class Unit:
         self.numel = ws * self.chunk
         dev = fs.device
         self.full = torch.zeros(self.numel, device=dev, dtype=torch.float32)
+        # param_dtype bf16: the all-gather moves bf16 (half the bytes on xGMI) into this
+        # buffer, upcast into ``full`` after the wait (FSDP MixedPrecision(param_dtype=bf16):
+        # compute sees bf16-rounded weights, the sharded fp32 masters are what the optimizer
+        # updates)
+        self.full16 = (torch.zeros(self.numel, device=dev, dtype=fs.param_dtype)
+                       if fs.param_dtype is not None else None)
         self.gfull = torch.zeros(self.numel, device=dev, dtype=torch.float32)
         self.views = []
         with torch.no_grad():
@@ -189,16 +195,32 @@ class Unit:
             st.resize_(0)
 
     # ------------------------------------------------------------ gather / reshard
-    def gather(self, wait=True):
+    def gather(self, wait=True, exact=False):
+        """All-gather this unit's parameters (``exact``: fp32 wire even with a bf16
+        param_dtype -- checkpoint I/O)."""
         fs = self.fs
         if not self.gathered and self.work is None:
             self._alloc(self.full)
             fs._account()
-            src = fs.shard_chunk(self)
-            self.work = dist.all_gather_into_tensor(self.full, src, group=fs.pg, async_op=True)
+            lowp = self.full16 is not None and not exact
+            self._lowp = lowp
+            dst = self.full16 if lowp else self.full
+            if fs.offload and fs.copy_stream is not None:
+                # pinned-host shard -> device staging on the copy stream, and the all-gather
+                # launched from that stream (RCCL orders after the copy): the compute stream
+                # only meets this unit at its wait
+                fs.copy_stream.wait_stream(torch.cuda.current_stream(fs.device))  # staging reuse
+                with torch.cuda.stream(fs.copy_stream):
+                    src = fs.shard_chunk(self, lowp)
+                    self.work = dist.all_gather_into_tensor(dst, src, group=fs.pg, async_op=True)
+            else:
+                src = fs.shard_chunk(self, lowp)
+                self.work = dist.all_gather_into_tensor(dst, src, group=fs.pg, async_op=True)
         if wait and self.work is not None:
             self.work.wait()
             self.work = None
+            if getattr(self, "_lowp", False):
+                self.full.copy_(self.full16)  # bf16 wire -> the fp32 views the modules read
             self.gathered = True
 
     def reshard(self):
@@ -242,6 +264,13 @@ class Unit:
         op = dist.ReduceOp.AVG if fs.use_avg else dist.ReduceOp.SUM
         self.rs_work = dist.reduce_scatter_tensor(fs.grad_chunk(self), self.gfull, op=op, group=fs.pg,
                                                   async_op=True)
+        if fs.offload and fs.copy_stream is not None:
+            # the averaged shard gradient goes back to pinned host memory on the copy stream as
+            # soon as its reduce-scatter lands, overlapping the rest of backward
+            with torch.cuda.stream(fs.copy_stream):
+                self.rs_work.wait()
+                lo, hi = self.shard_off, self.shard_off + self.chunk
+                fs.shard_grad[lo:hi].copy_(fs.stage_grad[lo:hi], non_blocking=True)
         # at most two unit gradient buffers alive: the previously launched reduce-scatter
         # is ordered before further compute (a stream wait on RCCL) and its buffer released
         prev = fs.last_rs
@@ -270,13 +299,14 @@ class FullyShardedDP:
     sharded_optimizer = True
 
     def __init__(self, model: nn.Module, device=None, units=None, mode="flat", offload=False, process_group=None,
-                 prefetch=True, engine_units=(), static=False):
+                 prefetch=True, engine_units=(), static=False, param_dtype=None):
         """units: [(name, module)] (None: ``default_units``); mode: 'flat' | 'param' (NGD);
         engine_units: names of units whose forward/backward an engine drives explicitly
         (no module hooks installed on them); static: persistent buffers, HIP-graph capture
         (see the module docstring)."""
         self.model = model
         self.static = bool(static)
+        self.param_dtype = param_dtype if param_dtype not in (None, torch.float32) else None
         self.pg = process_group
         self.ws = dist.get_world_size(process_group)
         self.rank = dist.get_rank(process_group)
@@ -323,6 +353,8 @@ class FullyShardedDP:
             self.stage_data = torch.empty(total, device=self.device)
             self.stage_grad = torch.empty(total, device=self.device)
             self.copy_stream = torch.cuda.Stream(self.device) if self.device.type == "cuda" else None
+        else:
+            self.copy_stream = None
         off = 0
         slots = []
         for u in self.units:
@@ -334,6 +366,8 @@ class FullyShardedDP:
                 slots.append(Slot(n, p, off + rel, p.numel(), p.shape))
             off += u.chunk
         self.space = SpaceView(self.shard_data, self.shard_grad, slots, sdev)
+        self.stage16 = (torch.empty(total, device=self.device, dtype=self.param_dtype)
+                        if self.param_dtype is not None else None)
         self.view = self.space  # (trainer interface shared with the sharded-optimizer DP)
         self.peak_full_bytes = 0
         self.last_rs = None  # unit whose reduce-scatter was launched last
@@ -348,12 +382,16 @@ class FullyShardedDP:
         model._fsdp_sharded = self  # checkpoint I/O gathers through summon_full_params
 
     # ------------------------------------------------------------ shard views
-    def shard_chunk(self, u):
+    def shard_chunk(self, u, lowp=False):
         c = self.shard_data[u.shard_off:u.shard_off + u.chunk]
         if self.offload:
             st = self.stage_data[u.shard_off:u.shard_off + u.chunk]
             st.copy_(c, non_blocking=True)
-            return st
+            c = st
+        if lowp:
+            c16 = self.stage16[u.shard_off:u.shard_off + u.chunk]
+            c16.copy_(c)  # fp32 master shard -> bf16 wire copy
+            return c16
         return c
 
     def grad_chunk(self, u):
@@ -496,7 +534,12 @@ class FullyShardedDP:
                 u.finish()
         self.last_rs = None
         if self.offload:
-            self.shard_grad.copy_(self.stage_grad, non_blocking=False)
+            if self.copy_stream is not None:
+                # the per-unit D2H copies were queued on the copy stream as each reduce-scatter
+                # landed; the host optimizer reads the shard next
+                self.copy_stream.synchronize()
+            else:
+                self.shard_grad.copy_(self.stage_grad, non_blocking=False)
         if not self.use_avg:
             self.shard_grad.div_(self.ws)
         for u in self.units:
@@ -518,9 +561,12 @@ class FullyShardedDP:
 
     @contextlib.contextmanager
     def summon_full_params(self):
-        """All units gathered (checkpointing / state_dict); resharded on exit."""
+        """All units gathered (checkpointing / state_dict) with the exact fp32 masters (also
+        under a bf16 param_dtype); resharded on exit."""
         for u in self.units:
-            u.gather(wait=True)
+            if u.full16 is not None and u.work is None:
+                u.gathered = False  # (a bf16-rounded gather is not the master copy)
+            u.gather(wait=True, exact=True)
         try:
             yield
         finally:

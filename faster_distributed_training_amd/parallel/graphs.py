@@ -183,14 +183,24 @@ _UNSAFE = ("nonzero", "masked_select", "unique", "_unique", "unique_consecutive"
            "masked_scatter", "_embedding_bag_backward", "bincount", "histc")
 
 
+def _on_device(args, kwargs):
+    def dev(x):
+        if isinstance(x, torch.Tensor):
+            return x.device.type != "cpu"
+        if isinstance(x, (list, tuple)):
+            return any(dev(y) for y in x)
+        return False
+    return dev(args) or dev(list((kwargs or {}).values()))
+
+
 class _CaptureGuardMode(TorchDispatchMode):
     def __torch_dispatch__(self, func, types, args=(), kwargs=None):
         name = func.overloadpacket.__name__
-        if name in _UNSAFE:
+        if name in _UNSAFE and _on_device(args, kwargs):  # (host tensors are not captured)
             raise CaptureUnsafeOp(f"{func} inside a HIP-graph capture: its output size / host value depends on the "
                                   f"data, so replays would reuse the capture-time size (not graph-safe)")
-        if name == "index" and any(isinstance(t, torch.Tensor) and t.dtype == torch.bool
-                                   for t in (args[1] if len(args) > 1 else ())):
+        if name == "index" and _on_device(args, kwargs) and any(
+                isinstance(t, torch.Tensor) and t.dtype == torch.bool for t in (args[1] if len(args) > 1 else ())):
             raise CaptureUnsafeOp("boolean-mask indexing inside a HIP-graph capture (data-dependent output size)")
         return func(*args, **(kwargs or {}))
 

@@ -60,6 +60,7 @@ class ResNetConfig:
     comm_dtype: str = "fp32"
     fsdp: bool = False
     fsdp_offload: bool = False         # FSDP shards + optimizer state in pinned host memory (CPUOffload)
+    fsdp_param_dtype: str = "fp32"     # fp32 | bf16: all-gather wire / compute copy of the parameters
     shard_ngd: bool = True             # distributed NGD: each rank owns + preconditions 1/world of the params
     scheduler: str = "auto"
     resume: bool = False
@@ -128,6 +129,7 @@ class ResNetTrainer:
             self.model.graph_engine = static
             self.fsdp = FullyShardedDP(self.model, self.device, mode="param" if ngd_opt else "flat",
                                        offload=cfg.fsdp_offload, static=static,
+                                       param_dtype={"fp32": None, "bf16": torch.bfloat16}[cfg.fsdp_param_dtype],
                                        engine_units=("conv1",) + STAGES if engine else ())
             if engine:
                 self.model._fsdp = self.fsdp

@@ -61,6 +61,7 @@ class TransformerConfig:
     faithful: bool = False
     fsdp: bool = False
     fsdp_offload: bool = False       # FSDP shards + optimizer state in pinned host memory (reference CPUOffload)
+    fsdp_param_dtype: str = "fp32"   # fp32 | bf16: all-gather wire / compute copy of the parameters
     shard_ngd: bool = True           # distributed NGD: each rank owns + preconditions 1/world of the params
     bucket_mb: float = 8.0
     resume: bool = False
@@ -115,7 +116,8 @@ class TransformerTrainer:
             # reduce-scattered from gradient hooks; NGD sees whole parameters (Q17)
             from ..parallel.fsdp import FullyShardedDP
             self.fsdp = FullyShardedDP(self.model, self.device, mode="param" if ngd_opt else "flat",
-                                       offload=cfg.fsdp_offload)
+                                       offload=cfg.fsdp_offload,
+                                       param_dtype={"fp32": None, "bf16": torch.bfloat16}[cfg.fsdp_param_dtype])
             self.flat = self.fsdp.space
         else:
             part = self.world if (cfg.distributed and ngd_opt and cfg.shard_ngd) else 0

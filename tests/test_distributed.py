@@ -408,3 +408,40 @@ def _trainer_fsdp_vs_ddp_worker(rank, world, tmp, model):
 @pytest.mark.parametrize("model", ["resnet", "transformer"])
 def test_trainer_fsdp_matches_ddp(tmp_path, model):
     run_world(_trainer_fsdp_vs_ddp_worker, world=2, args=(str(tmp_path), model), timeout=600)
+
+
+def _fsdp_bf16_worker(rank, world):
+    """FSDP param_dtype=bf16: the all-gather moves bf16 (half the bytes), the modules compute
+    with the bf16-rounded weights, the optimizer updates the fp32 master shards, and
+    checkpoint I/O (full_state_dict) returns the exact fp32 masters."""
+    from faster_distributed_training_amd.optim.flat_optim import SGD
+    from faster_distributed_training_amd.parallel.fsdp import FullyShardedDP
+    m = _units_model(seed=rank)
+    units = [(str(i), m[i]) for i in range(0, len(m), 2)]
+    fs = FullyShardedDP(m, torch.device("cpu"), units=units, mode="flat", param_dtype=torch.bfloat16)
+    opt = SGD(fs.space, lr=0.05, momentum=0.9)
+    seen = {}
+
+    def grab(mod, args):
+        seen[id(mod)] = mod.weight.detach().clone()
+    hooks = [m[i].register_forward_pre_hook(grab) for i in range(0, len(m), 2)]
+    for step in range(3):
+        x, y = _batch(rank + 10 * step)
+        F.cross_entropy(m(x), y).backward()
+        fs.finish_backward()
+        opt.step()
+        fs.after_step()
+    for h in hooks:
+        h.remove()
+    for w in seen.values():  # what the layers computed with: bf16-representable values
+        assert torch.equal(w, w.to(torch.bfloat16).float())
+    sd = fs.full_state_dict()
+    full = torch.cat([sd[k].reshape(-1) for k in sd])
+    assert not torch.equal(full, full.to(torch.bfloat16).float())  # fp32 masters, not the wire copy
+    other = full.clone()
+    dist.broadcast(other, 0)
+    assert torch.equal(full, other)
+
+
+def test_fsdp_bf16_param_gather():
+    run_world(_fsdp_bf16_worker, world=2)

@@ -104,7 +104,7 @@ def test_ddp_engine_hip_graphs_two_ranks(cuda):
     run_world(_graph_worker, world=2, native=True, timeout=400)
 
 
-def _fsdp_engine_worker(rank, world):
+def _fsdp_engine_worker(rank, world, offload=False):
     """FSDP full-shard driving the fused ResNet engine stage by stage (gather + per-stage
     weight packing before each stage's forward and backward, reduce-scatter at each stage
     boundary): every rank's shard gradient equals its chunk of the average of the per-rank
@@ -124,7 +124,7 @@ def _fsdp_engine_worker(rank, world):
     torch.manual_seed(rank)
     m = R.resnet50(10).to(dev)
     m.fast_path = True
-    fs = FullyShardedDP(m, dev, engine_units=("conv1",) + STAGES)  # broadcasts rank 0's weights
+    fs = FullyShardedDP(m, dev, engine_units=("conv1",) + STAGES, offload=offload)  # broadcasts rank 0's weights
     m._fsdp = fs
     ref.load_state_dict(fs.full_state_dict())
     fs.peak_full_bytes = 0  # (summon_full_params above gathered everything on purpose)
@@ -148,7 +148,7 @@ def _fsdp_engine_worker(rank, world):
                 s = rslots[n]
                 full[u.pos[i]:u.pos[i] + p.numel()] = g[s.offset:s.offset + s.numel]
             mine = full[rank * u.chunk:(rank + 1) * u.chunk]
-            got = fs.shard_grad[u.shard_off:u.shard_off + u.chunk]
+            got = fs.shard_grad[u.shard_off:u.shard_off + u.chunk].to(dev)
             err = ((got - mine).norm() / (mine.norm() + 1e-12)).item()
             assert err < 1e-5, (it, u.name, err)
         fs.space.grad.zero_()
@@ -225,8 +225,11 @@ def _fsdp_peak_bound(fs):
                       for i in range(len(b)))
 
 
-def test_fsdp_engine_two_ranks_one_gpu(cuda):
-    run_world(_fsdp_engine_worker, world=2, native=True, timeout=400)
+@pytest.mark.parametrize("offload", [False, True])
+def test_fsdp_engine_two_ranks_one_gpu(cuda, offload):
+    """offload: pinned-host shards, H2D staging + all-gather issued from the copy stream,
+    per-unit D2H of the reduce-scattered gradient queued there as it lands."""
+    run_world(_fsdp_engine_worker, world=2, native=True, timeout=400, args=(offload,))
 
 
 def _rccl_worker(rank, world):
