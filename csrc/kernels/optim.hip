@@ -104,7 +104,10 @@ __global__ __launch_bounds__(kOB) void sgd_kernel(float* __restrict__ p, float* 
                                                   int zero_grad, const float* __restrict__ lr_dev) {
   if (skip_step(found_inf)) { skip_zero(g, n4 * 4, zero_grad); return; }
   const float c = gscale(gsc);
-  if (lr_dev) lr = *lr_dev;  // device learning rate: a captured HIP graph follows the schedule
+  if (lr_dev) {  // device [lr, momentum]: a captured HIP graph follows the schedules (OneCycle cycles both)
+    lr = lr_dev[0];
+    momentum = lr_dev[1];
+  }
   float4* p4 = reinterpret_cast<float4*>(p);
   float4* g4 = reinterpret_cast<float4*>(g);
   float4* b4 = reinterpret_cast<float4*>(buf);

@@ -606,7 +606,7 @@ class NGD(SGD):
     def _eager_step(self, grad_scale, defer_out=None):
         g = self.group
         if self.lr_dev is not None and not torch.cuda.is_current_stream_capturing():
-            self.lr_dev.fill_(float(g["lr"]))  # (the SGD kernel reads it once graphs exist)
+            self._fill_hp()  # (the SGD kernel reads [lr, momentum] from it once graphs exist)
         self._precondition(self.flat.grad, grad_scale, defer_out)
         wd = g["weight_decay"]
         g["weight_decay"] = 0.0
@@ -653,14 +653,21 @@ class NGD(SGD):
         g = self.group
         st = self._graph_states()[0]
         upd = st.t % st.update_period == 0
-        return (upd, float(g["momentum"]), float(g["dampening"]), float(g["weight_decay"]), bool(g["nesterov"]),
+        # lr and momentum are read from ``lr_dev`` by the kernel (OneCycleLR cycles both every
+        # step); only whether momentum is on (a momentum buffer in the capture) is baked
+        return (upd, g["momentum"] != 0, float(g["dampening"]), float(g["weight_decay"]), bool(g["nesterov"]),
                 0 if grad_scale is None else grad_scale.data_ptr())
+
+    def _fill_hp(self):
+        g = self.group
+        self.lr_dev[0].fill_(float(g["lr"]))  # (two scalar fills: no pageable host copy)
+        self.lr_dev[1].fill_(float(g["momentum"]))
 
     def _graph_step(self, grad_scale):
         key = self._graph_key(grad_scale)
         if self.lr_dev is None:
-            self.lr_dev = torch.zeros(1, device=self.flat.device, dtype=torch.float32)
-        self.lr_dev.fill_(float(self.group["lr"]))
+            self.lr_dev = torch.zeros(2, device=self.flat.device, dtype=torch.float32)  # [lr, momentum]
+        self._fill_hp()
         ent = self._gcache.get(key)
         if ent is None:
             ent = self._gcache[key] = self._capture(grad_scale)

@@ -27,6 +27,9 @@ def test_ngd_graph_replay_matches_eager_over_three_update_periods(cuda):
         if step == 15:
             for o in (oa, ob):  # a scheduler changing the learning rate between replays
                 o.param_groups[0]["lr"] = 0.02
+        if step >= 17:
+            for o in (oa, ob):  # ... and the momentum every step (OneCycleLR's cycle_momentum)
+                o.param_groups[0]["momentum"] = 0.85 + 0.01 * (step % 5)
         g = (torch.randn(fa.numel, generator=gen) * 1e-2).to(cuda)
         fa.grad.copy_(g)
         fb.grad.copy_(g)
@@ -39,7 +42,7 @@ def test_ngd_graph_replay_matches_eager_over_three_update_periods(cuda):
         err = ((fa.data - fb.data).abs().max() / fa.data.abs().max()).item()
         assert err <= 1e-6, (step, err)
     assert ob.graph_replays == 14 and oa.graph_replays == 0
-    assert {k[0] for k in ob._gcache} == {True, False}  # update and plain step kinds captured
+    assert {k[0] for k in ob._gcache} == {True, False} and len(ob._gcache) == 2  # captured once per kind
     for (sa, _), (sb, _) in zip(oa.groups, ob.groups):
         for (_, xa), (_, xb) in zip(sa.axes, sb.axes):
             assert xa.t == xb.t and torch.allclose(xa.W, xb.W, rtol=1e-5, atol=1e-7)
