@@ -58,8 +58,11 @@ def orthonormal_special(rank: int, dim: int, dtype=torch.float32, device=None) -
 FUSED = os.environ.get("FDT_NGD_FUSED", "1") != "0"
 # one eigensolver launch per optimizer step for all update-step Z matrices (see Deferred)
 DEFER = os.environ.get("FDT_NGD_DEFER", "1") != "0"
-# steady-state optimizer steps replayed as HIP graphs (NGD._graph_step)
-GRAPHS = os.environ.get("FDT_NGD_GRAPHS", "1") != "0"
+# steady-state optimizer steps replayed as HIP graphs (NGD._graph_step).  Off by default:
+# measured on MI355X (profiles/r3/ngd_graphs.txt) a replay is no faster than the eager step
+# (ResNet-50 NGD+meta 30.4 vs 30.2-30.7 ms, transformer bs256 11.5 vs 11.4-12.2 ms) and slower
+# at batch 32 (5.39 vs 5.04 ms): the step is GPU-bound, not launch-bound.  FDT_NGD_GRAPHS=1
+GRAPHS = os.environ.get("FDT_NGD_GRAPHS", "0") == "1"
 
 
 def _fused_small_math(X, R) -> bool:

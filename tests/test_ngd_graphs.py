@@ -14,7 +14,7 @@ def _opt(cuda, graphs):
     m = nn.Sequential(nn.Conv2d(64, 64, 3), nn.Conv2d(64, 128, 1), nn.Linear(256, 512), nn.Linear(512, 96)).to(cuda)
     flat = FlatParams(m, device=cuda)
     opt = NGD(flat, lr=0.05, momentum=0.9, weight_decay=1e-4)
-    opt.graphs = graphs
+    opt.graphs = graphs  # (the graph path is opt-in: FDT_NGD_GRAPHS=1)
     return flat, opt
 
 
