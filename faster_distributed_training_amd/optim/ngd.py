@@ -351,7 +351,8 @@ class NGState:
         P, R, D = G.shape[0], self.rank, self.dim
         N = A * B
         nj = P * R * D if updating else 0
-        buf = torch.zeros(2 * P + nj + (P * R * R if updating else 0), device=G.device, dtype=torch.float32)
+        # (every output is assigned by ngd_small_sums, none accumulated: no zero fill)
+        buf = torch.empty(2 * P + nj + (P * R * R if updating else 0), device=G.device, dtype=torch.float32)
         sums = buf[:2 * P]
         ip, fp = sums[:P], sums[P:]
         J = buf[2 * P:2 * P + nj].view(P, R, D) if updating else None
@@ -405,7 +406,8 @@ class NGState:
         need_hh = updating and N <= D  # L = H^T H (else J W^T, a [R, D] x [D, R] product)
         nj = P * R * D if updating else 0
         nh = P * R * R if need_hh else 0
-        buf = torch.zeros(2 * P + nj + nh, device=G.device, dtype=torch.float32)
+        # (|X|^2, |Y|^2, J, H^T H are assigned by the fixed-order sum kernels: no zero fill)
+        buf = torch.empty(2 * P + nj + nh, device=G.device, dtype=torch.float32)
         ip = ip_in if ip_in is not None else buf[:P]
         fp = buf[P:2 * P]
         J = buf[2 * P:2 * P + nj].view(P, R, D) if updating else None
