@@ -22,7 +22,13 @@ dropped instead of shifting the alignment.  Columns (per step = totals / --steps
           ~0.3 ms, so it is not used as the cycle base)
   ldsc%   SQ_LDS_BANK_CONFLICT / SQ_LDS_IDX_ACTIVE
   roof%   max(bytes / 6.3 TB/s, FLOP / 2.5 PF) / measured time
-  GHz     GRBM_GUI_ACTIVE / 8 / kernel time, shown only for dispatches >= 0.3 ms
+  GHz     per-row clock: (GRBM_GUI_ACTIVE / 8 - fitted window overhead x calls) / the same
+          pass's kernel time.  GRBM_GUI_ACTIVE counts a counter window that opens before and
+          closes after each dispatch, so raw GRBM / time reads above the 2.4 GHz peak on short
+          dispatches; a least-squares fit of cycles = clock x time + overhead over every
+          dispatch of the GRBM pass gives the clock and the per-dispatch window overhead
+          (header line).  Shown to one decimal (the fit residual is a few 0.01 GHz) for rows
+          whose dispatches average >= 0.1 ms.
 
     python scripts/pmc_table.py gpurun_out/pmc_x_1024 --steps 4 [--out profiles/x.md]
 """
@@ -98,6 +104,25 @@ def load_pmc(d):
     return out
 
 
+def clock_fit(d):
+    """(clock Hz, window overhead cycles per dispatch, {key: same-pass kernel time}) from the
+    counter pass holding GRBM_GUI_ACTIVE, or None."""
+    import numpy as np
+    for p in sorted(glob.glob(os.path.join(d, "p*"))):
+        if not os.path.isdir(p):
+            continue
+        c = load_pmc(p)
+        if not any("GRBM_GUI_ACTIVE" in v for v in c.values()):
+            continue
+        t = load_time(p)
+        ks = [k for k, v in c.items() if k in t and "GRBM_GUI_ACTIVE" in v]
+        x = np.array([t[k] for k in ks])
+        y = np.array([c[k]["GRBM_GUI_ACTIVE"] / 8 for k in ks])
+        (a, b), *_ = np.linalg.lstsq(np.stack([x, np.ones_like(x)], 1), y, rcond=None)
+        return a, b, {k: t[k] for k in ks}
+    return None
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("dir")
@@ -111,6 +136,7 @@ def main():
         if os.path.isdir(p):
             for k, v in load_pmc(p).items():
                 ctr[k].update(v)
+    fit = clock_fit(a.dir)
     agg = collections.defaultdict(lambda: collections.Counter())
     for k, t in tm.items():
         name, grid, _ = k
@@ -122,6 +148,9 @@ def main():
             g["matched"] += 1
             for n, v in c.items():
                 g[n] += v
+            if fit and k in fit[2]:
+                g["t_grbm"] += fit[2][k]
+                g["n_grbm"] += 1
     S = a.steps
     rows = []
     tot_t = sum(g["t"] for g in agg.values()) / S
@@ -136,15 +165,24 @@ def main():
         flop = g["SQ_VALU_MFMA_BUSY_CYCLES"] * fpc / S
         mf = g["SQ_VALU_MFMA_BUSY_CYCLES"] / S / (t * PEAK_GHZ * 1e9 * 1024) if t else 0.0
         per_call = t / max(g["calls"] / S, 1e-9)
-        ghz = g["GRBM_GUI_ACTIVE"] / 8 / S / t * 1e-9 if (t and per_call >= 3e-4) else None
+        ghz = None
+        if fit and g["t_grbm"] and g["t_grbm"] / g["n_grbm"] >= 1e-4:
+            ghz = (g["GRBM_GUI_ACTIVE"] / 8 - fit[1] * g["n_grbm"]) / g["t_grbm"] * 1e-9
         ldsc = g["SQ_LDS_BANK_CONFLICT"] / g["SQ_LDS_IDX_ACTIVE"] if g["SQ_LDS_IDX_ACTIVE"] else 0.0
         roof = max((rd + wr) / HBM, flop / MFMA)
         rows.append((t, name + (" n" if narrow else ""), grid, g["calls"] / S, rd, wr, flop, mf, ldsc, roof, ghz))
     rows.sort(reverse=True)
     lines = [f"# per-kernel roofline ({a.dir}, {S} steps)", "",
+             "Eager launches (scripts/pmc_step.sh runs bench.py --no-graphs so each dispatch is "
+             "counted on its own); the graph-replayed step additionally folds the 1x1-conv "
+             "residual joins (FDT_JOIN_FOLD) and is a few % faster.", "",
              f"total kernel time {tot_t * 1e3:.3f} ms/step; rdGB = FETCH_SIZE x {f16:.2f} (calibrated 16-B stream; "
              f"'n' rows: x {fnar:.2f}, 64-B requests); TF/s = MFMA busy x {fpc:.0f}; mfma% at {PEAK_GHZ} GHz; "
              "roof% = max(bytes/6.3TB/s, FLOP/2.5PF)/time",
+             "",
+             (f"clock fit over {len(fit[2])} dispatches of the GRBM pass: {fit[0] * 1e-9:.3f} GHz + "
+              f"{fit[1]:.0f} cycles ({fit[1] / fit[0] * 1e6:.1f} us) of counter window per dispatch"
+              if fit else "no GRBM pass"),
              "",
              "| ms/step | calls | kernel | grid | rdGB | wrGB | TB/s | TF/s | mfma% | ldsc% | roof% | GHz |",
              "|---:|---:|---|---:|---:|---:|---:|---:|---:|---:|---:|---:|"]
@@ -154,7 +192,7 @@ def main():
     for t, name, grid, calls, rd, wr, flop, mf, ldsc, roof, ghz in rows[: a.top]:
         lines.append(f"| {t * 1e3:.3f} | {calls:.1f} | `{name}` | {grid} | {rd / 1e9:.3f} | {wr / 1e9:.3f} | "
                      f"{(rd + wr) / t / 1e12:.2f} | {flop / t / 1e12:.0f} | {mf * 100:.1f} | {ldsc * 100:.1f} | "
-                     f"{roof / t * 100:.0f} | {'—' if ghz is None else f'{ghz:.2f}'} |")
+                     f"{roof / t * 100:.0f} | {'—' if ghz is None else f'{ghz:.1f}'} |")
     lines += ["", f"sum of per-kernel roofline bounds {sum_roof * 1e3:.3f} ms/step vs measured {tot_t * 1e3:.3f} ms/step "
               f"({sum_roof / tot_t * 100:.0f} % of roofline overall)"]
     txt = "\n".join(lines)
