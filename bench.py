@@ -117,6 +117,7 @@ def main():
     for _ in range(args.steps):
         x, y = next(it)
         tr.train_step(x, y)
+    host = time.perf_counter() - t0  # host submission time of the K steps (no sync inside)
     sync()
     elapsed = time.perf_counter() - t0
     if dist.is_initialized():
@@ -144,6 +145,7 @@ def main():
                    "optimizer": "ngd" if args.ngd else args.optimizer, "mixup": "meta" if args.meta_learning else "input",
                    "native_kernels": native, "hip_graphs": graphs, "deterministic": args.deterministic},
         "epoch_time_s": round(50000.0 / value, 3),
+        "host_ms_per_step": round(host / args.steps * 1e3, 3),
         "peak_mem_gb": round(torch.cuda.max_memory_allocated() / 2**30, 2) if cuda else None,
     }
     _sharding_fields(tr, rec)
@@ -213,6 +215,7 @@ def bench_transformer(args):
     t0 = time.perf_counter()
     for _ in range(args.steps):
         tr.train_step(*next(it))
+    host = time.perf_counter() - t0
     sync()
     elapsed = time.perf_counter() - t0
     if dist.is_initialized():
@@ -228,7 +231,8 @@ def bench_transformer(args):
            "config": {"model": "transformer 6x512 (vocab 30522)", "global_batch": gb, "seq_len": list(buckets),
                       "truncation": "none (pad to the smallest bucket >= the batch's longest sample)",
                       "parallelism": f"{'fsdp' if args.fsdp else 'dp'}{world}", "optimizer": "ngd"},
-           "peak_mem_gb": round(torch.cuda.max_memory_allocated() / 2**30, 2) if cuda else None}
+           "peak_mem_gb": round(torch.cuda.max_memory_allocated() / 2**30, 2) if cuda else None,
+           "host_ms_per_step": round(host / args.steps * 1e3, 3)}
     _sharding_fields(tr, rec)
     if tr.rank == 0:
         print(json.dumps(rec), flush=True)

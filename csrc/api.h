@@ -118,6 +118,10 @@ void dropout_bwd(uint64_t g, uint64_t gy, long n, float p, uint64_t seed, uint64
 void gelu_dropout_fwd(uint64_t a, uint64_t h, long n, float p, uint64_t seed, uint64_t seed_ptr, uint64_t stream);
 void gelu_dropout_bwd(uint64_t g, uint64_t a, uint64_t ga, long n, float p, uint64_t seed, uint64_t seed_ptr,
                       uint64_t stream);
+void dropout_bwd_colsum(uint64_t g, uint64_t gy, uint64_t gb, long rows, int cols, float p, uint64_t seed,
+                        uint64_t seed_ptr, uint64_t stream);
+void gelu_dropout_bwd_colsum(uint64_t g, uint64_t a, uint64_t ga, uint64_t gb, long rows, int cols, float p,
+                             uint64_t seed, uint64_t seed_ptr, uint64_t stream);
 // ngd.hip
 void ngd_sumsq(uint64_t X, long per, int G, uint64_t out, uint64_t stream);
 bool ngd_small_supported(int D, int R);

@@ -144,7 +144,76 @@ __global__ __launch_bounds__(256) void gelu_dropout_bwd_kernel(const bf16* __res
   }
 }
 
+// The two backward passes above with the bias gradient of the linear layer that PRODUCED the
+// dropout input folded in: gb[c] += sum over rows of the stored gradient (what a separate
+// colsum pass would re-read from HBM).  2-D layout: a block is 32 column groups (8 columns,
+// one 16-B vector each) x 8 row lanes over a chunk of rows; element e = r*cols + c0 keeps
+// the forward's hash index (chunk e/8), so the masks are the grid-stride kernels' masks.
+// KIND 0: g fp32 -> gy = keep*g*scale (bf16);  KIND 1: g, a bf16 -> ga = keep*g*scale*gelu'(a).
+template <int KIND>
+__global__ __launch_bounds__(256) void dropout_bwd_colsum_kernel(const void* __restrict__ gin,
+                                                                 const bf16* __restrict__ a, bf16* __restrict__ out,
+                                                                 float* __restrict__ gb, long rows, int cols,
+                                                                 int rows_per_blk, uint32_t thr, float scale,
+                                                                 uint64_t seed, const uint64_t* seed_ptr) {
+  __shared__ float red[256 * 8];
+  const uint64_t s = live_seed(seed, seed_ptr);
+  const int lanes = min(cols / 8 - (int)blockIdx.x * 32, 32);
+  const int cg = threadIdx.x % 32, rl = threadIdx.x / 32;
+  const long r0 = (long)blockIdx.y * rows_per_blk;
+  const long r1 = min(rows, r0 + rows_per_blk);
+  const int c0 = (blockIdx.x * 32 + cg) * 8;
+  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if (cg < lanes) {
+    for (long r = r0 + rl; r < r1; r += 8) {
+      const long c = (r * cols + c0) >> 3;  // 16-B chunk index = the forward's hash index
+      const uint32_t m = thr ? keep8(c, s, thr) : 0xffu;
+      float f[8];
+      if constexpr (KIND == 0) {
+        const float4 g0 = reinterpret_cast<const float4*>(gin)[2 * c];
+        const float4 g1 = reinterpret_cast<const float4*>(gin)[2 * c + 1];
+        const float gf[8] = {g0.x, g0.y, g0.z, g0.w, g1.x, g1.y, g1.z, g1.w};
+#pragma unroll
+        for (int j = 0; j < 8; ++j) f[j] = (m >> j) & 1 ? gf[j] * scale : 0.f;
+      } else {
+        float fa[8];
+        unpack8(reinterpret_cast<const uint4*>(a)[c], fa);
+        unpack8(reinterpret_cast<const uint4*>(gin)[c], f);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) f[j] = (m >> j) & 1 ? f[j] * scale * gelu_erf_grad(fa[j]) : 0.f;
+      }
+      const uint4 o = pack8(f);
+      reinterpret_cast<uint4*>(out)[c] = o;
+      // the bias gradient sums the STORED (bf16-rounded) values, as a colsum pass would
+      float q[8];
+      unpack8(o, q);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[j] += q[j];
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) red[(rl * 32 + cg) * 8 + j] = acc[j];
+  __syncthreads();
+  const int col = threadIdx.x;  // cg * 8 + j
+  if (col / 8 < lanes) {
+    float t = 0.f;
+#pragma unroll
+    for (int l = 0; l < 8; ++l) t += red[(l * 32 + col / 8) * 8 + (col % 8)];
+    atomicAdd(gb + blockIdx.x * 256 + col, t);
+  }
+}
+
 unsigned grid_for(long n8) { return (unsigned)std::max<long>(1, std::min<long>((n8 + 255) / 256, 4096)); }
+
+// ~1024 workgroups over (column blocks x row chunks), >= 64 rows (8 per row lane) per block
+dim3 colsum_grid(long rows, int cols, int* rpb_out) {
+  const int cblk = (cols / 8 + 31) / 32;
+  long rpb = rows * cblk / 1024;
+  if (rpb < 64) rpb = 64;
+  rpb = (rpb + 7) / 8 * 8;
+  *rpb_out = (int)rpb;
+  return dim3((unsigned)cblk, (unsigned)((rows + rpb - 1) / rpb));
+}
 
 uint32_t threshold(float p) {
   FDT_CHECK(p >= 0.f && p < 1.f, "dropout: p in [0, 1)");
@@ -168,6 +237,32 @@ void dropout_bwd(uint64_t g, uint64_t gy, long n, float p, uint64_t seed, uint64
   if (n == 0) return;
   dropout_bwd_kernel<<<grid_for(n / 8), 256, 0, as_stream(stream)>>>(
       P<const float>(g), P<bf16>(gy), n / 8, threshold(p), 1.f / (1.f - p), seed, P<const uint64_t>(seed_ptr));
+  FDT_LAUNCH_CHECK();
+}
+
+void dropout_bwd_colsum(uint64_t g, uint64_t gy, uint64_t gb, long rows, int cols, float p, uint64_t seed,
+                        uint64_t seed_ptr, uint64_t stream) {
+  FDT_CHECK(cols % 8 == 0 && g % 16 == 0 && gy % 16 == 0 && gb % 4 == 0 && gb != 0,
+            "dropout_bwd_colsum: cols % 8, 16-B aligned rows, fp32 bias gradient");
+  if (rows == 0) return;
+  int rpb;
+  const dim3 grid = colsum_grid(rows, cols, &rpb);
+  dropout_bwd_colsum_kernel<0><<<grid, 256, 0, as_stream(stream)>>>(
+      P<const void>(g), nullptr, P<bf16>(gy), P<float>(gb), rows, cols, rpb, threshold(p), 1.f / (1.f - p), seed,
+      P<const uint64_t>(seed_ptr));
+  FDT_LAUNCH_CHECK();
+}
+
+void gelu_dropout_bwd_colsum(uint64_t g, uint64_t a, uint64_t ga, uint64_t gb, long rows, int cols, float p,
+                             uint64_t seed, uint64_t seed_ptr, uint64_t stream) {
+  FDT_CHECK(cols % 8 == 0 && g % 16 == 0 && a % 16 == 0 && ga % 16 == 0 && gb % 4 == 0 && gb != 0,
+            "gelu_dropout_bwd_colsum: cols % 8, 16-B aligned rows, fp32 bias gradient");
+  if (rows == 0) return;
+  int rpb;
+  const dim3 grid = colsum_grid(rows, cols, &rpb);
+  dropout_bwd_colsum_kernel<1><<<grid, 256, 0, as_stream(stream)>>>(
+      P<const void>(g), P<const bf16>(a), P<bf16>(ga), P<float>(gb), rows, cols, rpb, threshold(p), 1.f / (1.f - p),
+      seed, P<const uint64_t>(seed_ptr));
   FDT_LAUNCH_CHECK();
 }
 

@@ -18,10 +18,12 @@
 #include <pybind11/stl.h>
 
 #include <cstring>
+#include <memory>
 #include <stdexcept>
 #include <string>
 #include <vector>
 
+#include "ordered_worker.h"
 #include "runtime_api.h"
 
 namespace py = pybind11;
@@ -42,13 +44,15 @@ class PinnedPrefetcher {
     RT_CHECK(hipStreamCreateWithFlags(&copy_stream_, hipStreamNonBlocking));
     slots_.resize(nslots, nullptr);
     events_.resize(nslots, nullptr);
-    used_.resize(nslots, false);
+    used_.resize(nslots, 0);
+    slot_seq_.resize(nslots, 0);
     for (int i = 0; i < nslots; ++i) {
       RT_CHECK(hipHostMalloc(&slots_[i], slot_bytes_, hipHostMallocDefault));
       RT_CHECK(hipEventCreateWithFlags(&events_[i], hipEventDisableTiming));
     }
   }
   ~PinnedPrefetcher() {
+    worker_.reset();  // drains the queued jobs, joins the thread
     hipSetDevice(device_);
     if (copy_stream_) hipStreamSynchronize(copy_stream_);
     for (auto e : events_) if (e) hipEventDestroy(e);
@@ -69,7 +73,7 @@ class PinnedPrefetcher {
       std::memcpy(slots_[s], reinterpret_cast<const void*>(src), nbytes);
       RT_CHECK(hipMemcpyAsync(reinterpret_cast<void*>(dst), slots_[s], nbytes, hipMemcpyHostToDevice, copy_stream_));
       RT_CHECK(hipEventRecord(events_[s], copy_stream_));
-      used_[s] = true;
+      used_[s] = 1;
     }
     return s;
   }
@@ -94,50 +98,88 @@ class PinnedPrefetcher {
         off += (sizes[i] + 255) / 256 * 256;
       }
       RT_CHECK(hipEventRecord(events_[s], copy_stream_));
-      used_[s] = true;
+      used_[s] = 1;
     }
     return s;
   }
 
-  // Make `compute_stream` wait for slot `s`'s H2D copy (no host blocking).
+  // Background form of stage_many: queue the job (slot-reuse wait, memcpy into the pinned
+  // slot, H2D enqueue) to the worker thread and return the slot at once.  `wait_event`
+  // (a hipEvent_t, or 0) is waited on by the copy stream before the H2D: the compute
+  // stream's release of the slot's device buffer.  The caller keeps the source arrays and
+  // the event alive until wait(s) returned.
+  int submit(const std::vector<uint64_t>& srcs, const std::vector<size_t>& sizes, const std::vector<uint64_t>& dsts,
+             uint64_t wait_event) {
+    if (srcs.size() != sizes.size() || srcs.size() != dsts.size())
+      throw std::runtime_error("PinnedPrefetcher.submit: srcs / sizes / dsts lengths differ");
+    size_t total = 0;
+    for (auto n : sizes) total += (n + 255) / 256 * 256;
+    if (total > slot_bytes_) throw std::runtime_error("PinnedPrefetcher: batch larger than slot");
+    const int s = next_;
+    next_ = (next_ + 1) % (int)slots_.size();
+    if (!worker_) worker_ = std::make_unique<OrderedWorker<Job>>([this](Job& j) { issue(j); });
+    slot_seq_[s] = worker_->submit(Job{s, srcs, sizes, dsts, wait_event});
+    return s;
+  }
+
+  // Make `compute_stream` wait for slot `s`'s H2D copy (no host blocking on the copy; with
+  // submit() the call first waits, GIL released, until the worker has issued slot s's job).
   void wait(int s, uint64_t compute_stream) {
+    if (s < 0 || s >= (int)slots_.size()) throw std::runtime_error("PinnedPrefetcher.wait: bad slot");
+    if (worker_) {
+      py::gil_scoped_release nogil;
+      worker_->wait_issued(slot_seq_[s]);
+    }
     RT_CHECK(hipStreamWaitEvent(reinterpret_cast<hipStream_t>(compute_stream), events_.at(s), 0));
   }
-  void synchronize() { RT_CHECK(hipStreamSynchronize(copy_stream_)); }
+  uint64_t submitted() const { return worker_ ? worker_->submitted() : 0; }
+  void synchronize() {
+    if (worker_) {
+      py::gil_scoped_release nogil;
+      worker_->drain();
+    }
+    RT_CHECK(hipStreamSynchronize(copy_stream_));
+  }
   uint64_t copy_stream() const { return reinterpret_cast<uint64_t>(copy_stream_); }
   size_t slot_bytes() const { return slot_bytes_; }
   int num_slots() const { return (int)slots_.size(); }
 
  private:
+  struct Job {
+    int slot;
+    std::vector<uint64_t> srcs;
+    std::vector<size_t> sizes;
+    std::vector<uint64_t> dsts;
+    uint64_t wait_event;
+  };
+
+  // runs on the worker thread, jobs in submission order (the copy stream sees that order)
+  void issue(Job& j) {
+    RT_CHECK(hipSetDevice(device_));
+    if (j.wait_event) RT_CHECK(hipStreamWaitEvent(copy_stream_, reinterpret_cast<hipEvent_t>(j.wait_event), 0));
+    if (used_[j.slot]) RT_CHECK(hipEventSynchronize(events_[j.slot]));  // pinned slot's last H2D done
+    size_t off = 0;
+    char* base = static_cast<char*>(slots_[j.slot]);
+    for (size_t i = 0; i < j.srcs.size(); ++i) {
+      std::memcpy(base + off, reinterpret_cast<const void*>(j.srcs[i]), j.sizes[i]);
+      RT_CHECK(hipMemcpyAsync(reinterpret_cast<void*>(j.dsts[i]), base + off, j.sizes[i], hipMemcpyHostToDevice,
+                              copy_stream_));
+      off += (j.sizes[i] + 255) / 256 * 256;
+    }
+    RT_CHECK(hipEventRecord(events_[j.slot], copy_stream_));
+    used_[j.slot] = 1;
+  }
+
   int device_;
   size_t slot_bytes_;
   hipStream_t copy_stream_ = nullptr;
   std::vector<void*> slots_;
   std::vector<hipEvent_t> events_;
-  std::vector<bool> used_;
+  std::vector<char> used_;           // (not vector<bool>: the worker thread writes it)
   int next_ = 0;
+  std::vector<uint64_t> slot_seq_;   // worker sequence number of the job last submitted per slot
+  std::unique_ptr<OrderedWorker<Job>> worker_;  // background mode (submit); one mode per prefetcher
 };
-
-// sizes: bytes per parameter in REGISTRATION order.  Returns buckets as lists of
-// parameter indices, in the order they become ready in backward (reverse order).
-std::vector<std::vector<int>> plan_buckets(const std::vector<size_t>& sizes, size_t first_cap, size_t cap) {
-  std::vector<std::vector<int>> buckets;
-  std::vector<int> cur;
-  size_t acc = 0;
-  size_t limit = first_cap;
-  for (int i = (int)sizes.size() - 1; i >= 0; --i) {
-    cur.push_back(i);
-    acc += sizes[i];
-    if (acc >= limit) {
-      buckets.push_back(cur);
-      cur.clear();
-      acc = 0;
-      limit = cap;
-    }
-  }
-  if (!cur.empty()) buckets.push_back(cur);
-  return buckets;
-}
 
 // Device properties needed by the Python side without initialising torch.cuda.
 py::dict device_info(int device) {
@@ -158,6 +200,9 @@ void register_runtime(py::module_& m) {
       .def(py::init<int, size_t, int>(), py::arg("device"), py::arg("slot_bytes"), py::arg("nslots") = 3)
       .def("stage", &PinnedPrefetcher::stage)
       .def("stage_many", &PinnedPrefetcher::stage_many)
+      .def("submit", &PinnedPrefetcher::submit, py::arg("srcs"), py::arg("sizes"), py::arg("dsts"),
+           py::arg("wait_event") = 0)
+      .def_property_readonly("submitted", &PinnedPrefetcher::submitted)
       .def("wait", &PinnedPrefetcher::wait)
       .def("synchronize", &PinnedPrefetcher::synchronize)
       .def_property_readonly("copy_stream", &PinnedPrefetcher::copy_stream)

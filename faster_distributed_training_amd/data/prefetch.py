@@ -5,9 +5,13 @@ Reference: ``DataLoaderX`` (prefetch_generator.BackgroundGenerator) + ``pin_memo
 transformer_test.py:68-70,106-138,242-245).
 
 MI355X design: the native ``PinnedPrefetcher`` (csrc/runtime/runtime.cpp) owns a ring of
-pinned host slots (hipHostMalloc) and a non-blocking HIP copy stream; ``stage_many``
-memcpy's a host batch into a free pinned slot with the GIL released and enqueues the
-``hipMemcpyAsync`` H2D on the copy stream.  This module adds the device half of the ring:
+pinned host slots (hipHostMalloc), a non-blocking HIP copy stream and a C++ worker thread;
+``submit`` queues a host batch to the worker, which waits for the slot's previous H2D,
+memcpy's the batch into the pinned slot and enqueues the ``hipMemcpyAsync`` on the copy
+stream -- the training thread never does the copy (the reference's pin-memory thread).
+The host half of a batch (the numpy gather) runs ahead in a Python background thread
+(``StagedIterator``, the reference's ``BackgroundGenerator``).  This module adds the device
+half of the ring:
 
 * one device buffer per slot, so a staged batch is never overwritten while the compute
   stream still reads it: before the copy into slot ``s`` the copy stream waits on the
@@ -18,9 +22,12 @@ memcpy's a host batch into a free pinned slot with the GIL released and enqueues
 
 Loaders stage batch k+1 before handing out batch k (``StagedIterator``), so with 3 slots
 the copy of the next batch, the step on the current one and the host gather of the one
-after overlap.  Nothing here ever does a pageable ``.to(device)``.
+after (background thread) overlap.  Nothing here ever does a pageable ``.to(device)``.
 """
 from __future__ import annotations
+
+import queue
+import threading
 
 import numpy as np
 import torch
@@ -54,17 +61,18 @@ class PinnedStager:
         self.copy_stream.wait_event(ev)
         self.next = 0
         self.staged = 0  # batches staged (tests / diagnostics)
+        self._keep: list = [None] * nslots  # sources + release event alive until the job is issued
 
     def stage(self, arrays):
         """Copy host arrays (numpy or CPU tensors) to the device through the next slot.
         Returns (slot, [device tensors with the arrays' dtypes and shapes]); the tensors
-        may be read on the compute stream only after ``acquire(slot)``."""
+        may be read on the compute stream only after ``acquire(slot)``.  The copy itself is
+        done by the native worker thread (``PinnedPrefetcher.submit``); the copy stream first
+        waits for the slot's previous readers (their release event)."""
         s = self.next
         self.next = (s + 1) % self.nslots
         ev = self.released[s]
-        if ev is not None:
-            self.copy_stream.wait_event(ev)  # the slot's previous readers are done
-        srcs, sizes, dsts, outs, keep = [], [], [], [], []
+        srcs, sizes, dsts, outs, keep = [], [], [], [], [ev]
         off = 0
         for a in arrays:
             t = torch.from_numpy(np.ascontiguousarray(a)) if isinstance(a, np.ndarray) else a.contiguous()
@@ -78,14 +86,17 @@ class PinnedStager:
             dsts.append(self.dev[s].data_ptr() + off)
             outs.append(self.dev[s][off:off + n].view(t.dtype).view(t.shape))
             off += _aligned(n)
-        got = self.pf.stage_many(srcs, sizes, dsts)  # memcpy to pinned (GIL released) + async H2D
+        got = self.pf.submit(srcs, sizes, dsts, ev.cuda_event if ev is not None else 0)
         assert got == s, (got, s)
+        self._keep[s] = keep
         self.staged += 1
         return s, outs
 
     def acquire(self, s: int):
-        """Order the current compute stream after slot ``s``'s H2D copy (device-side wait)."""
+        """Order the current compute stream after slot ``s``'s H2D copy (device-side wait; the
+        host only waits for the worker to have ISSUED the copy)."""
         self.pf.wait(s, _native.stream_ptr(self.device))
+        self._keep[s] = None
 
     def release(self, s: int):
         """Every compute-stream reader of slot ``s`` has been enqueued: the next copy into
@@ -98,29 +109,85 @@ class PinnedStager:
         self.pf.synchronize()
 
 
+class _Producer:
+    """Background host producer (the reference's ``prefetch_generator.BackgroundGenerator``):
+    a daemon thread computes ``host(b)`` for b = 0..nb-1 in order into a bounded queue
+    (``depth`` batches ahead); numpy's gathers release the GIL, so they overlap the training
+    thread's kernel launches.  Exceptions are re-raised in the consumer."""
+
+    _END = object()
+
+    def __init__(self, host, nb: int, depth: int = 2):
+        self.q: queue.Queue = queue.Queue(maxsize=depth)
+        self.stop = threading.Event()
+        self.t = threading.Thread(target=self._run, args=(host, nb), daemon=True, name="fdt-host-producer")
+        self.t.start()
+
+    def _put(self, x) -> bool:
+        while not self.stop.is_set():
+            try:
+                self.q.put(x, timeout=0.1)
+                return True
+            except queue.Full:
+                continue
+        return False
+
+    def _run(self, host, nb):
+        try:
+            for b in range(nb):
+                if not self._put((None, host(b))):
+                    return
+            self._put((None, self._END))
+        except BaseException as e:  # noqa: BLE001 -- handed to the consumer
+            self._put((e, None))
+
+    def get(self):
+        err, item = self.q.get()
+        if err is not None:
+            raise err
+        return item
+
+    def close(self):
+        self.stop.set()
+        try:
+            while True:
+                self.q.get_nowait()
+        except queue.Empty:
+            pass
+        self.t.join(timeout=5)
+
+
 class StagedIterator:
-    """Runs ``host(b) -> (arrays, meta)`` + ``stage`` one batch ahead of
-    ``device(arrays, meta) -> batch``.
+    """Runs ``host(b) -> (arrays, meta)`` in a background thread and ``stage`` one batch ahead
+    of ``device(arrays, meta) -> batch``.
 
     ``host`` builds batch b's host arrays (gather/pad in numpy) plus host-side metadata
-    (e.g. the padded length); ``device`` turns the staged device tensors into the batch
-    the trainer consumes (gathers, casts, GPU augmentation) on the compute stream."""
+    (e.g. the padded length) -- it must be a pure function of b (it runs on another thread);
+    ``device`` turns the staged device tensors into the batch the trainer consumes (gathers,
+    casts, GPU augmentation) on the compute stream.  ``background=False``: host(b) inline."""
 
-    def __init__(self, stager: PinnedStager, nb: int, host, device):
+    def __init__(self, stager: PinnedStager, nb: int, host, device, background: bool = True, depth: int = 2):
         self.stager, self.nb, self.host, self.device = stager, nb, host, device
-
-    def _stage(self, b):
-        arrays, meta = self.host(b)
-        return self.stager.stage(arrays), meta
+        self.background, self.depth = background, depth
 
     def __iter__(self):
         st = self.stager
-        pending = self._stage(0) if self.nb > 0 else None
-        for b in range(self.nb):
-            nxt = self._stage(b + 1) if b + 1 < self.nb else None  # in flight during step b
-            (s, arrs), meta = pending
-            st.acquire(s)
-            out = self.device(arrs, meta)
-            st.release(s)
-            yield out
-            pending = nxt
+        prod = _Producer(self.host, self.nb, self.depth) if (self.background and self.nb > 1) else None
+
+        def stage(b):
+            arrays, meta = prod.get() if prod is not None else self.host(b)
+            return st.stage(arrays), meta
+
+        try:
+            pending = stage(0) if self.nb > 0 else None
+            for b in range(self.nb):
+                nxt = stage(b + 1) if b + 1 < self.nb else None  # in flight during step b
+                (s, arrs), meta = pending
+                st.acquire(s)
+                out = self.device(arrs, meta)
+                st.release(s)
+                yield out
+                pending = nxt
+        finally:
+            if prod is not None:
+                prod.close()

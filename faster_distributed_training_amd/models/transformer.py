@@ -166,9 +166,12 @@ class PositionalWiseFFN(nn.Module):
         self.w_2 = nn.Linear(d_ff, d_model)
         self.dropout = nn.Dropout(dropout)
 
-    def forward(self, x):
-        h = gelu_dropout(linear(x, self.w_1.weight, self.w_1.bias), self.dropout.p, self.training)
-        return linear(h, self.w_2.weight, self.w_2.bias)
+    def forward(self, x, fuse_out_bias=False):
+        """``fuse_out_bias``: the caller's dropout_add computes w_2's bias gradient (ops/dropout.py
+        ``bias=``); w_1's is always computed inside the GELU-dropout backward."""
+        h = gelu_dropout(linear(x, self.w_1.weight, self.w_1.bias, bias_grad=False), self.dropout.p, self.training,
+                         bias=self.w_1.bias)
+        return linear(h, self.w_2.weight, self.w_2.bias, bias_grad=not fuse_out_bias)
 
 
 class MultiheadAttention(nn.Module):
@@ -187,19 +190,23 @@ class MultiheadAttention(nn.Module):
         self.faithful = faithful
         self.attn = None
 
-    def forward(self, query, key, value, mask=None):
+    def forward(self, query, key, value, mask=None, fuse_out_bias=False):
+        """``fuse_out_bias``: the caller's dropout_add computes the output projection's bias
+        gradient (ops/dropout.py ``bias=``)."""
         b, L, _ = query.shape
         if query is key and key is value:
             qkv = linear_cat(query, [l.weight for l in self.heads], [l.bias for l in self.heads])
             qkv = qkv.view(b, L, 3, self.h, self.d_k)
             p = self.dropout.p if self.training else 0.0
             x = packed_attention(qkv, mask, dropout_p=p, mask_value=(-1e-9 if self.faithful else None))
-            return linear(x.reshape(b, L, self.h * self.d_k), self.output.weight, self.output.bias)
+            return linear(x.reshape(b, L, self.h * self.d_k), self.output.weight, self.output.bias,
+                          bias_grad=not fuse_out_bias)
         q, k, v = [l(t).view(b, -1, self.h, self.d_k) for l, t in zip(self.heads, (query, key, value))]
         p = self.dropout.p if self.training else 0.0
         x = scaled_dot_product_attention(q, k, v, mask, dropout_p=p,
                                          mask_value=(-1e-9 if self.faithful else None))
-        return linear(x.reshape(b, L, self.h * self.d_k), self.output.weight, self.output.bias)
+        return linear(x.reshape(b, L, self.h * self.d_k), self.output.weight, self.output.bias,
+                      bias_grad=not fuse_out_bias)
 
 
 class LayerNorm(nn.Module):
@@ -225,8 +232,8 @@ class sublayerConnectionAttention(nn.Module):  # noqa: N801 (reference name)
     def forward(self, x, mask=None):
         res = ResidualGrad()  # skip gradient handed to the LayerNorm backward (no add pass)
         y = self.layernorm(x, res)
-        y = self.multiheads(y, y, y, mask)
-        return dropout_add(y, x, self.dropout.p, self.training, res)
+        y = self.multiheads(y, y, y, mask, fuse_out_bias=True)
+        return dropout_add(y, x, self.dropout.p, self.training, res, bias=self.multiheads.output.bias)
 
 
 class sublayerConnectionFFN(nn.Module):  # noqa: N801 (reference name)
@@ -238,7 +245,8 @@ class sublayerConnectionFFN(nn.Module):  # noqa: N801 (reference name)
 
     def forward(self, x):
         res = ResidualGrad()
-        return dropout_add(self.ffn(self.layernorm(x, res)), x, self.dropout.p, self.training, res)
+        y = self.ffn(self.layernorm(x, res), fuse_out_bias=True)
+        return dropout_add(y, x, self.dropout.p, self.training, res, bias=self.ffn.w_2.bias)
 
 
 class Classifier(nn.Module):

@@ -144,7 +144,7 @@ def bias_grad(gy: torch.Tensor) -> torch.Tensor:
 
 class _Linear(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, w, b, dt):
+    def forward(ctx, x, w, b, dt, bias_grad=True):
         xin_dtype = x.dtype
         xc = x.to(dt)
         wc = cast_weight(w, dt)
@@ -152,6 +152,7 @@ class _Linear(torch.autograd.Function):
         ctx.save_for_backward(xc, wc)
         ctx.meta = (xin_dtype, w.dtype, None if b is None else b.dtype)
         ctx.params = (w, b)  # leaves whose gradient may be written in place (direct_target)
+        ctx.bias_grad = bias_grad
         return y
 
     @staticmethod
@@ -171,26 +172,30 @@ class _Linear(torch.autograd.Function):
                 mark_ready(w)
             else:
                 dw = wgrad(g2, x2).to(wd)
-        if bd is not None and ctx.needs_input_grad[2]:
+        if bd is not None and ctx.needs_input_grad[2] and ctx.bias_grad:
             tgt = direct_target(b)
             if tgt is not None:
                 bias_grad_into(g2, tgt)
                 mark_ready(b)
             else:
                 db = bias_grad(g2).to(bd)
-        return dx, dw, db, None
+        return dx, dw, db, None, None
 
 
-def linear(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor | None = None) -> torch.Tensor:
+def linear(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor | None = None,
+           bias_grad: bool = True) -> torch.Tensor:
     """``F.linear`` semantics (incl. autocast's compute dtype) with the split-K weight
-    gradient on the GPU; plain ``F.linear`` elsewhere (CPU, fp32 compute)."""
+    gradient on the GPU; plain ``F.linear`` elsewhere (CPU, fp32 compute).
+    ``bias_grad=False``: the bias is added but its gradient is left to the consumer of the
+    output (ops/dropout.py ``bias=``: the column sums fused into the dropout backward)."""
+    b_fwd = bias if (bias_grad or bias is None) else bias.detach()
     if not x.is_cuda:
-        return F.linear(x, weight, bias)
+        return F.linear(x, weight, b_fwd)
     dt = torch.get_autocast_dtype("cuda") if torch.is_autocast_enabled("cuda") else x.dtype
     if dt not in (torch.bfloat16, torch.float16) or x.numel() // x.shape[-1] < 4096:
-        return F.linear(x, weight, bias)
+        return F.linear(x, weight, b_fwd)
     with torch.autocast("cuda", enabled=False):
-        return _Linear.apply(x, weight, bias, dt)
+        return _Linear.apply(x, weight, bias, dt, bias_grad)
 
 
 class _LinearCat(torch.autograd.Function):

@@ -96,7 +96,13 @@ class BucketReducer:
                 self.bucket_of[id(flat.slots[i].param)] = b
         self.pending = [len(idx) for (_, _, idx) in self.buckets]
         self.works = [None] * len(self.buckets)
-        self.tmp = [None] * len(self.buckets)
+        # reduced-precision wire format: ONE persistent buffer shaped like the flat gradient,
+        # each bucket a view of it (no per-step allocation; the cast in and out are the only
+        # extra passes)
+        self.wire = None
+        if comm_dtype is not None and comm_dtype != flat.grad.dtype:
+            self.wire = torch.empty(flat.numel, device=flat.grad.device, dtype=comm_dtype)
+        self.cast = [False] * len(self.buckets)
         from ..ops.resnet_fused import register_grad_ready_hook
         # autograd-managed params fire the post-accumulate hook; params whose gradient the
         # fused ResNet engine writes directly fire the engine's grad-ready hook
@@ -132,9 +138,10 @@ class BucketReducer:
             return
         s, e, _ = self.buckets[b]
         view = self.flat.grad[s:e]
-        if self.comm_dtype is not None and self.comm_dtype != view.dtype:
-            buf = view.to(self.comm_dtype)
-            self.tmp[b] = buf
+        if self.wire is not None:
+            buf = self.wire[s:e]
+            buf.copy_(view)
+            self.cast[b] = True
         else:
             buf = view
         op = dist.ReduceOp.AVG if self.use_avg else dist.ReduceOp.SUM
@@ -148,9 +155,9 @@ class BucketReducer:
         for b, w in enumerate(self.works):
             w.wait()
             s, e, _ = self.buckets[b]
-            if self.tmp[b] is not None:
-                self.flat.grad[s:e].copy_(self.tmp[b])
-                self.tmp[b] = None
+            if self.cast[b]:
+                self.flat.grad[s:e].copy_(self.wire[s:e])
+                self.cast[b] = False
             if not self.use_avg:
                 self.flat.grad[s:e].div_(self.ws)
         self.works = [None] * len(self.buckets)

@@ -21,19 +21,24 @@ def _batch(rank, n=8):
     return torch.randn(n, 10, generator=g), torch.randint(0, 4, (n,), generator=g)
 
 
-def _ddp_worker(rank, world, bucket_mb):
+def _ddp_worker(rank, world, bucket_mb, wire=None):
     from faster_distributed_training_amd.parallel.ddp import BucketReducer
     from faster_distributed_training_amd.utils.flat import FlatParams
     m = _model(seed=rank)  # different init per rank: the reducer must broadcast rank 0's
     flat = FlatParams(m)
-    red = BucketReducer(flat, m, bucket_mb=bucket_mb, first_bucket_mb=bucket_mb / 4)
+    red = BucketReducer(flat, m, bucket_mb=bucket_mb, first_bucket_mb=bucket_mb / 4, comm_dtype=wire)
     ref = _model(seed=0)
     for p, q in zip(m.parameters(), ref.parameters()):
         assert torch.equal(p, q)
     assert len(red.buckets) >= 2
-    x, y = _batch(rank)
-    F.cross_entropy(m(x), y).backward()
-    red.finish()
+    wire_buf = red.wire
+    for _ in range(2):  # the persistent wire buffer is reused, never reallocated
+        for p in m.parameters():
+            p.grad.zero_()
+        x, y = _batch(rank)
+        F.cross_entropy(m(x), y).backward()
+        red.finish()
+        assert red.wire is wire_buf
     # reference: average of every rank's local gradient on the same (rank-0) weights
     grads = []
     for r in range(world):
@@ -42,13 +47,21 @@ def _ddp_worker(rank, world, bucket_mb):
         F.cross_entropy(ref(xr), yr).backward()
         grads.append([p.grad.clone() for p in ref.parameters()])
     for i, p in enumerate(m.parameters()):
-        avg = sum(g[i] for g in grads) / world
-        assert torch.allclose(p.grad, avg, atol=1e-6), i
+        if wire is None:
+            avg = sum(g[i] for g in grads) / world
+            assert torch.allclose(p.grad, avg, atol=1e-6), i
+        else:  # each rank's gradient rounded to the wire format, summed in it, averaged
+            avg = sum(g[i].to(wire).float() for g in grads) / world
+            assert torch.allclose(p.grad, avg, rtol=2e-2, atol=1e-3), i
 
 
 @pytest.mark.parametrize("world", [2, 3])
 def test_bucket_reducer_averages_gradients(world):
     run_world(_ddp_worker, world=world, args=(0.0005,))
+
+
+def test_bucket_reducer_bf16_wire():
+    run_world(_ddp_worker, world=2, args=(0.0005, torch.bfloat16))
 
 
 def _zero_worker(rank, world):

@@ -149,3 +149,47 @@ def test_linear_cat_matches_reference(cuda, direct):
         want = r.grad + (1.0 if direct else 0.0)
         err = ((p.grad - want).norm() / want.norm()).item()
         assert err < 1e-2, err
+
+
+@pytest.mark.parametrize("direct", [False, True])
+@pytest.mark.parametrize("kind", ["dropout_add", "gelu_dropout"])
+def test_bias_grad_fused_into_dropout_backward(cuda, kind, direct):
+    """linear(bias_grad=False) -> dropout op(bias=b): the bias gradient comes out of the
+    dropout backward kernel's column sums (*_bwd_colsum) and equals the column sum of the
+    input gradient it stores; the rest of the gradients match the unfused composition."""
+    from faster_distributed_training_amd.ops.dropout import dropout_add, gelu_dropout
+    from faster_distributed_training_amd.ops.linear import enable_direct_grads, linear
+    torch.manual_seed(4)
+    M, K, N = 8192, 256, 1024 if kind == "gelu_dropout" else 512
+    w = (torch.randn(N, K, device=cuda) * 0.05).requires_grad_(True)
+    b = (torch.randn(N, device=cuda) * 0.1).requires_grad_(True)
+    if direct:
+        w.grad, b.grad = torch.ones_like(w), torch.ones_like(b)
+        enable_direct_grads([w, b])
+    h = torch.randn(M, K, device=cuda, requires_grad=True)
+    x = torch.randn(M, N, device=cuda)
+    p = 0.2
+    torch.manual_seed(9)
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        y = linear(h, w, b, bias_grad=False)
+        out = dropout_add(y, x, p, True, None, bias=b) if kind == "dropout_add" else gelu_dropout(y, p, bias=b)
+    y.retain_grad()
+    g = torch.randn_like(out)
+    out.backward(g)
+    want = y.grad.float().sum(0) + (1.0 if direct else 0.0)
+    torch.testing.assert_close(b.grad, want, rtol=1e-4, atol=1e-3)
+    # the same draw without the fusion: every other gradient is unchanged
+    gh, gw = h.grad.clone(), w.grad.clone()
+    h.grad = None
+    if direct:
+        w.grad = torch.ones_like(w)
+    else:
+        w.grad = None
+    torch.manual_seed(9)
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        y2 = linear(h, w, b.detach())
+        out2 = dropout_add(y2, x, p, True, None) if kind == "dropout_add" else gelu_dropout(y2, p)
+    assert torch.equal(out, out2)
+    out2.backward(g)
+    torch.testing.assert_close(h.grad, gh, rtol=0, atol=0)
+    torch.testing.assert_close(w.grad, gw, rtol=1e-6, atol=1e-6)

@@ -163,3 +163,29 @@ def test_attention_masking_is_real():
     # faithful mask value (-1e-9) reproduces the reference bug (no masking)
     a = attention_reference(q, k, v, mask, mask_value=-1e-9)
     assert not torch.allclose(a, attention_reference(q, k2, v2, mask, mask_value=-1e-9))
+
+
+def test_fused_bias_grad_cpu_path_matches_plain_linear():
+    """CPU / plain-PyTorch path of ``bias=`` (ops/dropout._BiasGradTap): a linear called with
+    ``bias_grad=False`` feeding dropout_add / gelu_dropout(bias=...) gets the same bias
+    gradient as an ordinary linear."""
+    import torch.nn.functional as F
+    from faster_distributed_training_amd.ops.dropout import dropout_add, gelu_dropout
+    from faster_distributed_training_amd.ops.linear import linear
+    torch.manual_seed(0)
+    h = torch.randn(64, 32, requires_grad=True)
+    x = torch.randn(64, 16)
+    w = torch.randn(16, 32, requires_grad=True)
+    b = torch.randn(16, requires_grad=True)
+    g = torch.randn(64, 16)
+    for fn in (lambda y, bias: dropout_add(y, x, 0.0, True, None, bias=bias),
+               lambda y, bias: gelu_dropout(y, 0.0, True, bias=bias)):
+        for t in (h, w, b):
+            t.grad = None
+        fn(linear(h, w, b, bias_grad=False), b).backward(g)
+        got = [t.grad.clone() for t in (h, w, b)]
+        for t in (h, w, b):
+            t.grad = None
+        fn(F.linear(h, w, b), None).backward(g)
+        for a, r in zip(got, (h.grad, w.grad, b.grad)):
+            torch.testing.assert_close(a, r)

@@ -78,3 +78,22 @@ def test_cifar_streamed_matches_resident(cuda):
     stm = DeviceCIFARLoader(data, tg, 64, cuda, train=True, seed=2, out_dtype=torch.float32, resident=False)
     for (xa, ya), (xb, yb) in zip(res, stm):
         assert torch.equal(xa, xb) and torch.equal(ya, yb)
+
+
+def test_submit_runs_on_worker_thread(cuda):
+    """PinnedPrefetcher.submit: jobs issued by the native worker in order, wait() returns once
+    a slot's job is issued, the device sees every batch."""
+    from faster_distributed_training_amd.ops import _native
+    nat = _native.native()
+    pf = nat.PinnedPrefetcher(cuda.index or 0, 1 << 16, 3)
+    dst = [torch.empty(1 << 14, dtype=torch.uint8, device=cuda) for _ in range(3)]
+    srcs = [np.full(1 << 14, k, dtype=np.uint8) for k in range(9)]
+    out = []
+    for k in range(9):
+        s = pf.submit([srcs[k].ctypes.data], [srcs[k].nbytes], [dst[k % 3].data_ptr()], 0)
+        assert s == k % 3
+        pf.wait(s, _native.stream_ptr(cuda))
+        out.append(dst[s].float().mean())
+    assert pf.submitted == 9
+    pf.synchronize()
+    assert [float(v) for v in torch.stack(out).cpu()] == [float(k) for k in range(9)]
