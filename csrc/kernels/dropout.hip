@@ -165,30 +165,52 @@ __global__ __launch_bounds__(256) void dropout_bwd_colsum_kernel(const void* __r
   const int c0 = (blockIdx.x * 32 + cg) * 8;
   float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   if (cg < lanes) {
-    for (long r = r0 + rl; r < r1; r += 8) {
-      const long c = (r * cols + c0) >> 3;  // 16-B chunk index = the forward's hash index
-      const uint32_t m = thr ? keep8(c, s, thr) : 0xffu;
-      float f[8];
-      if constexpr (KIND == 0) {
-        const float4 g0 = reinterpret_cast<const float4*>(gin)[2 * c];
-        const float4 g1 = reinterpret_cast<const float4*>(gin)[2 * c + 1];
-        const float gf[8] = {g0.x, g0.y, g0.z, g0.w, g1.x, g1.y, g1.z, g1.w};
+    // 4 rows per trip (row lanes stride 8): all loads of a trip are issued before any use
+    constexpr int U = 4;
+    for (long rb = r0 + rl; rb < r1; rb += 8 * U) {
+      float4 g4[U][2];
+      uint4 gu[U], au[U];
 #pragma unroll
-        for (int j = 0; j < 8; ++j) f[j] = (m >> j) & 1 ? gf[j] * scale : 0.f;
-      } else {
-        float fa[8];
-        unpack8(reinterpret_cast<const uint4*>(a)[c], fa);
-        unpack8(reinterpret_cast<const uint4*>(gin)[c], f);
-#pragma unroll
-        for (int j = 0; j < 8; ++j) f[j] = (m >> j) & 1 ? f[j] * scale * gelu_erf_grad(fa[j]) : 0.f;
+      for (int u = 0; u < U; ++u) {
+        const long r = rb + 8 * u;
+        if (r < r1) {
+          const long c = (r * cols + c0) >> 3;
+          if constexpr (KIND == 0) {
+            g4[u][0] = reinterpret_cast<const float4*>(gin)[2 * c];
+            g4[u][1] = reinterpret_cast<const float4*>(gin)[2 * c + 1];
+          } else {
+            gu[u] = reinterpret_cast<const uint4*>(gin)[c];
+            au[u] = reinterpret_cast<const uint4*>(a)[c];
+          }
+        }
       }
-      const uint4 o = pack8(f);
-      reinterpret_cast<uint4*>(out)[c] = o;
-      // the bias gradient sums the STORED (bf16-rounded) values, as a colsum pass would
-      float q[8];
-      unpack8(o, q);
 #pragma unroll
-      for (int j = 0; j < 8; ++j) acc[j] += q[j];
+      for (int u = 0; u < U; ++u) {
+        const long r = rb + 8 * u;
+        if (r >= r1) break;
+        const long c = (r * cols + c0) >> 3;  // 16-B chunk index = the forward's hash index
+        const uint32_t m = thr ? keep8(c, s, thr) : 0xffu;
+        float f[8];
+        if constexpr (KIND == 0) {
+          const float gf[8] = {g4[u][0].x, g4[u][0].y, g4[u][0].z, g4[u][0].w,
+                               g4[u][1].x, g4[u][1].y, g4[u][1].z, g4[u][1].w};
+#pragma unroll
+          for (int j = 0; j < 8; ++j) f[j] = (m >> j) & 1 ? gf[j] * scale : 0.f;
+        } else {
+          float fa[8];
+          unpack8(au[u], fa);
+          unpack8(gu[u], f);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) f[j] = (m >> j) & 1 ? f[j] * scale * gelu_erf_grad(fa[j]) : 0.f;
+        }
+        const uint4 o = pack8(f);
+        reinterpret_cast<uint4*>(out)[c] = o;
+        // the bias gradient sums the STORED (bf16-rounded) values, as a colsum pass would
+        float q[8];
+        unpack8(o, q);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[j] += q[j];
+      }
     }
   }
 #pragma unroll
@@ -205,11 +227,15 @@ __global__ __launch_bounds__(256) void dropout_bwd_colsum_kernel(const void* __r
 
 unsigned grid_for(long n8) { return (unsigned)std::max<long>(1, std::min<long>((n8 + 255) / 256, 4096)); }
 
-// ~1024 workgroups over (column blocks x row chunks), >= 64 rows (8 per row lane) per block
+// Row chunks per column block: few enough that same-address fp32 atomics (serialised in L2)
+// stay cheap -- 256 for one or two column blocks, 512 when wider rows already give >= 4
+// column blocks of parallelism (measured: 512 -> 256 chunks at 512 columns 36 -> 24 us,
+// 256 -> 512 at 1024 columns 66 -> 60 us) -- and >= 32 rows (4 per row lane) per block
 dim3 colsum_grid(long rows, int cols, int* rpb_out) {
   const int cblk = (cols / 8 + 31) / 32;
-  long rpb = rows * cblk / 1024;
-  if (rpb < 64) rpb = 64;
+  const long chunks = cblk >= 4 ? 512 : 256;
+  long rpb = (rows + chunks - 1) / chunks;
+  if (rpb < 32) rpb = 32;
   rpb = (rpb + 7) / 8 * 8;
   *rpb_out = (int)rpb;
   return dim3((unsigned)cblk, (unsigned)((rows + rpb - 1) / rpb));
