@@ -85,10 +85,10 @@ void conv_igemm(uint64_t x, uint64_t x2, uint64_t ps, uint64_t pt, uint64_t pg, 
                 int Wi, int Cx, int Ho, int Wo, int S, const std::vector<int>& dh, const std::vector<int>& dw,
                 const std::vector<int>& wt, int Cout, int ldw, int Hout, int Wout, int OS, int oy, int ox, int pro,
                 int pro_act, float pro_alpha, int epi, int epi_act, float epi_alpha, int BM, int BN, int BK, int nsplit,
-                uint64_t slab, uint64_t cnt, uint64_t stream);
+                uint64_t slab, uint64_t cnt, int kg, uint64_t stream);
 void conv_igemm_join(uint64_t y, uint64_t r, uint64_t s, uint64_t t, uint64_t s2, uint64_t t2, uint64_t w, uint64_t out,
                      uint64_t part, int part_rows, uint64_t jout, uint64_t jmask, long Nb, int H, int W, int Cx, int Cout,
-                     int ldw, int BM, int BN, int BK, int nsplit, uint64_t slab, uint64_t cnt, uint64_t stream);
+                     int ldw, int BM, int BN, int BK, int nsplit, uint64_t slab, uint64_t cnt, int kg, uint64_t stream);
 int conv_num_row_blocks(long M, int BM);
 std::vector<long> conv_splitk_workspace(long M, int Cout, int BM, int BN, int nsplit);
 // conv_wgrad.hip

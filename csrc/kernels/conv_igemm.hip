@@ -11,7 +11,7 @@ static void conv_igemm_impl(uint64_t x, uint64_t x2, uint64_t ps, uint64_t pt, u
                             const std::vector<int>& dh, const std::vector<int>& dw, const std::vector<int>& wt, int Cout,
                             int ldw, int Hout, int Wout, int OS, int oy, int ox, int pro, int pro_act, float pro_alpha,
                             int epi, int epi_act, float epi_alpha, int BM, int BN, int BK, int nsplit, uint64_t slab,
-                            uint64_t cnt, uint64_t pt2, uint64_t pout, uint64_t pmask, uint64_t stream) {
+                            uint64_t cnt, uint64_t pt2, uint64_t pout, uint64_t pmask, int kg, uint64_t stream) {
   using namespace conv;
   ConvArgs a{};
   a.pt2 = P<const float>(pt2);
@@ -80,8 +80,11 @@ static void conv_igemm_impl(uint64_t x, uint64_t x2, uint64_t ps, uint64_t pt, u
   hipStream_t st = as_stream(stream);
   if (a.M == 0) return;
   const int act = (pro == kProAffineAct || pro == kProJoin) ? pro_act : ((epi == kEpiActBwd || epi == kEpiJoinBwd) ? epi_act : 0);
-  if (launch_cases_fwd(pro, epi, act, a, BM, BN, BK, pure, st) || launch_cases_fold(pro, epi, act, a, BM, BN, BK, pure, st) ||
-      launch_cases_join(pro, epi, act, a, BM, BN, BK, pure, st) || launch_cases_plain(pro, epi, act, a, BM, BN, BK, pure, st))
+  if (kg == 2 && a.nsplit > 1) kg = 1;  // K groups and split-K are alternatives
+  if (launch_cases_fwd(pro, epi, act, a, BM, BN, BK, kg, pure, st) ||
+      launch_cases_fold(pro, epi, act, a, BM, BN, BK, kg, pure, st) ||
+      launch_cases_join(pro, epi, act, a, BM, BN, BK, kg, pure, st) ||
+      launch_cases_plain(pro, epi, act, a, BM, BN, BK, kg, pure, st))
     return;
   FDT_CHECK(false, "unsupported (prologue, epilogue) combination");
 }
@@ -91,11 +94,12 @@ void conv_igemm(uint64_t x, uint64_t x2, uint64_t ps, uint64_t pt, uint64_t pg, 
                 int Wi, int Cx, int Ho, int Wo, int S,
                 const std::vector<int>& dh, const std::vector<int>& dw, const std::vector<int>& wt, int Cout, int ldw,
                 int Hout, int Wout, int OS, int oy, int ox, int pro, int pro_act, float pro_alpha, int epi, int epi_act,
-                float epi_alpha, int BM, int BN, int BK, int nsplit, uint64_t slab, uint64_t cnt, uint64_t stream) {
+                float epi_alpha, int BM, int BN, int BK, int nsplit, uint64_t slab, uint64_t cnt, int kg,
+                uint64_t stream) {
   FDT_CHECK(pro != conv::kProJoin, "the join prologue goes through conv_igemm_join");
   conv_igemm_impl(x, x2, ps, pt, pg, w, out, part, part_rows, ex, es, et, jmask, jyb, jout, Nb, Hi, Wi, Cx, Ho, Wo, S, dh,
                   dw, wt, Cout, ldw, Hout, Wout, OS, oy, ox, pro, pro_act, pro_alpha, epi, epi_act, epi_alpha, BM, BN, BK,
-                  nsplit, slab, cnt, 0, 0, 0, stream);
+                  nsplit, slab, cnt, 0, 0, 0, kg, stream);
 }
 
 // Forward 1x1 convolution whose operand is the previous residual block's join (PRO_JOIN):
@@ -103,11 +107,12 @@ void conv_igemm(uint64_t x, uint64_t x2, uint64_t ps, uint64_t pt, uint64_t pg, 
 // mask stored on the way.
 void conv_igemm_join(uint64_t y, uint64_t r, uint64_t s, uint64_t t, uint64_t s2, uint64_t t2, uint64_t w, uint64_t out,
                      uint64_t part, int part_rows, uint64_t jout, uint64_t jmask, long Nb, int H, int W, int Cx, int Cout,
-                     int ldw, int BM, int BN, int BK, int nsplit, uint64_t slab, uint64_t cnt, uint64_t stream) {
+                     int ldw, int BM, int BN, int BK, int nsplit, uint64_t slab, uint64_t cnt, int kg,
+                     uint64_t stream) {
   const std::vector<int> z{0};
   conv_igemm_impl(y, r, s, t, s2, w, out, part, part_rows, 0, 0, 0, 0, 0, 0, Nb, H, W, Cx, H, W, 1, z, z, z, Cout, ldw, H,
                   W, 1, 0, 0, conv::kProJoin, kActRelu, 1.f, conv::kEpiStats, 0, 1.f, BM, BN, BK, nsplit, slab, cnt, t2,
-                  jout, jmask, stream);
+                  jout, jmask, kg, stream);
 }
 
 int conv_num_row_blocks(long M, int BM) { return (int)((M + BM - 1) / BM); }

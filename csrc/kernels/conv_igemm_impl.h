@@ -51,6 +51,14 @@
 // slabs with sc1 loads (no L2 write-back / invalidate fences) and runs the normal fused
 // epilogue.  Counters are reset by the last arriver.
 //
+// K groups (KG = 2, small-M layers): the workgroup is 8 waves = two 4-wave groups, each with its
+// own double-buffered LDS tiles, taking alternate K tiles of the same output tile; group 1
+// hands its accumulators to group 0 through LDS and group 0 runs the epilogue.  At the
+// per-GPU batch of an 8-GPU run the 8x8 / 4x4 stages launch ~256 workgroups -- one 4-wave
+// workgroup per CU leaves each SIMD a single wave that serialises load waits, prologue VALU,
+// LDS reads and MFMAs (measured 44 % of wave time waiting, 23 % VALU, 10 % MFMA); two waves
+// per SIMD overlap them with no extra global traffic (unlike split-K's fp32 slabs).
+//
 // Strided convolutions: forward uses the input stride S; the dgrad of a stride-2
 // convolution is split by output parity into 4 dense classes (each its own tap table and
 // output row map: hi = ho*OS + oy), so no MFMA work is spent on structural zeros.
@@ -187,8 +195,9 @@ constexpr int kMinWavesPerEU =
     (BM == 128 && BN == 128 && BK == 32 && (PRO == kProNone || (PRO == kProAffineAct && PURE))) ? 4
     : (BM == 128 && BN == 128 && (BK == 32 || (PRO != 2 && PRO != 3))) ? 3 : 1;
 
-template <int BM, int BN, int BK, int PRO, int EPI, bool PURE, int ACT>
-__global__ __launch_bounds__(256, (kMinWavesPerEU<BM, BN, BK, PRO, PURE>)) void igemm_kernel(const ConvArgs a) {
+template <int BM, int BN, int BK, int PRO, int EPI, bool PURE, int ACT, int KG>
+__global__ __launch_bounds__(256 * KG, (KG == 1 ? kMinWavesPerEU<BM, BN, BK, PRO, PURE> : 1)) void igemm_kernel(
+    const ConvArgs a) {
   constexpr int CPR = BK / 8;        // 16-B chunks per LDS row
   constexpr int RPR = 256 / CPR;     // rows covered by one load round
   constexpr int NXL = BM / RPR;      // activation chunks per thread per tile
@@ -213,7 +222,11 @@ __global__ __launch_bounds__(256, (kMinWavesPerEU<BM, BN, BK, PRO, PURE>)) void 
   const int hdr = ((NPRM * a.Cx + 4 * NQ * BN + 24) * 4 + 15) & ~15;
   bf16* tiles = reinterpret_cast<bf16*>(smem + hdr);                   // [nbuf][WT + XT]
 
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  // tid / lane / wid are local to the K group (every load / fragment / epilogue mapping below
+  // is written for 256 threads); grp selects the group's K tiles and LDS buffers
+  const int tid = threadIdx.x & 255, lane = tid & 63, wid = tid >> 6;
+  const int grp = KG == 1 ? 0 : (int)(threadIdx.x >> 8);
+  static_assert(KG == 1 || KG == 2, "one or two K groups");
   const int wn = wid & 1, wm = wid >> 1;
   // a tile's splits are consecutive ids -> the same XCD after the remap
   const int rid = xcd_remap(blockIdx.x, a.nbm * a.nbn * a.nsplit);
@@ -302,8 +315,9 @@ __global__ __launch_bounds__(256, (kMinWavesPerEU<BM, BN, BK, PRO, PURE>)) void 
     }
   };
 
+  bf16* const gtiles = tiles + grp * 2 * (WT + XT);  // this K group's two LDS buffers
   auto store_tile = [&](const Stage& S, int buf) {
-    bf16* Wl = tiles + buf * (WT + XT);
+    bf16* Wl = gtiles + buf * (WT + XT);
     bf16* Xl = Wl + WT;
 #pragma unroll
     for (int j = 0; j < NWL; ++j) {
@@ -394,7 +408,7 @@ __global__ __launch_bounds__(256, (kMinWavesPerEU<BM, BN, BK, PRO, PURE>)) void 
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
   auto compute = [&](int buf) {
-    const bf16* Wl = tiles + buf * (WT + XT);
+    const bf16* Wl = gtiles + buf * (WT + XT);
     const bf16* Xl = Wl + WT;
 #pragma unroll
     for (int ks = 0; ks < BK / 16; ++ks) {
@@ -417,9 +431,13 @@ __global__ __launch_bounds__(256, (kMinWavesPerEU<BM, BN, BK, PRO, PURE>)) void 
     }
   };
 
-  // this split's K tiles [kb, kb + nk)
+  // this split's K tiles [kb, kb + nk); K group g takes tiles kb + i*KG + g, i < nkk (the
+  // same trip count in both groups -- a group's tile past nk loads zeros -- so both groups
+  // meet every barrier)
   const int kb = split * a.kps;
   const int nk = min(nkt - kb, a.kps);
+  const int nkk = (nk + KG - 1) / KG;
+  auto ld = [&](Stage& S, int i) { load_tile(S, kb + i * KG + grp, i < nkk && i * KG + grp < nk); };
 
   {
   // prologue: tile 0 -> LDS buf 0; tile 1 pending in B; tile 2 in flight in A.
@@ -429,65 +447,92 @@ __global__ __launch_bounds__(256, (kMinWavesPerEU<BM, BN, BK, PRO, PURE>)) void 
   // memory-bound layers run many short workgroups).
   Stage SA, SB;
   if constexpr (PURE) {
-    if (nk > 0) {
-      load_tile(SA, kb, true);
+    if (nkk > 0) {
+      ld(SA, 0);
       __builtin_amdgcn_sched_barrier(0);  // issue order SA, SB, SA' pinned (exact vmcnt counting)
-      load_tile(SB, kb + 1, nk > 1);
+      ld(SB, 1);
       __builtin_amdgcn_sched_barrier(0);
     }
   }
-  if constexpr (HASPRO) {
-    for (int i = tid; i < a.Cx; i += 256) {
-      pst[i] = a.ps[i];
-      pst[a.Cx + i] = a.pt[i];
-      if constexpr (PRO == kProFold) pst[2 * a.Cx + i] = a.pg ? a.pg[i] : 1.f;
-      if constexpr (PRO == kProJoin) {
-        pst[2 * a.Cx + i] = a.pg ? a.pg[i] : 1.f;
-        pst[3 * a.Cx + i] = a.pg ? a.pt2[i] : 0.f;
+  if (grp == 0) {
+    if constexpr (HASPRO) {
+      for (int i = tid; i < a.Cx; i += 256) {
+        pst[i] = a.ps[i];
+        pst[a.Cx + i] = a.pt[i];
+        if constexpr (PRO == kProFold) pst[2 * a.Cx + i] = a.pg ? a.pg[i] : 1.f;
+        if constexpr (PRO == kProJoin) {
+          pst[2 * a.Cx + i] = a.pg ? a.pg[i] : 1.f;
+          pst[3 * a.Cx + i] = a.pg ? a.pt2[i] : 0.f;
+        }
       }
     }
-  }
-  if (tid < 12) {
-    const int dh = a.dh[tid], dw = a.dw[tid];
-    tapt[tid] = dh * a.Wi + dw;
-    tapw[tid] = (int)(uint8_t)a.dh[tid] | ((int)(uint8_t)a.dw[tid] << 8) | ((int)(uint8_t)a.wt[tid] << 16);
+    if (tid < 12) {
+      const int dh = a.dh[tid], dw = a.dw[tid];
+      tapt[tid] = dh * a.Wi + dw;
+      tapw[tid] = (int)(uint8_t)a.dh[tid] | ((int)(uint8_t)a.dw[tid] << 8) | ((int)(uint8_t)a.wt[tid] << 16);
+    }
   }
 
   __syncthreads();
   if constexpr (!PURE) {
-    if (nk > 0) {
-      load_tile(SA, kb, true);
+    if (nkk > 0) {
+      ld(SA, 0);
       __builtin_amdgcn_sched_barrier(0);
-      load_tile(SB, kb + 1, nk > 1);
+      ld(SB, 1);
       __builtin_amdgcn_sched_barrier(0);
     }
   }
-  if (nk > 0) {
+  if (nkk > 0) {
     store_tile(SA, 0);
-    load_tile(SA, kb + 2, nk > 2);
+    ld(SA, 2);
     __builtin_amdgcn_sched_barrier(0);
     __syncthreads();
   }
-  for (int kt = 0; kt < nk; kt += 2) {
+  for (int kt = 0; kt < nkk; kt += 2) {
     // even tile kt in buf 0; SB holds kt+1, SA holds kt+2 (in flight)
     compute(0);
-    if (kt + 1 >= nk) break;
+    if (kt + 1 >= nkk) break;
     store_tile(SB, 1);
     __syncthreads();
-    load_tile(SB, kb + kt + 3, kt + 3 < nk);
+    ld(SB, kt + 3);
     __builtin_amdgcn_sched_barrier(0);  // keep the prefetch issued ahead of the MFMAs
     // odd tile kt+1 in buf 1; SA holds kt+2, SB holds kt+3 (in flight)
     compute(1);
-    if (kt + 2 >= nk) break;
+    if (kt + 2 >= nkk) break;
     store_tile(SA, 0);
     __syncthreads();
-    load_tile(SA, kb + kt + 4, kt + 4 < nk);
+    ld(SA, kt + 4);
     __builtin_amdgcn_sched_barrier(0);
   }
   }
 
+  if constexpr (KG == 2) {
+    // group 1's partial sums -> LDS -> group 0 (register order [reg][thread]: conflict-free)
+    float* xs = reinterpret_cast<float*>(tiles);
+    __syncthreads();  // every wave is done reading its K tiles
+    if (grp == 1) {
+#pragma unroll
+      for (int i = 0; i < TN; ++i)
+#pragma unroll
+        for (int j = 0; j < TM; ++j)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) xs[((i * TM + j) * 16 + r) * 256 + tid] = acc[i][j][r];
+    }
+    __syncthreads();
+    if (grp == 0) {
+#pragma unroll
+      for (int i = 0; i < TN; ++i)
+#pragma unroll
+        for (int j = 0; j < TM; ++j)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) acc[i][j][r] += xs[((i * TM + j) * 16 + r) * 256 + tid];
+    }
+    // (the epilogue's first barrier orders these reads before its staging writes)
+  }
+
   // ------------------------------------------------------------------ split-K combine
-  if (a.nsplit > 1) {
+  // (KG == 2 launches never split K over workgroups: the host refuses nsplit > 1 there)
+  if (KG == 1 && a.nsplit > 1) {
     constexpr int NR4 = TN * TM * 4;  // float4 registers per thread
     // this tile's slabs [nsplit][NR4][256] float4 behind one buffer descriptor
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
@@ -575,12 +620,15 @@ __global__ __launch_bounds__(256, (kMinWavesPerEU<BM, BN, BK, PRO, PURE>)) void 
     float q0[8], q1[8], q2[8];
 #pragma unroll
     for (int k = 0; k < 8; ++k) { q0[k] = 0.f; q1[k] = 0.f; q2[k] = 0.f; }
+    // K group 1 (KG == 2) only meets the barriers below; group 0 owns the whole epilogue
+    const bool ew = grp == 0;
     __syncthreads();  // every wave is done with the K tiles (and the split-K flag)
 #pragma unroll
     for (int j = 0; j < TM; ++j) {
       // ---- stage accumulator block j: local row = wm*32 + pixel, 8 channels per (i, p)
 #pragma unroll
       for (int i = 0; i < TN; ++i) {
+        if (!ew) break;
 #pragma unroll
         for (int p = 0; p < 2; ++p) {
           const int g = 2 * p;
@@ -603,7 +651,7 @@ __global__ __launch_bounds__(256, (kMinWavesPerEU<BM, BN, BK, PRO, PURE>)) void 
       for (int sw = 0; sw < NSW; ++sw) {
         const int lr = rs + sw * RPS;
         const long m = m0 + (lr >> 5) * (BM / 2) + j * 32 + (lr & 31);
-        if (m < a.M) {
+        if (ew && m < a.M) {
           uint32_t orow;
           if (dense) {
             orow = (uint32_t)m;
@@ -670,6 +718,7 @@ __global__ __launch_bounds__(256, (kMinWavesPerEU<BM, BN, BK, PRO, PURE>)) void 
       // lanes l, l + CG, l + 2CG, ... of a wave hold the same channels
 #pragma unroll
       for (int o = CG; o < 64; o <<= 1) {
+        if (!ew) break;
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
           q0[k] += __shfl_xor(q0[k], o, 64);
@@ -677,7 +726,7 @@ __global__ __launch_bounds__(256, (kMinWavesPerEU<BM, BN, BK, PRO, PURE>)) void 
           if constexpr (NQ == 3) q2[k] += __shfl_xor(q2[k], o, 64);
         }
       }
-      if (lane < CG) {
+      if (ew && lane < CG) {
         float* rw = red + wid * NQ * BN + cg * 8;
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
@@ -687,7 +736,7 @@ __global__ __launch_bounds__(256, (kMinWavesPerEU<BM, BN, BK, PRO, PURE>)) void 
         }
       }
       __syncthreads();
-      for (int e = tid; e < NQ * BN; e += 256) {
+      for (int e = tid; ew && e < NQ * BN; e += 256) {
         const float t = red[e] + red[NQ * BN + e] + red[2 * NQ * BN + e] + red[3 * NQ * BN + e];
         const int q = e / BN, cc2 = e - q * BN;
         atomicAdd(&a.part[((long)(bm & a.slot_mask) * NQ + q) * a.Cout + n0 + cc2], t);
@@ -701,57 +750,77 @@ struct Cfg {
   int BM, BN;
 };
 
-template <int BM, int BN, int BK, int PRO, int EPI, bool PURE, int ACT>
+template <int BM, int BN, int BK, int PRO, int EPI, bool PURE, int ACT, int KG>
 static void launch_one(const ConvArgs& a, size_t lds, hipStream_t st) {
-  auto kern = igemm_kernel<BM, BN, BK, PRO, EPI, PURE, ACT>;
+  auto kern = igemm_kernel<BM, BN, BK, PRO, EPI, PURE, ACT, KG>;
   static size_t attr_set = 64 * 1024;  // default dynamic-LDS limit; raise only when needed
   if (lds > attr_set) {
     FDT_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
                                       (int)lds));
     attr_set = lds;
   }
-  hipLaunchKernelGGL(kern, dim3(a.nbm * a.nbn * a.nsplit), dim3(256), lds, st, a);
+  hipLaunchKernelGGL(kern, dim3(a.nbm * a.nbn * a.nsplit), dim3(256 * KG), lds, st, a);
   FDT_LAUNCH_CHECK();
 }
 
-template <int BM, int BN, int BK, int PRO, int EPI, int ACT>
+template <int BM, int BN, int BK, int PRO, int EPI, int ACT, int KG>
 static void launch_pure(const ConvArgs& a, bool pure, size_t lds, hipStream_t st) {
   if constexpr (PRO == kProJoin) {
     FDT_CHECK(pure, "the join prologue needs a 1x1 stride-1 convolution");
-    launch_one<BM, BN, BK, PRO, EPI, true, ACT>(a, lds, st);
+    launch_one<BM, BN, BK, PRO, EPI, true, ACT, KG>(a, lds, st);
   } else {
-    if (pure) launch_one<BM, BN, BK, PRO, EPI, true, ACT>(a, lds, st);
-    else launch_one<BM, BN, BK, PRO, EPI, false, ACT>(a, lds, st);
+    if (pure) launch_one<BM, BN, BK, PRO, EPI, true, ACT, KG>(a, lds, st);
+    else launch_one<BM, BN, BK, PRO, EPI, false, ACT, KG>(a, lds, st);
   }
 }
 
 template <int PRO, int EPI, int ACT>
-static void launch_tile(const ConvArgs& a, int BM, int BN, int BK, bool pure, hipStream_t st) {
+static void launch_tile(const ConvArgs& a, int BM, int BN, int BK, int kg, bool pure, hipStream_t st) {
   const int nkt = (a.K + BK - 1) / BK;
   const size_t nbuf = nkt > 1 ? 2 : 1;
-  // header (must match the kernel's hdr) + max(K tiles, epilogue staging [64][BN + 4] fp32)
+  FDT_CHECK(kg == 1 || (kg == 2 && a.nsplit == 1 && nkt >= 2), "K groups: kg 1 | 2 (2: no split-K, >= 2 K tiles)");
+  // header (must match the kernel's hdr) + max(K tiles of every K group, epilogue staging
+  // [64][BN + 4] fp32, K-group hand-off [BM*BN] fp32)
   const int nprm = PRO == kProJoin ? 4 : (PRO == kProFold ? 3 : ((PRO == kProAffineAct) ? 2 : 0));
   const size_t hdr = (((size_t)nprm * a.Cx + 4 * (EPI == kEpiJoinBwd ? 3 : 2) * BN + 24) * 4 + 15) & ~(size_t)15;
-  const size_t tiles = nbuf * (BM + BN) * BK * 2, stage = (size_t)64 * (BN + 4) * 4;
-  size_t lds = hdr + (tiles > stage ? tiles : stage);
+  const size_t tiles = (kg == 2 ? 2 * 2 : nbuf) * (BM + BN) * BK * 2, stage = (size_t)64 * (BN + 4) * 4;
+  const size_t hand = kg == 2 ? (size_t)BM * BN * 4 : 0;
+  size_t body = tiles > stage ? tiles : stage;
+  if (hand > body) body = hand;
+  size_t lds = hdr + body;
 #define FDT_T(BM_, BN_, BK_) \
-  if (BM == BM_ && BN == BN_ && BK == BK_) { launch_pure<BM_, BN_, BK_, PRO, EPI, ACT>(a, pure, lds, st); return; }
-  FDT_T(128, 128, 64) FDT_T(128, 64, 64) FDT_T(64, 128, 64) FDT_T(64, 64, 64) FDT_T(256, 64, 64)
+  if (BM == BM_ && BN == BN_ && BK == BK_) { launch_pure<BM_, BN_, BK_, PRO, EPI, ACT, 1>(a, pure, lds, st); return; }
+  // two K groups: the tiles the small-M (latency-bound, ~256-workgroup) layers use
+#define FDT_T2(BM_, BN_, BK_)                                                                   \
+  if (BM == BM_ && BN == BN_ && BK == BK_) {                                                   \
+    if (kg == 2) launch_pure<BM_, BN_, BK_, PRO, EPI, ACT, 2>(a, pure, lds, st);              \
+    else launch_pure<BM_, BN_, BK_, PRO, EPI, ACT, 1>(a, pure, lds, st);                      \
+    return;                                                                                    \
+  }
+  // (K groups at 128x64x128 / 64x128x128 spill with the two-operand prologues under the
+  // 256-VGPR budget of 8-wave workgroups: those tiles stay single-group)
+  FDT_CHECK(kg == 1 || BK == 64 || (BM == 64 && BN == 64), "K groups: unsupported tile");
+  FDT_T2(128, 128, 64) FDT_T2(128, 64, 64) FDT_T2(64, 128, 64) FDT_T2(64, 64, 64) FDT_T(256, 64, 64)
   FDT_T(128, 128, 32) FDT_T(128, 64, 32) FDT_T(64, 128, 32) FDT_T(64, 64, 32) FDT_T(256, 128, 32)
   // BK = 128: half the K-loop trips for the latency-bound small-M layers (8x8 / 4x4 stages at
   // the 8-GPU per-GPU batch), twice the bytes in flight per prefetch stage
-  FDT_T(64, 64, 128) FDT_T(128, 64, 128) FDT_T(64, 128, 128)
+  FDT_T2(64, 64, 128) FDT_T(128, 64, 128) FDT_T(64, 128, 128)
 #undef FDT_T
+#undef FDT_T2
   FDT_CHECK(false, "unsupported conv tile");
 }
 
 
 // (PRO, EPI, ACT) case groups, each instantiated in its own translation unit so the
 // kernel matrix compiles in parallel (conv_igemm_inst_*.hip)
-bool launch_cases_fwd(int pro, int epi, int act, const ConvArgs& a, int BM, int BN, int BK, bool pure, hipStream_t st);
-bool launch_cases_fold(int pro, int epi, int act, const ConvArgs& a, int BM, int BN, int BK, bool pure, hipStream_t st);
-bool launch_cases_join(int pro, int epi, int act, const ConvArgs& a, int BM, int BN, int BK, bool pure, hipStream_t st);
-bool launch_cases_plain(int pro, int epi, int act, const ConvArgs& a, int BM, int BN, int BK, bool pure, hipStream_t st);
+bool launch_cases_fwd(int pro, int epi, int act, const ConvArgs& a, int BM, int BN, int BK, int kg, bool pure,
+                      hipStream_t st);
+bool launch_cases_fold(int pro, int epi, int act, const ConvArgs& a, int BM, int BN, int BK, int kg, bool pure,
+                       hipStream_t st);
+bool launch_cases_join(int pro, int epi, int act, const ConvArgs& a, int BM, int BN, int BK, int kg, bool pure,
+                       hipStream_t st);
+bool launch_cases_plain(int pro, int epi, int act, const ConvArgs& a, int BM, int BN, int BK, int kg, bool pure,
+                        hipStream_t st);
 
 }  // namespace conv
 }  // namespace fdt

@@ -4,9 +4,10 @@
 namespace fdt {
 namespace conv {
 
-bool launch_cases_plain(int pro, int epi, int act, const ConvArgs& a, int BM, int BN, int BK, bool pure, hipStream_t st) {
+bool launch_cases_plain(int pro, int epi, int act, const ConvArgs& a, int BM, int BN, int BK, int kg, bool pure,
+                      hipStream_t st) {
 #define FDT_CONV_CASE(P_, E_, A_) \
-  if (pro == P_ && epi == E_ && act == A_) { launch_tile<P_, E_, A_>(a, BM, BN, BK, pure, st); return true; }
+  if (pro == P_ && epi == E_ && act == A_) { launch_tile<P_, E_, A_>(a, BM, BN, BK, kg, pure, st); return true; }
   FDT_CONV_CASE(kProNone, kEpiActBwd, kActRelu)
   FDT_CONV_CASE(kProNone, kEpiActBwd, kActCelu)
   FDT_CONV_CASE(kProNone, kEpiStore, kActNone)

@@ -155,7 +155,23 @@ def _tile3(tile, M, N):
         return pick_tile(M, N)
     if len(tile) == 2:
         return tile[0], tile[1], 64
-    return tuple(tile)
+    return tuple(tile[:3])
+
+
+# K groups (csrc/kernels/conv_igemm_impl.h): 8-wave workgroups whose two 4-wave halves take
+# alternate K tiles -- for the small-M layers whose ~256-workgroup grids leave one wave per SIMD
+KGROUPS = os.environ.get("FDT_KGROUPS", "1") != "0"
+KG_TILES = {(128, 128, 64), (128, 64, 64), (64, 128, 64), (64, 64, 64), (64, 64, 128)}
+
+
+def _kg(ent, kg, tile3, ns, K):
+    """K groups of one launch: explicit ``kg``, else the tuned entry's, else 1."""
+    if kg is None:
+        kg = int(ent.get("kg", 1)) if ent else 1
+    bk = tile3[2]
+    if not KGROUPS or kg != 2 or ns != 1 or tuple(tile3) not in KG_TILES or -(-K // bk) < 2:
+        return 1
+    return 2
 
 
 @dataclass
@@ -216,7 +232,7 @@ def stat_slots(nq: int, C: int, device, M: int | None = None) -> torch.Tensor:
 
 
 def conv_fwd(x, wf, shp: ConvShape, s=None, t=None, act=0, alpha=1.0, tile=None, part=None, nsplit=None,
-             fin=None):
+             fin=None, kg=None):
     """y = conv(act(x*s+t)) (or conv(x) when s is None and act == 0); returns
     (y [N,Ho,Wo,Cout] bf16, part [STAT_SLOTS,2,Cout] fp32 slots whose row sum is
     (sum y, sum y^2)).  ``part``: a zeroed slot buffer to accumulate into.
@@ -237,6 +253,7 @@ def conv_fwd(x, wf, shp: ConvShape, s=None, t=None, act=0, alpha=1.0, tile=None,
     if nsplit is not None:
         ent = {"nsplit": nsplit}
     ns, slab_p, cnt_p = _splitk_args(ent, M, shp.cout, shp.ntaps * C, bm, bn, bk, x.device)
+    kgv = _kg(ent, kg, (bm, bn, bk), ns, shp.ntaps * C)
     y = torch.empty(N, Ho, Wo, shp.cout, device=x.device, dtype=torch.bfloat16)
     if part is None:
         part = stat_slots(2, shp.cout, x.device, M)
@@ -247,14 +264,15 @@ def conv_fwd(x, wf, shp: ConvShape, s=None, t=None, act=0, alpha=1.0, tile=None,
     nat.conv_igemm(x.data_ptr(), 0, _p(s), _p(t), 0, wf.data_ptr(), y.data_ptr(), part.data_ptr(), part.shape[0],
                    0, 0, 0, 0, 0, 0,
                    N, H, W, C, Ho, Wo, shp.stride, list(dh), list(dw), list(wt), shp.cout, shp.ntaps * shp.cxp,
-                   Ho, Wo, 1, 0, 0, pro, int(act), float(alpha), EPI_STATS, 0, 1.0, bm, bn, bk, ns, slab_p, cnt_p, _sp())
+                   Ho, Wo, 1, 0, 0, pro, int(act), float(alpha), EPI_STATS, 0, 1.0, bm, bn, bk, ns, slab_p, cnt_p, kgv,
+                   _sp())
     if fin is not None:
         _finalize_standalone(nat, 1, part, 2, shp.cout, fin[0], fin[1])
     return y, part
 
 
 def conv_fwd_join(y, r, s, t, s2, t2, wf, shp: ConvShape, jout, jmask=None, tile=None, part=None, nsplit=None,
-                  fin=None):
+                  fin=None, kg=None):
     """1x1 stride-1 forward conv of a residual block's joined output, computed on the fly:
     the operand is a = relu(y*s + t + (r*s2 + t2 if s2 is not None else r)) -- the previous
     block's join (BN'd residual branch y + BN'd or identity shortcut r).  ``jout`` receives
@@ -278,12 +296,13 @@ def conv_fwd_join(y, r, s, t, s2, t2, wf, shp: ConvShape, jout, jmask=None, tile
     if nsplit is not None:
         ent = {"nsplit": nsplit}
     ns, slab_p, cnt_p = _splitk_args(ent, M, shp.cout, C, bm, bn, bk, y.device)
+    kgv = _kg(ent, kg, (bm, bn, bk), ns, C)
     out = torch.empty(N, H, W, shp.cout, device=y.device, dtype=torch.bfloat16)
     if part is None:
         part = stat_slots(2, shp.cout, y.device, M)
     nat.conv_igemm_join(y.data_ptr(), r.data_ptr(), s.data_ptr(), t.data_ptr(), _p(s2), _p(t2), wf.data_ptr(),
                         out.data_ptr(), part.data_ptr(), part.shape[0], jout.data_ptr(), _p(jmask), N, H, W, C,
-                        shp.cout, shp.ntaps * shp.cxp, bm, bn, bk, ns, slab_p, cnt_p, _sp())
+                        shp.cout, shp.ntaps * shp.cxp, bm, bn, bk, ns, slab_p, cnt_p, kgv, _sp())
     if fin is not None:
         _finalize_standalone(nat, 1, part, 2, shp.cout, fin[0], fin[1])
     return out, part
@@ -291,7 +310,7 @@ def conv_fwd_join(y, r, s, t, s2, t2, wf, shp: ConvShape, jout, jmask=None, tile
 
 def conv_dgrad(g, y, al, be, wd, shp: ConvShape, x_shape, epi=EPI_STORE, out=None, ex=None, es=None, et=None,
                act=0, alpha=1.0, tile=None, part=None, nsplit=None, gs=None, jmask=None, jyb=None, jout=None,
-               coef=None):
+               coef=None, kg=None):
     """Data gradient of y = conv(a): dA = conv^T(g*gs + al + be*y)  (gs None: 1).
 
     epi: EPI_STORE -> write dA; EPI_ADD -> out += dA; EPI_ACTBWD -> through the lazy
@@ -335,6 +354,7 @@ def conv_dgrad(g, y, al, be, wd, shp: ConvShape, x_shape, epi=EPI_STORE, out=Non
             continue
         bm, bn, bk = _tile3(tile, M, shp.cin)
         ns, slab_p, cnt_p = _splitk_args(ent, M, shp.cin, len(dh) * Cy, bm, bn, bk, g.device)
+        kgv = _kg(ent, kg, (bm, bn, bk), ns, len(dh) * Cy)
         pro = PRO_FOLD if al is not None else PRO_NONE  # al None: g is already folded
         assert gs is None or pro == PRO_FOLD, "gs needs the fold prologue (al/be)"
         nat.conv_igemm(g.data_ptr(), _p(y) if pro == PRO_FOLD else 0, _p(al), _p(be), _p(gs), wd.data_ptr(),
@@ -342,7 +362,7 @@ def conv_dgrad(g, y, al, be, wd, shp: ConvShape, x_shape, epi=EPI_STORE, out=Non
                        part.shape[0] if part is not None else 0, _p(ex), _p(es), _p(et),
                        _p(jmask), _p(jyb), _p(jout), N, Hy, Wy, Cy, Ha, Wa, 1,
                        list(dh), list(dw), list(wt), shp.cin, shp.ntaps * shp.cout, Hx, Wx, shp.stride, py, px,
-                       pro, 0, 1.0, epi, int(act), float(alpha), bm, bn, bk, ns, slab_p, cnt_p, _sp())
+                       pro, 0, 1.0, epi, int(act), float(alpha), bm, bn, bk, ns, slab_p, cnt_p, kgv, _sp())
     if coef is not None:
         _finalize_standalone(nat, 2, part, 3 if epi == EPI_JOINBWD else 2, shp.cin, coef[0], coef[1])
     return out, (part if epi in (EPI_ACTBWD, EPI_JOINBWD) else None)

@@ -7,6 +7,7 @@ OUT=gpurun_out/${1:-pmcs}
 mkdir -p "$OUT"
 run() {  # name shape op
   local name=$1 shape=$2 op=$3
+  mkdir -p "$OUT/$name"
   for grp in "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_VMEM SQ_VALU_MFMA_BUSY_CYCLES" \
              "SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_WAVES SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_SALU" \
              "TCC_HIT_sum TCC_MISS_sum TCP_TCC_READ_REQ_sum" ; do

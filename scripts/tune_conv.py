@@ -36,6 +36,8 @@ def main():
     ap.add_argument("--max-m", type=int, default=0, help="only shapes with N*Ho*Wo <= this (0 = all)")
     ap.add_argument("--splits", type=int, nargs="+", default=[1, 2, 4, 8],
                     help="split-K candidates for fwd/dgrad when the tile grid is small")
+    ap.add_argument("--kg", type=int, nargs="+", default=[1, 2],
+                    help="K-group candidates for fwd/dgrad (2: 8-wave workgroups, conv_igemm.KG_TILES, no split-K)")
     ap.add_argument("--base", default=None, help="table to start from (default: --out if it exists, else the "
                                                  "in-tree table)")
     ap.add_argument("--out", default=os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
@@ -81,25 +83,30 @@ def main():
                         continue
                     ntiles = -(-M // t[0]) * (Nn // t[1])
                     for ns in (a.splits if ntiles < 768 else [1]):
-                        ms = timeit(lambda: fn(t, ns), a.reps)
-                        if best is None or ms < best[0]:
-                            best = (ms, t, ns)
+                        for kg in a.kg:
+                            if kg == 2 and (ns != 1 or tuple(t) not in ci.KG_TILES):
+                                continue
+                            ms = timeit(lambda: fn(t, ns, kg), a.reps)
+                            if best is None or ms < best[0]:
+                                best = (ms, t, ns, kg)
                 res[name] = dict(tile=best[1], nsplit=best[2], us=round(best[0] * 1e3, 1))
+                if best[3] != 1:
+                    res[name]["kg"] = best[3]
 
             # modes the fused engine actually launches (ops/resnet_fused.py): 3x3 convs get a
             # materialised input / pre-folded gradient; 1x1 convs fuse the transforms
             fwd_modes = [0] if k > 1 else [0, 1]
             for pro in fwd_modes:
-                sweep(f"fwd{pro}", lambda t, ns: ci.conv_fwd(x, wf, shp, sv if pro else None, tv if pro else None,
-                                                              pro, 1.0, tile=t, nsplit=ns),
+                sweep(f"fwd{pro}", lambda t, ns, kg: ci.conv_fwd(x, wf, shp, sv if pro else None, tv if pro else None,
+                                                                  pro, 1.0, tile=t, nsplit=ns, kg=kg),
                       FWD_TILES, lambda t: Cout % t[1] == 0, N * Ho * Wo, Cout)
             if Cin >= 8:
                 dg = [(0, ci.EPI_ACTBWD)] if k > 1 else [(2, ci.EPI_ACTBWD), (2, ci.EPI_STORE)]
                 for pro, epi in dg:
                     sweep(f"dgrad{pro}{epi}",
-                          lambda t, ns: ci.conv_dgrad(g, yy if pro else None, al if pro else None,
-                                                      be if pro else None, wd, shp, (N, H, H, Cin), epi=epi, ex=ex,
-                                                      es=es, et=et, act=1, tile=t, nsplit=ns),
+                          lambda t, ns, kg: ci.conv_dgrad(g, yy if pro else None, al if pro else None,
+                                                          be if pro else None, wd, shp, (N, H, H, Cin), epi=epi,
+                                                          ex=ex, es=es, et=et, act=1, tile=t, nsplit=ns, kg=kg),
                           FWD_TILES, lambda t: Cin % t[1] == 0, N * H * H // (s * s), Cin)
             ldw = shp.ntaps * shp.cxp
             slab = torch.empty(1024 * Cout * ldw // 4 + 1, device=dev)

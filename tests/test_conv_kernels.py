@@ -339,3 +339,61 @@ def test_strided_dgrad_store_writes_every_parity_class(cuda):
     ci.conv_dgrad(g, None, None, None, wd, shp, xs, epi=ci.EPI_STORE, out=out)
     ref = nhwc(torch.nn.grad.conv2d_input((2, 64, 8, 8), w.to(BF).float(), nchw(g), stride=2, padding=0))
     assert torch.isfinite(out.float()).all() and rel(out, ref) < 1e-2
+
+
+@pytest.mark.parametrize("tile", [(64, 64, 64), (128, 64, 64), (64, 128, 64), (128, 128, 64), (64, 64, 128)])
+def test_kgroups_match_reference(cuda, tile):
+    """K groups (kg=2: 8-wave workgroups whose halves take alternate K tiles, partial sums
+    handed over in LDS) for the forward conv with/without the lazy-BN prologue, the join
+    prologue and the folded dgrad with the activation-backward epilogue, odd and even K-tile
+    counts, against fp32 PyTorch; the statistics slots too."""
+    torch.manual_seed(7)
+    for (N, H, Cin, Cout, k, stride, pad) in [(2, 8, 64, 128, 3, 1, 1), (2, 4, 512, 128, 3, 1, 1),
+                                             (3, 5, 256, 128, 1, 1, 0), (2, 8, 64, 256, 1, 2, 0)]:
+        if Cout % tile[1]:
+            continue
+        shp = ci.ConvShape(Cin, Cout, k, stride, pad)
+        x = padc(make((N, H, H, Cin), cuda), shp.cxp)
+        w = torch.randn(Cout, Cin, k, k, device=cuda) / (Cin * k * k) ** 0.5
+        wf, wd = ci.alloc_packed(shp, cuda)
+        ci.pack_weights([(w, wf, wd, shp)])
+        s = torch.rand(Cin, device=cuda) + 0.5
+        t = torch.randn(Cin, device=cuda) * 0.3
+        for pro in ("plain", "relu"):
+            a = x.float() if pro == "plain" else torch.relu(x.float() * s + t).to(BF).float()
+            ref = nhwc(F.conv2d(nchw(a), w.to(BF).float(), stride=stride, padding=pad))
+            y, part = ci.conv_fwd(x, wf, shp, None if pro == "plain" else s, None if pro == "plain" else t,
+                                  0 if pro == "plain" else 1, 1.0, tile=tile, nsplit=1, kg=2)
+            assert rel(y, ref) < 1e-2, (tile, pro, rel(y, ref))
+            ps, yf = part.sum(0), ref.reshape(-1, Cout)
+            assert rel(ps[0], yf.sum(0)) < 2e-3 and rel(ps[1], (yf * yf).sum(0)) < 2e-3
+        # dgrad: fold prologue + ReLU activation backward epilogue
+        Ho, Wo = ci.out_hw(H, H, shp)
+        g, yy = make((N, Ho, Wo, Cout), cuda), make((N, Ho, Wo, Cout), cuda)
+        al, be = torch.randn(Cout, device=cuda) * 0.1, torch.randn(Cout, device=cuda) * 0.1
+        gt = (g.float() + al + be * yy.float()).to(BF).float()
+        dref = nhwc(torch.nn.grad.conv2d_input((N, Cin, H, H), w.to(BF).float(), nchw(gt), stride=stride,
+                                               padding=pad))
+        if Cin % tile[1] == 0:
+            xs = (N, H, H, Cin)
+            out, _ = ci.conv_dgrad(g, yy, al, be, wd, shp, xs, epi=ci.EPI_STORE, tile=tile, nsplit=1, kg=2)
+            assert rel(out, dref) < 1e-2, (tile, "dgrad")
+            ex = make(xs, cuda)
+            es, et = torch.rand(Cin, device=cuda) + 0.5, torch.randn(Cin, device=cuda) * 0.3
+            gp = dref * ((ex.float() * es + et) > 0).float()
+            out, part = ci.conv_dgrad(g, yy, al, be, wd, shp, xs, epi=ci.EPI_ACTBWD, ex=ex, es=es, et=et, act=1,
+                                      tile=tile, nsplit=1, kg=2)
+            assert rel(out, gp * es) < 1e-2, (tile, "actbwd")
+            ps = part.sum(0)
+            assert rel(ps[0], (gp * ex.float()).reshape(-1, Cin).sum(0)) < 1e-2
+            assert rel(ps[1], gp.reshape(-1, Cin).sum(0)) < 1e-2
+        # join prologue (1x1 stride-1 only)
+        if k == 1 and stride == 1:
+            yj, rj = make((N, H, H, Cin), cuda), make((N, H, H, Cin), cuda)
+            joined = torch.relu(yj.float() * s + t + rj.float())
+            jref = nhwc(F.conv2d(nchw(joined.to(BF).float()), w.to(BF).float()))
+            jout = torch.empty_like(yj)
+            jmask = torch.zeros(yj.numel() // 8, device=cuda, dtype=torch.uint8)
+            out, _ = ci.conv_fwd_join(yj, rj, s, t, None, None, wf, shp, jout, jmask, tile=tile, nsplit=1, kg=2)
+            assert rel(out, jref) < 1e-2, (tile, "join")
+            assert rel(jout, joined) < 1e-2
