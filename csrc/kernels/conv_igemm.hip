@@ -2,6 +2,8 @@
 // (prologue, epilogue, activation) instantiations: conv_igemm_inst_*.hip).
 #include "conv_igemm_impl.h"
 
+#include <algorithm>
+
 namespace fdt {
 
 // Python-facing launchers.  taps: list of (dh, dw, wt) triples encoded as int8 arrays.
@@ -84,7 +86,8 @@ static void conv_igemm_impl(uint64_t x, uint64_t x2, uint64_t ps, uint64_t pt, u
   if (launch_cases_fwd(pro, epi, act, a, BM, BN, BK, kg, pure, st) ||
       launch_cases_fold(pro, epi, act, a, BM, BN, BK, kg, pure, st) ||
       launch_cases_join(pro, epi, act, a, BM, BN, BK, kg, pure, st) ||
-      launch_cases_plain(pro, epi, act, a, BM, BN, BK, kg, pure, st))
+      launch_cases_plain(pro, epi, act, a, BM, BN, BK, kg, pure, st) ||
+      launch_cases_ffn(pro, epi, act, a, BM, BN, BK, kg, pure, st))
     return;
   FDT_CHECK(false, "unsupported (prologue, epilogue) combination");
 }
@@ -113,6 +116,56 @@ void conv_igemm_join(uint64_t y, uint64_t r, uint64_t s, uint64_t t, uint64_t s2
   conv_igemm_impl(y, r, s, t, s2, w, out, part, part_rows, 0, 0, 0, 0, 0, 0, Nb, H, W, Cx, H, W, 1, z, z, z, Cout, ldw, H,
                   W, 1, 0, 0, conv::kProJoin, kActRelu, 1.f, conv::kEpiStats, 0, 1.f, BM, BN, BK, nsplit, slab, cnt, t2,
                   jout, jmask, kg, stream);
+}
+
+// Transformer FFN GEMMs on the implicit-GEMM kernel (a token GEMM is a 1x1 convolution over
+// M "pixels"): out[M][N] = x[M][K] W[N][K]^T with
+//   epi 5 (GELU_FWD): out = a = acc + bias[N] (bf16), out2 = h = dropout(gelu(a))
+//   epi 6 (GELU_BWD): out = ga = keep*scale*gelu'(a_in)*acc, gb[N] += column sums of ga
+// K must be a power of two >= 8 (d_model), N a multiple of BN.
+void ffn_gemm(uint64_t x, uint64_t w, uint64_t out, long M, int K, int N, int epi, uint64_t bias, uint64_t out2,
+              uint64_t a_in, uint64_t gb, float p, uint64_t seed, uint64_t seed_ptr, int BM, int BN, int BK, int kg,
+              uint64_t stream) {
+  using namespace conv;
+  FDT_CHECK(epi == kEpiGeluFwd || epi == kEpiGeluBwd, "ffn_gemm: epi 5 (GELU_FWD) | 6 (GELU_BWD)");
+  FDT_CHECK(epi != kEpiGeluFwd || (bias != 0 && out2 != 0), "GELU_FWD needs bias and the h output");
+  FDT_CHECK(epi != kEpiGeluBwd || (a_in != 0 && gb != 0), "GELU_BWD needs a and the bias-gradient buffer");
+  FDT_CHECK(p >= 0.f && p < 1.f, "dropout p in [0, 1)");
+  FDT_CHECK(x % 16 == 0 && w % 16 == 0 && out % 16 == 0 && out2 % 16 == 0 && a_in % 16 == 0 && bias % 16 == 0,
+            "ffn_gemm: 16-B aligned operands");
+  ConvArgs a{};
+  a.x = P<const bf16>(x);
+  a.w = P<const bf16>(w);
+  a.out = P<bf16>(out);
+  a.ex = P<const bf16>(a_in);
+  a.fbias = P<const float>(bias);
+  a.out2 = P<bf16>(out2);
+  a.gb = P<float>(gb);
+  a.drop_thr = (uint32_t)std::min((double)p * 4294967296.0, 4294967295.0);
+  a.drop_scale = 1.f / (1.f - p);
+  a.drop_seed = seed;
+  a.drop_seed_ptr = P<const uint64_t>(seed_ptr);
+  FDT_CHECK(K >= 8 && (K & (K - 1)) == 0, "ffn_gemm: K must be a power of two >= 8");
+  FDT_CHECK(N % BN == 0 && N % 8 == 0, "ffn_gemm: N must be a multiple of BN");
+  a.M = M;
+  a.Hi = a.Wi = a.Ho = a.Wo = a.Hout = a.Wout = 1;
+  a.Cx = K;
+  a.log2Cx = 31 - __builtin_clz((unsigned)K);
+  a.S = a.OS = 1;
+  a.ntaps = 1;
+  a.K = K;
+  a.Cout = N;
+  a.ldw = K;
+  a.Nb_HiWi_Cx_bytes = M * (long)K * 2;
+  a.w_bytes = (long)N * K * 2;
+  FDT_CHECK(a.Nb_HiWi_Cx_bytes < 0x7FFFFFF0L && M * (long)N < 0x7FFFFFFFL, "ffn_gemm: operand exceeds 2 GiB");
+  a.nbm = (int)((M + BM - 1) / BM);
+  a.nbn = N / BN;
+  a.nsplit = 1;
+  a.kps = (K + BK - 1) / BK;
+  if (M == 0) return;
+  if (launch_cases_ffn(kProNone, epi, kActNone, a, BM, BN, BK, kg, true, as_stream(stream))) return;
+  FDT_CHECK(false, "ffn_gemm: no instantiation");
 }
 
 int conv_num_row_blocks(long M, int BM) { return (int)((M + BM - 1) / BM); }

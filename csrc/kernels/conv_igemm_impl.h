@@ -34,6 +34,13 @@
 //      EPI_ACTBWD  dgrad through the producer's lazy act(x*s+t): gx = g*act'(z)*s and
 //                  per-channel (sum g_pre*x, sum g_pre) slabs
 //      EPI_STORE / EPI_ADD  plain bf16 store / accumulate into an existing gradient.
+//      EPI_GELU_FWD  the transformer FFN's first linear as a GEMM (x [tokens][d_model] the
+//                  "pixels", W_1 the weights): a = acc + bias stored (bf16, the backward's
+//                  GELU input) AND h = dropout(gelu(a)) stored -- the separate GELU-dropout
+//                  pass (read a, write h) disappears (reference transformer.py:175-176)
+//      EPI_GELU_BWD  the data gradient of the FFN's second linear (g_y W_2 -> dL/dh) finished
+//                  through the GELU-dropout backward: ga = keep*scale*gelu'(a)*acc stored, and
+//                  the column sums of ga = W_1's bias gradient accumulated (fp32 atomics)
 //      EPI_JOINBWD  accumulate into the existing gradient of a residual-block output AND
 //                  run that block's join backward on it: g_pre = g*act'(out) (ReLU bit
 //                  mask or the stored CELU output), stored in place, plus the per-channel
@@ -68,6 +75,7 @@
 #pragma once
 #include "common.h"
 #include "bn_math.h"
+#include "dropout_math.h"
 #include <vector>
 
 namespace fdt {
@@ -77,7 +85,8 @@ typedef short bf16x8_t __attribute__((ext_vector_type(8)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 enum Pro : int { kProNone = 0, kProAffineAct = 1, kProFold = 2, kProJoin = 3 };
-enum Epi : int { kEpiStats = 0, kEpiActBwd = 1, kEpiStore = 2, kEpiAdd = 3, kEpiJoinBwd = 4 };
+enum Epi : int { kEpiStats = 0, kEpiActBwd = 1, kEpiStore = 2, kEpiAdd = 3, kEpiJoinBwd = 4, kEpiGeluFwd = 5,
+                 kEpiGeluBwd = 6 };
 
 struct ConvArgs {
   const bf16* x;     // activation operand [Nb][Hi][Wi][Cx]   (PRO_FOLD: the gradient G)
@@ -100,6 +109,13 @@ struct ConvArgs {
   const uint8_t* jmask;  // JOINBWD: ReLU join bit mask (bit i of byte e/8 = out[e] > 0), or nullptr
   const bf16* jyb;       // JOINBWD: shortcut-branch y (nullptr: identity shortcut)
   const bf16* jout;      // JOINBWD: join output (CELU joins; read when jmask is nullptr)
+  const float* fbias;    // GELU_FWD: per-column bias [Cout]
+  bf16* out2;            // GELU_FWD: h = dropout(gelu(a)) [M][Cout]   (GELU_BWD: a is `ex`)
+  float* gb;             // GELU_BWD: bias-gradient accumulator [Cout] (fp32 atomics)
+  uint32_t drop_thr;     // GELU_*: dropout keep threshold on the 32-bit hash (0: no dropout)
+  float drop_scale;      // 1 / (1 - p)
+  uint64_t drop_seed;    // host seed, XORed with *drop_seed_ptr when set (per-replay word)
+  const uint64_t* drop_seed_ptr;
   long M;            // Nb*Ho*Wo GEMM rows
   int Hi, Wi, Cx, log2Cx;
   int Ho, Wo, S;
@@ -610,6 +626,14 @@ __global__ __launch_bounds__(256 * KG, (KG == 1 ? kMinWavesPerEU<BM, BN, BK, PRO
     const int c = n0 + cg * 8;  // this thread's 8 output channels
     const bool dense = a.OS == 1 && a.oy == 0 && a.ox == 0 && a.Hout == a.Ho && a.Wout == a.Wo;
     float sv[8], tv[8];
+    constexpr bool GELU = EPI == kEpiGeluFwd || EPI == kEpiGeluBwd;
+    uint64_t dseed = 0;
+    if constexpr (GELU) dseed = drop::live_seed(a.drop_seed, a.drop_seed_ptr);
+    if constexpr (EPI == kEpiGeluFwd) {
+      const float4* bp = reinterpret_cast<const float4*>(a.fbias + c);
+      const float4 b0 = bp[0], b1 = bp[1];
+      sv[0] = b0.x; sv[1] = b0.y; sv[2] = b0.z; sv[3] = b0.w; sv[4] = b1.x; sv[5] = b1.y; sv[6] = b1.z; sv[7] = b1.w;
+    }
     if constexpr (EPI == kEpiActBwd) {
       const float4* sp = reinterpret_cast<const float4*>(a.es + c);
       const float4* tp = reinterpret_cast<const float4*>(a.et + c);
@@ -707,12 +731,62 @@ __global__ __launch_bounds__(256 * KG, (KG == 1 ? kMinWavesPerEU<BM, BN, BK, PRO
 #pragma unroll
             for (int k = 0; k < 8; ++k) v[k] += e8[k];
             Vec8<bf16>::store(a.out + e, v);
+          } else if constexpr (EPI == kEpiGeluFwd) {
+            // a = acc + bias, rounded to bf16 as stored (the backward reads the stored a);
+            // h from the rounded a, exactly as the standalone GELU-dropout pass computes it
+            uint32_t pa[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) pa[q] = pk_bf16(v[2 * q] + sv[2 * q], v[2 * q + 1] + sv[2 * q + 1]);
+            *reinterpret_cast<uint4*>(a.out + e) = make_uint4(pa[0], pa[1], pa[2], pa[3]);
+            const uint32_t mk = a.drop_thr ? drop::keep8((long)(e >> 3), dseed, a.drop_thr) : 0xffu;
+            float h[8];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+              h[2 * q] = bf16_lo(pa[q]);
+              h[2 * q + 1] = bf16_hi(pa[q]);
+            }
+#pragma unroll
+            for (int k = 0; k < 8; ++k) h[k] = ((mk >> k) & 1u) ? drop::gelu_erf(h[k]) * a.drop_scale : 0.f;
+            Vec8<bf16>::store(a.out2 + e, h);
+          } else if constexpr (EPI == kEpiGeluBwd) {
+            // ga = keep * scale * gelu'(a) * dL/dh; the bias gradient sums the stored ga
+            float a8[8];
+            Vec8<bf16>::load(a.ex + e, a8);
+            const uint32_t mk = a.drop_thr ? drop::keep8((long)(e >> 3), dseed, a.drop_thr) : 0xffu;
+            uint32_t pg[4];
+#pragma unroll
+            for (int k = 0; k < 8; ++k)
+              v[k] = ((mk >> k) & 1u) ? v[k] * a.drop_scale * drop::gelu_erf_grad(a8[k]) : 0.f;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+              pg[q] = pk_bf16(v[2 * q], v[2 * q + 1]);
+              q0[2 * q] += bf16_lo(pg[q]);
+              q0[2 * q + 1] += bf16_hi(pg[q]);
+            }
+            *reinterpret_cast<uint4*>(a.out + e) = make_uint4(pg[0], pg[1], pg[2], pg[3]);
           } else {
             Vec8<bf16>::store(a.out + e, v);
           }
         }
       }
       if (j + 1 < TM) __syncthreads();  // the next pass overwrites the staging rows
+    }
+    if constexpr (EPI == kEpiGeluBwd) {
+      // column sums of ga: rows of a thread -> lanes sharing its columns -> 4 waves -> one
+      // fp32 atomic per column per workgroup into the bias gradient
+#pragma unroll
+      for (int o = CG; o < 64; o <<= 1) {
+        if (!ew) break;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) q0[k] += __shfl_xor(q0[k], o, 64);
+      }
+      if (ew && lane < CG) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) red[wid * BN + cg * 8 + k] = q0[k];
+      }
+      __syncthreads();
+      for (int e = tid; ew && e < BN; e += 256)
+        atomicAdd(&a.gb[n0 + e], red[e] + red[BN + e] + red[2 * BN + e] + red[3 * BN + e]);
     }
     if constexpr (STATS) {
       // lanes l, l + CG, l + 2CG, ... of a wave hold the same channels
@@ -821,6 +895,8 @@ bool launch_cases_join(int pro, int epi, int act, const ConvArgs& a, int BM, int
                        hipStream_t st);
 bool launch_cases_plain(int pro, int epi, int act, const ConvArgs& a, int BM, int BN, int BK, int kg, bool pure,
                         hipStream_t st);
+bool launch_cases_ffn(int pro, int epi, int act, const ConvArgs& a, int BM, int BN, int BK, int kg, bool pure,
+                      hipStream_t st);
 
 }  // namespace conv
 }  // namespace fdt

@@ -11,33 +11,17 @@
 // Layout: 8 elements per lane (one 16-B bf16 load), one 64-bit hash per 2 elements (its two
 // 32-bit halves), grid-stride loop over n / 8 lane-chunks.
 #include "common.h"
+#include "dropout_math.h"
 
 #include <algorithm>
 
 namespace fdt {
 namespace {
-
-__device__ __forceinline__ uint64_t drop_hash(uint64_t i, uint64_t seed) {
-  uint64_t x = i ^ seed;
-  x ^= x >> 33;
-  x *= 0xff51afd7ed558ccdull;
-  x ^= x >> 33;
-  x *= 0xc4ceb9fe1a85ec53ull;
-  x ^= x >> 33;
-  return x;
-}
-
-// keep mask of the 8 elements [8c, 8c + 8): bit j set = element kept
-__device__ __forceinline__ uint32_t keep8(long c, uint64_t seed, uint32_t thr) {
-  uint32_t m = 0;
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const uint64_t h = drop_hash((uint64_t)c * 4 + j, seed);
-    m |= (uint32_t)((uint32_t)h >= thr) << (2 * j);
-    m |= (uint32_t)((uint32_t)(h >> 32) >= thr) << (2 * j + 1);
-  }
-  return m;
-}
+using drop::drop_hash;
+using drop::keep8;
+using drop::gelu_erf;
+using drop::gelu_erf_grad;
+using drop::live_seed;
 
 __device__ __forceinline__ void unpack8(const uint4 v, float* f) {
   const uint32_t w[4] = {v.x, v.y, v.z, v.w};
@@ -58,17 +42,6 @@ __device__ __forceinline__ uint32_t pack2(float a, float b) {
 
 __device__ __forceinline__ uint4 pack8(const float* f) {
   return make_uint4(pack2(f[0], f[1]), pack2(f[2], f[3]), pack2(f[4], f[5]), pack2(f[6], f[7]));
-}
-
-__device__ __forceinline__ float gelu_erf(float a) { return 0.5f * a * (1.f + erff(a * 0.70710678118654752f)); }
-__device__ __forceinline__ float gelu_erf_grad(float a) {
-  const float cdf = 0.5f * (1.f + erff(a * 0.70710678118654752f));
-  const float pdf = 0.39894228040143268f * __expf(-0.5f * a * a);
-  return cdf + a * pdf;
-}
-
-__device__ __forceinline__ uint64_t live_seed(uint64_t seed, const uint64_t* seed_ptr) {
-  return seed_ptr != nullptr ? (seed ^ *seed_ptr) : seed;
 }
 
 // out = x + keep * y * scale   (y bf16, x / out fp32: the residual stream)

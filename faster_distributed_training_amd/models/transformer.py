@@ -27,6 +27,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
+from ..ops import ffn
 from ..ops.dropout import dropout_add, gelu_dropout
 from ..ops.attention import packed_attention, scaled_dot_product_attention
 from ..ops.embedding import embedding_sum
@@ -168,7 +169,12 @@ class PositionalWiseFFN(nn.Module):
 
     def forward(self, x, fuse_out_bias=False):
         """``fuse_out_bias``: the caller's dropout_add computes w_2's bias gradient (ops/dropout.py
-        ``bias=``); w_1's is always computed inside the GELU-dropout backward."""
+        ``bias=``); w_1's is always computed inside the GELU-dropout backward.  On the GPU the
+        w_1 GEMM carries the bias + GELU + dropout epilogue and w_2's data gradient the
+        GELU-dropout backward (ops/ffn.py)."""
+        if ffn.fusable(x, self.w_1.in_features, self.w_1.out_features):
+            return ffn.ffn_core(x, self.w_1.weight, self.w_1.bias, self.w_2.weight, self.w_2.bias, self.dropout.p,
+                                self.training, out_bias_grad=not fuse_out_bias)
         h = gelu_dropout(linear(x, self.w_1.weight, self.w_1.bias, bias_grad=False), self.dropout.p, self.training,
                          bias=self.w_1.bias)
         return linear(h, self.w_2.weight, self.w_2.bias, bias_grad=not fuse_out_bias)

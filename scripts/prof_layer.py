@@ -17,6 +17,8 @@ ap.add_argument("--shape", default="32,64,64,3,1,1")
 ap.add_argument("--batch", type=int, default=1024)
 ap.add_argument("--tile", default=None)
 ap.add_argument("--reps", type=int, default=5)
+ap.add_argument("--pro", default="affine", choices=["affine", "none"], help="fwd: lazy-BN prologue or a plain operand")
+ap.add_argument("--kg", type=int, default=None)
 a = ap.parse_args()
 H, Cin, Cout, k, s, p = map(int, a.shape.split(","))
 tile = tuple(map(int, a.tile.split(","))) if a.tile else None
@@ -37,7 +39,10 @@ tv = torch.zeros(shp.cxp, device=dev)
 gw = torch.empty(Cout, Cin, k, k, device=dev)
 for _ in range(a.reps):
     if a.op == "fwd":
-        ci.conv_fwd(x, wf, shp, sv, tv, 1, 1.0, tile=tile)
+        if a.pro == "none":
+            ci.conv_fwd(x, wf, shp, None, None, 0, 1.0, tile=tile, kg=a.kg)
+        else:
+            ci.conv_fwd(x, wf, shp, sv, tv, 1, 1.0, tile=tile, kg=a.kg)
     elif a.op == "dgrad":
         ci.conv_dgrad(g, yy, al, be, wd, shp, (N, H, H, Cin), tile=tile)
     else:

@@ -43,3 +43,47 @@ def test_residual_grad_handoff_matches_autograd_sum(cuda, kind):
     assert torch.allclose(gx1, gx0, rtol=1e-5, atol=1e-5), (gx1 - gx0).abs().max()
     for a, b in zip(gp1, gp0):
         assert torch.allclose(a, b, rtol=1e-4, atol=1e-5)
+
+
+@pytest.mark.parametrize("p", [0.0, 0.1])
+@pytest.mark.parametrize("direct", [False, True])
+def test_ffn_fused_epilogues_match_unfused(cuda, p, direct):
+    """ops/ffn.py (w_1 GEMM with the bias + GELU + dropout epilogue, w_2's data gradient with
+    the GELU-dropout backward + b_1 column sums) against the unfused composition (hipBLASLt
+    GEMMs + standalone dropout kernels) on the same dropout draw."""
+    from faster_distributed_training_amd.models import transformer as T
+    from faster_distributed_training_amd.ops import ffn
+    from faster_distributed_training_amd.ops.linear import enable_direct_grads
+    torch.manual_seed(0)
+    m = T.PositionalWiseFFN(512, 1024, p).to(cuda)
+    x = torch.randn(8, 1024, 512, device=cuda).to(torch.bfloat16).requires_grad_(True)
+    g = torch.randn(8, 1024, 512, device=cuda)
+    ffn.FUSED = True
+    assert ffn.fusable(x, 512, 1024)
+
+    def run(fused):
+        ffn.FUSED = fused
+        x.grad = None
+        for q in m.parameters():
+            q.grad = torch.full_like(q, 0.5) if direct else None
+        enable_direct_grads(m.parameters(), direct)
+        torch.manual_seed(5)
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            y = m(x)
+        y.float().backward(g)
+        torch.cuda.synchronize()
+        return y.detach().float(), x.grad.float().clone(), [q.grad.clone() for q in m.parameters()]
+
+    try:
+        y0, gx0, gp0 = run(False)
+        y1, gx1, gp1 = run(True)
+    finally:
+        ffn.FUSED = True
+        enable_direct_grads(m.parameters(), False)
+
+    def rel(a, b):
+        return ((a - b).norm() / b.norm()).item()
+    assert rel(y1, y0) < 1e-2, rel(y1, y0)
+    assert rel(gx1, gx0) < 2e-2, rel(gx1, gx0)
+    for a_, b_, name in zip(gp1, gp0, ["w1", "b1", "w2", "b2"]):
+        assert rel(a_, b_) < 2e-2, (name, rel(a_, b_))
