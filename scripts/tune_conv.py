@@ -34,6 +34,8 @@ def main():
     ap.add_argument("--batches", type=int, nargs="+", default=[1024, 128])
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--max-m", type=int, default=0, help="only shapes with N*Ho*Wo <= this (0 = all)")
+    ap.add_argument("--ksize", type=int, default=0, help="only kernels of this size (0 = all)")
+    ap.add_argument("--ops", default="fwd,dgrad,wgrad", help="which ops to sweep")
     ap.add_argument("--splits", type=int, nargs="+", default=[1, 2, 4, 8],
                     help="split-K candidates for fwd/dgrad when the tile grid is small")
     ap.add_argument("--kg", type=int, nargs="+", default=[1, 2],
@@ -55,6 +57,9 @@ def main():
             Ho0, Wo0 = ci.out_hw(H, H, shp)
             if a.max_m and N * Ho0 * Wo0 > a.max_m:
                 continue
+            if a.ksize and k != a.ksize:
+                continue
+            ops = set(a.ops.split(","))
             torch.manual_seed(0)
             x = torch.randn(N, H, H, shp.cxp, device=dev).to(torch.bfloat16)
             w = torch.randn(Cout, Cin, k, k, device=dev) / (Cin * k * k) ** 0.5
@@ -95,12 +100,12 @@ def main():
 
             # modes the fused engine actually launches (ops/resnet_fused.py): 3x3 convs get a
             # materialised input / pre-folded gradient; 1x1 convs fuse the transforms
-            fwd_modes = [0] if k > 1 else [0, 1]
+            fwd_modes = ([0] if k > 1 else [0, 1]) if "fwd" in ops else []
             for pro in fwd_modes:
                 sweep(f"fwd{pro}", lambda t, ns, kg: ci.conv_fwd(x, wf, shp, sv if pro else None, tv if pro else None,
                                                                   pro, 1.0, tile=t, nsplit=ns, kg=kg),
                       FWD_TILES, lambda t: Cout % t[1] == 0, N * Ho * Wo, Cout)
-            if Cin >= 8:
+            if Cin >= 8 and "dgrad" in ops:
                 dg = [(0, ci.EPI_ACTBWD)] if k > 1 else [(2, ci.EPI_ACTBWD), (2, ci.EPI_STORE)]
                 for pro, epi in dg:
                     sweep(f"dgrad{pro}{epi}",
@@ -113,6 +118,8 @@ def main():
             wg_modes = [(0, 0)] if k > 1 else [(1, 1), (1, 0)]
             if Cin < 8:
                 wg_modes = [(1, 0)]
+            if "wgrad" not in ops:
+                wg_modes = []
             for fold, xaff in wg_modes:
                 best = None
                 for t in WG_TILES:
