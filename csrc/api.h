@@ -131,7 +131,6 @@ void dropout_bwd_colsum(uint64_t g, uint64_t gy, uint64_t gb, long rows, int col
 void gelu_dropout_bwd_colsum(uint64_t g, uint64_t a, uint64_t ga, uint64_t gb, long rows, int cols, float p,
                              uint64_t seed, uint64_t seed_ptr, uint64_t stream);
 // ngd.hip
-void ngd_wupdate(uint64_t A, uint64_t J, uint64_t wc, uint64_t W, int G, int R, int D, uint64_t stream);
 void ngd_sumsq(uint64_t X, long per, int G, uint64_t out, uint64_t stream);
 bool ngd_small_supported(int D, int R);
 bool ngd_proj_supported(int D, int R);

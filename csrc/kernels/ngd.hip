@@ -131,62 +131,6 @@ __global__ __launch_bounds__(256) void ngd_post_eigh_kernel(const float* __restr
   }
 }
 
-// ---------------------------------------------------------------- W update
-// W <- A (J + wc (.) W) in place (reference ngd_optimizer.py:315-322: W_t+1 = A B with
-// B = J + wc * W).  PyTorch needs an addcmul pass plus a batched fp32 GEMM of [R x R] x
-// [R x D] per (shape group, axis) -- ~40 us per call at R = 80 for ~60 MFLOP, the library's
-// 256 x 80 tiles leaving most of the chip idle.  Here one workgroup owns one 64-column block
-// of one preconditioner's W for ALL R rows: it stages A (R x R) and that block of B in LDS
-// (reading the block of W before any write, so the update is safely in place; blocks are
-// disjoint), then each thread accumulates R/4 rows of one column in fp32 registers.
-constexpr int kWuCols = 64;
-constexpr int kWuRowsPerThread = kNgdMaxR / 4;
-
-__global__ __launch_bounds__(256) void ngd_wupdate_kernel(const float* __restrict__ A, const float* __restrict__ J,
-                                                          const float* __restrict__ wc, float* __restrict__ W, int R,
-                                                          int D, int dblocks) {
-  extern __shared__ float wsm[];
-  float* sA = wsm;                     // [R][R + 1]
-  float* sB = sA + R * (R + 1);        // [R][kWuCols + 4]
-  constexpr int LB = kWuCols + 4;
-  const int g = blockIdx.x / dblocks, db = blockIdx.x - (blockIdx.x / dblocks) * dblocks;
-  const int d0 = db * kWuCols;
-  const int tid = threadIdx.x;
-  const float* Ag = A + (long)g * R * R;
-  const float* Jg = J + (long)g * R * D;
-  float* Wg = W + (long)g * R * D;
-  for (int e = tid; e < R * R; e += 256) {
-    const int i = e / R, k = e - i * R;
-    sA[i * (R + 1) + k] = Ag[e];
-  }
-  for (int e = tid; e < R * kWuCols; e += 256) {
-    const int k = e / kWuCols, dd = e - k * kWuCols;
-    const int d = d0 + dd;
-    sB[k * LB + dd] = d < D ? Jg[(long)k * D + d] + wc[(long)g * R + k] * Wg[(long)k * D + d] : 0.f;
-  }
-  __syncthreads();  // every read of this W block happened: the writes below are in place
-  const int dd = tid & (kWuCols - 1), r0 = tid >> 6;
-  float acc[kWuRowsPerThread];
-#pragma unroll
-  for (int i = 0; i < kWuRowsPerThread; ++i) acc[i] = 0.f;
-  for (int k = 0; k < R; ++k) {
-    const float b = sB[k * LB + dd];
-#pragma unroll
-    for (int i = 0; i < kWuRowsPerThread; ++i) {
-      const int r = r0 + 4 * i;
-      if (r < R) acc[i] = fmaf(sA[r * (R + 1) + k], b, acc[i]);  // wave-uniform row: LDS broadcast
-    }
-  }
-  const int d = d0 + dd;
-  if (d < D) {
-#pragma unroll
-    for (int i = 0; i < kWuRowsPerThread; ++i) {
-      const int r = r0 + 4 * i;
-      if (r < R) Wg[(long)r * D + d] = acc[i];
-    }
-  }
-}
-
 // ---------------------------------------------------------------- norm-preserving rescale
 // The preconditioned direction keeps the Frobenius norm of the input per matrix g
 // (reference ngd_optimizer.py:151-168):  Y <- isnan(|Y|^2) ? X : Y * sqrt(|X|^2 / |Y|^2).
@@ -989,22 +933,4 @@ void ngd_post_eigh(uint64_t c, uint64_t U, uint64_t ise, uint64_t drho, uint64_t
   FDT_LAUNCH_CHECK();
 }
 
-}  // namespace fdt
-
-namespace fdt {
-void ngd_wupdate(uint64_t A, uint64_t J, uint64_t wc, uint64_t W, int G, int R, int D, uint64_t stream) {
-  FDT_CHECK(R >= 1 && R <= kNgdMaxR && D >= 1, "ngd_wupdate: 1 <= R <= 128");
-  if (G == 0) return;
-  const int dblocks = (D + kWuCols - 1) / kWuCols;
-  const size_t lds = ((size_t)R * (R + 1) + (size_t)R * (kWuCols + 4)) * sizeof(float);
-  static size_t attr_set = 64 * 1024;
-  if (lds > attr_set) {
-    FDT_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(ngd_wupdate_kernel),
-                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-    attr_set = lds;
-  }
-  ngd_wupdate_kernel<<<(unsigned)((long)G * dblocks), 256, lds, as_stream(stream)>>>(
-      P<const float>(A), P<const float>(J), P<const float>(wc), P<float>(W), R, D, dblocks);
-  FDT_LAUNCH_CHECK();
-}
 }  // namespace fdt

@@ -319,13 +319,8 @@ class NGState:
                           zs.data_ptr(), dsum.data_ptr(), tr.data_ptr(), self.d.data_ptr(), self.rho.data_ptr(),
                           A.data_ptr(), wc.data_ptr(), G, R, self.alpha, self.eta, float(N), float(D),
                           _native.stream_ptr())
-        if hasattr(nat, "ngd_wupdate") and self.W.is_contiguous():
-            # W <- A (J + wc W) in one launch, in place (csrc/kernels/ngd.hip ngd_wupdate)
-            nat.ngd_wupdate(A.data_ptr(), J.contiguous().data_ptr(), wc.data_ptr(), self.W.data_ptr(), G, R, D,
-                            _native.stream_ptr())
-        else:
-            B = torch.addcmul(J, wc.unsqueeze(2), self.W)         # J + wc W
-            torch.bmm(A, B, out=self.W)                           # W <- A B (in place)
+        B = torch.addcmul(J, wc.unsqueeze(2), self.W)             # J + wc W
+        torch.bmm(A, B, out=self.W)                               # W <- A B (in place)
 
     # ------------------------------------------------- tiny-dim axes (HIP, no transposes)
     def small_ok(self, G: torch.Tensor) -> bool:

@@ -642,20 +642,3 @@ def test_ngd_step_bitwise_repeatable(cuda):
 
     assert torch.equal(run(), run())
 
-
-@pytest.mark.parametrize("G,R,D", [(3, 80, 4608), (5, 80, 64), (2, 17, 100), (1, 128, 513), (7, 80, 80)])
-def test_ngd_wupdate_in_place_vs_torch(cuda, G, R, D):
-    """ngd_wupdate: W <- A (J + wc W) in place, against torch.bmm / addcmul in fp32 (column
-    blocks of 64 with a ragged tail, R up to the 128 maximum)."""
-    from faster_distributed_training_amd.ops import _native
-    torch.manual_seed(7)
-    A = torch.randn(G, R, R, device=cuda) / R ** 0.5
-    J = torch.randn(G, R, D, device=cuda)
-    wc = torch.rand(G, R, device=cuda) * 3
-    W = torch.randn(G, R, D, device=cuda)
-    ref = torch.bmm(A.double(), (J + wc.unsqueeze(2) * W).double()).float()
-    Wk = W.clone()
-    _native.native().ngd_wupdate(A.data_ptr(), J.data_ptr(), wc.data_ptr(), Wk.data_ptr(), G, R, D,
-                                 _native.stream_ptr())
-    torch.cuda.synchronize()
-    assert rel(Wk, ref) < 1e-5, rel(Wk, ref)
