@@ -92,11 +92,6 @@ void conv_igemm_join(uint64_t y, uint64_t r, uint64_t s, uint64_t t, uint64_t s2
 void ffn_gemm(uint64_t x, uint64_t w, uint64_t out, long M, int K, int N, int epi, uint64_t bias, uint64_t out2,
               uint64_t a_in, uint64_t gb, float p, uint64_t seed, uint64_t seed_ptr, int BM, int BN, int BK, int kg,
               uint64_t stream);
-bool conv3x3_halo_supported(long Nb, int H, int W, int Cx, int Cout, int BN);
-void conv3x3_halo(uint64_t x, uint64_t w, uint64_t out, uint64_t part, int part_rows, uint64_t ex, uint64_t es,
-                  uint64_t et, long Nb, int H, int W, int Cx, int Cout, int ldw, const std::vector<int>& dh,
-                  const std::vector<int>& dw, const std::vector<int>& wt, int epi, int act, float alpha, int BN,
-                  uint64_t stream);
 int conv_num_row_blocks(long M, int BM);
 std::vector<long> conv_splitk_workspace(long M, int Cout, int BM, int BN, int nsplit);
 // conv_wgrad.hip

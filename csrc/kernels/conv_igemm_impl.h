@@ -211,228 +211,6 @@ constexpr int kMinWavesPerEU =
     (BM == 128 && BN == 128 && BK == 32 && (PRO == kProNone || (PRO == kProAffineAct && PURE))) ? 4
     : (BM == 128 && BN == 128 && (BK == 32 || (PRO != 2 && PRO != 3))) ? 3 : 1;
 
-// The fused epilogue shared by the implicit-GEMM kernel and the 3x3 halo kernel
-// (conv3x3_halo.hip): both hold the accumulators as acc[TN][TM] of a 2 x 2 wave grid over a
-// BM x BN (pixels x channels) tile.  ``grp`` != 0: a K group that only meets the barriers.
-template <int BM, int BN, int EPI, int ACT, int TN, int TM>
-__device__ __forceinline__ void igemm_epilogue(const ConvArgs& a, f32x16 (&acc)[TN][TM], char* smem, int hdr,
-                                               float* red, long m0, int n0, int bm, int grp, float inv_alpha) {
-  const int tid = threadIdx.x & 255, lane = tid & 63, wid = tid >> 6;
-  const int wn = wid & 1, wm = wid >> 1;
-  constexpr int NQ = EPI == kEpiJoinBwd ? 3 : 2;
-  // The accumulators are transposed through LDS before touching memory: a lane's MFMA
-  // result is 8 channels of ONE pixel, so a direct store / load covers 32 pixels x 32 B per
-  // wave instruction (32 partial cache lines).  Staged as fp32 rows [64 pixels][BN] (one
-  // pass per 32-pixel block j), each thread then owns 8 channels of whole rows and every
-  // wave instruction moves full contiguous 128-256 B row segments; per-channel statistics
-  // reduce over a thread's rows, then across the lanes sharing its channels (shuffles),
-  // then across the 4 waves in LDS.  Rows padded by 4 floats: conflict-free ds_write_b128
-  // of the accumulator layout and ds_read_b128 of the row layout.
-  {
-    constexpr int SW = BN + 4;     // staged row stride (floats)
-    constexpr int CG = BN / 8;     // 8-channel groups per row
-    constexpr int RPS = 256 / CG;  // rows per sweep
-    constexpr int NSW = 64 / RPS;  // sweeps per 64-row pass
-    constexpr bool STATS = EPI == kEpiStats || EPI == kEpiActBwd || EPI == kEpiJoinBwd;
-    const int h = lane >> 5;
-    float* stg = reinterpret_cast<float*>(smem + hdr);
-    const int cg = tid % CG, rs = tid / CG;
-    const int c = n0 + cg * 8;  // this thread's 8 output channels
-    const bool dense = a.OS == 1 && a.oy == 0 && a.ox == 0 && a.Hout == a.Ho && a.Wout == a.Wo;
-    float sv[8], tv[8];
-    constexpr bool GELU = EPI == kEpiGeluFwd || EPI == kEpiGeluBwd;
-    uint64_t dseed = 0;
-    if constexpr (GELU) dseed = drop::live_seed(a.drop_seed, a.drop_seed_ptr);
-    if constexpr (EPI == kEpiGeluFwd) {
-      const float4* bp = reinterpret_cast<const float4*>(a.fbias + c);
-      const float4 b0 = bp[0], b1 = bp[1];
-      sv[0] = b0.x; sv[1] = b0.y; sv[2] = b0.z; sv[3] = b0.w; sv[4] = b1.x; sv[5] = b1.y; sv[6] = b1.z; sv[7] = b1.w;
-    }
-    if constexpr (EPI == kEpiActBwd) {
-      const float4* sp = reinterpret_cast<const float4*>(a.es + c);
-      const float4* tp = reinterpret_cast<const float4*>(a.et + c);
-      const float4 s0 = sp[0], s1 = sp[1], t0 = tp[0], t1 = tp[1];
-      sv[0] = s0.x; sv[1] = s0.y; sv[2] = s0.z; sv[3] = s0.w; sv[4] = s1.x; sv[5] = s1.y; sv[6] = s1.z; sv[7] = s1.w;
-      tv[0] = t0.x; tv[1] = t0.y; tv[2] = t0.z; tv[3] = t0.w; tv[4] = t1.x; tv[5] = t1.y; tv[6] = t1.z; tv[7] = t1.w;
-    }
-    float q0[8], q1[8], q2[8];
-#pragma unroll
-    for (int k = 0; k < 8; ++k) { q0[k] = 0.f; q1[k] = 0.f; q2[k] = 0.f; }
-    // K group 1 (KG == 2) only meets the barriers below; group 0 owns the whole epilogue
-    const bool ew = grp == 0;
-    __syncthreads();  // every wave is done with the K tiles (and the split-K flag)
-#pragma unroll
-    for (int j = 0; j < TM; ++j) {
-      // ---- stage accumulator block j: local row = wm*32 + pixel, 8 channels per (i, p)
-#pragma unroll
-      for (int i = 0; i < TN; ++i) {
-        if (!ew) break;
-#pragma unroll
-        for (int p = 0; p < 2; ++p) {
-          const int g = 2 * p;
-          float v[8];
-#pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            float lo = acc[i][j][4 * g + q], hi = acc[i][j][4 * g + 4 + q];
-            swap32(lo, hi);
-            v[q] = lo;
-            v[4 + q] = hi;
-          }
-          float* dst = stg + (wm * 32 + (lane & 31)) * SW + wn * (BN / 2) + i * 32 + 16 * p + 8 * h;
-          *reinterpret_cast<float4*>(dst) = make_float4(v[0], v[1], v[2], v[3]);
-          *reinterpret_cast<float4*>(dst + 4) = make_float4(v[4], v[5], v[6], v[7]);
-        }
-      }
-      __syncthreads();
-      // ---- rows of this pass: 8 channels x NSW rows per thread
-#pragma unroll
-      for (int sw = 0; sw < NSW; ++sw) {
-        const int lr = rs + sw * RPS;
-        const long m = m0 + (lr >> 5) * (BM / 2) + j * 32 + (lr & 31);
-        if (ew && m < a.M) {
-          uint32_t orow;
-          if (dense) {
-            orow = (uint32_t)m;
-          } else {
-            const int mi = (int)m, hw = a.Ho * a.Wo;
-            const int n = mi / hw, rem = mi - n * hw;
-            const int oh = rem / a.Wo, ow = rem - oh * a.Wo;
-            orow = (uint32_t)((n * a.Hout + oh * a.OS + a.oy) * a.Wout + ow * a.OS + a.ox);
-          }
-          const uint32_t e = orow * (uint32_t)a.Cout + c;
-          const float4 va = *reinterpret_cast<const float4*>(stg + lr * SW + cg * 8);
-          const float4 vb = *reinterpret_cast<const float4*>(stg + lr * SW + cg * 8 + 4);
-          float v[8] = {va.x, va.y, va.z, va.w, vb.x, vb.y, vb.z, vb.w};
-          if constexpr (EPI == kEpiStats) {
-#pragma unroll
-            for (int k = 0; k < 8; ++k) { q0[k] += v[k]; q1[k] = fmaf(v[k], v[k], q1[k]); }
-            Vec8<bf16>::store(a.out + e, v);
-          } else if constexpr (EPI == kEpiActBwd) {
-            float x8[8];
-            Vec8<bf16>::load(a.ex + e, x8);
-#pragma unroll
-            for (int k = 0; k < 8; ++k) {
-              const float gp = v[k] * actg<ACT>(fmaf(x8[k], sv[k], tv[k]), inv_alpha);
-              v[k] = gp * sv[k];
-              q0[k] = fmaf(gp, x8[k], q0[k]);
-              q1[k] += gp;
-            }
-            Vec8<bf16>::store(a.out + e, v);
-          } else if constexpr (EPI == kEpiJoinBwd) {
-            float e8[8], ya[8], yb[8], o8[8];
-            Vec8<bf16>::load(a.out + e, e8);
-            Vec8<bf16>::load(a.ex + e, ya);
-            const bool hb = a.jyb != nullptr;
-            if (hb) Vec8<bf16>::load(a.jyb + e, yb);
-            uint32_t mk = 0;
-            if constexpr (ACT == kActRelu) mk = a.jmask[e >> 3];
-            else Vec8<bf16>::load(a.jout + e, o8);
-#pragma unroll
-            for (int k = 0; k < 8; ++k) {
-              const float gv = v[k] + e8[k];
-              float gp;
-              if constexpr (ACT == kActRelu) gp = ((mk >> k) & 1u) ? gv : 0.f;
-              else gp = gv * actg_out<ACT>(o8[k], inv_alpha);
-              v[k] = gp;
-              q0[k] = fmaf(gp, ya[k], q0[k]);
-              q1[k] += gp;
-              if (hb) q2[k] = fmaf(gp, yb[k], q2[k]);
-            }
-            Vec8<bf16>::store(a.out + e, v);
-          } else if constexpr (EPI == kEpiAdd) {
-            float e8[8];
-            Vec8<bf16>::load(a.out + e, e8);
-#pragma unroll
-            for (int k = 0; k < 8; ++k) v[k] += e8[k];
-            Vec8<bf16>::store(a.out + e, v);
-          } else if constexpr (EPI == kEpiGeluFwd) {
-            // a = acc + bias, rounded to bf16 as stored (the backward reads the stored a);
-            // h from the rounded a, exactly as the standalone GELU-dropout pass computes it
-            uint32_t pa[4];
-#pragma unroll
-            for (int q = 0; q < 4; ++q) pa[q] = pk_bf16(v[2 * q] + sv[2 * q], v[2 * q + 1] + sv[2 * q + 1]);
-            *reinterpret_cast<uint4*>(a.out + e) = make_uint4(pa[0], pa[1], pa[2], pa[3]);
-            const uint32_t mk = a.drop_thr ? drop::keep8((long)(e >> 3), dseed, a.drop_thr) : 0xffu;
-            float h[8];
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-              h[2 * q] = bf16_lo(pa[q]);
-              h[2 * q + 1] = bf16_hi(pa[q]);
-            }
-#pragma unroll
-            for (int k = 0; k < 8; ++k) h[k] = ((mk >> k) & 1u) ? drop::gelu_erf(h[k]) * a.drop_scale : 0.f;
-            Vec8<bf16>::store(a.out2 + e, h);
-          } else if constexpr (EPI == kEpiGeluBwd) {
-            // ga = keep * scale * gelu'(a) * dL/dh; the bias gradient sums the stored ga
-            float a8[8];
-            Vec8<bf16>::load(a.ex + e, a8);
-            const uint32_t mk = a.drop_thr ? drop::keep8((long)(e >> 3), dseed, a.drop_thr) : 0xffu;
-            uint32_t pg[4];
-#pragma unroll
-            for (int k = 0; k < 8; ++k)
-              v[k] = ((mk >> k) & 1u) ? v[k] * a.drop_scale * drop::gelu_erf_grad(a8[k]) : 0.f;
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-              pg[q] = pk_bf16(v[2 * q], v[2 * q + 1]);
-              q0[2 * q] += bf16_lo(pg[q]);
-              q0[2 * q + 1] += bf16_hi(pg[q]);
-            }
-            *reinterpret_cast<uint4*>(a.out + e) = make_uint4(pg[0], pg[1], pg[2], pg[3]);
-          } else {
-            Vec8<bf16>::store(a.out + e, v);
-          }
-        }
-      }
-      if (j + 1 < TM) __syncthreads();  // the next pass overwrites the staging rows
-    }
-    if constexpr (EPI == kEpiGeluBwd) {
-      // column sums of ga: rows of a thread -> lanes sharing its columns -> 4 waves -> one
-      // fp32 atomic per column per workgroup into the bias gradient
-#pragma unroll
-      for (int o = CG; o < 64; o <<= 1) {
-        if (!ew) break;
-#pragma unroll
-        for (int k = 0; k < 8; ++k) q0[k] += __shfl_xor(q0[k], o, 64);
-      }
-      if (ew && lane < CG) {
-#pragma unroll
-        for (int k = 0; k < 8; ++k) red[wid * BN + cg * 8 + k] = q0[k];
-      }
-      __syncthreads();
-      for (int e = tid; ew && e < BN; e += 256)
-        atomicAdd(&a.gb[n0 + e], red[e] + red[BN + e] + red[2 * BN + e] + red[3 * BN + e]);
-    }
-    if constexpr (STATS) {
-      // lanes l, l + CG, l + 2CG, ... of a wave hold the same channels
-#pragma unroll
-      for (int o = CG; o < 64; o <<= 1) {
-        if (!ew) break;
-#pragma unroll
-        for (int k = 0; k < 8; ++k) {
-          q0[k] += __shfl_xor(q0[k], o, 64);
-          q1[k] += __shfl_xor(q1[k], o, 64);
-          if constexpr (NQ == 3) q2[k] += __shfl_xor(q2[k], o, 64);
-        }
-      }
-      if (ew && lane < CG) {
-        float* rw = red + wid * NQ * BN + cg * 8;
-#pragma unroll
-        for (int k = 0; k < 8; ++k) {
-          rw[k] = q0[k];
-          rw[BN + k] = q1[k];
-          if constexpr (NQ == 3) rw[2 * BN + k] = q2[k];
-        }
-      }
-      __syncthreads();
-      for (int e = tid; ew && e < NQ * BN; e += 256) {
-        const float t = red[e] + red[NQ * BN + e] + red[2 * NQ * BN + e] + red[3 * NQ * BN + e];
-        const int q = e / BN, cc2 = e - q * BN;
-        atomicAdd(&a.part[((long)(bm & a.slot_mask) * NQ + q) * a.Cout + n0 + cc2], t);
-      }
-    }
-  }
-}
-
 template <int BM, int BN, int BK, int PRO, int EPI, bool PURE, int ACT, int KG>
 __global__ __launch_bounds__(256 * KG, (KG == 1 ? kMinWavesPerEU<BM, BN, BK, PRO, PURE> : 1)) void igemm_kernel(
     const ConvArgs a) {
@@ -828,7 +606,217 @@ __global__ __launch_bounds__(256 * KG, (KG == 1 ? kMinWavesPerEU<BM, BN, BK, PRO
   }
 
   // ------------------------------------------------------------------ epilogue
-  igemm_epilogue<BM, BN, EPI, ACT, TN, TM>(a, acc, smem, hdr, red, m0, n0, bm, grp, inv_alpha);
+  // The accumulators are transposed through LDS before touching memory: a lane's MFMA
+  // result is 8 channels of ONE pixel, so a direct store / load covers 32 pixels x 32 B per
+  // wave instruction (32 partial cache lines).  Staged as fp32 rows [64 pixels][BN] (one
+  // pass per 32-pixel block j), each thread then owns 8 channels of whole rows and every
+  // wave instruction moves full contiguous 128-256 B row segments; per-channel statistics
+  // reduce over a thread's rows, then across the lanes sharing its channels (shuffles),
+  // then across the 4 waves in LDS.  Rows padded by 4 floats: conflict-free ds_write_b128
+  // of the accumulator layout and ds_read_b128 of the row layout.
+  {
+    constexpr int SW = BN + 4;     // staged row stride (floats)
+    constexpr int CG = BN / 8;     // 8-channel groups per row
+    constexpr int RPS = 256 / CG;  // rows per sweep
+    constexpr int NSW = 64 / RPS;  // sweeps per 64-row pass
+    constexpr bool STATS = EPI == kEpiStats || EPI == kEpiActBwd || EPI == kEpiJoinBwd;
+    const int h = lane >> 5;
+    float* stg = reinterpret_cast<float*>(smem + hdr);
+    const int cg = tid % CG, rs = tid / CG;
+    const int c = n0 + cg * 8;  // this thread's 8 output channels
+    const bool dense = a.OS == 1 && a.oy == 0 && a.ox == 0 && a.Hout == a.Ho && a.Wout == a.Wo;
+    float sv[8], tv[8];
+    constexpr bool GELU = EPI == kEpiGeluFwd || EPI == kEpiGeluBwd;
+    uint64_t dseed = 0;
+    if constexpr (GELU) dseed = drop::live_seed(a.drop_seed, a.drop_seed_ptr);
+    if constexpr (EPI == kEpiGeluFwd) {
+      const float4* bp = reinterpret_cast<const float4*>(a.fbias + c);
+      const float4 b0 = bp[0], b1 = bp[1];
+      sv[0] = b0.x; sv[1] = b0.y; sv[2] = b0.z; sv[3] = b0.w; sv[4] = b1.x; sv[5] = b1.y; sv[6] = b1.z; sv[7] = b1.w;
+    }
+    if constexpr (EPI == kEpiActBwd) {
+      const float4* sp = reinterpret_cast<const float4*>(a.es + c);
+      const float4* tp = reinterpret_cast<const float4*>(a.et + c);
+      const float4 s0 = sp[0], s1 = sp[1], t0 = tp[0], t1 = tp[1];
+      sv[0] = s0.x; sv[1] = s0.y; sv[2] = s0.z; sv[3] = s0.w; sv[4] = s1.x; sv[5] = s1.y; sv[6] = s1.z; sv[7] = s1.w;
+      tv[0] = t0.x; tv[1] = t0.y; tv[2] = t0.z; tv[3] = t0.w; tv[4] = t1.x; tv[5] = t1.y; tv[6] = t1.z; tv[7] = t1.w;
+    }
+    float q0[8], q1[8], q2[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) { q0[k] = 0.f; q1[k] = 0.f; q2[k] = 0.f; }
+    // K group 1 (KG == 2) only meets the barriers below; group 0 owns the whole epilogue
+    const bool ew = grp == 0;
+    __syncthreads();  // every wave is done with the K tiles (and the split-K flag)
+#pragma unroll
+    for (int j = 0; j < TM; ++j) {
+      // ---- stage accumulator block j: local row = wm*32 + pixel, 8 channels per (i, p)
+#pragma unroll
+      for (int i = 0; i < TN; ++i) {
+        if (!ew) break;
+#pragma unroll
+        for (int p = 0; p < 2; ++p) {
+          const int g = 2 * p;
+          float v[8];
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            float lo = acc[i][j][4 * g + q], hi = acc[i][j][4 * g + 4 + q];
+            swap32(lo, hi);
+            v[q] = lo;
+            v[4 + q] = hi;
+          }
+          float* dst = stg + (wm * 32 + (lane & 31)) * SW + wn * (BN / 2) + i * 32 + 16 * p + 8 * h;
+          *reinterpret_cast<float4*>(dst) = make_float4(v[0], v[1], v[2], v[3]);
+          *reinterpret_cast<float4*>(dst + 4) = make_float4(v[4], v[5], v[6], v[7]);
+        }
+      }
+      __syncthreads();
+      // ---- rows of this pass: 8 channels x NSW rows per thread
+#pragma unroll
+      for (int sw = 0; sw < NSW; ++sw) {
+        const int lr = rs + sw * RPS;
+        const long m = m0 + (lr >> 5) * (BM / 2) + j * 32 + (lr & 31);
+        if (ew && m < a.M) {
+          uint32_t orow;
+          if (dense) {
+            orow = (uint32_t)m;
+          } else {
+            const int mi = (int)m, hw = a.Ho * a.Wo;
+            const int n = mi / hw, rem = mi - n * hw;
+            const int oh = rem / a.Wo, ow = rem - oh * a.Wo;
+            orow = (uint32_t)((n * a.Hout + oh * a.OS + a.oy) * a.Wout + ow * a.OS + a.ox);
+          }
+          const uint32_t e = orow * (uint32_t)a.Cout + c;
+          const float4 va = *reinterpret_cast<const float4*>(stg + lr * SW + cg * 8);
+          const float4 vb = *reinterpret_cast<const float4*>(stg + lr * SW + cg * 8 + 4);
+          float v[8] = {va.x, va.y, va.z, va.w, vb.x, vb.y, vb.z, vb.w};
+          if constexpr (EPI == kEpiStats) {
+#pragma unroll
+            for (int k = 0; k < 8; ++k) { q0[k] += v[k]; q1[k] = fmaf(v[k], v[k], q1[k]); }
+            Vec8<bf16>::store(a.out + e, v);
+          } else if constexpr (EPI == kEpiActBwd) {
+            float x8[8];
+            Vec8<bf16>::load(a.ex + e, x8);
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+              const float gp = v[k] * actg<ACT>(fmaf(x8[k], sv[k], tv[k]), inv_alpha);
+              v[k] = gp * sv[k];
+              q0[k] = fmaf(gp, x8[k], q0[k]);
+              q1[k] += gp;
+            }
+            Vec8<bf16>::store(a.out + e, v);
+          } else if constexpr (EPI == kEpiJoinBwd) {
+            float e8[8], ya[8], yb[8], o8[8];
+            Vec8<bf16>::load(a.out + e, e8);
+            Vec8<bf16>::load(a.ex + e, ya);
+            const bool hb = a.jyb != nullptr;
+            if (hb) Vec8<bf16>::load(a.jyb + e, yb);
+            uint32_t mk = 0;
+            if constexpr (ACT == kActRelu) mk = a.jmask[e >> 3];
+            else Vec8<bf16>::load(a.jout + e, o8);
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+              const float gv = v[k] + e8[k];
+              float gp;
+              if constexpr (ACT == kActRelu) gp = ((mk >> k) & 1u) ? gv : 0.f;
+              else gp = gv * actg_out<ACT>(o8[k], inv_alpha);
+              v[k] = gp;
+              q0[k] = fmaf(gp, ya[k], q0[k]);
+              q1[k] += gp;
+              if (hb) q2[k] = fmaf(gp, yb[k], q2[k]);
+            }
+            Vec8<bf16>::store(a.out + e, v);
+          } else if constexpr (EPI == kEpiAdd) {
+            float e8[8];
+            Vec8<bf16>::load(a.out + e, e8);
+#pragma unroll
+            for (int k = 0; k < 8; ++k) v[k] += e8[k];
+            Vec8<bf16>::store(a.out + e, v);
+          } else if constexpr (EPI == kEpiGeluFwd) {
+            // a = acc + bias, rounded to bf16 as stored (the backward reads the stored a);
+            // h from the rounded a, exactly as the standalone GELU-dropout pass computes it
+            uint32_t pa[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) pa[q] = pk_bf16(v[2 * q] + sv[2 * q], v[2 * q + 1] + sv[2 * q + 1]);
+            *reinterpret_cast<uint4*>(a.out + e) = make_uint4(pa[0], pa[1], pa[2], pa[3]);
+            const uint32_t mk = a.drop_thr ? drop::keep8((long)(e >> 3), dseed, a.drop_thr) : 0xffu;
+            float h[8];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+              h[2 * q] = bf16_lo(pa[q]);
+              h[2 * q + 1] = bf16_hi(pa[q]);
+            }
+#pragma unroll
+            for (int k = 0; k < 8; ++k) h[k] = ((mk >> k) & 1u) ? drop::gelu_erf(h[k]) * a.drop_scale : 0.f;
+            Vec8<bf16>::store(a.out2 + e, h);
+          } else if constexpr (EPI == kEpiGeluBwd) {
+            // ga = keep * scale * gelu'(a) * dL/dh; the bias gradient sums the stored ga
+            float a8[8];
+            Vec8<bf16>::load(a.ex + e, a8);
+            const uint32_t mk = a.drop_thr ? drop::keep8((long)(e >> 3), dseed, a.drop_thr) : 0xffu;
+            uint32_t pg[4];
+#pragma unroll
+            for (int k = 0; k < 8; ++k)
+              v[k] = ((mk >> k) & 1u) ? v[k] * a.drop_scale * drop::gelu_erf_grad(a8[k]) : 0.f;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+              pg[q] = pk_bf16(v[2 * q], v[2 * q + 1]);
+              q0[2 * q] += bf16_lo(pg[q]);
+              q0[2 * q + 1] += bf16_hi(pg[q]);
+            }
+            *reinterpret_cast<uint4*>(a.out + e) = make_uint4(pg[0], pg[1], pg[2], pg[3]);
+          } else {
+            Vec8<bf16>::store(a.out + e, v);
+          }
+        }
+      }
+      if (j + 1 < TM) __syncthreads();  // the next pass overwrites the staging rows
+    }
+    if constexpr (EPI == kEpiGeluBwd) {
+      // column sums of ga: rows of a thread -> lanes sharing its columns -> 4 waves -> one
+      // fp32 atomic per column per workgroup into the bias gradient
+#pragma unroll
+      for (int o = CG; o < 64; o <<= 1) {
+        if (!ew) break;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) q0[k] += __shfl_xor(q0[k], o, 64);
+      }
+      if (ew && lane < CG) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) red[wid * BN + cg * 8 + k] = q0[k];
+      }
+      __syncthreads();
+      for (int e = tid; ew && e < BN; e += 256)
+        atomicAdd(&a.gb[n0 + e], red[e] + red[BN + e] + red[2 * BN + e] + red[3 * BN + e]);
+    }
+    if constexpr (STATS) {
+      // lanes l, l + CG, l + 2CG, ... of a wave hold the same channels
+#pragma unroll
+      for (int o = CG; o < 64; o <<= 1) {
+        if (!ew) break;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          q0[k] += __shfl_xor(q0[k], o, 64);
+          q1[k] += __shfl_xor(q1[k], o, 64);
+          if constexpr (NQ == 3) q2[k] += __shfl_xor(q2[k], o, 64);
+        }
+      }
+      if (ew && lane < CG) {
+        float* rw = red + wid * NQ * BN + cg * 8;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          rw[k] = q0[k];
+          rw[BN + k] = q1[k];
+          if constexpr (NQ == 3) rw[2 * BN + k] = q2[k];
+        }
+      }
+      __syncthreads();
+      for (int e = tid; ew && e < NQ * BN; e += 256) {
+        const float t = red[e] + red[NQ * BN + e] + red[2 * NQ * BN + e] + red[3 * NQ * BN + e];
+        const int q = e / BN, cc2 = e - q * BN;
+        atomicAdd(&a.part[((long)(bm & a.slot_mask) * NQ + q) * a.Cout + n0 + cc2], t);
+      }
+    }
+  }
 }
 
 // ---------------------------------------------------------------------- host side

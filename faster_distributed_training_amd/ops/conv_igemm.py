@@ -164,28 +164,6 @@ KGROUPS = os.environ.get("FDT_KGROUPS", "1") != "0"
 KG_TILES = {(128, 128, 64), (128, 64, 64), (64, 128, 64), (64, 64, 64), (64, 64, 128)}
 
 
-# stride-1 3x3 convolutions (forward, and the data gradient of a pre-folded gradient) on the
-# halo kernel (csrc/kernels/conv3x3_halo.hip): the input is staged once per 16-channel chunk
-# as an LDS halo tile instead of re-loaded for each of the 9 taps
-HALO = os.environ.get("FDT_HALO3X3", "0") != "0"  # opt-in: measured no faster (README)
-HALO_BN = int(os.environ.get("FDT_HALO_BN", "0"))  # 0: per layer (tuned entry / 64)
-
-
-def _halo_bn(ent, N, H, W, Cx, Cout, want):
-    """Channel tile of a halo launch, or 0 when the halo kernel does not apply."""
-    if want is False or not HALO:
-        return 0
-    nat = _native.native()
-    if not hasattr(nat, "conv3x3_halo"):
-        return 0
-    bn = HALO_BN or (int(ent.get("halo_bn", 0)) if ent else 0) or 64
-    if want is not None and want is not True:
-        bn = int(want)
-    if Cout % bn:
-        bn = 64
-    return bn if nat.conv3x3_halo_supported(N, H, W, Cx, Cout, bn) else 0
-
-
 def _kg(ent, kg, tile3, ns, K):
     """K groups of one launch: explicit ``kg``, else the tuned entry's, else 1."""
     if kg is None:
@@ -254,7 +232,7 @@ def stat_slots(nq: int, C: int, device, M: int | None = None) -> torch.Tensor:
 
 
 def conv_fwd(x, wf, shp: ConvShape, s=None, t=None, act=0, alpha=1.0, tile=None, part=None, nsplit=None,
-             fin=None, kg=None, halo=None):
+             fin=None, kg=None):
     """y = conv(act(x*s+t)) (or conv(x) when s is None and act == 0); returns
     (y [N,Ho,Wo,Cout] bf16, part [STAT_SLOTS,2,Cout] fp32 slots whose row sum is
     (sum y, sum y^2)).  ``part``: a zeroed slot buffer to accumulate into.
@@ -267,24 +245,10 @@ def conv_fwd(x, wf, shp: ConvShape, s=None, t=None, act=0, alpha=1.0, tile=None,
     Ho, Wo = out_hw(H, W, shp)
     M = N * Ho * Wo
     pro = PRO_AFFINE_ACT if (s is not None or act != 0) else PRO_NONE
-    auto = tile is None and nsplit is None and kg is None  # launch config left to the engine
     ent = None
     if tile is None:
         ent = tuned(f"fwd{pro}", N, H, shp) or tuned("fwd", N, H, shp)
         tile = tuple(ent["tile"]) if ent else None
-    hbn = 0
-    if pro == PRO_NONE and shp.k == 3 and shp.stride == 1 and shp.pad == 1 and (halo or (halo is None and auto)):
-        hbn = _halo_bn(ent, N, H, W, C, shp.cout, halo)
-    if hbn:
-        y = torch.empty(N, H, W, shp.cout, device=x.device, dtype=torch.bfloat16)
-        if part is None:
-            part = stat_slots(2, shp.cout, x.device, M)
-        dh, dw, wt = taps_fwd(3, 1)
-        nat.conv3x3_halo(x.data_ptr(), wf.data_ptr(), y.data_ptr(), part.data_ptr(), part.shape[0], 0, 0, 0, N, H, W,
-                         C, shp.cout, shp.ntaps * shp.cxp, list(dh), list(dw), list(wt), EPI_STATS, 0, 1.0, hbn, _sp())
-        if fin is not None:
-            _finalize_standalone(nat, 1, part, 2, shp.cout, fin[0], fin[1])
-        return y, part
     bm, bn, bk = _tile3(tile, M, shp.cout)
     if nsplit is not None:
         ent = {"nsplit": nsplit}
@@ -346,7 +310,7 @@ def conv_fwd_join(y, r, s, t, s2, t2, wf, shp: ConvShape, jout, jmask=None, tile
 
 def conv_dgrad(g, y, al, be, wd, shp: ConvShape, x_shape, epi=EPI_STORE, out=None, ex=None, es=None, et=None,
                act=0, alpha=1.0, tile=None, part=None, nsplit=None, gs=None, jmask=None, jyb=None, jout=None,
-               coef=None, kg=None, halo=None):
+               coef=None, kg=None):
     """Data gradient of y = conv(a): dA = conv^T(g*gs + al + be*y)  (gs None: 1).
 
     epi: EPI_STORE -> write dA; EPI_ADD -> out += dA; EPI_ACTBWD -> through the lazy
@@ -372,7 +336,6 @@ def conv_dgrad(g, y, al, be, wd, shp: ConvShape, x_shape, epi=EPI_STORE, out=Non
         part = stat_slots(2, shp.cin, g.device, Nx * Hx * Wx)
     if epi == EPI_JOINBWD:
         assert shp.stride == 1 and ex is not None and part is not None and (jmask is not None or jout is not None)
-    auto = tile is None and nsplit is None and kg is None
     ent = None
     if tile is None:
         pro = PRO_FOLD if al is not None else PRO_NONE
@@ -383,18 +346,6 @@ def conv_dgrad(g, y, al, be, wd, shp: ConvShape, x_shape, epi=EPI_STORE, out=Non
         ent = {"nsplit": nsplit}
     classes = dgrad_classes(shp.k, shp.stride, shp.pad)
     assert coef is None or epi in (EPI_ACTBWD, EPI_JOINBWD)
-    hbn = 0
-    if (al is None and epi == EPI_ACTBWD and shp.k == 3 and shp.stride == 1 and shp.pad == 1 and Hx == Hy
-            and (halo or (halo is None and auto))):
-        hbn = _halo_bn(ent, N, Hy, Wy, Cy, shp.cin, halo)
-    if hbn:
-        (_, _, dh, dw, wt), = classes
-        nat.conv3x3_halo(g.data_ptr(), wd.data_ptr(), out.data_ptr(), part.data_ptr(), part.shape[0], _p(ex), _p(es),
-                         _p(et), N, Hy, Wy, Cy, shp.cin, shp.ntaps * shp.cout, list(dh), list(dw), list(wt),
-                         EPI_ACTBWD, int(act), float(alpha), hbn, _sp())
-        if coef is not None:
-            _finalize_standalone(nat, 2, part, 2, shp.cin, coef[0], coef[1])
-        return out, part
     for (py, px, dh, dw, wt) in classes:
         Ha = (Hx - py + shp.stride - 1) // shp.stride
         Wa = (Wx - px + shp.stride - 1) // shp.stride

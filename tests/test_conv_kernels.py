@@ -398,43 +398,3 @@ def test_kgroups_match_reference(cuda, tile):
             assert rel(out, jref) < 1e-2, (tile, "join")
             assert rel(jout, joined) < 1e-2
 
-
-@pytest.mark.parametrize("case", [(2, 32, 64, 64), (4, 16, 128, 128), (4, 8, 256, 256), (8, 4, 512, 512),
-                                  (2, 32, 64, 128), (8, 8, 32, 64)])
-@pytest.mark.parametrize("bn", [64, 128])
-def test_conv3x3_halo_matches_reference(cuda, case, bn):
-    """Stride-1 3x3 convolutions on the halo kernel (csrc/kernels/conv3x3_halo.hip): forward
-    with the statistics epilogue and the data gradient of a pre-folded gradient through a ReLU
-    activation backward, every image width the engine uses (whole rows / whole images per
-    128-pixel tile), against fp32 PyTorch."""
-    N, H, Cin, Cout = case
-    if Cout % bn or Cin % bn:
-        pytest.skip("channel tile")
-    torch.manual_seed(11)
-    shp = ci.ConvShape(Cin, Cout, 3, 1, 1)
-    if not ci._native.native().conv3x3_halo_supported(N, H, H, Cin, Cout, bn):
-        pytest.skip("unsupported geometry")
-    x = make((N, H, H, Cin), cuda)
-    w = torch.randn(Cout, Cin, 3, 3, device=cuda) / (Cin * 9) ** 0.5
-    wf, wd = ci.alloc_packed(shp, cuda)
-    ci.pack_weights([(w, wf, wd, shp)])
-    ref = nhwc(F.conv2d(nchw(x), w.to(BF).float(), padding=1))
-    y, part = ci.conv_fwd(x, wf, shp, halo=bn)
-    assert rel(y, ref) < 1e-2, rel(y, ref)
-    ps, yf = part.sum(0), ref.reshape(-1, Cout)
-    assert rel(ps[0], yf.sum(0)) < 2e-3 and rel(ps[1], (yf * yf).sum(0)) < 2e-3
-    # the generic kernel on the same problem agrees to bf16 rounding of the output
-    y2, _ = ci.conv_fwd(x, wf, shp, halo=False)
-    assert rel(y, y2) < 1e-2
-    # data gradient: conv^T of a folded gradient, through relu(ex*es + et)
-    g = make((N, H, H, Cout), cuda)
-    dref = nhwc(torch.nn.grad.conv2d_input((N, Cin, H, H), w.to(BF).float(), nchw(g), padding=1))
-    ex = make((N, H, H, Cin), cuda)
-    es, et = torch.rand(Cin, device=cuda) + 0.5, torch.randn(Cin, device=cuda) * 0.3
-    gp = dref * ((ex.float() * es + et) > 0).float()
-    out, part = ci.conv_dgrad(g, None, None, None, wd, shp, (N, H, H, Cin), epi=ci.EPI_ACTBWD, ex=ex, es=es, et=et,
-                              act=1, halo=bn)
-    assert rel(out, gp * es) < 1e-2, rel(out, gp * es)
-    ps = part.sum(0)
-    assert rel(ps[0], (gp * ex.float()).reshape(-1, Cin).sum(0)) < 1e-2
-    assert rel(ps[1], gp.reshape(-1, Cin).sum(0)) < 1e-2
