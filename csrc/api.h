@@ -32,14 +32,15 @@ void affine_fold(uint64_t gy, uint64_t y, uint64_t alpha, uint64_t beta, uint64_
 void residual_act_fwd(uint64_t ya, uint64_t sa, uint64_t ta, uint64_t yb, uint64_t sb, uint64_t tb, uint64_t xid,
                       uint64_t out, uint64_t mask, long M, int C, int act, float alpha, int dt, uint64_t stream);
 void residual_act_bwd(uint64_t g, uint64_t out, uint64_t mask, uint64_t ya, uint64_t yb, uint64_t gpre, uint64_t part,
-                      int part_rows, long M, int C, int act, float alpha, int dt, uint64_t stream);
+                      int part_rows, long M, int C, int act, float alpha, int dt, uint64_t stream, int ghw);
 // deterministic mode (common.h): no-wrap statistics slots, ordered split-K sums
 void set_deterministic_mode(bool on);
 bool deterministic_mode();
 // optim.hip
 void grad_sumsq(uint64_t g, long n, uint64_t inv_scale, int unscale, uint64_t part, int nb, uint64_t found_inf,
                 uint64_t stream);
-void grad_norm_finalize(uint64_t part, int nb, float max_norm, uint64_t out, uint64_t stream);
+void grad_norm_finalize(uint64_t part, int nb, float max_norm, uint64_t out, uint64_t total, int phase,
+                        uint64_t stream);
 void sgd_step(uint64_t p, uint64_t g, uint64_t buf, uint64_t shadow, long n, float lr, float momentum, float dampening,
               float wd, int nesterov, int first, uint64_t gsc, uint64_t found_inf, int zero_grad, uint64_t lr_dev, uint64_t stream);
 void madgrad_step(uint64_t p, uint64_t g, uint64_t gss, uint64_t s, uint64_t x0, uint64_t shadow, long n, float lr,
@@ -52,6 +53,11 @@ void adam_step(uint64_t p, uint64_t g, uint64_t m, uint64_t v, uint64_t shadow, 
                float eps, float wd, int adamw, long step, uint64_t kskip, uint64_t gsc, uint64_t found_inf,
                int zero_grad, uint64_t stream);
 void cast_bf16(uint64_t x, uint64_t y, long n, uint64_t stream);
+// head.hip
+void head_fwd(uint64_t h, uint64_t W, uint64_t b, uint64_t pooled, uint64_t logits, int N, int HW, int C, int K,
+              uint64_t stream);
+void head_bwd(uint64_t dl, uint64_t W, uint64_t pooled, uint64_t dpool, uint64_t gW, uint64_t gb, int N, int HW,
+              int C, int K, uint64_t stream);
 // mixup.hip
 void mixup_fwd(uint64_t x, uint64_t perm, uint64_t lam, uint64_t out, int b, long inner, int dt, uint64_t stream);
 void mixup_bwd(uint64_t g, uint64_t x, uint64_t perm, uint64_t inv, uint64_t lam, uint64_t gx, uint64_t dlam, int b,

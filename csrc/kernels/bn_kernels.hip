@@ -453,7 +453,7 @@ __global__ __launch_bounds__(kBlk) void residual_act_bwd_kernel(const T* __restr
                                                                 const T* __restrict__ ya, const T* __restrict__ yb,
                                                                 T* __restrict__ gpre, float* __restrict__ part,
                                                                 unsigned slot_mask, long M, int C, int TPR, int RPP,
-                                                                long rows_per_blk, int act, float alpha) {
+                                                                long rows_per_blk, int act, float alpha, int ghw) {
   __shared__ float sm[kBlk * 24];
   const int tid = threadIdx.x;
   const int gi = tid % TPR, rr = tid / TPR;
@@ -477,13 +477,16 @@ __global__ __launch_bounds__(kBlk) void residual_act_bwd_kernel(const T* __restr
     }
     Vec8<T>::store(gpre + e, gp8);
   };
+  // ghw > 0: g is [M/ghw, C] and broadcast over each group of ghw rows (the classifier
+  // head's pooled gradient, already divided by ghw: see head.hip)
+  auto gofs = [&](long rw, long e) { return ghw > 0 ? (rw / ghw) * C + c0 : e; };
   long r = r_begin + rr;
   for (; r + RPP < r_end; r += 2 * RPP) {
     const long e0 = r * C + c0, e1 = e0 + (long)RPP * C;
     float g0[8], a0[8], b0[8], o0[8], g1[8], a1[8], b1[8], o1[8];
     uint32_t m0 = 0, m1 = 0;
-    Vec8<T>::load(g + e0, g0);
-    Vec8<T>::load(g + e1, g1);
+    Vec8<T>::load(g + gofs(r, e0), g0);
+    Vec8<T>::load(g + gofs(r + RPP, e1), g1);
     Vec8<T>::load(ya + e0, a0);
     Vec8<T>::load(ya + e1, a1);
     if (yb) { Vec8<T>::load(yb + e0, b0); Vec8<T>::load(yb + e1, b1); }
@@ -496,7 +499,7 @@ __global__ __launch_bounds__(kBlk) void residual_act_bwd_kernel(const T* __restr
     const long e = r * C + c0;
     float gv[8], av[8], bv[8], ov[8];
     uint32_t m = 0;
-    Vec8<T>::load(g + e, gv);
+    Vec8<T>::load(g + gofs(r, e), gv);
     Vec8<T>::load(ya + e, av);
     if (yb) Vec8<T>::load(yb + e, bv);
     if (mask) m = mask[e >> 3];
@@ -706,8 +709,9 @@ void residual_act_fwd(uint64_t ya, uint64_t sa, uint64_t ta, uint64_t yb, uint64
 }
 
 void residual_act_bwd(uint64_t g, uint64_t out, uint64_t mask, uint64_t ya, uint64_t yb, uint64_t gpre, uint64_t part,
-                      int part_rows, long M, int C, int act, float alpha, int dt, uint64_t stream) {
+                      int part_rows, long M, int C, int act, float alpha, int dt, uint64_t stream, int ghw) {
   FDT_CHECK(out != 0 || mask != 0, "residual_act_bwd needs the output or its mask");
+  FDT_CHECK(ghw >= 0 && (ghw == 0 || M % ghw == 0), "residual_act_bwd: broadcast rows must divide M");
   ChanGeom gg = chan_geom(C);
   // ~1024 blocks: more waves in flight for this 4-5 stream kernel than the stats default
   constexpr long kBlocks = 1024;
@@ -721,7 +725,7 @@ void residual_act_bwd(uint64_t g, uint64_t out, uint64_t mask, uint64_t ya, uint
   DISPATCH_T(dt, {
     residual_act_bwd_kernel<T><<<grid, kBlk, 0, as_stream(stream)>>>(
         P<const T>(g), P<const T>(out), P<const uint8_t>(mask), P<const T>(ya), P<const T>(yb), P<T>(gpre), P<float>(part),
-        smask, M, C, gg.TPR, gg.RPP, r, act, alpha);
+        smask, M, C, gg.TPR, gg.RPP, r, act, alpha, ghw);
   });
   FDT_LAUNCH_CHECK();
 }

@@ -78,18 +78,29 @@ __global__ __launch_bounds__(kOB) void grad_sumsq_kernel(float* __restrict__ g, 
 
 // norm = sqrt(sum part); coef = min(1, max_norm/(norm+1e-6)) (torch clip_grad_norm_);
 // max_norm <= 0 -> coef = 1.  out[0] = norm, out[1] = coef
-__global__ void grad_norm_finalize_kernel(const float* __restrict__ part, int nb, float max_norm, float* __restrict__ out) {
+// phase 0: parts -> [norm, coef];  phase 1: parts -> fp64 total (a sharded gradient all-reduces
+// it);  phase 2: fp64 total -> [norm, coef].  Phases 1+2 give bitwise the phase-0 result on
+// one rank (same summation tree, same fp64 finalize), so sharded and unsharded runs agree.
+__global__ void grad_norm_finalize_kernel(const float* __restrict__ part, int nb, float max_norm, float* __restrict__ out,
+                                          double* __restrict__ total, int phase) {
   __shared__ double sm[256];
-  double a = 0.0;
-  for (int i = threadIdx.x; i < nb; i += blockDim.x) a += part[i];
-  sm[threadIdx.x] = a;
-  __syncthreads();
-  for (int o = blockDim.x / 2; o > 0; o >>= 1) {
-    if (threadIdx.x < o) sm[threadIdx.x] += sm[threadIdx.x + o];
+  if (phase != 2) {
+    double a = 0.0;
+    for (int i = threadIdx.x; i < nb; i += blockDim.x) a += part[i];
+    sm[threadIdx.x] = a;
     __syncthreads();
+    for (int o = blockDim.x / 2; o > 0; o >>= 1) {
+      if (threadIdx.x < o) sm[threadIdx.x] += sm[threadIdx.x + o];
+      __syncthreads();
+    }
   }
   if (threadIdx.x == 0) {
-    double norm = sqrt(sm[0]);
+    if (phase == 1) {
+      total[0] = sm[0];
+      return;
+    }
+    const double sq = phase == 2 ? total[0] : sm[0];
+    double norm = sqrt(sq);
     out[0] = (float)norm;
     double c = max_norm > 0.f ? (double)max_norm / (norm + 1e-6) : 1.0;
     out[1] = (float)(c < 1.0 ? c : 1.0);
@@ -243,8 +254,11 @@ void grad_sumsq(uint64_t g, long n, uint64_t inv_scale, int unscale, uint64_t pa
   FDT_LAUNCH_CHECK();
 }
 
-void grad_norm_finalize(uint64_t part, int nb, float max_norm, uint64_t out, uint64_t stream) {
-  grad_norm_finalize_kernel<<<1, 256, 0, as_stream(stream)>>>(P<const float>(part), nb, max_norm, P<float>(out));
+void grad_norm_finalize(uint64_t part, int nb, float max_norm, uint64_t out, uint64_t total, int phase,
+                        uint64_t stream) {
+  FDT_CHECK(phase >= 0 && phase <= 2 && (phase == 0 || total != 0), "grad_norm_finalize: phase / total");
+  grad_norm_finalize_kernel<<<1, 256, 0, as_stream(stream)>>>(P<const float>(part), nb, max_norm, P<float>(out),
+                                                             P<double>(total), phase);
   FDT_LAUNCH_CHECK();
 }
 

@@ -43,6 +43,9 @@ MATERIALIZE_3X3 = os.environ.get("FDT_MATERIALIZE_3X3", "1") != "0"
 # run a block's ReLU join inside the next block's first 1x1 conv (PRO_JOIN prologue) instead
 # of a standalone pass (see ResNetBodyFn.forward)
 JOIN_FOLD = os.environ.get("FDT_JOIN_FOLD", "1") != "0"
+# run the classifier head (average pool + fc, bf16 autocast numerics) as two engine kernels
+# inside the body's graphs instead of eager PyTorch ops (see csrc/kernels/head.hip)
+FUSED_HEAD = os.environ.get("FDT_FUSED_HEAD", "1") != "0"
 MODE_FCBN, MODE_BN_TRAIN, MODE_BN_EVAL = 0, 1, 2
 BF16 = torch.bfloat16
 
@@ -463,9 +466,13 @@ class ResNetBodyFn(torch.autograd.Function):
         if fs is not None:
             plan.release_stage(cur, fwd=True)
             fs.post_forward(cur)
+        head_rec = None
+        if getattr(plan, "head_on", False):
+            h, head_rec = head_forward(plan.fc, h)
         if need_grad:
             ctx.plan, ctx.training = plan, training
             ctx.recs, ctx.stem_rec = recs, stem_rec
+            ctx.head_rec = head_rec
         return h
 
     @staticmethod
@@ -480,7 +487,11 @@ class ResNetBodyFn(torch.autograd.Function):
         is always the stride-1 first unit."""
         nat = _native.native()
         plan, training = ctx.plan, ctx.training
-        g = g_out.contiguous()
+        ghw = 0  # > 0: g is the head's pooled gradient, broadcast over ghw rows per sample
+        if getattr(ctx, "head_rec", None) is not None:
+            g, ghw = head_backward(plan.fc, g_out, ctx.head_rec)
+        else:
+            g = g_out.contiguous()
         dev = g.device
         recs = ctx.recs
         nblk = len(plan.blocks)
@@ -511,7 +522,8 @@ class ResNetBodyFn(torch.autograd.Function):
                 nat.residual_act_bwd(g.data_ptr(), 0 if mask is not None else out.data_ptr(), _p(mask),
                                      y3.data_ptr(), _p(sc[0] if sc else None), gpre.data_ptr(), part.data_ptr(),
                                      part.shape[0], M, C,
-                                     b.join[0], float(b.join[1]), 1, _sp())
+                                     b.join[0], float(b.join[1]), 1, _sp(), ghw)
+                ghw = 0
             ul = b.units[-1]
             if joined:
                 (al, be), coef_sc = joined_coef  # finalised with the completing dgrad (below)
@@ -600,8 +612,62 @@ class ResNetBodyFn(torch.autograd.Function):
         if fs is not None:
             fs.post_backward("conv1")
         if not getattr(ctx, "keep", False):
-            ctx.recs = ctx.stem_rec = None
+            ctx.recs = ctx.stem_rec = ctx.head_rec = None
         return None, None, None, None
+
+
+# ------------------------------------------------------------------ classifier head
+def head_fusable(model, x, need_grad) -> bool:
+    """The fused head reproduces ``fc(mean_hw(body))`` under bf16 autocast for heads of at
+    most 32 classes with fp32 parameters / gradients; anything else keeps the PyTorch ops."""
+    fc = getattr(model, "fc", None)
+    if not FUSED_HEAD or not getattr(model, "fused_head", True) or not isinstance(fc, nn.Linear) or fc.bias is None or getattr(model, "_fsdp", None) is not None:
+        return False
+    if not isinstance(getattr(model, "avg_pool", None), nn.AdaptiveAvgPool2d) or fc._forward_hooks or fc._forward_pre_hooks:
+        return False
+    dt = x.device.type
+    if not (torch.is_autocast_enabled(dt) and torch.get_autocast_dtype(dt) == BF16):
+        return False
+    if not hasattr(_native.native(), "head_fwd"):
+        return False
+    K, C = fc.weight.shape
+    if K > 32 or C % 8:
+        return False
+    for p in (fc.weight, fc.bias):
+        if p.dtype != torch.float32 or not p.is_contiguous() or (need_grad and not p.requires_grad):
+            return False
+        if p.grad is not None and (p.grad.dtype != torch.float32 or not p.grad.is_contiguous()):
+            return False
+    return True
+
+
+def head_forward(fc, h):
+    """body [N,H,W,C] bf16 -> (logits [N,K] bf16, (pooled bf16 [N,C], H*W))."""
+    N, H, W, C = h.shape
+    K = fc.weight.shape[0]
+    pooled = torch.empty(N, C, device=h.device, dtype=BF16)
+    logits = torch.empty(N, K, device=h.device, dtype=BF16)
+    _native.native().head_fwd(h.data_ptr(), fc.weight.data_ptr(), fc.bias.data_ptr(), pooled.data_ptr(),
+                              logits.data_ptr(), N, H * W, C, K, _sp())
+    return logits, (pooled, H * W)
+
+
+def head_backward(fc, g_logits, rec):
+    """Accumulates fc.weight.grad / fc.bias.grad (signalling their readiness) and returns
+    the pooled gradient [N,C] bf16 (already / HW) with its broadcast row count HW."""
+    pooled, hw = rec
+    N, C = pooled.shape
+    K = fc.weight.shape[0]
+    dl = g_logits.to(BF16).contiguous()
+    for p in (fc.weight, fc.bias):
+        if p.grad is None:
+            p.grad = torch.zeros_like(p)
+    dpool = torch.empty(N, C, device=pooled.device, dtype=BF16)
+    _native.native().head_bwd(dl.data_ptr(), fc.weight.data_ptr(), pooled.data_ptr(), dpool.data_ptr(),
+                              fc.weight.grad.data_ptr(), fc.bias.grad.data_ptr(), N, hw, C, K, _sp())
+    grad_ready(fc.bias)
+    grad_ready(fc.weight)
+    return dpool, hw
 
 
 def to_engine_input(x: torch.Tensor, cxp: int = 8) -> torch.Tensor:
@@ -627,6 +693,8 @@ def resnet_engine_forward(model, x):
     plan.use_graphs = bool(getattr(model, "graph_engine", False)) and (plan.fsdp is None or plan.fsdp.static)
     xin = to_engine_input(x, plan.stem.shp.cxp)
     need_grad = torch.is_grad_enabled() and any(p.requires_grad for p in model.parameters())
+    plan.fc = model.fc
+    plan.head_on = head_fusable(model, x, need_grad)
     if need_grad:
         # the engine writes weight gradients itself; autograd sees one node whose only
         # differentiable input is a dummy (the image batch needs no gradient)
@@ -634,6 +702,8 @@ def resnet_engine_forward(model, x):
         body = _BodyWithDummy.apply(xin, dummy, plan, model.training)
     else:
         body = ResNetBodyFn.forward(_NoCtx(), xin, plan, model.training, False)
+    if plan.head_on:
+        return body  # logits of the fused head
     pooled = body.mean(dim=(1, 2), dtype=torch.float32)  # fp32 accumulation, no fp32 copy of the body
     return model.fc(pooled)
 
@@ -675,7 +745,7 @@ class _BodyWithDummy(torch.autograd.Function):
     def forward(ctx, xin, dummy, plan, training):
         st = None
         if graphs_enabled(plan):
-            key = (tuple(xin.shape), bool(training))
+            key = (tuple(xin.shape), bool(training), bool(getattr(plan, "head_on", False)))
             states = plan.__dict__.setdefault("_graphs", {})
             st = states.get(key)
             if st is None:

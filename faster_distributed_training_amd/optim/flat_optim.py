@@ -284,6 +284,7 @@ class GradClipper:
         self.part = torch.empty(nblocks, device=dev, dtype=torch.float32)
         self.out = torch.zeros(2, device=dev, dtype=torch.float32)  # [norm, coef]
         self.found_inf = torch.zeros(1, device=dev, dtype=torch.int32)
+        self.total = torch.zeros(1, device=dev, dtype=torch.float64)  # sharded: fp64 sum of squares
 
     @property
     def norm(self):
@@ -302,8 +303,16 @@ class GradClipper:
             nat.grad_sumsq(g.data_ptr(), g.numel(), _p(inv_scale), int(inv_scale is not None), self.part.data_ptr(),
                            self.nb, _p(self.found_inf) if check_inf else 0, _sp())
             if self.sharded:
-                return self._sharded_finalize(self.part.sum(), max_norm)
-            nat.grad_norm_finalize(self.part.data_ptr(), self.nb, float(max_norm), self.out.data_ptr(), _sp())
+                # fp64 total with the unsharded finalize's summation tree, all-reduced in fp64:
+                # one rank reproduces the unsharded norm / coefficient bitwise
+                nat.grad_norm_finalize(self.part.data_ptr(), self.nb, float(max_norm), self.out.data_ptr(),
+                                       self.total.data_ptr(), 1, _sp())
+                import torch.distributed as dist
+                dist.all_reduce(self.total, group=self.pg)
+                nat.grad_norm_finalize(self.part.data_ptr(), self.nb, float(max_norm), self.out.data_ptr(),
+                                       self.total.data_ptr(), 2, _sp())
+                return self.out[0]
+            nat.grad_norm_finalize(self.part.data_ptr(), self.nb, float(max_norm), self.out.data_ptr(), 0, 0, _sp())
         else:
             if inv_scale is not None:
                 g.mul_(inv_scale)

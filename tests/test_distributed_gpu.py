@@ -121,6 +121,7 @@ def _fsdp_engine_worker(rank, world, offload=False):
     torch.manual_seed(0)
     ref = R.resnet50(10).to(dev)
     ref.fast_path = True
+    ref.fused_head = False  # FSDP models keep the PyTorch classifier head: compare like with like
     torch.manual_seed(rank)
     m = R.resnet50(10).to(dev)
     m.fast_path = True
@@ -174,6 +175,7 @@ def _fsdp_static_graph_worker(rank, world):
     torch.manual_seed(0)
     ref = R.resnet50(10).to(dev)
     ref.fast_path = True
+    ref.fused_head = False  # FSDP models keep the PyTorch classifier head: compare like with like
     torch.manual_seed(rank)
     m = R.resnet50(10).to(dev)
     m.fast_path = True

@@ -66,7 +66,9 @@ def _train_step_vs_reference(cuda, arch):
         assert pe.grad is not None, n
         e_e, e_b = rel(pe.grad, pr.grad), rel(pb.grad, pr.grad)
         worst.append((e_e / max(e_b, 1e-6), n, e_e, e_b))
-        assert e_e <= max(2.0 * e_b, 5e-3), (n, e_e, e_b)
+        # fc.bias: sum over the batch of softmax - onehot, the most cancellation-heavy
+        # gradient (its bf16 error varies run to run with the engine's atomic statistics)
+        assert e_e <= max(2.0 * e_b, 1e-2 if n == "fc.bias" else 5e-3), (n, e_e, e_b)
     worst.sort(reverse=True)
     print("worst engine/autocast gradient error ratios:", [(n, round(r, 2)) for r, n, _, _ in worst[:5]])
     for (n, br), (_, be) in zip(m_ref.named_buffers(), m_eng.named_buffers()):
@@ -177,3 +179,86 @@ def test_engine_hip_graph_replay_matches_eager(cuda):
     assert rel(og, o1) <= 3 * noise_o + 2e-3, (rel(og, o1), noise_o)
     assert rel(gg, g1) <= 3 * noise_g + 2e-3, (rel(gg, g1), noise_g)
     assert rel(og2, og) <= 3 * noise_o + 2e-3
+
+
+@pytest.mark.parametrize("N,K,C,HW", [(64, 10, 2048, 16), (1024, 10, 2048, 16), (96, 20, 512, 16), (512, 32, 256, 49)])
+def test_fused_head_kernels_match_fp32(cuda, N, K, C, HW):
+    """head_fwd / head_bwd (csrc/kernels/head.hip) against the fp32 PyTorch head
+    fc(mean_hw(body)) and its gradients."""
+    from faster_distributed_training_amd.ops import _native
+    nat = _native.native()
+    g = torch.Generator(device=cuda).manual_seed(N + K)
+    body = torch.randn(N, HW, C, device=cuda, generator=g).relu().to(torch.bfloat16)
+    W = torch.randn(K, C, device=cuda, generator=g) * C ** -0.5
+    b = torch.randn(K, device=cuda, generator=g)
+    pooled = torch.empty(N, C, device=cuda, dtype=torch.bfloat16)
+    logits = torch.empty(N, K, device=cuda, dtype=torch.bfloat16)
+    nat.head_fwd(body.data_ptr(), W.data_ptr(), b.data_ptr(), pooled.data_ptr(), logits.data_ptr(), N, HW, C, K,
+                 torch.cuda.current_stream().cuda_stream)
+    p_ref = body.float().mean(1)
+    l_ref = p_ref @ W.t() + b
+    assert rel(pooled, p_ref) < 4e-3
+    assert rel(logits, l_ref) < 1e-2, rel(logits, l_ref)
+    dl = torch.randn(N, K, device=cuda, generator=g).to(torch.bfloat16)
+    gW0 = torch.randn(K, C, device=cuda, generator=g)
+    gb0 = torch.randn(K, device=cuda, generator=g)
+    gW, gb = gW0.clone(), gb0.clone()
+    dpool = torch.empty(N, C, device=cuda, dtype=torch.bfloat16)
+    nat.head_bwd(dl.data_ptr(), W.data_ptr(), pooled.data_ptr(), dpool.data_ptr(), gW.data_ptr(), gb.data_ptr(),
+                 N, HW, C, K, torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    assert rel(dpool, dl.float() @ W / HW) < 1e-2
+    assert rel(gW - gW0, dl.float().t() @ p_ref) < 1e-2
+    assert rel(gb - gb0, dl.float().sum(0)) < 1e-4
+
+
+def test_engine_fused_head_matches_pytorch_head(cuda):
+    """Under bf16 autocast the engine runs the classifier head itself (FUSED_HEAD); its
+    logits and every gradient match the PyTorch head (mean + F.linear) on the same engine
+    (deterministic mode: identical bodies), and the fc gradients fire the engine's
+    grad-ready hooks exactly once.  The loss is linear in the logits (fixed bf16 weights R)
+    so both heads see the same logit gradient."""
+    from faster_distributed_training_amd.models import resnet as R
+    from faster_distributed_training_amd.ops import _native
+    from faster_distributed_training_amd.ops import resnet_fused as rf
+    from faster_distributed_training_amd.ops.resnet_fused import register_grad_ready_hook
+    torch.manual_seed(0)
+    m = R.resnet50(10).to(cuda)
+    m.fast_path = True
+    x = torch.randn(64, 3, 32, 32, device=cuda)
+    r = torch.randn(64, 10, device=cuda).to(torch.bfloat16).float()
+
+    def step():
+        m.zero_grad(set_to_none=True)
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            out = m(x)
+        (out.float() * r).sum().backward()
+        torch.cuda.synchronize()
+        return out.detach().float(), {n: p.grad.clone() for n, p in m.named_parameters()}
+
+    saved = rf.FUSED_HEAD
+    _native.set_deterministic(True)
+    try:
+        rf.FUSED_HEAD = False
+        o1, g1 = step()
+        assert not m._plan.head_on
+        rf.FUSED_HEAD = True
+        seen = []
+        hs = [register_grad_ready_hook(p, lambda q: seen.append(id(q))) for p in (m.fc.weight, m.fc.bias)]
+        of, gf = step()
+        assert m._plan.head_on
+        assert sorted(seen) == sorted([id(m.fc.weight), id(m.fc.bias)])
+        for h in hs:
+            h.remove()
+    finally:
+        rf.FUSED_HEAD = saved
+        _native.set_deterministic(False)
+    assert rel(of, o1) < 1e-2, rel(of, o1)
+    errs = {n: rel(gf[n], g1[n]) for n in g1}
+    print("worst fused-head gradient differences:", sorted(errs.items(), key=lambda kv: -kv[1])[:4])
+    # (the PyTorch head rounds its weight / bias gradients to bf16, the fused head does not)
+    assert errs["fc.weight"] < 1e-2 and errs["fc.bias"] < 1e-2, (errs["fc.weight"], errs["fc.bias"])
+    assert max(v for n, v in errs.items() if not n.startswith("fc.")) < 1e-3
+    flat_f = torch.cat([gf[n].flatten() for n in g1])
+    flat_1 = torch.cat([g1[n].flatten() for n in g1])
+    assert rel(flat_f, flat_1) < 2e-2, rel(flat_f, flat_1)
