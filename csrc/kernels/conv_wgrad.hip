@@ -330,37 +330,55 @@ __global__ __launch_bounds__(256) void wgrad_kernel(const WgArgs a) {
     }
 }
 
-// slab [nsplit][Cout][ntaps*Cxp] -> fp32 OIHW grad [Cout][Cin][KH][KW] (fixed split order).
-// One workgroup per 64 consecutive slab columns of one output channel: lane = column
-// (coalesced slab reads), the 4 waves take interleaved splits, LDS combines them.
+// slab [nsplit][Cout][ntaps*Cxp] -> fp32 OIHW grad [Cout][Cin][KH][KW] (fixed summation
+// order: deterministic).  One workgroup per 64 consecutive slab columns of one output channel:
+// 16 column quads (16-B loads) x 16 split lanes, each thread keeping up to 8 independent loads
+// in flight (the small-batch splits are many and short: the earlier one-column-per-lane form
+// walked them two loads at a time and ran latency-bound, ~1 TB/s), LDS combines the lanes.
 __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restrict__ slab, float* __restrict__ out,
                                                            int nsplit, int Cout, int Cin, int ntaps, int Cxp,
                                                            int accumulate) {
-  __shared__ float red[4][64];
+  __shared__ float red[16][65];
   const int ld = ntaps * Cxp;
   const int cblk = (ld + 63) / 64;
   const int co = blockIdx.x / cblk;
-  const int col = (blockIdx.x - co * cblk) * 64 + (threadIdx.x & 63);
-  const int w = threadIdx.x >> 6;
+  const int c0 = (blockIdx.x - co * cblk) * 64;
+  const int q = threadIdx.x & 15, sl = threadIdx.x >> 4;
+  const int col = c0 + q * 4;
   const long sstride = (long)Cout * ld;
-  float a0 = 0.f, a1 = 0.f;
+  float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
+  auto add = [](float4& x, const float4& y) { x.x += y.x; x.y += y.y; x.z += y.z; x.w += y.w; };
   if (col < ld) {
     const float* p = slab + (long)co * ld + col;
-    int k = w;
-    for (; k + 4 < nsplit; k += 8) {
-      a0 += p[k * sstride];
-      a1 += p[(k + 4) * sstride];
+    auto ld4 = [&](int k) { return *reinterpret_cast<const float4*>(p + k * sstride); };
+    int k = sl;
+    for (; k + 7 * 16 < nsplit; k += 8 * 16) {
+      float4 v[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) v[i] = ld4(k + i * 16);
+      add(v[0], v[4]); add(v[1], v[5]); add(v[2], v[6]); add(v[3], v[7]);
+      add(v[0], v[2]); add(v[1], v[3]);
+      add(v[0], v[1]);
+      add(a, v[0]);
     }
-    if (k < nsplit) a0 += p[k * sstride];
+    for (; k < nsplit; k += 16) add(a, ld4(k));
   }
-  red[w][threadIdx.x & 63] = a0 + a1;
+  red[sl][q * 4 + 0] = a.x;
+  red[sl][q * 4 + 1] = a.y;
+  red[sl][q * 4 + 2] = a.z;
+  red[sl][q * 4 + 3] = a.w;
   __syncthreads();
-  if (w == 0 && col < ld) {
-    const float s = (red[0][threadIdx.x] + red[1][threadIdx.x]) + (red[2][threadIdx.x] + red[3][threadIdx.x]);
-    const int t = col / Cxp, ci = col - t * Cxp;
-    if (ci < Cin) {
-      const long e = ((long)co * Cin + ci) * ntaps + t;
-      out[e] = accumulate ? out[e] + s : s;
+  if (threadIdx.x < 64) {
+    const int c = c0 + threadIdx.x;
+    float s = 0.f;
+#pragma unroll
+    for (int l = 0; l < 16; ++l) s += red[l][threadIdx.x];
+    if (c < ld) {
+      const int t = c / Cxp, ci = c - t * Cxp;
+      if (ci < Cin) {
+        const long e = ((long)co * Cin + ci) * ntaps + t;
+        out[e] = accumulate ? out[e] + s : s;
+      }
     }
   }
 }
@@ -554,6 +572,7 @@ void conv_wgrad(uint64_t g, uint64_t y, uint64_t al, uint64_t be, uint64_t gs, u
 void wgrad_reduce(uint64_t slab, uint64_t out, int nsplit, int Cout, int Cin, int ntaps, int Cxp, int accumulate,
                   uint64_t stream) {
   const int ld = ntaps * Cxp;
+  FDT_CHECK(ld % 4 == 0 && slab % 16 == 0, "wgrad_reduce: 16-B aligned slab rows");
   const int grid = Cout * ((ld + 63) / 64);
   hipLaunchKernelGGL(wg::wgrad_reduce_kernel, dim3(grid), dim3(256), 0, as_stream(stream), P<const float>(slab),
                      P<float>(out), nsplit, Cout, Cin, ntaps, Cxp, accumulate);
