@@ -64,9 +64,9 @@ __global__ __launch_bounds__(256) void mixup_bwd_kernel(const T* __restrict__ g,
 
 // One row per THREAD when C <= 64 (CIFAR: 10 classes -- a wave per row would idle 54 of
 // its 64 lanes and serialise B/16 rows per wave), one row per WAVE otherwise.
-template <typename T, bool ROW_PER_THREAD>
-__global__ __launch_bounds__(1024) void mixup_ce_kernel(const T* __restrict__ logits, const int* __restrict__ ya,
-                                                        const int* __restrict__ yb, const float* __restrict__ lam,
+template <typename T, typename L, bool ROW_PER_THREAD>
+__global__ __launch_bounds__(1024) void mixup_ce_kernel(const T* __restrict__ logits, const L* __restrict__ ya,
+                                                        const L* __restrict__ yb, const float* __restrict__ lam,
                                                         float* __restrict__ loss, float* __restrict__ glog,
                                                         float* __restrict__ dlam, float* __restrict__ meter, int B,
                                                         int C) {
@@ -90,7 +90,7 @@ __global__ __launch_bounds__(1024) void mixup_ce_kernel(const T* __restrict__ lo
       float se = 0.f;
       for (int c = 0; c < C; ++c) se += __expf(to_f(row[c]) - mx);
       const float lse = mx + __logf(se);
-      const int a = ya[r], b = yb[r];
+      const int a = (int)ya[r], b = (int)yb[r];
       const float l = lam[r];
       const float cea = lse - to_f(row[a]), ceb = lse - to_f(row[b]);
       for (int c = 0; c < C; ++c) {
@@ -114,7 +114,7 @@ __global__ __launch_bounds__(1024) void mixup_ce_kernel(const T* __restrict__ lo
       for (int c = lane; c < C; c += 64) se += __expf(to_f(row[c]) - mx);
       se = wave_sum(se);
       const float lse = mx + __logf(se);
-      const int a = ya[r], b = yb[r];
+      const int a = (int)ya[r], b = (int)yb[r];
       int am = C;  // argmax, first occurrence (torch.argmax)
       if (meter) {
         for (int c = lane; c < C; c += 64)
@@ -181,17 +181,74 @@ void mixup_bwd(uint64_t g, uint64_t x, uint64_t perm, uint64_t inv, uint64_t lam
 }
 
 void mixup_ce_fwd(uint64_t logits, uint64_t ya, uint64_t yb, uint64_t lam, uint64_t loss, uint64_t glog, uint64_t dlam,
-                  uint64_t meter, int B, int C, int dt, uint64_t stream) {
-  DISPATCH_T(dt, {
+                  uint64_t meter, int B, int C, int dt, int labels64, uint64_t stream) {
+  auto go = [&](auto tag_t, auto tag_l) {
+    using T = decltype(tag_t);
+    using L = decltype(tag_l);
     if (C <= 64)
-      mixup_ce_kernel<T, true><<<1, 1024, 0, as_stream(stream)>>>(P<const T>(logits), P<const int>(ya), P<const int>(yb),
-                                                                  P<const float>(lam), P<float>(loss), P<float>(glog),
-                                                                  P<float>(dlam), P<float>(meter), B, C);
+      mixup_ce_kernel<T, L, true><<<1, 1024, 0, as_stream(stream)>>>(P<const T>(logits), P<const L>(ya), P<const L>(yb),
+                                                                     P<const float>(lam), P<float>(loss), P<float>(glog),
+                                                                     P<float>(dlam), P<float>(meter), B, C);
     else
-      mixup_ce_kernel<T, false><<<1, 1024, 0, as_stream(stream)>>>(P<const T>(logits), P<const int>(ya), P<const int>(yb),
-                                                                   P<const float>(lam), P<float>(loss), P<float>(glog),
-                                                                   P<float>(dlam), P<float>(meter), B, C);
+      mixup_ce_kernel<T, L, false><<<1, 1024, 0, as_stream(stream)>>>(P<const T>(logits), P<const L>(ya), P<const L>(yb),
+                                                                      P<const float>(lam), P<float>(loss), P<float>(glog),
+                                                                      P<float>(dlam), P<float>(meter), B, C);
+  };
+  DISPATCH_T(dt, {
+    if (labels64) go(T{}, int64_t{});
+    else go(T{}, int{});
   });
+  FDT_LAUNCH_CHECK();
+}
+
+// One workgroup: a uniformly random permutation of b <= 1024 samples (bitonic sort in LDS of
+// 64-bit counter-hash keys -- distinct, the hash is a bijection), the permuted labels and the
+// per-sample lambda vector: replaces randperm's sort passes, the int32 cast, the label gather
+// and the lambda fill of an input-mixup step (reference resnet50_test.py:355-376).
+__global__ __launch_bounds__(1024) void mixup_prep_kernel(const int64_t* __restrict__ y, int b, float lam,
+                                                          uint64_t seed, int* __restrict__ perm,
+                                                          int64_t* __restrict__ yb, float* __restrict__ lam_vec) {
+  __shared__ uint64_t key[1024];
+  __shared__ int idx[1024];
+  int n = 1;
+  while (n < b) n <<= 1;
+  for (int i = threadIdx.x; i < n; i += blockDim.x) {
+    key[i] = i < b ? mix64(seed + (uint64_t)i * 0xD1B54A32D192ED03ull) : ~0ull;
+    idx[i] = i;
+  }
+  __syncthreads();
+  for (int k = 2; k <= n; k <<= 1) {
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      for (int i = threadIdx.x; i < n; i += blockDim.x) {
+        const int p = i ^ j;
+        if (p > i) {
+          const bool up = (i & k) == 0;
+          const uint64_t a = key[i], c = key[p];
+          if ((a > c) == up) {
+            key[i] = c;
+            key[p] = a;
+            const int t = idx[i];
+            idx[i] = idx[p];
+            idx[p] = t;
+          }
+        }
+      }
+      __syncthreads();
+    }
+  }
+  for (int i = threadIdx.x; i < b; i += blockDim.x) {
+    const int j = idx[i];
+    perm[i] = j;
+    yb[i] = y[j];
+    lam_vec[i] = lam;
+  }
+}
+
+void mixup_prep(uint64_t y, int b, float lam, uint64_t seed, uint64_t perm, uint64_t yb, uint64_t lam_vec,
+                uint64_t stream) {
+  FDT_CHECK(b >= 1 && b <= 1024, "mixup_prep: 1 <= batch <= 1024");
+  mixup_prep_kernel<<<1, 1024, 0, as_stream(stream)>>>(P<const int64_t>(y), b, lam, seed, P<int>(perm),
+                                                       P<int64_t>(yb), P<float>(lam_vec));
   FDT_LAUNCH_CHECK();
 }
 

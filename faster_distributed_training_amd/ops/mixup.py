@@ -114,6 +114,18 @@ def mixup_data(x, y, alpha=0.99, intra_only=False, generator=None):
     ``intra_only`` keeps same-label pairs unmixed (vectorised, no per-sample loop)."""
     lam = sample_lambda(alpha, generator)
     b = x.size(0)
+    if (not intra_only and _native.use_native(x) and x.dtype in DT and 1 <= b <= 1024 and y.dtype == torch.int64
+            and y.is_cuda and hasattr(_native.native(), "mixup_prep")):
+        # one kernel: device permutation (seeded from the host generator, no sync), the
+        # permuted labels and the lambda vector
+        seed = int(torch.randint(0, 2**62, (1,), generator=generator).item())
+        perm = torch.empty(b, device=x.device, dtype=torch.int32)
+        yb = torch.empty(b, device=x.device, dtype=torch.int64)
+        lv = torch.empty(b, device=x.device, dtype=torch.float32)
+        yc = y.contiguous()
+        _native.native().mixup_prep(yc.data_ptr(), b, float(lam), seed, perm.data_ptr(), yb.data_ptr(), lv.data_ptr(),
+                                    _native.stream_ptr())
+        return mixup_interpolate(x, perm, lv), y, yb, lam
     perm = torch.randperm(b, device=x.device)
     if intra_only:
         same = (y == y[perm]).float()
@@ -180,14 +192,16 @@ class _MixupCENative(torch.autograd.Function):
         loss = torch.empty((), device=lg.device, dtype=torch.float32)
         glog = torch.empty(b, c, device=lg.device, dtype=torch.float32)
         dlam = torch.empty(b, device=lg.device, dtype=torch.float32)
-        # keep the int32 label copies referenced until the launch is enqueued: a temporary
-        # freed inside the argument list can be recycled by the caching allocator for the
-        # second copy (ya and yb would then alias)
-        ya32 = ya.to(torch.int32).contiguous()
-        yb32 = yb.to(torch.int32).contiguous()
-        nat.mixup_ce_fwd(lg.data_ptr(), ya32.data_ptr(), yb32.data_ptr(), lam_vec.data_ptr(), loss.data_ptr(),
+        # int64 labels are read as they are; anything else as int32 copies (kept referenced
+        # until the launch is enqueued: a temporary freed inside the argument list can be
+        # recycled by the caching allocator for the second copy -- ya and yb would alias)
+        l64 = ya.dtype == torch.int64 and yb.dtype == torch.int64
+        lt = torch.int64 if l64 else torch.int32
+        ya_c = ya.to(lt).contiguous()
+        yb_c = yb.to(lt).contiguous()
+        nat.mixup_ce_fwd(lg.data_ptr(), ya_c.data_ptr(), yb_c.data_ptr(), lam_vec.data_ptr(), loss.data_ptr(),
                          glog.data_ptr(), dlam.data_ptr(), 0 if meter_acc is None else meter_acc.data_ptr(), b, c,
-                         DT[lg.dtype], _native.stream_ptr())
+                         DT[lg.dtype], int(l64), _native.stream_ptr())
         ctx.save_for_backward(glog, dlam)
         ctx.dt = logits.dtype
         return loss

@@ -5,7 +5,7 @@ cd "$(dirname "$0")/.."
 export TMPDIR=/tmp
 OUT=gpurun_out/${1:-wgr}
 mkdir -p "$OUT"
-timeout -k 10 600 python -u -m pytest tests/test_conv_kernels.py tests/test_deterministic.py tests/test_resnet_engine.py -m gpu -v -p no:cacheprovider --timeout 200 --timeout-method thread > "$OUT/pytest.log" 2>&1; rc=$?
+timeout -k 10 600 python -u -m pytest tests/test_conv_kernels.py tests/test_deterministic.py tests/test_resnet_engine.py tests/test_gpu_kernels.py tests/test_distributed_gpu.py -m gpu -v -p no:cacheprovider --timeout 200 --timeout-method thread > "$OUT/pytest.log" 2>&1; rc=$?
 tail -2 "$OUT/pytest.log"
 case $rc in 0|1) ;; *) echo "pytest aborted rc=$rc"; exit 1;; esac
 grep -E "^(FAILED|ERROR)" "$OUT/pytest.log" | head -20

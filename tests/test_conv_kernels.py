@@ -214,12 +214,17 @@ def test_conv_wgrad(cuda, case, mode):
         gt = (g.float() + al + be * y.float()).to(BF).float()
         a = torch.relu(x.float() * xs + xt).to(BF).float()[..., :Cin]
     ref = torch.nn.grad.conv2d_weight(nchw(a), (Cout, Cin, k, k), nchw(gt), stride=stride, padding=pad)
-    for ns, tile in [(1, None), (3, None), (2, (64, 64, 32)), (1, (128, 128, 64))]:
+    # split counts <= 8 take the channel-major reduce for unpadded 3x3 layers, 12 the column form
+    for ns, tile in [(1, None), (3, None), (2, (64, 64, 32)), (1, (128, 128, 64)), (12, None)]:
         if tile and Cout % tile[0]:
             continue
         out = torch.empty(Cout, Cin, k, k, device=cuda)
         ci.conv_wgrad(g, y, al, be, x, shp, out, xs, xt, act, nsplit=ns, tile=tile)
         assert rel(out, ref) < 5e-3, (ns, tile, rel(out, ref))
+        prev = torch.randn_like(out)
+        acc = prev.clone()
+        ci.conv_wgrad(g, y, al, be, x, shp, acc, xs, xt, act, nsplit=ns, tile=tile, accumulate=True)
+        assert rel(acc - prev, ref) < 5e-3, (ns, tile, "accumulate")
 
 
 @pytest.mark.parametrize("cout,cin,k", [(64, 3, 3), (256, 64, 1), (512, 512, 3), (48, 72, 3), (2048, 512, 1)])

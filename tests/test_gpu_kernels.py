@@ -97,6 +97,37 @@ def test_mixup_kernels(cuda):
     ref = (lv * F.cross_entropy(l2, ya, reduction="none") + (1 - lv) * F.cross_entropy(l2, yb, reduction="none")).mean()
     ref.backward()
     assert abs(loss.item() - ref.item()) < 1e-5 and rel(logits.grad, l2.grad) < 1e-5
+    # int32 labels take the conversion path, int64 are read directly: same result
+    l3 = logits.detach().clone().requires_grad_()
+    loss32 = mixup_cross_entropy(l3, ya.int(), yb.int(), lv)
+    loss32.backward()
+    assert loss32.item() == loss.item() and torch.equal(l3.grad, logits.grad)
+
+
+@pytest.mark.parametrize("b", [1, 7, 128, 1000, 1024])
+def test_mixup_prep_kernel(cuda, b):
+    """mixup_data's one-kernel device path: a valid permutation (every index once), the
+    permuted labels, the lambda vector; different host seeds give different permutations,
+    the same generator state the same one; the mixed batch equals lam*x + (1-lam)*x[perm]."""
+    from faster_distributed_training_amd.ops.mixup import mixup_data
+    x = torch.randn(b, 3, 4, 4, device=cuda)
+    y = torch.randint(0, 10, (b,), device=cuda)
+    g = torch.Generator().manual_seed(3)
+    mixed, ya, yb, lam = mixup_data(x, y, alpha=0.99, generator=g)
+    assert ya is y and yb.dtype == torch.int64
+    # recover the permutation from the labels' source rows: x rows are distinct
+    d = ((mixed - lam * x).reshape(b, -1).unsqueeze(1) - (1 - lam) * x.reshape(1, b, -1)).abs().amax(-1)
+    perm = d.argmin(1)
+    assert torch.equal(perm.sort().values, torch.arange(b, device=cuda))
+    assert torch.equal(yb, y[perm])
+    ref = lam * x + (1 - lam) * x[perm]
+    assert rel(mixed, ref) < 1e-6
+    g2 = torch.Generator().manual_seed(3)
+    m2, _, yb2, lam2 = mixup_data(x, y, alpha=0.99, generator=g2)
+    assert lam2 == lam and torch.equal(m2, mixed) and torch.equal(yb2, yb)
+    if b >= 128:
+        m3, _, _, _ = mixup_data(x, y, alpha=0.99, generator=g2)
+        assert not torch.equal(m3, mixed)
 
 
 @pytest.mark.parametrize("C", [10, 100])
