@@ -62,8 +62,8 @@ void head_bwd(uint64_t dl, uint64_t W, uint64_t pooled, uint64_t dpool, uint64_t
 void mixup_fwd(uint64_t x, uint64_t perm, uint64_t lam, uint64_t out, int b, long inner, int dt, uint64_t stream);
 void mixup_bwd(uint64_t g, uint64_t x, uint64_t perm, uint64_t inv, uint64_t lam, uint64_t gx, uint64_t dlam, int b,
                long inner, int dt, uint64_t stream);
-void mixup_ce_fwd(uint64_t logits, uint64_t ya, uint64_t yb, uint64_t lam, uint64_t loss, uint64_t glog, uint64_t dlam,
-                  uint64_t meter, int B, int C, int dt, int labels64, uint64_t stream);
+void mixup_ce_fwd(uint64_t logits, uint64_t ya, uint64_t yb, uint64_t lam, float lam_s, uint64_t loss, uint64_t glog,
+                  uint64_t dlam, uint64_t meter, int B, int C, int dt, int labels64, uint64_t stream);
 void mixup_prep(uint64_t y, int b, float lam, uint64_t seed, uint64_t perm, uint64_t yb, uint64_t lam_vec,
                 uint64_t stream);
 // layernorm.hip

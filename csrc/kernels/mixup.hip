@@ -67,7 +67,7 @@ __global__ __launch_bounds__(256) void mixup_bwd_kernel(const T* __restrict__ g,
 template <typename T, typename L, bool ROW_PER_THREAD>
 __global__ __launch_bounds__(1024) void mixup_ce_kernel(const T* __restrict__ logits, const L* __restrict__ ya,
                                                         const L* __restrict__ yb, const float* __restrict__ lam,
-                                                        float* __restrict__ loss, float* __restrict__ glog,
+                                                        float lam_s, float* __restrict__ loss, T* __restrict__ glog,
                                                         float* __restrict__ dlam, float* __restrict__ meter, int B,
                                                         int C) {
   // meter (optional): training accumulators [loss sum, lambda-weighted correct, samples]
@@ -91,15 +91,15 @@ __global__ __launch_bounds__(1024) void mixup_ce_kernel(const T* __restrict__ lo
       for (int c = 0; c < C; ++c) se += __expf(to_f(row[c]) - mx);
       const float lse = mx + __logf(se);
       const int a = (int)ya[r], b = (int)yb[r];
-      const float l = lam[r];
+      const float l = lam ? lam[r] : lam_s;
       const float cea = lse - to_f(row[a]), ceb = lse - to_f(row[b]);
       for (int c = 0; c < C; ++c) {
         const float p = __expf(to_f(row[c]) - lse);
         const float t = (c == a ? l : 0.f) + (c == b ? 1.f - l : 0.f);
-        glog[(long)r * C + c] = (p - t) * invB;
+        glog[(long)r * C + c] = from_f<T>((p - t) * invB);
       }
       tot += l * cea + (1.f - l) * ceb;
-      dlam[r] = (cea - ceb) * invB;
+      if (dlam) dlam[r] = (cea - ceb) * invB;
       corr += (am == a ? l : 0.f) + (am == b ? 1.f - l : 0.f);
     }
     tot = wave_sum(tot);
@@ -122,16 +122,16 @@ __global__ __launch_bounds__(1024) void mixup_ce_kernel(const T* __restrict__ lo
 #pragma unroll
         for (int o = 32; o > 0; o >>= 1) am = min(am, __shfl_xor(am, o, 64));
       }
-      const float l = lam[r];
+      const float l = lam ? lam[r] : lam_s;
       const float cea = lse - to_f(row[a]), ceb = lse - to_f(row[b]);
       for (int c = lane; c < C; c += 64) {
         float p = __expf(to_f(row[c]) - lse);
         float t = (c == a ? l : 0.f) + (c == b ? 1.f - l : 0.f);
-        glog[(long)r * C + c] = (p - t) * invB;
+        glog[(long)r * C + c] = from_f<T>((p - t) * invB);
       }
       if (lane == 0) {
         tot += l * cea + (1.f - l) * ceb;
-        dlam[r] = (cea - ceb) * invB;
+        if (dlam) dlam[r] = (cea - ceb) * invB;
         corr += (am == a ? l : 0.f) + (am == b ? 1.f - l : 0.f);
       }
     }
@@ -180,18 +180,18 @@ void mixup_bwd(uint64_t g, uint64_t x, uint64_t perm, uint64_t inv, uint64_t lam
   FDT_LAUNCH_CHECK();
 }
 
-void mixup_ce_fwd(uint64_t logits, uint64_t ya, uint64_t yb, uint64_t lam, uint64_t loss, uint64_t glog, uint64_t dlam,
-                  uint64_t meter, int B, int C, int dt, int labels64, uint64_t stream) {
+void mixup_ce_fwd(uint64_t logits, uint64_t ya, uint64_t yb, uint64_t lam, float lam_s, uint64_t loss, uint64_t glog,
+                  uint64_t dlam, uint64_t meter, int B, int C, int dt, int labels64, uint64_t stream) {
   auto go = [&](auto tag_t, auto tag_l) {
     using T = decltype(tag_t);
     using L = decltype(tag_l);
     if (C <= 64)
       mixup_ce_kernel<T, L, true><<<1, 1024, 0, as_stream(stream)>>>(P<const T>(logits), P<const L>(ya), P<const L>(yb),
-                                                                     P<const float>(lam), P<float>(loss), P<float>(glog),
+                                                                     P<const float>(lam), lam_s, P<float>(loss), P<T>(glog),
                                                                      P<float>(dlam), P<float>(meter), B, C);
     else
       mixup_ce_kernel<T, L, false><<<1, 1024, 0, as_stream(stream)>>>(P<const T>(logits), P<const L>(ya), P<const L>(yb),
-                                                                      P<const float>(lam), P<float>(loss), P<float>(glog),
+                                                                      P<const float>(lam), lam_s, P<float>(loss), P<T>(glog),
                                                                       P<float>(dlam), P<float>(meter), B, C);
   };
   DISPATCH_T(dt, {

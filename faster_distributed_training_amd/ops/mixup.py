@@ -184,14 +184,19 @@ class AttentionMixup(nn.Module):
 # ----------------------------------------------------------------------------- losses
 
 class _MixupCENative(torch.autograd.Function):
+    """lam: per-sample fp32 vector (B,) or a python float (one lambda for the batch: no
+    lambda vector, no d(lambda))."""
+
     @staticmethod
-    def forward(ctx, logits, ya, yb, lam_vec, weights_mean, meter_acc=None):
+    def forward(ctx, logits, ya, yb, lam, weights_mean, meter_acc=None):
         nat = _native.native()
         lg = logits.contiguous()
         b, c = lg.shape
         loss = torch.empty((), device=lg.device, dtype=torch.float32)
-        glog = torch.empty(b, c, device=lg.device, dtype=torch.float32)
-        dlam = torch.empty(b, device=lg.device, dtype=torch.float32)
+        # d(logits) in the logits' dtype: the backward is one scaling kernel
+        glog = torch.empty(b, c, device=lg.device, dtype=lg.dtype)
+        vec = isinstance(lam, torch.Tensor)
+        dlam = torch.empty(b, device=lg.device, dtype=torch.float32) if vec else None
         # int64 labels are read as they are; anything else as int32 copies (kept referenced
         # until the launch is enqueued: a temporary freed inside the argument list can be
         # recycled by the caching allocator for the second copy -- ya and yb would alias)
@@ -199,31 +204,32 @@ class _MixupCENative(torch.autograd.Function):
         lt = torch.int64 if l64 else torch.int32
         ya_c = ya.to(lt).contiguous()
         yb_c = yb.to(lt).contiguous()
-        nat.mixup_ce_fwd(lg.data_ptr(), ya_c.data_ptr(), yb_c.data_ptr(), lam_vec.data_ptr(), loss.data_ptr(),
-                         glog.data_ptr(), dlam.data_ptr(), 0 if meter_acc is None else meter_acc.data_ptr(), b, c,
-                         DT[lg.dtype], int(l64), _native.stream_ptr())
+        nat.mixup_ce_fwd(lg.data_ptr(), ya_c.data_ptr(), yb_c.data_ptr(), lam.data_ptr() if vec else 0,
+                         0.0 if vec else float(lam), loss.data_ptr(), glog.data_ptr(), _native.ptr(dlam),
+                         0 if meter_acc is None else meter_acc.data_ptr(), b, c, DT[lg.dtype], int(l64),
+                         _native.stream_ptr())
         ctx.save_for_backward(glog, dlam)
-        ctx.dt = logits.dtype
         return loss
 
     @staticmethod
     def backward(ctx, gl):
         glog, dlam = ctx.saved_tensors
-        glam = dlam * gl if ctx.needs_input_grad[3] else None
-        return (glog * gl).to(ctx.dt), None, None, glam, None, None
+        glam = dlam * gl if (dlam is not None and ctx.needs_input_grad[3]) else None
+        return glog * gl, None, None, glam, None, None  # (0-dim fp32 gl: result stays in glog.dtype)
 
 
 def mixup_cross_entropy(logits, y_a, y_b, lam_vec, meter=None):
-    """mean_i [lam_i CE(p_i, ya_i) + (1-lam_i) CE(p_i, yb_i)].  ``meter``
-    (train.metrics.DeviceMeter): on the HIP path the same kernel also accumulates the
-    step's loss / lambda-weighted accuracy into it (``meter.fused`` is then set)."""
+    """mean_i [lam_i CE(p_i, ya_i) + (1-lam_i) CE(p_i, yb_i)]; ``lam_vec`` (B,) or a float.
+    ``meter`` (train.metrics.DeviceMeter): on the HIP path the same kernel also accumulates
+    the step's loss / lambda-weighted accuracy into it (``meter.fused`` is then set)."""
     if (_native.use_native(logits) and logits.dim() == 2 and logits.shape[1] <= 1024
             and logits.dtype in DT and hasattr(_native.native(), "mixup_ce_fwd")):
         acc = None
         if meter is not None and getattr(meter, "acc", None) is not None and meter.acc.device == logits.device:
             acc = meter.acc
             meter.fused = True
-        return _MixupCENative.apply(logits, y_a, y_b, lam_vec.float().contiguous(), False, acc)
+        lam = lam_vec.float().contiguous() if isinstance(lam_vec, torch.Tensor) else float(lam_vec)
+        return _MixupCENative.apply(logits, y_a, y_b, lam, False, acc)
     lf = logits.float()
     ce_a = F.cross_entropy(lf, y_a, reduction="none")
     ce_b = F.cross_entropy(lf, y_b, reduction="none")
@@ -233,10 +239,9 @@ def mixup_cross_entropy(logits, y_a, y_b, lam_vec, meter=None):
 def mixup_criterion(criterion, pred, y_a, y_b, lam, meter=None):
     """Scalar-lambda criterion (``resnet50_test.py:451-452``).  ``criterion`` is accepted
     for API parity; cross entropy is computed by the fused kernel."""
-    lv = torch.full((pred.shape[0],), float(lam), device=pred.device, dtype=torch.float32)
     if criterion is not None and not isinstance(criterion, nn.CrossEntropyLoss):
         return lam * criterion(pred, y_a) + (1 - lam) * criterion(pred, y_b)
-    return mixup_cross_entropy(pred, y_a, y_b, lv, meter=meter)
+    return mixup_cross_entropy(pred, y_a, y_b, float(lam), meter=meter)
 
 
 def mixup_criterion_meta(criterion, pred, y_a, y_b, lam, faithful=False, meter=None):

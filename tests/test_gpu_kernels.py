@@ -102,6 +102,13 @@ def test_mixup_kernels(cuda):
     loss32 = mixup_cross_entropy(l3, ya.int(), yb.int(), lv)
     loss32.backward()
     assert loss32.item() == loss.item() and torch.equal(l3.grad, logits.grad)
+    # one lambda for the batch as a python float (no lambda vector) == the same value per sample
+    l5, l6 = logits.detach().clone().requires_grad_(), logits.detach().clone().requires_grad_()
+    ls = mixup_cross_entropy(l5, ya, yb, 0.3)
+    lt = mixup_cross_entropy(l6, ya, yb, torch.full((64,), 0.3, device=cuda))
+    (ls * 2).backward()
+    (lt * 2).backward()
+    assert ls.item() == lt.item() and torch.equal(l5.grad, l6.grad)
 
 
 @pytest.mark.parametrize("b", [1, 7, 128, 1000, 1024])
