@@ -45,6 +45,9 @@ def parse():
                     help="--fsdp: parameter all-gather wire / compute-copy precision (masters stay fp32)")
     ap.add_argument("--sharded-ngd", action="store_true",
                     help="with --ngd at N=1: run the sharded-NGD data-parallel path over a world-1 group")
+    ap.add_argument("--ddp", action="store_true",
+                    help="at N=1: run the DDP bucket reducer over a world-1 group (graph cuts + all-reduce actions "
+                         "of the multi-GPU path, without the communication time)")
     ap.add_argument("--precision", default="bf16")
     ap.add_argument("--bucket-mb", type=float, default=8.0)
     ap.add_argument("--comm-dtype", default="fp32")
@@ -82,7 +85,7 @@ def main():
                        optimizer="ngd" if args.ngd else args.optimizer, fsdp=args.fsdp,
                        precision=args.precision, bucket_mb=args.bucket_mb, comm_dtype=args.comm_dtype,
                        fast_path=False if args.no_native else None, graphs=not args.no_graphs,
-                       deterministic=args.deterministic, force_sharded=args.sharded_ngd,
+                       deterministic=args.deterministic, force_sharded=args.sharded_ngd, force_ddp=args.ddp,
                        fsdp_param_dtype=args.fsdp_param_dtype)
     tr = ResNetTrainer(cfg)
     dev = tr.device
@@ -163,6 +166,12 @@ def _sharding_fields(tr, rec):
     if hasattr(tr.optimizer, "graph_replays"):
         cfg["ngd_graph_replays"] = int(tr.optimizer.graph_replays)
         cfg["ngd_graph_kinds"] = len(tr.optimizer._gcache)
+    if tr.reducer is not None:
+        cfg["ddp_buckets"] = len(tr.reducer.buckets)
+        plan = getattr(tr.model, "_plan", None)
+        states = list(getattr(plan, "_graphs", {}).values()) if plan is not None else []
+        if states and states[0].segments:
+            cfg["bwd_graph_segments"] = len(states[0].segments)
     if tr.fsdp is not None:
         cfg["fsdp_units"] = len(tr.fsdp.units)
         cfg["fsdp_peak_full_bytes"] = int(tr.fsdp.peak_full_bytes)

@@ -78,6 +78,8 @@ class ResNetConfig:
     profile_steps: int = 0             # per-phase device timing (+ roctx ranges) of the first K steps
     deterministic: bool = False        # bitwise-repeatable engine steps (ops/_native.set_deterministic)
     force_sharded: bool = False        # sharded-NGD path even at world size 1 (bench / tests)
+    force_ddp: bool = False            # DDP bucket reducer even at world size 1 (bench: the 8-GPU
+                                       # path's graph cuts + all-reduce actions on one GPU)
     extra: dict = field(default_factory=dict)
 
 
@@ -92,7 +94,8 @@ class ResNetTrainer:
     def __init__(self, cfg: ResNetConfig):
         self.cfg = cfg
         self.rank, self.world = 0, 1
-        if cfg.distributed or cfg.fsdp or cfg.force_sharded or int(os.environ.get("WORLD_SIZE", "1")) > 1:
+        if (cfg.distributed or cfg.fsdp or cfg.force_sharded or cfg.force_ddp
+                or int(os.environ.get("WORLD_SIZE", "1")) > 1):
             # (--fsdp always runs the sharded path, over a world-1 group on one GPU)
             if not torch.distributed.is_initialized():
                 pdist.setup_norank()
@@ -144,7 +147,7 @@ class ResNetTrainer:
                                            first_bucket_mb=cfg.first_bucket_mb, comm_dtype=cdt)
         else:
             self.flat = FlatParams(params_owner, device=self.device)
-            if cfg.distributed:
+            if cfg.distributed or cfg.force_ddp:
                 from ..parallel.ddp import BucketReducer
                 cdt = {"fp32": None, "bf16": torch.bfloat16}[cfg.comm_dtype]
                 self.reducer = BucketReducer(self.flat, self.model, bucket_mb=cfg.bucket_mb,
