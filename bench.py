@@ -49,7 +49,7 @@ def parse():
                     help="at N=1: run the DDP bucket reducer over a world-1 group (graph cuts + all-reduce actions "
                          "of the multi-GPU path, without the communication time)")
     ap.add_argument("--precision", default="bf16")
-    ap.add_argument("--bucket-mb", type=float, default=8.0)
+    ap.add_argument("--bucket-mb", type=float, default=25.0)
     ap.add_argument("--comm-dtype", default="fp32")
     ap.add_argument("--no-native", action="store_true", help="ablation: plain PyTorch ops (w/o tricks)")
     ap.add_argument("--profile-steps", type=int, default=0)

@@ -25,6 +25,12 @@ dominated above; the exposed cost is the LAST bucket.  Default: a 1 MB first buc
 (communication starts after the classifier/last stage) then 8 MB buckets — ResNet-50's
 89.6 MB fp32 gradient becomes ~12 buckets vs the reference's 5 x 25 MB, so the tail that
 cannot overlap is ~8 MB (~15 µs at 7-link bandwidth) instead of ~25 MB.
+Measured against that (round 3, ``bench.py --ddp`` = this reducer over a world-1 RCCL group,
+so every cost but the transfer itself): each bucket costs ~25 µs of graph cut + collective
+launch on the GPU timeline at ResNet-50 batch 128 -- 12 buckets 5.95 ms/step, 6 buckets
+5.78, 3 buckets 5.74, no reducer 5.52 (``profiles/r3s3/ddp_world1_*.json``).  The ResNet
+trainer and the bench therefore default to 25 MB buckets (after the 1 MB first one): ~0.17 ms
+less per step than 8 MB against ~0.1 ms more exposed tail at 8 GPUs.
 """
 from __future__ import annotations
 

@@ -55,7 +55,7 @@ class ResNetConfig:
     seed: int = 123456
     faithful: bool = False
     lr_scaling: str = "world"          # world | faithful4 | none   (Q11)
-    bucket_mb: float = 8.0
+    bucket_mb: float = 25.0           # DDP / ZeRO-2 buckets (parallel/ddp.py: bucket sizing)
     first_bucket_mb: float = 1.0
     comm_dtype: str = "fp32"
     fsdp: bool = False
