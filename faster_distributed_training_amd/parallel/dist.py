@@ -29,6 +29,17 @@ def _backend():
     return "nccl" if torch.cuda.is_available() else "gloo"
 
 
+def _comm_env():
+    """RCCL's collective streams come from the high-priority pool.  Measured (round 3, a
+    kernel trace of the DDP path at world 1): from the normal pool the stream
+    ProcessGroupNCCL took landed on the SAME hardware queue as the compute stream (HIP shares
+    GPU_MAX_HW_QUEUES = 4 queues round-robin), so every bucket all-reduce executed in queue
+    order between two backward kernels and could never overlap them; high-priority streams
+    get their own queue (``profiles/r3s3/ddp_queues.txt``)."""
+    os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    os.environ.setdefault("TORCH_NCCL_HIGH_PRIORITY", "1")
+
+
 def _bind_device():
     if torch.cuda.is_available():
         torch.cuda.set_device(local_rank() % torch.cuda.device_count())
@@ -37,7 +48,7 @@ def _bind_device():
 def setup(rank: int = 0, world_size: int = 1, master_addr: str = "127.0.0.1", master_port: int = 12355,
           backend: str | None = None, timeout_s: int = 1800):
     """Explicit-rank bootstrap (reference ``setup``, ``utils.py:13-17``)."""
-    os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    _comm_env()
     os.environ.setdefault("MASTER_ADDR", master_addr)
     os.environ.setdefault("MASTER_PORT", str(master_port))
     os.environ.setdefault("LOCAL_RANK", str(rank))
@@ -53,7 +64,7 @@ def setup(rank: int = 0, world_size: int = 1, master_addr: str = "127.0.0.1", ma
 def setup_norank(world_size: int | None = None, backend: str | None = None, timeout_s: int = 1800):
     """torchrun bootstrap: rank/world from the environment (reference ``setup_norank``,
     ``utils.py:20-23`` — the path the reference actually uses)."""
-    os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    _comm_env()
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
     os.environ.setdefault("MASTER_PORT", "12355")
     _bind_device()
@@ -71,6 +82,7 @@ def setup_sharedfile(world_size: int, path: str = "/tmp/fdt_sharedfile", backend
                      rank: int | None = None):
     """File-store rendezvous for multi-node on a shared filesystem (reference
     ``setup_sharedfile``, ``utils.py:26-30``)."""
+    _comm_env()
     _bind_device()
     r = rank if rank is not None else env_int("RANK", 0)
     dist.init_process_group(backend or _backend(), init_method=f"file://{path}", world_size=world_size, rank=r)
