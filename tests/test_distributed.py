@@ -458,3 +458,16 @@ def _fsdp_bf16_worker(rank, world):
 
 def test_fsdp_bf16_param_gather():
     run_world(_fsdp_bf16_worker, world=2)
+
+
+def test_comm_env_prefers_high_priority_rccl_streams(monkeypatch):
+    """parallel/dist._comm_env: RCCL collectives default to high-priority streams (their own
+    hardware queue, profiles/r3s3/ddp_queues.txt); an explicit user setting is kept."""
+    import os
+    from faster_distributed_training_amd.parallel import dist as pdist
+    monkeypatch.delenv("TORCH_NCCL_HIGH_PRIORITY", raising=False)
+    pdist._comm_env()
+    assert os.environ["TORCH_NCCL_HIGH_PRIORITY"] == "1"
+    monkeypatch.setenv("TORCH_NCCL_HIGH_PRIORITY", "0")
+    pdist._comm_env()
+    assert os.environ["TORCH_NCCL_HIGH_PRIORITY"] == "0"
