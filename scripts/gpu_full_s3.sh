@@ -4,7 +4,7 @@
 set -o pipefail
 cd "$(dirname "$0")/.."
 export TMPDIR=/tmp
-OUT=gpurun_out/${1:-full_s3}
+OUT=gpurun_out/${1:-full_s3b}
 mkdir -p "$OUT"
 timeout -k 10 900 python -u -m pytest tests -m gpu -v -p no:cacheprovider --timeout 300 --timeout-method thread > "$OUT/pytest.log" 2>&1; rc=$?
 echo "pytest rc=$rc" >> "$OUT/pytest.log"; tail -3 "$OUT/pytest.log"
