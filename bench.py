@@ -6,6 +6,7 @@ epoch time".  Reference number: ~680 img/s (derived from the refere
 published epoch time with its tricks enabled).
 
     python bench.py                               # 1 GPU, defaults
+    python bench.py --gpus 8                      # starts 8 ranks itself (child torchrun)
     python -m torch.distributed.run --nnodes=1 --nproc-per-node 8 --master-addr 127.0.0.1 \
         --master-port 29500 bench.py --gpus 8 --steps 50 --warmup 10
 
@@ -63,8 +64,38 @@ def parse():
     return ap.parse_args()
 
 
+def _launch_ranks(n: int) -> int:
+    """``--gpus N`` (N > 1) without a launcher: start N ranks ourselves, one process per GPU,
+    as a CHILD ``torch.distributed.run`` (never an exec, and before anything here touches the
+    GPU), relay rank 0's JSON line and return the child's exit code.  Same contract as the
+    reference's launcher (/root/reference/run_distributed.sh:2-3), which always starts its
+    ranks itself."""
+    import socket
+    import subprocess
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    proc = subprocess.Popen(cmd, stdout=subprocess.PIPE, text=True, env=env)
+    for line in proc.stdout:  # rank 0's record -> our stdout, anything else -> stderr
+        if line.startswith("{") and '"metric"' in line:
+            sys.stdout.write(line)
+            sys.stdout.flush()
+        else:
+            sys.stderr.write(line)
+    return proc.wait()
+
+
 def main():
     args = parse()
+    world_env = os.environ.get("WORLD_SIZE")
+    if world_env is None and args.gpus > 1:
+        sys.exit(_launch_ranks(args.gpus))
+    if world_env is not None and int(world_env) != args.gpus:
+        sys.exit(f"bench.py: --gpus {args.gpus} but this launcher started WORLD_SIZE={world_env} ranks")
     if args.no_native:
         os.environ["FDT_NATIVE"] = "0"
     if args.model == "transformer":
@@ -74,10 +105,7 @@ def main():
 
     from faster_distributed_training_amd.train.resnet_trainer import ResNetConfig, ResNetTrainer
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    if args.gpus != world and world > 1:
-        print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
-    n = world
+    n = int(os.environ.get("WORLD_SIZE", "1"))
     gb = args.global_batch
     assert gb % n == 0, "global batch must divide evenly over ranks"
     cfg = ResNetConfig(arch=args.arch, bs=gb // n, synthetic=True, eval=False, plot=False,
@@ -152,10 +180,23 @@ def main():
         "peak_mem_gb": round(torch.cuda.max_memory_allocated() / 2**30, 2) if cuda else None,
     }
     _sharding_fields(tr, rec)
+    _dist_fields(rec)
     if tr.rank == 0:
         print(json.dumps(rec), flush=True)
     if dist.is_initialized():
         dist.destroy_process_group()
+
+
+def _dist_fields(rec):
+    """The process group that actually ran: its size (must equal n_gpus) and backend."""
+    import torch.distributed as dist
+    if dist.is_initialized():
+        rec["dist_world"] = dist.get_world_size()
+        rec["backend"] = dist.get_backend()
+    else:
+        rec["dist_world"] = 1
+        rec["backend"] = None
+    assert rec["dist_world"] == rec["n_gpus"], (rec["dist_world"], rec["n_gpus"])
 
 
 def _sharding_fields(tr, rec):
@@ -243,6 +284,7 @@ def bench_transformer(args):
            "peak_mem_gb": round(torch.cuda.max_memory_allocated() / 2**30, 2) if cuda else None,
            "host_ms_per_step": round(host / args.steps * 1e3, 3)}
     _sharding_fields(tr, rec)
+    _dist_fields(rec)
     if tr.rank == 0:
         print(json.dumps(rec), flush=True)
     if dist.is_initialized():

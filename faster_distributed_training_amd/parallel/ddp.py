@@ -21,10 +21,9 @@ X2-X4) with a reducer designed around the flat gradient buffer (``utils/flat.py`
 Bucket sizing for MI355X: an 8-GPU node connects every GPU to every other by one xGMI
 link (7 x ~153 GB/s per GPU).  RCCL's multi-channel algorithms spread a large message
 over all links, so per-bucket cost is latency-dominated below a few MB and bandwidth-
-dominated above; the exposed cost is the LAST bucket.  Default: a 1 MB first bucket
-(communication starts after the classifier/last stage) then 8 MB buckets — ResNet-50's
-89.6 MB fp32 gradient becomes ~12 buckets vs the reference's 5 x 25 MB, so the tail that
-cannot overlap is ~8 MB (~15 µs at 7-link bandwidth) instead of ~25 MB.
+dominated above; the exposed cost is the LAST bucket.  Round 2 chose a 1 MB first bucket
+(communication starts after the classifier/last stage) then 8 MB buckets -- ResNet-50's
+89.6 MB fp32 gradient as ~12 buckets, an exposed tail of ~8 MB (~15 µs at 7-link bandwidth).
 Measured against that (round 3, ``bench.py --ddp`` = this reducer over a world-1 RCCL group,
 so every cost but the transfer itself): each bucket costs ~25 µs of graph cut + collective
 launch on the GPU timeline at ResNet-50 batch 128 -- 12 buckets 5.95 ms/step, 6 buckets
@@ -64,7 +63,7 @@ def plan_buckets(sizes, first_cap, cap):
 
 
 class BucketReducer:
-    def __init__(self, flat: FlatParams, module=None, process_group=None, bucket_mb: float = 8.0,
+    def __init__(self, flat: FlatParams, module=None, process_group=None, bucket_mb: float = 25.0,
                  first_bucket_mb: float = 1.0, comm_dtype: torch.dtype | None = None,
                  broadcast_buffers: bool = True, broadcast_init: bool = True):
         self.flat = flat

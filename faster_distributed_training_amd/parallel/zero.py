@@ -104,7 +104,7 @@ class ShardedOptimizerDP:
 
     sharded_optimizer = True
 
-    def __init__(self, flat: FlatParams, module=None, process_group=None, broadcast_init=True, bucket_mb=8.0,
+    def __init__(self, flat: FlatParams, module=None, process_group=None, broadcast_init=True, bucket_mb=25.0,
                  first_bucket_mb=1.0, comm_dtype=None):
         from .ddp import BucketReducer
         self.flat = flat

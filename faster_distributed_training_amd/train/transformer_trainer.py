@@ -63,7 +63,7 @@ class TransformerConfig:
     fsdp_offload: bool = False       # FSDP shards + optimizer state in pinned host memory (reference CPUOffload)
     fsdp_param_dtype: str = "fp32"   # fp32 | bf16: all-gather wire / compute copy of the parameters
     shard_ngd: bool = True           # distributed NGD: each rank owns + preconditions 1/world of the params
-    bucket_mb: float = 8.0
+    bucket_mb: float = 25.0           # measured faster than 8 MB (profiles/r3s3/ddp_world1_*.json)
     resume: bool = False
     checkpoint_dir: str = "./checkpoint"
     steps_per_epoch: int = 0

@@ -41,7 +41,7 @@ def parse(argv=None):
     p.add_argument("--seed", default=123456, type=int)
     p.add_argument("--precision", default="bf16", choices=["bf16", "fp16", "fp32"])
     p.add_argument("--fsdp", action="store_true")
-    p.add_argument("--bucket_mb", default=8.0, type=float)
+    p.add_argument("--bucket_mb", default=25.0, type=float)
     p.add_argument("--comm_dtype", default="fp32", choices=["fp32", "bf16"])
     p.add_argument("--faithful", action="store_true", help="reproduce reference quirks (lr x4, mixup loss form)")
     p.add_argument("--learnable_meta", action="store_true", help="optimise the meta-mixup lambda")

@@ -86,10 +86,34 @@ def test_bench_two_ranks_torchrun(tmp_path, extra, par, opt):
     assert len(lines) == 1, out  # rank 0 only
     rec = lines[0]
     assert rec["n_gpus"] == 2 and rec["steps"] == 2 and rec["config"]["parallelism"] == par
+    assert rec["dist_world"] == 2
     assert rec["config"]["optimizer"] == opt and rec["config"]["global_batch"] == 16
     assert rec["value"] > 0 and rec["ms_per_step"] > 0
     if "--fsdp" in extra:
         assert rec["config"]["fsdp_units"] > 1
+
+
+def test_bench_launches_its_own_ranks(tmp_path):
+    """``python bench.py --gpus 2`` with no launcher starts 2 ranks itself (child torchrun)
+    and relays exactly one JSON line naming a 2-rank process group."""
+    env = dict(os.environ, FDT_NATIVE="0", PYTHONPATH=ROOT, OMP_NUM_THREADS="2")
+    env.pop("WORLD_SIZE", None)
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--arch", "resnet18",
+                        "--global-batch", "16", "--steps", "2", "--warmup", "1"], cwd=tmp_path, env=env,
+                       capture_output=True, text=True, timeout=900)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.strip()]
+    assert len(lines) == 1, r.stdout
+    rec = json.loads(lines[0])
+    assert rec["n_gpus"] == 2 and rec["dist_world"] == 2 and rec["backend"] == "gloo"
+    assert rec["config"]["parallelism"] == "dp2"
+
+
+def test_bench_refuses_world_size_mismatch(tmp_path):
+    env = dict(os.environ, FDT_NATIVE="0", PYTHONPATH=ROOT, WORLD_SIZE="2", RANK="0")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "4", "--steps", "1"], cwd=tmp_path,
+                       env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode != 0 and "WORLD_SIZE=2" in r.stderr
 
 
 def test_bench_transformer_two_ranks_torchrun(tmp_path):

@@ -40,7 +40,7 @@ def parse(argv=None):
     p.add_argument("--seed", default=123456, type=int)
     p.add_argument("--precision", default="bf16", choices=["bf16", "fp16", "fp32"])
     p.add_argument("--fsdp", action="store_true", help="flat-sharded data parallel (reference: FSDP)")
-    p.add_argument("--bucket_mb", default=8.0, type=float)
+    p.add_argument("--bucket_mb", default=25.0, type=float)
     p.add_argument("--faithful", action="store_true", help="reproduce reference quirks (see README)")
     p.add_argument("--steps", default=0, type=int, help="max steps per epoch (0 = full epoch)")
     p.add_argument("--eval_steps", default=0, type=int)
