@@ -132,6 +132,15 @@ class PinnedPrefetcher {
     }
     RT_CHECK(hipStreamWaitEvent(reinterpret_cast<hipStream_t>(compute_stream), events_.at(s), 0));
   }
+  // Host-only: block (GIL released) until the worker has issued slot `s`'s last job, i.e. its
+  // memcpy from the caller's source arrays is done and they may be dropped.
+  void wait_issued(int s) {
+    if (s < 0 || s >= (int)slots_.size()) throw std::runtime_error("PinnedPrefetcher.wait_issued: bad slot");
+    if (worker_) {
+      py::gil_scoped_release nogil;
+      worker_->wait_issued(slot_seq_[s]);
+    }
+  }
   uint64_t submitted() const { return worker_ ? worker_->submitted() : 0; }
   void synchronize() {
     if (worker_) {
@@ -204,6 +213,7 @@ void register_runtime(py::module_& m) {
            py::arg("wait_event") = 0)
       .def_property_readonly("submitted", &PinnedPrefetcher::submitted)
       .def("wait", &PinnedPrefetcher::wait)
+      .def("wait_issued", &PinnedPrefetcher::wait_issued)
       .def("synchronize", &PinnedPrefetcher::synchronize)
       .def_property_readonly("copy_stream", &PinnedPrefetcher::copy_stream)
       .def_property_readonly("slot_bytes", &PinnedPrefetcher::slot_bytes)

@@ -71,6 +71,10 @@ class PinnedStager:
         waits for the slot's previous readers (their release event)."""
         s = self.next
         self.next = (s + 1) % self.nslots
+        if self._keep[s] is not None:
+            # the slot's previous job was never acquired (abandoned iterator): its sources
+            # must outlive the worker's memcpy from them before they are replaced below
+            self.pf.wait_issued(s)
         ev = self.released[s]
         srcs, sizes, dsts, outs, keep = [], [], [], [], [ev]
         off = 0

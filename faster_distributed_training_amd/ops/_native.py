@@ -45,11 +45,15 @@ def load():
         return None
     # provenance: the binary must have been built from the csrc/ next to it
     from ._provenance import source_hash
-    want = source_hash()
+    want = source_hash(arch=getattr(m, "arch", None))  # (the arch the binary was built for)
     got = m.source_hash() if hasattr(m, "source_hash") else None
     if want is not None and got != want and os.environ.get("FDT_ALLOW_STALE_NATIVE", "0") != "1":
         _err = (f"{path} is stale: built from sources with hash {got}, the tree has {want} "
                 f"(run `python build_native.py`)")
+        if os.environ.get("FDT_NATIVE") == "1":
+            raise RuntimeError(f"FDT_NATIVE=1 but {_err}")
+        import warnings
+        warnings.warn(f"HIP extension refused: {_err}", RuntimeWarning, stacklevel=2)
         return None
     _mod = m
     return _mod

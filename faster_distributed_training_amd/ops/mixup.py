@@ -190,10 +190,15 @@ class _MixupCENative(torch.autograd.Function):
     @staticmethod
     def forward(ctx, logits, ya, yb, lam, weights_mean, meter_acc=None):
         nat = _native.native()
-        lg = logits.contiguous()
+        ctx.out_dtype = logits.dtype
+        # fp16 logits (loss-scaled training): d(logits) = (p - t)/B must be kept in fp32 until the
+        # loss scale has multiplied it -- stored early in fp16, values below ~6e-5 would become
+        # subnormal / zero and the scaler would no longer protect them.  The [B, classes]
+        # upcast is negligible.  bf16 has fp32's exponent range and is stored directly.
+        lg = (logits.float() if logits.dtype == torch.float16 else logits).contiguous()
         b, c = lg.shape
         loss = torch.empty((), device=lg.device, dtype=torch.float32)
-        # d(logits) in the logits' dtype: the backward is one scaling kernel
+        # d(logits) in the (compute) logits' dtype: the backward is one scaling kernel
         glog = torch.empty(b, c, device=lg.device, dtype=lg.dtype)
         vec = isinstance(lam, torch.Tensor)
         dlam = torch.empty(b, device=lg.device, dtype=torch.float32) if vec else None
@@ -215,7 +220,10 @@ class _MixupCENative(torch.autograd.Function):
     def backward(ctx, gl):
         glog, dlam = ctx.saved_tensors
         glam = dlam * gl if (dlam is not None and ctx.needs_input_grad[3]) else None
-        return glog * gl, None, None, glam, None, None  # (0-dim fp32 gl: result stays in glog.dtype)
+        g = glog * gl  # (0-dim fp32 gl: result stays in glog.dtype)
+        if g.dtype != ctx.out_dtype:
+            g = g.to(ctx.out_dtype)  # fp16: cast AFTER the loss scale is applied
+        return g, None, None, glam, None, None
 
 
 def mixup_cross_entropy(logits, y_a, y_b, lam_vec, meter=None):

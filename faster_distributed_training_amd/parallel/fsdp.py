@@ -564,8 +564,10 @@ class FullyShardedDP:
         """All units gathered (checkpointing / state_dict) with the exact fp32 masters (also
         under a bf16 param_dtype); resharded on exit."""
         for u in self.units:
-            if u.full16 is not None and u.work is None:
-                u.gathered = False  # (a bf16-rounded gather is not the master copy)
+            if u.full16 is not None:
+                if u.work is not None:
+                    u.gather(wait=True)  # finish an in-flight (bf16) prefetch first ...
+                u.gathered = False       # ... a bf16-rounded gather is not the master copy
             u.gather(wait=True, exact=True)
         try:
             yield

@@ -140,7 +140,7 @@ def save_last(trainer, epoch: int):
     os.replace(path + ".tmp", path)
     barrier()  # every rank file of this save exists before the main file names it
     extra = {"global_step": step, "best_acc": float(trainer.best_acc), "world": world,
-             "sharded_optimizer": sharded, "last": True}
+             "sharded_optimizer": sharded, "last": True, "rank_files": "epoch_tagged"}
     if not sharded:
         extra.update(_optimizer_state(trainer))
     if getattr(trainer, "scheduler", None) is not None:
@@ -167,6 +167,8 @@ def restore_last(trainer) -> bool:
         raise RuntimeError(f"{path} was written by {ck['world']} ranks; resume with the same world size "
                            f"(this run has {world})")
     rp = rank_path(path, rank, int(ck["epoch"]))
+    if not os.path.isfile(rp) and ck.get("rank_files") != "epoch_tagged":
+        rp = rank_path(path, rank)  # written before rank files were epoch-tagged (untagged names)
     mine = ckpt.load_checkpoint(rp) if os.path.isfile(rp) else None
     if mine is not None and (int(mine.get("epoch", -1)) != int(ck["epoch"])
                              or int(mine.get("global_step", -1)) != int(ck.get("global_step", 0))):

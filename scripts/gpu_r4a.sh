@@ -9,6 +9,9 @@ mkdir -p "$OUT"
 timeout -k 10 180 python -u scripts/graph_comm_probe.py > "$OUT/probe.log" 2>&1; rc=$?
 cat "$OUT/probe.log" | tail -12
 [ $rc -eq 0 ] || { echo "probe rc=$rc"; exit 1; }
+timeout -k 10 300 python -u -m pytest tests/test_gpu_kernels.py tests/test_prefetch.py -m gpu -q -k "mixup or prefetch or staging or submit" -p no:cacheprovider --timeout 120 --timeout-method thread > "$OUT/pytest.log" 2>&1; rc=$?
+tail -2 "$OUT/pytest.log"
+case $rc in 0|1|5) ;; *) echo "pytest aborted rc=$rc"; exit 1;; esac
 run() {
   local name=$1; shift
   timeout -k 10 300 python bench.py "$@" > "$OUT/$name.log" 2>&1 || { echo "$name failed"; tail -5 "$OUT/$name.log"; exit 1; }

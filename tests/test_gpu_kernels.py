@@ -111,6 +111,31 @@ def test_mixup_kernels(cuda):
     assert ls.item() == lt.item() and torch.equal(l5.grad, l6.grad)
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("b", [128, 1024])
+def test_mixup_ce_fp16_loss_scaled(cuda, b):
+    """fp16 logits under a 65536 loss scale: the fused CE's d(logits) is scaled before it is
+    rounded to fp16: equals F.cross_entropy's fp32 gradient scaled then cast."""
+    from faster_distributed_training_amd.ops.mixup import mixup_cross_entropy
+    torch.manual_seed(0)
+    base = (torch.randn(b, 10, device=cuda) * 4).half()
+    ya, yb = torch.randint(0, 10, (b,), device=cuda), torch.randint(0, 10, (b,), device=cuda)
+    lv = torch.rand(b, device=cuda)
+    scale = 65536.0
+    lg = base.clone().requires_grad_()
+    loss = mixup_cross_entropy(lg, ya, yb, lv)
+    (loss * scale).backward()
+    assert lg.grad.dtype == torch.float16
+    l2 = base.float().requires_grad_()
+    ref = (lv * F.cross_entropy(l2, ya, reduction="none") + (1 - lv) * F.cross_entropy(l2, yb, reduction="none")).mean()
+    (ref * scale).backward()
+    want = l2.grad.half()
+    assert abs(loss.item() - ref.item()) < 1e-4
+    # the small entries survive: no more flushed-to-zero gradients than the reference has
+    assert int((lg.grad == 0).sum()) <= int((want == 0).sum())
+    assert rel(lg.grad.float(), want.float()) < 2e-3
+
+
 @pytest.mark.parametrize("b", [1, 7, 128, 1000, 1024])
 def test_mixup_prep_kernel(cuda, b):
     """mixup_data's one-kernel device path: a valid permutation (every index once), the

@@ -33,6 +33,13 @@ def test_stale_extension_refused(monkeypatch):
     monkeypatch.setattr(_native, "_err", None)
     monkeypatch.setattr(_provenance, "source_hash", lambda *a, **k: "0" * 64)
     monkeypatch.delenv("FDT_ALLOW_STALE_NATIVE", raising=False)
-    assert _native.load() is None and "stale" in _native._err
+    monkeypatch.delenv("FDT_NATIVE", raising=False)
+    with pytest.warns(RuntimeWarning, match="stale"):  # refused loudly, not silently
+        assert _native.load() is None and "stale" in _native._err
     with pytest.raises(RuntimeError, match="stale"):
         _native.native()
+    # an explicit FDT_NATIVE=1 makes the refusal an error at load time
+    monkeypatch.setattr(_native, "_err", None)
+    monkeypatch.setenv("FDT_NATIVE", "1")
+    with pytest.raises(RuntimeError, match="FDT_NATIVE=1"):
+        _native.load()
