@@ -15,18 +15,24 @@ MI355X design:
 * ``length_buckets`` (e.g. 64/128/256/512) round each batch's padded length up so the
   attention/GEMM shapes repeat (kernel tuning and HIP-graph friendly); ``None`` pads to
   the longest sample in the batch exactly like the reference;
-* tokenizer: a local HuggingFace tokenizer (``bert-base-uncased`` from the HF cache or a
-  path) when available; otherwise ``HashWordPieceTokenizer`` — a dependency-free
-  lower-casing word tokenizer hashing words into the BERT id range with BERT's special
-  ids ([PAD]=0, [CLS]=101, [SEP]=102), so shapes, vocab size and masks match;
-* no network: CSV files (``train.csv``/``test.csv`` in the AG News layout
-  ``"class","title","description"``) are read from ``root`` when present, otherwise
-  ``synthetic_agnews`` provides an AG-News-shaped corpus (120k/7.6k samples, 4 classes,
-  AG-News-like length distribution, class-dependent vocabulary so models can learn).
+* tokenizer: the HuggingFace tokenizer the reference uses (``bert-base-uncased``, from the
+  local HF cache or a directory path).  If it cannot be loaded the run FAILS; the
+  dependency-free ``HashWordPieceTokenizer`` (lower-casing word tokenizer hashing words into
+  the BERT id range with BERT's special ids [PAD]=0, [CLS]=101, [SEP]=102) is used only when
+  asked for by name (``--tokenizer hash``);
+* data: the AG News CSVs (``train.csv``/``test.csv``, rows ``"class","title","description"``,
+  the files torchtext's ``AG_NEWS`` reads) under ``root/ag_news``, downloaded with MD5 checks
+  (``AGNEWS_URLS`` / ``AGNEWS_MD5``) when missing.  A run that asks for real data and cannot
+  get it raises; ``synthetic_agnews`` (an AG-News-shaped corpus: 120k/7.6k samples, 4
+  classes, AG-News-like lengths, class-dependent vocabulary) is used only with
+  ``synthetic=True`` (``--synthetic``);
+* the tokenised corpus is cached next to the CSV (``tokens_<tokenizer>_<max_len>.npz``,
+  keyed by the CSV's MD5), so later runs skip tokenisation.
 """
 from __future__ import annotations
 
 import csv
+import hashlib
 import os
 import re
 import zlib
@@ -39,8 +45,18 @@ PAD_ID, CLS_ID, SEP_ID = 0, 101, 102
 NUM_CLASSES = 4
 TRAIN_SIZE, TEST_SIZE = 120000, 7600
 
-_HTML = re.compile(r"<[^>]+>")
-_URL = re.compile(r"https?://\S+|www\.\S+")
+# the reference's cleaning regexes (transformer_test.py:73-79): tags removed without a
+# separator, www-style URLs replaced by one space
+_HTML = re.compile(r"<.*?>")
+_URL = re.compile(r"\s*(?:https?://)?www\.\S*\.[A-Za-z]{2,5}\s*")
+
+# The AG News CSVs (Zhang et al. 2015, as distributed with the char-CNN data and read by
+# torchtext's AG_NEWS dataset, which the reference uses: transformer_test.py:88-93).
+AGNEWS_URLS = {
+    "train": "https://raw.githubusercontent.com/mhjabreel/CharCnn_Keras/master/data/ag_news_csv/train.csv",
+    "test": "https://raw.githubusercontent.com/mhjabreel/CharCnn_Keras/master/data/ag_news_csv/test.csv",
+}
+AGNEWS_MD5 = {"train": "b1a00f826fdfbd249f79597b59e1dc12", "test": "d52ea96a97a2d943681189a97654912d"}
 _WORD = re.compile(r"[a-z0-9]+(?:'[a-z]+)?|[^\sa-z0-9]")
 
 # A compact English stopword list (gensim's STOPWORDS is not installed here; this covers
@@ -54,9 +70,10 @@ while who whom why will with would you your yours yourself yourselves""".split()
 
 
 def clean_text(s: str) -> str:
-    """HTML strip + URL strip + stopword removal (reference ``transformer_test.py:73-79``)."""
-    s = _HTML.sub(" ", s)
-    s = _URL.sub(" ", s)
+    """HTML strip + URL strip + stopword removal (reference ``transformer_test.py:73-79``,
+    applied per sample in ``generate_batch``)."""
+    s = _HTML.sub("", s)
+    s = _URL.sub(" ", s).strip()
     return " ".join(w for w in s.split() if w.lower() not in STOPWORDS)
 
 
@@ -65,6 +82,7 @@ class HashWordPieceTokenizer:
 
     vocab_size = VOCAB_SIZE
     first_regular = 1000  # BERT's [unused]/special block lives below
+    name = "hash"
 
     def _id(self, w: str) -> int:
         return self.first_regular + zlib.crc32(w.encode()) % (VOCAB_SIZE - self.first_regular)
@@ -75,23 +93,37 @@ class HashWordPieceTokenizer:
         return ids
 
 
+class TokenizerUnavailable(RuntimeError):
+    pass
+
+
 def get_tokenizer(name_or_path: str | None = "bert-base-uncased"):
-    """HF tokenizer from the local cache / a path if it loads offline, else the fallback."""
-    if name_or_path:
-        try:
-            os.environ.setdefault("HF_HUB_OFFLINE", "1")
-            from transformers import AutoTokenizer
-            tok = AutoTokenizer.from_pretrained(name_or_path, local_files_only=True)
+    """The named HF tokenizer (local cache or a directory; no network), or the hash
+    tokenizer when ``name_or_path`` is ``"hash"``.  Raises ``TokenizerUnavailable`` when the
+    named tokenizer cannot be loaded -- never substitutes another one silently."""
+    if name_or_path in (None, "", "hash"):
+        if name_or_path != "hash":
+            raise TokenizerUnavailable("no tokenizer named (use 'bert-base-uncased', a path, or 'hash')")
+        return HashWordPieceTokenizer()
+    os.environ.setdefault("HF_HUB_OFFLINE", "1")
+    try:
+        from transformers import AutoTokenizer
+        tok = AutoTokenizer.from_pretrained(name_or_path, local_files_only=True)
+    except Exception as e:  # noqa: BLE001 - any loader failure is reported as one error
+        raise TokenizerUnavailable(
+            f"tokenizer {name_or_path!r} cannot be loaded offline ({type(e).__name__}: {e}); put it in the HF cache "
+            f"or pass a directory, or pass --tokenizer hash to use the built-in hash tokenizer explicitly") from e
 
-            class _HF:
-                vocab_size = tok.vocab_size
+    class _HF:
+        vocab_size = tok.vocab_size
+        name = str(name_or_path)
 
-                def encode(self, text, max_len=512):
-                    return tok(text, truncation=True, max_length=max_len)["input_ids"]
-            return _HF()
-        except Exception:
-            pass
-    return HashWordPieceTokenizer()
+        def encode(self, text, max_len=512):
+            return tok(text, truncation=True, max_length=max_len)["input_ids"]
+
+        def encode_batch(self, texts, max_len=512):
+            return tok(list(texts), truncation=True, max_length=max_len)["input_ids"]
+    return _HF()
 
 
 def get_tokenizer_size(name_or_path: str | None = "bert-base-uncased") -> int:
@@ -118,14 +150,15 @@ class TokenStore:
 
 
 def read_agnews_csv(path: str):
-    """AG News CSV rows ``"class","title","description"`` -> (texts, 0-based labels)."""
+    """AG News CSV rows ``"class","title","description"`` -> (texts, 0-based labels); the
+    text is the row's fields after the class joined by a space (torchtext's AG_NEWS)."""
     texts, labels = [], []
     with open(path, newline="", encoding="utf-8") as f:
         for row in csv.reader(f):
-            if len(row) < 3:
+            if len(row) < 2:
                 continue
             labels.append(int(row[0]) - 1)  # reference shifts labels by -1 (transformer_test.py:242)
-            texts.append(clean_text(row[1] + " " + row[2]))
+            texts.append(clean_text(" ".join(row[1:])))
     return texts, labels
 
 
@@ -147,16 +180,72 @@ def synthetic_agnews(n: int, seed: int = 0, max_len: int = 512, vocab: int = VOC
     return TokenStore(seqs, labels)
 
 
+def agnews_csv(root: str, split: str) -> str:
+    return os.path.join(root, "ag_news", f"{split}.csv")
+
+
+def download_agnews(root: str = "./data", splits=("train", "test")) -> list[str]:
+    """Fetch the AG News CSVs into ``root/ag_news`` (skipped when present with the right
+    MD5; a corrupted or truncated file is fetched again).  Call on one rank, then barrier."""
+    from .download import download_url
+    out = []
+    for sp in splits:
+        out.append(download_url(AGNEWS_URLS[sp], os.path.join(root, "ag_news"), f"{sp}.csv", AGNEWS_MD5[sp]))
+    return out
+
+
+def _tokenize_cached(path: str, tok, max_len: int) -> TokenStore:
+    with open(path, "rb") as fh:
+        digest = hashlib.md5(fh.read(), usedforsecurity=False).hexdigest()
+    name = re.sub(r"[^A-Za-z0-9_.-]+", "_", getattr(tok, "name", type(tok).__name__))
+    cache = os.path.join(os.path.dirname(path), f"tokens_{os.path.basename(path)[:-4]}_{name}_{max_len}.npz")
+    if os.path.isfile(cache):
+        z = np.load(cache)  # (allow_pickle=False: plain arrays only)
+        if str(z["md5"]) == digest:
+            st = TokenStore.__new__(TokenStore)
+            st.offsets, st.tokens, st.labels = z["offsets"], z["tokens"], z["labels"]
+            st.lengths = np.diff(st.offsets)
+            return st
+    texts, labels = read_agnews_csv(path)
+    if hasattr(tok, "encode_batch"):
+        seqs = []
+        for i in range(0, len(texts), 4096):
+            seqs.extend(tok.encode_batch(texts[i:i + 4096], max_len))
+    else:
+        seqs = [tok.encode(t, max_len) for t in texts]
+    st = TokenStore(seqs, labels)
+    try:
+        tmp = cache + ".tmp.npz"
+        np.savez(tmp, offsets=st.offsets, tokens=st.tokens, labels=st.labels, md5=np.array(digest))
+        os.replace(tmp, cache)
+    except OSError:
+        pass  # read-only data directory: no cache
+    return st
+
+
 def load_agnews(root: str = "./data", train: bool = True, tokenizer=None, max_len: int = 512,
-                synthetic: bool = False, seed: int = 0):
-    """TokenStore for the split: real CSV under ``root/ag_news`` if present (and not
-    ``synthetic``), otherwise the synthetic AG-News-shaped corpus."""
-    path = os.path.join(root, "ag_news", "train.csv" if train else "test.csv")
-    if not synthetic and os.path.isfile(path):
-        tok = tokenizer or get_tokenizer()
-        texts, labels = read_agnews_csv(path)
-        return TokenStore([tok.encode(t, max_len) for t in texts], labels)
-    return synthetic_agnews(TRAIN_SIZE if train else TEST_SIZE, seed=seed + (0 if train else 1), max_len=max_len)
+                synthetic: bool = False, seed: int = 0, download: bool = True):
+    """TokenStore for the split.  ``synthetic``: the AG-News-shaped synthetic corpus.
+    Otherwise the real CSV under ``root/ag_news`` -- downloaded first when missing and
+    ``download`` -- tokenised with ``tokenizer``; raises ``FileNotFoundError`` when the data
+    cannot be had (no silent substitute)."""
+    if synthetic:
+        return synthetic_agnews(TRAIN_SIZE if train else TEST_SIZE, seed=seed + (0 if train else 1),
+                                max_len=max_len)
+    split = "train" if train else "test"
+    path = agnews_csv(root, split)
+    if not os.path.isfile(path) and download:
+        try:
+            download_agnews(root, (split,))
+        except Exception as e:  # noqa: BLE001
+            raise FileNotFoundError(f"AG News {split} split not found at {path} and the download failed "
+                                    f"({type(e).__name__}: {e}); place the CSV there or pass --synthetic") from e
+    if not os.path.isfile(path):
+        raise FileNotFoundError(f"AG News {split} split not found at {path} (download disabled); "
+                                f"place the CSV there or pass --synthetic")
+    if tokenizer is None:
+        raise TokenizerUnavailable("load_agnews: real data needs a tokenizer (get_tokenizer(...))")
+    return _tokenize_cached(path, tokenizer, max_len)
 
 
 def _round_up(L, buckets):

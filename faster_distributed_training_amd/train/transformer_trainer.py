@@ -22,7 +22,7 @@ import numpy as np
 import torch
 import torch.nn as nn
 
-from ..data.agnews import NUM_CLASSES, TextBatchLoader, get_tokenizer, load_agnews
+from ..data.agnews import NUM_CLASSES, TextBatchLoader, download_agnews, get_tokenizer, load_agnews
 from ..models.transformer import Transformer
 from ..ops.mixup import mixup_criterion
 from ..optim.flat_optim import SGD, Adam, DeviceGradScaler, GradClipper, MirrorMADGRAD, MADGRAD
@@ -163,8 +163,18 @@ class TransformerTrainer:
 
     def _build_data(self):
         cfg = self.cfg
-        tr = load_agnews(cfg.data_root, True, self.tokenizer, cfg.maxlen, cfg.synthetic, seed=1)
-        te = load_agnews(cfg.data_root, False, self.tokenizer, cfg.maxlen, cfg.synthetic, seed=1)
+        if not cfg.synthetic:
+            # one rank downloads (reference: AG_NEWS(root='./data'), transformer_test.py:88-93);
+            # everyone then reads, and fails the same way if the data is still missing
+            if self.rank == 0:
+                try:
+                    download_agnews(cfg.data_root)
+                except Exception as e:  # noqa: BLE001 - reported by load_agnews below on every rank
+                    print(f"AG News download failed: {type(e).__name__}: {e}", flush=True)
+            from ..parallel.dist import barrier
+            barrier()
+        tr = load_agnews(cfg.data_root, True, self.tokenizer, cfg.maxlen, cfg.synthetic, seed=1, download=False)
+        te = load_agnews(cfg.data_root, False, self.tokenizer, cfg.maxlen, cfg.synthetic, seed=1, download=False)
         sub = cfg.extra.get("subset_stride")
         if sub:
             from ..data.agnews import TokenStore

@@ -36,7 +36,8 @@ def parse(argv=None):
     p.add_argument("--scheduler", default="onecycle", choices=["onecycle", "multistep"])
     p.add_argument("--synthetic", action="store_true", help="AG-News-shaped synthetic corpus (no download)")
     p.add_argument("--data_root", default="./data")
-    p.add_argument("--tokenizer", default="bert-base-uncased")
+    p.add_argument("--tokenizer", default="bert-base-uncased",
+                   help="HF tokenizer name (local cache) or directory; 'hash' = built-in hash tokenizer (explicit only)")
     p.add_argument("--seed", default=123456, type=int)
     p.add_argument("--precision", default="bf16", choices=["bf16", "fp16", "fp32"])
     p.add_argument("--fsdp", action="store_true", help="flat-sharded data parallel (reference: FSDP)")
