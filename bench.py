@@ -44,6 +44,8 @@ def parse():
     ap.add_argument("--fsdp", action="store_true")
     ap.add_argument("--fsdp-param-dtype", default="bf16", choices=["bf16", "fp32"],
                     help="--fsdp: parameter all-gather wire / compute-copy precision (masters stay fp32)")
+    ap.add_argument("--fsdp-schedule", default="full_shard", choices=["full_shard", "shard_grad_op"],
+                    help="--fsdp: FULL_SHARD (reshard after forward, re-gather in backward) or SHARD_GRAD_OP")
     ap.add_argument("--sharded-ngd", action="store_true",
                     help="with --ngd at N=1: run the sharded-NGD data-parallel path over a world-1 group")
     ap.add_argument("--ddp", action="store_true",
@@ -114,7 +116,7 @@ def main():
                        precision=args.precision, bucket_mb=args.bucket_mb, comm_dtype=args.comm_dtype,
                        fast_path=False if args.no_native else None, graphs=not args.no_graphs,
                        deterministic=args.deterministic, force_sharded=args.sharded_ngd, force_ddp=args.ddp,
-                       fsdp_param_dtype=args.fsdp_param_dtype)
+                       fsdp_param_dtype=args.fsdp_param_dtype, fsdp_schedule=args.fsdp_schedule)
     tr = ResNetTrainer(cfg)
     dev = tr.device
     cuda = dev.type == "cuda"
@@ -218,6 +220,9 @@ def _sharding_fields(tr, rec):
         cfg["fsdp_peak_full_bytes"] = int(tr.fsdp.peak_full_bytes)
         cfg["fsdp_shard_numel"] = int(tr.fsdp.space.numel)
         cfg["fsdp_static_graphs"] = bool(tr.fsdp.static)
+        # what actually ran: the static ring is FULL_SHARD; static without it SHARD_GRAD_OP;
+        # eager FSDP reshards after forward (FULL_SHARD)
+        cfg["fsdp_schedule"] = "shard_grad_op" if (tr.fsdp.static and not tr.fsdp.ring) else "full_shard"
         cfg["fsdp_param_dtype"] = str(tr.fsdp.param_dtype or torch.float32).replace("torch.", "")
     elif tr.zero is not None:
         cfg["optimizer_sharding"] = "ngd-owner-shards (bucketed all-reduce overlapped with backward + all-gather)"

@@ -155,6 +155,7 @@ class Unit:
             self.owned = [(i, self.pos[i] - lo) for i in range(len(params))
                           if self.pos[i] >= lo and self.pos[i] + params[i][1].numel() <= hi]
         self.numel = ws * self.chunk
+        self.slot = None  # full-shard static mode: index of the ring slot holding this unit
         dev = fs.device
         self.full = torch.zeros(self.numel, device=dev, dtype=torch.float32)
         # param_dtype bf16: the all-gather moves bf16 (half the bytes on xGMI) into this
@@ -195,10 +196,40 @@ class Unit:
             st.resize_(0)
 
     # ------------------------------------------------------------ gather / reshard
+    def bind_ring(self, slot, full, full16, gfull):
+        """Full-shard static mode: this unit's gathered parameters / gradient live in ring
+        slot ``slot`` (fixed addresses shared with the other units of that slot)."""
+        self.slot = slot
+        self.full, self.full16, self.gfull = full[:self.numel], (None if full16 is None else full16[:self.numel]), \
+            gfull[:self.numel]
+        with torch.no_grad():
+            for i, (n, p) in enumerate(self.params):
+                v = self.full[self.pos[i]:self.pos[i] + p.numel()].view(p.shape)
+                self.views[i] = v
+                p.data = v
+        self.gathered = False
+
+    def _claim_slot(self):
+        """Ring: take this unit's slot from its previous owner (whose parameters are about to
+        be overwritten; an in-flight gather of theirs is ordered first)."""
+        fs = self.fs
+        owner = fs.slot_owner[self.slot]
+        if owner is self:
+            return
+        if owner is not None:
+            if owner.work is not None:
+                owner.work.wait()
+                owner.work = None
+            owner.gathered = False
+        fs.slot_owner[self.slot] = self
+        self.gathered = False
+
     def gather(self, wait=True, exact=False):
         """All-gather this unit's parameters (``exact``: fp32 wire even with a bf16
         param_dtype -- checkpoint I/O)."""
         fs = self.fs
+        if self.slot is not None:
+            self._claim_slot()
         if not self.gathered and self.work is None:
             self._alloc(self.full)
             fs._account()
@@ -260,6 +291,8 @@ class Unit:
             self.rs_work = dist.reduce_scatter_tensor(fs.grad_chunk(self), self.gfull, op=op, group=fs.pg,
                                                       async_op=True)
             self.grads_live = False
+            if self.slot is not None:
+                fs.grad_owner[self.slot] = self
             return
         op = dist.ReduceOp.AVG if fs.use_avg else dist.ReduceOp.SUM
         self.rs_work = dist.reduce_scatter_tensor(fs.grad_chunk(self), self.gfull, op=op, group=fs.pg,
@@ -299,13 +332,15 @@ class FullyShardedDP:
     sharded_optimizer = True
 
     def __init__(self, model: nn.Module, device=None, units=None, mode="flat", offload=False, process_group=None,
-                 prefetch=True, engine_units=(), static=False, param_dtype=None):
+                 prefetch=True, engine_units=(), static=False, param_dtype=None, reshard_after_forward=True):
         """units: [(name, module)] (None: ``default_units``); mode: 'flat' | 'param' (NGD);
         engine_units: names of units whose forward/backward an engine drives explicitly
-        (no module hooks installed on them); static: persistent buffers, HIP-graph capture
-        (see the module docstring)."""
+        (no module hooks installed on them); static: fixed-address buffers, HIP-graph capture
+        (see the module docstring); reshard_after_forward (static mode): FULL_SHARD on a
+        two-slot ring (True) or SHARD_GRAD_OP with every unit's buffers persistent (False)."""
         self.model = model
         self.static = bool(static)
+        self.ring = self.static and bool(reshard_after_forward)
         self.param_dtype = param_dtype if param_dtype not in (None, torch.float32) else None
         self.pg = process_group
         self.ws = dist.get_world_size(process_group)
@@ -366,12 +401,30 @@ class FullyShardedDP:
                 slots.append(Slot(n, p, off + rel, p.numel(), p.shape))
             off += u.chunk
         self.space = SpaceView(self.shard_data, self.shard_grad, slots, sdev)
+        self.order = [u for u in self.units if not u.root]
+        self.slot_owner, self.grad_owner, self.ring_bytes = [], [], 0
+        if self.ring:
+            # two slots, units alternating in forward order (neighbours -- the unit in use and
+            # the one being prefetched -- never share a slot); a slot is sized for its largest
+            # unit, so the gathered footprint is the two largest units (conv4_x + conv5_x for
+            # ResNet-50), parameters and gradients alike.  The shards were taken above from the
+            # private initial buffers, which are dropped here.
+            nslot = 2 if len(self.order) > 1 else 1
+            for k in range(nslot):
+                size = max(u.numel for i, u in enumerate(self.order) if i % nslot == k)
+                full = torch.zeros(size, device=self.device, dtype=torch.float32)
+                f16 = torch.zeros(size, device=self.device, dtype=self.param_dtype) if self.param_dtype else None
+                gfull = torch.zeros(size, device=self.device, dtype=torch.float32)
+                for i, u in enumerate(self.order):
+                    if i % nslot == k:
+                        u.bind_ring(k, full, f16, gfull)
+                self.ring_bytes += 2 * size * 4
+            self.slot_owner, self.grad_owner = [None] * nslot, [None] * nslot
         self.stage16 = (torch.empty(total, device=self.device, dtype=self.param_dtype)
                         if self.param_dtype is not None else None)
         self.view = self.space  # (trainer interface shared with the sharded-optimizer DP)
         self.peak_full_bytes = 0
         self.last_rs = None  # unit whose reduce-scatter was launched last
-        self.order = [u for u in self.units if not u.root]
         self.engine_units = set(engine_units)
         self._hooks = []
         self._install_hooks()
@@ -400,12 +453,14 @@ class FullyShardedDP:
         return self.shard_grad[u.shard_off:u.shard_off + u.chunk]
 
     def _account(self):
-        b = sum(u._bytes() for u in self.units if u.full.untyped_storage().size() != 0)
-        b += sum(u._bytes() for u in self.units if u.gfull.untyped_storage().size() != 0)
-        self.peak_full_bytes = max(self.peak_full_bytes, b)
+        own = [u for u in self.units if u.slot is None]
+        b = sum(u._bytes() for u in own if u.full.untyped_storage().size() != 0)
+        b += sum(u._bytes() for u in own if u.gfull.untyped_storage().size() != 0)
+        self.peak_full_bytes = max(self.peak_full_bytes, b + self.ring_bytes)
 
     def resident_param_bytes(self):
-        return sum(u._bytes() for u in self.units if u.full.untyped_storage().size() != 0)
+        own = sum(u._bytes() for u in self.units if u.slot is None and u.full.untyped_storage().size() != 0)
+        return own + self.ring_bytes // 2
 
     # ------------------------------------------------------------ unit API (hooks / engine)
     def _next(self, u, step):
@@ -448,6 +503,18 @@ class FullyShardedDP:
 
     def pre_backward(self, name):
         u = self.by_name[name]
+        if self.ring:
+            # FULL_SHARD on the ring: before the unit's backward segment, its gradient slot's
+            # previous reduce-scatter must have read the slot, its parameters are gathered again
+            # unless still resident from forward, and the previous unit is prefetched -- one
+            # action between graph segments (engine units), or now (module-hook units); the
+            # gradient slot is then zeroed in stream order (captured)
+            if name in self.engine_units:
+                self._deferred(lambda: self._ring_bwd_prepare(u))
+            else:
+                self._ring_bwd_prepare(u)
+            u.begin_backward(gather=False)
+            return
         if self.static:
             # parameters are still gathered from this step's forward (engine units: always --
             # while capturing, the forward's gathers are deferred actions, so the host flag
@@ -458,6 +525,18 @@ class FullyShardedDP:
         if self.prefetch:
             prv = self._next(u, -1)
             if prv is not None and not prv.bwd_started:
+                prv.gather(wait=False)
+
+    def _ring_bwd_prepare(self, u):
+        o = self.grad_owner[u.slot]
+        if o is not None and o is not u and o.rs_work is not None:
+            o.rs_work.wait()  # (stream wait: the slot's reduce-scatter has read it)
+            o.rs_work = None
+        self.grad_owner[u.slot] = u
+        u.gather(wait=True)
+        if self.prefetch:
+            prv = self._next(u, -1)
+            if prv is not None:
                 prv.gather(wait=False)
 
     def post_backward(self, name):
@@ -526,12 +605,15 @@ class FullyShardedDP:
     def finish_backward(self):
         """Complete every unit's gradient reduce-scatter (launch what is left, e.g. units
         whose parameters got no gradient), land the averaged shard gradients."""
+        unused = []
         for u in self.units:
             if u.bwd_started or u.grads_live or u.rs_work is not None:
                 u.finish()
-            else:  # unused this step: contributes zeros (every rank must join the collective)
-                u.begin_backward(gather=False)
-                u.finish()
+            else:
+                unused.append(u)
+        for u in unused:  # contributes zeros (every rank must join the collective); after the
+            u.begin_backward(gather=False)  # others, whose reduce-scatters may read a shared ring slot
+            u.finish()
         self.last_rs = None
         if self.offload:
             if self.copy_stream is not None:
@@ -562,7 +644,12 @@ class FullyShardedDP:
     @contextlib.contextmanager
     def summon_full_params(self):
         """All units gathered (checkpointing / state_dict) with the exact fp32 masters (also
-        under a bf16 param_dtype); resharded on exit."""
+        under a bf16 param_dtype); resharded on exit.  Not available on the full-shard ring
+        (units share slots): use ``full_state_dict`` / ``load_full_state_dict``, which stream
+        unit by unit."""
+        if self.ring:
+            raise RuntimeError("summon_full_params: full-shard ring mode holds two units at a time; "
+                               "use full_state_dict() / load_full_state_dict()")
         for u in self.units:
             if u.full16 is not None:
                 if u.work is not None:
@@ -577,6 +664,8 @@ class FullyShardedDP:
 
     def load_full_state_dict(self, sd, strict=True):
         """Load a full (reference-schema) state_dict: every rank keeps its shard of it."""
+        if self.ring:
+            return self._ring_load(sd, strict)
         with self.summon_full_params():
             res = self.model.load_state_dict(sd, strict=strict)
             with torch.no_grad():
@@ -586,8 +675,45 @@ class FullyShardedDP:
         return res
 
     def full_state_dict(self):
+        if self.ring:
+            return self._ring_state_dict()
         with self.summon_full_params():
             return {k: v.detach().clone().cpu() for k, v in self.model.state_dict().items()}
+
+    def _ring_state_dict(self):
+        """Unit by unit: exact fp32 gather into the unit's slot, copy out (collective)."""
+        vals = {}
+        for u in self.units:
+            u.gather(wait=True, exact=True)
+            for _, p in u.params:
+                vals[id(p)] = p.detach().clone().cpu()
+        for u in self.units:  # (exact masters are not the bf16-wire values forward expects)
+            if u.slot is not None:
+                u.gathered = False
+        return {k: (vals[id(v)] if id(v) in vals else v.detach().clone().cpu())
+                for k, v in self.model.state_dict(keep_vars=True).items()}
+
+    @torch.no_grad()
+    def _ring_load(self, sd, strict):
+        keys = list(self.model.state_dict(keep_vars=True).keys())
+        missing = [k for k in keys if k not in sd]
+        unexpected = [k for k in sd if k not in set(keys)]
+        if strict and (missing or unexpected):
+            raise RuntimeError(f"load_full_state_dict: missing {missing[:5]}, unexpected {unexpected[:5]}")
+        for u in self.units:
+            if u.slot is not None:
+                u._claim_slot()
+            for n, p in u.params:
+                if n in sd:
+                    p.data.copy_(sd[n].to(p.device, p.dtype).view(p.shape))
+            lo = self.rank * u.chunk
+            self.shard_data[u.shard_off:u.shard_off + u.chunk].copy_(u.full[lo:lo + u.chunk])
+            if u.slot is not None:
+                u.gathered = False
+        for n, b in self.model.named_buffers():
+            if n in sd:
+                b.copy_(sd[n].to(b.device, b.dtype).view(b.shape))
+        return missing, unexpected
 
     def remove(self):
         for h in self._hooks:

@@ -38,8 +38,7 @@ def model_state(model, module_prefix=False):
     collective and must run on every rank."""
     fs = _sharded(model)
     if fs is not None:
-        with fs.summon_full_params():
-            sd = _compact(model.state_dict())
+        sd = fs.full_state_dict()  # (compact CPU copies, unit by unit on the full-shard ring)
     else:
         sd = _compact(model.state_dict())
     if module_prefix:

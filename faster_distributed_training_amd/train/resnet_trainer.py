@@ -61,6 +61,7 @@ class ResNetConfig:
     fsdp: bool = False
     fsdp_offload: bool = False         # FSDP shards + optimizer state in pinned host memory (CPUOffload)
     fsdp_param_dtype: str = "fp32"     # fp32 | bf16: all-gather wire / compute copy of the parameters
+    fsdp_schedule: str = "full_shard"  # full_shard (reshard after forward) | shard_grad_op (graph path only)
     shard_ngd: bool = True             # distributed NGD: each rank owns + preconditions 1/world of the params
     scheduler: str = "auto"
     resume: bool = False
@@ -125,13 +126,16 @@ class ResNetTrainer:
                 raise ValueError("--fsdp does not shard the learnable meta-mixup parameters")
             from ..parallel.fsdp import FullyShardedDP
             engine = self.model.use_fast_path(torch.empty(1, device=self.device))
-            # HIP graphs under FSDP: static mode (persistent unit buffers, SHARD_GRAD_OP-style
-            # schedule, collectives between graph segments); eager FSDP is the full ZeRO-3
-            # reshard-after-forward schedule
+            # HIP graphs under FSDP: static mode (fixed-address unit buffers, collectives between
+            # graph segments) -- FULL_SHARD on a two-slot ring (default) or SHARD_GRAD_OP with
+            # every unit's buffers persistent; eager FSDP is the full ZeRO-3 schedule
             static = bool(engine and cfg.graphs and not cfg.fsdp_offload and cfg.extra.get("fsdp_static", True))
+            if cfg.fsdp_schedule not in ("full_shard", "shard_grad_op"):
+                raise ValueError(f"fsdp_schedule {cfg.fsdp_schedule!r}")
             self.model.graph_engine = static
             self.fsdp = FullyShardedDP(self.model, self.device, mode="param" if ngd_opt else "flat",
                                        offload=cfg.fsdp_offload, static=static,
+                                       reshard_after_forward=cfg.fsdp_schedule == "full_shard",
                                        param_dtype={"fp32": None, "bf16": torch.bfloat16}[cfg.fsdp_param_dtype],
                                        engine_units=("conv1",) + STAGES if engine else ())
             if engine:

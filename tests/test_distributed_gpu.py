@@ -158,7 +158,7 @@ def _fsdp_engine_worker(rank, world, offload=False):
     assert fs.peak_full_bytes <= _fsdp_peak_bound(fs) < sum(2 * u._bytes() for u in fs.units)
 
 
-def _fsdp_static_graph_worker(rank, world):
+def _fsdp_static_graph_worker(rank, world, schedule="shard_grad_op"):
     """FSDP static mode (the engine's HIP-graph path): the body is captured as
     graph segments cut at the stage boundaries, each unit's all-gather wait / prefetch and
     reduce-scatter running as actions between them; over eager warm-up, capture and replays
@@ -180,7 +180,9 @@ def _fsdp_static_graph_worker(rank, world):
     m = R.resnet50(10).to(dev)
     m.fast_path = True
     m.graph_engine = True
-    fs = FullyShardedDP(m, dev, engine_units=("conv1",) + STAGES, static=True)
+    fs = FullyShardedDP(m, dev, engine_units=("conv1",) + STAGES, static=True,
+                        reshard_after_forward=schedule == "full_shard")
+    assert fs.ring == (schedule == "full_shard")
     m._fsdp = fs
     ref.load_state_dict(fs.full_state_dict())
     rflat = FlatParams(ref, device=dev)
@@ -212,10 +214,17 @@ def _fsdp_static_graph_worker(rank, world):
     assert st.stage == "ready"
     assert len(st.fwd.segments) >= len(STAGES) + 1  # cut before every stage's forward
     assert sum(len(a) for _, a in st.rec.segments) >= len(STAGES)  # reduce-scatters between segments
+    if schedule == "full_shard":
+        # re-gather / grad-slot actions before the stages' backward segments as well
+        assert sum(len(a) for _, a in st.rec.segments) >= 2 * len(STAGES) - 1
+        sizes = sorted((u._bytes() for u in fs.order), reverse=True)
+        root = sum(2 * u._bytes() for u in fs.units if u.root)
+        assert fs.peak_full_bytes <= 2 * (sizes[0] + sizes[1]) + root, (fs.peak_full_bytes, sizes[:2])
 
 
-def test_fsdp_static_graphs_two_ranks_one_gpu(cuda):
-    run_world(_fsdp_static_graph_worker, world=2, native=True, timeout=400)
+@pytest.mark.parametrize("schedule", ["shard_grad_op", "full_shard"])
+def test_fsdp_static_graphs_two_ranks_one_gpu(cuda, schedule):
+    run_world(_fsdp_static_graph_worker, world=2, native=True, timeout=400, args=(schedule,))
 
 
 def _fsdp_peak_bound(fs):
