@@ -214,7 +214,10 @@ def _sharding_fields(tr, rec):
         plan = getattr(tr.model, "_plan", None)
         states = list(getattr(plan, "_graphs", {}).values()) if plan is not None else []
         if states and states[0].segments:
+            from faster_distributed_training_amd.parallel import graphs
             cfg["bwd_graph_segments"] = len(states[0].segments)
+            cfg["bwd_comm_event_points"] = int(getattr(states[0].rec, "event_points", 0))
+            cfg["graph_comm"] = graphs.DETACHED_MODE
     if tr.fsdp is not None:
         cfg["fsdp_units"] = len(tr.fsdp.units)
         cfg["fsdp_peak_full_bytes"] = int(tr.fsdp.peak_full_bytes)
@@ -248,7 +251,8 @@ def bench_transformer(args):
     buckets = tuple(sorted(int(b) for b in args.seq_buckets.split(",")))
     cfg = TransformerConfig(batch_size=gb // world, synthetic=True, eval=False, plot=False, distributed=world > 1,
                             ngd=True, precision=args.precision, length_buckets=buckets,
-                            bucket_mb=args.bucket_mb, fsdp=args.fsdp, epoch=1, fsdp_param_dtype=args.fsdp_param_dtype)
+                            bucket_mb=args.bucket_mb, fsdp=args.fsdp, epoch=1, fsdp_param_dtype=args.fsdp_param_dtype,
+                            fsdp_schedule=args.fsdp_schedule)
     tr = TransformerTrainer(cfg)
     longest = int(tr.train_loader.store.lengths.max())
     assert longest <= buckets[-1], f"largest bucket {buckets[-1]} would truncate samples of length {longest}"
@@ -288,6 +292,7 @@ def bench_transformer(args):
                       "parallelism": f"{'fsdp' if args.fsdp else 'dp'}{world}", "optimizer": "ngd"},
            "peak_mem_gb": round(torch.cuda.max_memory_allocated() / 2**30, 2) if cuda else None,
            "host_ms_per_step": round(host / args.steps * 1e3, 3)}
+    rec["config"]["hip_graphs"] = bool(tr._graphs_on()) if cuda else False
     _sharding_fields(tr, rec)
     _dist_fields(rec)
     if tr.rank == 0:

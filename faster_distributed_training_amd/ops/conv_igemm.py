@@ -98,6 +98,16 @@ def tune_key(batch: int, h: int, shp) -> str:
     return f"{batch}:{h}:{shp.cin}:{shp.cout}:{shp.k}:{shp.stride}:{shp.pad}"
 
 
+# Launch record (tests): when a list, every conv launch appends (kind, tune key, tuned entry
+# found, (bm, bn, bk), nsplit, K groups) -- which shipped tile-table choices actually ran.
+LAUNCH_LOG = None
+
+
+def _log(kind, batch, h, shp, ent, tile3, ns, kg=1):
+    if LAUNCH_LOG is not None:
+        LAUNCH_LOG.append((kind, tune_key(batch, h, shp), bool(ent and "tile" in ent), tuple(tile3), int(ns), int(kg)))
+
+
 def tuned(op: str, batch: int, h: int, shp):
     """Tuned launch config (scripts/tune_conv.py) for this exact problem, or None."""
     global _TUNED
@@ -254,6 +264,7 @@ def conv_fwd(x, wf, shp: ConvShape, s=None, t=None, act=0, alpha=1.0, tile=None,
         ent = {"nsplit": nsplit}
     ns, slab_p, cnt_p = _splitk_args(ent, M, shp.cout, shp.ntaps * C, bm, bn, bk, x.device)
     kgv = _kg(ent, kg, (bm, bn, bk), ns, shp.ntaps * C)
+    _log("fwd", N, H, shp, ent, (bm, bn, bk), ns, kgv)
     y = torch.empty(N, Ho, Wo, shp.cout, device=x.device, dtype=torch.bfloat16)
     if part is None:
         part = stat_slots(2, shp.cout, x.device, M)
@@ -297,6 +308,7 @@ def conv_fwd_join(y, r, s, t, s2, t2, wf, shp: ConvShape, jout, jmask=None, tile
         ent = {"nsplit": nsplit}
     ns, slab_p, cnt_p = _splitk_args(ent, M, shp.cout, C, bm, bn, bk, y.device)
     kgv = _kg(ent, kg, (bm, bn, bk), ns, C)
+    _log("fwd_join", N, H, shp, ent, (bm, bn, bk), ns, kgv)
     out = torch.empty(N, H, W, shp.cout, device=y.device, dtype=torch.bfloat16)
     if part is None:
         part = stat_slots(2, shp.cout, y.device, M)
@@ -355,6 +367,7 @@ def conv_dgrad(g, y, al, be, wd, shp: ConvShape, x_shape, epi=EPI_STORE, out=Non
         bm, bn, bk = _tile3(tile, M, shp.cin)
         ns, slab_p, cnt_p = _splitk_args(ent, M, shp.cin, len(dh) * Cy, bm, bn, bk, g.device)
         kgv = _kg(ent, kg, (bm, bn, bk), ns, len(dh) * Cy)
+        _log("dgrad", N, Hx, shp, ent, (bm, bn, bk), ns, kgv)
         pro = PRO_FOLD if al is not None else PRO_NONE  # al None: g is already folded
         assert gs is None or pro == PRO_FOLD, "gs needs the fold prologue (al/be)"
         nat.conv_igemm(g.data_ptr(), _p(y) if pro == PRO_FOLD else 0, _p(al), _p(be), _p(gs), wd.data_ptr(),
@@ -384,6 +397,7 @@ def conv_wgrad(g, y, al, be, x, shp: ConvShape, out, xs=None, xt=None, act=0, al
     assert Cx == shp.cxp and Cy == shp.cout
     M = N * Hy * Wy
     ldw = shp.ntaps * shp.cxp
+    ent = None
     if tile is None:
         ent = tuned(f"wgrad{int(al is not None)}{int(xs is not None or act != 0)}", N, H, shp) or \
             tuned("wgrad", N, H, shp)
@@ -400,6 +414,7 @@ def conv_wgrad(g, y, al, be, x, shp: ConvShape, out, xs=None, xt=None, act=0, al
         bm, bn, bk = tile
     tiles = (shp.cout // bm) * (-(-ldw // bn))
     ns = nsplit or wgrad_split(M, tiles)
+    _log("wgrad", N, H, shp, ent, (bm, bn, bk), ns)
     # 1x1 without channel padding: the slab row layout IS OIHW -> every split adds into
     # `out` with fp32 atomics (no slab, no reduce launch); deterministic mode keeps the
     # ordered slab reduction

@@ -128,7 +128,7 @@ class BucketReducer:
         b = self.bucket_of[id(p)]
         self.pending[b] -= 1
         if self.pending[b] == 0:
-            act = lambda: self._launch(b)  # noqa: E731
+            act = graphs.detached(lambda: self._launch(b))  # nothing in the graph waits for it
             if defer:
                 return act
             rec = graphs.active()

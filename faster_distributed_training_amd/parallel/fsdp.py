@@ -278,6 +278,18 @@ class Unit:
     def grad_ready(self):
         self.pending -= 1
         if self.pending == 0:
+            if self.fs.static:
+                from . import graphs
+                if graphs.active() is not None:
+                    # backward being captured (module-hook units, e.g. the transformer's
+                    # sublayers): the reduce-scatter is an action of every replay
+                    self.grads_live = False
+
+                    def act(u=self):
+                        u.grads_live = True
+                        u.reduce()
+                    self.fs._deferred(graphs.detached(act))
+                    return
             self.reduce()
 
     def reduce(self):
@@ -480,7 +492,7 @@ class FullyShardedDP:
             fn()
 
     def pre_forward(self, name):
-        if self.static and name in self.engine_units:
+        if self.static:  # (a cut while a capture records, now otherwise)
             return self._deferred(lambda: self._pre_forward_now(name))
         self._pre_forward_now(name)
 
@@ -509,17 +521,16 @@ class FullyShardedDP:
             # unless still resident from forward, and the previous unit is prefetched -- one
             # action between graph segments (engine units), or now (module-hook units); the
             # gradient slot is then zeroed in stream order (captured)
-            if name in self.engine_units:
-                self._deferred(lambda: self._ring_bwd_prepare(u))
-            else:
-                self._ring_bwd_prepare(u)
+            self._deferred(lambda: self._ring_bwd_prepare(u))
             u.begin_backward(gather=False)
             return
         if self.static:
-            # parameters are still gathered from this step's forward (engine units: always --
-            # while capturing, the forward's gathers are deferred actions, so the host flag
-            # cannot tell); the gradient buffer is zeroed in stream order (a captured memset)
-            u.begin_backward(gather=(not u.gathered) and name not in self.engine_units)
+            # parameters are still gathered from this step's forward (SHARD_GRAD_OP keeps every
+            # unit; while capturing, the forward's gathers are deferred actions, so the host
+            # flag cannot tell); the gradient buffer is zeroed in stream order (captured)
+            from . import graphs
+            u.begin_backward(gather=(not u.gathered) and name not in self.engine_units
+                             and graphs.active() is None)
             return
         u.begin_backward()
         if self.prefetch:
@@ -549,7 +560,9 @@ class FullyShardedDP:
                 def act(u=u):
                     u.grads_live = True
                     u.reduce()
-                return self._deferred(act)
+                # nothing in the graph waits for the reduce-scatter (on the ring, the next user
+                # of the gradient slot waits for it in its own pre-backward action, issued after)
+                return self._deferred(graphs.detached(act))
         u.reduce()
 
     # ------------------------------------------------------------ module hooks

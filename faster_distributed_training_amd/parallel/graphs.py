@@ -17,6 +17,7 @@ that it runs on autograd's device thread like the hooks that cut it).  Reference
 from __future__ import annotations
 
 import contextlib
+import os
 
 import torch
 from torch.utils._python_dispatch import TorchDispatchMode
@@ -25,9 +26,53 @@ from torch.utils._python_dispatch import TorchDispatchMode
 # grad_ready from the autograd thread); None outside a capture.
 _ACTIVE = None
 
+# How DETACHED actions are placed -- collectives that nothing later in the graph waits for
+# (DDP / ZeRO bucket all-reduces, FSDP SHARD_GRAD_OP reduce-scatters; the compute stream meets
+# them only after the step's backward):
+#   "event": the capture is NOT cut.  An external event-record node marks the point in the
+#            graph, and the replay issues the action on a side stream that waits for that node,
+#            so the collective starts when the graph reaches it while the backward stays one
+#            graph (no graph-boundary bubbles on the compute queue).
+#   "cut":   the capture is cut there and the action runs between the two replayed segments
+#            (round-3 scheme: ~25-50 us of compute-queue idle per cut, profiles/r3s3/).
+DETACHED_MODE = os.environ.get("FDT_GRAPH_COMM", "event")
+
 
 def active():
     return _ACTIVE
+
+
+def detached(fn):
+    """Mark ``fn`` (a deferred GPU action) as one nothing in the captured graph depends on."""
+    fn.detached = True
+    return fn
+
+
+_COMM_SIDE = {}
+
+
+def _comm_side_stream(device):
+    """High-priority side stream the event-gated actions are issued from (its own hardware
+    queue: a wait on it never sits in the compute queue)."""
+    idx = torch.device(device).index if torch.device(device).index is not None else torch.cuda.current_device()
+    st = _COMM_SIDE.get(idx)
+    if st is None:
+        st = _COMM_SIDE[idx] = torch.cuda.Stream(device=idx, priority=-1)
+    return st
+
+
+class _OnEvent:
+    """A detached action gated on an event-record node of the replayed graph."""
+
+    detached = True
+
+    def __init__(self, event, fn, side):
+        self.event, self.fn, self.side = event, fn, side
+
+    def __call__(self):
+        with torch.cuda.stream(self.side):
+            self.side.wait_event(self.event)
+            self.fn()
 
 
 class Recorder:
@@ -45,6 +90,8 @@ class Recorder:
         self.cur = None
         self.stream = None
         self.foreign_cuts = 0  # cuts requested from a stream other than the capture stream
+        self.pending = []      # event-gated detached actions of the open segment
+        self.event_points = 0  # detached actions placed on event-record nodes (no cut)
 
     def begin(self):
         if self.stream is None:
@@ -61,16 +108,27 @@ class Recorder:
 
     def cut(self, actions):
         self._join()
+        if DETACHED_MODE == "event" and actions and all(getattr(a, "detached", False) for a in actions):
+            # no cut: an external event-record node here, the actions gated on it at replay
+            ev = torch.cuda.Event(external=True)
+            with torch.cuda.stream(self.stream):
+                ev.record(self.stream)
+            side = _comm_side_stream(self.stream.device)
+            self.pending += [_OnEvent(ev, a, side) for a in actions]
+            self.event_points += 1
+            return
         with torch.cuda.stream(self.stream):
             self.cur.capture_end()
-        self.segments.append((self.cur, list(actions)))
+        self.segments.append((self.cur, self.pending + list(actions)))
+        self.pending = []
         self.begin()
 
     def end(self):
         self._join()
         with torch.cuda.stream(self.stream):
             self.cur.capture_end()
-        self.segments.append((self.cur, []))
+        self.segments.append((self.cur, self.pending))
+        self.pending = []
         self.cur = None
 
     def replay(self):
@@ -146,11 +204,18 @@ class SegmentedStep:
         rec = Recorder(self.pool)
         self.one = torch.ones((), device=self.device)  # static seed gradient of the loss
         with torch.cuda.stream(side):
-            self.fwd = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(self.fwd, pool=self.pool, stream=side, capture_error_mode="thread_local"), \
-                    capture_guard():
-                out = fwd()
-                loss = _BackwardCaptureStart.apply(out[0], rec)
+            # the forward is a Recorder too: FSDP's per-unit gathers (static mode) cut it into
+            # segments, each unit's all-gather wait / next-unit prefetch between them
+            frec = Recorder(self.pool)
+            frec.stream = side
+            with recording(frec), capture_guard():
+                frec.begin()
+                try:
+                    out = fwd()
+                    loss = _BackwardCaptureStart.apply(out[0], rec)
+                finally:
+                    frec.end()
+            self.fwd = frec
             assert loss.dim() == 0 and loss.dtype == torch.float32, "SegmentedStep: scalar fp32 loss"
             with recording(rec), capture_guard():
                 loss.backward(self.one)
@@ -161,7 +226,7 @@ class SegmentedStep:
 
     @property
     def num_segments(self):
-        return 1 + (len(self.rec.segments) if self.rec else 0)
+        return len(self.fwd.segments) + (len(self.rec.segments) if self.rec else 0)
 
     def replay(self):
         self.fwd.replay()

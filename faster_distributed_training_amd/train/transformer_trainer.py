@@ -62,6 +62,7 @@ class TransformerConfig:
     fsdp: bool = False
     fsdp_offload: bool = False       # FSDP shards + optimizer state in pinned host memory (reference CPUOffload)
     fsdp_param_dtype: str = "fp32"   # fp32 | bf16: all-gather wire / compute copy of the parameters
+    fsdp_schedule: str = "full_shard"  # full_shard | shard_grad_op (the HIP-graph path's static FSDP)
     shard_ngd: bool = True           # distributed NGD: each rank owns + preconditions 1/world of the params
     bucket_mb: float = 25.0           # measured faster than 8 MB (profiles/r3s3/ddp_world1_*.json)
     resume: bool = False
@@ -115,8 +116,15 @@ class TransformerTrainer:
             # embedding / attention / FFN sublayer / head, gathered with prefetch and
             # reduce-scattered from gradient hooks; NGD sees whole parameters (Q17)
             from ..parallel.fsdp import FullyShardedDP
+            if cfg.fsdp_schedule not in ("full_shard", "shard_grad_op"):
+                raise ValueError(f"fsdp_schedule {cfg.fsdp_schedule!r}")
+            # static mode (fixed-address unit buffers) when the step will be captured as HIP
+            # graphs: each unit's gather / prefetch and reduce-scatter become actions between
+            # graph segments (parallel/graphs.SegmentedStep)
+            static = bool(self._graphs_wanted() and not cfg.fsdp_offload and cfg.extra.get("fsdp_static", True))
             self.fsdp = FullyShardedDP(self.model, self.device, mode="param" if ngd_opt else "flat",
-                                       offload=cfg.fsdp_offload,
+                                       offload=cfg.fsdp_offload, static=static,
+                                       reshard_after_forward=cfg.fsdp_schedule == "full_shard",
                                        param_dtype={"fp32": None, "bf16": torch.bfloat16}[cfg.fsdp_param_dtype])
             self.flat = self.fsdp.space
         else:
@@ -238,17 +246,23 @@ class TransformerTrainer:
     # flat gradient buffer (static; the optimizer zeroes it).  Under DDP the capture is cut
     # where a gradient bucket completes (parallel/graphs.SegmentedStep) and the replay
     # launches each bucket's all-reduce between segments (also under the sharded NGD
-    # optimizer, whose gradient all-reduce is the same bucket reducer).  bf16 only; not with FSDP (collectives inside forward).
-    def _graphs_on(self):
+    # optimizer, whose gradient all-reduce is the same bucket reducer).  Under static FSDP the
+    # forward is cut at every unit too (gather wait + prefetch between segments).  bf16 only.
+    def _graphs_wanted(self):
         # (the --no-native ablation is plain eager PyTorch by default: graphs are one of the
         # "tricks".  ``extra["graphs_torch_ops"]`` captures the torch-op step too -- graph-safe
         # since its embedding backward is a static-shape index_add (ops/embedding._GatherRows;
         # ATen's dense embedding backward sized its unique/partition buffers at capture time
         # and faulted on replay), with parallel.graphs.capture_guard refusing any such op)
         from ..ops import _native
-        native_ok = _native.enabled() or bool(self.cfg.extra.get("graphs_torch_ops"))
-        return (TR_GRAPHS and self.device.type == "cuda" and self.fsdp is None and native_ok
-                and not self.scaler.enabled and self.cfg.profile_steps <= 0 and not self.cfg.faithful
+        cfg = self.cfg
+        native_ok = _native.enabled() or bool(cfg.extra.get("graphs_torch_ops"))
+        return (TR_GRAPHS and self.device.type == "cuda" and native_ok and cfg.precision != "fp16"
+                and cfg.profile_steps <= 0 and not cfg.faithful)
+
+    def _graphs_on(self):
+        # under FSDP only the static (fixed-address) mode can be captured
+        return (self._graphs_wanted() and (self.fsdp is None or self.fsdp.static) and not self.scaler.enabled
                 and self.model.training)
 
     def _fwd_bwd(self, tokens, labels, types, masks):
@@ -307,11 +321,13 @@ class TransformerTrainer:
             AN.DEVICE_SEED = st["seed"]
             self.model.mix_override = (st["perm"], st["lam"])
             try:
-                if self.reducer is not None or self.zero is not None:
-                    # segments cut at bucket boundaries; all-reduces launched between them
+                if self.reducer is not None or self.zero is not None or self.fsdp is not None:
+                    # bucket all-reduces / FSDP reduce-scatters gated on event nodes of the
+                    # backward graph (or launched between segments), FSDP gathers between the
+                    # forward's segments
                     step = SegmentedStep(self.device, self._graph_pool, stream=self._graph_stream)
                     loss, logits = step.capture(fwd)
-                    st.update(replay=step.replay, segments=step.num_segments)
+                    st.update(replay=step.replay, segments=step.num_segments, step=step)
                 else:
                     g = torch.cuda.CUDAGraph()
                     with torch.cuda.graph(g, pool=self._graph_pool), _graph_guard():

@@ -20,6 +20,7 @@ def main():
     ap.add_argument("--world", type=int, default=1,
                     help="simulate the ZeRO-2 sharded NGD of this many ranks: time each rank's shard optimizer")
     ap.add_argument("--balance", default="ngd", choices=["ngd", "numel"])
+    ap.add_argument("--graphs", action="store_true", help="steady-state steps replayed as HIP graphs (NGD.graphs)")
     a = ap.parse_args()
     from faster_distributed_training_amd.optim.ngd import NGD
     from faster_distributed_training_amd.utils.flat import FlatParams
@@ -37,14 +38,17 @@ def main():
         per = []
         for r, (lo_s, hi_s) in enumerate(full.runs):
             v = ShardView(full, r * full.chunk, (r + 1) * full.chunk, full.slots[lo_s:hi_s])
-            per.append((r, time_steps(NGD(v, lr=0.01, momentum=0.9, weight_decay=1e-4), v, a.steps, dev)))
+            o = NGD(v, lr=0.01, momentum=0.9, weight_decay=1e-4)
+            o.graphs = a.graphs
+            per.append((r, time_steps(o, v, a.steps, dev)))
         for r, t in per:
             print(f"{a.model}: world {a.world} rank {r}: " + ", ".join(f"{k} median {v:.2f} ms" for k, v in t.items()))
         worst = {k: max(t[k] for _, t in per) for k in per[0][1]}
-        print(f"{a.model}: world {a.world} ({a.balance}-balanced) slowest rank: " + ", ".join(f"{k} {v:.2f} ms" for k, v in worst.items()))
+        print(f"{a.model}: world {a.world} ({a.balance}-balanced{', graphs' if a.graphs else ''}) slowest rank: " + ", ".join(f"{k} {v:.2f} ms" for k, v in worst.items()))
         return
     f = FlatParams(m, device=dev)
     o = NGD(f, lr=0.01, momentum=0.9, weight_decay=1e-4)
+    o.graphs = a.graphs
     g = torch.Generator(device=dev).manual_seed(0)
     times = {True: [], False: []}
     for s in range(a.steps):

@@ -70,8 +70,10 @@ def test_ddp_engine_two_ranks_one_gpu(cuda):
     run_world(_worker, world=2, native=True, timeout=400)
 
 
-def _graph_worker(rank, world):
+def _graph_worker(rank, world, mode="event"):
     import torch.distributed as dist
+    from faster_distributed_training_amd.parallel import graphs
+    graphs.DETACHED_MODE = mode
     from faster_distributed_training_amd.models import resnet as R
     from faster_distributed_training_amd.parallel.ddp import BucketReducer
     from faster_distributed_training_amd.utils.flat import FlatParams
@@ -97,11 +99,17 @@ def _graph_worker(rank, world):
         dist.all_gather(alls, chk)
         assert all(torch.equal(alls[0], t) for t in alls), it
     st = list(m._plan._graphs.values())[0]
-    assert st.stage == "ready" and len(st.segments) > 2  # backward cut at bucket boundaries
+    assert st.stage == "ready"
+    assert sum(len(a) for _, a in st.segments) == len(red.buckets)  # every bucket launched from the replay
+    if mode == "cut":
+        assert len(st.segments) > 2  # backward cut at bucket boundaries
+    else:
+        assert len(st.segments) == 1 and st.rec.event_points == len(red.buckets)  # one graph, event nodes
 
 
-def test_ddp_engine_hip_graphs_two_ranks(cuda):
-    run_world(_graph_worker, world=2, native=True, timeout=400)
+@pytest.mark.parametrize("mode", ["event", "cut"])
+def test_ddp_engine_hip_graphs_two_ranks(cuda, mode):
+    run_world(_graph_worker, world=2, native=True, timeout=400, args=(mode,))
 
 
 def _fsdp_engine_worker(rank, world, offload=False):
@@ -320,11 +328,14 @@ def test_rccl_world1_code_paths(cuda):
     run_world(_rccl_worker, world=1, native=True, backend="nccl", timeout=400)
 
 
-def _segmented_worker(rank, world):
+def _segmented_worker(rank, world, mode="event"):
     """An autograd backward captured as HIP-graph segments cut at DDP bucket boundaries
-    (parallel/graphs.SegmentedStep): replays give the eager reducer's averaged gradient."""
+    (parallel/graphs.SegmentedStep; or one graph with event-record nodes there): replays give
+    the eager reducer's averaged gradient."""
     import torch.distributed as dist
     import torch.nn as nn
+    from faster_distributed_training_amd.parallel import graphs
+    graphs.DETACHED_MODE = mode
     from faster_distributed_training_amd.parallel.ddp import BucketReducer
     from faster_distributed_training_amd.parallel.graphs import SegmentedStep
     from faster_distributed_training_amd.utils.flat import FlatParams
@@ -355,7 +366,9 @@ def _segmented_worker(rank, world):
     flat.grad.zero_()
     step.capture(body)
     red.finish()  # (the capture launched nothing; reset the bucket state)
-    assert step.num_segments == len(red.buckets) + 2, (step.num_segments, len(red.buckets))  # fwd + cuts + tail
+    cuts = step.num_segments - 2 + step.rec.event_points
+    assert cuts == len(red.buckets), (step.num_segments, step.rec.event_points, len(red.buckets))  # fwd + cuts + tail
+    assert (step.rec.event_points == 0) == (mode == "cut")
     for x, y, w in zip(xs, ys, want):
         sx.copy_(x)
         sy.copy_(y)
@@ -367,8 +380,9 @@ def _segmented_worker(rank, world):
         assert err < 1e-6, err
 
 
-def test_segmented_graph_ddp_matches_eager(cuda):
-    run_world(_segmented_worker, world=2, native=True, timeout=300)
+@pytest.mark.parametrize("mode", ["event", "cut"])
+def test_segmented_graph_ddp_matches_eager(cuda, mode):
+    run_world(_segmented_worker, world=2, native=True, timeout=300, args=(mode,))
 
 
 def _transformer_ddp_graph_worker(rank, world):
@@ -389,11 +403,51 @@ def _transformer_ddp_graph_worker(rank, world):
         dist.all_gather(alls, chk)
         assert all(torch.equal(alls[0], t) for t in alls)  # replicas stay in sync
     ent = [e for e in tr._graphs.values() if isinstance(e, dict)][0]
-    assert ent["segments"] > 2
+    assert ent["segments"] - 2 + ent["step"].rec.event_points == len(tr.reducer.buckets)  # one launch per bucket
 
 
 def test_transformer_ddp_hip_graphs_two_ranks(cuda):
     run_world(_transformer_ddp_graph_worker, world=2, native=True, timeout=400)
+
+
+def _transformer_fsdp_graph_worker(rank, world, schedule):
+    """The transformer under static FSDP captured as HIP graphs: the forward is
+    cut at every wrap unit (gather wait + prefetch between segments), the reduce-scatters are
+    event-gated actions of the backward graph (plus, FULL_SHARD, the re-gathers before each
+    unit's backward); 6 steps equal the eager FSDP run (dropout off, lambda 0)."""
+    import torch.nn as nn
+    import faster_distributed_training_amd.train.transformer_trainer as T
+    torch.cuda.set_device(0)
+
+    def run(graphs):
+        T.TR_GRAPHS = graphs
+        torch.manual_seed(0)
+        cfg = T.TransformerConfig(batch_size=16, synthetic=True, eval=False, plot=False, distributed=True, fsdp=True,
+                                  fsdp_schedule=schedule, optimizer="mirror_madgrad", epoch=1, length_buckets=(128,),
+                                  n_layers=2, extra={"subset_stride": 50})
+        tr = T.TransformerTrainer(cfg)
+        for mod in tr.model.modules():
+            if isinstance(mod, nn.Dropout):
+                mod.p = 0.0
+        tr.model.alpha = 0.0
+        it = iter(tr.train_loader)
+        losses = [float(tr.train_step(*next(it))) for _ in range(6)]
+        torch.cuda.synchronize()
+        return losses, tr.space.data.clone(), tr
+
+    le, pe, te = run(False)
+    assert not te.fsdp.static and not te._graphs_on()
+    lg, pg, tg = run(True)
+    assert tg.fsdp.static and tg._graphs_on() and tg.fsdp.ring == (schedule == "full_shard")
+    ent = [e for e in tg._graphs.values() if isinstance(e, dict)][0]
+    assert len(ent["step"].fwd.segments) >= len(tg.fsdp.order)  # forward cut at every unit
+    assert max(abs(a - b) / max(abs(a), 1e-6) for a, b in zip(le, lg)) < 1e-3, (le, lg)
+    assert ((pe - pg).norm() / pe.norm()).item() < 1e-4
+
+
+@pytest.mark.parametrize("schedule", ["full_shard", "shard_grad_op"])
+def test_transformer_fsdp_hip_graphs_two_ranks(cuda, schedule):
+    run_world(_transformer_fsdp_graph_worker, world=2, native=True, timeout=500, args=(schedule,))
 
 
 def _zero_graph_worker(rank, world):
