@@ -144,6 +144,9 @@ void ngd_small_proj(uint64_t X, uint64_t Y, uint64_t W, int G, int A, int D, int
                     uint64_t HH, uint64_t part, uint64_t stream);
 long ngd_small_part_numel(int G, int A, int D, int B, int R);
 void ngd_rescale(uint64_t X, uint64_t Y, long per, int G, uint64_t ip, uint64_t fp, uint64_t stream);
+long ngd_gram_slab_numel(int G, int R, int D, bool with_l);
+void ngd_gram(uint64_t J, uint64_t W, uint64_t K, uint64_t L, uint64_t slab, int G, int R, int D, uint64_t stream);
+void ngd_wupdate(uint64_t A, uint64_t J, uint64_t wc, uint64_t W, int G, int R, int D, uint64_t stream);
 void ngd_pre_eigh(uint64_t K, uint64_t L, uint64_t d, uint64_t rho, uint64_t Z, uint64_t ise, uint64_t drho, uint64_t zs,
                   uint64_t dsum, int G, int R, float alpha, float eta, float N, float D, uint64_t stream);
 void ngd_post_eigh(uint64_t c, uint64_t U, uint64_t ise, uint64_t drho, uint64_t zs, uint64_t dsum, uint64_t trXX,

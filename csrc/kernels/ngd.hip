@@ -933,4 +933,187 @@ void ngd_post_eigh(uint64_t c, uint64_t U, uint64_t ise, uint64_t drho, uint64_t
   FDT_LAUNCH_CHECK();
 }
 
+// ---------------------------------------------------------------- rank x rank products
+// The R x R products of an update step (reference ngd_optimizer.py:215-218 / :319), which the
+// library GEMMs ran as [G,R,D] x [G,D,R] batched launches with 80x256 macro tiles (mostly
+// padding at R <= 80):
+//   ngd_gram : K = J J^T (upper tiles only, mirrored) and, in the same launch, L = J W^T --
+//              32 x 32 output tiles, each over a contiguous d range (split so that the grid
+//              fills the chip), partial tiles to a slab summed in split order (no atomics:
+//              an NGD step stays bitwise repeatable)
+//   ngd_wupdate: W <- A (J + wc W) in place, one workgroup per (g, 64-column block): A and
+//              the block of J + wc W in LDS, 20 outputs per thread
+constexpr int kGT = 32;
+
+__global__ __launch_bounds__(256) void ngd_gram_partial_kernel(const float* __restrict__ J, const float* __restrict__ W,
+                                                               float* __restrict__ slab, int R, int D, int nt,
+                                                               int tiles_per_g, int S, int dlen) {
+  __shared__ float a[kGT][kGT + 1], b[kGT][kGT + 1];
+  const int s = blockIdx.x % S;
+  const int t = (blockIdx.x / S) % tiles_per_g;
+  const int g = blockIdx.x / (S * tiles_per_g);
+  // tile t: first the upper-triangle tiles of K (ti <= tj), then the nt x nt tiles of L
+  const int nsym = nt * (nt + 1) / 2;
+  int ti, tj;
+  const float* Bsrc;
+  if (t < nsym) {
+    int r = t, i = 0;
+    while (r >= nt - i) { r -= nt - i; ++i; }
+    ti = i; tj = i + r;
+    Bsrc = J;
+  } else {
+    ti = (t - nsym) / nt; tj = (t - nsym) % nt;
+    Bsrc = W;
+  }
+  const long base = (long)g * R * D;
+  const int i0 = ti * kGT, j0 = tj * kGT;
+  const int d0 = s * dlen, d1 = min(D, d0 + dlen);
+  const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
+  float acc[2][2] = {{0.f, 0.f}, {0.f, 0.f}};
+  for (int dc = d0; dc < d1; dc += kGT) {
+    for (int e = threadIdx.x; e < kGT * kGT; e += 256) {
+      const int r = e / kGT, c = e % kGT, d = dc + c;
+      a[r][c] = (i0 + r < R && d < d1) ? J[base + (long)(i0 + r) * D + d] : 0.f;
+      b[r][c] = (j0 + r < R && d < d1) ? Bsrc[base + (long)(j0 + r) * D + d] : 0.f;
+    }
+    __syncthreads();
+#pragma unroll 8
+    for (int c = 0; c < kGT; ++c) {
+      const float a0 = a[ty * 2][c], a1 = a[ty * 2 + 1][c], b0 = b[tx * 2][c], b1 = b[tx * 2 + 1][c];
+      acc[0][0] = fmaf(a0, b0, acc[0][0]);
+      acc[0][1] = fmaf(a0, b1, acc[0][1]);
+      acc[1][0] = fmaf(a1, b0, acc[1][0]);
+      acc[1][1] = fmaf(a1, b1, acc[1][1]);
+    }
+    __syncthreads();
+  }
+  float* o = slab + ((long)(g * tiles_per_g + t) * S + s) * (kGT * kGT);
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) o[(ty * 2 + i) * kGT + tx * 2 + j] = acc[i][j];
+}
+
+__global__ __launch_bounds__(256) void ngd_gram_sum_kernel(const float* __restrict__ slab, float* __restrict__ K,
+                                                           float* __restrict__ L, int R, int nt, int tiles_per_g,
+                                                           int S, long total) {
+  const long e = (long)blockIdx.x * 256 + threadIdx.x;
+  if (e >= total) return;
+  const int w = (int)(e % (kGT * kGT));
+  const long gt = e / (kGT * kGT);
+  const int t = (int)(gt % tiles_per_g), g = (int)(gt / tiles_per_g);
+  const int nsym = nt * (nt + 1) / 2;
+  int ti, tj;
+  bool sym = t < nsym;
+  if (sym) {
+    int r = t, i = 0;
+    while (r >= nt - i) { r -= nt - i; ++i; }
+    ti = i; tj = i + r;
+  } else {
+    ti = (t - nsym) / nt; tj = (t - nsym) % nt;
+  }
+  const int i = ti * kGT + w / kGT, j = tj * kGT + w % kGT;
+  if (i >= R || j >= R) return;
+  const float* src = slab + gt * S * (kGT * kGT) + w;
+  float v = 0.f;
+  for (int s = 0; s < S; ++s) v += src[(long)s * (kGT * kGT)];  // split order: deterministic
+  if (sym) {
+    if (ti == tj && j < i) return;  // diagonal tile: the lower half comes from the mirror below
+    K[((long)g * R + i) * R + j] = v;
+    K[((long)g * R + j) * R + i] = v;
+  } else {
+    L[((long)g * R + i) * R + j] = v;
+  }
+}
+
+static void gram_split(int G, int tiles_per_g, int D, int& S, int& dlen) {
+  // ~1024 workgroups in all, each reducing >= 256 of d (and a multiple of the 32-wide chunk)
+  const long wgs = (long)G * tiles_per_g;
+  long s = (1024 + wgs - 1) / wgs;
+  long smax = (D + 255) / 256;
+  if (s > smax) s = smax;
+  if (s < 1) s = 1;
+  dlen = (int)(((D + s - 1) / s + kGT - 1) / kGT * kGT);
+  S = (D + dlen - 1) / dlen;
+}
+
+long ngd_gram_slab_numel(int G, int R, int D, bool with_l) {
+  const int nt = (R + kGT - 1) / kGT;
+  const int tpg = nt * (nt + 1) / 2 + (with_l ? nt * nt : 0);
+  int S, dlen;
+  gram_split(G, tpg, D, S, dlen);
+  return (long)G * tpg * S * kGT * kGT;
+}
+
+void ngd_gram(uint64_t J, uint64_t W, uint64_t K, uint64_t L, uint64_t slab, int G, int R, int D, uint64_t stream) {
+  FDT_CHECK(R >= 1 && R <= kNgdMaxR && D >= 1, "ngd_gram: shape");
+  if (G == 0) return;
+  const bool with_l = L != 0;
+  FDT_CHECK(!with_l || W != 0, "ngd_gram: L needs W");
+  const int nt = (R + kGT - 1) / kGT;
+  const int tpg = nt * (nt + 1) / 2 + (with_l ? nt * nt : 0);
+  int S, dlen;
+  gram_split(G, tpg, D, S, dlen);
+  hipStream_t st = as_stream(stream);
+  ngd_gram_partial_kernel<<<G * tpg * S, 256, 0, st>>>(P<const float>(J), P<const float>(W), P<float>(slab), R, D, nt,
+                                                       tpg, S, dlen);
+  FDT_LAUNCH_CHECK();
+  const long total = (long)G * tpg * kGT * kGT;
+  ngd_gram_sum_kernel<<<(int)((total + 255) / 256), 256, 0, st>>>(P<const float>(slab), P<float>(K), P<float>(L), R,
+                                                                  nt, tpg, S, total);
+  FDT_LAUNCH_CHECK();
+}
+
+constexpr int kWuCols = 64;
+
+__global__ __launch_bounds__(256) void ngd_wupdate_kernel(const float* __restrict__ A, const float* __restrict__ J,
+                                                          const float* __restrict__ wc, float* __restrict__ W, int R,
+                                                          int D, int nblk) {
+  extern __shared__ float lds[];
+  float* As = lds;                        // [R][R + 1]
+  float* Bs = lds + R * (R + 1);          // [R][kWuCols + 1]
+  const int g = blockIdx.x / nblk, blk = blockIdx.x % nblk;
+  const int c0 = blk * kWuCols;
+  const float* Ag = A + (long)g * R * R;
+  for (int e = threadIdx.x; e < R * R; e += 256) As[(e / R) * (R + 1) + e % R] = Ag[e];
+  const long base = (long)g * R * D;
+  for (int e = threadIdx.x; e < R * kWuCols; e += 256) {
+    const int r = e / kWuCols, c = e % kWuCols, d = c0 + c;
+    float v = 0.f;
+    if (d < D) v = fmaf(wc[(long)g * R + r], W[base + (long)r * D + d], J[base + (long)r * D + d]);
+    Bs[r * (kWuCols + 1) + c] = v;
+  }
+  __syncthreads();  // (every W value of this block is in LDS before any is overwritten)
+  const int c = threadIdx.x % kWuCols, r0 = threadIdx.x / kWuCols;  // a wave shares r0: A reads broadcast
+  const int d = c0 + c;
+  float acc[(kNgdMaxR + 3) / 4];
+#pragma unroll
+  for (int q = 0; q < (kNgdMaxR + 3) / 4; ++q) acc[q] = 0.f;
+  for (int k = 0; k < R; ++k) {
+    const float bk = Bs[k * (kWuCols + 1) + c];
+#pragma unroll
+    for (int q = 0; q < (kNgdMaxR + 3) / 4; ++q) {
+      const int r = r0 + 4 * q;
+      if (r < R) acc[q] = fmaf(As[r * (R + 1) + k], bk, acc[q]);
+    }
+  }
+  if (d < D) {
+#pragma unroll
+    for (int q = 0; q < (kNgdMaxR + 3) / 4; ++q) {
+      const int r = r0 + 4 * q;
+      if (r < R) W[base + (long)r * D + d] = acc[q];
+    }
+  }
+}
+
+void ngd_wupdate(uint64_t A, uint64_t J, uint64_t wc, uint64_t W, int G, int R, int D, uint64_t stream) {
+  FDT_CHECK(R >= 1 && R <= kNgdMaxR && D >= 1, "ngd_wupdate: shape");
+  if (G == 0) return;
+  const int nblk = (D + kWuCols - 1) / kWuCols;
+  const size_t lds = ((size_t)R * (R + 1) + (size_t)R * (kWuCols + 1)) * sizeof(float);
+  ngd_wupdate_kernel<<<G * nblk, 256, lds, as_stream(stream)>>>(P<const float>(A), P<const float>(J), P<const float>(wc),
+                                                              P<float>(W), R, D, nblk);
+  FDT_LAUNCH_CHECK();
+}
+
 }  // namespace fdt

@@ -43,6 +43,9 @@ MATERIALIZE_3X3 = os.environ.get("FDT_MATERIALIZE_3X3", "1") != "0"
 # run a block's ReLU join inside the next block's first 1x1 conv (PRO_JOIN prologue) instead
 # of a standalone pass (see ResNetBodyFn.forward)
 JOIN_FOLD = os.environ.get("FDT_JOIN_FOLD", "1") != "0"
+# widest next-block 1x1 (output channels) that still takes the join fold: up to 128 with the
+# 128-row tiles, 256 with the 256-row tiles (one output-channel tile either way)
+JOIN_FOLD_MAX = int(os.environ.get("FDT_JOIN_FOLD_MAX", "64"))
 # run the classifier head (average pool + fc, bf16 autocast numerics) as two engine kernels
 # inside the body's graphs instead of eager PyTorch ops (see csrc/kernels/head.hip)
 FUSED_HEAD = os.environ.get("FDT_FUSED_HEAD", "1") != "0"
@@ -292,7 +295,9 @@ def conv_bn_fwd_join(pj, u: Unit, training, dev):
     y, s, t, r, s2, t2, out, mask = pj
     M = y.numel() // y.shape[-1]
     st, fin = _fin_args(u, M, training, dev)
-    yo, _ = ci.conv_fwd_join(y, r, s, t, s2, t2, u.wf, u.shp, out, mask, part=slots(2, u.shp.cout, dev, M), fin=fin)
+    tile = (256, 128, 32) if u.shp.cout > 128 else None  # one output-channel tile
+    yo, _ = ci.conv_fwd_join(y, r, s, t, s2, t2, u.wf, u.shp, out, mask, part=slots(2, u.shp.cout, dev, M), fin=fin,
+                             tile=tile)
     return yo, st, M
 
 
@@ -304,7 +309,7 @@ def _join_foldable(b_next) -> bool:
     arithmetic (measured 1.5-2x slower than conv + join pass at stages 2-4)."""
     u = b_next.units[0]
     return (JOIN_FOLD and u.shp.k == 1 and u.shp.stride == 1 and u.shp.pad == 0 and u.shp.cin == u.shp.cxp
-            and u.shp.cin >= 8 and u.shp.cout <= 64)
+            and u.shp.cin >= 8 and u.shp.cout <= min(JOIN_FOLD_MAX, 256))
 
 
 def _fin_args(u: Unit, M, training, dev):

@@ -63,6 +63,42 @@ DEFER = os.environ.get("FDT_NGD_DEFER", "1") != "0"
 # (ResNet-50 NGD+meta 30.4 vs 30.2-30.7 ms, transformer bs256 11.5 vs 11.4-12.2 ms) and slower
 # at batch 32 (5.39 vs 5.04 ms): the step is GPU-bound, not launch-bound.  FDT_NGD_GRAPHS=1
 GRAPHS = os.environ.get("FDT_NGD_GRAPHS", "0") == "1"
+# the R x R products of an update step (K = J J^T, L = J W^T, W <- A (J + wc W)) on the
+# hand-written ngd.hip kernels (ngd_gram / ngd_wupdate) instead of batched library GEMMs
+SMALL_GEMM = os.environ.get("FDT_NGD_GEMM", "1") != "0"
+
+
+def _gemm_native(J) -> bool:
+    return SMALL_GEMM and J.is_cuda and _native.enabled() and hasattr(_native.native(), "ngd_gram")
+
+
+def gram(J, W=None):
+    """(K = J J^T, L = J W^T or None) for J, W [G, R, D] fp32 -- ngd_gram (split-d partial tiles
+    summed in a fixed order) or two batched GEMMs."""
+    if not _gemm_native(J):
+        K = torch.bmm(J, J.transpose(1, 2))
+        return K, (torch.bmm(J, W.transpose(1, 2)) if W is not None else None)
+    nat = _native.native()
+    G, R, D = J.shape
+    Jc = J.contiguous()
+    Wc = W.contiguous() if W is not None else None
+    K = torch.empty(G, R, R, device=J.device, dtype=torch.float32)
+    L = torch.empty(G, R, R, device=J.device, dtype=torch.float32) if W is not None else None
+    slab = torch.empty(nat.ngd_gram_slab_numel(G, R, D, W is not None), device=J.device, dtype=torch.float32)
+    nat.ngd_gram(Jc.data_ptr(), Wc.data_ptr() if Wc is not None else 0, K.data_ptr(),
+                 L.data_ptr() if L is not None else 0, slab.data_ptr(), G, R, D, _native.stream_ptr())
+    return K, L
+
+
+def w_update(A, J, wc, W):
+    """W <- A (J + wc W) in place (W, J [G, R, D]; A [G, R, R]; wc [G, R])."""
+    if not (_gemm_native(J) and W.is_contiguous()):
+        torch.bmm(A, torch.addcmul(J, wc.unsqueeze(2), W), out=W)
+        return
+    G, R, D = W.shape
+    Ac, Jc, wcc = A.contiguous(), J.contiguous(), wc.contiguous()
+    _native.native().ngd_wupdate(Ac.data_ptr(), Jc.data_ptr(), wcc.data_ptr(), W.data_ptr(), G, R, D,
+                                 _native.stream_ptr())
 
 
 def _fused_small_math(X, R) -> bool:
@@ -319,8 +355,7 @@ class NGState:
                           zs.data_ptr(), dsum.data_ptr(), tr.data_ptr(), self.d.data_ptr(), self.rho.data_ptr(),
                           A.data_ptr(), wc.data_ptr(), G, R, self.alpha, self.eta, float(N), float(D),
                           _native.stream_ptr())
-        B = torch.addcmul(J, wc.unsqueeze(2), self.W)             # J + wc W
-        torch.bmm(A, B, out=self.W)                               # W <- A B (in place)
+        w_update(A, J, wc, self.W)                                # W <- A (J + wc W), in place
 
     # ------------------------------------------------- tiny-dim axes (HIP, no transposes)
     def small_ok(self, G: torch.Tensor) -> bool:
@@ -364,8 +399,8 @@ class NGState:
                            _native.stream_ptr())
         self.last_ip = ip
         if updating:
-            L = torch.bmm(J, self.W.transpose(1, 2)) if N > D else HH
-            K = torch.bmm(J, J.transpose(1, 2))
+            K, L = gram(J, self.W if N > D else None)
+            L = HH if L is None else L
             yield from self._fused_update(J, K, L, ip, N)
         nat.ngd_rescale(G.data_ptr(), Y.data_ptr(), G.numel() // P, P, ip.data_ptr(), fp.data_ptr(),
                         _native.stream_ptr())
@@ -421,8 +456,8 @@ class NGState:
                      J.data_ptr() if updating else 0, HH.data_ptr() if need_hh else 0, sp)
         self.last_ip = ip
         if updating:
-            L = HH if need_hh else torch.bmm(J, self.W.transpose(1, 2))
-            K = torch.bmm(J, J.transpose(1, 2))
+            K, L = gram(J, None if need_hh else self.W)
+            L = HH if need_hh else L
             yield from self._fused_update(J, K, L, ip, N)
         nat.ngd_rescale(G.data_ptr(), Y.data_ptr(), G.numel() // P, P, ip.data_ptr(), fp.data_ptr(), sp)
         return Y

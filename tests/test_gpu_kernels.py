@@ -705,3 +705,29 @@ def test_ngd_step_bitwise_repeatable(cuda):
 
     assert torch.equal(run(), run())
 
+
+
+# ---------------------------------------------------------------- NGD R x R products
+@pytest.mark.parametrize("G,R,D", [(3, 1, 9), (2, 17, 27), (4, 32, 64), (3, 80, 513), (2, 80, 4608), (1, 128, 300)])
+def test_ngd_gram_and_wupdate_match_fp64(cuda, G, R, D):
+    """ngd_gram (K = J J^T, L = J W^T: split-d partial tiles summed in a fixed order) and
+    ngd_wupdate (W <- A (J + wc W) in place) against fp64 products; repeated calls are
+    bitwise identical."""
+    from faster_distributed_training_amd.optim.ngd import gram, w_update
+    g = torch.Generator(device=cuda).manual_seed(G * 1000 + R * 10 + D)
+    J = torch.randn(G, R, D, device=cuda, generator=g)
+    W = torch.randn(G, R, D, device=cuda, generator=g)
+    K, L = gram(J, W)
+    Jd, Wd = J.double(), W.double()
+    assert rel(K, Jd @ Jd.transpose(1, 2)) < 1e-6 and rel(L, Jd @ Wd.transpose(1, 2)) < 1e-6
+    assert torch.equal(K, K.transpose(1, 2))  # symmetric by construction
+    K2, L2 = gram(J, W)
+    assert torch.equal(K, K2) and torch.equal(L, L2)
+    K3, L3 = gram(J)
+    assert L3 is None and torch.equal(K3, K)
+    A = torch.randn(G, R, R, device=cuda, generator=g)
+    wc = torch.rand(G, R, device=cuda, generator=g)
+    want = A.double() @ (Jd + wc.double().unsqueeze(2) * Wd)
+    Wn = W.clone()
+    w_update(A, J, wc, Wn)
+    assert rel(Wn, want) < 1e-6
