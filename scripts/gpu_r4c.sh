@@ -1,0 +1,33 @@
+#!/usr/bin/env bash
+# Round 4, A/B call: join fold width at bs1024 / bs128, NGD graph replay for the transformer
+# and the ResNet NGD+meta path, sharded NGD at world 1.
+set -o pipefail
+cd "$(dirname "$0")/.."
+export TMPDIR=/tmp
+OUT=gpurun_out/${1:-r4c}
+mkdir -p "$OUT"
+run() {
+  local name=$1; shift
+  timeout -k 10 300 python bench.py "$@" > "$OUT/$name.log" 2>&1 || { echo "$name failed"; tail -5 "$OUT/$name.log"; exit 1; }
+  grep -h '"value"' "$OUT/$name.log" > "$OUT/$name.json"
+  echo "$name $(grep -o '"ms_per_step": [0-9.]*' "$OUT/$name.json") $(grep -o '"host_ms_per_step": [0-9.]*' "$OUT/$name.json")"
+}
+run bs1024_fold64 --steps 30 --warmup 5
+FDT_JOIN_FOLD_MAX=128 run bs1024_fold128 --steps 30 --warmup 5
+FDT_JOIN_FOLD_MAX=256 run bs1024_fold256 --steps 30 --warmup 5
+run bs1024_fold64b --steps 30 --warmup 5
+FDT_JOIN_FOLD_MAX=128 run bs128_fold128 --steps 40 --warmup 5 --global-batch 128
+FDT_JOIN_FOLD_MAX=256 run bs128_fold256 --steps 40 --warmup 5 --global-batch 128
+run bs128_fold64 --steps 40 --warmup 5 --global-batch 128
+run tr_b32 --model transformer --global-batch 32 --steps 40 --warmup 12
+FDT_NGD_GRAPHS=1 run tr_b32_ngdg --model transformer --global-batch 32 --steps 40 --warmup 12
+FDT_NGD_GRAPHS=1 run tr_b256_ngdg --model transformer --steps 20 --warmup 12
+run ngd_meta --ngd --meta_learning --steps 20 --warmup 12
+FDT_NGD_GRAPHS=1 run ngd_meta_ngdg --ngd --meta_learning --steps 20 --warmup 12
+FDT_NGD_GEMM=0 run ngd_meta_libgemm --ngd --meta_learning --steps 20 --warmup 12
+run ngd_meta_sharded --ngd --meta_learning --sharded-ngd --steps 20 --warmup 12
+
+mkdir -p "$OUT/pmc"
+timeout -k 10 300 python scripts/roofline_layers.py --batch 1024 --md "$OUT/pmc/r4_bs1024_roofline.md" > "$OUT/roof1024.log" 2>&1 && tail -1 "$OUT/roof1024.log"
+timeout -k 10 300 python scripts/roofline_layers.py --batch 128 --md "$OUT/pmc/r4_bs128_roofline.md" > "$OUT/roof128.log" 2>&1 && tail -1 "$OUT/roof128.log"
+echo done

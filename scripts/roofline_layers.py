@@ -1,0 +1,109 @@
+#!/usr/bin/env python3
+"""Per-layer roofline of the ResNet-50 (CIFAR) convolutions at the tuned launch configs the
+engine uses (ops/conv_tuned.json): measured device time of every (shape, op) against its
+ALGORITHMIC minimum -- each operand read once, each result written once, FLOPs at the dense
+bf16 MFMA peak -- rather than against the bytes the kernel happened to fetch.
+
+    python scripts/roofline_layers.py --batch 1024 --md profiles/pmc/r4_bs1024_roofline.md
+
+Calls mirror the engine's: forward with the lazy-BN prologue (x*s+t, ReLU) and the statistics
+epilogue; dgrad with the BN-backward fold prologue (g + alpha + beta*y) and a plain store;
+wgrad with the fold on g and the lazy-BN transform on x.  Minimum bytes per op:
+  fwd   x + W + y            dgrad  g + y + W + dx          wgrad  g + y + x + dW (fp32)
+Bound = max(bytes / BW, FLOPs / PEAK) with BW = 6.3 TB/s (the streaming rate measured on this
+part, profiles/pmc/calibration.md) and PEAK = 2.5 PFLOP/s dense bf16.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import torch
+
+from bench_conv import SHAPES, timeit
+from faster_distributed_training_amd.ops import conv_igemm as ci
+
+BW = 6.3e12
+PEAK = 2.5e15
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--batch", type=int, default=1024)
+    ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--md", default=None)
+    ap.add_argument("--json", default=None)
+    a = ap.parse_args()
+    dev = torch.device("cuda")
+    N = a.batch
+    rows = []
+    for (H, Cin, Cout, k, s, p, cnt) in SHAPES:
+        shp = ci.ConvShape(Cin, Cout, k, s, p)
+        torch.manual_seed(0)
+        x = torch.randn(N, H, H, shp.cxp, device=dev).to(torch.bfloat16)
+        w = torch.randn(Cout, Cin, k, k, device=dev) / (Cin * k * k) ** 0.5
+        wf, wd = ci.alloc_packed(shp, dev, dgrad=Cin >= 8)
+        ci.pack_weights([(w, wf, wd, shp)])
+        Ho, Wo = ci.out_hw(H, H, shp)
+        g = torch.randn(N, Ho, Wo, Cout, device=dev).to(torch.bfloat16)
+        yy = torch.randn(N, Ho, Wo, Cout, device=dev).to(torch.bfloat16)
+        al = torch.zeros(Cout, device=dev)
+        be = torch.zeros(Cout, device=dev)
+        sv = torch.ones(shp.cxp, device=dev)
+        tv = torch.zeros(shp.cxp, device=dev)
+        gw = torch.empty(Cout, Cin, k, k, device=dev)
+        M = N * Ho * Wo
+        xb, yb = N * H * H * Cin * 2, M * Cout * 2
+        wb = Cout * Cin * k * k * 2
+        flops = 2.0 * M * Cout * Cin * k * k
+        ops = {"fwd": (lambda: ci.conv_fwd(x, wf, shp, sv, tv, 1, 1.0), xb + wb + yb)}
+        if Cin >= 8:
+            ops["dgrad"] = (lambda: ci.conv_dgrad(g, yy, al, be, wd, shp, (N, H, H, Cin)), 2 * yb + wb + xb)
+        slab = torch.empty(64 * Cout * shp.ntaps * shp.cxp, device=dev)
+        ops["wgrad"] = (lambda: ci.conv_wgrad(g, yy, al, be, x, shp, gw, sv, tv, 1, slab=slab), 2 * yb + xb + 2 * wb)
+        for op, (fn, nbytes) in ops.items():
+            t = timeit(fn, a.reps) * 1e3  # us
+            bound = max(nbytes / BW, flops / PEAK) * 1e6
+            rows.append(dict(shape=f"{H}x{H} {Cin}->{Cout} k{k} s{s}", count=cnt, op=op, us=t, min_mb=nbytes / 1e6,
+                             gflop=flops / 1e9, bound_us=bound, pct=100.0 * bound / t,
+                             limiter="bytes" if nbytes / BW > flops / PEAK else "mfma"))
+            r = rows[-1]
+            print(f"{r['shape']:26s} x{cnt} {op:5s} {t:8.1f} us  min {r['min_mb']:8.1f} MB {r['gflop']:7.2f} GF  "
+                  f"bound {bound:7.1f} us ({r['limiter']})  {r['pct']:5.1f} %", flush=True)
+    tot = sum(r["us"] * r["count"] for r in rows)
+    totb = sum(r["bound_us"] * r["count"] for r in rows)
+    byop = {}
+    for r in rows:
+        o = byop.setdefault(r["op"], [0.0, 0.0])
+        o[0] += r["us"] * r["count"]
+        o[1] += r["bound_us"] * r["count"]
+    print(f"network convolutions: {tot / 1e3:.3f} ms measured vs {totb / 1e3:.3f} ms algorithmic bound "
+          f"({100 * totb / tot:.1f} %); " + ", ".join(f"{k} {v[0] / 1e3:.3f} / {v[1] / 1e3:.3f} ms" for k, v in byop.items()))
+    if a.json:
+        with open(a.json, "w") as f:
+            json.dump(dict(batch=N, rows=rows), f, indent=1)
+    if a.md:
+        with open(a.md, "w") as f:
+            f.write(f"# Per-layer convolution roofline, batch {N} (scripts/roofline_layers.py)\n\n")
+            f.write("Measured: device time of the tuned launch (HIP events, random data, the engine's prologue / "
+                    "epilogue variants).  Algorithmic minimum bytes: every operand read once, every result written "
+                    f"once (bf16 activations / packed weights, fp32 dW).  Bound = max(bytes / {BW / 1e12:.1f} TB/s, "
+                    f"FLOPs / {PEAK / 1e15:.1f} PFLOP/s).\n\n")
+            f.write("| layer | count | op | measured us | min MB | GFLOP | bound us | limiter | % of bound |\n")
+            f.write("|---|---:|---|---:|---:|---:|---:|---|---:|\n")
+            for r in rows:
+                f.write(f"| {r['shape']} | {r['count']} | {r['op']} | {r['us']:.1f} | {r['min_mb']:.1f} | "
+                        f"{r['gflop']:.2f} | {r['bound_us']:.1f} | {r['limiter']} | {r['pct']:.1f} |\n")
+            f.write(f"\nNetwork convolutions (weighted by layer count): **{tot / 1e3:.3f} ms measured vs "
+                    f"{totb / 1e3:.3f} ms algorithmic bound ({100 * totb / tot:.1f} %)**; by op: " +
+                    ", ".join(f"{k} {v[0] / 1e3:.3f} / {v[1] / 1e3:.3f} ms ({100 * v[1] / v[0]:.0f} %)"
+                              for k, v in byop.items()) + ".\n")
+
+
+if __name__ == "__main__":
+    main()
