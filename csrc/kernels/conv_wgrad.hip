@@ -78,8 +78,12 @@ constexpr uint32_t kWOOB = 0xFFFFFFF0u;
 
 // ADDR: 0 = 1x1 stride-1 (input pixel == output pixel), 1 = power-of-two Ho/Wo (shifts),
 //       2 = general (integer division).  ACT: input transform act(x*s+t) (XAFF only).
-template <int BM, int BN, int BK, bool FOLD, bool XAFF, int ADDR, int ACT>
+// NS: register-staged K tiles in flight (the prefetch distance).  2 for the big tiles; the
+// small tiles of the small-batch layers (a 64 x 64 tile has 2 MFMAs per wave per 32-pixel K
+// tile: latency-bound per iteration, ~1 us each at batch 128) keep 4 in flight.
+template <int BM, int BN, int BK, bool FOLD, bool XAFF, int ADDR, int ACT, int NS = 2>
 __global__ __launch_bounds__(256) void wgrad_kernel(const WgArgs a) {
+  static_assert(NS >= 2 && NS % 2 == 0, "even number of register stages (static LDS buffer parity)");
   constexpr int GC = BM / 8, XC = BN / 8;      // 16-B chunks per LDS row
   constexpr int GR = 256 / GC, XR = 256 / XC;  // rows per load round
   constexpr int NG = BK / GR, NX = BK / XR;    // chunks per thread per tile
@@ -280,30 +284,30 @@ __global__ __launch_bounds__(256) void wgrad_kernel(const WgArgs a) {
   };
 
   const int nkt = p_end > p_begin ? (p_end - p_begin + BK - 1) / BK : 0;
-  Stage SA, SB;
+  // register stage i holds K tile t with t % NS == i; the stage stored at iteration k (tile
+  // k + 1) is reloaded at once with tile k + 1 + NS
+  Stage S[NS];
   if (nkt > 0) {
-    load_tile(SA, p_begin);
-    __builtin_amdgcn_sched_barrier(0);  // issue order SA, SB, SA' pinned (exact vmcnt counting)
-    load_tile(SB, p_begin + BK);
-    __builtin_amdgcn_sched_barrier(0);
-    store_tile(SA, 0);
-    load_tile(SA, p_begin + 2 * BK);
+#pragma unroll
+    for (int i = 0; i < NS; ++i) {
+      load_tile(S[i], p_begin + i * BK);
+      __builtin_amdgcn_sched_barrier(0);  // issue order pinned (exact vmcnt counting)
+    }
+    store_tile(S[0], 0);
+    load_tile(S[0], p_begin + NS * BK);
     __builtin_amdgcn_sched_barrier(0);
     __syncthreads();
   }
-  for (int kt = 0; kt < nkt; kt += 2) {
-    compute(0);
-    if (kt + 1 >= nkt) break;
-    store_tile(SB, 1);
-    __syncthreads();
-    load_tile(SB, p_begin + (kt + 3) * BK);
-    __builtin_amdgcn_sched_barrier(0);  // keep the prefetch issued ahead of the MFMAs
-    compute(1);
-    if (kt + 2 >= nkt) break;
-    store_tile(SA, 0);
-    __syncthreads();
-    load_tile(SA, p_begin + (kt + 4) * BK);
-    __builtin_amdgcn_sched_barrier(0);
+  for (int kt = 0; kt < nkt; kt += NS) {
+#pragma unroll
+    for (int u = 0; u < NS; ++u) {
+      compute(u & 1);
+      if (kt + u + 1 >= nkt) break;
+      store_tile(S[(u + 1) % NS], (u + 1) & 1);
+      __syncthreads();
+      load_tile(S[(u + 1) % NS], p_begin + (kt + u + 1 + NS) * BK);
+      __builtin_amdgcn_sched_barrier(0);  // keep the prefetch issued ahead of the MFMAs
+    }
   }
 
   // epilogue: C[co][k]: lane column k = lane&31, rows co = (r&3) + 8(r>>2) + 4h
@@ -527,7 +531,7 @@ void conv_wgrad(uint64_t g, uint64_t y, uint64_t al, uint64_t be, uint64_t gs, u
                 uint64_t slab,
                 long Nb, int Hi, int Wi, int Cx, int Ho, int Wo, int S, const std::vector<int>& dh,
                 const std::vector<int>& dw, int Cout, int ldw, int act, float act_alpha, int BM, int BN, int BK,
-                int nsplit, int direct, uint64_t stream) {
+                int nsplit, int direct, int stages, uint64_t stream) {
   using namespace wg;
   WgArgs a{};
   a.g = P<const bf16>(g); a.y = P<const bf16>(y);
@@ -567,9 +571,14 @@ void conv_wgrad(uint64_t g, uint64_t y, uint64_t al, uint64_t be, uint64_t gs, u
   dim3 grid(a.nbm * a.nbn, nsplit);
   hipStream_t st = as_stream(stream);
   const int wact = xaff ? act : 0;
+  // 4 register stages only where they are instantiated (the small tiles); 2 elsewhere
+  const bool deep = stages >= 4 && BM * BN <= 64 * 128 && BK == 32;
 #define FDT_WG(BM_, BN_, BK_, F_, X_, A_, ACT_)                                                           \
   if (BM == BM_ && BN == BN_ && BK == BK_ && fold == F_ && xaff == X_ && addr == A_ && wact == ACT_) {  \
-    auto k = wgrad_kernel<BM_, BN_, BK_, F_, X_, A_, ACT_>;                                             \
+    auto k = wgrad_kernel<BM_, BN_, BK_, F_, X_, A_, ACT_, 2>;                                          \
+    if constexpr (BM_ * BN_ <= 64 * 128 && BK_ == 32) {                                                 \
+      if (deep) k = wgrad_kernel<BM_, BN_, BK_, F_, X_, A_, ACT_, 4>;                                   \
+    }                                                                                                   \
     static size_t set = 64 * 1024;                                                                      \
     if (lds > set) {                                                                                    \
       FDT_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(k),                               \

@@ -168,6 +168,11 @@ def _tile3(tile, M, N):
     return tuple(tile[:3])
 
 
+# register-staged K tiles in flight in the weight-gradient kernel (csrc/kernels/conv_wgrad.hip):
+# 4 is instantiated for the small BK = 32 tiles of the small-batch layers; a tuned entry's
+# "stages" overrides this default
+WG_STAGES = int(os.environ.get("FDT_WG_STAGES", "2"))
+
 # K groups (csrc/kernels/conv_igemm_impl.h): 8-wave workgroups whose two 4-wave halves take
 # alternate K tiles -- for the small-M layers whose ~256-workgroup grids leave one wave per SIMD
 KGROUPS = os.environ.get("FDT_KGROUPS", "1") != "0"
@@ -430,9 +435,10 @@ def conv_wgrad(g, y, al, be, x, shp: ConvShape, out, xs=None, xt=None, act=0, al
         xs = torch.ones(Cx, device=x.device, dtype=torch.float32)
         xt = torch.zeros(Cx, device=x.device, dtype=torch.float32)
     assert gs is None or al is not None, "gs needs the fold (al/be)"
+    stages = int(ent.get("stages", WG_STAGES)) if ent else WG_STAGES
     nat.conv_wgrad(g.data_ptr(), _p(y), _p(al), _p(be), _p(gs), x.data_ptr(), _p(xs), _p(xt), slab.data_ptr(),
                    N, H, W, Cx, Hy, Wy, shp.stride, list(dh), list(dw), shp.cout, ldw, int(act), float(alpha),
-                   bm, bn, bk, ns, int(direct), _sp())
+                   bm, bn, bk, ns, int(direct), stages, _sp())
     if not direct:
         nat.wgrad_reduce(slab.data_ptr(), out.data_ptr(), ns, shp.cout, shp.cin, shp.ntaps, shp.cxp,
                          int(accumulate), _sp())
