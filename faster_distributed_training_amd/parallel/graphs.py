@@ -35,7 +35,7 @@ _ACTIVE = None
 #            graph (no graph-boundary bubbles on the compute queue).
 #   "cut":   the capture is cut there and the action runs between the two replayed segments
 #            (round-3 scheme: ~25-50 us of compute-queue idle per cut, profiles/r3s3/).
-DETACHED_MODE = os.environ.get("FDT_GRAPH_COMM", "event")
+DETACHED_MODE = os.environ.get("FDT_GRAPH_COMM", "cut")  # "event" once verified on the GPU (probe + tests)
 
 
 def active():

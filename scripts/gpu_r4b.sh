@@ -19,7 +19,7 @@ run() {
   echo "$name $(grep -o '"ms_per_step": [0-9.]*' "$OUT/$name.json") $(grep -o '"host_ms_per_step": [0-9.]*' "$OUT/$name.json") $(grep -o '"bwd_graph_segments": [0-9]*' "$OUT/$name.json")"
 }
 run bs128 --steps 40 --warmup 5 --global-batch 128
-run bs128_ddp_event --steps 40 --warmup 5 --global-batch 128 --ddp
+FDT_GRAPH_COMM=event run bs128_ddp_event --steps 40 --warmup 5 --global-batch 128 --ddp
 FDT_GRAPH_COMM=cut run bs128_ddp_cut --steps 40 --warmup 5 --global-batch 128 --ddp
 run fsdp_full --fsdp --steps 10 --warmup 3
 run fsdp_sgo --fsdp --fsdp-schedule shard_grad_op --steps 10 --warmup 3
