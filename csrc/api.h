@@ -107,7 +107,8 @@ void conv_wgrad(uint64_t g, uint64_t y, uint64_t al, uint64_t be, uint64_t gs, u
                 uint64_t slab,
                 long Nb, int Hi, int Wi, int Cx, int Ho, int Wo, int S, const std::vector<int>& dh,
                 const std::vector<int>& dw, int Cout, int ldw, int act, float act_alpha, int BM, int BN, int BK,
-                int nsplit, int direct, int stages, uint64_t stream);
+                int nsplit, int direct, int stages, uint64_t out, uint64_t cnt, int Cin, int accumulate,
+                uint64_t stream);
 void wgrad_reduce(uint64_t slab, uint64_t out, int nsplit, int Cout, int Cin, int ntaps, int Cxp, int accumulate,
                   uint64_t stream);
 void pack_weights(const std::vector<uint64_t>& src, const std::vector<uint64_t>& wf, const std::vector<uint64_t>& wd,

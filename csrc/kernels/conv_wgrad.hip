@@ -40,6 +40,7 @@ struct WgArgs {
   const float* xs;   // s [Cx] (nullptr: identity input transform)
   const float* xt;   // t [Cx]
   float* slab;       // [nsplit][Cout][ldw]; direct: the fp32 OIHW gradient itself
+  float* slab_out;   // fused_reduce: the fp32 OIHW gradient
   int direct;        // 1x1, Cx == Cin: every split atomically adds into the gradient (no reduce)
   long M;            // Nb*Ho*Wo
   int Hi, Wi, Cx, log2Cx, Ho, Wo, S, log2Ho, log2Wo;
@@ -49,7 +50,22 @@ struct WgArgs {
   long px_per_split;  // multiple of BK
   int8_t dh[12], dw[12];
   long g_bytes, x_bytes;  // buffer-descriptor ranges
+  // split-K combined in-kernel (few splits, slab-reduced layers): the partial tiles go to the
+  // slab in register order with write-through stores, the last of a tile's splits to arrive
+  // (ticket in cnt[tile]) sums them and writes the OIHW gradient -- no wgrad_reduce launch
+  int* cnt;          // tickets [tiles], zero between launches (reset by each last arriver)
+  int fused_reduce, accumulate, det, Cin;
 };
+
+__device__ __forceinline__ void wst16_sc1(__amdgpu_buffer_rsrc_t r, uint32_t byte_off, float4 v) {
+  typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+  u32x4 u = {__float_as_uint(v.x), __float_as_uint(v.y), __float_as_uint(v.z), __float_as_uint(v.w)};
+  __builtin_amdgcn_raw_buffer_store_b128(u, r, byte_off, 0, 16);
+}
+__device__ __forceinline__ float4 wld16_sc1(__amdgpu_buffer_rsrc_t r, uint32_t byte_off) {
+  auto v = __builtin_amdgcn_raw_buffer_load_b128(r, byte_off, 0, 16);
+  return make_float4(__uint_as_float(v[0]), __uint_as_float(v[1]), __uint_as_float(v[2]), __uint_as_float(v[3]));
+}
 
 __device__ __forceinline__ int xcd_remap(int bid, int nblk) {
   const int q = nblk >> 3, r = nblk & 7, xcd = bid & 7;
@@ -314,6 +330,78 @@ __global__ __launch_bounds__(256) void wgrad_kernel(const WgArgs a) {
   // direct (1x1 with Cx == Cin: slab row layout == OIHW): fp32 atomics accumulate every
   // split straight into the gradient (each wave instruction = two 128-B row segments);
   // otherwise a plain store into this split's slab for wgrad_reduce.
+  if (a.fused_reduce) {
+    // ---- split-K combine (same protocol as the conv kernels' split-K, conv_igemm_impl.h)
+    constexpr int NR4 = TM * TN * 4;
+    __shared__ int last_flag;
+    const int tile = bm * a.nbn + bn, split = blockIdx.y;
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(reinterpret_cast<float4*>(a.slab) + (long)tile * a.nsplit * NR4 * 256), (short)0,
+        (int)(a.nsplit * NR4 * 256 * 16), 0x00020000);
+    {
+      const uint32_t mine = (uint32_t)((split * NR4 * 256 + tid) * 16);
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+          for (int q = 0; q < 4; ++q)
+            wst16_sc1(rs, mine + (uint32_t)(((i * TN + j) * 4 + q) * 256 * 16),
+                      make_float4(acc[i][j][4 * q], acc[i][j][4 * q + 1], acc[i][j][4 * q + 2], acc[i][j][4 * q + 3]));
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every writing wave drains its write-through stores
+    __syncthreads();
+    if (tid == 0) {
+      const int t = __hip_atomic_fetch_add(&a.cnt[tile], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const int last = t == a.nsplit - 1;
+      if (last) __hip_atomic_store(&a.cnt[tile], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      last_flag = last;
+    }
+    __syncthreads();
+    if (!last_flag) return;
+    if (a.det) {  // fixed summation order whichever split arrived last
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+    }
+    for (int sp = 0; sp < a.nsplit; ++sp) {
+      if (sp == split && !a.det) continue;
+      const uint32_t other = (uint32_t)((sp * NR4 * 256 + tid) * 16);
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const float4 v = wld16_sc1(rs, other + (uint32_t)(((i * TN + j) * 4 + q) * 256 * 16));
+            acc[i][j][4 * q] += v.x;
+            acc[i][j][4 * q + 1] += v.y;
+            acc[i][j][4 * q + 2] += v.z;
+            acc[i][j][4 * q + 3] += v.w;
+          }
+    }
+    // OIHW: slab column kk = tap * Cx + ci -> ((co * Cin + ci) * ntaps + tap)
+    float* out = a.slab_out;
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int kk = k0 + wn * (BN / 2) + j * 32 + (lane & 31);
+        const int t = kk >> a.log2Cx, ci = kk & (a.Cx - 1);
+        if (kk < a.ldw && t < a.ntaps && ci < a.Cin) {
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int co = co0 + wm * (BM / 2) + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+            float* o = out + ((long)co * a.Cin + ci) * a.ntaps + t;
+            *o = a.accumulate ? *o + acc[i][j][r] : acc[i][j][r];
+          }
+        }
+      }
+    return;
+  }
   const bool direct = a.direct != 0;
   float* dst = direct ? a.slab : a.slab + (long)blockIdx.y * a.Cout * a.ldw;
 #pragma unroll
@@ -531,9 +619,18 @@ void conv_wgrad(uint64_t g, uint64_t y, uint64_t al, uint64_t be, uint64_t gs, u
                 uint64_t slab,
                 long Nb, int Hi, int Wi, int Cx, int Ho, int Wo, int S, const std::vector<int>& dh,
                 const std::vector<int>& dw, int Cout, int ldw, int act, float act_alpha, int BM, int BN, int BK,
-                int nsplit, int direct, int stages, uint64_t stream) {
+                int nsplit, int direct, int stages, uint64_t out, uint64_t cnt, int Cin, int accumulate,
+                uint64_t stream) {
   using namespace wg;
   WgArgs a{};
+  // out != 0: combine the splits in-kernel (last arriver) into the OIHW gradient `out`
+  a.fused_reduce = out != 0 && nsplit > 1 && !direct;
+  a.slab_out = P<float>(out);
+  a.cnt = P<int>(cnt);
+  a.Cin = Cin;
+  a.accumulate = accumulate;
+  a.det = deterministic() ? 1 : 0;
+  FDT_CHECK(!a.fused_reduce || cnt != 0, "fused wgrad reduce needs a ticket buffer");
   a.g = P<const bf16>(g); a.y = P<const bf16>(y);
   a.al = P<const float>(al); a.be = P<const float>(be);
   a.gs = P<const float>(gs);

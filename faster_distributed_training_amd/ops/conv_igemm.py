@@ -172,6 +172,10 @@ def _tile3(tile, M, N):
 # 4 is instantiated for the small BK = 32 tiles of the small-batch layers; a tuned entry's
 # "stages" overrides this default
 WG_STAGES = int(os.environ.get("FDT_WG_STAGES", "2"))
+# few-split slab-reduced weight gradients (3x3, padded stem) combine their splits in-kernel
+# (last arriver per tile) instead of a separate wgrad_reduce launch
+WG_FUSED_REDUCE = os.environ.get("FDT_WG_FUSED_REDUCE", "0") == "1"
+WG_FUSED_MAX_SPLITS = 8
 
 # K groups (csrc/kernels/conv_igemm_impl.h): 8-wave workgroups whose two 4-wave halves take
 # alternate K tiles -- for the small-M layers whose ~256-workgroup grids leave one wave per SIMD
@@ -428,6 +432,12 @@ def conv_wgrad(g, y, al, be, x, shp: ConvShape, out, xs=None, xt=None, act=0, al
         if not accumulate:
             out.zero_()
         slab = out
+    fused = (WG_FUSED_REDUCE and not direct and 1 < ns <= WG_FUSED_MAX_SPLITS and out.is_contiguous())
+    if fused:
+        # splits combined in-kernel by the last arriver of each tile (no wgrad_reduce launch):
+        # partial tiles in register order in the persistent split-K workspace
+        tiles = (shp.cout // bm) * (-(-ldw // bn))
+        slab, cnt = splitk_workspace(g.device, tiles * ns * bm * bn, tiles)
     elif slab is None or slab.numel() < ns * shp.cout * ldw:
         slab = torch.empty(ns * shp.cout * ldw, device=g.device, dtype=torch.float32)
     dh, dw, _ = taps_fwd(shp.k, shp.pad)
@@ -438,8 +448,9 @@ def conv_wgrad(g, y, al, be, x, shp: ConvShape, out, xs=None, xt=None, act=0, al
     stages = int(ent.get("stages", WG_STAGES)) if ent else WG_STAGES
     nat.conv_wgrad(g.data_ptr(), _p(y), _p(al), _p(be), _p(gs), x.data_ptr(), _p(xs), _p(xt), slab.data_ptr(),
                    N, H, W, Cx, Hy, Wy, shp.stride, list(dh), list(dw), shp.cout, ldw, int(act), float(alpha),
-                   bm, bn, bk, ns, int(direct), stages, _sp())
-    if not direct:
+                   bm, bn, bk, ns, int(direct), stages, out.data_ptr() if fused else 0,
+                   cnt.data_ptr() if fused else 0, shp.cin, int(accumulate), _sp())
+    if not direct and not fused:
         nat.wgrad_reduce(slab.data_ptr(), out.data_ptr(), ns, shp.cout, shp.cin, shp.ntaps, shp.cxp,
                          int(accumulate), _sp())
     return out

@@ -192,7 +192,13 @@ WGRAD_CASES = [
 
 @pytest.mark.parametrize("case", WGRAD_CASES)
 @pytest.mark.parametrize("mode", ["plain", "affine"])
-def test_conv_wgrad(cuda, case, mode):
+@pytest.mark.parametrize("variant", ["default", "fused_reduce_stages4"])
+def test_conv_wgrad(cuda, case, mode, variant, monkeypatch):
+    """variant fused_reduce_stages4: the splits combined in-kernel by each tile's last arriver
+    (no wgrad_reduce launch) and 4 register-staged K tiles in flight."""
+    if variant != "default":
+        monkeypatch.setattr(ci, "WG_FUSED_REDUCE", True)
+        monkeypatch.setattr(ci, "WG_STAGES", 4)
     N, H, Cin, Cout, k, stride, pad = case
     torch.manual_seed(2)
     shp = ci.ConvShape(Cin, Cout, k, stride, pad)
