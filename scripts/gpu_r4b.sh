@@ -8,7 +8,7 @@ export TMPDIR=/tmp
 OUT=gpurun_out/${1:-r4b}
 mkdir -p "$OUT"
 timeout -k 10 900 python -u -m pytest tests/test_distributed_gpu.py tests/test_resnet_engine.py tests/test_transformer_graphs.py \
-  tests/test_gpu_kernels.py::test_ngd_gram_and_wupdate_match_fp64 tests/test_ngd_graphs.py -m gpu -v -p no:cacheprovider --timeout 300 --timeout-method thread > "$OUT/pytest.log" 2>&1; rc=$?
+  tests/test_gpu_kernels.py::test_ngd_gram_and_wupdate_match_fp64 tests/test_ngd_graphs.py tests/test_conv_kernels.py::test_conv_wgrad -m gpu -v -p no:cacheprovider --timeout 300 --timeout-method thread > "$OUT/pytest.log" 2>&1; rc=$?
 echo "pytest rc=$rc"; tail -3 "$OUT/pytest.log"
 case $rc in 0|1) ;; *) echo "pytest aborted rc=$rc"; exit 1;; esac
 grep -E "^(FAILED|ERROR)" "$OUT/pytest.log" | head -20

@@ -21,6 +21,9 @@ FDT_JOIN_FOLD_MAX=256 run bs128_fold256 --steps 40 --warmup 5 --global-batch 128
 run bs128_fold64 --steps 40 --warmup 5 --global-batch 128
 FDT_WG_STAGES=4 run bs128_wg4 --steps 40 --warmup 5 --global-batch 128
 FDT_WG_STAGES=4 run bs1024_wg4 --steps 30 --warmup 5
+FDT_WG_FUSED_REDUCE=1 run bs128_wgfr --steps 40 --warmup 5 --global-batch 128
+FDT_WG_FUSED_REDUCE=1 FDT_WG_STAGES=4 run bs128_wgfr4 --steps 40 --warmup 5 --global-batch 128
+FDT_WG_FUSED_REDUCE=1 run bs1024_wgfr --steps 30 --warmup 5
 run tr_b32 --model transformer --global-batch 32 --steps 40 --warmup 12
 FDT_NGD_GRAPHS=1 run tr_b32_ngdg --model transformer --global-batch 32 --steps 40 --warmup 12
 FDT_NGD_GRAPHS=1 run tr_b256_ngdg --model transformer --steps 20 --warmup 12
