@@ -216,7 +216,7 @@ def _sharding_fields(tr, rec):
         if states and states[0].segments:
             from faster_distributed_training_amd.parallel import graphs
             cfg["bwd_graph_segments"] = len(states[0].segments)
-            cfg["bwd_comm_event_points"] = int(getattr(states[0].rec, "event_points", 0))
+            cfg["bwd_captured_collectives"] = int(getattr(states[0].rec, "captured", 0))
             cfg["graph_comm"] = graphs.DETACHED_MODE
     if tr.fsdp is not None:
         cfg["fsdp_units"] = len(tr.fsdp.units)

@@ -108,6 +108,7 @@ class BucketReducer:
         if comm_dtype is not None and comm_dtype != flat.grad.dtype:
             self.wire = torch.empty(flat.numel, device=flat.grad.device, dtype=comm_dtype)
         self.cast = [False] * len(self.buckets)
+        self.in_graph = set()  # buckets whose all-reduce was captured into a backward graph
         from ..ops.resnet_fused import register_grad_ready_hook
         # autograd-managed params fire the post-accumulate hook; params whose gradient the
         # fused ResNet engine writes directly fire the engine's grad-ready hook
@@ -128,7 +129,9 @@ class BucketReducer:
         b = self.bucket_of[id(p)]
         self.pending[b] -= 1
         if self.pending[b] == 0:
-            act = graphs.detached(lambda: self._launch(b))  # nothing in the graph waits for it
+            # nothing in the graph reads the averaged bucket: under capture (RCCL) the
+            # all-reduce can become a node on a side branch of the backward graph
+            act = graphs.detached(lambda: self._launch(b), capturable=self.use_avg)
             if defer:
                 return act
             rec = graphs.active()
@@ -139,25 +142,45 @@ class BucketReducer:
         return None
 
     def _launch(self, b):
+        """Launch bucket b's all-reduce.  Inside a HIP-graph capture (graphs.Recorder in
+        "capture" mode) the collective is recorded into the graph on a side branch: returns
+        the joiner the recorder calls where the branch rejoins (wait + bf16 wire copy-back,
+        both captured); every replay then runs it, and ``finish`` leaves the bucket alone."""
         if self.works[b] is not None:
-            return
+            return None
         s, e, _ = self.buckets[b]
         view = self.flat.grad[s:e]
         if self.wire is not None:
             buf = self.wire[s:e]
             buf.copy_(view)
-            self.cast[b] = True
         else:
             buf = view
         op = dist.ReduceOp.AVG if self.use_avg else dist.ReduceOp.SUM
-        self.works[b] = dist.all_reduce(buf, op=op, group=self.pg, async_op=True)
+        work = dist.all_reduce(buf, op=op, group=self.pg, async_op=True)
+        if torch.cuda.is_available() and torch.cuda.is_current_stream_capturing():
+            self.in_graph.add(b)
+
+            def join(w=work, s=s, e=e):
+                w.wait()
+                if self.wire is not None:
+                    self.flat.grad[s:e].copy_(self.wire[s:e])
+            return join
+        self.works[b] = work
+        self.cast[b] = self.wire is not None
+        return None
 
     def finish(self):
-        """Complete the gradient all-reduce (call once after backward)."""
+        """Complete the gradient all-reduce (call once after backward).  Buckets whose
+        all-reduce is part of the replayed backward graph are complete when the graph is; in
+        a step where every hook fired inside a replay (no eager launch at all) they are
+        skipped, any other bucket not launched yet (unused parameters) is launched now."""
+        eager = any(w is not None for w in self.works)
         for b in range(len(self.buckets)):
-            if self.works[b] is None:
+            if self.works[b] is None and (eager or b not in self.in_graph):
                 self._launch(b)
         for b, w in enumerate(self.works):
+            if w is None:
+                continue
             w.wait()
             s, e, _ = self.buckets[b]
             if self.cast[b]:

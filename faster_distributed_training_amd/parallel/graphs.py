@@ -26,25 +26,33 @@ from torch.utils._python_dispatch import TorchDispatchMode
 # grad_ready from the autograd thread); None outside a capture.
 _ACTIVE = None
 
-# How DETACHED actions are placed -- collectives that nothing later in the graph waits for
-# (DDP / ZeRO bucket all-reduces, FSDP SHARD_GRAD_OP reduce-scatters; the compute stream meets
-# them only after the step's backward):
-#   "event": the capture is NOT cut.  An external event-record node marks the point in the
-#            graph, and the replay issues the action on a side stream that waits for that node,
-#            so the collective starts when the graph reaches it while the backward stays one
-#            graph (no graph-boundary bubbles on the compute queue).
+# How DETACHED actions are placed -- collectives that nothing later in the graph reads
+# (DDP / ZeRO bucket all-reduces; the compute stream meets them only after the step's backward):
+#   "capture": the capture is NOT cut.  The action runs INSIDE the capture, from a side stream
+#            forked off the capture stream at that point, so the collective (RCCL) becomes a
+#            node on a side branch of the backward graph; the branch is joined into the capture
+#            stream only where the segment ends.  HIP graph replays run forked branches
+#            concurrently (measured: two 1 ms branches replay in 1.03 ms,
+#            profiles/r4/graph_comm_probe.txt), so the all-reduce overlaps the rest of backward
+#            while the backward stays ONE graph -- no graph-boundary bubbles on the compute queue.
+#            Needs a capturable backend (nccl = RCCL); with gloo the action falls back to a cut.
 #   "cut":   the capture is cut there and the action runs between the two replayed segments
 #            (round-3 scheme: ~25-50 us of compute-queue idle per cut, profiles/r3s3/).
-DETACHED_MODE = os.environ.get("FDT_GRAPH_COMM", "cut")  # "event" once verified on the GPU (probe + tests)
+# (An external event-record node, the CUDA idiom for "start this stream mid-graph", is refused
+# by torch on ROCm: "External events are disallowed in rocm".)
+DETACHED_MODE = os.environ.get("FDT_GRAPH_COMM", "cut")
 
 
 def active():
     return _ACTIVE
 
 
-def detached(fn):
-    """Mark ``fn`` (a deferred GPU action) as one nothing in the captured graph depends on."""
+def detached(fn, capturable=False):
+    """Mark ``fn`` (a deferred GPU action) as one nothing in the captured graph reads.
+    ``capturable``: ``fn`` may run inside the capture (a RCCL collective) and returns a
+    joiner -- a callable that orders its completion into the current stream."""
     fn.detached = True
+    fn.capturable = bool(capturable)
     return fn
 
 
@@ -52,27 +60,13 @@ _COMM_SIDE = {}
 
 
 def _comm_side_stream(device):
-    """High-priority side stream the event-gated actions are issued from (its own hardware
-    queue: a wait on it never sits in the compute queue)."""
+    """Side stream the captured detached actions are issued from (high priority: in eager
+    use it never shares the compute stream's hardware queue)."""
     idx = torch.device(device).index if torch.device(device).index is not None else torch.cuda.current_device()
     st = _COMM_SIDE.get(idx)
     if st is None:
         st = _COMM_SIDE[idx] = torch.cuda.Stream(device=idx, priority=-1)
     return st
-
-
-class _OnEvent:
-    """A detached action gated on an event-record node of the replayed graph."""
-
-    detached = True
-
-    def __init__(self, event, fn, side):
-        self.event, self.fn, self.side = event, fn, side
-
-    def __call__(self):
-        with torch.cuda.stream(self.side):
-            self.side.wait_event(self.event)
-            self.fn()
 
 
 class Recorder:
@@ -90,8 +84,8 @@ class Recorder:
         self.cur = None
         self.stream = None
         self.foreign_cuts = 0  # cuts requested from a stream other than the capture stream
-        self.pending = []      # event-gated detached actions of the open segment
-        self.event_points = 0  # detached actions placed on event-record nodes (no cut)
+        self.joiners = []      # captured detached actions of the open segment, joined at its end
+        self.captured = 0      # detached actions captured on a side branch (no cut)
 
     def begin(self):
         if self.stream is None:
@@ -108,27 +102,33 @@ class Recorder:
 
     def cut(self, actions):
         self._join()
-        if DETACHED_MODE == "event" and actions and all(getattr(a, "detached", False) for a in actions):
-            # no cut: an external event-record node here, the actions gated on it at replay
-            ev = torch.cuda.Event(external=True)
-            with torch.cuda.stream(self.stream):
-                ev.record(self.stream)
+        if (DETACHED_MODE == "capture" and actions
+                and all(getattr(a, "detached", False) and getattr(a, "capturable", False) for a in actions)):
+            # no cut: fork a side branch here and run the collectives inside the capture
             side = _comm_side_stream(self.stream.device)
-            self.pending += [_OnEvent(ev, a, side) for a in actions]
-            self.event_points += 1
+            side.wait_stream(self.stream)
+            with torch.cuda.stream(side):
+                for a in actions:
+                    j = a()
+                    if j is not None:
+                        self.joiners.append(j)
+            self.joiners.append(lambda s=side: torch.cuda.current_stream().wait_stream(s))
+            self.captured += len(actions)
             return
-        with torch.cuda.stream(self.stream):
-            self.cur.capture_end()
-        self.segments.append((self.cur, self.pending + list(actions)))
-        self.pending = []
+        self._end_segment(actions)
         self.begin()
+
+    def _end_segment(self, actions):
+        with torch.cuda.stream(self.stream):
+            for j in self.joiners:  # every side branch forked in this segment rejoins before its end
+                j()
+            self.joiners = []
+            self.cur.capture_end()
+        self.segments.append((self.cur, list(actions)))
 
     def end(self):
         self._join()
-        with torch.cuda.stream(self.stream):
-            self.cur.capture_end()
-        self.segments.append((self.cur, self.pending))
-        self.pending = []
+        self._end_segment([])
         self.cur = None
 
     def replay(self):

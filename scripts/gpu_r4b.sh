@@ -1,7 +1,7 @@
 #!/usr/bin/env bash
-# Round 4, second call: the new GPU tests (event-gated DDP graphs, FSDP full-shard ring under
+# Round 4, second call: the new GPU tests (DDP collectives captured in the backward graph, FSDP full-shard ring under
 # graphs, transformer under static FSDP, batch-128 shipped tile table, fp16 CE), convergence
-# parity, DDP event-vs-cut at batch 128, FSDP schedules, transformer FSDP, NGD shard graphs.
+# parity, DDP capture-vs-cut at batch 128, FSDP schedules, transformer FSDP, NGD shard graphs.
 set -o pipefail
 cd "$(dirname "$0")/.."
 export TMPDIR=/tmp
@@ -19,7 +19,8 @@ run() {
   echo "$name $(grep -o '"ms_per_step": [0-9.]*' "$OUT/$name.json") $(grep -o '"host_ms_per_step": [0-9.]*' "$OUT/$name.json") $(grep -o '"bwd_graph_segments": [0-9]*' "$OUT/$name.json")"
 }
 run bs128 --steps 40 --warmup 5 --global-batch 128
-FDT_GRAPH_COMM=event run bs128_ddp_event --steps 40 --warmup 5 --global-batch 128 --ddp
+FDT_GRAPH_COMM=capture run bs128_ddp_capture --steps 40 --warmup 5 --global-batch 128 --ddp
+FDT_GRAPH_COMM=capture run bs1024_ddp_capture --steps 20 --warmup 5 --ddp
 FDT_GRAPH_COMM=cut run bs128_ddp_cut --steps 40 --warmup 5 --global-batch 128 --ddp
 run fsdp_full --fsdp --steps 10 --warmup 3
 run fsdp_sgo --fsdp --fsdp-schedule shard_grad_op --steps 10 --warmup 3

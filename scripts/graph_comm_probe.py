@@ -59,6 +59,13 @@ def probe_branches(cyc):
 
 
 def probe_external_event(cyc):
+    try:
+        ev = torch.cuda.Event(external=True)
+        ev.record()
+    except RuntimeError as e:  # torch on ROCm refuses external events
+        print(f"[2] external event record nodes: unavailable ({e})", flush=True)
+        _probe_in_graph_fork(cyc)
+        return
     ev = torch.cuda.Event(external=True)
     g = torch.cuda.CUDAGraph()
     with torch.cuda.graph(g):
@@ -85,6 +92,10 @@ def probe_external_event(cyc):
     verdict = "MID-GRAPH (fires at the node)" if 0.7 < t_o < 1.6 else ("AT GRAPH END" if t_o > 2.5 else "NO WAIT")
     print(f"[2] external event: other stream released after {t_o:.3f} ms, graph done {t_m:.3f} ms -> {verdict}",
           flush=True)
+    _probe_in_graph_fork(cyc)
+
+
+def _probe_in_graph_fork(cyc):
     # A wait captured in the SAME graph on a forked stream (no host involvement)
     g2 = torch.cuda.CUDAGraph()
     side = torch.cuda.Stream()
@@ -123,8 +134,8 @@ def probe_costs():
                 evs[i // (n // k_events)].record()
 
     res = {}
-    for k in (0, 10):
-        evs = [torch.cuda.Event(external=True) for _ in range(max(k, 1))]
+    for k in (0,):
+        evs = []
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g):
             body(k, evs)
@@ -163,8 +174,7 @@ def probe_costs():
             g.replay()
     host = (time.perf_counter() - t0) / 20 * 1e6
     torch.cuda.synchronize()
-    print(f"[3] 200 tiny kernels: one graph {res[0]:.1f} us, + 10 external event records {res[10]:.1f} us "
-          f"({(res[10] - res[0]) / 10:.2f} us each), as 11 graphs {t_split:.1f} us "
+    print(f"[3] 200 tiny kernels: one graph {res[0]:.1f} us, as 11 graphs {t_split:.1f} us "
           f"({(t_split - res[0]) / 10:.2f} us per boundary; host {host:.1f} us)", flush=True)
 
 
@@ -200,6 +210,35 @@ def probe_rccl_capture(cyc):
         torch.cuda.synchronize()
         print(f"[4] RCCL all-reduce captured on a forked stream: value ok={ok}, replay {ms(s, e) / 5:.3f} ms "
               f"(sleep branch 1.0 ms)", flush=True)
+        # the DDP pattern: compute A, all-reduce of A's output on a side branch (async_op +
+        # wait() joined at the END), more compute B on the main branch
+        big = torch.ones(16 << 20, device="cuda")
+        g3 = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g3):
+            big.mul_(3.0)                      # A
+            w = dist.all_reduce(big, async_op=True)
+            torch.cuda._sleep(cyc)             # B (1 ms) on the main branch
+            w.wait()                           # join before the capture ends
+        big.fill_(1.0)
+        g3.replay()
+        torch.cuda.synchronize()
+        ok3 = bool((big == 3.0).all().item())
+        s.record()
+        for _ in range(5):
+            g3.replay()
+        e.record()
+        torch.cuda.synchronize()
+        t3 = ms(s, e) / 5
+        # alone: the all-reduce of 64 MB
+        s.record()
+        for _ in range(5):
+            dist.all_reduce(big)
+        e.record()
+        torch.cuda.synchronize()
+        tar = ms(s, e) / 5
+        print(f"[5] async all_reduce captured + wait() at the end: value ok={ok3}, replay {t3:.3f} ms "
+              f"(sleep 1.0 ms + all-reduce alone {tar:.3f} ms -> {'OVERLAPPED' if t3 < 1.0 + 0.5 * tar else 'SERIAL'})",
+              flush=True)
     except Exception as ex:  # noqa: BLE001
         print(f"[4] RCCL capture failed: {type(ex).__name__}: {ex}", flush=True)
     dist.destroy_process_group()

@@ -70,7 +70,7 @@ def test_ddp_engine_two_ranks_one_gpu(cuda):
     run_world(_worker, world=2, native=True, timeout=400)
 
 
-def _graph_worker(rank, world, mode="event"):
+def _graph_worker(rank, world, mode="cut"):
     import torch.distributed as dist
     from faster_distributed_training_amd.parallel import graphs
     graphs.DETACHED_MODE = mode
@@ -101,14 +101,12 @@ def _graph_worker(rank, world, mode="event"):
     st = list(m._plan._graphs.values())[0]
     assert st.stage == "ready"
     assert sum(len(a) for _, a in st.segments) == len(red.buckets)  # every bucket launched from the replay
-    if mode == "cut":
-        assert len(st.segments) > 2  # backward cut at bucket boundaries
-    else:
-        assert len(st.segments) == 1 and st.rec.event_points == len(red.buckets)  # one graph, event nodes
+    assert len(st.segments) > 2 and st.rec.captured == 0  # backward cut at bucket boundaries (gloo: no capture)
 
 
-@pytest.mark.parametrize("mode", ["event", "cut"])
+@pytest.mark.parametrize("mode", ["capture", "cut"])
 def test_ddp_engine_hip_graphs_two_ranks(cuda, mode):
+    """gloo: not capturable, so "capture" mode must fall back to cuts (same result)."""
     run_world(_graph_worker, world=2, native=True, timeout=400, args=(mode,))
 
 
@@ -283,7 +281,10 @@ def _rccl_worker(rank, world):
     bflat = FlatParams(base, device=dev)
     grads(base, bflat)
     g0 = bflat.grad.clone()
-    for cdt, graphs in ((None, False), (torch.bfloat16, False), (None, True)):
+    from faster_distributed_training_amd.parallel import graphs as G
+    for cdt, graphs, mode in ((None, False, "cut"), (torch.bfloat16, False, "cut"), (None, True, "cut"),
+                              (None, True, "capture"), (torch.bfloat16, True, "capture")):
+        G.DETACHED_MODE = mode
         torch.manual_seed(0)
         m = R.resnet18(10).to(dev)
         m.fast_path = True
@@ -291,13 +292,21 @@ def _rccl_worker(rank, world):
         flat = FlatParams(m, device=dev)
         red = BucketReducer(flat, m, bucket_mb=1.0, first_bucket_mb=0.25, comm_dtype=cdt)
         assert red.use_avg  # ReduceOp.AVG on RCCL
-        for it in range(3 if graphs else 1):
+        for it in range(4 if graphs else 1):
             grads(m, flat)
-            assert all(w is not None for w in red.works)
+            if mode == "capture" and it >= 1:
+                # the all-reduces are nodes of the replayed backward graph: nothing left to launch
+                assert all(w is None for w in red.works) and red.in_graph == set(range(len(red.buckets)))
+            else:
+                assert all(w is not None for w in red.works)
             red.finish()
-        err = ((flat.grad - g0).norm() / g0.norm()).item()
-        assert err < (1e-2 if cdt is not None else 1e-6), (cdt, graphs, err)
+            err = ((flat.grad - g0).norm() / g0.norm()).item()
+            assert err < (1e-2 if cdt is not None else 1e-6), (cdt, graphs, mode, it, err)
+        if mode == "capture":
+            st = list(m._plan._graphs.values())[0]
+            assert len(st.segments) == 1 and st.rec.captured == len(red.buckets)  # one backward graph
         red.remove()
+    G.DETACHED_MODE = "cut"
     pdist.barrier()  # dist.barrier(device_ids=[...]) on RCCL
     # sharded optimizer (ZeRO-2) and FSDP full-shard over RCCL
     torch.manual_seed(0)
@@ -328,9 +337,9 @@ def test_rccl_world1_code_paths(cuda):
     run_world(_rccl_worker, world=1, native=True, backend="nccl", timeout=400)
 
 
-def _segmented_worker(rank, world, mode="event"):
+def _segmented_worker(rank, world, mode="cut"):
     """An autograd backward captured as HIP-graph segments cut at DDP bucket boundaries
-    (parallel/graphs.SegmentedStep; or one graph with event-record nodes there): replays give
+    (parallel/graphs.SegmentedStep; gloo is not capturable, so "capture" mode falls back to cuts): replays give
     the eager reducer's averaged gradient."""
     import torch.distributed as dist
     import torch.nn as nn
@@ -366,9 +375,7 @@ def _segmented_worker(rank, world, mode="event"):
     flat.grad.zero_()
     step.capture(body)
     red.finish()  # (the capture launched nothing; reset the bucket state)
-    cuts = step.num_segments - 2 + step.rec.event_points
-    assert cuts == len(red.buckets), (step.num_segments, step.rec.event_points, len(red.buckets))  # fwd + cuts + tail
-    assert (step.rec.event_points == 0) == (mode == "cut")
+    assert step.num_segments == len(red.buckets) + 2, (step.num_segments, len(red.buckets))  # fwd + cuts + tail
     for x, y, w in zip(xs, ys, want):
         sx.copy_(x)
         sy.copy_(y)
@@ -380,7 +387,7 @@ def _segmented_worker(rank, world, mode="event"):
         assert err < 1e-6, err
 
 
-@pytest.mark.parametrize("mode", ["event", "cut"])
+@pytest.mark.parametrize("mode", ["capture", "cut"])
 def test_segmented_graph_ddp_matches_eager(cuda, mode):
     run_world(_segmented_worker, world=2, native=True, timeout=300, args=(mode,))
 
@@ -403,7 +410,7 @@ def _transformer_ddp_graph_worker(rank, world):
         dist.all_gather(alls, chk)
         assert all(torch.equal(alls[0], t) for t in alls)  # replicas stay in sync
     ent = [e for e in tr._graphs.values() if isinstance(e, dict)][0]
-    assert ent["segments"] - 2 + ent["step"].rec.event_points == len(tr.reducer.buckets)  # one launch per bucket
+    assert ent["segments"] - 2 + ent["step"].rec.captured == len(tr.reducer.buckets)  # one launch per bucket
 
 
 def test_transformer_ddp_hip_graphs_two_ranks(cuda):
@@ -413,7 +420,7 @@ def test_transformer_ddp_hip_graphs_two_ranks(cuda):
 def _transformer_fsdp_graph_worker(rank, world, schedule):
     """The transformer under static FSDP captured as HIP graphs: the forward is
     cut at every wrap unit (gather wait + prefetch between segments), the reduce-scatters are
-    event-gated actions of the backward graph (plus, FULL_SHARD, the re-gathers before each
+    actions between backward segments (plus, FULL_SHARD, the re-gathers before each
     unit's backward); 6 steps equal the eager FSDP run (dropout off, lambda 0)."""
     import torch.nn as nn
     import faster_distributed_training_amd.train.transformer_trainer as T
