@@ -438,7 +438,7 @@ def conv_wgrad(g, y, al, be, x, shp: ConvShape, out, xs=None, xt=None, act=0, al
         # partial tiles in register order in the persistent split-K workspace
         tiles = (shp.cout // bm) * (-(-ldw // bn))
         slab, cnt = splitk_workspace(g.device, tiles * ns * bm * bn, tiles)
-    elif slab is None or slab.numel() < ns * shp.cout * ldw:
+    elif not direct and (slab is None or slab.numel() < ns * shp.cout * ldw):
         slab = torch.empty(ns * shp.cout * ldw, device=g.device, dtype=torch.float32)
     dh, dw, _ = taps_fwd(shp.k, shp.pad)
     if xs is None and act != 0:

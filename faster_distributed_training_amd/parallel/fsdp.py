@@ -541,8 +541,10 @@ class FullyShardedDP:
     def _ring_bwd_prepare(self, u):
         o = self.grad_owner[u.slot]
         if o is not None and o is not u and o.rs_work is not None:
-            o.rs_work.wait()  # (stream wait: the slot's reduce-scatter has read it)
-            o.rs_work = None
+            # (stream wait: the slot's reduce-scatter has read it).  rs_work stays set: under
+            # graph replay it is the only per-step sign that o took part (finish_backward would
+            # otherwise treat o as unused and re-reduce a zeroed slot)
+            o.rs_work.wait()
         self.grad_owner[u.slot] = u
         u.gather(wait=True)
         if self.prefetch:
@@ -584,11 +586,19 @@ class FullyShardedDP:
             if not u.bwd_started:
                 # a gradient that arrived before the unit's output hook (root unit, or an
                 # output without grad): start the unit's backward, keep what was accumulated
-                g = p.grad
-                u.begin_backward()
-                if g is not None:
-                    with torch.no_grad():
-                        p.grad.add_(g)
+                if self.static and p.grad is not None and u.gfull.untyped_storage().data_ptr() == \
+                        p.grad.untyped_storage().data_ptr():
+                    # static mode: p.grad is still bound to the unit's gradient buffer (zeroed at
+                    # the end of the previous step, finish_backward) and autograd accumulated into
+                    # it in place -- zeroing it now would drop this gradient
+                    u.bwd_started = u.grads_live = True
+                    u.pending = sum(1 for _, q in u.params if q.requires_grad)
+                else:
+                    g = p.grad
+                    u.begin_backward()
+                    if g is not None:
+                        with torch.no_grad():
+                            p.grad.add_(g)
             u.grad_ready()
         return hook
 
@@ -627,6 +637,10 @@ class FullyShardedDP:
         for u in unused:  # contributes zeros (every rank must join the collective); after the
             u.begin_backward(gather=False)  # others, whose reduce-scatters may read a shared ring slot
             u.finish()
+        if self.static:
+            for u in self.units:
+                if u.root:  # (its first gradient of the next step accumulates in place, see the hook)
+                    u.gfull.zero_()
         self.last_rs = None
         if self.offload:
             if self.copy_stream is not None:

@@ -430,7 +430,7 @@ def _transformer_fsdp_graph_worker(rank, world, schedule):
         T.TR_GRAPHS = graphs
         torch.manual_seed(0)
         cfg = T.TransformerConfig(batch_size=16, synthetic=True, eval=False, plot=False, distributed=True, fsdp=True,
-                                  fsdp_schedule=schedule, optimizer="mirror_madgrad", epoch=1, length_buckets=(128,),
+                                  fsdp_schedule=schedule, optimizer="sgd", epoch=1, length_buckets=(128,),
                                   n_layers=2, extra={"subset_stride": 50})
         tr = T.TransformerTrainer(cfg)
         for mod in tr.model.modules():
