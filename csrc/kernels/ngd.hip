@@ -945,10 +945,13 @@ void ngd_post_eigh(uint64_t c, uint64_t U, uint64_t ise, uint64_t drho, uint64_t
 //              the block of J + wc W in LDS, 20 outputs per thread
 constexpr int kGT = 32;
 
+constexpr int kGK = 64;  // d per LDS chunk
+
+template <bool VEC>
 __global__ __launch_bounds__(256) void ngd_gram_partial_kernel(const float* __restrict__ J, const float* __restrict__ W,
                                                                float* __restrict__ slab, int R, int D, int nt,
                                                                int tiles_per_g, int S, int dlen) {
-  __shared__ float a[kGT][kGT + 1], b[kGT][kGT + 1];
+  __shared__ float a[kGT][kGK + 1], b[kGT][kGK + 1];
   const int s = blockIdx.x % S;
   const int t = (blockIdx.x / S) % tiles_per_g;
   const int g = blockIdx.x / (S * tiles_per_g);
@@ -970,15 +973,59 @@ __global__ __launch_bounds__(256) void ngd_gram_partial_kernel(const float* __re
   const int d0 = s * dlen, d1 = min(D, d0 + dlen);
   const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
   float acc[2][2] = {{0.f, 0.f}, {0.f, 0.f}};
-  for (int dc = d0; dc < d1; dc += kGT) {
-    for (int e = threadIdx.x; e < kGT * kGT; e += 256) {
-      const int r = e / kGT, c = e % kGT, d = dc + c;
-      a[r][c] = (i0 + r < R && d < d1) ? J[base + (long)(i0 + r) * D + d] : 0.f;
-      b[r][c] = (j0 + r < R && d < d1) ? Bsrc[base + (long)(j0 + r) * D + d] : 0.f;
+  // register-staged loads of the NEXT chunk are in flight while the current one is computed
+  // (the loop is latency-bound: 256 FMAs per thread per chunk against one global round trip)
+  constexpr int NL = kGT * kGK / 256;  // floats per thread per operand (8)
+  float ra[NL], rb[NL];
+  auto load = [&](int dc) {
+    if constexpr (VEC) {
+#pragma unroll
+      for (int q = 0; q < NL / 4; ++q) {
+        const int e = threadIdx.x + q * 256;
+        const int r = e / (kGK / 4), c = (e % (kGK / 4)) * 4, d = dc + c;
+        float4 va = make_float4(0.f, 0.f, 0.f, 0.f), vb = va;
+        if (d < d1) {  // (d1 and D are multiples of 4 here: a float4 never straddles the end)
+          if (i0 + r < R) va = *reinterpret_cast<const float4*>(J + base + (long)(i0 + r) * D + d);
+          if (j0 + r < R) vb = *reinterpret_cast<const float4*>(Bsrc + base + (long)(j0 + r) * D + d);
+        }
+        ra[4 * q] = va.x; ra[4 * q + 1] = va.y; ra[4 * q + 2] = va.z; ra[4 * q + 3] = va.w;
+        rb[4 * q] = vb.x; rb[4 * q + 1] = vb.y; rb[4 * q + 2] = vb.z; rb[4 * q + 3] = vb.w;
+      }
+    } else {
+#pragma unroll
+      for (int q = 0; q < NL; ++q) {
+        const int e = threadIdx.x + q * 256;
+        const int r = e / kGK, c = e % kGK, d = dc + c;
+        ra[q] = (i0 + r < R && d < d1) ? J[base + (long)(i0 + r) * D + d] : 0.f;
+        rb[q] = (j0 + r < R && d < d1) ? Bsrc[base + (long)(j0 + r) * D + d] : 0.f;
+      }
     }
+  };
+  auto store = [&]() {
+    if constexpr (VEC) {
+#pragma unroll
+      for (int q = 0; q < NL / 4; ++q) {
+        const int e = threadIdx.x + q * 256;
+        const int r = e / (kGK / 4), c = (e % (kGK / 4)) * 4;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) { a[r][c + k] = ra[4 * q + k]; b[r][c + k] = rb[4 * q + k]; }
+      }
+    } else {
+#pragma unroll
+      for (int q = 0; q < NL; ++q) {
+        const int e = threadIdx.x + q * 256;
+        a[e / kGK][e % kGK] = ra[q];
+        b[e / kGK][e % kGK] = rb[q];
+      }
+    }
+  };
+  if (d0 < d1) load(d0);
+  for (int dc = d0; dc < d1; dc += kGK) {
+    store();
     __syncthreads();
-#pragma unroll 8
-    for (int c = 0; c < kGT; ++c) {
+    if (dc + kGK < d1) load(dc + kGK);
+#pragma unroll 16
+    for (int c = 0; c < kGK; ++c) {
       const float a0 = a[ty * 2][c], a1 = a[ty * 2 + 1][c], b0 = b[tx * 2][c], b1 = b[tx * 2 + 1][c];
       acc[0][0] = fmaf(a0, b0, acc[0][0]);
       acc[0][1] = fmaf(a0, b1, acc[0][1]);
@@ -1027,13 +1074,13 @@ __global__ __launch_bounds__(256) void ngd_gram_sum_kernel(const float* __restri
 }
 
 static void gram_split(int G, int tiles_per_g, int D, int& S, int& dlen) {
-  // ~1024 workgroups in all, each reducing >= 256 of d (and a multiple of the 32-wide chunk)
+  // ~2048 workgroups in all, each reducing >= 128 of d (a multiple of the 64-wide chunk)
   const long wgs = (long)G * tiles_per_g;
-  long s = (1024 + wgs - 1) / wgs;
-  long smax = (D + 255) / 256;
+  long s = (2048 + wgs - 1) / wgs;
+  long smax = (D + 127) / 128;
   if (s > smax) s = smax;
   if (s < 1) s = 1;
-  dlen = (int)(((D + s - 1) / s + kGT - 1) / kGT * kGT);
+  dlen = (int)(((D + s - 1) / s + kGK - 1) / kGK * kGK);
   S = (D + dlen - 1) / dlen;
 }
 
@@ -1055,8 +1102,9 @@ void ngd_gram(uint64_t J, uint64_t W, uint64_t K, uint64_t L, uint64_t slab, int
   int S, dlen;
   gram_split(G, tpg, D, S, dlen);
   hipStream_t st = as_stream(stream);
-  ngd_gram_partial_kernel<<<G * tpg * S, 256, 0, st>>>(P<const float>(J), P<const float>(W), P<float>(slab), R, D, nt,
-                                                       tpg, S, dlen);
+  const bool vec = D % 4 == 0 && J % 16 == 0 && (W == 0 || W % 16 == 0);
+  (vec ? ngd_gram_partial_kernel<true> : ngd_gram_partial_kernel<false>)<<<G * tpg * S, 256, 0, st>>>(
+      P<const float>(J), P<const float>(W), P<float>(slab), R, D, nt, tpg, S, dlen);
   FDT_LAUNCH_CHECK();
   const long total = (long)G * tpg * kGT * kGT;
   ngd_gram_sum_kernel<<<(int)((total + 255) / 256), 256, 0, st>>>(P<const float>(slab), P<float>(K), P<float>(L), R,
@@ -1070,8 +1118,10 @@ __global__ __launch_bounds__(256) void ngd_wupdate_kernel(const float* __restric
                                                           const float* __restrict__ wc, float* __restrict__ W, int R,
                                                           int D, int nblk) {
   extern __shared__ float lds[];
+  constexpr int LB = kWuCols + 4;         // B row stride (16-B aligned rows)
   float* As = lds;                        // [R][R + 1]
-  float* Bs = lds + R * (R + 1);          // [R][kWuCols + 1]
+  float* Bs = lds + R * (R + 1);          // [R][LB]  (R*(R+1) is even; Bs 8-B aligned, see the 16-B fix below)
+  Bs = reinterpret_cast<float*>((reinterpret_cast<uintptr_t>(Bs) + 15) & ~(uintptr_t)15);
   const int g = blockIdx.x / nblk, blk = blockIdx.x % nblk;
   const int c0 = blk * kWuCols;
   const float* Ag = A + (long)g * R * R;
@@ -1081,27 +1131,41 @@ __global__ __launch_bounds__(256) void ngd_wupdate_kernel(const float* __restric
     const int r = e / kWuCols, c = e % kWuCols, d = c0 + c;
     float v = 0.f;
     if (d < D) v = fmaf(wc[(long)g * R + r], W[base + (long)r * D + d], J[base + (long)r * D + d]);
-    Bs[r * (kWuCols + 1) + c] = v;
+    Bs[r * LB + c] = v;
   }
   __syncthreads();  // (every W value of this block is in LDS before any is overwritten)
-  const int c = threadIdx.x % kWuCols, r0 = threadIdx.x / kWuCols;  // a wave shares r0: A reads broadcast
-  const int d = c0 + c;
-  float acc[(kNgdMaxR + 3) / 4];
+  // thread: 4 consecutive columns x rows rg, rg + 16, ... (A reads broadcast over the 16
+  // column groups of a row group, one 16-B B read per k)
+  const int cg = threadIdx.x & 15, rg = threadIdx.x >> 4;
+  constexpr int MR = (kNgdMaxR + 15) / 16;
+  float acc[MR][4];
 #pragma unroll
-  for (int q = 0; q < (kNgdMaxR + 3) / 4; ++q) acc[q] = 0.f;
+  for (int q = 0; q < MR; ++q)
+#pragma unroll
+    for (int k = 0; k < 4; ++k) acc[q][k] = 0.f;
   for (int k = 0; k < R; ++k) {
-    const float bk = Bs[k * (kWuCols + 1) + c];
+    const float4 bk = *reinterpret_cast<const float4*>(Bs + k * LB + cg * 4);
 #pragma unroll
-    for (int q = 0; q < (kNgdMaxR + 3) / 4; ++q) {
-      const int r = r0 + 4 * q;
-      if (r < R) acc[q] = fmaf(As[r * (R + 1) + k], bk, acc[q]);
+    for (int q = 0; q < MR; ++q) {
+      const int r = rg + 16 * q;
+      if (r < R) {
+        const float av = As[r * (R + 1) + k];
+        acc[q][0] = fmaf(av, bk.x, acc[q][0]);
+        acc[q][1] = fmaf(av, bk.y, acc[q][1]);
+        acc[q][2] = fmaf(av, bk.z, acc[q][2]);
+        acc[q][3] = fmaf(av, bk.w, acc[q][3]);
+      }
     }
   }
-  if (d < D) {
 #pragma unroll
-    for (int q = 0; q < (kNgdMaxR + 3) / 4; ++q) {
-      const int r = r0 + 4 * q;
-      if (r < R) W[base + (long)r * D + d] = acc[q];
+  for (int q = 0; q < MR; ++q) {
+    const int r = rg + 16 * q;
+    if (r < R) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int d = c0 + cg * 4 + k;
+        if (d < D) W[base + (long)r * D + d] = acc[q][k];
+      }
     }
   }
 }
@@ -1110,7 +1174,7 @@ void ngd_wupdate(uint64_t A, uint64_t J, uint64_t wc, uint64_t W, int G, int R, 
   FDT_CHECK(R >= 1 && R <= kNgdMaxR && D >= 1, "ngd_wupdate: shape");
   if (G == 0) return;
   const int nblk = (D + kWuCols - 1) / kWuCols;
-  const size_t lds = ((size_t)R * (R + 1) + (size_t)R * (kWuCols + 1)) * sizeof(float);
+  const size_t lds = ((size_t)R * (R + 1) + (size_t)R * (kWuCols + 4) + 4) * sizeof(float);
   ngd_wupdate_kernel<<<G * nblk, 256, lds, as_stream(stream)>>>(P<const float>(A), P<const float>(J), P<const float>(wc),
                                                               P<float>(W), R, D, nblk);
   FDT_LAUNCH_CHECK();

@@ -40,8 +40,11 @@ def batched_eigh(Z: torch.Tensor, sweeps: int = SWEEPS, tol: float = TOL):
         V = torch.empty(G, n, n, device=Z.device, dtype=torch.float32)
         nat.jacobi_eigh(A.data_ptr(), w.data_ptr(), V.data_ptr(), 0, G, n, sweeps, tol, _native.stream_ptr())
         return w, V
-    if Z.is_cuda:
-        return torch.linalg.eigh(Z)
+    # everything else: fp64, upper triangle -- the reference's CPU eigh (ngd_optimizer.py:262-265).
+    # (fp32 rocSOLVER on the lower triangle, the previous GPU fallback, read a slightly
+    # different Z -- L = J W^T is not symmetric -- and lost the near-degenerate eigenvectors of
+    # the initialisation schedule: the FDT_NATIVE=0 NGD run diverged within 20 steps,
+    # profiles/r4/convergence_first_run_ngd_lr0.05.json)
     return eigh_reference(Z)
 
 

