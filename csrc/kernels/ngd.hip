@@ -1125,13 +1125,74 @@ __global__ __launch_bounds__(256) void ngd_wupdate_kernel(const float* __restric
   const int g = blockIdx.x / nblk, blk = blockIdx.x % nblk;
   const int c0 = blk * kWuCols;
   const float* Ag = A + (long)g * R * R;
-  for (int e = threadIdx.x; e < R * R; e += 256) As[(e / R) * (R + 1) + e % R] = Ag[e];
   const long base = (long)g * R * D;
-  for (int e = threadIdx.x; e < R * kWuCols; e += 256) {
-    const int r = e / kWuCols, c = e % kWuCols, d = c0 + c;
-    float v = 0.f;
-    if (d < D) v = fmaf(wc[(long)g * R + r], W[base + (long)r * D + d], J[base + (long)r * D + d]);
-    Bs[r * LB + c] = v;
+  // operand staging with several loads in flight per thread (a load-then-store loop waits out
+  // one global round trip per element: ~27 us per launch at R = 80, ~20x the arithmetic)
+  constexpr int IF = 4;
+  if ((R & 3) == 0) {
+    const float4* A4 = reinterpret_cast<const float4*>(Ag);
+    const int n4 = R * R / 4;
+    for (int e0 = threadIdx.x; e0 < n4; e0 += 256 * IF) {
+      float4 v[IF];
+#pragma unroll
+      for (int q = 0; q < IF; ++q) {
+        const int i = e0 + q * 256;
+        v[q] = i < n4 ? A4[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+#pragma unroll
+      for (int q = 0; q < IF; ++q) {
+        const int i = e0 + q * 256;
+        if (i < n4) {
+          const float vv[4] = {v[q].x, v[q].y, v[q].z, v[q].w};
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            const int e = 4 * i + k;
+            As[(e / R) * (R + 1) + e % R] = vv[k];
+          }
+        }
+      }
+    }
+  } else {
+    for (int e = threadIdx.x; e < R * R; e += 256) As[(e / R) * (R + 1) + e % R] = Ag[e];
+  }
+  const bool vec = (D & 3) == 0 && c0 + kWuCols <= D;
+  if (vec) {
+    constexpr int C4 = kWuCols / 4;
+    const int n4 = R * C4;
+    for (int e0 = threadIdx.x; e0 < n4; e0 += 256 * IF) {
+      float4 vw[IF], vj[IF];
+      float sc[IF];
+#pragma unroll
+      for (int q = 0; q < IF; ++q) {
+        const int i = e0 + q * 256;
+        const int r = i / C4, c = (i % C4) * 4;
+        if (i < n4) {
+          vw[q] = *reinterpret_cast<const float4*>(W + base + (long)r * D + c0 + c);
+          vj[q] = *reinterpret_cast<const float4*>(J + base + (long)r * D + c0 + c);
+          sc[q] = wc[(long)g * R + r];
+        }
+      }
+#pragma unroll
+      for (int q = 0; q < IF; ++q) {
+        const int i = e0 + q * 256;
+        if (i < n4) {
+          const int r = i / C4, c = (i % C4) * 4;
+          float4 o;
+          o.x = fmaf(sc[q], vw[q].x, vj[q].x);
+          o.y = fmaf(sc[q], vw[q].y, vj[q].y);
+          o.z = fmaf(sc[q], vw[q].z, vj[q].z);
+          o.w = fmaf(sc[q], vw[q].w, vj[q].w);
+          *reinterpret_cast<float4*>(Bs + r * LB + c) = o;
+        }
+      }
+    }
+  } else {
+    for (int e = threadIdx.x; e < R * kWuCols; e += 256) {
+      const int r = e / kWuCols, c = e % kWuCols, d = c0 + c;
+      float v = 0.f;
+      if (d < D) v = fmaf(wc[(long)g * R + r], W[base + (long)r * D + d], J[base + (long)r * D + d]);
+      Bs[r * LB + c] = v;
+    }
   }
   __syncthreads();  // (every W value of this block is in LDS before any is overwritten)
   // thread: 4 consecutive columns x rows rg, rg + 16, ... (A reads broadcast over the 16
