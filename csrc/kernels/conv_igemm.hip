@@ -83,6 +83,7 @@ static void conv_igemm_impl(uint64_t x, uint64_t x2, uint64_t ps, uint64_t pt, u
   if (a.M == 0) return;
   const int act = (pro == kProAffineAct || pro == kProJoin) ? pro_act : ((epi == kEpiActBwd || epi == kEpiJoinBwd) ? epi_act : 0);
   if (kg == 2 && a.nsplit > 1) kg = 1;  // K groups and split-K are alternatives
+  if (kg == 3 && pro != kProNone) kg = 1;  // the LDS-DMA ring cannot apply a prologue
   if (launch_cases_fwd(pro, epi, act, a, BM, BN, BK, kg, pure, st) ||
       launch_cases_fold(pro, epi, act, a, BM, BN, BK, kg, pure, st) ||
       launch_cases_join(pro, epi, act, a, BM, BN, BK, kg, pure, st) ||

@@ -211,9 +211,16 @@ constexpr int kMinWavesPerEU =
     (BM == 128 && BN == 128 && BK == 32 && (PRO == kProNone || (PRO == kProAffineAct && PURE))) ? 4
     : (BM == 128 && BN == 128 && (BK == 32 || (PRO != 2 && PRO != 3))) ? 3 : 1;
 
+// KG: 1 = one 4-wave K group, register-staged 2-deep; 2 = two K groups (see above);
+// 3 = one group whose operand tiles move global -> LDS by LDS-DMA (buffer_load ... lds) into a
+// 3-buffer ring, two tiles in flight ACROSS the per-tile barrier (counted vmcnt + raw
+// s_barrier: __syncthreads() would drain every in-flight DMA) -- prologue-free convolutions
+// only (the DMA cannot transform), no staging registers and no ds_write pass.
 template <int BM, int BN, int BK, int PRO, int EPI, bool PURE, int ACT, int KG>
-__global__ __launch_bounds__(256 * KG, (KG == 1 ? kMinWavesPerEU<BM, BN, BK, PRO, PURE> : 1)) void igemm_kernel(
-    const ConvArgs a) {
+__global__ __launch_bounds__(256 * (KG == 2 ? 2 : 1), (KG == 1 ? kMinWavesPerEU<BM, BN, BK, PRO, PURE> : 1)) void
+igemm_kernel(const ConvArgs a) {
+  constexpr bool GL = KG == 3;
+  static_assert(!GL || PRO == kProNone, "LDS-DMA staging moves bytes untransformed: prologue-free convolutions only");
   constexpr int CPR = BK / 8;        // 16-B chunks per LDS row
   constexpr int RPR = 256 / CPR;     // rows covered by one load round
   constexpr int NXL = BM / RPR;      // activation chunks per thread per tile
@@ -241,8 +248,8 @@ __global__ __launch_bounds__(256 * KG, (KG == 1 ? kMinWavesPerEU<BM, BN, BK, PRO
   // tid / lane / wid are local to the K group (every load / fragment / epilogue mapping below
   // is written for 256 threads); grp selects the group's K tiles and LDS buffers
   const int tid = threadIdx.x & 255, lane = tid & 63, wid = tid >> 6;
-  const int grp = KG == 1 ? 0 : (int)(threadIdx.x >> 8);
-  static_assert(KG == 1 || KG == 2, "one or two K groups");
+  const int grp = KG == 2 ? (int)(threadIdx.x >> 8) : 0;
+  static_assert(KG == 1 || KG == 2 || KG == 3, "one or two K groups, or the LDS-DMA ring");
   const int wn = wid & 1, wm = wid >> 1;
   // a tile's splits are consecutive ids -> the same XCD after the remap
   const int rid = xcd_remap(blockIdx.x, a.nbm * a.nbn * a.nsplit);
@@ -452,10 +459,81 @@ __global__ __launch_bounds__(256 * KG, (KG == 1 ? kMinWavesPerEU<BM, BN, BK, PRO
   // meet every barrier)
   const int kb = split * a.kps;
   const int nk = min(nkt - kb, a.kps);
-  const int nkk = (nk + KG - 1) / KG;
-  auto ld = [&](Stage& S, int i) { load_tile(S, kb + i * KG + grp, i < nkk && i * KG + grp < nk); };
+  constexpr int KGN = KG == 2 ? 2 : 1;
+  const int nkk = (nk + KGN - 1) / KGN;
+  auto ld = [&](Stage& S, int i) { load_tile(S, kb + i * KGN + grp, i < nkk && i * KGN + grp < nk); };
 
-  {
+  if constexpr (GL) {
+    // ---- LDS-DMA ring: tile t lands in buffer t % 3.  Lane l of a wave instruction writes
+    // LDS base + 16 l, so a wave's 64 lanes fill 64 consecutive 16-B slots; the slot of
+    // (row, chunk) is row*CPR + chunk (= tid + 256 j for this thread's j-th chunk), and the XOR
+    // swizzle the fragment reads expect is applied on the SOURCE address (the lane filling
+    // physical chunk cc fetches logical chunk cc ^ swz(row)).  Out-of-range offsets (padding,
+    // K tail, past this split) read zeros.
+    constexpr int G = NXL + NWL;  // DMA instructions per tile per thread
+    if (tid < 12) {
+      const int dh = a.dh[tid], dw = a.dw[tid];
+      tapt[tid] = dh * a.Wi + dw;
+      tapw[tid] = (int)(uint8_t)a.dh[tid] | ((int)(uint8_t)a.dw[tid] << 8) | ((int)(uint8_t)a.wt[tid] << 16);
+    }
+    __syncthreads();              // LDS header (tap table) ready
+    // (readfirstlane: the DMA's LDS base goes to M0 -- a base the compiler cannot prove
+    // wave-uniform is issued as a waterfall loop of exec-masked DMAs)
+    const int wave_slot = __builtin_amdgcn_readfirstlane(wid) * 64;
+    auto issue = [&](int i) {
+      const int kt = kb + i;
+      const bool live = i < nk;
+      bf16* Wl = tiles + (i % 3) * (WT + XT);
+      bf16* Xl = Wl + WT;
+#pragma unroll
+      for (int j = 0; j < NXL; ++j) {
+        const int row = tid / CPR + j * RPR;
+        const int lc = cc ^ swz<CPR>(row);
+        const int k = kt * BK + lc * 8;
+        const int tap = k >> a.log2Cx;
+        const int ci = k & (a.Cx - 1);
+        bool v = rv[j] & live & (tap < a.ntaps);
+        int toff = 0;
+        if constexpr (!PURE) {
+          const int tq = tap < 12 ? tap : 11;
+          const int e = tapw[tq];
+          const int dh = (int)(int8_t)(e & 0xff), dw = (int)(int8_t)((e >> 8) & 0xff);
+          toff = tapt[tq];
+          v = v & ((unsigned)(ohs[j] + dh) < (unsigned)a.Hi) & ((unsigned)(ows[j] + dw) < (unsigned)a.Wi);
+        }
+        const uint32_t off = v ? (((uint32_t)(pixb[j] + toff) << a.log2Cx) + ci) * 2u : kOOB;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(
+            rx_d, (__attribute__((address_space(3))) void*)(Xl + (wave_slot + j * 256) * 8), 16, off, 0, 0, 0);
+      }
+#pragma unroll
+      for (int j = 0; j < NWL; ++j) {
+        const int row = tid / CPR + j * RPR;
+        const int lc = cc ^ swz<CPR>(row);
+        const int k = kt * BK + lc * 8;
+        const int tap = k >> a.log2Cx;
+        const int ci = k & (a.Cx - 1);
+        const bool tok = live & (tap < a.ntaps);
+        int wt = 0;
+        if constexpr (!PURE) wt = (tapw[tap < 12 ? tap : 11] >> 16) & 0xff;
+        const uint32_t off = tok ? ((uint32_t)(n0 + row) * (uint32_t)a.ldw + (uint32_t)(wt * a.Cx + ci)) * 2u : kOOB;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(
+            rw_d, (__attribute__((address_space(3))) void*)(Wl + (wave_slot + j * 256) * 8), 16, off, 0, 0, 0);
+      }
+    };
+    if (nk > 0) {
+      issue(0);
+      issue(1);  // (a tile past nk loads zeros: the count below stays exact)
+    }
+    for (int t = 0; t < nk; ++t) {
+      // tile t landed (this wave's DMAs: all but the G of tile t+1), then everyone's
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(G) : "memory");
+      __builtin_amdgcn_s_barrier();
+      // buffer (t+2) % 3 held tile t-1: every wave finished its MFMAs before this barrier
+      issue(t + 2);
+      compute(t % 3);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (the zero-tiles past nk)
+  } else {
   // prologue: tile 0 -> LDS buf 0; tile 1 pending in B; tile 2 in flight in A.
   // 1x1 convolutions address their operands without the LDS tap table, so their first two
   // K tiles are requested BEFORE the LDS setup (prologue parameters, tap table) and its
@@ -548,7 +626,7 @@ __global__ __launch_bounds__(256 * KG, (KG == 1 ? kMinWavesPerEU<BM, BN, BK, PRO
 
   // ------------------------------------------------------------------ split-K combine
   // (KG == 2 launches never split K over workgroups: the host refuses nsplit > 1 there)
-  if (KG == 1 && a.nsplit > 1) {
+  if (KG != 2 && a.nsplit > 1) {
     constexpr int NR4 = TN * TM * 4;  // float4 registers per thread
     // this tile's slabs [nsplit][NR4][256] float4 behind one buffer descriptor
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
@@ -833,7 +911,7 @@ static void launch_one(const ConvArgs& a, size_t lds, hipStream_t st) {
                                       (int)lds));
     attr_set = lds;
   }
-  hipLaunchKernelGGL(kern, dim3(a.nbm * a.nbn * a.nsplit), dim3(256 * KG), lds, st, a);
+  hipLaunchKernelGGL(kern, dim3(a.nbm * a.nbn * a.nsplit), dim3(KG == 2 ? 512 : 256), lds, st, a);
   FDT_LAUNCH_CHECK();
 }
 
@@ -851,8 +929,10 @@ static void launch_pure(const ConvArgs& a, bool pure, size_t lds, hipStream_t st
 template <int PRO, int EPI, int ACT>
 static void launch_tile(const ConvArgs& a, int BM, int BN, int BK, int kg, bool pure, hipStream_t st) {
   const int nkt = (a.K + BK - 1) / BK;
-  const size_t nbuf = nkt > 1 ? 2 : 1;
-  FDT_CHECK(kg == 1 || (kg == 2 && a.nsplit == 1 && nkt >= 2), "K groups: kg 1 | 2 (2: no split-K, >= 2 K tiles)");
+  const size_t nbuf = kg == 3 ? 3 : (nkt > 1 ? 2 : 1);
+  FDT_CHECK(kg == 1 || kg == 3 || (kg == 2 && a.nsplit == 1 && nkt >= 2),
+            "K groups: kg 1 | 2 (2: no split-K, >= 2 K tiles) | 3 (LDS-DMA ring)");
+  FDT_CHECK(kg != 3 || PRO == kProNone, "the LDS-DMA ring is for prologue-free convolutions");
   // header (must match the kernel's hdr) + max(K tiles of every K group, epilogue staging
   // [64][BN + 4] fp32, K-group hand-off [BM*BN] fp32)
   const int nprm = PRO == kProJoin ? 4 : (PRO == kProFold ? 3 : ((PRO == kProAffineAct) ? 2 : 0));
@@ -862,18 +942,27 @@ static void launch_tile(const ConvArgs& a, int BM, int BN, int BK, int kg, bool 
   size_t body = tiles > stage ? tiles : stage;
   if (hand > body) body = hand;
   size_t lds = hdr + body;
-#define FDT_T(BM_, BN_, BK_) \
-  if (BM == BM_ && BN == BN_ && BK == BK_) { launch_pure<BM_, BN_, BK_, PRO, EPI, ACT, 1>(a, pure, lds, st); return; }
+#define FDT_T(BM_, BN_, BK_)                                                              \
+  if (BM == BM_ && BN == BN_ && BK == BK_) {                                              \
+    if constexpr (PRO == kProNone) {                                                      \
+      if (kg == 3) { launch_pure<BM_, BN_, BK_, PRO, EPI, ACT, 3>(a, pure, lds, st); return; } \
+    }                                                                                     \
+    launch_pure<BM_, BN_, BK_, PRO, EPI, ACT, 1>(a, pure, lds, st);                       \
+    return;                                                                               \
+  }
   // two K groups: the tiles the small-M (latency-bound, ~256-workgroup) layers use
 #define FDT_T2(BM_, BN_, BK_)                                                                   \
   if (BM == BM_ && BN == BN_ && BK == BK_) {                                                   \
+    if constexpr (PRO == kProNone) {                                                           \
+      if (kg == 3) { launch_pure<BM_, BN_, BK_, PRO, EPI, ACT, 3>(a, pure, lds, st); return; }  \
+    }                                                                                          \
     if (kg == 2) launch_pure<BM_, BN_, BK_, PRO, EPI, ACT, 2>(a, pure, lds, st);              \
     else launch_pure<BM_, BN_, BK_, PRO, EPI, ACT, 1>(a, pure, lds, st);                      \
     return;                                                                                    \
   }
   // (K groups at 128x64x128 / 64x128x128 spill with the two-operand prologues under the
   // 256-VGPR budget of 8-wave workgroups: those tiles stay single-group)
-  FDT_CHECK(kg == 1 || BK == 64 || (BM == 64 && BN == 64), "K groups: unsupported tile");
+  FDT_CHECK(kg != 2 || BK == 64 || (BM == 64 && BN == 64), "K groups: unsupported tile");
   FDT_T2(128, 128, 64) FDT_T2(128, 64, 64) FDT_T2(64, 128, 64) FDT_T2(64, 64, 64) FDT_T(256, 64, 64)
   FDT_T(128, 128, 32) FDT_T(128, 64, 32) FDT_T(64, 128, 32) FDT_T(64, 64, 32) FDT_T(256, 128, 32)
   // BK = 128: half the K-loop trips for the latency-bound small-M layers (8x8 / 4x4 stages at

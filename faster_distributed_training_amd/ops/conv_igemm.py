@@ -183,10 +183,23 @@ KGROUPS = os.environ.get("FDT_KGROUPS", "1") != "0"
 KG_TILES = {(128, 128, 64), (128, 64, 64), (64, 128, 64), (64, 64, 64), (64, 64, 128)}
 
 
-def _kg(ent, kg, tile3, ns, K):
-    """K groups of one launch: explicit ``kg``, else the tuned entry's, else 1."""
+# prologue-free launches (3x3 convs on materialised operands, plain dgrads) can stage their tiles
+# by LDS-DMA into a 3-buffer ring (kg = 3, csrc/kernels/conv_igemm_impl.h): bitwise equal to the
+# register-staged path, measured neutral at batch 128 (5.519 vs 5.518 ms) and slower at batch
+# 1024 (26.04 -> 26.73 ms; the 32x32 / strided dgrads lose 13-32 %), profiles/r4/ab_glds_* --
+# so opt-in
+GLDS = os.environ.get("FDT_CONV_GLDS", "0") == "1"
+
+
+def _kg(ent, kg, tile3, ns, K, pro=None):
+    """K groups of one launch: explicit ``kg``, else the tuned entry's, else 1 (3 = the
+    LDS-DMA ring, prologue-free launches only)."""
     if kg is None:
         kg = int(ent.get("kg", 1)) if ent else 1
+        if GLDS and pro == PRO_NONE and kg != 2:
+            kg = 3
+    if kg == 3:
+        return 3 if pro == PRO_NONE else 1
     bk = tile3[2]
     if not KGROUPS or kg != 2 or ns != 1 or tuple(tile3) not in KG_TILES or -(-K // bk) < 2:
         return 1
@@ -272,7 +285,7 @@ def conv_fwd(x, wf, shp: ConvShape, s=None, t=None, act=0, alpha=1.0, tile=None,
     if nsplit is not None:
         ent = {"nsplit": nsplit}
     ns, slab_p, cnt_p = _splitk_args(ent, M, shp.cout, shp.ntaps * C, bm, bn, bk, x.device)
-    kgv = _kg(ent, kg, (bm, bn, bk), ns, shp.ntaps * C)
+    kgv = _kg(ent, kg, (bm, bn, bk), ns, shp.ntaps * C, pro)
     _log("fwd", N, H, shp, ent, (bm, bn, bk), ns, kgv)
     y = torch.empty(N, Ho, Wo, shp.cout, device=x.device, dtype=torch.bfloat16)
     if part is None:
@@ -375,9 +388,9 @@ def conv_dgrad(g, y, al, be, wd, shp: ConvShape, x_shape, epi=EPI_STORE, out=Non
             continue
         bm, bn, bk = _tile3(tile, M, shp.cin)
         ns, slab_p, cnt_p = _splitk_args(ent, M, shp.cin, len(dh) * Cy, bm, bn, bk, g.device)
-        kgv = _kg(ent, kg, (bm, bn, bk), ns, len(dh) * Cy)
-        _log("dgrad", N, Hx, shp, ent, (bm, bn, bk), ns, kgv)
         pro = PRO_FOLD if al is not None else PRO_NONE  # al None: g is already folded
+        kgv = _kg(ent, kg, (bm, bn, bk), ns, len(dh) * Cy, pro)
+        _log("dgrad", N, Hx, shp, ent, (bm, bn, bk), ns, kgv)
         assert gs is None or pro == PRO_FOLD, "gs needs the fold prologue (al/be)"
         nat.conv_igemm(g.data_ptr(), _p(y) if pro == PRO_FOLD else 0, _p(al), _p(be), _p(gs), wd.data_ptr(),
                        out.data_ptr(), _p(part) if epi in (EPI_ACTBWD, EPI_JOINBWD) else 0,

@@ -1,0 +1,19 @@
+#!/usr/bin/env bash
+# Round 4, sixth call: kernel-time breakdown at the 8-GPU per-GPU share -- transformer at 32
+# samples (NGD) and ResNet-50 at 128 images (MADGRAD) -- at HEAD.
+set -o pipefail
+cd "$(dirname "$0")/.."
+export TMPDIR=/tmp
+OUT=gpurun_out/${1:-r4f}
+mkdir -p "$OUT"
+prof() {
+  local name=$1 steps=$2; shift 2
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/$name" -o run -- python bench.py "$@" > "$OUT/$name.log" 2>&1 || { echo "$name failed"; tail -20 "$OUT/$name.log"; exit 1; }
+  f=$(find "$OUT/$name" -name '*kernel_stats.csv' | head -n 1)
+  python scripts/kstats.py "$f" --steps "$steps" --top 45 > "$OUT/kstats_$name.txt"
+  head -1 "$OUT/kstats_$name.txt"; grep -h '"value"' "$OUT/$name.log" | grep -o '"ms_per_step": [0-9.]*'
+}
+prof tr_b32 40 --model transformer --global-batch 32 --steps 30 --warmup 10
+prof rn_b128 35 --global-batch 128 --steps 30 --warmup 5
+rm -rf "$OUT"/tr_b32/*/ 2>/dev/null; true
+echo done

@@ -6,10 +6,12 @@ bf16 MFMA peak -- rather than against the bytes the kernel happened to fetch (VE
 
     python scripts/roofline_layers.py --batch 1024 --md profiles/pmc/r4_bs1024_roofline.md
 
-Calls mirror the engine's: forward with the lazy-BN prologue (x*s+t, ReLU) and the statistics
-epilogue; dgrad with the BN-backward fold prologue (g + alpha + beta*y) and a plain store;
-wgrad with the fold on g and the lazy-BN transform on x.  Minimum bytes per op:
-  fwd   x + W + y            dgrad  g + y + W + dx          wgrad  g + y + x + dW (fp32)
+Calls mirror the engine's: 1x1 forward with the lazy-BN prologue (x*s+t, ReLU) and the
+statistics epilogue, dgrad with the BN-backward fold prologue (g + alpha + beta*y), wgrad with the
+fold on g and the lazy-BN transform on x; 3x3 convolutions read operands materialised once
+(FDT_MATERIALIZE_3X3: no prologue) and their dgrad runs through the producer's activation.
+Minimum bytes per op (1x1 / 3x3):
+  fwd   x + W + y            dgrad  g + y + W + dx / g + W + dx + ex     wgrad  g + y + x + dW / g + x + dW
 Bound = max(bytes / BW, FLOPs / PEAK) with BW = 6.3 TB/s (the streaming rate measured on this
 part, profiles/pmc/calibration.md) and PEAK = 2.5 PFLOP/s dense bf16.
 """
@@ -25,11 +27,32 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 import torch
 
-from bench_conv import SHAPES, timeit
+from bench_conv import SHAPES
 from faster_distributed_training_amd.ops import conv_igemm as ci
 
 BW = 6.3e12
 PEAK = 2.5e15
+
+
+def timeit(fn, reps=20):
+    """Device time per call: ``reps`` calls captured in one HIP graph and replayed, so small
+    launches are not timed at the Python wrapper's host rate (the engine replays graphs too)."""
+    for _ in range(3):
+        fn()
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        for _ in range(reps):
+            fn()
+    g.replay()
+    torch.cuda.synchronize()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(3):
+        g.replay()
+    e.record()
+    torch.cuda.synchronize()
+    return s.elapsed_time(e) / (3 * reps)
 
 
 def main():
@@ -61,11 +84,25 @@ def main():
         xb, yb = N * H * H * Cin * 2, M * Cout * 2
         wb = Cout * Cin * k * k * 2
         flops = 2.0 * M * Cout * Cin * k * k
-        ops = {"fwd": (lambda: ci.conv_fwd(x, wf, shp, sv, tv, 1, 1.0), xb + wb + yb)}
-        if Cin >= 8:
-            ops["dgrad"] = (lambda: ci.conv_dgrad(g, yy, al, be, wd, shp, (N, H, H, Cin)), 2 * yb + wb + xb)
         slab = torch.empty(64 * Cout * shp.ntaps * shp.cxp, device=dev)
-        ops["wgrad"] = (lambda: ci.conv_wgrad(g, yy, al, be, x, shp, gw, sv, tv, 1, slab=slab), 2 * yb + xb + 2 * wb)
+        if k > 1:
+            # the engine's 3x3 variants: input and gradient materialised once (FDT_MATERIALIZE_3X3),
+            # so the conv itself has no prologue; dgrad through the producer's activation
+            ex = torch.randn(N, H, H, Cin, device=dev).to(torch.bfloat16) if Cin >= 8 else None
+            es = torch.ones(Cin, device=dev)
+            et = torch.zeros(Cin, device=dev)
+            ops = {"fwd": (lambda: ci.conv_fwd(x, wf, shp), xb + wb + yb)}
+            if Cin >= 8:
+                ops["dgrad"] = (lambda: ci.conv_dgrad(g, None, None, None, wd, shp, (N, H, H, Cin), epi=ci.EPI_ACTBWD,
+                                                      ex=ex, es=es, et=et, act=1), yb + wb + 2 * xb)
+            ops["wgrad"] = (lambda: ci.conv_wgrad(g, None, None, None, x, shp, gw, slab=slab), yb + xb + 2 * wb)
+        else:
+            # 1x1: the lazy-BN prologue on the input, the BN-backward fold on the gradient
+            ops = {"fwd": (lambda: ci.conv_fwd(x, wf, shp, sv, tv, 1, 1.0), xb + wb + yb)}
+            if Cin >= 8:
+                ops["dgrad"] = (lambda: ci.conv_dgrad(g, yy, al, be, wd, shp, (N, H, H, Cin)), 2 * yb + wb + xb)
+            ops["wgrad"] = (lambda: ci.conv_wgrad(g, yy, al, be, x, shp, gw, sv, tv, 1, slab=slab),
+                            2 * yb + xb + 2 * wb)
         for op, (fn, nbytes) in ops.items():
             t = timeit(fn, a.reps) * 1e3  # us
             bound = max(nbytes / BW, flops / PEAK) * 1e6
@@ -90,7 +127,7 @@ def main():
     if a.md:
         with open(a.md, "w") as f:
             f.write(f"# Per-layer convolution roofline, batch {N} (scripts/roofline_layers.py)\n\n")
-            f.write("Measured: device time of the tuned launch (HIP events, random data, the engine's prologue / "
+            f.write("Measured: device time of the tuned launch (HIP-graph replay of 20 calls, random data, the engine's prologue / "
                     "epilogue variants).  Algorithmic minimum bytes: every operand read once, every result written "
                     f"once (bf16 activations / packed weights, fp32 dW).  Bound = max(bytes / {BW / 1e12:.1f} TB/s, "
                     f"FLOPs / {PEAK / 1e15:.1f} PFLOP/s).\n\n")

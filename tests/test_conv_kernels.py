@@ -409,3 +409,47 @@ def test_kgroups_match_reference(cuda, tile):
             assert rel(out, jref) < 1e-2, (tile, "join")
             assert rel(jout, joined) < 1e-2
 
+
+
+@pytest.mark.parametrize("tile", [(128, 128, 32), (64, 64, 32), (128, 64, 64), (64, 128, 64), (256, 64, 64),
+                                  (64, 64, 128)])
+@pytest.mark.parametrize("nsplit", [1, 2])
+def test_lds_dma_ring_matches_register_path(cuda, tile, nsplit):
+    """kg=3 (operand tiles staged global -> LDS by LDS-DMA into a 3-buffer ring) runs the same
+    MFMA sequence as the register-staged path: bitwise-equal forward / dgrad outputs for 3x3
+    (padding taps, strides) and 1x1 convolutions, split-K included, and both within bf16
+    tolerance of fp32 PyTorch."""
+    torch.manual_seed(11)
+    for (N, H, Cin, Cout, k, stride, pad) in [(2, 8, 64, 128, 3, 1, 1), (2, 9, 128, 256, 3, 2, 1),
+                                             (3, 5, 256, 128, 1, 1, 0), (2, 4, 512, 512, 3, 1, 1)]:
+        if Cout % tile[1]:
+            continue
+        shp = ci.ConvShape(Cin, Cout, k, stride, pad)
+        x = padc(make((N, H, H, Cin), cuda), shp.cxp)
+        w = torch.randn(Cout, Cin, k, k, device=cuda) / (Cin * k * k) ** 0.5
+        wf, wd = ci.alloc_packed(shp, cuda)
+        ci.pack_weights([(w, wf, wd, shp)])
+        ref = nhwc(F.conv2d(nchw(x.float()), w.to(BF).float(), stride=stride, padding=pad))
+        y1, p1 = ci.conv_fwd(x, wf, shp, tile=tile, nsplit=nsplit, kg=1)
+        y3, p3 = ci.conv_fwd(x, wf, shp, tile=tile, nsplit=nsplit, kg=3)
+        assert rel(y3, ref) < 1e-2, (tile, "fwd", rel(y3, ref))
+        assert torch.equal(y1, y3), (tile, "fwd bitwise", (y1.float() - y3.float()).abs().max().item())
+        assert torch.equal(p1, p3)
+        if Cin % tile[1]:
+            continue
+        Ho, Wo = ci.out_hw(H, H, shp)
+        g = make((N, Ho, Wo, Cout), cuda)
+        xs = (N, H, H, Cin)
+        dref = nhwc(torch.nn.grad.conv2d_input((N, Cin, H, H), w.to(BF).float(), nchw(g), stride=stride,
+                                               padding=pad))
+        d1, _ = ci.conv_dgrad(g, None, None, None, wd, shp, xs, epi=ci.EPI_STORE, tile=tile, nsplit=nsplit, kg=1)
+        d3, _ = ci.conv_dgrad(g, None, None, None, wd, shp, xs, epi=ci.EPI_STORE, tile=tile, nsplit=nsplit, kg=3)
+        assert rel(d3, dref) < 1e-2, (tile, "dgrad", rel(d3, dref))
+        assert torch.equal(d1, d3), (tile, "dgrad bitwise")
+        ex = make(xs, cuda)
+        es, et = torch.rand(Cin, device=cuda) + 0.5, torch.randn(Cin, device=cuda) * 0.3
+        a1, q1 = ci.conv_dgrad(g, None, None, None, wd, shp, xs, epi=ci.EPI_ACTBWD, ex=ex, es=es, et=et, act=1,
+                               tile=tile, nsplit=nsplit, kg=1)
+        a3, q3 = ci.conv_dgrad(g, None, None, None, wd, shp, xs, epi=ci.EPI_ACTBWD, ex=ex, es=es, et=et, act=1,
+                               tile=tile, nsplit=nsplit, kg=3)
+        assert torch.equal(a1, a3) and torch.equal(q1, q3), (tile, "actbwd bitwise")
