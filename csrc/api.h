@@ -138,6 +138,7 @@ void gelu_dropout_bwd_colsum(uint64_t g, uint64_t a, uint64_t ga, uint64_t gb, l
 void ngd_sumsq(uint64_t X, long per, int G, uint64_t out, uint64_t stream);
 bool ngd_small_supported(int D, int R);
 bool ngd_proj_supported(int D, int R);
+int ngd_mfma(int on);  // NGD projection on the matrix cores: set (on >= 0), returns the previous setting
 void ngd_proj(uint64_t X, uint64_t Y, uint64_t W, uint64_t Hbuf, int G, int A, int D, int B, int R, uint64_t ip,
               uint64_t fp, uint64_t J, uint64_t HH, uint64_t stream);
 long ngd_proj_hbuf_numel(int G, int A, int D, int B, int R, bool need_ip, bool need_j, bool need_hh);

@@ -506,7 +506,27 @@ struct ProjArgs {
   int tiles, ds, dlen;  // row tiles, d splits, d per split (multiple of kPD)
 };
 
-template <bool VEC>
+// MF: the chunk products run on the matrix cores (v_mfma_f32_16x16x4_f32: exact fp32, one
+// rounding per product, k-ordered -- the same fmaf chain in the same d / r / n order as the
+// VALU loops, so both forms give identical bits).  Operand map of 16x16x4: lane l supplies
+// A[l & 15][k = l >> 4] and B[k = l >> 4][l & 15]; C[4 (l >> 4) + v][l & 15] in register v.
+typedef float ngd_f32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ ngd_f32x4 mfma4(float a, float b, ngd_f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+
+// 1 = the matrix-core forms (default), 0 = the VALU loops (FDT_NGD_MFMA=0, A/B; ngd_mfma())
+static int g_ngd_mfma = -1;
+static bool ngd_mfma_on() {
+  if (g_ngd_mfma < 0) {
+    const char* e = getenv("FDT_NGD_MFMA");
+    g_ngd_mfma = (e && e[0] == '0') ? 0 : 1;
+  }
+  return g_ngd_mfma != 0;
+}
+
+template <bool VEC, bool MF>
 __global__ __launch_bounds__(256) void ngd_proj_h_kernel(ProjArgs p) {
   __shared__ __attribute__((aligned(16))) float Xs[kPN * kXs];
   __shared__ __attribute__((aligned(16))) float Ws[kPR * kWr];
@@ -528,6 +548,9 @@ __global__ __launch_bounds__(256) void ngd_proj_h_kernel(ProjArgs p) {
   for (int i = 0; i < 4; ++i)
 #pragma unroll
     for (int j = 0; j < 5; ++j) acc[i][j] = 0.f;
+  ngd_f32x4 hm[5];
+#pragma unroll
+  for (int t = 0; t < 5; ++t) hm[t] = ngd_f32x4{0.f, 0.f, 0.f, 0.f};
   float xv8[8], wv12[12];
   if (dbeg < dend) {
     proj_load_x<VEC>(xv8, x, n0, N, dend, D, p.B, dbeg, tid);
@@ -542,6 +565,16 @@ __global__ __launch_bounds__(256) void ngd_proj_h_kernel(ProjArgs p) {
       proj_load_w<VEC>(wv12, w, R, D, dend, d0 + kPD, tid);
     }
     __syncthreads();
+    if constexpr (MF) {
+      // wave w: rows 16w..16w+15 x the 5 rank tiles (5 independent accumulators)
+      const int lr = tid & 15, lk = (tid >> 4) & 3, w = tid >> 6;
+#pragma unroll
+      for (int kk = 0; kk < kPD / 4; ++kk) {
+        const float a = Xs[(16 * w + lr) * kXs + 4 * kk + lk];
+#pragma unroll
+        for (int t = 0; t < 5; ++t) hm[t] = mfma4(a, Ws[(16 * t + lr) * kWr + 4 * kk + lk], hm[t]);
+      }
+    } else {
 #pragma unroll 2
     for (int dq = 0; dq < kPD; dq += 4) {
       float4 xv[4], wv[5];
@@ -559,9 +592,24 @@ __global__ __launch_bounds__(256) void ngd_proj_h_kernel(ProjArgs p) {
           acc[i][j] = fmaf(xv[i].w, wv[j].w, acc[i][j]);
         }
     }
+    }
     __syncthreads();
   }
   float* h = p.H + g * N * R;
+  if constexpr (MF) {
+    const int lr = tid & 15, lk = (tid >> 4) & 3, w = tid >> 6;
+#pragma unroll
+    for (int t = 0; t < 5; ++t) {
+      const int r = 16 * t + lr;
+#pragma unroll
+      for (int v = 0; v < 4; ++v) {
+        const long n = n0 + 16 * w + 4 * lk + v;
+        if (n >= N || r >= R) continue;
+        if (p.ds == 1) h[n * R + r] = hm[t][v];
+        else p.H[((long)sp * (gridDim.x / per_g) + g) * N * R + n * R + r] = hm[t][v];
+      }
+    }
+  } else {
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const long n = n0 + 4 * tr + i;
@@ -574,6 +622,7 @@ __global__ __launch_bounds__(256) void ngd_proj_h_kernel(ProjArgs p) {
       else p.H[((long)sp * (gridDim.x / per_g) + g) * N * R + n * R + r] = acc[i][j];  // slab sp
     }
   }
+  }
   if (p.ipp != nullptr) {
     sx = block_sum256(sx, red);
     if (tid == 0) p.ipp[(long)g * per_g + rem] = sx;
@@ -585,7 +634,7 @@ __global__ __launch_bounds__(256) void ngd_proj_h_kernel(ProjArgs p) {
 // float4 feeds 32 FMAs (W reads are wave-uniform broadcasts); the [4 rows x 2 d] mapping
 // needed an LDS round trip and two extra barriers per chunk for the strided store and sat
 // at ~0.63 of its wave cycles waiting (profiles/pmc/ngd_proj_counters.md).
-template <bool VEC, bool STR>
+template <bool VEC, bool STR, bool MF>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void ngd_proj_y_kernel(ProjArgs p) {
   __shared__ __attribute__((aligned(16))) float Xs[kPN * kXs];
   __shared__ __attribute__((aligned(16))) float Ws[kPD * kWd];
@@ -648,7 +697,35 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void n
     }
     float yv[4][2];
     float ys[8];
-    if (STR) {
+    ngd_f32x4 ym[2];
+    const int lr = tid & 15, lk = (tid >> 4) & 3, wv_ = tid >> 6;
+    const int nk4 = (R + 3) >> 2;  // (H / W columns past R are zero)
+    if constexpr (MF) {
+      if constexpr (STR) {
+        // Y^T [d][n] = X^T - W^T H^T: C columns = rows n (lanes -> consecutive b: coalesced
+        // strided stores); wave w: n tile w, d tiles 0 and 1
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+          for (int v = 0; v < 4; ++v) ym[j][v] = Xs[(16 * wv_ + lr) * kXs + 16 * j + 4 * lk + v];
+        for (int kk = 0; kk < nk4; ++kk) {
+          const float hb = -Hs[(16 * wv_ + lr) * kWd + 4 * kk + lk];
+#pragma unroll
+          for (int j = 0; j < 2; ++j) ym[j] = mfma4(Ws[(16 * j + lr) * kWd + 4 * kk + lk], hb, ym[j]);
+        }
+      } else {
+        // Y [n][d] = X - H W: C columns = d; wave w: rows 16w.., d tiles 0 and 1
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+          for (int v = 0; v < 4; ++v) ym[j][v] = Xs[(16 * wv_ + 4 * lk + v) * kXs + 16 * j + lr];
+        for (int kk = 0; kk < nk4; ++kk) {
+          const float ha = -Hs[(16 * wv_ + lr) * kWd + 4 * kk + lk];
+#pragma unroll
+          for (int j = 0; j < 2; ++j) ym[j] = mfma4(ha, Ws[(16 * j + lr) * kWd + 4 * kk + lk], ym[j]);
+        }
+      }
+    } else if (STR) {
       const int row = tid & 63, dq = tid >> 6;
       const float4 a0 = *reinterpret_cast<const float4*>(Xs + row * kXs + 8 * dq);
       const float4 a1 = *reinterpret_cast<const float4*>(Xs + row * kXs + 8 * dq + 4);
@@ -693,7 +770,37 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void n
         }
     }
     }
-    if (p.Jp != nullptr) {  // J[r][d] += sum_n H[n][r] X[n][d]: thread d = tid & 31, r = (tid >> 5) + 8 j
+    if (MF && p.Jp != nullptr) {
+      // J[r][d] = sum_n H[n][r] X[n][d] over the tile's 64 rows: A = H^T (k = n), B = X;
+      // wave w: d tile w & 1, rank tiles (w >> 1) + 2 i (5 tiles over 2 wave pairs)
+      const int jd = wv_ & 1, t0 = wv_ >> 1;
+      ngd_f32x4 jm[3];
+#pragma unroll
+      for (int i = 0; i < 3; ++i) jm[i] = ngd_f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll 4
+      for (int kk = 0; kk < kPN / 4; ++kk) {
+        const int n = 4 * kk + lk;
+        const float xb = Xs[n * kXs + 16 * jd + lr];
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+          const int t = t0 + 2 * i;
+          if (t < 5) jm[i] = mfma4(Hs[n * kWd + 16 * t + lr], xb, jm[i]);
+        }
+      }
+      const int d = d0 + 16 * jd + lr;
+      if (d < dend) {
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+          const int t = t0 + 2 * i;
+          if (t >= 5) continue;
+#pragma unroll
+          for (int v = 0; v < 4; ++v) {
+            const int r = 16 * t + 4 * lk + v;
+            if (r < R) p.Jp[(((long)tile * (gridDim.x / per_g) + g) * R + r) * D + d] = jm[i][v];
+          }
+        }
+      }
+    } else if (p.Jp != nullptr) {  // J[r][d] += sum_n H[n][r] X[n][d]: thread d = tid & 31, r = (tid >> 5) + 8 j
       const int dd = tid & 31, d = d0 + dd;
       float ja[10];
 #pragma unroll
@@ -712,7 +819,46 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void n
         }
       }
     }
-    if (STR) {  // lanes = consecutive rows (b): one coalesced store per d
+    if (MF && STR) {  // C columns = rows n: lanes -> consecutive b
+      const long n = n0 + 16 * wv_ + lr;
+      if (n < N) {
+        const long a = n / p.B, b = n - a * p.B;
+        float* yr = y + a * (long)D * p.B + b;
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+          for (int v = 0; v < 4; ++v) {
+            const int d = d0 + 16 * j + 4 * lk + v;
+            if (d < dend) {
+              yr[(long)d * p.B] = ym[j][v];
+              sy = fmaf(ym[j][v], ym[j][v], sy);
+            }
+          }
+      }
+      __syncthreads();  // Xs / Ws reads done before the next chunk is staged
+    } else if (MF && VEC) {  // rows contiguous in d: 16 lanes = 64 contiguous bytes
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int v = 0; v < 4; ++v) {
+          const long n = n0 + 16 * wv_ + 4 * lk + v;
+          const int d = d0 + 16 * j + lr;
+          if (n < N && d < dend) {
+            y[n * D + d] = ym[j][v];
+            sy = fmaf(ym[j][v], ym[j][v], sy);
+          }
+        }
+      __syncthreads();
+    } else if (MF) {  // B = 1, unaligned: stage Y through Xs for the coalesced store
+      __syncthreads();
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int v = 0; v < 4; ++v) Xs[(16 * wv_ + 4 * lk + v) * kXs + 16 * j + lr] = ym[j][v];
+      __syncthreads();
+      proj_store_y(Xs, y, n0, N, dend, D, p.B, d0, tid, &sy);
+      __syncthreads();
+    } else if (STR) {  // lanes = consecutive rows (b): one coalesced store per d
       const int row = tid & 63, dq = tid >> 6;
       const long n = n0 + row;
       if (n < N) {
@@ -789,6 +935,12 @@ __global__ __launch_bounds__(256) void ngd_slab_sum_kernel(const float* __restri
 
 bool ngd_proj_supported(int D, int R) { return D >= 9 && R >= 1 && R <= kPR; }
 
+int ngd_mfma(int on) {
+  const int prev = ngd_mfma_on() ? 1 : 0;
+  if (on >= 0) g_ngd_mfma = on ? 1 : 0;
+  return prev;
+}
+
 static void proj_split(int G, long N, int D, int& tiles, int& ds, int& dlen) {
   tiles = (int)((N + kPN - 1) / kPN);
   const int chunks = (D + kPD - 1) / kPD;
@@ -862,17 +1014,31 @@ void ngd_proj(uint64_t X, uint64_t Y, uint64_t W, uint64_t Hbuf, int G, int A, i
   const long hn = (long)G * N * R;
   // float4 path: rows contiguous in d (the last axis) and 16-B aligned rows / matrices
   const bool vec = B == 1 && D % 4 == 0 && X % 16 == 0 && Y % 16 == 0 && W % 16 == 0;
-  if (vec) ngd_proj_h_kernel<true><<<(unsigned)grid, 256, 0, st>>>(p);
-  else ngd_proj_h_kernel<false><<<(unsigned)grid, 256, 0, st>>>(p);
+  const bool mf = ngd_mfma_on();
+  if (vec) {
+    if (mf) ngd_proj_h_kernel<true, true><<<(unsigned)grid, 256, 0, st>>>(p);
+    else ngd_proj_h_kernel<true, false><<<(unsigned)grid, 256, 0, st>>>(p);
+  } else {
+    if (mf) ngd_proj_h_kernel<false, true><<<(unsigned)grid, 256, 0, st>>>(p);
+    else ngd_proj_h_kernel<false, false><<<(unsigned)grid, 256, 0, st>>>(p);
+  }
   FDT_LAUNCH_CHECK();
   if (p.ds > 1) {
     ngd_slab_sum_kernel<<<slab_blocks(hn), 256, 0, st>>>(sc + L.hslab, sc + L.h, hn, p.ds, nullptr, nullptr, 0);
     FDT_LAUNCH_CHECK();
     p.H = sc + L.h;
   }
-  if (vec) ngd_proj_y_kernel<true, false><<<(unsigned)grid, 256, 0, st>>>(p);
-  else if (B > 1) ngd_proj_y_kernel<false, true><<<(unsigned)grid, 256, 0, st>>>(p);
-  else ngd_proj_y_kernel<false, false><<<(unsigned)grid, 256, 0, st>>>(p);
+#define FDT_PROJ_Y(V_, S_)                                                   \
+  if (mf) ngd_proj_y_kernel<V_, S_, true><<<(unsigned)grid, 256, 0, st>>>(p); \
+  else ngd_proj_y_kernel<V_, S_, false><<<(unsigned)grid, 256, 0, st>>>(p);
+  if (vec) {
+    FDT_PROJ_Y(true, false)
+  } else if (B > 1) {
+    FDT_PROJ_Y(false, true)
+  } else {
+    FDT_PROJ_Y(false, false)
+  }
+#undef FDT_PROJ_Y
   FDT_LAUNCH_CHECK();
   const int nwg = p.tiles * p.ds;
   ngd_proj_sums_kernel<<<ip ? 2 * G : G, 256, 0, st>>>(p.fpp, P<float>(fp), p.ipp, P<float>(ip), G, nwg);

@@ -7,11 +7,14 @@ showed the main stream idle for the whole ~1.4 ms of every eigensolve.  Times:
   [a] eigh alone, [b] main-stream sleep alone, [c] eigh on side + sleep on main launched
   right after, [d] the same with the host launching the sleep first.
 """
+import os
+import sys
 import time
 
-import torch
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch  # noqa: E402
 
-from faster_distributed_training_amd.ops import eigh as E
+from faster_distributed_training_amd.ops import eigh as E  # noqa: E402
 
 
 def ev():
@@ -34,6 +37,9 @@ def main():
     s.record(); torch.cuda._sleep(1 << 21); e.record(); torch.cuda.synchronize()
     t_sleep = s.elapsed_time(e)
     print(f"[a] eigh alone {t_eigh:.3f} ms   [b] sleep alone {t_sleep:.3f} ms", flush=True)
+    with torch.cuda.stream(side):  # (the first launch on a stream creates its queue: ~5 ms)
+        E.batched_eigh(Z)
+    torch.cuda.synchronize()
     for order in ("eigh_first", "sleep_first"):
         torch.cuda.synchronize()
         t0 = time.perf_counter()
@@ -57,6 +63,28 @@ def main():
         verdict = "CONCURRENT" if tot < 0.8 * (t_eigh + t_sleep) else "SERIALISED"
         print(f"[{order}] both {tot:.3f} ms (sum {t_eigh + t_sleep:.3f}) -> {verdict}; host launch "
               f"{(th - t0) * 1e3:.3f} ms, host total {host:.3f} ms", flush=True)
+    # the optimizer's pattern: main work, side waits on main, cat + eigh + small kernels on
+    # side, then small main-stream kernels (foreach copy) + a sleep: when does main finish?
+    xs = [torch.randn(512, 512, device=dev) for _ in range(40)]
+    ys = [torch.empty_like(t) for t in xs]
+    for _ in range(2):
+        torch.cuda.synchronize()
+        s.record()
+        torch.cuda._sleep(1 << 18)
+        side.wait_stream(torch.cuda.current_stream())
+        e_side = ev()
+        with torch.cuda.stream(side):
+            Zc = torch.cat([Z.reshape(-1)]).view_as(Z)
+            E.batched_eigh(Zc)
+            for t in xs[:8]:
+                t.mul_(1.0)
+            e_side.record(side)
+        torch._foreach_copy_(ys, xs)
+        torch.cuda._sleep(1 << 20)
+        e.record()
+        torch.cuda.synchronize()
+        print(f"[pattern] main done at {s.elapsed_time(e):.3f} ms, side done at {s.elapsed_time(e_side):.3f} ms "
+              f"-> main {'OVERLAPPED the eigh' if s.elapsed_time(e) < s.elapsed_time(e_side) else 'waited'}", flush=True)
     # a GEMM stream on main against the eigh on side
     a = torch.randn(4096, 4096, device=dev, dtype=torch.bfloat16)
     for _ in range(3):

@@ -621,6 +621,24 @@ def test_ngd_proj_kernel_vs_torch(cuda, D, R, A, B):
     torch.cuda.synchronize()
     assert torch.equal(Y3, Y) and torch.equal(ip3, ip) and torch.equal(fp3, fp)
     assert torch.equal(J3, J) and torch.equal(HH3, HH)
+    # the matrix-core form (default) against the VALU form: the same k-ordered fp32 fmaf
+    # chains (v_mfma_f32_16x16x4_f32 rounds once per product, in k order) -> identical bits
+    prev = nat.ngd_mfma(0)
+    try:
+        ip4, fp4 = torch.zeros(P, device=cuda), torch.zeros(P, device=cuda)
+        J4, HH4 = torch.zeros_like(J), torch.zeros_like(HH)
+        Y4 = torch.empty_like(X)
+        nat.ngd_proj(X.data_ptr(), Y4.data_ptr(), W.data_ptr(), Hb.data_ptr(), P, A, D, B, R, ip4.data_ptr(),
+                     fp4.data_ptr(), J4.data_ptr(), HH4.data_ptr(), sp)
+        torch.cuda.synchronize()
+    finally:
+        nat.ngd_mfma(prev)
+    assert prev == 1
+    assert torch.equal(Y4, Y), rel(Y4.double(), Y.double())
+    assert torch.equal(J4, J), rel(J4.double(), J.double())
+    assert torch.equal(ip4, ip) and torch.equal(HH4, HH)
+    # |Y|^2: the same Y, but each thread's partial sum covers other elements (C-fragment map)
+    assert rel(fp4.double(), fp.double()) < 1e-6
 
 
 def test_ngd_proj_axes_match_gemm_path(cuda, monkeypatch):
