@@ -35,6 +35,8 @@ constexpr int kEighMaxN = 128;
 constexpr int kEighMaxPairs = kEighMaxN / 2;
 // upper 2x2 blocks per thread: 64*65/2 = 2080 blocks / 1024 threads
 constexpr int kEighBlkPerThread = (kEighMaxPairs * (kEighMaxPairs + 1) / 2 + kEighThreads - 1) / kEighThreads;
+// V elements (row, pair) per thread: 128 x 64 / 1024
+constexpr int kEighVecPerThread = (kEighMaxN * kEighMaxPairs + kEighThreads - 1) / kEighThreads;
 
 __global__ __launch_bounds__(kEighThreads) void jacobi_eigh_kernel(const float* __restrict__ Ain,
                                                                    float* __restrict__ wout, float* __restrict__ Vout,
@@ -84,15 +86,29 @@ __global__ __launch_bounds__(kEighThreads) void jacobi_eigh_kernel(const float* 
     bk1[u] = b - k2 * (k2 + 1) / 2;
   }
   const int nvec = n * npairs;
+  // this thread's V elements (row i, pair slot k), decoded once: the per-round loop below is
+  // VALU-issue bound (16 waves per CU), so no integer division runs inside it
+  int vk[kEighVecPerThread], vrow[kEighVecPerThread];
+#pragma unroll
+  for (int u = 0; u < kEighVecPerThread; ++u) {
+    const int e = tid + u * kEighThreads;
+    const int k = e / n;
+    vk[u] = e < nvec ? k : -1;
+    vrow[u] = (e - k * n) * ld;
+  }
+  // A is kept in its UPPER triangle only (a 2x2 block update writes 4 entries, not 8)
+  auto at = [ld](int a, int b) { return a < b ? a * ld + b : b * ld + a; };
   __syncthreads();
 
   for (int sweep = 0; sweep < max_sweeps; ++sweep) {
     float o = 0.f, t = 0.f;
     for (int e = tid; e < n * n; e += kEighThreads) {
       const int i = e / n, j = e - (e / n) * n;
+      if (i > j) continue;
       const float v = A[i * ld + j];
-      t += v * v;
-      if (i != j) o += v * v;
+      const float v2 = i == j ? v * v : 2.f * v * v;
+      t += v2;
+      if (i != j) o += v2;
     }
     o = wave_sum(o);
     t = wave_sum(t);
@@ -108,8 +124,12 @@ __global__ __launch_bounds__(kEighThreads) void jacobi_eigh_kernel(const float* 
       // ---- 1. rotation per pair (tournament pairing: slot 0 fixed, slots 1..m-1 rotate)
       if (tid < npairs) {
         const int i = tid;
-        const int a = i == 0 ? 0 : 1 + (i - 1 + r) % (m - 1);
-        const int b = 1 + (m - 2 - i + r) % (m - 1);
+        // (i - 1 + r, m - 2 - i + r < 2 (m - 1): the modulo is one conditional subtract)
+        int ta = i - 1 + r, tb = m - 2 - i + r;
+        ta = ta >= m - 1 ? ta - (m - 1) : ta;
+        tb = tb >= m - 1 ? tb - (m - 1) : tb;
+        const int a = i == 0 ? 0 : 1 + ta;
+        const int b = 1 + tb;
         int p = a < b ? a : b, q = a < b ? b : a;
         float c = 1.f, s = 0.f, dp = 0.f, dq = 0.f;
         if (q < n) {
@@ -145,37 +165,41 @@ __global__ __launch_bounds__(kEighThreads) void jacobi_eigh_kernel(const float* 
             const float4 r1 = prm[k1];
             A[i1.x * ld + i1.x] = r1.z;
             A[i1.y * ld + i1.y] = r1.w;
-            A[i1.x * ld + i1.y] = 0.f;
-            A[i1.y * ld + i1.x] = 0.f;
+            A[i1.x * ld + i1.y] = 0.f;  // (p < q: the upper entry)
           }
           continue;
         }
         const float4 r1 = prm[k1], r2 = prm[k2];
         const bool h1 = i1.y >= 0, h2 = i2.y >= 0;
-        const float a00 = A[i1.x * ld + i2.x];
-        const float a01 = h2 ? A[i1.x * ld + i2.y] : 0.f;
-        const float a10 = h1 ? A[i1.y * ld + i2.x] : 0.f;
-        const float a11 = (h1 && h2) ? A[i1.y * ld + i2.y] : 0.f;
+        const int o00 = at(i1.x, i2.x);
+        const int o01 = h2 ? at(i1.x, i2.y) : 0, o10 = h1 ? at(i1.y, i2.x) : 0;
+        const int o11 = (h1 && h2) ? at(i1.y, i2.y) : 0;
+        const float a00 = A[o00];
+        const float a01 = h2 ? A[o01] : 0.f;
+        const float a10 = h1 ? A[o10] : 0.f;
+        const float a11 = (h1 && h2) ? A[o11] : 0.f;
         // rows (pair k1): row_p <- c row_p - s row_q, row_q <- s row_p + c row_q
         const float b00 = r1.x * a00 - r1.y * a10, b01 = r1.x * a01 - r1.y * a11;
         const float b10 = r1.y * a00 + r1.x * a10, b11 = r1.y * a01 + r1.x * a11;
         // columns (pair k2)
         const float n00 = r2.x * b00 - r2.y * b01, n01 = r2.y * b00 + r2.x * b01;
         const float n10 = r2.x * b10 - r2.y * b11, n11 = r2.y * b10 + r2.x * b11;
-        A[i1.x * ld + i2.x] = n00;
-        A[i2.x * ld + i1.x] = n00;
-        if (h2) { A[i1.x * ld + i2.y] = n01; A[i2.y * ld + i1.x] = n01; }
-        if (h1) { A[i1.y * ld + i2.x] = n10; A[i2.x * ld + i1.y] = n10; }
-        if (h1 && h2) { A[i1.y * ld + i2.y] = n11; A[i2.y * ld + i1.y] = n11; }
+        A[o00] = n00;
+        if (h2) A[o01] = n01;
+        if (h1) A[o10] = n10;
+        if (h1 && h2) A[o11] = n11;
       }
-      for (int e = tid; e < nvec; e += kEighThreads) {
-        const int k = e / n, i = e - k * n;
+#pragma unroll
+      for (int u = 0; u < kEighVecPerThread; ++u) {
+        const int k = vk[u];
+        if (k < 0) continue;
         const int2 pq = pidx[k];
         if (pq.y < 0) continue;
         const float4 rr = prm[k];
-        const float vip = V[i * ld + pq.x], viq = V[i * ld + pq.y];
-        V[i * ld + pq.x] = rr.x * vip - rr.y * viq;
-        V[i * ld + pq.y] = rr.y * vip + rr.x * viq;
+        float* vr = V + vrow[u];
+        const float vip = vr[pq.x], viq = vr[pq.y];
+        vr[pq.x] = rr.x * vip - rr.y * viq;
+        vr[pq.y] = rr.y * vip + rr.x * viq;
       }
       __syncthreads();
     }

@@ -75,10 +75,20 @@ __global__ __launch_bounds__(64 * kLnWaves) void layernorm_bwd_kernel(const TG* 
   const long r0 = (long)blockIdx.x * rows_per_blk;
   long r1 = r0 + rows_per_blk;
   if (r1 > rows) r1 = rows;
+  // the next row's dy / x are requested before this row's math (one row of loads in flight
+  // behind the compute: the loop was latency-bound at a few rows per wave)
+  float gn[E], xn[E];
+  if (r0 + w < r1) {
+    ln_load<E>(gy + (r0 + w) * d, d, lane, gn);
+    ln_load<E>(x + (r0 + w) * d, d, lane, xn);
+  }
   for (long row = r0 + w; row < r1; row += kLnWaves) {
     float gv[E], xv[E];
-    ln_load<E>(gy + row * d, d, lane, gv);
-    ln_load<E>(x + row * d, d, lane, xv);
+    _Pragma("unroll") for (int k = 0; k < E; ++k) { gv[k] = gn[k]; xv[k] = xn[k]; }
+    if (row + kLnWaves < r1) {
+      ln_load<E>(gy + (row + kLnWaves) * d, d, lane, gn);
+      ln_load<E>(x + (row + kLnWaves) * d, d, lane, xn);
+    }
     const float mean = mean_in[row], r = rstd_in[row];
     float s1 = 0.f, s2 = 0.f;
     _Pragma("unroll") for (int k = 0; k < E; ++k) {

@@ -71,7 +71,9 @@ class _LayerNormNative(torch.autograd.Function):
         if not gy2.is_contiguous():
             gy2 = gy2.contiguous()
         gx = torch.empty_like(x2)
-        nblk = max(1, min(512, (rows + 31) // 32))
+        # ~8-16 rows per 4-wave block: enough workgroups to fill the chip at 32 samples / GPU
+        # (4096 rows: 512 blocks; the old 32 rows per block left half the CUs idle)
+        nblk = max(1, min(2048, (rows + 7) // 8))
         part = torch.empty(2, nblk, d, device=x2.device, dtype=torch.float32)
         gres = None
         if ctx.res is not None and ctx.res.g is not None:
