@@ -1,0 +1,275 @@
+#!/usr/bin/env python3
+"""Re-tune the conv launch table (ops/conv_tuned.json) under the engine's own timing
+conditions: each candidate (tile, split-K, K groups) of the engine-variant call (the same
+calls as scripts/roofline_layers.py: 3x3 on materialised operands, 1x1 with the lazy-BN
+prologue / BN-backward fold) is captured 20x in a HIP graph and replayed.  The original
+tuner timed eager launch loops; under graph replay some entries are not the fastest (e.g.
+the 8x8 256->256 3x3 weight gradient at batch 1024: tuned 128x64x64 / 7 splits 129.7 us,
+128x128x64 / 14 splits 103.5 us).  An entry is replaced only when the new best beats the
+current entry, timed in the same session, by more than --margin.
+
+    python scripts/retune_graph.py --batches 1024 128 --ops wgrad
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch  # noqa: E402
+
+from bench_conv import SHAPES  # noqa: E402
+from faster_distributed_training_amd.ops import conv_igemm as ci  # noqa: E402
+from roofline_layers import timeit  # noqa: E402
+from tune_conv import FWD_TILES, WG_TILES  # noqa: E402
+
+WG_SPLITS = [1, 2, 4, 7, 8, 14, 16, 28, 32, 56, 64, 102, 128]
+FD_SPLITS = [1, 2, 4, 8]
+
+
+def engine_calls(N, H, shp, dev):
+    """op kind -> zero-arg call of the engine's variant (roofline_layers.py)."""
+    Cin, Cout, k = shp.cin, shp.cout, shp.k
+    torch.manual_seed(0)
+    x = torch.randn(N, H, H, shp.cxp, device=dev).to(torch.bfloat16)
+    w = torch.randn(Cout, Cin, k, k, device=dev) / (Cin * k * k) ** 0.5
+    wf, wd = ci.alloc_packed(shp, dev, dgrad=Cin >= 8)
+    ci.pack_weights([(w, wf, wd, shp)])
+    Ho, Wo = ci.out_hw(H, H, shp)
+    g = torch.randn(N, Ho, Wo, Cout, device=dev).to(torch.bfloat16)
+    yy = torch.randn(N, Ho, Wo, Cout, device=dev).to(torch.bfloat16)
+    al, be = torch.zeros(Cout, device=dev), torch.zeros(Cout, device=dev)
+    sv, tv = torch.ones(shp.cxp, device=dev), torch.zeros(shp.cxp, device=dev)
+    gw = torch.empty(Cout, Cin, k, k, device=dev)
+    slab = torch.empty(max(WG_SPLITS) * Cout * shp.ntaps * shp.cxp, device=dev)
+    keep = [x, w, wf, wd, g, yy, al, be, sv, tv, gw, slab]
+    if k > 1:
+        ex = torch.randn(N, H, H, Cin, device=dev).to(torch.bfloat16) if Cin >= 8 else None
+        es, et = torch.ones(Cin, device=dev), torch.zeros(Cin, device=dev)
+        keep += [ex, es, et]
+        ops = {"fwd": lambda: ci.conv_fwd(x, wf, shp)}
+        if Cin >= 8:
+            ops["dgrad"] = lambda: ci.conv_dgrad(g, None, None, None, wd, shp, (N, H, H, Cin), epi=ci.EPI_ACTBWD,
+                                                 ex=ex, es=es, et=et, act=1)
+        ops["wgrad"] = lambda: ci.conv_wgrad(g, None, None, None, x, shp, gw, slab=slab)
+    else:
+        ops = {"fwd": lambda: ci.conv_fwd(x, wf, shp, sv, tv, 1, 1.0)}
+        if Cin >= 8:
+            ops["dgrad"] = lambda: ci.conv_dgrad(g, yy, al, be, wd, shp, (N, H, H, Cin))
+        ops["wgrad"] = lambda: ci.conv_wgrad(g, yy, al, be, x, shp, gw, sv, tv, 1, slab=slab)
+    return ops, keep
+
+
+def variant_call(op_key, N, H, shp, dev):
+    """The engine's call for one tuned-table op key (scripts/engine_launch_keys.py lists the
+    keys one training step consults): fwd{pro}, dgrad{pro}{epi}, wgrad{fold}{xaff}."""
+    Cin, Cout, k = shp.cin, shp.cout, shp.k
+    torch.manual_seed(0)
+    x = torch.randn(N, H, H, shp.cxp, device=dev).to(torch.bfloat16)
+    w = torch.randn(Cout, Cin, k, k, device=dev) / (Cin * k * k) ** 0.5
+    wf, wd = ci.alloc_packed(shp, dev, dgrad=Cin >= 8)
+    ci.pack_weights([(w, wf, wd, shp)])
+    Ho, Wo = ci.out_hw(H, H, shp)
+    g = torch.randn(N, Ho, Wo, Cout, device=dev).to(torch.bfloat16)
+    yy = torch.randn(N, Ho, Wo, Cout, device=dev).to(torch.bfloat16)
+    al, be = torch.zeros(Cout, device=dev), torch.zeros(Cout, device=dev)
+    sv, tv = torch.ones(shp.cxp, device=dev), torch.zeros(shp.cxp, device=dev)
+    es, et = torch.ones(Cin, device=dev), torch.zeros(Cin, device=dev)
+    ex = torch.randn(N, H, H, Cin, device=dev).to(torch.bfloat16) if Cin >= 8 else None
+    gw = torch.empty(Cout, Cin, k, k, device=dev)
+    xs = (N, H, H, Cin)
+    keep = [x, w, wf, wd, g, yy, al, be, sv, tv, es, et, ex, gw]
+    if op_key == "fwd0":
+        return (lambda: ci.conv_fwd(x, wf, shp)), keep
+    if op_key == "fwd1":
+        return (lambda: ci.conv_fwd(x, wf, shp, sv, tv, 1, 1.0)), keep
+    if op_key == "fwd3":
+        r = torch.randn_like(x)
+        jout = torch.empty_like(x)
+        jmask = torch.zeros(x.numel() // 8, device=dev, dtype=torch.uint8)
+        keep += [r, jout, jmask]
+        return (lambda: ci.conv_fwd_join(x, r, sv, tv, None, None, wf, shp, jout, jmask)), keep
+    if op_key == "dgrad01":
+        return (lambda: ci.conv_dgrad(g, None, None, None, wd, shp, xs, epi=ci.EPI_ACTBWD, ex=ex, es=es, et=et,
+                                      act=1)), keep
+    if op_key == "dgrad21":
+        return (lambda: ci.conv_dgrad(g, yy, al, be, wd, shp, xs, epi=ci.EPI_ACTBWD, ex=ex, es=es, et=et,
+                                      act=1)), keep
+    if op_key == "dgrad22":
+        return (lambda: ci.conv_dgrad(g, yy, al, be, wd, shp, xs)), keep
+    slab = torch.empty(max(WG_SPLITS) * Cout * shp.ntaps * shp.cxp, device=dev)
+    keep.append(slab)
+    if op_key == "wgrad00":
+        return (lambda: ci.conv_wgrad(g, None, None, None, x, shp, gw, slab=slab)), keep
+    if op_key == "wgrad10":
+        return (lambda: ci.conv_wgrad(g, yy, al, be, x, shp, gw, slab=slab)), keep
+    if op_key == "wgrad11":
+        return (lambda: ci.conv_wgrad(g, yy, al, be, x, shp, gw, sv, tv, 1, slab=slab)), keep
+    return None, keep
+
+
+def lookup_key(fn, orig):
+    """The tuned-table op key the call consults first."""
+    seen = []
+
+    def spy(op, batch, h, shp):
+        seen.append(op)
+        return orig(op, batch, h, shp)
+    ci.tuned = spy
+    try:
+        fn()
+    finally:
+        ci.tuned = orig
+    torch.cuda.synchronize()
+    return seen[0] if seen else None
+
+
+def candidates(kind, shp, N, H):
+    Ho, Wo = ci.out_hw(H, H, shp)
+    M = N * Ho * Wo
+    out = []
+    if kind == "wgrad":
+        for t in WG_TILES:
+            if shp.cout % t[0]:
+                continue
+            for ns in WG_SPLITS:
+                if M // ns < 2 * t[2] or ns > M // 256:
+                    continue
+                out.append({"tile": list(t), "nsplit": ns})
+    else:
+        n_out = shp.cout if kind == "fwd" else shp.cin
+        for t in FWD_TILES:
+            if n_out % t[1]:
+                continue
+            for ns in FD_SPLITS:
+                out.append({"tile": list(t), "nsplit": ns})
+                if ns == 1 and tuple(t) in ci.KG_TILES:
+                    out.append({"tile": list(t), "nsplit": 1, "kg": 2})
+    return out
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--batches", type=int, nargs="+", default=[1024, 128])
+    ap.add_argument("--ops", default="wgrad")
+    ap.add_argument("--margin", type=float, default=0.03)
+    ap.add_argument("--reps", type=int, default=10)
+    ap.add_argument("--out", default=ci._TUNED_PATH)
+    ap.add_argument("--log", default=None)
+    ap.add_argument("--keys", nargs="*", default=None,
+                    help="engine_launch_keys.py outputs: tune exactly the (shape key, op key) pairs listed")
+    a = ap.parse_args()
+    dev = torch.device("cuda")
+    with open(ci._TUNED_PATH) as f:
+        table = json.load(f)
+    orig = ci.tuned
+    changes = []
+    t_start = time.time()
+    if a.keys:
+        jobs = []
+        for path in a.keys:
+            for line in open(path):
+                parts = line.split()
+                if len(parts) >= 3 and parts[0].count(":") == 6 and parts[2] in ("hit", "MISS"):
+                    jobs.append((parts[0], parts[1], int(parts[3][1:]) if len(parts) > 3 else 1))
+        for key, op_key, cnt in jobs:
+            N, H, Cin, Cout, k, s, p = map(int, key.split(":"))
+            kind = op_key.rstrip("0123456789")
+            if kind not in a.ops.split(","):
+                continue
+            shp = ci.ConvShape(Cin, Cout, k, s, p)
+            fn, keep = variant_call(op_key, N, H, shp, dev)
+            if fn is None:
+                continue
+            cur = table.get(key, {}).get(op_key)
+            ci._TUNED = None
+            timeit(fn, a.reps)
+            t_cur = timeit(fn, a.reps) * 1e3
+            best = (t_cur, None)
+            for cand in candidates(kind, shp, N, H):
+                ent = dict(cand)
+                if cur and "stages" in cur:
+                    ent["stages"] = cur["stages"]
+                ci.tuned = (lambda op, b, h, s_, e=ent, ok=op_key: e if op == ok else None)
+                try:
+                    us = timeit(fn, a.reps) * 1e3
+                except Exception as ex:  # noqa: BLE001
+                    print(f"  {key} {op_key} {cand}: {type(ex).__name__} {str(ex)[:60]}", flush=True)
+                    continue
+                finally:
+                    ci.tuned = orig
+                if us < best[0]:
+                    best = (us, ent)
+            t_cur = min(t_cur, timeit(fn, a.reps) * 1e3)
+            if best[1] is not None and cur is not None and all(
+                    best[1].get(f, d) == cur.get(f, d) for f, d in (("tile", None), ("nsplit", 1), ("kg", 1))):
+                best = (best[0], None)
+            msg = f"b{N} {key:22s} {op_key:8s} x{cnt}: current {cur} {t_cur:7.1f} us -> best {best[1]} {best[0]:7.1f} us"
+            if best[1] is not None and best[0] < (1 - a.margin) * t_cur:
+                ent = dict(best[1])
+                ent["us"] = round(best[0], 1)
+                table.setdefault(key, {})[op_key] = ent
+                changes.append((N, key, op_key, t_cur, best[0], cnt))
+                msg += "  REPLACED"
+            print(msg + f"   [{time.time() - t_start:.0f} s]", flush=True)
+            del keep
+            torch.cuda.empty_cache()
+        a.batches = sorted({c[0] for c in changes}, reverse=True) or a.batches
+    for N in ([] if a.keys else a.batches):
+        for (H, Cin, Cout, k, s, p, cnt) in SHAPES:
+            shp = ci.ConvShape(Cin, Cout, k, s, p)
+            ops, keep = engine_calls(N, H, shp, dev)
+            key = ci.tune_key(N, H, shp)
+            for kind, fn in ops.items():
+                if kind not in a.ops.split(","):
+                    continue
+                op_key = lookup_key(fn, orig)
+                cur = table.get(key, {}).get(op_key)
+                ci._TUNED = None
+                timeit(fn, a.reps)  # warm-up (first captures of a shape run slow)
+                t_cur = timeit(fn, a.reps) * 1e3  # the current table's choice (or the heuristic)
+                best = (t_cur, None)
+                for cand in candidates(kind, shp, N, H):
+                    ent = dict(cand)
+                    if cur and "stages" in cur:
+                        ent["stages"] = cur["stages"]
+                    ci.tuned = (lambda op, b, h, s_, e=ent, ok=op_key: e if op == ok else None)
+                    try:
+                        us = timeit(fn, a.reps) * 1e3
+                    except Exception as ex:  # noqa: BLE001
+                        print(f"  {key} {op_key} {cand}: {type(ex).__name__} {str(ex)[:60]}", flush=True)
+                        continue
+                    finally:
+                        ci.tuned = orig
+                    if us < best[0]:
+                        best = (us, ent)
+                # the current choice again, now warm: noise must not pass for a gain
+                t_cur = min(t_cur, timeit(fn, a.reps) * 1e3)
+                if best[1] is not None and cur is not None and all(
+                        best[1].get(f, d) == cur.get(f, d) for f, d in (("tile", None), ("nsplit", 1), ("kg", 1))):
+                    best = (best[0], None)  # the same configuration
+                msg = (f"b{N} {key:22s} {op_key:8s} x{cnt}: current {cur} {t_cur:7.1f} us -> best {best[1]} "
+                       f"{best[0]:7.1f} us")
+                if best[1] is not None and best[0] < (1 - a.margin) * t_cur:
+                    ent = dict(best[1])
+                    ent["us"] = round(best[0], 1)
+                    table.setdefault(key, {})[op_key] = ent
+                    changes.append((N, key, op_key, t_cur, best[0], cnt))
+                    msg += "  REPLACED"
+                print(msg + f"   [{time.time() - t_start:.0f} s]", flush=True)
+            del keep
+            torch.cuda.empty_cache()
+    with open(a.out, "w") as f:
+        json.dump(table, f, indent=1, sort_keys=True)
+    for N in a.batches:
+        gain = sum((t0 - t1) * c for (n, _, _, t0, t1, c) in changes if n == N)
+        print(f"batch {N}: {sum(1 for c in changes if c[0] == N)} entries replaced, "
+              f"~{gain / 1e3:.3f} ms per step saved (layer counts)", flush=True)
+
+
+if __name__ == "__main__":
+    main()

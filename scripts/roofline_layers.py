@@ -61,10 +61,15 @@ def main():
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--md", default=None)
     ap.add_argument("--json", default=None)
+    ap.add_argument("--keys", default=None,
+                    help="engine_launch_keys.py output for this batch: time exactly the (shape, variant) calls "
+                         "one engine step makes, weighted by their counts (instead of one variant per shape)")
     a = ap.parse_args()
     dev = torch.device("cuda")
     N = a.batch
     rows = []
+    if a.keys:
+        return keyed(a, dev)
     for (H, Cin, Cout, k, s, p, cnt) in SHAPES:
         shp = ci.ConvShape(Cin, Cout, k, s, p)
         torch.manual_seed(0)
@@ -137,6 +142,79 @@ def main():
                 f.write(f"| {r['shape']} | {r['count']} | {r['op']} | {r['us']:.1f} | {r['min_mb']:.1f} | "
                         f"{r['gflop']:.2f} | {r['bound_us']:.1f} | {r['limiter']} | {r['pct']:.1f} |\n")
             f.write(f"\nNetwork convolutions (weighted by layer count): **{tot / 1e3:.3f} ms measured vs "
+                    f"{totb / 1e3:.3f} ms algorithmic bound ({100 * totb / tot:.1f} %)**; by op: " +
+                    ", ".join(f"{k} {v[0] / 1e3:.3f} / {v[1] / 1e3:.3f} ms ({100 * v[1] / v[0]:.0f} %)"
+                              for k, v in byop.items()) + ".\n")
+
+
+def min_bytes(op_key, N, H, shp):
+    Ho, Wo = ci.out_hw(H, H, shp)
+    M = N * Ho * Wo
+    xb, yb = N * H * H * shp.cin * 2, M * shp.cout * 2
+    wb = shp.cout * shp.cin * shp.k * shp.k * 2
+    return {"fwd0": xb + wb + yb, "fwd1": xb + wb + yb, "fwd3": 3 * xb + wb + yb,
+            "dgrad01": yb + wb + 2 * xb, "dgrad21": 2 * yb + wb + 2 * xb, "dgrad22": 2 * yb + wb + xb,
+            "wgrad00": yb + xb + 2 * wb, "wgrad10": 2 * yb + xb + 2 * wb, "wgrad11": 2 * yb + xb + 2 * wb}[op_key]
+
+
+def keyed(a, dev):
+    from retune_graph import variant_call
+    rows = []
+    for line in open(a.keys):
+        parts = line.split()
+        if not (len(parts) >= 4 and parts[0].count(":") == 6 and parts[2] in ("hit", "MISS")):
+            continue
+        key, op_key, cnt = parts[0], parts[1], int(parts[3][1:])
+        N, H, Cin, Cout, k, s, p = map(int, key.split(":"))
+        if N != a.batch:
+            continue
+        shp = ci.ConvShape(Cin, Cout, k, s, p)
+        fn, keep = variant_call(op_key, N, H, shp, dev)
+        if fn is None:
+            continue
+        Ho, Wo = ci.out_hw(H, H, shp)
+        flops = 2.0 * N * Ho * Wo * Cout * Cin * k * k
+        nbytes = min_bytes(op_key, N, H, shp)
+        t = timeit(fn, a.reps) * 1e3
+        bound = max(nbytes / BW, flops / PEAK) * 1e6
+        rows.append(dict(shape=f"{H}x{H} {Cin}->{Cout} k{k} s{s}", count=cnt, op=op_key, us=t, min_mb=nbytes / 1e6,
+                         gflop=flops / 1e9, bound_us=bound, pct=100.0 * bound / t,
+                         limiter="bytes" if nbytes / BW > flops / PEAK else "mfma"))
+        r = rows[-1]
+        print(f"{r['shape']:26s} x{cnt} {op_key:8s} {t:8.1f} us  bound {bound:7.1f} us ({r['limiter']})  {r['pct']:5.1f} %",
+              flush=True)
+        del keep
+    report(a, rows)
+
+
+def report(a, rows):
+    tot = sum(r["us"] * r["count"] for r in rows)
+    totb = sum(r["bound_us"] * r["count"] for r in rows)
+    byop = {}
+    for r in rows:
+        o = byop.setdefault(r["op"].rstrip("0123456789"), [0.0, 0.0])
+        o[0] += r["us"] * r["count"]
+        o[1] += r["bound_us"] * r["count"]
+    print(f"network convolutions: {tot / 1e3:.3f} ms measured vs {totb / 1e3:.3f} ms algorithmic bound "
+          f"({100 * totb / tot:.1f} %); " + ", ".join(f"{k} {v[0] / 1e3:.3f} / {v[1] / 1e3:.3f} ms" for k, v in byop.items()))
+    if a.json:
+        with open(a.json, "w") as f:
+            json.dump(dict(batch=a.batch, rows=rows), f, indent=1)
+    if a.md:
+        with open(a.md, "w") as f:
+            f.write(f"# Per-layer convolution roofline, batch {a.batch} (scripts/roofline_layers.py --keys)\n\n")
+            f.write("Measured: device time of the tuned launch of exactly the calls one engine training step makes "
+                    "(variant = tuned-table op key: fwd{prologue}, dgrad{prologue}{epilogue}, wgrad{fold}{input "
+                    "transform}; counts from scripts/engine_launch_keys.py), HIP-graph replay of 20 calls, random "
+                    "data.  Algorithmic minimum bytes: every operand read once, every result written once (bf16 "
+                    f"activations / packed weights, fp32 dW).  Bound = max(bytes / {BW / 1e12:.1f} TB/s, FLOPs / "
+                    f"{PEAK / 1e15:.1f} PFLOP/s).\n\n")
+            f.write("| layer | count | variant | measured us | min MB | GFLOP | bound us | limiter | % of bound |\n")
+            f.write("|---|---:|---|---:|---:|---:|---:|---|---:|\n")
+            for r in rows:
+                f.write(f"| {r['shape']} | {r['count']} | {r['op']} | {r['us']:.1f} | {r['min_mb']:.1f} | "
+                        f"{r['gflop']:.2f} | {r['bound_us']:.1f} | {r['limiter']} | {r['pct']:.1f} |\n")
+            f.write(f"\nNetwork convolutions (weighted by call count): **{tot / 1e3:.3f} ms measured vs "
                     f"{totb / 1e3:.3f} ms algorithmic bound ({100 * totb / tot:.1f} %)**; by op: " +
                     ", ".join(f"{k} {v[0] / 1e3:.3f} / {v[1] / 1e3:.3f} ms ({100 * v[1] / v[0]:.0f} %)"
                               for k, v in byop.items()) + ".\n")
