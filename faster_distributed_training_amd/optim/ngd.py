@@ -62,6 +62,8 @@ DEFER = os.environ.get("FDT_NGD_DEFER", "1") != "0"
 # measured on MI355X (profiles/r3/ngd_graphs.txt) a replay is no faster than the eager step
 # (ResNet-50 NGD+meta 30.4 vs 30.2-30.7 ms, transformer bs256 11.5 vs 11.4-12.2 ms) and slower
 # at batch 32 (5.39 vs 5.04 ms): the step is GPU-bound, not launch-bound.  FDT_NGD_GRAPHS=1
+# forces it on everywhere; the ResNet trainer turns it on for the sharded path, where a rank
+# preconditions 1/world of the parameters and the step IS launch-bound (train/resnet_trainer.py)
 GRAPHS = os.environ.get("FDT_NGD_GRAPHS", "0") == "1"
 # the R x R products of an update step (K = J J^T, L = J W^T, W <- A (J + wc W)) on the
 # hand-written ngd.hip kernels (ngd_gram / ngd_wupdate) instead of batched library GEMMs
