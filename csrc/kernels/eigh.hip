@@ -1,19 +1,22 @@
 // Batched symmetric eigendecomposition for the NGD preconditioner (gfx950 / CDNA4).
 //
 // NGD (reference ngd_optimizer.py:265) needs eigh of many small symmetric R x R matrices
-// (R <= 80 by default) on every Fisher-update step; the reference calls LAPACK/cuSOLVER
+// (R <= 80 by default); the reference calls LAPACK/cuSOLVER
 // once per (parameter, axis) with a host round-trip each.  Here one 1024-thread workgroup
-// owns one matrix: A and the eigenvector accumulator V live in LDS ([n][n+1] fp32, odd
-// stride against bank conflicts, 2 x 80 x 81 x 4 B = 52 KB at R = 80), and cyclic
-// two-sided Jacobi runs with the round-robin (tournament) ordering -- every round rotates
-// n/2 disjoint (p,q) pairs at once.
+// owns one matrix: A ([n][n+1] fp32, odd stride against bank conflicts, upper triangle only)
+// and the TRANSPOSED eigenvector accumulator Vt ([n][n+4], 16-B rows: a column rotation of V
+// is a float4 rotation of two Vt rows) live in LDS (~52 KB at R = 80), and cyclic two-sided
+// Jacobi runs with the round-robin (tournament) ordering -- every round rotates n/2 disjoint
+// (p,q) pairs at once.  1024 threads measured fastest (1024 / 512 / 256: 0.92 / 1.16 / 2.00
+// ms on the transformer's 147 80x80 matrices, profiles/r4/eigh_threads_*.txt): a round is
+// LDS / VALU throughput bound, not latency bound.
 //
 // Round structure (two barriers):
 //   1. one lane per pair computes (c, s) and the closed-form new diagonal entries;
 //   2. A <- J^T A J as independent 2x2 blocks: the pairs partition the indices, so every
 //      element belongs to exactly one (pair k1, pair k2) block and each block's update
-//      needs only its own four entries.  Only upper blocks (k1 <= k2) are computed; the
-//      result is written to both (k1,k2) and (k2,k1), keeping A exactly symmetric.  The
+//      needs only its own four entries.  Only upper blocks (k1 <= k2) are computed, and only
+//      the upper-triangle entries are stored.  The
 //      diagonal block of a rotated pair is written in closed form (a_pq <- 0 exactly, a_pp
 //      and a_qq from t) -- without exact annihilation, fp32 rounding residue in a_pq stalls
 //      convergence at ~1e-4 relative.  V <- V J runs in the same phase.
@@ -30,18 +33,25 @@
 
 namespace fdt {
 
-constexpr int kEighThreads = 1024;
+constexpr int kEighThreadsMax = 1024;
 constexpr int kEighMaxN = 128;
 constexpr int kEighMaxPairs = kEighMaxN / 2;
 // upper 2x2 blocks per thread: 64*65/2 = 2080 blocks / 1024 threads
-constexpr int kEighBlkPerThread = (kEighMaxPairs * (kEighMaxPairs + 1) / 2 + kEighThreads - 1) / kEighThreads;
-// V elements (row, pair) per thread: 128 x 64 / 1024
-constexpr int kEighVecPerThread = (kEighMaxN * kEighMaxPairs + kEighThreads - 1) / kEighThreads;
+template <int NT>
+constexpr int eigh_blk_per_thread() { return (kEighMaxPairs * (kEighMaxPairs + 1) / 2 + NT - 1) / NT; }
+// V tasks (pair, 4-row chunk) per thread: 64 x 32 / 1024
+template <int NT>
+constexpr int eigh_vt_per_thread() { return (kEighMaxPairs * (kEighMaxN / 4) + NT - 1) / NT; }
+// Vt row stride: float4 rows, +4 floats so consecutive rows start on other banks
+__host__ __device__ constexpr int eigh_ldv(int n) { return ((n + 3) & ~3) + 4; }
 
+template <int kEighThreads>
 __global__ __launch_bounds__(kEighThreads) void jacobi_eigh_kernel(const float* __restrict__ Ain,
                                                                    float* __restrict__ wout, float* __restrict__ Vout,
                                                                    const int* __restrict__ table, int n_uniform,
                                                                    int max_sweeps, float tol) {
+  constexpr int kEighBlkPerThread = eigh_blk_per_thread<kEighThreads>();
+  constexpr int kEighVtPerThread = eigh_vt_per_thread<kEighThreads>();
   extern __shared__ __attribute__((aligned(16))) float sm[];
   const long mat = blockIdx.x;
   int n = n_uniform;
@@ -57,7 +67,11 @@ __global__ __launch_bounds__(kEighThreads) void jacobi_eigh_kernel(const float* 
   float* red = reinterpret_cast<float*>(pidx + kEighMaxPairs);      // [32]
   int* rank = reinterpret_cast<int*>(red + 32);                     // [128]
   float* A = reinterpret_cast<float*>(rank + kEighMaxN);            // [n][ld]
-  float* V = A + n * ld;                                            // [n][ld]
+  // the eigenvector accumulator TRANSPOSED: Vt[j][i] = V[i][j], so V <- V J (a rotation of
+  // columns p, q of V) is a rotation of two contiguous rows -- float4 LDS reads / writes, one
+  // (pair, 4-row chunk) task per thread instead of four scalar (row, pair) elements
+  const int ldv = eigh_ldv(n);
+  float* Vt = A + ((n * ld + 3) & ~3);                              // [n][ldv], 16-B rows
   const int tid = threadIdx.x;
   const int lane = tid & 63, wid = tid >> 6;
   const float* src = Ain + offA;
@@ -67,7 +81,10 @@ __global__ __launch_bounds__(kEighThreads) void jacobi_eigh_kernel(const float* 
     // symmetrise from the upper triangle (torch UPLO='U' convention)
     const float v = i <= j ? src[(long)i * n + j] : src[(long)j * n + i];
     A[i * ld + j] = v;
-    V[i * ld + j] = (i == j) ? 1.f : 0.f;
+  }
+  for (int e = tid; e < n * ldv; e += kEighThreads) {
+    const int j = e / ldv, i = e - j * ldv;
+    Vt[e] = (i == j) ? 1.f : 0.f;  // (padding columns i >= n stay finite: never output)
   }
 
   const int m = (n + 1) & ~1;  // players (a dummy when n is odd)
@@ -85,16 +102,16 @@ __global__ __launch_bounds__(kEighThreads) void jacobi_eigh_kernel(const float* 
     bk2[u] = b < nblk ? k2 : -1;
     bk1[u] = b - k2 * (k2 + 1) / 2;
   }
-  const int nvec = n * npairs;
-  // this thread's V elements (row i, pair slot k), decoded once: the per-round loop below is
-  // VALU-issue bound (16 waves per CU), so no integer division runs inside it
-  int vk[kEighVecPerThread], vrow[kEighVecPerThread];
+  // this thread's V tasks (pair slot k, 4-element chunk c of the two Vt rows), decoded once:
+  // no integer division inside the round loop
+  const int nch = (n + 3) >> 2, ntask = npairs * nch;
+  int vk[kEighVtPerThread], vc[kEighVtPerThread];
 #pragma unroll
-  for (int u = 0; u < kEighVecPerThread; ++u) {
-    const int e = tid + u * kEighThreads;
-    const int k = e / n;
-    vk[u] = e < nvec ? k : -1;
-    vrow[u] = (e - k * n) * ld;
+  for (int u = 0; u < kEighVtPerThread; ++u) {
+    const int t = tid + u * kEighThreads;
+    const int k = t / nch;
+    vk[u] = t < ntask ? k : -1;
+    vc[u] = (t - k * nch) * 4;
   }
   // A is kept in its UPPER triangle only (a 2x2 block update writes 4 entries, not 8)
   auto at = [ld](int a, int b) { return a < b ? a * ld + b : b * ld + a; };
@@ -190,16 +207,19 @@ __global__ __launch_bounds__(kEighThreads) void jacobi_eigh_kernel(const float* 
         if (h1 && h2) A[o11] = n11;
       }
 #pragma unroll
-      for (int u = 0; u < kEighVecPerThread; ++u) {
+      for (int u = 0; u < kEighVtPerThread; ++u) {
         const int k = vk[u];
         if (k < 0) continue;
         const int2 pq = pidx[k];
         if (pq.y < 0) continue;
         const float4 rr = prm[k];
-        float* vr = V + vrow[u];
-        const float vip = vr[pq.x], viq = vr[pq.y];
-        vr[pq.x] = rr.x * vip - rr.y * viq;
-        vr[pq.y] = rr.y * vip + rr.x * viq;
+        float4* vp = reinterpret_cast<float4*>(Vt + pq.x * ldv + vc[u]);
+        float4* vq = reinterpret_cast<float4*>(Vt + pq.y * ldv + vc[u]);
+        const float4 a = *vp, b = *vq;
+        *vp = make_float4(rr.x * a.x - rr.y * b.x, rr.x * a.y - rr.y * b.y, rr.x * a.z - rr.y * b.z,
+                          rr.x * a.w - rr.y * b.w);
+        *vq = make_float4(rr.y * a.x + rr.x * b.x, rr.y * a.y + rr.x * b.y, rr.y * a.z + rr.x * b.z,
+                          rr.y * a.w + rr.x * b.w);
       }
       __syncthreads();
     }
@@ -221,7 +241,7 @@ __global__ __launch_bounds__(kEighThreads) void jacobi_eigh_kernel(const float* 
   __syncthreads();
   for (int e = tid; e < n * n; e += kEighThreads) {
     const int i = e / n, j = e - (e / n) * n;
-    vo[(long)i * n + rank[j]] = V[i * ld + j];
+    vo[(long)i * n + rank[j]] = Vt[j * ldv + i];
   }
 }
 
@@ -230,15 +250,28 @@ void jacobi_eigh(uint64_t A, uint64_t w, uint64_t V, uint64_t table, int batch, 
   // n: the uniform size, or (with a table) the largest n in the table (sizes the LDS)
   FDT_CHECK(n >= 1 && n <= kEighMaxN, "jacobi_eigh: n must be in [1, 128]");
   if (batch == 0) return;
-  const size_t lds = (size_t)2 * n * (n + 1) * 4 + kEighMaxPairs * (16 + 8) + 32 * 4 + kEighMaxN * 4;
-  static size_t set = 64 * 1024;
-  if (lds > set) {
-    FDT_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(jacobi_eigh_kernel),
-                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-    set = lds;
-  }
-  hipLaunchKernelGGL(jacobi_eigh_kernel, dim3(batch), dim3(kEighThreads), lds, as_stream(stream), P<const float>(A),
-                     P<float>(w), P<float>(V), P<const int>(table), n, max_sweeps, tol);
+  const size_t lds = (size_t)((n * (n + 1) + 3) & ~3) * 4 + (size_t)n * eigh_ldv(n) * 4 + kEighMaxPairs * (16 + 8) +
+                     32 * 4 + kEighMaxN * 4;
+  // workgroup size: 1024 threads (16 waves) by default; FDT_EIGH_THREADS = 512 / 256 (A/B)
+  static const int nt = [] {
+    const char* e = getenv("FDT_EIGH_THREADS");
+    const int v = e ? atoi(e) : 1024;
+    return (v == 256 || v == 512) ? v : 1024;
+  }();
+  auto go = [&](auto kern, int threads) {
+    static size_t set[3] = {64 * 1024, 64 * 1024, 64 * 1024};
+    size_t& s_ = set[threads == 1024 ? 0 : (threads == 512 ? 1 : 2)];
+    if (lds > s_) {
+      FDT_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                        (int)lds));
+      s_ = lds;
+    }
+    hipLaunchKernelGGL(kern, dim3(batch), dim3(threads), lds, as_stream(stream), P<const float>(A), P<float>(w),
+                       P<float>(V), P<const int>(table), n, max_sweeps, tol);
+  };
+  if (nt == 256) go(jacobi_eigh_kernel<256>, 256);
+  else if (nt == 512) go(jacobi_eigh_kernel<512>, 512);
+  else go(jacobi_eigh_kernel<1024>, 1024);
   FDT_LAUNCH_CHECK();
 }
 
