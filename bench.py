@@ -44,6 +44,9 @@ def parse():
     ap.add_argument("--fsdp", action="store_true")
     ap.add_argument("--fsdp-param-dtype", default="bf16", choices=["bf16", "fp32"],
                     help="--fsdp: parameter all-gather wire / compute-copy precision (masters stay fp32)")
+    ap.add_argument("--fsdp-wrap", default="model", choices=["sublayer", "model"],
+                    help="--model transformer --fsdp: wrap units (sublayers, or the whole model as one unit "
+                         "like the reference's FSDP(model))")
     ap.add_argument("--fsdp-schedule", default="full_shard", choices=["full_shard", "shard_grad_op"],
                     help="--fsdp: FULL_SHARD (reshard after forward, re-gather in backward) or SHARD_GRAD_OP")
     ap.add_argument("--sharded-ngd", action="store_true",
@@ -220,6 +223,7 @@ def _sharding_fields(tr, rec):
             cfg["graph_comm"] = graphs.DETACHED_MODE
     if tr.fsdp is not None:
         cfg["fsdp_units"] = len(tr.fsdp.units)
+        cfg["fsdp_wrap"] = "model" if len(tr.fsdp.units) == 1 and tr.fsdp.units[0].name == "" else "per-unit"
         cfg["fsdp_peak_full_bytes"] = int(tr.fsdp.peak_full_bytes)
         cfg["fsdp_shard_numel"] = int(tr.fsdp.space.numel)
         cfg["fsdp_static_graphs"] = bool(tr.fsdp.static)
@@ -252,7 +256,7 @@ def bench_transformer(args):
     cfg = TransformerConfig(batch_size=gb // world, synthetic=True, eval=False, plot=False, distributed=world > 1,
                             ngd=True, precision=args.precision, length_buckets=buckets,
                             bucket_mb=args.bucket_mb, fsdp=args.fsdp, epoch=1, fsdp_param_dtype=args.fsdp_param_dtype,
-                            fsdp_schedule=args.fsdp_schedule)
+                            fsdp_schedule=args.fsdp_schedule, fsdp_wrap=args.fsdp_wrap)
     tr = TransformerTrainer(cfg)
     longest = int(tr.train_loader.store.lengths.max())
     assert longest <= buckets[-1], f"largest bucket {buckets[-1]} would truncate samples of length {longest}"

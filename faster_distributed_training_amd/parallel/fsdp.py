@@ -345,7 +345,9 @@ class FullyShardedDP:
 
     def __init__(self, model: nn.Module, device=None, units=None, mode="flat", offload=False, process_group=None,
                  prefetch=True, engine_units=(), static=False, param_dtype=None, reshard_after_forward=True):
-        """units: [(name, module)] (None: ``default_units``); mode: 'flat' | 'param' (NGD);
+        """units: [(name, module)] (None: ``default_units``; ``[("", model)]``: the whole model
+        as one unit, the reference's ``FSDP(model)`` without an auto-wrap policy); mode: 'flat' |
+        'param' (NGD);
         engine_units: names of units whose forward/backward an engine drives explicitly
         (no module hooks installed on them); static: fixed-address buffers, HIP-graph capture
         (see the module docstring); reshard_after_forward (static mode): FULL_SHARD on a
@@ -378,11 +380,11 @@ class FullyShardedDP:
         for ui, (name, mod) in enumerate(unit_list):
             for pn, p in mod.named_parameters():
                 if p.requires_grad and id(p) not in owner and len(seen[id(p)]) == 1:
-                    owner[id(p)] = (ui, f"{name}.{pn}")
+                    owner[id(p)] = (ui, f"{name}.{pn}" if name else pn)
         root_params = [(n, p) for n, p in model.named_parameters() if p.requires_grad and id(p) not in owner]
         self.units = []
         for ui, (name, mod) in enumerate(unit_list):
-            ps = [(f"{name}.{pn}", p) for pn, p in mod.named_parameters() if p.requires_grad
+            ps = [(f"{name}.{pn}" if name else pn, p) for pn, p in mod.named_parameters() if p.requires_grad
                   and owner.get(id(p), (None,))[0] == ui]
             if ps:
                 self.units.append(Unit(self, len(self.units), name, ps, mode))

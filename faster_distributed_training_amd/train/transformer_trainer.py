@@ -63,6 +63,13 @@ class TransformerConfig:
     fsdp_offload: bool = False       # FSDP shards + optimizer state in pinned host memory (reference CPUOffload)
     fsdp_param_dtype: str = "fp32"   # fp32 | bf16: all-gather wire / compute copy of the parameters
     fsdp_schedule: str = "full_shard"  # full_shard | shard_grad_op (the HIP-graph path's static FSDP)
+    # FSDP wrap units: "model" = the whole model as ONE unit, as the reference wraps it
+    # (transformer_test.py:387-392 FSDP(model), no auto-wrap policy): one gather + one
+    # reduce-scatter per step -- 12.5 ms/step at batch 256 on one GPU; "sublayer" = embedding /
+    # each attention and FFN sublayer / pooler / classifier (gathers prefetched behind compute,
+    # ~45 collective actions per step between graph segments, host-bound: 13.8 ms;
+    # profiles/r4/tr_fsdp_wrap_*.json)
+    fsdp_wrap: str = "model"
     shard_ngd: bool = True           # distributed NGD: each rank owns + preconditions 1/world of the params
     bucket_mb: float = 25.0           # measured faster than 8 MB (profiles/r3s3/ddp_world1_*.json)
     resume: bool = False
@@ -122,7 +129,10 @@ class TransformerTrainer:
             # graphs: each unit's gather / prefetch and reduce-scatter become actions between
             # graph segments (parallel/graphs.SegmentedStep)
             static = bool(self._graphs_wanted() and not cfg.fsdp_offload and cfg.extra.get("fsdp_static", True))
+            if cfg.fsdp_wrap not in ("sublayer", "model"):
+                raise ValueError(f"fsdp_wrap {cfg.fsdp_wrap!r}")
             self.fsdp = FullyShardedDP(self.model, self.device, mode="param" if ngd_opt else "flat",
+                                       units=[("", self.model)] if cfg.fsdp_wrap == "model" else None,
                                        offload=cfg.fsdp_offload, static=static,
                                        reshard_after_forward=cfg.fsdp_schedule == "full_shard",
                                        param_dtype={"fp32": None, "bf16": torch.bfloat16}[cfg.fsdp_param_dtype])

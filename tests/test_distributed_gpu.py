@@ -417,7 +417,7 @@ def test_transformer_ddp_hip_graphs_two_ranks(cuda):
     run_world(_transformer_ddp_graph_worker, world=2, native=True, timeout=400)
 
 
-def _transformer_fsdp_graph_worker(rank, world, schedule):
+def _transformer_fsdp_graph_worker(rank, world, schedule, wrap="sublayer"):
     """The transformer under static FSDP captured as HIP graphs: the forward is
     cut at every wrap unit (gather wait + prefetch between segments), the reduce-scatters are
     actions between backward segments (plus, FULL_SHARD, the re-gathers before each
@@ -431,7 +431,7 @@ def _transformer_fsdp_graph_worker(rank, world, schedule):
         torch.manual_seed(0)
         cfg = T.TransformerConfig(batch_size=16, synthetic=True, eval=False, plot=False, distributed=True, fsdp=True,
                                   fsdp_schedule=schedule, optimizer="sgd", epoch=1, length_buckets=(128,),
-                                  n_layers=2, extra={"subset_stride": 50})
+                                  n_layers=2, fsdp_wrap=wrap, extra={"subset_stride": 50})
         tr = T.TransformerTrainer(cfg)
         for mod in tr.model.modules():
             if isinstance(mod, nn.Dropout):
@@ -452,9 +452,10 @@ def _transformer_fsdp_graph_worker(rank, world, schedule):
     assert ((pe - pg).norm() / pe.norm()).item() < 1e-4
 
 
-@pytest.mark.parametrize("schedule", ["full_shard", "shard_grad_op"])
-def test_transformer_fsdp_hip_graphs_two_ranks(cuda, schedule):
-    run_world(_transformer_fsdp_graph_worker, world=2, native=True, timeout=500, args=(schedule,))
+@pytest.mark.parametrize("schedule,wrap", [("full_shard", "sublayer"), ("shard_grad_op", "sublayer"),
+                                           ("full_shard", "model")])
+def test_transformer_fsdp_hip_graphs_two_ranks(cuda, schedule, wrap):
+    run_world(_transformer_fsdp_graph_worker, world=2, native=True, timeout=500, args=(schedule, wrap))
 
 
 def _zero_graph_worker(rank, world):

@@ -42,6 +42,8 @@ def parse(argv=None):
     p.add_argument("--precision", default="bf16", choices=["bf16", "fp16", "fp32"])
     p.add_argument("--fsdp", action="store_true", help="flat-sharded data parallel (reference: FSDP)")
     p.add_argument("--fsdp_schedule", default="full_shard", choices=["full_shard", "shard_grad_op"])
+    p.add_argument("--fsdp_wrap", default="model", choices=["model", "sublayer"],
+                   help="FSDP units: the whole model (the reference's FSDP(model)) or one per sublayer")
     p.add_argument("--bucket_mb", default=25.0, type=float)
     p.add_argument("--faithful", action="store_true", help="reproduce reference quirks (see README)")
     p.add_argument("--steps", default=0, type=int, help="max steps per epoch (0 = full epoch)")
@@ -73,7 +75,7 @@ def config_from_args(a):
                              distributed=a.distributed, ngd=a.ngd, optimizer=a.optimizer,
                              weight_decay=a.weight_decay, precision=a.precision, synthetic=a.synthetic,
                              data_root=a.data_root, tokenizer=a.tokenizer, seed=a.seed, faithful=a.faithful,
-                             fsdp=a.fsdp, fsdp_schedule=a.fsdp_schedule, bucket_mb=a.bucket_mb, resume=a.resume, checkpoint_dir=a.checkpoint_dir,
+                             fsdp=a.fsdp, fsdp_schedule=a.fsdp_schedule, fsdp_wrap=a.fsdp_wrap, bucket_mb=a.bucket_mb, resume=a.resume, checkpoint_dir=a.checkpoint_dir,
                              steps_per_epoch=a.steps, eval=not a.no_eval, log_path=a.log, plot=not a.no_plot,
                              workers=a.workers, n_layers=a.layers, d_model=a.d_model, heads=heads,
                              d_ff=2 * a.d_model, d_hidden=2 * a.d_model, auto_resume=a.auto_resume,
