@@ -199,11 +199,12 @@ class ResNetTrainer:
         if kind == "ngd":
             wd = 1e-4 if cfg.weight_decay is None else cfg.weight_decay
             opt = NGD(self.space, lr=lr, momentum=cfg.momentum, weight_decay=wd)
-            if self.zero is not None and "FDT_NGD_GRAPHS" not in os.environ:
+            if self.zero is not None and self.zero.ws > 1 and "FDT_NGD_GRAPHS" not in os.environ:
                 # a rank preconditions ~1/world of the parameters: the step is launch-bound
                 # there, and replaying it as HIP graphs wins (world 8 slowest rank, non-update
                 # 1.01 -> 0.63 ms, update 3.17 -> 3.01 ms: profiles/r4/ngd_w8_*); at full size
-                # (one GPU) the eager step stays the default (GPU-bound: 30.1 vs 30.8 ms)
+                # (one GPU, world 1 included) the eager step stays the default (GPU-bound:
+                # 30.1 vs 30.8 ms unsharded; sharded world 1 30.7 ms with graphs)
                 opt.graphs = True
         elif kind == "madgrad":
             wd = 5e-6 if cfg.weight_decay is None else cfg.weight_decay
