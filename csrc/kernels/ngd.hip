@@ -920,16 +920,34 @@ __global__ __launch_bounds__(256) void ngd_proj_sums_kernel(const float* __restr
 
 // dst[e] = sum_{k < ns} src[k n + e], k in order; a second (src2, dst2, n2) slab set in the
 // same launch (J and H^T H of an update step) follows the first in the index space
+// Block = 64 columns x 4 slab lanes: lane r sums slabs r, r+4, ... and the four partials are
+// added in a fixed order (deterministic).  The embedding's J / H slabs (~240-480 slabs of
+// 40960 floats) left one thread per column on ~160 workgroups latency-bound (135 us).
 __global__ __launch_bounds__(256) void ngd_slab_sum_kernel(const float* __restrict__ src, float* __restrict__ dst,
                                                            long n, int ns, const float* __restrict__ src2,
                                                            float* __restrict__ dst2, long n2) {
-  for (long e = (long)blockIdx.x * 256 + threadIdx.x; e < n + n2; e += (long)gridDim.x * 256) {
+  __shared__ float red[4][64];
+  const int cl = threadIdx.x & 63, rl = threadIdx.x >> 6;
+  for (long e0 = (long)blockIdx.x * 64; e0 < n + n2; e0 += (long)gridDim.x * 64) {
+    const long e = e0 + cl;
+    const bool ok = e < n + n2;
     const bool two = e >= n;
     const float* s_ = two ? src2 : src;
     const long m = two ? n2 : n, i = two ? e - n : e;
     float s = 0.f;
-    for (int k = 0; k < ns; ++k) s += s_[(long)k * m + i];
-    (two ? dst2 : dst)[i] = s;
+    if (ok) {
+      int k = rl;
+      for (; k + 12 < ns; k += 16) {  // four independent loads in flight per lane
+        const float a = s_[(long)k * m + i], b = s_[(long)(k + 4) * m + i];
+        const float c = s_[(long)(k + 8) * m + i], d = s_[(long)(k + 12) * m + i];
+        s += a; s += b; s += c; s += d;
+      }
+      for (; k < ns; k += 4) s += s_[(long)k * m + i];
+    }
+    red[rl][cl] = s;
+    __syncthreads();
+    if (rl == 0 && ok) (two ? dst2 : dst)[i] = (red[0][cl] + red[1][cl]) + (red[2][cl] + red[3][cl]);
+    __syncthreads();
   }
 }
 
@@ -983,7 +1001,7 @@ long ngd_proj_hbuf_numel(int G, int A, int D, int B, int R, bool need_ip, bool n
 }
 
 static int slab_blocks(long n) {
-  long nb = (n + 255) / 256;
+  long nb = (n + 63) / 64;  // (ngd_slab_sum_kernel: 64 columns per workgroup)
   return (int)(nb > 4096 ? 4096 : (nb < 1 ? 1 : nb));
 }
 
