@@ -570,8 +570,11 @@ class NGD(SGD):
                          nesterov=nesterov, **kw)
         self.group.update(ngd=ngd, alpha=alpha, rank=rank, update_period=update_period, eta=eta)
         self.groups = None
-        # deferred eigensolves on a side stream, overlapping the next step (see drive)
-        self.overlap_eigh = overlap_eigh
+        # deferred eigensolves on a side stream, overlapping the next step (see drive);
+        # FDT_NGD_OVERLAP=0: solved inline on the caller's stream instead (A/B: beside the next
+        # step's library GEMMs the one-workgroup-per-matrix solver delays them,
+        # profiles/r4/probe_side_eigh.txt)
+        self.overlap_eigh = overlap_eigh and os.environ.get("FDT_NGD_OVERLAP", "1") != "0"
         self._side = None
         self._pending = None
         self.graphs = GRAPHS
