@@ -493,3 +493,38 @@ def _zero_graph_worker(rank, world):
 
 def test_sharded_ngd_allreduce_between_graph_segments(cuda):
     run_world(_zero_graph_worker, world=1, native=True, backend="nccl", timeout=400)
+
+
+def _zero_ngd_graphs_world2_worker(rank, world):
+    """Sharded NGD at world > 1 replays its optimizer step as HIP graphs by default (a rank
+    preconditions 1/world of the parameters: launch-bound).  Two gloo ranks on one GPU: the
+    sharded run (graphs on, through the init schedule into graph replays) ends where the
+    unsharded NGD run (full preconditioning on every rank, DDP averaging) does."""
+    import torch.distributed as dist
+    from faster_distributed_training_amd.train.resnet_trainer import ResNetConfig, ResNetTrainer
+    torch.cuda.set_device(0)
+    assert dist.get_world_size() == 2
+    base = dict(arch="resnet18", bs=16, synthetic=True, eval=False, plot=False, ngd=True, optimizer="ngd",
+                distributed=True, deterministic=True, extra={"subset_stride": 50})
+    runs = {}
+    for shard in (False, True):
+        tr = ResNetTrainer(ResNetConfig(shard_ngd=shard, bucket_mb=2.0, first_bucket_mb=0.5, **base))
+        assert (tr.zero is not None) == shard
+        if shard:
+            assert tr.optimizer.graphs  # the world > 1 default
+        it = iter(tr.train_loader)
+        for _ in range(16):  # 10 init steps, then update / plain steps replayed as graphs
+            x, y = next(it)
+            loss = tr.train_step(x, y)
+        torch.cuda.synchronize()
+        assert torch.isfinite(loss).item()
+        if shard:
+            assert tr.optimizer.graph_replays > 0
+        runs[shard] = {k: v.detach().clone() for k, v in tr.model.state_dict().items()}
+    for k, v in runs[False].items():
+        if v.dtype.is_floating_point:
+            assert torch.allclose(runs[True][k], v, rtol=1e-4, atol=1e-5), (k, (runs[True][k] - v).abs().max())
+
+
+def test_sharded_ngd_graphs_world2(cuda):
+    run_world(_zero_ngd_graphs_world2_worker, world=2, native=True, timeout=600)
