@@ -157,15 +157,22 @@ class ShardedOptimizerDP:
 
     def after_step(self):
         """All-gather every rank's updated run into the full parameter buffer; clear the
-        backward-ordered gradient for the next accumulation (the optimizer cleared its run)."""
+        backward-ordered gradient for the next accumulation (the optimizer cleared its run).
+        The clear runs on the compute stream WHILE the all-gather runs on RCCL's stream (the
+        gather is issued async and joined after): the ~100 MB memset leaves the critical path.
+        (It cannot be dropped: the engine's 1x1 weight gradients accumulate with split-K
+        atomics, so every step starts from a zeroed buffer.)"""
+        work = None
         if self.ws > 1:
             if self.local is None:
-                dist.all_gather_into_tensor(self.flat.data, self.view.data, group=self.pg)
+                work = dist.all_gather_into_tensor(self.flat.data, self.view.data, group=self.pg, async_op=True)
             else:
                 self.local.copy_(self.view.data)
-                dist.all_gather_into_tensor(self.flat.data, self.local, group=self.pg)
-        self.flat.refresh_shadow()
+                work = dist.all_gather_into_tensor(self.flat.data, self.local, group=self.pg, async_op=True)
         self.grad_space.grad.zero_()
+        if work is not None:
+            work.wait()
+        self.flat.refresh_shadow()
 
     def sync_buffers(self, src: int = 0):
         from .dist import broadcast_buffers
