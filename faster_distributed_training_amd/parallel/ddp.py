@@ -155,7 +155,10 @@ class BucketReducer:
             buf.copy_(view)
         else:
             buf = view
-        op = dist.ReduceOp.AVG if self.use_avg else dist.ReduceOp.SUM
+        # (one rank: the average IS the sum -- RCCL's single-rank PreMulSum would run a whole
+        # extra pass over the bucket, a world-1 artifact that a ring all-reduce at N > 1 does
+        # not have: profiles/r4/kstats_bs128_{plain,ddp}.txt)
+        op = dist.ReduceOp.AVG if (self.use_avg and self.ws > 1) else dist.ReduceOp.SUM
         work = dist.all_reduce(buf, op=op, group=self.pg, async_op=True)
         if torch.cuda.is_available() and torch.cuda.is_current_stream_capturing():
             self.in_graph.add(b)
@@ -186,7 +189,7 @@ class BucketReducer:
             if self.cast[b]:
                 self.flat.grad[s:e].copy_(self.wire[s:e])
                 self.cast[b] = False
-            if not self.use_avg:
+            if not self.use_avg and self.ws > 1:
                 self.flat.grad[s:e].div_(self.ws)
         self.works = [None] * len(self.buckets)
         self.pending = [len(idx) for (_, _, idx) in self.buckets]

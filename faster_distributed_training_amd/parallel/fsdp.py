@@ -299,14 +299,14 @@ class Unit:
             return
         if fs.static:
             # gradient views stay bound to the persistent buffer; only the collective
-            op = dist.ReduceOp.AVG if fs.use_avg else dist.ReduceOp.SUM
+            op = dist.ReduceOp.AVG if (fs.use_avg and fs.ws > 1) else dist.ReduceOp.SUM  # (1 rank: sum)
             self.rs_work = dist.reduce_scatter_tensor(fs.grad_chunk(self), self.gfull, op=op, group=fs.pg,
                                                       async_op=True)
             self.grads_live = False
             if self.slot is not None:
                 fs.grad_owner[self.slot] = self
             return
-        op = dist.ReduceOp.AVG if fs.use_avg else dist.ReduceOp.SUM
+        op = dist.ReduceOp.AVG if (fs.use_avg and fs.ws > 1) else dist.ReduceOp.SUM  # (1 rank: sum)
         self.rs_work = dist.reduce_scatter_tensor(fs.grad_chunk(self), self.gfull, op=op, group=fs.pg,
                                                   async_op=True)
         if fs.offload and fs.copy_stream is not None:
@@ -651,7 +651,7 @@ class FullyShardedDP:
                 self.copy_stream.synchronize()
             else:
                 self.shard_grad.copy_(self.stage_grad, non_blocking=False)
-        if not self.use_avg:
+        if not self.use_avg and self.ws > 1:
             self.shard_grad.div_(self.ws)
         for u in self.units:
             if not u.root:
