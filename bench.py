@@ -56,6 +56,9 @@ def parse():
                          "of the multi-GPU path, without the communication time)")
     ap.add_argument("--precision", default="bf16")
     ap.add_argument("--bucket-mb", type=float, default=25.0)
+    ap.add_argument("--first-bucket-mb", type=float, default=None,
+                    help="ResNet DDP / sharded NGD: size of the first (classifier-side) bucket (default: the "
+                         "trainer's)")
     ap.add_argument("--comm-dtype", default="fp32")
     ap.add_argument("--no-native", action="store_true", help="ablation: plain PyTorch ops (w/o tricks)")
     ap.add_argument("--profile-steps", type=int, default=0)
@@ -119,7 +122,8 @@ def main():
                        precision=args.precision, bucket_mb=args.bucket_mb, comm_dtype=args.comm_dtype,
                        fast_path=False if args.no_native else None, graphs=not args.no_graphs,
                        deterministic=args.deterministic, force_sharded=args.sharded_ngd, force_ddp=args.ddp,
-                       fsdp_param_dtype=args.fsdp_param_dtype, fsdp_schedule=args.fsdp_schedule)
+                       fsdp_param_dtype=args.fsdp_param_dtype, fsdp_schedule=args.fsdp_schedule,
+                       **({} if args.first_bucket_mb is None else {"first_bucket_mb": args.first_bucket_mb}))
     tr = ResNetTrainer(cfg)
     dev = tr.device
     cuda = dev.type == "cuda"
