@@ -29,6 +29,9 @@ from tune_conv import FWD_TILES, WG_TILES  # noqa: E402
 
 WG_SPLITS = [1, 2, 4, 7, 8, 14, 16, 28, 32, 56, 64, 102, 128]
 FD_SPLITS = [1, 2, 4, 8]
+if os.environ.get("FDT_RETUNE_FINE") == "1":  # finer split-K grid (second pass)
+    WG_SPLITS = [1, 2, 3, 4, 5, 6, 7, 8, 10, 12, 14, 16, 20, 24, 28, 32, 40, 48, 56, 64, 80, 102, 128]
+    FD_SPLITS = [1, 2, 3, 4, 6, 8]
 
 
 def engine_calls(N, H, shp, dev):
