@@ -59,14 +59,32 @@ AGNEWS_URLS = {
 AGNEWS_MD5 = {"train": "b1a00f826fdfbd249f79597b59e1dc12", "test": "d52ea96a97a2d943681189a97654912d"}
 _WORD = re.compile(r"[a-z0-9]+(?:'[a-z]+)?|[^\sa-z0-9]")
 
-# A compact English stopword list (gensim's STOPWORDS is not installed here; this covers
-# the high-frequency function words it removes).
-STOPWORDS = frozenset("""a about above after again against all also am an and any are as at be because been before
-being below between both but by can could did do does doing down during each few for from further had has have having
-he her here hers herself him himself his how i if in into is it its itself just me more most my myself no nor not now
-of off on once only or other our ours ourselves out over own same she should so some such than that the their theirs
-them themselves then there these they this those through to too under until up very was we were what when where which
-while who whom why will with would you your yours yourself yourselves""".split())
+# gensim.parsing.preprocessing.STOPWORDS (gensim 3.x/4.x), the list the reference's
+# ``remove_stopwords`` uses (/root/reference/transformer_test.py:52,95): the 318-word Glasgow list
+# (= scikit-learn's ENGLISH_STOP_WORDS) plus 19 additions (computer, did, didn, does, doesn, doing,
+# don, just, kg, km, make, quite, really, regarding, say, unless, used, using, various) -- 337 words.
+# gensim is not installed here; the constant is in-tree so the token stream matches the reference.
+STOPWORDS = frozenset("""a about above across after afterwards again against all almost alone along already also although always am
+among amongst amoungst amount an and another any anyhow anyone anything anyway anywhere are around as at back
+be became because become becomes becoming been before beforehand behind being below beside besides between
+beyond bill both bottom but by call can cannot cant co computer con could couldnt cry de describe detail did
+didn do does doesn doing don done down due during each eg eight either eleven else elsewhere empty enough etc
+even ever every everyone everything everywhere except few fifteen fifty fill find fire first five for former
+formerly forty found four from front full further get give go had has hasnt have he hence her here hereafter
+hereby herein hereupon hers herself him himself his how however hundred i ie if in inc indeed interest into is
+it its itself just keep kg km last latter latterly least less ltd made make many may me meanwhile might mill
+mine more moreover most mostly move much must my myself name namely neither never nevertheless next nine no
+nobody none noone nor not nothing now nowhere of off often on once one only onto or other others otherwise our
+ours ourselves out over own part per perhaps please put quite rather re really regarding same say see seem
+seemed seeming seems serious several she should show side since sincere six sixty so some somehow someone
+something sometime sometimes somewhere still such system take ten than that the their them themselves then
+thence there thereafter thereby therefore therein thereupon these they thick thin third this those though
+three through throughout thru thus to together too top toward towards twelve twenty two un under unless until
+up upon us used using various very via was we well were what whatever when whence whenever where whereafter
+whereas whereby wherein whereupon wherever whether which while whither who whoever whole whom whose why will
+with within without would yet you your yours yourself yourselves""".split())
+assert len(STOPWORDS) == 337
+CLEAN_VERSION = "g337"  # cache tag of the cleaning rules (changes invalidate cached token stores)
 
 
 def clean_text(s: str) -> str:
@@ -74,7 +92,8 @@ def clean_text(s: str) -> str:
     applied per sample in ``generate_batch``)."""
     s = _HTML.sub("", s)
     s = _URL.sub(" ", s).strip()
-    return " ".join(w for w in s.split() if w.lower() not in STOPWORDS)
+    # gensim's remove_stopwords: whitespace split, CASE-SENSITIVE membership ("The" stays)
+    return " ".join(w for w in s.split() if w not in STOPWORDS)
 
 
 class HashWordPieceTokenizer:
@@ -198,7 +217,7 @@ def _tokenize_cached(path: str, tok, max_len: int) -> TokenStore:
     with open(path, "rb") as fh:
         digest = hashlib.md5(fh.read(), usedforsecurity=False).hexdigest()
     name = re.sub(r"[^A-Za-z0-9_.-]+", "_", getattr(tok, "name", type(tok).__name__))
-    cache = os.path.join(os.path.dirname(path), f"tokens_{os.path.basename(path)[:-4]}_{name}_{max_len}.npz")
+    cache = os.path.join(os.path.dirname(path), f"tokens_{os.path.basename(path)[:-4]}_{name}_{max_len}_{CLEAN_VERSION}.npz")
     if os.path.isfile(cache):
         z = np.load(cache)  # (allow_pickle=False: plain arrays only)
         if str(z["md5"]) == digest:

@@ -7,8 +7,9 @@ Reference: ``resnet.py:72-113`` (``FusedConvBN2DFunction``) and ``resnet.py:116-
 * **unbiased** variance and ``(y - mean) / (sqrt(var) + eps)`` with ``eps = 1e-3``.
 
 This file holds the pure-PyTorch implementation (CPU path and numerics oracle).  The
-MI355X path lives in ``ops/conv_unit.py`` and fuses the normalisation into the HIP
-kernels; both compute the same function.
+MI355X path is the ResNet engine (``ops/resnet_fused.py`` driving the implicit-GEMM kernels
+of ``ops/conv_igemm.py``), which fuses the normalisation into the HIP kernels; both compute
+the same function.
 """
 from __future__ import annotations
 
@@ -37,7 +38,7 @@ def conv_bn_reference(x: torch.Tensor, w: torch.Tensor, stride: int = 1, padding
 class FusedConvBN2DFunction(torch.autograd.Function):
     """Hand-derived forward/backward with the reference's contract (saves only X and W,
     recomputes the conv in backward).  Used by the gradcheck parity tests and by the
-    ``--faithful`` CPU path; ``ops/conv_unit.py`` is the production GPU path."""
+    ``--faithful`` CPU path; ``ops/resnet_fused.py`` is the production GPU path."""
 
     @staticmethod
     def forward(ctx, X, W, stride=1, padding=1, eps=1e-3):

@@ -588,11 +588,15 @@ class FullyShardedDP:
             if not u.bwd_started:
                 # a gradient that arrived before the unit's output hook (root unit, or an
                 # output without grad): start the unit's backward, keep what was accumulated
-                if self.static and p.grad is not None and u.gfull.untyped_storage().data_ptr() == \
+                if self.static and u.root and p.grad is not None and u.gfull.untyped_storage().data_ptr() == \
                         p.grad.untyped_storage().data_ptr():
-                    # static mode: p.grad is still bound to the unit's gradient buffer (zeroed at
-                    # the end of the previous step, finish_backward) and autograd accumulated into
-                    # it in place -- zeroing it now would drop this gradient
+                    # static mode, ROOT unit only: p.grad is still bound to the root's gradient
+                    # buffer, which finish_backward zeroed at the end of the previous step, and
+                    # autograd accumulated into it in place -- zeroing it now would drop this
+                    # gradient.  (Other static units' bindings are dropped by finish_backward --
+                    # a ring slot's buffer holds another unit's gradient, a SHARD_GRAD_OP unit's
+                    # last step's -- so their early gradient arrives in a fresh tensor and takes
+                    # the branch below.)
                     u.bwd_started = u.grads_live = True
                     u.pending = sum(1 for _, q in u.params if q.requires_grad)
                 else:
@@ -643,6 +647,11 @@ class FullyShardedDP:
             for u in self.units:
                 if u.root:  # (its first gradient of the next step accumulates in place, see the hook)
                     u.gfull.zero_()
+                elif u.name not in self.engine_units:
+                    # module-hook units rebind p.grad to their buffer in begin_backward; until
+                    # then a gradient must not accumulate into the (shared / stale) buffer
+                    for _, q in u.params:
+                        q.grad = None
         self.last_rs = None
         if self.offload:
             if self.copy_stream is not None:
@@ -709,9 +718,20 @@ class FullyShardedDP:
         with self.summon_full_params():
             return {k: v.detach().clone().cpu() for k, v in self.model.state_dict().items()}
 
+    def _drop_lowp_gathers(self):
+        """A unit still gathered from a bf16 wire (e.g. after an eval forward) holds rounded
+        parameters, not the fp32 masters: finish any in-flight gather, then mark it stale so
+        the next exact gather re-fetches the shards (as ``summon_full_params`` does)."""
+        for u in self.units:
+            if u.full16 is not None:
+                if u.work is not None:
+                    u.gather(wait=True)
+                u.gathered = False
+
     def _ring_state_dict(self):
         """Unit by unit: exact fp32 gather into the unit's slot, copy out (collective)."""
         vals = {}
+        self._drop_lowp_gathers()
         for u in self.units:
             u.gather(wait=True, exact=True)
             for _, p in u.params:
@@ -729,9 +749,12 @@ class FullyShardedDP:
         unexpected = [k for k in sd if k not in set(keys)]
         if strict and (missing or unexpected):
             raise RuntimeError(f"load_full_state_dict: missing {missing[:5]}, unexpected {unexpected[:5]}")
+        self._drop_lowp_gathers()
         for u in self.units:
-            if u.slot is not None:
-                u._claim_slot()
+            # the slot must hold THIS unit's current values before the keys of ``sd`` are written
+            # over it (a key missing with strict=False keeps them; claiming the slot alone
+            # would leave the previous owner's parameters there)
+            u.gather(wait=True, exact=True)
             for n, p in u.params:
                 if n in sd:
                     p.data.copy_(sd[n].to(p.device, p.dtype).view(p.shape))

@@ -49,6 +49,22 @@ def test_clean_text_matches_reference_rules():
     assert s.split() == ["Stocks", "rise", "market"]  # stopwords "in", "the" removed
 
 
+def test_stopwords_are_gensims():
+    """gensim's STOPWORDS (337 words) = scikit-learn's Glasgow list + 19 additions; gensim's
+    remove_stopwords is case-sensitive (reference transformer_test.py:52,95)."""
+    assert len(A.STOPWORDS) == 337
+    try:
+        from sklearn.feature_extraction.text import ENGLISH_STOP_WORDS
+    except ImportError:
+        ENGLISH_STOP_WORDS = None
+    if ENGLISH_STOP_WORDS is not None:
+        assert set(ENGLISH_STOP_WORDS) <= A.STOPWORDS
+        assert sorted(A.STOPWORDS - set(ENGLISH_STOP_WORDS)) == sorted(
+            "computer did didn does doesn doing don just kg km make quite really regarding say unless used using "
+            "various".split())
+    assert A.clean_text("The computer using km rose") == "The rose"
+
+
 def test_download_clean_tokenize_store(mirror):
     tok = A.get_tokenizer("hash")
     st = A.load_agnews(str(mirror), True, tok, max_len=64)

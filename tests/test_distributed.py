@@ -247,6 +247,41 @@ def test_fsdp_full_shard_ring_static(world, mode):
     run_world(_fsdp_ring_worker, world=world, args=(mode,))
 
 
+def _fsdp_ring_bf16_ckpt_worker(rank, world):
+    """on the full-shard ring with a bf16 param_dtype, (a) a checkpoint taken right
+    after an eval forward (units still gathered from the bf16 wire) holds the fp32 masters,
+    not bf16-rounded copies; (b) a strict=False load with a key missing keeps THAT unit's
+    current value (not the previous slot owner's)."""
+    from faster_distributed_training_amd.parallel.fsdp import FullyShardedDP
+    m = _units_model(seed=0)
+    # two units (one per ring slot: each still owns its slot after a forward) + a root unit
+    units = [(str(i), m[i]) for i in (0, 2)]
+    ref = {k: v.clone() for k, v in _units_model(seed=0).state_dict().items()}
+    fs = FullyShardedDP(m, torch.device("cpu"), units=units, mode="flat", static=True, reshard_after_forward=True,
+                        param_dtype=torch.bfloat16)
+    assert fs.ring
+    with torch.no_grad():
+        m.eval()
+        m(_batch(rank)[0])  # eval forward: the last units stay gathered (bf16 wire)
+    sd = fs.full_state_dict()
+    for k, v in ref.items():
+        assert torch.equal(sd[k], v), k  # exact masters
+    assert any(not torch.equal(v, v.bfloat16().float()) for v in sd.values())  # not bf16-representable
+    # strict=False load with one key missing: that parameter keeps its own value
+    missing_key = "2.weight"
+    sd2 = {k: v + 1.0 for k, v in sd.items() if k != missing_key}
+    with torch.no_grad():
+        m(_batch(rank)[0])
+    fs.load_full_state_dict(sd2, strict=False)
+    back = fs.full_state_dict()
+    assert torch.equal(back[missing_key], ref[missing_key])
+    assert all(torch.equal(back[k], sd2[k]) for k in sd2)
+
+
+def test_fsdp_ring_bf16_checkpoint_exact():
+    run_world(_fsdp_ring_bf16_ckpt_worker, world=2)
+
+
 class _Tied(nn.Module):
     def __init__(self, seed):
         super().__init__()
