@@ -44,6 +44,8 @@ def parse():
     ap.add_argument("--fsdp", action="store_true")
     ap.add_argument("--fsdp-param-dtype", default="bf16", choices=["bf16", "fp32"],
                     help="--fsdp: parameter all-gather wire / compute-copy precision (masters stay fp32)")
+    ap.add_argument("--fsdp-offload", action="store_true",
+                    help="--fsdp: shards + optimizer state in pinned host memory (the reference's CPUOffload; eager)")
     ap.add_argument("--fsdp-wrap", default="model", choices=["sublayer", "model"],
                     help="--model transformer --fsdp: wrap units (sublayers, or the whole model as one unit "
                          "like the reference's FSDP(model))")
@@ -123,6 +125,7 @@ def main():
                        fast_path=False if args.no_native else None, graphs=not args.no_graphs,
                        deterministic=args.deterministic, force_sharded=args.sharded_ngd, force_ddp=args.ddp,
                        fsdp_param_dtype=args.fsdp_param_dtype, fsdp_schedule=args.fsdp_schedule,
+                       fsdp_offload=args.fsdp_offload,
                        **({} if args.first_bucket_mb is None else {"first_bucket_mb": args.first_bucket_mb}))
     tr = ResNetTrainer(cfg)
     dev = tr.device
@@ -235,6 +238,7 @@ def _sharding_fields(tr, rec):
         # eager FSDP reshards after forward (FULL_SHARD)
         cfg["fsdp_schedule"] = "shard_grad_op" if (tr.fsdp.static and not tr.fsdp.ring) else "full_shard"
         cfg["fsdp_param_dtype"] = str(tr.fsdp.param_dtype or torch.float32).replace("torch.", "")
+        cfg["fsdp_offload"] = bool(tr.fsdp.offload)
     elif tr.zero is not None:
         cfg["optimizer_sharding"] = "ngd-owner-shards (bucketed all-reduce overlapped with backward + all-gather)"
         cfg["owner_shard_numel"] = int(tr.zero.view.numel)
@@ -260,7 +264,8 @@ def bench_transformer(args):
     cfg = TransformerConfig(batch_size=gb // world, synthetic=True, eval=False, plot=False, distributed=world > 1,
                             ngd=True, precision=args.precision, length_buckets=buckets,
                             bucket_mb=args.bucket_mb, fsdp=args.fsdp, epoch=1, fsdp_param_dtype=args.fsdp_param_dtype,
-                            fsdp_schedule=args.fsdp_schedule, fsdp_wrap=args.fsdp_wrap)
+                            fsdp_schedule=args.fsdp_schedule, fsdp_wrap=args.fsdp_wrap,
+                            fsdp_offload=args.fsdp_offload)
     tr = TransformerTrainer(cfg)
     longest = int(tr.train_loader.store.lengths.max())
     assert longest <= buckets[-1], f"largest bucket {buckets[-1]} would truncate samples of length {longest}"

@@ -104,6 +104,11 @@ class TransformerTrainer:
                 pdist.setup_norank()
             self.rank, self.world = pdist.rank(), pdist.world()
             cfg.distributed = self.world > 1
+        if cfg.distributed and cfg.faithful and not cfg.fsdp:
+            # the reference's --distributed IS FullyShardedDataParallel(model, size_based_auto_wrap_policy,
+            # cpu_offload=CPUOffload(offload_params=True)) (transformer_test.py:387-392): at 29.3M
+            # parameters the size policy wraps nothing, i.e. ONE unit = the whole model
+            cfg.fsdp, cfg.fsdp_wrap, cfg.fsdp_offload = True, "model", True
         self.device = default_device()
         seed_everything(cfg.seed)
         self.tokenizer = get_tokenizer(cfg.tokenizer) if not cfg.synthetic else None
@@ -151,6 +156,9 @@ class TransformerTrainer:
                 from ..parallel.ddp import BucketReducer
                 self.reducer = BucketReducer(self.flat, self.model, bucket_mb=cfg.bucket_mb)
         self.sharder = self.fsdp if self.fsdp is not None else self.zero
+        self.dist_path = self._describe_path(ngd_opt)
+        if cfg.distributed or cfg.fsdp:
+            print0(f"distributed path: {self.dist_path}")
         if self.fsdp is None and DIRECT_GRADS:
             from ..ops.linear import enable_direct_grads
             enable_direct_grads(self.model.parameters())
@@ -170,6 +178,22 @@ class TransformerTrainer:
         self._graphs, self._graph_stream, self._graph_pool = {}, None, None
         if cfg.auto_resume and resilience.restore_last(self):
             print0(f"auto-resume: restored {self.last_path}, continuing at epoch {self.start_epoch}")
+
+    def _describe_path(self, ngd_opt):
+        """Which data-parallel path this run takes (printed at start; the reference's
+        --distributed is FSDP(model) + CPU offload, ``--faithful`` selects exactly that)."""
+        cfg = self.cfg
+        if self.fsdp is not None:
+            wrap = "whole model as one unit" if cfg.fsdp_wrap == "model" else "one unit per sublayer"
+            mode = "static, HIP-graph segments" if self.fsdp.static else "eager"
+            off = ", CPU offload (host optimizer)" if cfg.fsdp_offload else ""
+            ref = " -- the reference's FSDP(model, CPUOffload)" if (cfg.fsdp_offload and cfg.fsdp_wrap == "model") else ""
+            return f"FSDP {cfg.fsdp_schedule} ({wrap}, {mode}{off}), world {self.world}{ref}"
+        if self.zero is not None:
+            return f"DDP buckets + ZeRO-2 sharded NGD, world {self.world} (reference: FSDP + CPU offload; --faithful)"
+        if self.reducer is not None:
+            return f"DDP bucket reducer, world {self.world} (reference: FSDP + CPU offload; --faithful)"
+        return "single process"
 
     @property
     def ckpt_path(self):

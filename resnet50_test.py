@@ -3,7 +3,7 @@
 
 Reference flags (``resnet50_test.py:46-59``): --lr, --resume/-r, --epoch, --alpha, --bs,
 --workers, --meta_learning, --distributed, --ngd.  Additional flags: --synthetic,
---seed, --precision, --fsdp, --bucket_mb, --faithful, --optimizer, --arch, --steps,
+--seed, --precision, --fsdp, --fsdp_offload, --bucket_mb, --faithful, --optimizer, --arch, --steps,
 --weight_decay/--gamma (tuning variant), --data_root, --log, --no_eval.
 
 Examples (single MI355X, or via torchrun / run_distributed.sh for several):
@@ -42,6 +42,8 @@ def parse(argv=None):
     p.add_argument("--precision", default="bf16", choices=["bf16", "fp16", "fp32"])
     p.add_argument("--fsdp", action="store_true")
     p.add_argument("--fsdp_schedule", default="full_shard", choices=["full_shard", "shard_grad_op"])
+    p.add_argument("--fsdp_offload", action="store_true",
+                   help="--fsdp: shards + optimizer state in pinned host memory (reference CPUOffload; eager, host optimizer)")
     p.add_argument("--bucket_mb", default=25.0, type=float)
     p.add_argument("--comm_dtype", default="fp32", choices=["fp32", "bf16"])
     p.add_argument("--faithful", action="store_true", help="reproduce reference quirks (lr x4, mixup loss form)")
@@ -78,7 +80,7 @@ def config_from_args(a):
                         optimizer=a.optimizer, weight_decay=a.weight_decay, precision=a.precision,
                         synthetic=a.synthetic, data_root=a.data_root, seed=a.seed, faithful=a.faithful,
                         lr_scaling="faithful4" if a.faithful else "world", bucket_mb=a.bucket_mb,
-                        comm_dtype=a.comm_dtype, fsdp=a.fsdp, fsdp_schedule=a.fsdp_schedule, scheduler=sched, resume=a.resume,
+                        comm_dtype=a.comm_dtype, fsdp=a.fsdp, fsdp_schedule=a.fsdp_schedule, fsdp_offload=a.fsdp_offload, scheduler=sched, resume=a.resume,
                         checkpoint_dir=a.checkpoint_dir, steps_per_epoch=a.steps, eval=not a.no_eval,
                         log_path=a.log, plot=not a.no_plot, workers=a.workers, auto_resume=a.auto_resume,
                         save_last=a.save_last, nonfinite_guard=not a.no_nonfinite_guard,

@@ -140,3 +140,22 @@ def test_run_distributed_two_ranks(tmp_path):
                        capture_output=True, text=True, timeout=900)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     assert "epoch 0:" in r.stdout
+
+
+def test_transformer_distributed_faithful_is_fsdp_offload(tmp_path):
+    """The reference's ``transformer_test.py --distributed`` is FSDP(whole model) with
+    CPUOffload(offload_params=True) (reference transformer_test.py:387-392); ``--faithful``
+    selects exactly that path (printed), and it ends where eager FSDP without offload ends."""
+    cli = os.path.join(ROOT, "transformer_test.py")
+    common = ["--synthetic", "-b", "4", "--epoch", "1", "--steps", "2", "--eval_steps", "1", "--layers", "2",
+              "--d_model", "64", "--no_plot", "--ngd", "--distributed", "--faithful"]
+    out = _torchrun([cli] + common + ["--checkpoint_dir", str(tmp_path / "off")], tmp_path)
+    assert "distributed path: FSDP full_shard (whole model as one unit, eager, CPU offload" in out, out[-2000:]
+    assert "the reference's FSDP(model, CPUOffload)" in out
+    out2 = _torchrun([cli] + common + ["--fsdp", "--checkpoint_dir", str(tmp_path / "dev")], tmp_path)
+    assert "CPU offload" not in out2 and "distributed path: FSDP full_shard (whole model as one unit" in out2
+    a = torch.load(tmp_path / "off" / "transformer_ckpt.pth", weights_only=True)["net"]
+    b = torch.load(tmp_path / "dev" / "transformer_ckpt.pth", weights_only=True)["net"]
+    assert a.keys() == b.keys()
+    for k in a:
+        assert torch.allclose(a[k].float(), b[k].float(), atol=1e-6, rtol=0), k

@@ -4,10 +4,12 @@
 
 Reference flags (``transformer_test.py:350-361``): --batch_size/-b, --epoch, --lr,
 --resume, --workers, --alpha, --distributed, --ngd.  Additional flags: --synthetic,
---seed, --precision, --fsdp, --faithful, --optimizer, --steps, --tokenizer, --data_root,
+--seed, --precision, --fsdp, --fsdp_offload, --faithful, --optimizer, --steps, --tokenizer, --data_root,
 --layers/--d_model (smaller models for smoke tests), --log, --no_eval, --no_plot.
 
     python transformer_test.py --synthetic -b 64 --epoch 1
+    # the reference's distributed path (transformer_test.py:387-392): FSDP(whole model, CPUOffload)
+    torchrun --nproc-per-node 4 transformer_test.py --distributed --faithful --ngd
     bash run_distributed.sh        # torchrun, one rank per GPU
 """
 from __future__ import annotations
@@ -42,6 +44,8 @@ def parse(argv=None):
     p.add_argument("--precision", default="bf16", choices=["bf16", "fp16", "fp32"])
     p.add_argument("--fsdp", action="store_true", help="flat-sharded data parallel (reference: FSDP)")
     p.add_argument("--fsdp_schedule", default="full_shard", choices=["full_shard", "shard_grad_op"])
+    p.add_argument("--fsdp_offload", action="store_true",
+                   help="--fsdp: shards + optimizer state in pinned host memory (reference CPUOffload; eager, host optimizer)")
     p.add_argument("--fsdp_wrap", default="model", choices=["model", "sublayer"],
                    help="FSDP units: the whole model (the reference's FSDP(model)) or one per sublayer")
     p.add_argument("--bucket_mb", default=25.0, type=float)
@@ -75,7 +79,7 @@ def config_from_args(a):
                              distributed=a.distributed, ngd=a.ngd, optimizer=a.optimizer,
                              weight_decay=a.weight_decay, precision=a.precision, synthetic=a.synthetic,
                              data_root=a.data_root, tokenizer=a.tokenizer, seed=a.seed, faithful=a.faithful,
-                             fsdp=a.fsdp, fsdp_schedule=a.fsdp_schedule, fsdp_wrap=a.fsdp_wrap, bucket_mb=a.bucket_mb, resume=a.resume, checkpoint_dir=a.checkpoint_dir,
+                             fsdp=a.fsdp, fsdp_schedule=a.fsdp_schedule, fsdp_wrap=a.fsdp_wrap, fsdp_offload=a.fsdp_offload, bucket_mb=a.bucket_mb, resume=a.resume, checkpoint_dir=a.checkpoint_dir,
                              steps_per_epoch=a.steps, eval=not a.no_eval, log_path=a.log, plot=not a.no_plot,
                              workers=a.workers, n_layers=a.layers, d_model=a.d_model, heads=heads,
                              d_ff=2 * a.d_model, d_hidden=2 * a.d_model, auto_resume=a.auto_resume,
