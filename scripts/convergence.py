@@ -56,18 +56,22 @@ def make_task(n_train=4096, n_test=1024, noise=3.0, seed=1234, device="cpu"):
     return sample(n_train), sample(n_test)
 
 
-def train_curve(native: bool, opt: str, steps: int, bs: int = 128, lr=None, device="cuda", seed=0, task=None):
-    """Loss curve + final test accuracy of ResNet-18 trained ``steps`` steps."""
+def train_curve(native: bool, opt: str, steps: int, bs: int = 128, lr=None, device="cuda", seed=0, task=None,
+                bf16=None, arch="resnet18"):
+    """Loss curve + final test accuracy of a ResNet (``arch``) trained ``steps`` steps.
+    ``native``: the HIP engine (bf16); otherwise plain PyTorch, in fp32 or -- ``bf16=True`` --
+    under torch's bf16 autocast (the noise budget of the engine's bf16 arithmetic)."""
     prev = os.environ.get("FDT_NATIVE")
     os.environ["FDT_NATIVE"] = "1" if native else "0"
+    amp = native if bf16 is None else bool(bf16)
     try:
-        from faster_distributed_training_amd.models.resnet import resnet18
+        from faster_distributed_training_amd.models import resnet as R
         from faster_distributed_training_amd.optim import flat_optim as O
         from faster_distributed_training_amd.optim.ngd import NGD
         from faster_distributed_training_amd.utils.flat import FlatParams
         (xtr, ytr), (xte, yte) = task if task is not None else make_task(device=device)
         torch.manual_seed(seed)
-        m = resnet18(10).to(device)
+        m = getattr(R, arch)(10).to(device)
         m.fast_path = bool(native)
         flat = FlatParams(m, device=device)
         if opt == "madgrad":
@@ -83,7 +87,7 @@ def train_curve(native: bool, opt: str, steps: int, bs: int = 128, lr=None, devi
         for s in range(steps):
             idx = torch.randint(0, xtr.shape[0], (bs,), generator=g).to(device)
             x, y = xtr[idx], ytr[idx]
-            if native:
+            if amp:
                 with torch.autocast("cuda", dtype=torch.bfloat16):
                     out = m(x)
             else:
@@ -99,7 +103,7 @@ def train_curve(native: bool, opt: str, steps: int, bs: int = 128, lr=None, devi
         with torch.no_grad():
             for i in range(0, xte.shape[0], 256):
                 xb = xte[i:i + 256]
-                if native:
+                if amp:
                     with torch.autocast("cuda", dtype=torch.bfloat16):
                         out = m(xb)
                 else:
@@ -113,30 +117,42 @@ def train_curve(native: bool, opt: str, steps: int, bs: int = 128, lr=None, devi
             os.environ["FDT_NATIVE"] = prev
 
 
-def compare(opt: str, steps: int, device="cuda"):
+def compare(opt: str, steps: int, device="cuda", arch="resnet18", bs=128, tail_frac=0.2):
+    """Three runs from the same weights on the same batches: the HIP engine, fp32 PyTorch (the
+    reference numerics) and PyTorch under bf16 autocast (FDT_NATIVE=0: how far bf16 arithmetic
+    alone moves the result -- the engine's error budget).  Final loss = mean of the last
+    ``tail_frac`` of the steps."""
     task = make_task(device=device)
-    eng = train_curve(True, opt, steps, device=device, task=task)
-    ref = train_curve(False, opt, steps, device=device, task=task)
-    tail = max(10, steps // 10)
-    le, lr_ = sum(eng["losses"][-tail:]) / tail, sum(ref["losses"][-tail:]) / tail
-    return {"optimizer": opt, "steps": steps, "engine_final_loss": le, "reference_final_loss": lr_,
+    kw = dict(device=device, task=task, arch=arch, bs=bs)
+    eng = train_curve(True, opt, steps, **kw)
+    ref = train_curve(False, opt, steps, bf16=False, **kw)
+    b16 = train_curve(False, opt, steps, bf16=True, **kw)
+    tail = max(10, int(steps * tail_frac))
+    fin = lambda r: sum(r["losses"][-tail:]) / tail  # noqa: E731
+    return {"optimizer": opt, "arch": arch, "batch": bs, "steps": steps, "tail_steps": tail,
+            "engine_final_loss": fin(eng), "reference_final_loss": fin(ref), "bf16_torch_final_loss": fin(b16),
             "engine_test_acc": eng["test_acc"], "reference_test_acc": ref["test_acc"],
+            "bf16_torch_test_acc": b16["test_acc"],
             "initial_loss": sum(ref["losses"][:5]) / 5,
-            "engine_s": eng["seconds"], "reference_s": ref["seconds"],
-            "engine_curve": eng["losses"][::5], "reference_curve": ref["losses"][::5]}
+            "engine_s": eng["seconds"], "reference_s": ref["seconds"], "bf16_torch_s": b16["seconds"],
+            "engine_curve": eng["losses"][::5], "reference_curve": ref["losses"][::5],
+            "bf16_torch_curve": b16["losses"][::5]}
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--steps", type=int, default=300)
     ap.add_argument("--opts", default="madgrad,ngd")
+    ap.add_argument("--arch", default="resnet18")
+    ap.add_argument("--bs", type=int, default=128)
     ap.add_argument("--out", default=None)
     a = ap.parse_args()
-    res = [compare(o, a.steps) for o in a.opts.split(",")]
+    res = [compare(o, a.steps, arch=a.arch, bs=a.bs) for o in a.opts.split(",")]
     for r in res:
         print(f"{r['optimizer']}: final loss engine {r['engine_final_loss']:.4f} vs fp32 {r['reference_final_loss']:.4f}"
               f" (start {r['initial_loss']:.3f}); test acc engine {r['engine_test_acc']:.3f} vs fp32 "
-              f"{r['reference_test_acc']:.3f}; {r['engine_s']:.1f} s vs {r['reference_s']:.1f} s", flush=True)
+              f"{r['reference_test_acc']:.3f}; bf16 torch loss {r['bf16_torch_final_loss']:.4f} acc "
+              f"{r['bf16_torch_test_acc']:.3f}; {r['engine_s']:.1f} s vs {r['reference_s']:.1f} s", flush=True)
     if a.out:
         os.makedirs(os.path.dirname(os.path.abspath(a.out)), exist_ok=True)
         with open(a.out, "w") as f:

@@ -1,6 +1,13 @@
 """Convergence parity of the bf16 HIP engine with the fp32 PyTorch path over 300 optimizer
-steps of ResNet-18 on a learnable synthetic CIFAR task (scripts/convergence.py; VERDICT r3
-#7b).  Real CIFAR-10 is not available offline: parity on it is unpinned."""
+steps on a learnable synthetic CIFAR task (scripts/convergence.py; VERDICT r3 #7b, r4 #7).
+
+The error budget is what bf16 arithmetic alone costs: a third run, plain PyTorch under bf16
+autocast (FDT_NATIVE=0) from the same weights on the same batches.  The engine must land at
+most twice as far from the fp32 run as that run does (plus a small epsilon for the step-to-
+step noise of a 60-step loss mean), on the final loss AND the held-out accuracy -- no
+absolute floor.  ResNet-18 (both optimizers) and ResNet-50 at batch 128, i.e. through the
+shipped tile table's batch-128 entries (the 8-GPU per-GPU batch).  Real CIFAR-10 is not
+available offline: parity on it is unpinned (reference README.md:56-73)."""
 import os
 import sys
 
@@ -10,15 +17,22 @@ pytestmark = pytest.mark.gpu
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
+EPS_LOSS = 0.02   # absolute, on a mean over the last 60 steps
+EPS_ACC = 0.01    # 10 of 1024 held-out samples
 
-@pytest.mark.parametrize("opt", ["madgrad", "ngd"])
-def test_engine_converges_like_fp32_reference(cuda, opt):
+
+@pytest.mark.parametrize("opt,arch", [("madgrad", "resnet18"), ("ngd", "resnet18"), ("madgrad", "resnet50")])
+def test_engine_converges_like_fp32_reference(cuda, opt, arch):
     from scripts.convergence import compare
-    r = compare(opt, 300)
+    r = compare(opt, 300, arch=arch, bs=128)
     print({k: v for k, v in r.items() if not k.endswith("curve")})
-    # both runs learn the task ...
-    assert r["reference_final_loss"] < 0.5 * r["initial_loss"], r["reference_final_loss"]
-    assert r["engine_final_loss"] < 0.5 * r["initial_loss"], r["engine_final_loss"]
-    # ... to the same place: final loss (mean of the last 30 steps) and held-out accuracy
-    assert abs(r["engine_final_loss"] - r["reference_final_loss"]) <= max(0.1, 0.3 * r["reference_final_loss"])
-    assert abs(r["engine_test_acc"] - r["reference_test_acc"]) <= 0.05
+    # every run learns the task ...
+    for k in ("reference_final_loss", "engine_final_loss", "bf16_torch_final_loss"):
+        assert r[k] < 0.5 * r["initial_loss"], (k, r[k])
+    # ... and the engine lands as close to fp32 as bf16 arithmetic allows
+    d_loss = abs(r["engine_final_loss"] - r["reference_final_loss"])
+    b_loss = abs(r["bf16_torch_final_loss"] - r["reference_final_loss"])
+    assert d_loss <= 2 * b_loss + EPS_LOSS, (d_loss, b_loss)
+    d_acc = abs(r["engine_test_acc"] - r["reference_test_acc"])
+    b_acc = abs(r["bf16_torch_test_acc"] - r["reference_test_acc"])
+    assert d_acc <= 2 * b_acc + EPS_ACC, (d_acc, b_acc)
