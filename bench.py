@@ -227,7 +227,10 @@ def _sharding_fields(tr, rec):
             from faster_distributed_training_amd.parallel import graphs
             cfg["bwd_graph_segments"] = len(states[0].segments)
             cfg["bwd_captured_collectives"] = int(getattr(states[0].rec, "captured", 0))
-            cfg["graph_comm"] = graphs.DETACHED_MODE
+            cfg["graph_comm"] = graphs.comm_status()
+    if tr.reducer is not None or getattr(tr, "zero", None) is not None:
+        from faster_distributed_training_amd.parallel import graphs
+        cfg["graph_comm"] = graphs.comm_status()
     if tr.fsdp is not None:
         cfg["fsdp_units"] = len(tr.fsdp.units)
         cfg["fsdp_wrap"] = "model" if len(tr.fsdp.units) == 1 and tr.fsdp.units[0].name == "" else "per-unit"

@@ -811,4 +811,11 @@ class _BodyWithDummy(torch.autograd.Function):
         else:
             st.g.copy_(g)
         st.rec.replay()
+        if st.rec.needs_check:
+            # first replay of a backward whose bucket all-reduces were captured in-graph:
+            # checked against eager all-reduces (parallel/graphs.py); the checking graph (it
+            # snapshots every bucket) is dropped and the next step recaptures the backward --
+            # in capture mode, or with cuts if the check failed
+            st.rec.check_collectives()
+            st.stage, st.rec, st.segments = "fwd", None, None
         return None, None, None, None

@@ -159,12 +159,24 @@ class BucketReducer:
         # extra pass over the bucket, a world-1 artifact that a ring all-reduce at N > 1 does
         # not have: profiles/r4/kstats_bs128_{plain,ddp}.txt)
         op = dist.ReduceOp.AVG if (self.use_avg and self.ws > 1) else dist.ReduceOp.SUM
+        capturing = torch.cuda.is_available() and torch.cuda.is_current_stream_capturing()
+        rec = graphs.active() if capturing else None
+        if rec is not None and rec.checking:
+            # in-graph collective check (graphs.py): snapshot the bucket in stream order right
+            # before its captured all-reduce; compared with an eager all-reduce after replay
+            def fix(ref, s=s, e=e, buf=buf):
+                buf.copy_(ref)
+                if self.wire is not None:
+                    self.flat.grad[s:e].copy_(ref)
+            rec.checks.append((buf.clone(), buf, op, self.pg, fix))
         work = dist.all_reduce(buf, op=op, group=self.pg, async_op=True)
-        if torch.cuda.is_available() and torch.cuda.is_current_stream_capturing():
+        if capturing:
             self.in_graph.add(b)
 
-            def join(w=work, s=s, e=e):
+            def join(w=work, s=s, e=e, buf=buf):
                 w.wait()
+                if graphs.CORRUPT_FOR_TEST:
+                    buf.add_(1.0)  # (test hook: a broken in-graph collective)
                 if self.wire is not None:
                     self.flat.grad[s:e].copy_(self.wire[s:e])
             return join

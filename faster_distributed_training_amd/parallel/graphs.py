@@ -40,7 +40,42 @@ _ACTIVE = None
 #            (round-3 scheme: ~25-50 us of compute-queue idle per cut, profiles/r3s3/).
 # (An external event-record node, the CUDA idiom for "start this stream mid-graph", is refused
 # by torch on ROCm: "External events are disallowed in rocm".)
-DETACHED_MODE = os.environ.get("FDT_GRAPH_COMM", "cut")
+#
+# FDT_GRAPH_COMM selects: "auto" (default) = "capture", CHECKED IN-RUN: the first backward captured
+# with collectives inside also snapshots every bucket right before its in-graph all-reduce; after
+# that graph's first replay each bucket's in-graph result is compared with an eager all-reduce of
+# its snapshot (same data, same group).  Equal: the process keeps capture mode (the checking graph
+# is dropped and the backward recaptured without snapshots).  Different on any rank: the step's
+# buckets are overwritten with the eager results, the process switches to "cut" for the rest of
+# the run (no restart: the owner just recaptures) and ``STATUS`` says "cut(fallback)" -- bench.py
+# reports it as ``graph_comm``.  "capture" = capture unchecked, "cut" = always cut.
+_REQUESTED = os.environ.get("FDT_GRAPH_COMM", "auto")
+DETACHED_MODE = "cut" if _REQUESTED == "cut" else "capture"
+CHECK = _REQUESTED == "auto"
+# "unchecked" until the check ran; then "capture" | "capture(order-tolerant)" | "cut(fallback)";
+# "cut" / "capture(unchecked)" when FDT_GRAPH_COMM forces a mode
+STATUS = {"auto": "unchecked", "capture": "capture(unchecked)"}.get(_REQUESTED, "cut")
+# test hook (tests/test_distributed_gpu.py): the captured join of every bucket corrupts its
+# all-reduced buffer, as a broken in-graph collective would -- the check must fall back
+CORRUPT_FOR_TEST = os.environ.get("FDT_GRAPH_COMM_CORRUPT", "0") == "1"
+
+
+def comm_status():
+    """What the detached collectives of this process do now (bench JSON ``graph_comm``)."""
+    return STATUS if DETACHED_MODE == "capture" or STATUS == "cut(fallback)" else "cut"
+
+
+def checking():
+    """True while the in-graph collective check is still to be done in this process."""
+    return CHECK and DETACHED_MODE == "capture" and STATUS == "unchecked"
+
+
+def reset_check(requested: str = "auto"):
+    """(tests) re-arm the mode selection as if FDT_GRAPH_COMM were ``requested``."""
+    global DETACHED_MODE, CHECK, STATUS
+    DETACHED_MODE = "cut" if requested == "cut" else "capture"
+    CHECK = requested == "auto"
+    STATUS = {"auto": "unchecked", "capture": "capture(unchecked)"}.get(requested, "cut")
 
 
 def active():
@@ -86,6 +121,10 @@ class Recorder:
         self.foreign_cuts = 0  # cuts requested from a stream other than the capture stream
         self.joiners = []      # captured detached actions of the open segment, joined at its end
         self.captured = 0      # detached actions captured on a side branch (no cut)
+        # in-graph collective check (module docstring, FDT_GRAPH_COMM=auto): collectives captured
+        # while ``checking`` register (snapshot, result buffer, op, group, fix) here
+        self.checking = checking()
+        self.checks = []
 
     def begin(self):
         if self.stream is None:
@@ -136,6 +175,48 @@ class Recorder:
             graph.replay()
             for a in acts:
                 a()
+
+    @property
+    def needs_check(self):
+        return self.checking and bool(self.checks)
+
+    def check_collectives(self):
+        """After the FIRST replay of a checking capture: compare every captured collective's
+        result with an eager all-reduce of its pre-collective snapshot.  Every rank runs the
+        same checks in the same order (same capture), then agrees on the verdict (MAX).
+        Returns True when capture mode stands; on a mismatch the buckets of this step get the
+        eager results and the process falls back to cut mode.  Either way the caller drops
+        this recorder's graphs and recaptures (without snapshots)."""
+        global DETACHED_MODE, STATUS
+        import torch.distributed as dist
+        torch.cuda.current_stream().synchronize()
+        worst, exact, pg = 0.0, True, None
+        for shadow, buf, op, group, fix in self.checks:
+            ref = shadow.clone()
+            dist.all_reduce(ref, op=op, group=group)
+            pg = group
+            if not torch.equal(ref, buf):
+                exact = False
+                scale = float(ref.float().abs().max()) or 1.0
+                worst = max(worst, float((ref.float() - buf.float()).abs().max()) / scale)
+                fix(ref)
+        verdict = torch.tensor([worst, 0.0 if exact else 1.0], dtype=torch.float64, device=self.stream.device)
+        dist.all_reduce(verdict, op=dist.ReduceOp.MAX, group=pg)
+        worst, inexact = float(verdict[0]), bool(verdict[1] > 0)
+        self.checks = []
+        self.checking = False
+        # (a sum in another order differs in the last bits; a broken hand-off does not stop there)
+        if not inexact:
+            STATUS = "capture"
+        elif worst <= 1e-5:
+            STATUS = "capture(order-tolerant)"
+        else:
+            STATUS = "cut(fallback)"
+            DETACHED_MODE = "cut"
+            if dist.get_rank() == 0:
+                print(f"[graphs] in-graph collectives disagree with eager all-reduce (max rel diff {worst:.3g}): "
+                      f"falling back to graph cuts for this run", flush=True)
+        return DETACHED_MODE == "capture"
 
 
 class recording:

@@ -243,6 +243,11 @@ class TransformerTrainer:
         wd = cfg.weight_decay
         if kind == "ngd":
             opt = NGD(self.space, lr=lr, weight_decay=wd or 0.0)
+            if self.zero is not None and self.zero.ws > 1 and "FDT_NGD_GRAPHS" not in os.environ:
+                # as the ResNet trainer (resnet_trainer.py _build_optimizer): a rank preconditions
+                # ~1/world of the parameters, so its NGD step is launch-bound and replays as HIP
+                # graphs; the full-size step (one GPU) stays eager (GPU-bound)
+                opt.graphs = True
         elif kind == "mirror_madgrad":
             opt = MirrorMADGRAD(self.space, lr=lr, momentum=0.9, weight_decay=wd or 0.0)
         elif kind == "madgrad":
@@ -375,6 +380,13 @@ class TransformerTrainer:
             self._graphs[key] = ent = st
         lam = self._graph_fill(ent, tokens, labels, types, masks)
         ent["replay"]()
+        step = ent.get("step")
+        if step is not None and step.rec.needs_check:
+            # first replay with the bucket all-reduces captured in-graph: checked against eager
+            # all-reduces (parallel/graphs.py); the next step recaptures without the snapshots
+            # (capture mode stands) or with cuts (fallback)
+            step.rec.check_collectives()
+            self._graphs[key] = 2
         return ent["loss"], ent["logits"], ent["perm"], lam
 
     def train_step(self, tokens, labels, types, masks):

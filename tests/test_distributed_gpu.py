@@ -110,6 +110,70 @@ def test_ddp_engine_hip_graphs_two_ranks(cuda, mode):
     run_world(_graph_worker, world=2, native=True, timeout=400, args=(mode,))
 
 
+def _graph_comm_check_worker(rank, world, corrupt):
+    """FDT_GRAPH_COMM=auto (the default): the bucket all-reduces are captured INTO the
+    engine's backward graph, and the first replay is checked against eager all-reduces of a
+    snapshot of the same pre-reduction buckets (parallel/graphs.py).  A sound capture keeps
+    capture mode (one backward graph after the recapture); a broken one (``corrupt``: the
+    captured join damages every reduced bucket) is detected, that step's buckets are repaired
+    from the eager results and the process falls back to cuts -- the gradients of every step
+    equal the uncommunicated ones either way."""
+    import torch.distributed as dist
+    from faster_distributed_training_amd.models import resnet as R
+    from faster_distributed_training_amd.ops import _native
+    from faster_distributed_training_amd.parallel import graphs as G
+    from faster_distributed_training_amd.parallel.ddp import BucketReducer
+    from faster_distributed_training_amd.utils.flat import FlatParams
+    assert dist.get_backend() == "nccl"
+    _native.set_deterministic(True)
+    dev = torch.device("cuda", 0)
+    x, y = _batch(0)
+    x, y = x.to(dev), y.to(dev)
+
+    def grads(model, flat):
+        flat.grad.zero_()
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            out = model(x)
+        F.cross_entropy(out.float(), y).backward()
+
+    torch.manual_seed(0)
+    base = R.resnet18(10).to(dev)
+    base.fast_path = True
+    bflat = FlatParams(base, device=dev)
+    grads(base, bflat)
+    g0 = bflat.grad.clone()
+    G.reset_check("auto")
+    G.CORRUPT_FOR_TEST = corrupt
+    try:
+        torch.manual_seed(0)
+        m = R.resnet18(10).to(dev)
+        m.fast_path = True
+        m.graph_engine = True
+        flat = FlatParams(m, device=dev)
+        red = BucketReducer(flat, m, bucket_mb=1.0, first_bucket_mb=0.25)
+        for it in range(5):
+            grads(m, flat)
+            red.finish()
+            assert G.comm_status() == ("unchecked" if it == 0 else ("cut(fallback)" if corrupt else "capture")), \
+                (it, G.comm_status())
+            err = ((flat.grad - g0).norm() / g0.norm()).item()
+            assert err < 1e-6, (it, err)  # the checked step included: repaired on a mismatch
+        st = list(m._plan._graphs.values())[0]
+        if corrupt:
+            assert len(st.segments) > 1 and st.rec.captured == 0  # recaptured with cuts
+        else:
+            assert len(st.segments) == 1 and st.rec.captured == len(red.buckets) and not st.rec.checks
+        red.remove()
+    finally:
+        G.CORRUPT_FOR_TEST = False
+        G.reset_check("cut")
+
+
+@pytest.mark.parametrize("corrupt", [False, True])
+def test_graph_comm_capture_checked_with_fallback(cuda, corrupt):
+    run_world(_graph_comm_check_worker, world=1, native=True, backend="nccl", timeout=400, args=(corrupt,))
+
+
 def _fsdp_engine_worker(rank, world, offload=False):
     """FSDP full-shard driving the fused ResNet engine stage by stage (gather + per-stage
     weight packing before each stage's forward and backward, reduce-scatter at each stage
@@ -528,3 +592,37 @@ def _zero_ngd_graphs_world2_worker(rank, world):
 
 def test_sharded_ngd_graphs_world2(cuda):
     run_world(_zero_ngd_graphs_world2_worker, world=2, native=True, timeout=600)
+
+
+def _zero_ngd_graphs_transformer_worker(rank, world):
+    """The transformer's sharded NGD at world > 1 replays its optimizer step as HIP graphs
+    too (as the ResNet trainer): two gloo ranks on one GPU, sharded (graphs on
+    by default) vs unsharded NGD (DDP averaging, full preconditioning on every rank) from the
+    same weights on the same batches end at the same parameters."""
+    import torch.distributed as dist
+    from faster_distributed_training_amd.train.transformer_trainer import TransformerConfig, TransformerTrainer
+    torch.cuda.set_device(0)
+    assert dist.get_world_size() == 2
+    base = dict(batch_size=8, synthetic=True, eval=False, plot=False, ngd=True, optimizer="ngd", distributed=True,
+                n_layers=2, d_model=64, heads=4, d_ff=128, d_hidden=128, length_buckets=(64, 128), bucket_mb=1.0,
+                epoch=1, lr=1e-3)
+    runs = {}
+    for shard in (False, True):
+        tr = TransformerTrainer(TransformerConfig(shard_ngd=shard, **base))
+        assert (tr.zero is not None) == shard
+        if shard:
+            assert tr.optimizer.graphs  # the world > 1 default
+        it = iter(tr.train_loader)
+        for _ in range(16):  # 10 init steps, then update / plain steps replayed as graphs
+            loss = tr.train_step(*next(it))
+        torch.cuda.synchronize()
+        assert torch.isfinite(torch.as_tensor(loss)).all().item()
+        if shard:
+            assert tr.optimizer.graph_replays > 0
+        runs[shard] = {k: v.detach().float().clone() for k, v in tr.model.state_dict().items()}
+    for k, v in runs[False].items():
+        assert torch.allclose(runs[True][k], v, rtol=2e-3, atol=2e-4), (k, (runs[True][k] - v).abs().max())
+
+
+def test_sharded_ngd_graphs_transformer_world2(cuda):
+    run_world(_zero_ngd_graphs_transformer_worker, world=2, native=True, timeout=600)
