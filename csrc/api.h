@@ -31,6 +31,13 @@ void affine_fold(uint64_t gy, uint64_t y, uint64_t alpha, uint64_t beta, uint64_
                  int dt, uint64_t stream);
 void residual_act_fwd(uint64_t ya, uint64_t sa, uint64_t ta, uint64_t yb, uint64_t sb, uint64_t tb, uint64_t xid,
                       uint64_t out, uint64_t mask, long M, int C, int act, float alpha, int dt, uint64_t stream);
+// lazy-statistics consumers (bn_math.h LazyStats): the producer's finalize runs inside them
+void act_affine_lazy(uint64_t x, const std::vector<uint64_t>& lz_ptr, const std::vector<double>& lz_val, uint64_t out,
+                     long M, int C, int act, float alpha, int dt, uint64_t stream);
+void residual_act_lazy(uint64_t ya, const std::vector<uint64_t>& la_ptr, const std::vector<double>& la_val,
+                       uint64_t yb, const std::vector<uint64_t>& lb_ptr, const std::vector<double>& lb_val,
+                       uint64_t sb, uint64_t tb, uint64_t xid, uint64_t out, uint64_t mask, long M, int C, int act,
+                       float alpha, int dt, uint64_t stream);
 void residual_act_bwd(uint64_t g, uint64_t out, uint64_t mask, uint64_t ya, uint64_t yb, uint64_t gpre, uint64_t part,
                       int part_rows, long M, int C, int act, float alpha, int dt, uint64_t stream, int ghw);
 // deterministic mode (common.h): no-wrap statistics slots, ordered split-K sums
@@ -93,10 +100,13 @@ void conv_igemm(uint64_t x, uint64_t x2, uint64_t ps, uint64_t pt, uint64_t pg, 
                 int Wi, int Cx, int Ho, int Wo, int S, const std::vector<int>& dh, const std::vector<int>& dw,
                 const std::vector<int>& wt, int Cout, int ldw, int Hout, int Wout, int OS, int oy, int ox, int pro,
                 int pro_act, float pro_alpha, int epi, int epi_act, float epi_alpha, int BM, int BN, int BK, int nsplit,
-                uint64_t slab, uint64_t cnt, int kg, uint64_t stream);
+                uint64_t slab, uint64_t cnt, int kg, uint64_t stream, const std::vector<uint64_t>& lz_ptr,
+                const std::vector<double>& lz_val);
 void conv_igemm_join(uint64_t y, uint64_t r, uint64_t s, uint64_t t, uint64_t s2, uint64_t t2, uint64_t w, uint64_t out,
                      uint64_t part, int part_rows, uint64_t jout, uint64_t jmask, long Nb, int H, int W, int Cx, int Cout,
-                     int ldw, int BM, int BN, int BK, int nsplit, uint64_t slab, uint64_t cnt, int kg, uint64_t stream);
+                     int ldw, int BM, int BN, int BK, int nsplit, uint64_t slab, uint64_t cnt, int kg, uint64_t stream,
+                     const std::vector<uint64_t>& lz1_ptr, const std::vector<double>& lz1_val,
+                     const std::vector<uint64_t>& lz2_ptr, const std::vector<double>& lz2_val);
 void ffn_gemm(uint64_t x, uint64_t w, uint64_t out, long M, int K, int N, int epi, uint64_t bias, uint64_t out2,
               uint64_t a_in, uint64_t gb, float p, uint64_t seed, uint64_t seed_ptr, int BM, int BN, int BK, int kg,
               uint64_t stream);

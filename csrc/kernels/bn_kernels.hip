@@ -518,6 +518,99 @@ __global__ __launch_bounds__(kBlk) void residual_act_bwd_kernel(const T* __restr
   }
 }
 
+// ------------------------------------------------------------------ lazy-statistics consumers
+// The finalize of the producer's batch statistics moves INTO its elementwise consumer: every
+// workgroup finalises all C channels from the slot rows into LDS (workgroup 0 also writes the
+// unit's s / t / saved mean / sd, bn_math.h LazyStats), then streams.  One launch instead of
+// finalize + pass.  The first two vectors of each thread are loaded BEFORE the slot reduction
+// (independent of it) so their latency overlaps it; the grid is sized so the per-workgroup slot
+// reads stay a small fraction of the streamed bytes (host: lazy_grid).
+template <typename T>
+__global__ __launch_bounds__(kBlk) void act_affine_lazy_kernel(const T* __restrict__ x, const LazyStats L,
+                                                              T* __restrict__ out, long nvec, int C, int act, float alpha) {
+  extern __shared__ float sst[];  // [2][C]
+  const long stride = (long)gridDim.x * blockDim.x;
+  long v = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  float a0[8], a1[8];
+  const bool h0 = v < nvec, h1 = v + stride < nvec;
+  if (h0) Vec8<T>::load(x + v * 8, a0);
+  if (h1) Vec8<T>::load(x + (v + stride) * 8, a1);
+  lazy_fill<kBlk>(L, C, sst, sst + C, threadIdx.x, blockIdx.x == 0);
+  __syncthreads();
+  const unsigned G = (unsigned)(C / 8);
+  auto fin = [&](long w, float* a) {
+    const int c = (int)((unsigned long)w % G) * 8;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) a[i] = act_fwd(fmaf(a[i], sst[c + i], sst[C + c + i]), act, alpha);
+    Vec8<T>::store(out + w * 8, a);
+  };
+  if (h0) fin(v, a0);
+  if (h1) fin(v + stride, a1);
+  for (v += 2 * stride; v < nvec; v += stride) {
+    float a[8];
+    Vec8<T>::load(x + v * 8, a);
+    fin(v, a);
+  }
+}
+
+// out = act(ya*sa + ta + (yb ? yb*sb + tb : xid)); (sa, ta) from La; (sb, tb) from Lb when lazy,
+// else the finalised vectors sb / tb
+template <typename T>
+__global__ __launch_bounds__(kBlk) void residual_act_lazy_kernel(const T* __restrict__ ya, const LazyStats La,
+                                                                const T* __restrict__ yb, const LazyStats Lb,
+                                                                const float* __restrict__ sb,
+                                                                const float* __restrict__ tb,
+                                                                const T* __restrict__ xid, T* __restrict__ out,
+                                                                uint8_t* __restrict__ mask, long nvec, int C, int act,
+                                                                float alpha) {
+  extern __shared__ float sst[];  // [4][C]: sa ta sb tb
+  const long stride = (long)gridDim.x * blockDim.x;
+  long v = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const T* src2 = yb ? yb : xid;
+  float a0[8], b0[8];
+  const bool h0 = v < nvec;
+  if (h0) {
+    Vec8<T>::load(ya + v * 8, a0);
+    Vec8<T>::load(src2 + v * 8, b0);
+  }
+  const bool w0 = blockIdx.x == 0;
+  lazy_fill<kBlk>(La, C, sst, sst + C, threadIdx.x, w0);
+  if (yb) {
+    if (Lb.base) {
+      lazy_fill<kBlk>(Lb, C, sst + 2 * C, sst + 3 * C, threadIdx.x, w0);
+    } else {
+      for (int c = threadIdx.x; c < C; c += kBlk) {
+        sst[2 * C + c] = sb[c];
+        sst[3 * C + c] = tb[c];
+      }
+    }
+  }
+  __syncthreads();
+  const unsigned G = (unsigned)(C / 8);
+  auto fin = [&](long w, float* a, float* b) {
+    const int c = (int)((unsigned long)w % G) * 8;
+    if (yb) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) b[i] = fmaf(b[i], sst[2 * C + c + i], sst[3 * C + c + i]);
+    }
+    uint32_t m = 0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      a[i] = act_fwd(fmaf(a[i], sst[c + i], sst[C + c + i]) + b[i], act, alpha);
+      m |= (a[i] > 0.f ? 1u : 0u) << i;
+    }
+    Vec8<T>::store(out + w * 8, a);
+    if (mask) mask[w] = (uint8_t)m;
+  };
+  if (h0) fin(v, a0, b0);
+  for (v += stride; v < nvec; v += stride) {
+    float a[8], b[8];
+    Vec8<T>::load(ya + v * 8, a);
+    Vec8<T>::load(src2 + v * 8, b);
+    fin(v, a, b);
+  }
+}
+
 // ------------------------------------------------------------------ launchers
 inline int ew_grid(long nvec) {
   long g = (nvec + kBlk - 1) / kBlk;
@@ -704,6 +797,58 @@ void residual_act_fwd(uint64_t ya, uint64_t sa, uint64_t ta, uint64_t yb, uint64
     kern<<<(int)g, kBlk, 0, as_stream(stream)>>>(
         P<const T>(ya), P<const float>(sa), P<const float>(ta), P<const T>(yb), P<const float>(sb), P<const float>(tb),
         P<const T>(xid), P<T>(out), P<uint8_t>(mask), nvec, C / 8, act, alpha);
+  });
+  FDT_LAUNCH_CHECK();
+}
+
+// grid of a lazy-statistics consumer: per-workgroup slot reads (rows x nq x C fp32) at most
+// ~1/4 of the bytes the pass streams, at least 32 workgroups, at most the plain pass's grid
+static int lazy_grid(long nvec, long stream_bytes, long stats_bytes) {
+  long g = stream_bytes / (4 * (stats_bytes > 0 ? stats_bytes : 1));
+  const long cap = ew_grid(nvec);
+  if (g > cap) g = cap;
+  if (g < 32) g = 32;
+  if (g > (nvec + kBlk - 1) / kBlk) g = (nvec + kBlk - 1) / kBlk;
+  return (int)(g < 1 ? 1 : g);
+}
+
+void act_affine_lazy(uint64_t x, const std::vector<uint64_t>& lz_ptr, const std::vector<double>& lz_val, uint64_t out,
+                     long M, int C, int act, float alpha, int dt, uint64_t stream) {
+  FDT_CHECK(C % 8 == 0 && C <= 8192, "act_affine_lazy: C % 8 == 0, C <= 8192");
+  const LazyStats L = make_lazy(lz_ptr, lz_val);
+  FDT_CHECK(L.base != nullptr, "act_affine_lazy: lazy statistics required");
+  const long nvec = M * (long)C / 8;
+  if (nvec == 0) return;
+  const int T = dt == kF32 ? 4 : 2;
+  const int g = lazy_grid(nvec, 2 * M * (long)C * T, (long)L.rows * 2 * C * 4);
+  const size_t lds = (size_t)2 * C * sizeof(float);
+  DISPATCH_T(dt, {
+    act_affine_lazy_kernel<T><<<g, kBlk, lds, as_stream(stream)>>>(P<const T>(x), L, P<T>(out), nvec, C, act, alpha);
+  });
+  FDT_LAUNCH_CHECK();
+}
+
+void residual_act_lazy(uint64_t ya, const std::vector<uint64_t>& la_ptr, const std::vector<double>& la_val,
+                       uint64_t yb, const std::vector<uint64_t>& lb_ptr, const std::vector<double>& lb_val,
+                       uint64_t sb, uint64_t tb, uint64_t xid, uint64_t out, uint64_t mask, long M, int C, int act,
+                       float alpha, int dt, uint64_t stream) {
+  FDT_CHECK(C % 8 == 0 && C <= 4096, "residual_act_lazy: C % 8 == 0, C <= 4096");
+  FDT_CHECK((yb != 0) != (xid != 0), "residual_act_lazy: a projection shortcut yb or an identity xid");
+  FDT_CHECK(mask == 0 || act == kActRelu, "the activation bit mask is for ReLU joins");
+  const LazyStats La = make_lazy(la_ptr, la_val);
+  const LazyStats Lb = make_lazy(lb_ptr, lb_val);
+  FDT_CHECK(La.base != nullptr, "residual_act_lazy: the residual branch's statistics must be lazy");
+  FDT_CHECK(yb == 0 || Lb.base != nullptr || (sb != 0 && tb != 0), "residual_act_lazy: shortcut statistics");
+  const long nvec = M * (long)C / 8;
+  if (nvec == 0) return;
+  const int T = dt == kF32 ? 4 : 2;
+  const long sbytes = ((long)La.rows + (Lb.base ? Lb.rows : 0)) * 2 * C * 4;
+  const int g = lazy_grid(nvec, 3 * M * (long)C * T, sbytes);
+  const size_t lds = (size_t)4 * C * sizeof(float);
+  DISPATCH_T(dt, {
+    residual_act_lazy_kernel<T><<<g, kBlk, lds, as_stream(stream)>>>(
+        P<const T>(ya), La, P<const T>(yb), Lb, P<const float>(sb), P<const float>(tb), P<const T>(xid), P<T>(out),
+        P<uint8_t>(mask), nvec, C, act, alpha);
   });
   FDT_LAUNCH_CHECK();
 }

@@ -9,6 +9,7 @@
 // save_mean[c], save_aux[c]: mode 0 -> sd ; modes 1/2 -> invstd
 #pragma once
 #include "common.h"
+#include <vector>
 
 namespace fdt {
 
@@ -28,43 +29,141 @@ struct FinArgs {
   float* save_aux;
 };
 
-__device__ __forceinline__ void bn_finalize_channel(const FinArgs& f, int c, double S, double Q) {
+// (s, t) of channel c from its fp64 sums; ``write``: also the unit's outputs (out_s / out_t,
+// saved mean / aux, running statistics, num_batches_tracked) -- exactly one thread per channel
+// may write them
+__device__ __forceinline__ void bn_finalize_st(const FinArgs& f, int c, double S, double Q, float& s_out,
+                                               float& t_out, bool write) {
+  double sc, tt, mean, aux;
   if (f.mode == 0) {
-    const double mean = S / f.count;
+    mean = S / f.count;
     double var = (Q - S * mean) / (f.count - 1.0);
     if (var < 0.0) var = 0.0;
-    const double sd = sqrt(var);
-    const double sc = 1.0 / (sd + (double)f.eps);
-    f.out_s[c] = (float)sc;
-    f.out_t[c] = (float)(-mean * sc);
-    f.save_mean[c] = (float)mean;
-    f.save_aux[c] = (float)sd;
+    aux = sqrt(var);
+    sc = 1.0 / (aux + (double)f.eps);
+    tt = -mean * sc;
   } else if (f.mode == 1) {
-    const double mean = S / f.count;
+    mean = S / f.count;
     double m2 = Q - S * mean;
     if (m2 < 0.0) m2 = 0.0;
     const double var_b = m2 / f.count;
     const double var_u = f.count > 1.0 ? m2 / (f.count - 1.0) : var_b;
-    const double inv = 1.0 / sqrt(var_b + (double)f.eps);
+    aux = 1.0 / sqrt(var_b + (double)f.eps);
     const double g = f.gamma ? (double)f.gamma[c] : 1.0, b = f.beta ? (double)f.beta[c] : 0.0;
-    f.out_s[c] = (float)(g * inv);
-    f.out_t[c] = (float)(b - mean * g * inv);
-    f.save_mean[c] = (float)mean;
-    f.save_aux[c] = (float)inv;
-    if (f.run_mean) {
+    sc = g * aux;
+    tt = b - mean * g * aux;
+    if (write && f.run_mean) {
       f.run_mean[c] = (float)((1.0 - f.momentum) * f.run_mean[c] + f.momentum * mean);
       f.run_var[c] = (float)((1.0 - f.momentum) * f.run_var[c] + f.momentum * var_u);
     }
-    if (f.nbt && c == 0) f.nbt[0] += 1;
+    if (write && f.nbt && c == 0) f.nbt[0] += 1;
   } else {
-    const double mean = f.run_mean[c];
-    const double inv = 1.0 / sqrt((double)f.run_var[c] + (double)f.eps);
+    mean = f.run_mean[c];
+    aux = 1.0 / sqrt((double)f.run_var[c] + (double)f.eps);
     const double g = f.gamma ? (double)f.gamma[c] : 1.0, b = f.beta ? (double)f.beta[c] : 0.0;
-    f.out_s[c] = (float)(g * inv);
-    f.out_t[c] = (float)(b - mean * g * inv);
-    f.save_mean[c] = (float)mean;
-    f.save_aux[c] = (float)inv;
+    sc = g * aux;
+    tt = b - mean * g * aux;
   }
+  s_out = (float)sc;
+  t_out = (float)tt;
+  if (write) {
+    f.out_s[c] = s_out;
+    f.out_t[c] = t_out;
+    f.save_mean[c] = (float)mean;
+    f.save_aux[c] = (float)aux;
+  }
+}
+
+__device__ __forceinline__ void bn_finalize_channel(const FinArgs& f, int c, double S, double Q) {
+  float s, t;
+  bn_finalize_st(f, c, S, Q, s, t, true);
+}
+
+// Lazy batch statistics (FusedConvBN units, mode 0): the producer's slot rows and the unit's
+// outputs live in ONE region  [rows][2][C] slots | s[C] | t[C] | save_mean[C] | save_aux[C]
+// (C = the unit's channels); the slots are finalised by the unit's CONSUMER while staging its
+// own inputs (the channels it needs; rows summed in fp64 in a fixed order) instead of by a
+// standalone finalize launch between the two, and the consumer's workgroup 0 also writes the
+// four output vectors (the backward reads them).  base == nullptr: not lazy (the consumer reads
+// the finalised s / t).  Compact on purpose: it travels in the conv kernels' arguments (SGPRs).
+struct LazyStats {
+  float* base;
+  int rows;
+  float eps;
+  float count;  // rows of the producer's output (N*H*W), exact in fp32 up to 2^24
+};
+
+// (s, t) of channel c; ``write``: also the four output vectors (one writer per channel)
+__device__ __forceinline__ void lazy_finish(const LazyStats& L, int C, int c, double S, double Q, float& s, float& t,
+                                            bool write) {
+  const double n = (double)L.count;
+  const double mean = S / n;
+  double var = (Q - S * mean) / (n - 1.0);
+  if (var < 0.0) var = 0.0;
+  const float sd = (float)sqrt(var);
+  s = 1.f / (sd + L.eps);  // unbiased sd + eps (resnet.py:75-100), fp32 reciprocal
+  t = (float)(-mean) * s;
+  if (write) {
+    float* o = L.base + (long)L.rows * 2 * C;
+    o[c] = s;
+    o[C + c] = t;
+    o[2 * C + c] = (float)mean;
+    o[3 * C + c] = sd;
+  }
+}
+
+__device__ __forceinline__ void lazy_st(const LazyStats& L, int C, int c, float& s, float& t, bool write) {
+  double S = 0.0, Q = 0.0;
+  const float* p = L.base;
+  for (int r = 0; r < L.rows; ++r) {
+    S += (double)p[(long)(2 * r) * C + c];
+    Q += (double)p[(long)(2 * r + 1) * C + c];
+  }
+  lazy_finish(L, C, c, S, Q, s, t, write);
+}
+
+// every channel of L into s_out[C] / t_out[C] (LDS) by NT threads: four channels per thread and
+// pass, every slot-row load of a pass issued before the sums
+template <int NT>
+__device__ __forceinline__ void lazy_fill(const LazyStats& L, int C, float* s_out, float* t_out, int tid, bool w0) {
+  for (int c0 = tid; c0 < C; c0 += 4 * NT) {
+    double S[4] = {0.0, 0.0, 0.0, 0.0}, Q[4] = {0.0, 0.0, 0.0, 0.0};
+    for (int r = 0; r < L.rows; ++r) {
+      const float* p = L.base + (long)(2 * r) * C;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int c = c0 + NT * k;
+        if (c < C) {
+          S[k] += (double)p[c];
+          Q[k] += (double)p[C + c];
+        }
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int c = c0 + NT * k;
+      if (c < C) {
+        float sv, tv;
+        lazy_finish(L, C, c, S[k], Q[k], sv, tv, w0);
+        s_out[c] = sv;
+        t_out[c] = tv;
+      }
+    }
+  }
+}
+
+// host: LazyStats from the Python launch lists -- ptr = [region base], val = [rows, eps, count];
+// empty lists = not lazy
+inline LazyStats make_lazy(const std::vector<uint64_t>& ptr, const std::vector<double>& val) {
+  LazyStats L{};
+  if (ptr.empty()) return L;
+  FDT_CHECK(ptr.size() == 1 && val.size() == 3, "lazy statistics: [base] + [rows, eps, count]");
+  L.base = P<float>(ptr[0]);
+  L.rows = (int)val[0];
+  L.eps = (float)val[1];
+  L.count = (float)val[2];
+  FDT_CHECK(L.base != nullptr && L.rows >= 1 && L.count > 1.f && val[2] < 16777216.0, "lazy statistics: values");
+  return L;
 }
 
 // BN-backward coefficients from the per-channel reductions (g_s, g_t) of dL/dy; see the mode

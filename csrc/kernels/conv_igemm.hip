@@ -13,14 +13,20 @@ static void conv_igemm_impl(uint64_t x, uint64_t x2, uint64_t ps, uint64_t pt, u
                             const std::vector<int>& dh, const std::vector<int>& dw, const std::vector<int>& wt, int Cout,
                             int ldw, int Hout, int Wout, int OS, int oy, int ox, int pro, int pro_act, float pro_alpha,
                             int epi, int epi_act, float epi_alpha, int BM, int BN, int BK, int nsplit, uint64_t slab,
-                            uint64_t cnt, uint64_t pt2, uint64_t pout, uint64_t pmask, int kg, uint64_t stream) {
+                            uint64_t cnt, uint64_t pt2, uint64_t pout, uint64_t pmask, int kg, uint64_t stream,
+                            const LazyStats& ls1 = LazyStats{}, const LazyStats& ls2 = LazyStats{}) {
   using namespace conv;
   ConvArgs a{};
+  a.ls1 = ls1;
+  a.ls2 = ls2;
+  FDT_CHECK(!ls1.base || pro == kProAffineAct || pro == kProJoin, "lazy statistics need the affine / join prologue");
+  FDT_CHECK(!ls2.base || pro == kProJoin, "lazy shortcut statistics: join prologue");
   a.pt2 = P<const float>(pt2);
   a.pout = P<bf16>(pout);
   a.pmask = P<uint8_t>(pmask);
   if (pro == kProJoin) {
-    FDT_CHECK(x2 != 0 && pout != 0 && ps != 0 && pt != 0 && (pg == 0 || pt2 != 0), "join prologue: y, r, s, t, out");
+    FDT_CHECK(x2 != 0 && pout != 0 && ((ps != 0 && pt != 0) || ls1.base) && (pg == 0 || pt2 != 0),
+              "join prologue: y, r, s, t, out");
     FDT_CHECK(dh.size() == 1 && S == 1 && Hi == Ho && Wi == Wo, "join prologue: 1x1 stride-1 convolution only");
   }
   a.x = P<const bf16>(x);
@@ -82,7 +88,7 @@ static void conv_igemm_impl(uint64_t x, uint64_t x2, uint64_t ps, uint64_t pt, u
   hipStream_t st = as_stream(stream);
   if (a.M == 0) return;
   const int act = (pro == kProAffineAct || pro == kProJoin) ? pro_act : ((epi == kEpiActBwd || epi == kEpiJoinBwd) ? epi_act : 0);
-  if (kg == 2 && a.nsplit > 1) kg = 1;  // K groups and split-K are alternatives
+  if (kg == 2 && a.nsplit > 1) kg = 1;  // K groups and split-K are alternatives (kg 4: rotated loop, any split)
   if (kg == 3 && pro != kProNone) kg = 1;  // the LDS-DMA ring cannot apply a prologue
   if (launch_cases_fwd(pro, epi, act, a, BM, BN, BK, kg, pure, st) ||
       launch_cases_fold(pro, epi, act, a, BM, BN, BK, kg, pure, st) ||
@@ -99,11 +105,11 @@ void conv_igemm(uint64_t x, uint64_t x2, uint64_t ps, uint64_t pt, uint64_t pg, 
                 const std::vector<int>& dh, const std::vector<int>& dw, const std::vector<int>& wt, int Cout, int ldw,
                 int Hout, int Wout, int OS, int oy, int ox, int pro, int pro_act, float pro_alpha, int epi, int epi_act,
                 float epi_alpha, int BM, int BN, int BK, int nsplit, uint64_t slab, uint64_t cnt, int kg,
-                uint64_t stream) {
+                uint64_t stream, const std::vector<uint64_t>& lz_ptr, const std::vector<double>& lz_val) {
   FDT_CHECK(pro != conv::kProJoin, "the join prologue goes through conv_igemm_join");
   conv_igemm_impl(x, x2, ps, pt, pg, w, out, part, part_rows, ex, es, et, jmask, jyb, jout, Nb, Hi, Wi, Cx, Ho, Wo, S, dh,
                   dw, wt, Cout, ldw, Hout, Wout, OS, oy, ox, pro, pro_act, pro_alpha, epi, epi_act, epi_alpha, BM, BN, BK,
-                  nsplit, slab, cnt, 0, 0, 0, kg, stream);
+                  nsplit, slab, cnt, 0, 0, 0, kg, stream, make_lazy(lz_ptr, lz_val));
 }
 
 // Forward 1x1 convolution whose operand is the previous residual block's join (PRO_JOIN):
@@ -112,11 +118,12 @@ void conv_igemm(uint64_t x, uint64_t x2, uint64_t ps, uint64_t pt, uint64_t pg, 
 void conv_igemm_join(uint64_t y, uint64_t r, uint64_t s, uint64_t t, uint64_t s2, uint64_t t2, uint64_t w, uint64_t out,
                      uint64_t part, int part_rows, uint64_t jout, uint64_t jmask, long Nb, int H, int W, int Cx, int Cout,
                      int ldw, int BM, int BN, int BK, int nsplit, uint64_t slab, uint64_t cnt, int kg,
-                     uint64_t stream) {
+                     uint64_t stream, const std::vector<uint64_t>& lz1_ptr, const std::vector<double>& lz1_val,
+                     const std::vector<uint64_t>& lz2_ptr, const std::vector<double>& lz2_val) {
   const std::vector<int> z{0};
   conv_igemm_impl(y, r, s, t, s2, w, out, part, part_rows, 0, 0, 0, 0, 0, 0, Nb, H, W, Cx, H, W, 1, z, z, z, Cout, ldw, H,
                   W, 1, 0, 0, conv::kProJoin, kActRelu, 1.f, conv::kEpiStats, 0, 1.f, BM, BN, BK, nsplit, slab, cnt, t2,
-                  jout, jmask, kg, stream);
+                  jout, jmask, kg, stream, make_lazy(lz1_ptr, lz1_val), make_lazy(lz2_ptr, lz2_val));
 }
 
 // Transformer FFN GEMMs on the implicit-GEMM kernel (a token GEMM is a 1x1 convolution over

@@ -130,6 +130,9 @@ struct ConvArgs {
   float* slab;       // split-K partials [tiles][nsplit][TN*TM*4][256] float4
   int* cnt;          // split-K tickets [tiles], zero between launches
   int8_t dh[12], dw[12], wt[12];
+  // lazy batch statistics (bn_math.h): AFFINE_ACT / JOIN take (s, t) -- JOIN's shortcut (s2,
+  // t2) from ls2 -- by finalising the producer's slot rows in the prologue (ps / pt unused)
+  LazyStats ls1, ls2;
   long Nb_HiWi_Cx_bytes;  // bytes of the activation operand(s)
   long w_bytes;           // bytes of the packed weights
 };
@@ -211,13 +214,15 @@ constexpr int kMinWavesPerEU =
     (BM == 128 && BN == 128 && BK == 32 && (PRO == kProNone || (PRO == kProAffineAct && PURE))) ? 4
     : (BM == 128 && BN == 128 && (BK == 32 || (PRO != 2 && PRO != 3))) ? 3 : 1;
 
-// KG: 1 = one 4-wave K group, register-staged 2-deep; 2 = two K groups (see above);
+// KG: 1 = one 4-wave K group, register-staged (legacy K loop, see the main loop); 4 = the same with
+// the rotated K loop (a true 2-deep register prefetch); 2 = two K groups (see above);
 // 3 = one group whose operand tiles move global -> LDS by LDS-DMA (buffer_load ... lds) into a
 // 3-buffer ring, two tiles in flight ACROSS the per-tile barrier (counted vmcnt + raw
 // s_barrier: __syncthreads() would drain every in-flight DMA) -- prologue-free convolutions
 // only (the DMA cannot transform), no staging registers and no ds_write pass.
 template <int BM, int BN, int BK, int PRO, int EPI, bool PURE, int ACT, int KG>
-__global__ __launch_bounds__(256 * (KG == 2 ? 2 : 1), (KG == 1 ? kMinWavesPerEU<BM, BN, BK, PRO, PURE> : 1)) void
+__global__ __launch_bounds__(256 * (KG == 2 ? 2 : 1),
+                             ((KG == 1 || KG == 4) ? kMinWavesPerEU<BM, BN, BK, PRO, PURE> : 1)) void
 igemm_kernel(const ConvArgs a) {
   constexpr bool GL = KG == 3;
   static_assert(!GL || PRO == kProNone, "LDS-DMA staging moves bytes untransformed: prologue-free convolutions only");
@@ -249,7 +254,7 @@ igemm_kernel(const ConvArgs a) {
   // is written for 256 threads); grp selects the group's K tiles and LDS buffers
   const int tid = threadIdx.x & 255, lane = tid & 63, wid = tid >> 6;
   const int grp = KG == 2 ? (int)(threadIdx.x >> 8) : 0;
-  static_assert(KG == 1 || KG == 2 || KG == 3, "one or two K groups, or the LDS-DMA ring");
+  static_assert(KG == 1 || KG == 2 || KG == 3 || KG == 4, "one or two K groups, the LDS-DMA ring, or rotated");
   const int wn = wid & 1, wm = wid >> 1;
   // a tile's splits are consecutive ids -> the same XCD after the remap
   const int rid = xcd_remap(blockIdx.x, a.nbm * a.nbn * a.nsplit);
@@ -550,13 +555,26 @@ igemm_kernel(const ConvArgs a) {
   }
   if (grp == 0) {
     if constexpr (HASPRO) {
-      for (int i = tid; i < a.Cx; i += 256) {
-        pst[i] = a.ps[i];
-        pst[a.Cx + i] = a.pt[i];
-        if constexpr (PRO == kProFold) pst[2 * a.Cx + i] = a.pg ? a.pg[i] : 1.f;
-        if constexpr (PRO == kProJoin) {
-          pst[2 * a.Cx + i] = a.pg ? a.pg[i] : 1.f;
-          pst[3 * a.Cx + i] = a.pg ? a.pt2[i] : 0.f;
+      const bool w0 = blockIdx.x == 0;  // the one workgroup that writes a lazy unit's outputs
+      if (PRO != kProFold && a.ls1.base) {
+        lazy_fill<256>(a.ls1, a.Cx, pst, pst + a.Cx, tid, w0);
+      } else {
+        for (int i = tid; i < a.Cx; i += 256) {
+          pst[i] = a.ps[i];
+          pst[a.Cx + i] = a.pt[i];
+        }
+      }
+      if constexpr (PRO == kProFold) {
+        for (int i = tid; i < a.Cx; i += 256) pst[2 * a.Cx + i] = a.pg ? a.pg[i] : 1.f;
+      }
+      if constexpr (PRO == kProJoin) {
+        if (a.ls2.base) {
+          lazy_fill<256>(a.ls2, a.Cx, pst + 2 * a.Cx, pst + 3 * a.Cx, tid, w0);
+        } else {
+          for (int i = tid; i < a.Cx; i += 256) {
+            pst[2 * a.Cx + i] = a.pg ? a.pg[i] : 1.f;
+            pst[3 * a.Cx + i] = a.pg ? a.pt2[i] : 0.f;
+          }
         }
       }
     }
@@ -576,6 +594,34 @@ igemm_kernel(const ConvArgs a) {
       __builtin_amdgcn_sched_barrier(0);
     }
   }
+  if constexpr (KG == 4) {
+  // Main loop, two K tiles per trip, rotated so that every trip begins exactly as the loop
+  // is entered: tiles kt (SA) and kt+1 (SB) in flight, the older one stored first.  (hipcc's
+  // waitcnt pass merges the loop-entry and back-edge states; with the entry store peeled ahead
+  // of the loop and exits inside the trip -- the legacy form below -- it waits for EVERY
+  // outstanding load, vmcnt(0), at the first LDS store of each trip, draining the tile k+2
+  // prefetch: a 1-deep pipeline.  Which form is faster depends on the layer -- the deeper
+  // pipeline holds the loads' registers longer -- so the tuned table picks per layer: "loop".)
+  int kt = 0;
+  for (; kt + 1 < nkk; kt += 2) {
+    store_tile(SA, 0);                  // tile kt -> buf 0 (SB: kt+1 still in flight)
+    __syncthreads();
+    ld(SA, kt + 2);
+    __builtin_amdgcn_sched_barrier(0);  // keep the prefetch issued ahead of the MFMAs
+    compute(0);
+    store_tile(SB, 1);                  // tile kt+1 -> buf 1 (SA: kt+2 in flight)
+    __syncthreads();
+    ld(SB, kt + 3);
+    __builtin_amdgcn_sched_barrier(0);
+    compute(1);
+  }
+  if (kt < nkk) {  // odd tile count: the last tile
+    store_tile(SA, 0);
+    __syncthreads();
+    compute(0);
+  }
+  } else {
+  // legacy form: tile 0 stored ahead of the loop, exits inside the trip
   if (nkk > 0) {
     store_tile(SA, 0);
     ld(SA, 2);
@@ -583,20 +629,19 @@ igemm_kernel(const ConvArgs a) {
     __syncthreads();
   }
   for (int kt = 0; kt < nkk; kt += 2) {
-    // even tile kt in buf 0; SB holds kt+1, SA holds kt+2 (in flight)
     compute(0);
     if (kt + 1 >= nkk) break;
     store_tile(SB, 1);
     __syncthreads();
     ld(SB, kt + 3);
-    __builtin_amdgcn_sched_barrier(0);  // keep the prefetch issued ahead of the MFMAs
-    // odd tile kt+1 in buf 1; SA holds kt+2, SB holds kt+3 (in flight)
+    __builtin_amdgcn_sched_barrier(0);
     compute(1);
     if (kt + 2 >= nkk) break;
     store_tile(SA, 0);
     __syncthreads();
     ld(SA, kt + 4);
     __builtin_amdgcn_sched_barrier(0);
+  }
   }
   }
 
@@ -930,8 +975,8 @@ template <int PRO, int EPI, int ACT>
 static void launch_tile(const ConvArgs& a, int BM, int BN, int BK, int kg, bool pure, hipStream_t st) {
   const int nkt = (a.K + BK - 1) / BK;
   const size_t nbuf = kg == 3 ? 3 : (nkt > 1 ? 2 : 1);
-  FDT_CHECK(kg == 1 || kg == 3 || (kg == 2 && a.nsplit == 1 && nkt >= 2),
-            "K groups: kg 1 | 2 (2: no split-K, >= 2 K tiles) | 3 (LDS-DMA ring)");
+  FDT_CHECK(kg == 1 || kg == 3 || kg == 4 || (kg == 2 && a.nsplit == 1 && nkt >= 2),
+            "K groups: kg 1 | 2 (2: no split-K, >= 2 K tiles) | 3 (LDS-DMA ring) | 4 (rotated K loop)");
   FDT_CHECK(kg != 3 || PRO == kProNone, "the LDS-DMA ring is for prologue-free convolutions");
   // header (must match the kernel's hdr) + max(K tiles of every K group, epilogue staging
   // [64][BN + 4] fp32, K-group hand-off [BM*BN] fp32)
@@ -947,7 +992,8 @@ static void launch_tile(const ConvArgs& a, int BM, int BN, int BK, int kg, bool 
     if constexpr (PRO == kProNone) {                                                      \
       if (kg == 3) { launch_pure<BM_, BN_, BK_, PRO, EPI, ACT, 3>(a, pure, lds, st); return; } \
     }                                                                                     \
-    launch_pure<BM_, BN_, BK_, PRO, EPI, ACT, 1>(a, pure, lds, st);                       \
+    if (kg == 4) launch_pure<BM_, BN_, BK_, PRO, EPI, ACT, 4>(a, pure, lds, st);          \
+    else launch_pure<BM_, BN_, BK_, PRO, EPI, ACT, 1>(a, pure, lds, st);                  \
     return;                                                                               \
   }
   // two K groups: the tiles the small-M (latency-bound, ~256-workgroup) layers use
@@ -957,6 +1003,7 @@ static void launch_tile(const ConvArgs& a, int BM, int BN, int BK, int kg, bool 
       if (kg == 3) { launch_pure<BM_, BN_, BK_, PRO, EPI, ACT, 3>(a, pure, lds, st); return; }  \
     }                                                                                          \
     if (kg == 2) launch_pure<BM_, BN_, BK_, PRO, EPI, ACT, 2>(a, pure, lds, st);              \
+    else if (kg == 4) launch_pure<BM_, BN_, BK_, PRO, EPI, ACT, 4>(a, pure, lds, st);         \
     else launch_pure<BM_, BN_, BK_, PRO, EPI, ACT, 1>(a, pure, lds, st);                      \
     return;                                                                                    \
   }

@@ -191,6 +191,19 @@ KG_TILES = {(128, 128, 64), (128, 64, 64), (64, 128, 64), (64, 64, 64), (64, 64,
 GLDS = os.environ.get("FDT_CONV_GLDS", "0") == "1"
 
 
+# K-loop form of the implicit-GEMM kernels (conv_igemm_impl.h main loop) for single-group launches:
+# "rot" = the rotated loop with a true 2-deep register prefetch (kg 4), "old" = the legacy loop
+# (hipcc drains the prefetch at every trip); per layer from the tuned entry's "loop", else this
+# default (the legacy form: measured faster for most of the memory-bound batch-1024 layers)
+LOOP = os.environ.get("FDT_CONV_LOOP", "old")
+
+
+def _loop_kg(ent, kgv):
+    """kg 1 -> 4 when the launch takes the rotated K loop"""
+    lp = (ent.get("loop") if ent else None) or LOOP
+    return 4 if (kgv == 1 and lp == "rot") else kgv
+
+
 def _kg(ent, kg, tile3, ns, K, pro=None):
     """K groups of one launch: explicit ``kg``, else the tuned entry's, else 1 (3 = the
     LDS-DMA ring, prologue-free launches only)."""
@@ -263,20 +276,26 @@ def stat_slots(nq: int, C: int, device, M: int | None = None) -> torch.Tensor:
     return torch.zeros(slot_rows(M), nq, C, device=device, dtype=torch.float32)
 
 
+_NOLAZY = ([], [])
+
+
 def conv_fwd(x, wf, shp: ConvShape, s=None, t=None, act=0, alpha=1.0, tile=None, part=None, nsplit=None,
-             fin=None, kg=None):
+             fin=None, kg=None, lazy=None):
     """y = conv(act(x*s+t)) (or conv(x) when s is None and act == 0); returns
     (y [N,Ho,Wo,Cout] bf16, part [STAT_SLOTS,2,Cout] fp32 slots whose row sum is
     (sum y, sum y^2)).  ``part``: a zeroed slot buffer to accumulate into.
     ``fin`` = (fptr, fval): then finalise the batch-norm statistics (stats_finalize
     arguments: gamma beta run_mean run_var nbt s t save_mean save_aux / mode eps momentum
-    count) and re-zero the slots."""
+    count) and re-zero the slots.
+    ``lazy`` = (ptr list, value list) of the INPUT's statistics left in its producer's slot rows
+    (bn_math.h LazyStats): the prologue finalises them itself (s / t unused, written by
+    workgroup 0 for the backward)."""
     nat = _native.native()
     N, H, W, C = x.shape
     assert C == shp.cxp and x.dtype == torch.bfloat16 and x.is_contiguous()
     Ho, Wo = out_hw(H, W, shp)
     M = N * Ho * Wo
-    pro = PRO_AFFINE_ACT if (s is not None or act != 0) else PRO_NONE
+    pro = PRO_AFFINE_ACT if (s is not None or act != 0 or lazy is not None) else PRO_NONE
     ent = None
     if tile is None:
         ent = tuned(f"fwd{pro}", N, H, shp) or tuned("fwd", N, H, shp)
@@ -291,34 +310,36 @@ def conv_fwd(x, wf, shp: ConvShape, s=None, t=None, act=0, alpha=1.0, tile=None,
     if part is None:
         part = stat_slots(2, shp.cout, x.device, M)
     dh, dw, wt = taps_fwd(shp.k, shp.pad)
-    if pro == PRO_AFFINE_ACT and s is None:
+    if pro == PRO_AFFINE_ACT and s is None and lazy is None:
         s = torch.ones(C, device=x.device, dtype=torch.float32)
         t = torch.zeros(C, device=x.device, dtype=torch.float32)
+    lz = lazy if lazy is not None else _NOLAZY
     nat.conv_igemm(x.data_ptr(), 0, _p(s), _p(t), 0, wf.data_ptr(), y.data_ptr(), part.data_ptr(), part.shape[0],
                    0, 0, 0, 0, 0, 0,
                    N, H, W, C, Ho, Wo, shp.stride, list(dh), list(dw), list(wt), shp.cout, shp.ntaps * shp.cxp,
-                   Ho, Wo, 1, 0, 0, pro, int(act), float(alpha), EPI_STATS, 0, 1.0, bm, bn, bk, ns, slab_p, cnt_p, kgv,
-                   _sp())
+                   Ho, Wo, 1, 0, 0, pro, int(act), float(alpha), EPI_STATS, 0, 1.0, bm, bn, bk, ns, slab_p, cnt_p,
+                   _loop_kg(ent, kgv), _sp(), lz[0], lz[1])
     if fin is not None:
         _finalize_standalone(nat, 1, part, 2, shp.cout, fin[0], fin[1])
     return y, part
 
 
 def conv_fwd_join(y, r, s, t, s2, t2, wf, shp: ConvShape, jout, jmask=None, tile=None, part=None, nsplit=None,
-                  fin=None, kg=None):
+                  fin=None, kg=None, lazy=None, lazy2=None):
     """1x1 stride-1 forward conv of a residual block's joined output, computed on the fly:
     the operand is a = relu(y*s + t + (r*s2 + t2 if s2 is not None else r)) -- the previous
     block's join (BN'd residual branch y + BN'd or identity shortcut r).  ``jout`` receives
     ``a`` (bf16, the block output the next join and the backward read) and ``jmask`` its
     ReLU bit mask (None: not stored), written once by the first output-channel tile; the
     standalone join kernel and this conv's re-read of ``a`` become one pass.  Returns
-    (conv output, statistics slots) like ``conv_fwd``."""
+    (conv output, statistics slots) like ``conv_fwd``.  ``lazy`` / ``lazy2``: the branches'
+    statistics left in their producers' slot rows (see ``conv_fwd``; s / t and s2 / t2 unused)."""
     nat = _native.native()
     N, H, W, C = y.shape
     assert shp.k == 1 and shp.stride == 1 and shp.pad == 0 and C == shp.cin == shp.cxp
     for tt in (y, r, jout):
         assert tt.dtype == torch.bfloat16 and tt.is_contiguous() and tuple(tt.shape) == (N, H, W, C)
-    assert (s2 is None) == (t2 is None)
+    assert (s2 is None) == (t2 is None) and (lazy2 is None or lazy is not None)
     assert jmask is None or (jmask.dtype == torch.uint8 and jmask.numel() * 8 >= y.numel())
     M = N * H * W
     ent = None
@@ -334,9 +355,12 @@ def conv_fwd_join(y, r, s, t, s2, t2, wf, shp: ConvShape, jout, jmask=None, tile
     out = torch.empty(N, H, W, shp.cout, device=y.device, dtype=torch.bfloat16)
     if part is None:
         part = stat_slots(2, shp.cout, y.device, M)
-    nat.conv_igemm_join(y.data_ptr(), r.data_ptr(), s.data_ptr(), t.data_ptr(), _p(s2), _p(t2), wf.data_ptr(),
+    l1 = lazy if lazy is not None else _NOLAZY
+    l2 = lazy2 if lazy2 is not None else _NOLAZY
+    nat.conv_igemm_join(y.data_ptr(), r.data_ptr(), _p(s), _p(t), _p(s2), _p(t2), wf.data_ptr(),
                         out.data_ptr(), part.data_ptr(), part.shape[0], jout.data_ptr(), _p(jmask), N, H, W, C,
-                        shp.cout, shp.ntaps * shp.cxp, bm, bn, bk, ns, slab_p, cnt_p, kgv, _sp())
+                        shp.cout, shp.ntaps * shp.cxp, bm, bn, bk, ns, slab_p, cnt_p, _loop_kg(ent, kgv), _sp(),
+                        l1[0], l1[1], l2[0], l2[1])
     if fin is not None:
         _finalize_standalone(nat, 1, part, 2, shp.cout, fin[0], fin[1])
     return out, part
@@ -397,7 +421,8 @@ def conv_dgrad(g, y, al, be, wd, shp: ConvShape, x_shape, epi=EPI_STORE, out=Non
                        part.shape[0] if part is not None else 0, _p(ex), _p(es), _p(et),
                        _p(jmask), _p(jyb), _p(jout), N, Hy, Wy, Cy, Ha, Wa, 1,
                        list(dh), list(dw), list(wt), shp.cin, shp.ntaps * shp.cout, Hx, Wx, shp.stride, py, px,
-                       pro, 0, 1.0, epi, int(act), float(alpha), bm, bn, bk, ns, slab_p, cnt_p, kgv, _sp())
+                       pro, 0, 1.0, epi, int(act), float(alpha), bm, bn, bk, ns, slab_p, cnt_p, _loop_kg(ent, kgv),
+                       _sp(), [], [])
     if coef is not None:
         _finalize_standalone(nat, 2, part, 3 if epi == EPI_JOINBWD else 2, shp.cin, coef[0], coef[1])
     return out, (part if epi in (EPI_ACTBWD, EPI_JOINBWD) else None)

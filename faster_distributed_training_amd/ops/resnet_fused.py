@@ -51,6 +51,17 @@ JOIN_FOLD_MAX = int(os.environ.get("FDT_JOIN_FOLD_MAX", "64"))
 FUSED_HEAD = os.environ.get("FDT_FUSED_HEAD", "1") != "0"
 MODE_FCBN, MODE_BN_TRAIN, MODE_BN_EVAL = 0, 1, 2
 BF16 = torch.bfloat16
+# Lazy batch statistics (csrc/kernels/bn_math.h LazyStats): a unit whose statistics fit a few
+# slot rows leaves them there and its CONSUMER (next conv's prologue, the 3x3 materialisation,
+# the residual join) finalises them while staging its input -- no standalone finalize launch
+# (and its kernel boundary) between producer and consumer.  Budget: slot rows x channels a
+# consumer workgroup reduces (rows = one per 32 producer row blocks, so <= 32 fp32 atomic adders
+# per slot address, the full-rate regime of the memory-side atomics).
+LAZY_STATS = os.environ.get("FDT_LAZY_STATS", "0") == "1"
+LAZY_BUDGET = int(os.environ.get("FDT_LAZY_BUDGET", "2048"))
+# which consumers finalise lazily: "elementwise" (the 3x3 materialisation / stem pass and the
+# residual join pass) or "all" (also the conv prologues: AFFINE_ACT / JOIN)
+LAZY_SCOPE = os.environ.get("FDT_LAZY_SCOPE", "elementwise")
 
 # Parameters whose gradient the engine writes itself call these hooks (the DDP reducer
 # registers here in addition to autograd's post-accumulate-grad hooks).  A "deferrable"
@@ -210,6 +221,53 @@ class Plan:
     # ---- FSDP: units are gathered stage by stage, so weights are packed per stage (the
     # forward layout before the stage's forward, the dgrad layout before its backward) and
     # the packed copies are released with the gathered parameters
+    # ---- lazy statistics: which units leave their statistics to the consumer, and where
+    def lazy_layout(self, shape, dev):
+        """{id(unit): (offset, rows)} of the lazy units for an input of ``shape`` (NHWC) and the
+        zeroed slot arena they accumulate into (one arena per input shape: a captured graph's
+        addresses never move; zeroed at every forward, inside the captured graph)."""
+        if not lazy_enabled():
+            return {}, None
+        N, H, W = int(shape[0]), int(shape[1]), int(shape[2])
+        key = (N, H, W, str(dev))
+        cache = self.__dict__.setdefault("_lazy", {})
+        ent = cache.get(key)
+        if ent is None:
+            offs, tot = {}, 0
+
+            def add(u, h, w, conv_consumer=False):
+                nonlocal tot
+                ho, wo = ci.out_hw(h, w, u.shp)
+                r = lazy_rows(N * ho * wo)
+                # FusedConvBN units (mode 0) only: nn.BatchNorm2d units keep the standalone finalize
+                # (running statistics, affine)
+                if (u.bn is None and r * u.shp.cout <= LAZY_BUDGET and N * ho * wo > 1
+                        and (LAZY_SCOPE == "all" or not conv_consumer)):
+                    offs[id(u)] = (tot, r)
+                    tot += (r * 2 + 4) * u.shp.cout  # slots | s | t | mean | sd
+                return ho, wo
+
+            h, w = add(self.stem, H, W)
+            for bi, b in enumerate(self.blocks):
+                hin, win = h, w
+                nxt = self.blocks[bi + 1] if bi + 1 < len(self.blocks) else None
+                folded = nxt is not None and b.join[0] == ACT_RELU and _join_foldable(nxt)
+                for i, u in enumerate(b.units):
+                    if i + 1 < len(b.units):
+                        v = b.units[i + 1]  # consumer: a conv prologue unless a materialised 3x3
+                        cc = not (MATERIALIZE_3X3 and v.shp.k > 1)
+                    else:
+                        cc = folded  # the join: a pass, or the next block's first conv (PRO_JOIN)
+                    h, w = add(u, h, w, cc)
+                if b.shortcut is not None:
+                    add(b.shortcut, hin, win, folded)
+            arena = torch.zeros(max(tot, 1), device=dev, dtype=torch.float32)
+            ent = cache[key] = (offs, arena, tot)
+        offs, arena, tot = ent
+        if tot:
+            arena[:tot].zero_()
+        return offs, arena
+
     def stage_units(self, name):
         if name == "conv1":
             return [self.stem]
@@ -277,28 +335,62 @@ def _bn_fin_params(u: Unit, training):
     return mode, 0.0, None, None, None, None, None
 
 
-def conv_bn_fwd(x, u: Unit, s, t, act, training, dev):
-    """One unit's conv + batch statistics -> (y, (s, t, save_mean, save_aux), M).  The
-    statistics are finalised inside the conv launch when its grid is small (ci.conv_fwd)."""
+def lazy_enabled() -> bool:
+    return LAZY_STATS and not _native.deterministic() and hasattr(_native.native(), "act_affine_lazy")
+
+
+def lazy_rows(M: int) -> int:
+    """Slot rows of a lazy producer over M output rows: one per 32 row blocks of the smallest
+    (64-row) tile, a power of two <= 64."""
+    nb = -(-int(M) // 64)
+    r = 1
+    while r * 32 < nb and r < 64:
+        r *= 2
+    return r
+
+
+def _out_stats(u: Unit, M, training, dev, lay):
+    """(statistics outputs (s, t, save_mean, save_aux), slot view, standalone-finalize args
+    or None, lazy descriptor or None) of one unit's conv.  A lazy unit's outputs are views of
+    its arena region (bn_math.h LazyStats layout), written by its consumer."""
+    ent = lay[0].get(id(u)) if lay is not None else None
+    if ent is None:
+        st, fin = _fin_args(u, M, training, dev)
+        return st, slots(2, u.shp.cout, dev, M), fin, None
+    off, rows = ent
+    C = u.shp.cout
+    reg = lay[1][off:off + (rows * 2 + 4) * C]
+    part = reg[:rows * 2 * C].view(rows, 2, C)
+    outs = reg[rows * 2 * C:].view(4, C)
+    st = (outs[0], outs[1], outs[2], outs[3])
+    return st, part, None, ([reg.data_ptr()], [float(rows), float(u.eps), float(M)])
+
+
+def conv_bn_fwd(x, u: Unit, s, t, act, training, dev, lazy_in=None, lay=None):
+    """One unit's conv + batch statistics -> (y, (s, t, save_mean, save_aux), M, lazy).
+    ``lazy_in``: the input's statistics are finalised in this conv's prologue; ``lazy`` (not
+    None): this unit's own are left in the slot arena for its consumer (``Plan.lazy_layout``),
+    otherwise a standalone finalize follows the conv."""
     Ho, Wo = ci.out_hw(x.shape[1], x.shape[2], u.shp)
     M = x.shape[0] * Ho * Wo
-    st, fin = _fin_args(u, M, training, dev)
+    st, part, fin, lz = _out_stats(u, M, training, dev, lay)
     y, _ = ci.conv_fwd(x, u.wf, u.shp, s, t, act[0] if act else 0, act[1] if act else 1.0,
-                       part=slots(2, u.shp.cout, dev, M), fin=fin)
-    return y, st, M
+                       part=part, fin=fin, lazy=lazy_in)
+    return y, st, M, lz
 
 
-def conv_bn_fwd_join(pj, u: Unit, training, dev):
+def conv_bn_fwd_join(pj, u: Unit, training, dev, lay=None):
     """``conv_bn_fwd`` of a block's first (1x1) unit whose input is the PREVIOUS block's
     join, computed in the conv's operand staging (ci.conv_fwd_join); the join output (this
-    block's x_in) and its ReLU mask are stored on the way.  pj = (y, s, t, r, s2, t2, out, mask)."""
-    y, s, t, r, s2, t2, out, mask = pj
+    block's x_in) and its ReLU mask are stored on the way.  pj = (y, s, t, r, s2, t2, out,
+    mask, lazy, lazy2)."""
+    y, s, t, r, s2, t2, out, mask, lz1, lz2 = pj
     M = y.numel() // y.shape[-1]
-    st, fin = _fin_args(u, M, training, dev)
+    st, part, fin, lz = _out_stats(u, M, training, dev, lay)
     tile = (256, 128, 32) if u.shp.cout > 128 else None  # one output-channel tile
-    yo, _ = ci.conv_fwd_join(y, r, s, t, s2, t2, u.wf, u.shp, out, mask, part=slots(2, u.shp.cout, dev, M), fin=fin,
-                             tile=tile)
-    return yo, st, M
+    yo, _ = ci.conv_fwd_join(y, r, s, t, s2, t2, u.wf, u.shp, out, mask, part=part, fin=fin, tile=tile, lazy=lz1,
+                             lazy2=lz2)
+    return yo, st, M, lz
 
 
 def _join_foldable(b_next) -> bool:
@@ -406,12 +498,17 @@ class ResNetBodyFn(torch.autograd.Function):
             fs.pre_forward("conv1")
             plan.pack_stage("conv1", dev, fwd=True)
         recs = []
+        lay = plan.lazy_layout(x_nhwc.shape, dev)
         # stem: conv -> FCBN stats -> materialised CELU output
         st = plan.stem
-        y0, (s0, t0, sm0, sa0), M0 = conv_bn_fwd(x_nhwc, st, None, None, None, training, dev)
+        y0, (s0, t0, sm0, sa0), M0, lz0 = conv_bn_fwd(x_nhwc, st, None, None, None, training, dev, lay=lay)
         h = torch.empty_like(y0)
-        nat.act_affine_fwd(y0.data_ptr(), s0.data_ptr(), t0.data_ptr(), h.data_ptr(), M0, st.shp.cout,
-                           st.act_out[0], float(st.act_out[1]), 1, 1, _sp())
+        if lz0 is not None:
+            nat.act_affine_lazy(y0.data_ptr(), lz0[0], lz0[1], h.data_ptr(), M0, st.shp.cout, st.act_out[0],
+                                float(st.act_out[1]), 1, _sp())
+        else:
+            nat.act_affine_fwd(y0.data_ptr(), s0.data_ptr(), t0.data_ptr(), h.data_ptr(), M0, st.shp.cout,
+                               st.act_out[0], float(st.act_out[1]), 1, 1, _sp())
         stem_rec = (x_nhwc, y0, s0, t0, sm0, sa0)
         cur = "conv1"
         pending = None  # previous block's join, run inside this block's first conv
@@ -424,29 +521,35 @@ class ResNetBodyFn(torch.autograd.Function):
                 plan.pack_stage(cur, dev, fwd=True)
             x_in = h
             ys = []
-            raw, s, t, act = x_in, None, None, (ACT_NONE, 1.0)
+            raw, s, t, act, lz = x_in, None, None, (ACT_NONE, 1.0), None
             for ui, u in enumerate(b.units):
                 a_in = None
                 if ui == 0 and pending is not None:
                     # writes x_in (= the previous block's output) while staging it
-                    y, (su, tu, smu, sau), M = conv_bn_fwd_join(pending, u, training, dev)
+                    y, (su, tu, smu, sau), M, lzo = conv_bn_fwd_join(pending, u, training, dev, lay)
                     pending = None
                 elif MATERIALIZE_3X3 and u.shp.k > 1 and s is not None:
                     # 3x3: normalise + activate the input ONCE instead of in every one of the
-                    # 9 im2col re-reads of the conv's operand staging
+                    # 9 im2col re-reads of the conv's operand staging (lazy statistics: the
+                    # producer's finalize runs inside this pass)
                     a_in = torch.empty_like(raw)
-                    nat.act_affine_fwd(raw.data_ptr(), s.data_ptr(), t.data_ptr(), a_in.data_ptr(), _rows(raw),
-                                       raw.shape[-1], act[0], float(act[1]), 1, 1, _sp())
-                    y, (su, tu, smu, sau), M = conv_bn_fwd(a_in, u, None, None, None, training, dev)
+                    if lz is not None:
+                        nat.act_affine_lazy(raw.data_ptr(), lz[0], lz[1], a_in.data_ptr(), _rows(raw), raw.shape[-1],
+                                            act[0], float(act[1]), 1, _sp())
+                    else:
+                        nat.act_affine_fwd(raw.data_ptr(), s.data_ptr(), t.data_ptr(), a_in.data_ptr(), _rows(raw),
+                                           raw.shape[-1], act[0], float(act[1]), 1, 1, _sp())
+                    y, (su, tu, smu, sau), M, lzo = conv_bn_fwd(a_in, u, None, None, None, training, dev, lay=lay)
                 else:
-                    y, (su, tu, smu, sau), M = conv_bn_fwd(raw, u, s, t, act, training, dev)
+                    y, (su, tu, smu, sau), M, lzo = conv_bn_fwd(raw, u, s, t, act, training, dev, lazy_in=lz,
+                                                                lay=lay)
                 ys.append((y, su, tu, smu, sau, M, a_in))
-                raw, s, t, act = y, su, tu, u.act_out
-            y3, s3, t3 = ys[-1][0], ys[-1][1], ys[-1][2]
-            sc = None
+                raw, s, t, act, lz = y, su, tu, u.act_out, lzo
+            y3, s3, t3, lz3 = ys[-1][0], ys[-1][1], ys[-1][2], lz
+            sc, lzsc = None, None
             if b.shortcut is not None:
                 u = b.shortcut
-                ysc, (ssc, tsc, smsc, sasc), M = conv_bn_fwd(x_in, u, None, None, None, training, dev)
+                ysc, (ssc, tsc, smsc, sasc), M, lzsc = conv_bn_fwd(x_in, u, None, None, None, training, dev, lay=lay)
                 sc = (ysc, ssc, tsc, smsc, sasc, M, None)
             out = torch.empty_like(y3)
             C = y3.shape[-1]
@@ -459,7 +562,14 @@ class ResNetBodyFn(torch.autograd.Function):
             if nxt is not None and b.join[0] == ACT_RELU and _join_foldable(nxt):
                 # the next block's first 1x1 conv computes this join while staging its operand
                 # and stores `out` + mask (one pass instead of join pass + operand re-read)
-                pending = (y3, s3, t3, sc[0] if sc else x_in, sc[1] if sc else None, sc[2] if sc else None, out, mask)
+                pending = (y3, s3, t3, sc[0] if sc else x_in, sc[1] if sc else None, sc[2] if sc else None, out, mask,
+                           lz3, lzsc)
+            elif lz3 is not None:
+                lzb = lzsc if lzsc is not None else ([], [])
+                nat.residual_act_lazy(y3.data_ptr(), lz3[0], lz3[1], _p(sc[0] if sc else None), lzb[0], lzb[1],
+                                      _p(sc[1] if sc and lzsc is None else None),
+                                      _p(sc[2] if sc and lzsc is None else None), 0 if sc else x_in.data_ptr(),
+                                      out.data_ptr(), _p(mask), _rows(y3), C, b.join[0], float(b.join[1]), 1, _sp())
             else:
                 nat.residual_act_fwd(y3.data_ptr(), s3.data_ptr(), t3.data_ptr(), _p(sc[0] if sc else None),
                                      _p(sc[1] if sc else None), _p(sc[2] if sc else None),

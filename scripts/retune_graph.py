@@ -163,6 +163,8 @@ def main():
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--out", default=ci._TUNED_PATH)
     ap.add_argument("--log", default=None)
+    ap.add_argument("--loops", action="store_true",
+                    help="only choose the K-loop form (rotated / legacy) of each listed key's current entry")
     ap.add_argument("--keys", nargs="*", default=None,
                     help="engine_launch_keys.py outputs: tune exactly the (shape key, op key) pairs listed")
     a = ap.parse_args()
@@ -193,6 +195,32 @@ def main():
             timeit(fn, a.reps)
             t_cur = timeit(fn, a.reps) * 1e3
             best = (t_cur, None)
+            if a.loops and kind in ("fwd", "dgrad"):
+                # the K-loop form of the kernel the entry (or the heuristic) picks: time both
+                base = dict(cur) if cur else {}
+                base.pop("us", None)
+                res = {}
+                for lp in ("rot", "old", "rot", "old"):
+                    ent = dict(base, loop=lp)
+                    ci.tuned = (lambda op, b, h, s_, e=ent, ok=op_key: e if op == ok else None)
+                    try:
+                        us = timeit(fn, a.reps) * 1e3
+                    finally:
+                        ci.tuned = orig
+                    res[lp] = min(res.get(lp, 1e9), us)
+                pick = "rot" if res["rot"] <= res["old"] else "old"
+                ent = dict(cur) if cur else {}
+                ent["loop"] = pick
+                if cur:  # (a heuristic launch gets no entry: the default form applies)
+                    table.setdefault(key, {})[op_key] = ent
+                    changes.append((N, key, op_key, res["old"], res[pick], cnt))
+                print(f"b{N} {key:22s} {op_key:8s} x{cnt}: rot {res['rot']:7.1f} us  old {res['old']:7.1f} us -> {pick}"
+                      f"   [{time.time() - t_start:.0f} s]", flush=True)
+                del keep
+                torch.cuda.empty_cache()
+                continue
+            if a.loops:
+                continue
             for cand in candidates(kind, shp, N, H):
                 ent = dict(cand)
                 if cur and "stages" in cur:
