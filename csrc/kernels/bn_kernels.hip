@@ -20,6 +20,7 @@
 namespace fdt {
 
 constexpr int kBlk = 256;
+inline int wt_flag() { return conv_write_through() ? 1 : 0; }  // write-through streaming outputs (common.h st8)
 
 // Channel-group geometry for [M][C] with 8 channels per thread.
 struct ChanGeom {
@@ -50,7 +51,7 @@ __device__ __forceinline__ void load8f(const float* __restrict__ p, int c, float
 template <typename T, typename TO>
 __global__ __launch_bounds__(kBlk) void act_affine_fwd_kernel(const T* __restrict__ x, const float* __restrict__ s,
                                                               const float* __restrict__ t, TO* __restrict__ out,
-                                                              long nvec, int C, int act, float alpha) {
+                                                              long nvec, int C, int act, float alpha, int wt) {
   long stride = (long)gridDim.x * blockDim.x;
   for (long v = (long)blockIdx.x * blockDim.x + threadIdx.x; v < nvec; v += stride) {
     long e = v * 8;
@@ -67,7 +68,7 @@ __global__ __launch_bounds__(kBlk) void act_affine_fwd_kernel(const T* __restric
     }
 #pragma unroll
     for (int i = 0; i < 8; ++i) a[i] = act_fwd(a[i], act, alpha);
-    Vec8<TO>::store(out + e, a);
+    st8(out, e, a, wt);
   }
 }
 
@@ -168,7 +169,7 @@ __global__ __launch_bounds__(kBlk) void act_bwd_reduce_kernel(const T* __restric
                                                               const float* __restrict__ s, const float* __restrict__ t,
                                                               T* __restrict__ gx, float* __restrict__ part,
                                                               unsigned slot_mask, long M, int C, int TPR, int RPP,
-                                                              long rows_per_blk, int act, float alpha) {
+                                                              long rows_per_blk, int act, float alpha, int wt) {
   __shared__ float sm[kBlk * 16];
   const int tid = threadIdx.x;
   const int gi = tid % TPR, rr = tid / TPR;
@@ -192,7 +193,7 @@ __global__ __launch_bounds__(kBlk) void act_bwd_reduce_kernel(const T* __restric
       a1[i] = fmaf(gp, xv[i], a1[i]);
       a0[i] += gp;
     }
-    Vec8<T>::store(gx + r * C + c0, o);
+    st8(gx, r * C + c0, o, wt);
   }
 #pragma unroll
   for (int i = 0; i < 8; ++i) { sm[tid * 16 + i] = a1[i]; sm[tid * 16 + 8 + i] = a0[i]; }
@@ -308,7 +309,7 @@ template <typename T>
 __global__ __launch_bounds__(kBlk) void affine_fold_kernel(const T* __restrict__ gy, const T* __restrict__ y,
                                                            const float* __restrict__ alpha, const float* __restrict__ beta,
                                                            const float* __restrict__ gs, T* __restrict__ out, long nvec,
-                                                           int G) {
+                                                           int G, int wt) {
   // out = gy*gs + alpha + beta*y  (gs nullptr: 1; gy nullptr: 0)
   long stride = (long)gridDim.x * blockDim.x;
   for (long v = (long)blockIdx.x * blockDim.x + threadIdx.x; v < nvec; v += stride) {
@@ -331,7 +332,7 @@ __global__ __launch_bounds__(kBlk) void affine_fold_kernel(const T* __restrict__
     }
 #pragma unroll
     for (int i = 0; i < 8; ++i) gv[i] = fmaf(gv[i], sv[i], fmaf(bv[i], yv[i], av[i]));
-    Vec8<T>::store(out + e, gv);
+    st8(out, e, gv, wt);
   }
 }
 
@@ -345,7 +346,8 @@ __device__ __forceinline__ void residual_fwd_vec(const T* __restrict__ ya, const
                                                  const float* __restrict__ ta, const T* __restrict__ yb,
                                                  const float* __restrict__ sb, const float* __restrict__ tb,
                                                  const T* __restrict__ xid, T* __restrict__ out,
-                                                 uint8_t* __restrict__ mask, long v, int G, int act, float alpha) {
+                                                 uint8_t* __restrict__ mask, long v, int G, int act, float alpha,
+                                                 int wt) {
   const long e = v * 8;
   const int c = (int)((unsigned long)v % (unsigned)G) * 8;
   float a[8], b[8], s8[8], t8[8];
@@ -367,7 +369,7 @@ __device__ __forceinline__ void residual_fwd_vec(const T* __restrict__ ya, const
     a[i] = act_fwd(fmaf(a[i], s8[i], t8[i]) + b[i], act, alpha);
     m |= (a[i] > 0.f ? 1u : 0u) << i;
   }
-  Vec8<T>::store(out + e, a);
+  st8(out, e, a, wt);
   if (mask) mask[v] = (uint8_t)m;
 }
 
@@ -377,7 +379,7 @@ __device__ __forceinline__ void residual_fwd_vec_p(const T* __restrict__ ya, con
                                                    const T* __restrict__ yb, const float (&sb8)[8],
                                                    const float (&tb8)[8], const T* __restrict__ xid,
                                                    T* __restrict__ out, uint8_t* __restrict__ mask, long v, int act,
-                                                   float alpha) {
+                                                   float alpha, int wt) {
   const long e = v * 8;
   float a[8], b[8];
   Vec8<T>::load(ya + e, a);
@@ -394,7 +396,7 @@ __device__ __forceinline__ void residual_fwd_vec_p(const T* __restrict__ ya, con
     a[i] = act_fwd(fmaf(a[i], s8[i], t8[i]) + b[i], act, alpha);
     m |= (a[i] > 0.f ? 1u : 0u) << i;
   }
-  Vec8<T>::store(out + e, a);
+  st8(out, e, a, wt);
   if (mask) mask[v] = (uint8_t)m;
 }
 
@@ -407,7 +409,7 @@ __global__ __launch_bounds__(kBlk) void residual_act_fwd_kernel(const T* __restr
                                                                 const float* __restrict__ sb, const float* __restrict__ tb,
                                                                 const T* __restrict__ xid, T* __restrict__ out,
                                                                 uint8_t* __restrict__ mask, long nvec, int G, int act,
-                                                                float alpha) {
+                                                                float alpha, int wt) {
   const long stride = (long)gridDim.x * blockDim.x;
   long v = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (HOIST) {
@@ -423,17 +425,17 @@ __global__ __launch_bounds__(kBlk) void residual_act_fwd_kernel(const T* __restr
       for (int i = 0; i < 8; ++i) { sb8[i] = 1.f; tb8[i] = 0.f; }
     }
     for (; v + stride < nvec; v += 2 * stride) {
-      residual_fwd_vec_p(ya, s8, t8, yb, sb8, tb8, xid, out, mask, v, act, alpha);
-      residual_fwd_vec_p(ya, s8, t8, yb, sb8, tb8, xid, out, mask, v + stride, act, alpha);
+      residual_fwd_vec_p(ya, s8, t8, yb, sb8, tb8, xid, out, mask, v, act, alpha, wt);
+      residual_fwd_vec_p(ya, s8, t8, yb, sb8, tb8, xid, out, mask, v + stride, act, alpha, wt);
     }
-    if (v < nvec) residual_fwd_vec_p(ya, s8, t8, yb, sb8, tb8, xid, out, mask, v, act, alpha);
+    if (v < nvec) residual_fwd_vec_p(ya, s8, t8, yb, sb8, tb8, xid, out, mask, v, act, alpha, wt);
     return;
   }
   for (; v + stride < nvec; v += 2 * stride) {
-    residual_fwd_vec(ya, sa, ta, yb, sb, tb, xid, out, mask, v, G, act, alpha);
-    residual_fwd_vec(ya, sa, ta, yb, sb, tb, xid, out, mask, v + stride, G, act, alpha);
+    residual_fwd_vec(ya, sa, ta, yb, sb, tb, xid, out, mask, v, G, act, alpha, wt);
+    residual_fwd_vec(ya, sa, ta, yb, sb, tb, xid, out, mask, v + stride, G, act, alpha, wt);
   }
-  if (v < nvec) residual_fwd_vec(ya, sa, ta, yb, sb, tb, xid, out, mask, v, G, act, alpha);
+  if (v < nvec) residual_fwd_vec(ya, sa, ta, yb, sb, tb, xid, out, mask, v, G, act, alpha, wt);
 }
 
 // act'(z) from the activation OUTPUT o (ReLU: o>0; CELU: o>0 ? 1 : o/alpha + 1)
@@ -453,7 +455,8 @@ __global__ __launch_bounds__(kBlk) void residual_act_bwd_kernel(const T* __restr
                                                                 const T* __restrict__ ya, const T* __restrict__ yb,
                                                                 T* __restrict__ gpre, float* __restrict__ part,
                                                                 unsigned slot_mask, long M, int C, int TPR, int RPP,
-                                                                long rows_per_blk, int act, float alpha, int ghw) {
+                                                                long rows_per_blk, int act, float alpha, int ghw,
+                                                                int wt) {
   __shared__ float sm[kBlk * 24];
   const int tid = threadIdx.x;
   const int gi = tid % TPR, rr = tid / TPR;
@@ -475,7 +478,7 @@ __global__ __launch_bounds__(kBlk) void residual_act_bwd_kernel(const T* __restr
       p1[i] += gp;
       if (yb) p2[i] = fmaf(gp, bv[i], p2[i]);
     }
-    Vec8<T>::store(gpre + e, gp8);
+    st8(gpre, e, gp8, wt);
   };
   // ghw > 0: g is [M/ghw, C] and broadcast over each group of ghw rows (the classifier
   // head's pooled gradient, already divided by ghw: see head.hip)
@@ -654,7 +657,7 @@ void act_affine_fwd(uint64_t x, uint64_t s, uint64_t t, uint64_t out, long M, in
     using TI = T;
     DISPATCH_T(dt_out, {
       act_affine_fwd_kernel<TI, T><<<ew_grid(nvec), kBlk, 0, as_stream(stream)>>>(
-          P<const TI>(x), P<const float>(s), P<const float>(t), P<T>(out), nvec, C, act, alpha);
+          P<const TI>(x), P<const float>(s), P<const float>(t), P<T>(out), nvec, C, act, alpha, wt_flag());
     });
   });
   FDT_LAUNCH_CHECK();
@@ -701,7 +704,7 @@ void act_bwd_reduce(uint64_t g, uint64_t x, uint64_t s, uint64_t t, uint64_t gx,
   DISPATCH_T(dt, {
     act_bwd_reduce_kernel<T><<<grid, kBlk, 0, as_stream(stream)>>>(P<const T>(g), P<const T>(x), P<const float>(s),
                                                                   P<const float>(t), P<T>(gx), P<float>(part), mask, M,
-                                                                  C, gg.TPR, gg.RPP, r, act, alpha);
+                                                                  C, gg.TPR, gg.RPP, r, act, alpha, wt_flag());
   });
   FDT_LAUNCH_CHECK();
 }
@@ -777,7 +780,7 @@ void affine_fold(uint64_t gy, uint64_t y, uint64_t alpha, uint64_t beta, uint64_
   DISPATCH_T(dt, {
     affine_fold_kernel<T><<<ew_grid(nvec), kBlk, 0, as_stream(stream)>>>(
         P<const T>(gy), P<const T>(y), P<const float>(alpha), P<const float>(beta), P<const float>(gs), P<T>(out), nvec,
-        C / 8);
+        C / 8, wt_flag());
   });
   FDT_LAUNCH_CHECK();
 }
@@ -796,7 +799,7 @@ void residual_act_fwd(uint64_t ya, uint64_t sa, uint64_t ta, uint64_t yb, uint64
     auto kern = hoist ? residual_act_fwd_kernel<T, true> : residual_act_fwd_kernel<T, false>;
     kern<<<(int)g, kBlk, 0, as_stream(stream)>>>(
         P<const T>(ya), P<const float>(sa), P<const float>(ta), P<const T>(yb), P<const float>(sb), P<const float>(tb),
-        P<const T>(xid), P<T>(out), P<uint8_t>(mask), nvec, C / 8, act, alpha);
+        P<const T>(xid), P<T>(out), P<uint8_t>(mask), nvec, C / 8, act, alpha, wt_flag());
   });
   FDT_LAUNCH_CHECK();
 }
@@ -870,7 +873,7 @@ void residual_act_bwd(uint64_t g, uint64_t out, uint64_t mask, uint64_t ya, uint
   DISPATCH_T(dt, {
     residual_act_bwd_kernel<T><<<grid, kBlk, 0, as_stream(stream)>>>(
         P<const T>(g), P<const T>(out), P<const uint8_t>(mask), P<const T>(ya), P<const T>(yb), P<T>(gpre), P<float>(part),
-        smask, M, C, gg.TPR, gg.RPP, r, act, alpha, ghw);
+        smask, M, C, gg.TPR, gg.RPP, r, act, alpha, ghw, wt_flag());
   });
   FDT_LAUNCH_CHECK();
 }

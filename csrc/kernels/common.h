@@ -102,6 +102,25 @@ template <> struct Vec8<float> {
   }
 };
 
+// 8-wide store of a streaming output at element e of base: wt = write-through (sc1) for bf16 --
+// the bytes leave the XCD's L2 as written instead of in the end-of-kernel write-back the next
+// dependent launch waits for (the conv epilogues' st_out does the same); plain otherwise.
+template <typename T>
+__device__ __forceinline__ void st8(T* __restrict__ base, long e, const float* v, int wt) {
+  if constexpr (sizeof(T) == 2) {
+    if (wt) {
+      const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, (int)0xFFFFFFFF, 0x00020000);
+      typedef unsigned int u32x4v __attribute__((ext_vector_type(4)));
+      uint4 u;
+      Vec8<T>::store(reinterpret_cast<T*>(&u), v);
+      u32x4v w = {u.x, u.y, u.z, u.w};
+      __builtin_amdgcn_raw_buffer_store_b128(w, r, (uint32_t)(e * 2), 0, 16);
+      return;
+    }
+  }
+  Vec8<T>::store(base + e, v);
+}
+
 // Per-channel statistics producers (conv epilogues, BN-backward reductions) add their
 // per-workgroup partial sums with fp32 atomics into at most kStatSlots rows (row = block index
 // mod rows, spreading contention); the fp64 finalize/reduce kernel sums the rows and
@@ -118,6 +137,12 @@ inline int& deterministic_flag() {
   return f;
 }
 inline void set_deterministic(bool on) { deterministic_flag() = on ? 1 : 0; }
+// conv epilogues: write-through (sc1) output stores (conv_igemm_impl.h st_out)
+inline int& conv_write_through_flag() {
+  static int f = 0;
+  return f;
+}
+inline bool conv_write_through() { return conv_write_through_flag() != 0; }
 inline bool deterministic() { return deterministic_flag() != 0; }
 // slot index mask for a launch whose slot buffer holds `rows` rows (nblocks: the launch's
 // block count along the slot axis)

@@ -133,6 +133,7 @@ struct ConvArgs {
   // lazy batch statistics (bn_math.h): AFFINE_ACT / JOIN take (s, t) -- JOIN's shortcut (s2,
   // t2) from ls2 -- by finalising the producer's slot rows in the prologue (ps / pt unused)
   LazyStats ls1, ls2;
+  int wthru;              // epilogue output stores write-through (sc1): see st_out
   long Nb_HiWi_Cx_bytes;  // bytes of the activation operand(s)
   long w_bytes;           // bytes of the packed weights
 };
@@ -200,6 +201,18 @@ __device__ __forceinline__ float4 ld_buf16_sc1(__amdgpu_buffer_rsrc_t r, uint32_
 }
 
 constexpr uint32_t kOOB = 0xFFFFFFF0u;  // byte offset past any buffer: the load returns zeros
+
+// Epilogue output store.  wt: write-through (sc1) -- the bytes leave the XCD's L2 as they are
+// written instead of in the end-of-kernel write-back that the next (dependent) launch waits for
+// (MI355X_MICROARCH: a boundary costs + dirty bytes / 6 TB/s); plain stores otherwise.
+__device__ __forceinline__ void st_out(__amdgpu_buffer_rsrc_t r, uint32_t byte_off, bf16* p, const float* v, int wt) {
+  if (wt) {
+    u32x4_t u = {pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]), pack_bf16x2(v[4], v[5]), pack_bf16x2(v[6], v[7])};
+    __builtin_amdgcn_raw_buffer_store_b128(u, r, byte_off, 0, 16);
+  } else {
+    Vec8<bf16>::store(p, v);
+  }
+}
 
 // Occupancy floor per instantiation: the 128x128x32 tiles whose prologue / epilogue fit in
 // 128 registers without spilling (no fold prologue, no epilogue loads beyond one tensor:
@@ -745,6 +758,8 @@ igemm_kernel(const ConvArgs a) {
     constexpr bool STATS = EPI == kEpiStats || EPI == kEpiActBwd || EPI == kEpiJoinBwd;
     const int h = lane >> 5;
     float* stg = reinterpret_cast<float*>(smem + hdr);
+    const __amdgpu_buffer_rsrc_t ro = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)a.out, (short)0, (int)0xFFFFFFFF, 0x00020000);
     const int cg = tid % CG, rs = tid / CG;
     const int c = n0 + cg * 8;  // this thread's 8 output channels
     const bool dense = a.OS == 1 && a.oy == 0 && a.ox == 0 && a.Hout == a.Ho && a.Wout == a.Wo;
@@ -815,7 +830,7 @@ igemm_kernel(const ConvArgs a) {
           if constexpr (EPI == kEpiStats) {
 #pragma unroll
             for (int k = 0; k < 8; ++k) { q0[k] += v[k]; q1[k] = fmaf(v[k], v[k], q1[k]); }
-            Vec8<bf16>::store(a.out + e, v);
+            st_out(ro, e * 2u, a.out + e, v, a.wthru);
           } else if constexpr (EPI == kEpiActBwd) {
             float x8[8];
             Vec8<bf16>::load(a.ex + e, x8);
@@ -826,7 +841,7 @@ igemm_kernel(const ConvArgs a) {
               q0[k] = fmaf(gp, x8[k], q0[k]);
               q1[k] += gp;
             }
-            Vec8<bf16>::store(a.out + e, v);
+            st_out(ro, e * 2u, a.out + e, v, a.wthru);
           } else if constexpr (EPI == kEpiJoinBwd) {
             float e8[8], ya[8], yb[8], o8[8];
             Vec8<bf16>::load(a.out + e, e8);
@@ -847,13 +862,13 @@ igemm_kernel(const ConvArgs a) {
               q1[k] += gp;
               if (hb) q2[k] = fmaf(gp, yb[k], q2[k]);
             }
-            Vec8<bf16>::store(a.out + e, v);
+            st_out(ro, e * 2u, a.out + e, v, a.wthru);
           } else if constexpr (EPI == kEpiAdd) {
             float e8[8];
             Vec8<bf16>::load(a.out + e, e8);
 #pragma unroll
             for (int k = 0; k < 8; ++k) v[k] += e8[k];
-            Vec8<bf16>::store(a.out + e, v);
+            st_out(ro, e * 2u, a.out + e, v, a.wthru);
           } else if constexpr (EPI == kEpiGeluFwd) {
             // a = acc + bias, rounded to bf16 as stored (the backward reads the stored a);
             // h from the rounded a, exactly as the standalone GELU-dropout pass computes it
@@ -888,7 +903,7 @@ igemm_kernel(const ConvArgs a) {
             }
             *reinterpret_cast<uint4*>(a.out + e) = make_uint4(pg[0], pg[1], pg[2], pg[3]);
           } else {
-            Vec8<bf16>::store(a.out + e, v);
+            st_out(ro, e * 2u, a.out + e, v, a.wthru);
           }
         }
       }
