@@ -112,6 +112,7 @@ void ffn_gemm(uint64_t x, uint64_t w, uint64_t out, long M, int K, int N, int ep
               uint64_t stream);
 int conv_num_row_blocks(long M, int BM);
 void set_conv_write_through(bool on);
+void set_conv_debug_flags(int f);
 std::vector<long> conv_splitk_workspace(long M, int Cout, int BM, int BN, int nsplit);
 // conv_wgrad.hip
 void conv_wgrad(uint64_t g, uint64_t y, uint64_t al, uint64_t be, uint64_t gs, uint64_t x, uint64_t xs, uint64_t xt,

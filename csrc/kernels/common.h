@@ -143,6 +143,12 @@ inline int& conv_write_through_flag() {
   return f;
 }
 inline bool conv_write_through() { return conv_write_through_flag() != 0; }
+// cost-probe switches of the conv kernels (never set in training: scripts/conv_probe2.py)
+inline int& conv_debug_flags_ref() {
+  static int f = 0;
+  return f;
+}
+inline int conv_debug_flags() { return conv_debug_flags_ref(); }
 inline bool deterministic() { return deterministic_flag() != 0; }
 // slot index mask for a launch whose slot buffer holds `rows` rows (nblocks: the launch's
 // block count along the slot axis)

@@ -74,6 +74,7 @@ static void conv_igemm_impl(uint64_t x, uint64_t x2, uint64_t ps, uint64_t pt, u
   a.nbn = Cout / BN;
   a.det = deterministic() ? 1 : 0;
   a.wthru = conv_write_through() ? 1 : 0;
+  a.dbg = conv_debug_flags();
   a.slot_mask = part ? stat_slot_mask(part_rows, a.nbm) : 0u;
   {
     const int nkt = (a.K + BK - 1) / BK;
@@ -180,6 +181,7 @@ void ffn_gemm(uint64_t x, uint64_t w, uint64_t out, long M, int K, int N, int ep
 int conv_num_row_blocks(long M, int BM) { return (int)((M + BM - 1) / BM); }
 
 void set_conv_write_through(bool on) { conv_write_through_flag() = on ? 1 : 0; }
+void set_conv_debug_flags(int f) { conv_debug_flags_ref() = f; }
 
 // split-K workspace sizes for a launch: (slab floats, ticket ints)
 std::vector<long> conv_splitk_workspace(long M, int Cout, int BM, int BN, int nsplit) {

@@ -134,6 +134,7 @@ struct ConvArgs {
   // t2) from ls2 -- by finalising the producer's slot rows in the prologue (ps / pt unused)
   LazyStats ls1, ls2;
   int wthru;              // epilogue output stores write-through (sc1): see st_out
+  int dbg;                // cost probes (scripts/conv_probe2.py): bit 0 = skip the statistics atomics
   long Nb_HiWi_Cx_bytes;  // bytes of the activation operand(s)
   long w_bytes;           // bytes of the packed weights
 };
@@ -951,7 +952,7 @@ igemm_kernel(const ConvArgs a) {
       for (int e = tid; ew && e < NQ * BN; e += 256) {
         const float t = red[e] + red[NQ * BN + e] + red[2 * NQ * BN + e] + red[3 * NQ * BN + e];
         const int q = e / BN, cc2 = e - q * BN;
-        atomicAdd(&a.part[((long)(bm & a.slot_mask) * NQ + q) * a.Cout + n0 + cc2], t);
+        if (!(a.dbg & 1)) atomicAdd(&a.part[((long)(bm & a.slot_mask) * NQ + q) * a.Cout + n0 + cc2], t);
       }
     }
   }

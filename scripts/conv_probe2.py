@@ -43,11 +43,24 @@ def main():
         part = torch.zeros(rows, 2, cout, device=dev)
         t_stats = timeit(lambda: conv_direct(x, wf, shp, ci.EPI_STATS, part, tile), 20) * 1e3
         t_store = timeit(lambda: conv_direct(x, wf, shp, ci.EPI_STORE, None, tile), 20) * 1e3
+        nat.set_conv_debug_flags(1)
+        t_noatom = timeit(lambda: conv_direct(x, wf, shp, ci.EPI_STATS, part, tile), 20) * 1e3
+        nat.set_conv_debug_flags(0)
+        part64 = torch.zeros(64, 2, cout, device=dev)
+        t_256 = None
+        if rows == 64:
+            # (more slot rows = fewer adders per address; the deterministic-mode path sizes them
+            # one per row block: the kernel's slot mask comes from the row count)
+            prt = torch.zeros(1 << max(6, (-(-N * H * H // tile[0]) - 1).bit_length()), 2, cout, device=dev)
+            _native.native().set_deterministic_mode(True)
+            t_256 = timeit(lambda: conv_direct(x, wf, shp, ci.EPI_STATS, prt, tile), 20) * 1e3
+            _native.native().set_deterministic_mode(False)
         s, t, sm, sa = (torch.empty(cout, device=dev) for _ in range(4))
         t_fin = timeit(lambda: nat.stats_finalize(part.data_ptr(), rows, cout, float(N * H * H), 0, 1e-3, 0.1, 0, 0, 0,
                                                   0, 0, s.data_ptr(), t.data_ptr(), sm.data_ptr(), sa.data_ptr(), 1,
                                                   _native.stream_ptr()), 20) * 1e3
         print(f"N {N} {H}x{H} {cin}->{cout} k{k} tile {tile} ({rows} slot rows): stats epilogue {t_stats:6.1f} us, "
+              f"stats without the atomics {t_noatom:6.1f} us, one slot row per workgroup {t_256 or 0:6.1f} us, "
               f"store epilogue {t_store:6.1f} us, finalize alone {t_fin:5.1f} us", flush=True)
     e = torch.empty(1, device=dev)
     print(f"empty fill kernel: {timeit(lambda: e.fill_(1.0), 20) * 1e3:5.1f} us per launch")

