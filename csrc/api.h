@@ -11,6 +11,7 @@ namespace fdt {
 void act_affine_fwd(uint64_t x, uint64_t s, uint64_t t, uint64_t out, long M, int C, int act, float alpha, int dt_in,
                     int dt_out, uint64_t stream);
 int stats_num_blocks(long M, int C);
+void set_ew_unroll(bool on);
 void channel_stats_partial(uint64_t y, uint64_t part, long M, int C, int dt, uint64_t stream);
 void stats_finalize(uint64_t part, int nb, int C, double count, int mode, float eps, float momentum, uint64_t gamma,
                     uint64_t beta, uint64_t run_mean, uint64_t run_var, uint64_t nbt, uint64_t out_s, uint64_t out_t,

@@ -72,6 +72,19 @@ __global__ __launch_bounds__(kBlk) void act_affine_fwd_kernel(const T* __restric
   }
 }
 
+// Streaming form of the BN-backward fold (kEwU vectors per thread per trip, every load of the
+// trip issued before the first store; the grid stride is a multiple of the channel-vector count
+// G -- host: ew_grid_u -- so a thread's channels and per-channel parameters are fixed, loaded
+// once): 5.0 -> 5.3-5.4 TB/s on the 268-537 MB batch-1024 tensors (scripts/ew_probe.py,
+// profiles/r5/ew_probe_bs1024.txt).  The same form of the join and normalise passes measured
+// 3-8 % SLOWER than their grid-stride loops, which already run at the device-copy rate of
+// those tensors (4.7-5.0 TB/s): those keep the one/two-vector loops.
+constexpr int kEwU = 4;
+inline int& ew_unroll_flag() {
+  static int f = 1;
+  return f;
+}
+
 // ------------------------------------------------------------------ stats partials
 // part[blk][q][C], q = 0: sum y, q = 1: sum y^2
 template <typename T>
@@ -117,21 +130,25 @@ __device__ __forceinline__ void zero_partials(float* part, int nb, int C, int c,
 template <int NQ>
 __device__ __forceinline__ void sum_partials_f64(const float* __restrict__ part, int nb, int C, int c, double* acc,
                                                  int w, int nw) {
+  // 4 rows per trip (4*NQ independent loads in flight): large-M producers spread their
+  // workgroups over hundreds of slot rows, and this loop is latency-bound
   double a0[NQ], a1[NQ];
 #pragma unroll
   for (int q = 0; q < NQ; ++q) { a0[q] = 0.0; a1[q] = 0.0; }
   int b = w;
-  for (; b + nw < nb; b += 2 * nw) {
-    float v0[NQ], v1[NQ];
+  for (; b + 3 * nw < nb; b += 4 * nw) {
+    float v[4][NQ];
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int q = 0; q < NQ; ++q) v[u][q] = part[((long)(b + u * nw) * NQ + q) * C + c];
 #pragma unroll
     for (int q = 0; q < NQ; ++q) {
-      v0[q] = part[((long)b * NQ + q) * C + c];
-      v1[q] = part[((long)(b + nw) * NQ + q) * C + c];
+      a0[q] += (double)v[0][q] + (double)v[2][q];
+      a1[q] += (double)v[1][q] + (double)v[3][q];
     }
-#pragma unroll
-    for (int q = 0; q < NQ; ++q) { a0[q] += (double)v0[q]; a1[q] += (double)v1[q]; }
   }
-  if (b < nb) {
+  for (; b < nb; b += nw) {
 #pragma unroll
     for (int q = 0; q < NQ; ++q) a0[q] += (double)part[((long)b * NQ + q) * C + c];
   }
@@ -332,6 +349,49 @@ __global__ __launch_bounds__(kBlk) void affine_fold_kernel(const T* __restrict__
     }
 #pragma unroll
     for (int i = 0; i < 8; ++i) gv[i] = fmaf(gv[i], sv[i], fmaf(bv[i], yv[i], av[i]));
+    st8(out, e, gv, wt);
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(kBlk) void affine_fold_u_kernel(const T* __restrict__ gy, const T* __restrict__ y,
+                                                             const float* __restrict__ alpha,
+                                                             const float* __restrict__ beta,
+                                                             const float* __restrict__ gs, T* __restrict__ out,
+                                                             long nvec, int G, int wt) {
+  const long stride = (long)gridDim.x * blockDim.x;
+  long v = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const int c = (int)((unsigned long)v % (unsigned)G) * 8;
+  float av[8], bv[8], sv[8];
+  load8f(alpha, c, av);
+  load8f(beta, c, bv);
+  if (gs) load8f(gs, c, sv);
+  else {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) sv[i] = 1.f;
+  }
+  for (; v + (kEwU - 1) * stride < nvec; v += kEwU * stride) {
+    float gv[kEwU][8], yv[kEwU][8];
+#pragma unroll
+    for (int u = 0; u < kEwU; ++u) {
+      const long e = (v + u * stride) * 8;
+      if (gy) Vec8<T>::load(gy + e, gv[u]);
+      Vec8<T>::load(y + e, yv[u]);
+    }
+#pragma unroll
+    for (int u = 0; u < kEwU; ++u) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) gv[u][i] = fmaf(gy ? gv[u][i] : 0.f, sv[i], fmaf(bv[i], yv[u][i], av[i]));
+      st8(out, (v + u * stride) * 8, gv[u], wt);
+    }
+  }
+  for (; v < nvec; v += stride) {
+    const long e = v * 8;
+    float gv[8], yv[8];
+    if (gy) Vec8<T>::load(gy + e, gv);
+    Vec8<T>::load(y + e, yv);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) gv[i] = fmaf(gy ? gv[i] : 0.f, sv[i], fmaf(bv[i], yv[i], av[i]));
     st8(out, e, gv, wt);
   }
 }
@@ -622,6 +682,20 @@ inline int ew_grid(long nvec) {
   return (int)g;
 }
 
+// grid of a streaming (_u) pass: <= 2048 blocks, kEwU vectors per thread per trip, and the
+// stride (blocks * kBlk) a multiple of G (channels fixed per thread); 0 = not applicable
+inline int ew_grid_u(long nvec, int G) {
+  if (!ew_unroll_flag()) return 0;
+  long g = (nvec + (long)kBlk * kEwU - 1) / ((long)kBlk * kEwU);
+  if (g > 2048) g = 2048;
+  if (g < 1) g = 1;
+  // round up to a multiple of G / gcd(G, kBlk) blocks (G a power of two here)
+  if ((G & (G - 1)) != 0) return 0;
+  const long q = G > kBlk ? G / kBlk : 1;
+  g = (g + q - 1) / q * q;
+  return (int)g;
+}
+
 // rows per block so that the grid holds ~1024-4096 blocks of >= RPP rows
 inline long rows_per_block(long M, const ChanGeom& g) {
   // ~512 partial rows per channel: enough blocks to fill 256 CUs (x gy channel tiles)
@@ -633,6 +707,8 @@ inline long rows_per_block(long M, const ChanGeom& g) {
   r = (r + g.RPP - 1) / g.RPP * g.RPP;
   return r;
 }
+
+void set_ew_unroll(bool on) { ew_unroll_flag() = on ? 1 : 0; }
 
 int stats_num_blocks(long M, int C) {
   ChanGeom g = chan_geom(C);
@@ -777,10 +853,16 @@ void affine_fold(uint64_t gy, uint64_t y, uint64_t alpha, uint64_t beta, uint64_
   FDT_CHECK(C % 8 == 0, "C % 8");
   long nvec = M * (long)C / 8;
   if (nvec == 0) return;
+  const int gu = ew_grid_u(nvec, C / 8);
   DISPATCH_T(dt, {
-    affine_fold_kernel<T><<<ew_grid(nvec), kBlk, 0, as_stream(stream)>>>(
-        P<const T>(gy), P<const T>(y), P<const float>(alpha), P<const float>(beta), P<const float>(gs), P<T>(out), nvec,
-        C / 8, wt_flag());
+    if (gu)
+      affine_fold_u_kernel<T><<<gu, kBlk, 0, as_stream(stream)>>>(
+          P<const T>(gy), P<const T>(y), P<const float>(alpha), P<const float>(beta), P<const float>(gs), P<T>(out),
+          nvec, C / 8, wt_flag());
+    else
+      affine_fold_kernel<T><<<ew_grid(nvec), kBlk, 0, as_stream(stream)>>>(
+          P<const T>(gy), P<const T>(y), P<const float>(alpha), P<const float>(beta), P<const float>(gs), P<T>(out),
+          nvec, C / 8, wt_flag());
   });
   FDT_LAUNCH_CHECK();
 }

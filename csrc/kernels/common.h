@@ -126,6 +126,9 @@ __device__ __forceinline__ void st8(T* __restrict__ base, long e, const float* v
 // mod rows, spreading contention); the fp64 finalize/reduce kernel sums the rows and
 // re-zeroes them.  Replaces per-workgroup slabs + a compaction pass.
 constexpr int kStatSlots = 64;
+// upper bound on the rows of a (non-deterministic) slot buffer: large-M convolutions spread
+// their workgroups over more rows (fewer adders per address; conv_igemm.py slot_rows)
+constexpr int kMaxStatRows = 16384;
 
 // Deterministic mode (--deterministic): every statistics producer writes slot = its block
 // index WITHOUT wrapping (the Python side sizes the slot buffer to >= the block count), so
@@ -154,8 +157,8 @@ inline bool deterministic() { return deterministic_flag() != 0; }
 // block count along the slot axis)
 inline unsigned stat_slot_mask(int rows, long nblocks) {
   if (!deterministic()) {
-    // rows: a power of two <= kStatSlots (fewer for small grids: less for the finalize to read)
-    FDT_CHECK(rows >= 1 && rows <= kStatSlots && (rows & (rows - 1)) == 0, "statistics slot rows");
+    // rows: a power of two (fewer for small grids: less for the finalize to read)
+    FDT_CHECK(rows >= 1 && rows <= kMaxStatRows && (rows & (rows - 1)) == 0, "statistics slot rows");
     return (unsigned)(rows - 1);
   }
   FDT_CHECK(nblocks <= rows, "deterministic mode: statistics slot buffer smaller than the block count");

@@ -1031,6 +1031,11 @@ static void launch_tile(const ConvArgs& a, int BM, int BN, int BK, int kg, bool 
   // BK = 128: half the K-loop trips for the latency-bound small-M layers (8x8 / 4x4 stages at
   // the 8-GPU per-GPU batch), twice the bytes in flight per prefetch stage
   FDT_T2(64, 64, 128) FDT_T(128, 64, 128) FDT_T(64, 128, 128)
+  // one 256-wide output-channel tile for the join prologue: each joined row is computed and
+  // stored once (with two column tiles every tile re-reads both join operands)
+  if constexpr (PRO == kProJoin) {
+    FDT_T(64, 256, 64) FDT_T(128, 256, 32) FDT_T(128, 256, 64)
+  }
 #undef FDT_T
 #undef FDT_T2
   FDT_CHECK(false, "unsupported conv tile");

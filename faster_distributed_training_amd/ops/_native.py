@@ -60,6 +60,9 @@ def load():
         # write-through (sc1) streaming outputs of the conv epilogues and the BN / join passes
         # (conv_igemm_impl.h st_out, common.h st8): measured bs128 5.56 -> 5.47 ms, bs1024 neutral
         m.set_conv_write_through(os.environ.get("FDT_CONV_WT", "1") == "1")
+    if hasattr(m, "set_ew_unroll"):
+        # loads-first streaming form of the join / normalise / fold passes (bn_kernels.hip kEwU)
+        m.set_ew_unroll(os.environ.get("FDT_EW_UNROLL", "1") == "1")
     return _mod
 
 

@@ -255,14 +255,26 @@ def _finalize_standalone(nat, kind, part, nq, C, fptr, fval):
         nat.stats_bwd_finalize(part.data_ptr(), part.shape[0], nq, C, *a, *b, _sp())
 
 
-def slot_rows(M: int | None = None) -> int:
+# large-M 3x3 convolutions (forward stats epilogue, BN-backward dgrad epilogue) spread their
+# workgroups over this many slot rows: at batch 1024 the 64-row layout's atomic contention costs
+# the 32x32 / 16x16 3x3 convs 4-10 us each in isolation, more than the longer finalize
+# (scripts/conv_probe3.py, profiles/r5/probe3_*.txt) -- but the whole step measured 25.37 ->
+# 25.44 ms (256 rows) / 25.56 (1024), profiles/r5/wide_rows_*.json: off by default (0)
+WIDE_ROWS = int(os.environ.get("FDT_STAT_WIDE_ROWS", "0"))
+WIDE_MIN_M = 1 << 18
+
+
+def slot_rows(M: int | None = None, wide: bool = False) -> int:
     """Statistics slot rows for a producer over M output rows: rows shared by workgroups
     (block index mod rows) -- STAT_SLOTS, or fewer for small M (a conv has at most M/64 row
-    blocks, and fewer rows are less for the finalize to read) -- or in deterministic mode
-    one row per workgroup (the BN-backward kernels cap their grid to the rows)."""
+    blocks, and fewer rows are less for the finalize to read), or WIDE_ROWS for a ``wide``
+    (3x3) producer over >= WIDE_MIN_M rows -- or in deterministic mode one row per workgroup
+    (the BN-backward kernels cap their grid to the rows)."""
     if not _native.deterministic():
         if M is None:
             return STAT_SLOTS
+        if wide and WIDE_ROWS > STAT_SLOTS and M >= WIDE_MIN_M:
+            return WIDE_ROWS
         need = min(STAT_SLOTS, max(1, -(-int(M) // 64)))
         return 1 << (need - 1).bit_length()
     assert M is not None, "deterministic mode sizes the slots by the producer's row count"
@@ -270,10 +282,10 @@ def slot_rows(M: int | None = None) -> int:
     return 1 << (need - 1).bit_length()
 
 
-def stat_slots(nq: int, C: int, device, M: int | None = None) -> torch.Tensor:
-    """A fresh zeroed statistics-slot buffer [slot_rows(M), nq, C] (the engine instead
+def stat_slots(nq: int, C: int, device, M: int | None = None, wide: bool = False) -> torch.Tensor:
+    """A fresh zeroed statistics-slot buffer [slot_rows(M, wide), nq, C] (the engine instead
     reuses one persistent workspace that its finalize kernels re-zero)."""
-    return torch.zeros(slot_rows(M), nq, C, device=device, dtype=torch.float32)
+    return torch.zeros(slot_rows(M, wide), nq, C, device=device, dtype=torch.float32)
 
 
 _NOLAZY = ([], [])

@@ -43,9 +43,12 @@ MATERIALIZE_3X3 = os.environ.get("FDT_MATERIALIZE_3X3", "1") != "0"
 # run a block's ReLU join inside the next block's first 1x1 conv (PRO_JOIN prologue) instead
 # of a standalone pass (see ResNetBodyFn.forward)
 JOIN_FOLD = os.environ.get("FDT_JOIN_FOLD", "1") != "0"
-# widest next-block 1x1 (output channels) that still takes the join fold: up to 128 with the
-# 128-row tiles, 256 with the 256-row tiles (one output-channel tile either way)
-JOIN_FOLD_MAX = int(os.environ.get("FDT_JOIN_FOLD_MAX", "64"))
+# widest next-block 1x1 (output channels) that still takes the join fold (_join_fold_tile: one
+# output-channel tile, and 256 only at >= 65536 rows)
+JOIN_FOLD_MAX = int(os.environ.get("FDT_JOIN_FOLD_MAX", "256"))
+# ... and, past 64 output channels without a tuned "fwd3" entry, only over at least this many rows
+# (batch 128's stage-2 joins measured 0.2 % slower folded: profiles/r5/joinfold_bs128_*.json)
+JOIN_FOLD_MIN_M = int(os.environ.get("FDT_JOIN_FOLD_MIN_M", str(1 << 18)))
 # run the classifier head (average pool + fc, bf16 autocast numerics) as two engine kernels
 # inside the body's graphs instead of eager PyTorch ops (see csrc/kernels/head.hip)
 FUSED_HEAD = os.environ.get("FDT_FUSED_HEAD", "1") != "0"
@@ -251,7 +254,11 @@ class Plan:
             for bi, b in enumerate(self.blocks):
                 hin, win = h, w
                 nxt = self.blocks[bi + 1] if bi + 1 < len(self.blocks) else None
-                folded = nxt is not None and b.join[0] == ACT_RELU and _join_foldable(nxt)
+                ho_, wo_ = h, w
+                for u in b.units:
+                    ho_, wo_ = ci.out_hw(ho_, wo_, u.shp)
+                folded = (nxt is not None and b.join[0] == ACT_RELU
+                          and _join_fold_tile(nxt, (N, ho_, wo_)) is not None)
                 for i, u in enumerate(b.units):
                     if i + 1 < len(b.units):
                         v = b.units[i + 1]  # consumer: a conv prologue unless a materialised 3x3
@@ -305,14 +312,15 @@ def _restore(t):
 _SLOTS: dict = {}
 
 
-def slots(nq, C, dev, M):
+def slots(nq, C, dev, M, wide=False):
     """The persistent statistics-slot workspace viewed as [rows, nq, C] for a producer over
-    M output rows (rows = 64, or one per workgroup in deterministic mode: ci.slot_rows).
+    M output rows (rows = 64, more for a large-M 3x3 conv (``wide``), or one per workgroup in
+    deterministic mode: ci.slot_rows).
     Producers (conv epilogues, BN-backward reductions) add into it with fp32 atomics; the
     consuming finalize / reduce kernel sums it in fp64 and re-zeroes it, so the next
     producer needs no memset.  One workspace suffices: every producer is consumed before
     the next one (and a view only ever covers rows its finalize re-zeroes)."""
-    rows = ci.slot_rows(M)
+    rows = ci.slot_rows(M, wide)
     n = max(ci.STAT_SLOTS * 3 * 2048, rows * nq * C)
     ws = _SLOTS.get(dev)
     if ws is None or ws.numel() < n:
@@ -356,7 +364,7 @@ def _out_stats(u: Unit, M, training, dev, lay):
     ent = lay[0].get(id(u)) if lay is not None else None
     if ent is None:
         st, fin = _fin_args(u, M, training, dev)
-        return st, slots(2, u.shp.cout, dev, M), fin, None
+        return st, slots(2, u.shp.cout, dev, M, u.shp.k > 1), fin, None
     off, rows = ent
     C = u.shp.cout
     reg = lay[1][off:off + (rows * 2 + 4) * C]
@@ -379,29 +387,51 @@ def conv_bn_fwd(x, u: Unit, s, t, act, training, dev, lazy_in=None, lay=None):
     return y, st, M, lz
 
 
-def conv_bn_fwd_join(pj, u: Unit, training, dev, lay=None):
+def conv_bn_fwd_join(pj, u: Unit, training, dev, lay=None, tile=None):
     """``conv_bn_fwd`` of a block's first (1x1) unit whose input is the PREVIOUS block's
     join, computed in the conv's operand staging (ci.conv_fwd_join); the join output (this
     block's x_in) and its ReLU mask are stored on the way.  pj = (y, s, t, r, s2, t2, out,
-    mask, lazy, lazy2)."""
+    mask, lazy, lazy2); ``tile``: _join_fold_tile's choice (None / "tuned": the tuned table)."""
     y, s, t, r, s2, t2, out, mask, lz1, lz2 = pj
     M = y.numel() // y.shape[-1]
     st, part, fin, lz = _out_stats(u, M, training, dev, lay)
-    tile = (256, 128, 32) if u.shp.cout > 128 else None  # one output-channel tile
+    tile = None if tile == "tuned" else tile
     yo, _ = ci.conv_fwd_join(y, r, s, t, s2, t2, u.wf, u.shp, out, mask, part=part, fin=fin, tile=tile, lazy=lz1,
                              lazy2=lz2)
     return yo, st, M, lz
 
 
-def _join_foldable(b_next) -> bool:
-    """Fold a join into the next block's first conv only where that conv has ONE output-channel
-    tile (Cout <= 64): each joined row is then produced once and the fused kernel streams at
-    HBM rate (ResNet-50 stage 1 at batch 1024: 365 us vs 137 us conv + 355 us join pass).
-    With several column tiles every tile re-reads both join operands and re-runs the join
-    arithmetic (measured 1.5-2x slower than conv + join pass at stages 2-4)."""
+def _join_fold_tile(b_next, shape):
+    """Tile of the next block's first 1x1 conv when it computes this block's join in its operand
+    staging (PRO_JOIN), or None for a standalone join pass.  The fused kernel wins when ONE
+    output-channel tile covers the conv (each joined row is then computed and stored once;
+    with several column tiles every tile re-reads both join operands: 1.2-2x slower than
+    conv + join pass) -- scripts/join_probe.py, profiles/r5/join_probe_*.txt:
+      Cout 64  (stage 1): the tuned tile; batch 1024 475 -> 355 us, batch 128 50 -> 44 us
+      Cout 128 (stage 2): 128x128x64 at >= 2^17 rows (242 -> 195 us), else 64x128x64 (31 -> 25 us
+                          in isolation, yet the batch-128 step measured 0.2 % slower folded)
+      Cout 256 (stage 3): 128x256x64 at >= 2^16 rows (133 -> 124 us); slower at batch 128.
+    A shape with a conv_tuned.json "fwd3" entry (scripts/retune_graph.py) is folded at that
+    entry ("tuned"); others past 64 channels only over >= JOIN_FOLD_MIN_M rows.  Whole step at
+    batch 1024: 25.66 -> 25.33 ms (profiles/r5/joinfold_bs1024_*.json).  ``shape``: the join's
+    NHWC shape."""
     u = b_next.units[0]
-    return (JOIN_FOLD and u.shp.k == 1 and u.shp.stride == 1 and u.shp.pad == 0 and u.shp.cin == u.shp.cxp
-            and u.shp.cin >= 8 and u.shp.cout <= min(JOIN_FOLD_MAX, 256))
+    N, H = int(shape[0]), int(shape[1])
+    M = N * H * int(shape[2])
+    if not (JOIN_FOLD and u.shp.k == 1 and u.shp.stride == 1 and u.shp.pad == 0 and u.shp.cin == u.shp.cxp
+            and u.shp.cin >= 8 and u.shp.cout <= JOIN_FOLD_MAX):
+        return None
+    if u.shp.cout <= 64:
+        return "tuned"
+    if u.shp.cout > 256 or (u.shp.cout > 128 and M < (1 << 16)):
+        return None
+    if ci.tuned("fwd3", N, H, u.shp):
+        return "tuned"
+    if M < JOIN_FOLD_MIN_M:
+        return None
+    if u.shp.cout <= 128:
+        return (128, 128, 64) if M >= (1 << 17) else (64, 128, 64)
+    return (128, 256, 64)
 
 
 def _fin_args(u: Unit, M, training, dev):
@@ -512,6 +542,7 @@ class ResNetBodyFn(torch.autograd.Function):
         stem_rec = (x_nhwc, y0, s0, t0, sm0, sa0)
         cur = "conv1"
         pending = None  # previous block's join, run inside this block's first conv
+        pend_tile = None  # ... at this tile (_join_fold_tile)
         for bi, b in enumerate(plan.blocks):
             if fs is not None and plan.stage_of[bi] != cur:
                 plan.release_stage(cur, fwd=True)
@@ -526,7 +557,7 @@ class ResNetBodyFn(torch.autograd.Function):
                 a_in = None
                 if ui == 0 and pending is not None:
                     # writes x_in (= the previous block's output) while staging it
-                    y, (su, tu, smu, sau), M, lzo = conv_bn_fwd_join(pending, u, training, dev, lay)
+                    y, (su, tu, smu, sau), M, lzo = conv_bn_fwd_join(pending, u, training, dev, lay, pend_tile)
                     pending = None
                 elif MATERIALIZE_3X3 and u.shp.k > 1 and s is not None:
                     # 3x3: normalise + activate the input ONCE instead of in every one of the
@@ -559,7 +590,8 @@ class ResNetBodyFn(torch.autograd.Function):
             if need_grad and b.join[0] == ACT_RELU:
                 mask = torch.empty(out.numel() // 8, device=dev, dtype=torch.uint8)
             nxt = plan.blocks[bi + 1] if bi + 1 < len(plan.blocks) else None
-            if nxt is not None and b.join[0] == ACT_RELU and _join_foldable(nxt):
+            pend_tile = _join_fold_tile(nxt, y3.shape) if nxt is not None and b.join[0] == ACT_RELU else None
+            if pend_tile is not None:
                 # the next block's first 1x1 conv computes this join while staging its operand
                 # and stores `out` + mask (one pass instead of join pass + operand re-read)
                 pending = (y3, s3, t3, sc[0] if sc else x_in, sc[1] if sc else None, sc[2] if sc else None, out, mask,
@@ -667,7 +699,7 @@ class ResNetBodyFn(torch.autograd.Function):
                 if i > 0:
                     yp, sp_, tp = ys[i - 1][0], ys[i - 1][1], ys[i - 1][2]
                     actp = b.units[i - 1].act_out
-                    pp = slots(2, u.shp.cin, dev, _rows(yp))
+                    pp = slots(2, u.shp.cin, dev, _rows(yp), u.shp.k > 1)
                     up = b.units[i - 1]
                     cf, (al_p, be_p), _ = coef_args(up, (ys[i - 1][3], ys[i - 1][4], ys[i - 1][5]),
                                                     training=training, dev=dev)

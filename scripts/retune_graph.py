@@ -131,7 +131,10 @@ def lookup_key(fn, orig):
     return seen[0] if seen else None
 
 
-def candidates(kind, shp, N, H):
+JOIN_TILES = [(64, 256, 64), (128, 256, 32), (128, 256, 64)]  # PRO_JOIN only (conv_igemm_impl.h)
+
+
+def candidates(kind, shp, N, H, op_key=None):
     Ho, Wo = ci.out_hw(H, H, shp)
     M = N * Ho * Wo
     out = []
@@ -145,7 +148,7 @@ def candidates(kind, shp, N, H):
                 out.append({"tile": list(t), "nsplit": ns})
     else:
         n_out = shp.cout if kind == "fwd" else shp.cin
-        for t in FWD_TILES:
+        for t in list(FWD_TILES) + (JOIN_TILES if op_key == "fwd3" else []):
             if n_out % t[1]:
                 continue
             for ns in FD_SPLITS:
@@ -196,8 +199,11 @@ def main():
             t_cur = timeit(fn, a.reps) * 1e3
             best = (t_cur, None)
             if a.loops and kind in ("fwd", "dgrad"):
-                # the K-loop form of the kernel the entry (or the heuristic) picks: time both
-                base = dict(cur) if cur else {}
+                if not cur or "tile" not in cur:
+                    print(f"b{N} {key:22s} {op_key:8s}: no tuned entry (heuristic launch), loop form skipped", flush=True)
+                    continue
+                # the K-loop form of the kernel the entry picks: time both
+                base = dict(cur)
                 base.pop("us", None)
                 res = {}
                 for lp in ("rot", "old", "rot", "old"):
@@ -221,7 +227,7 @@ def main():
                 continue
             if a.loops:
                 continue
-            for cand in candidates(kind, shp, N, H):
+            for cand in candidates(kind, shp, N, H, op_key):
                 ent = dict(cand)
                 if cur and "stages" in cur:
                     ent["stages"] = cur["stages"]

@@ -111,7 +111,8 @@ def test_conv_fwd_join_prologue(cuda, case, proj):
     want_mask = (joined.reshape(-1, 8) > 0).to(torch.int32)
     want_mask = (want_mask << torch.arange(8, device=cuda, dtype=torch.int32)).sum(1).to(torch.uint8)
     for tile, ns in [(None, None), ((64, 64, 64), 1), ((128, 64, 32), 3), ((128, 128, 32), None),
-                     ((64, 128, 128), 2), ((64, 64, 128), 1)]:
+                     ((64, 128, 128), 2), ((64, 64, 128), 1), ((128, 128, 64), 1), ((64, 128, 64), 1),
+                     ((128, 256, 64), 1), ((64, 256, 64), 2), ((128, 256, 32), 1)]:
         if tile and Cout % tile[1]:
             continue
         jout = torch.full_like(y, float("nan"))
