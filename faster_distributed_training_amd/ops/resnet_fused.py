@@ -104,6 +104,11 @@ def grad_ready(param):
             fn(param)
     if not acts:
         return
+    br = _ACTIVE_BRANCH
+    if br is not None and torch.cuda.current_stream() == br.main:
+        # a bucket completed by a gradient the main stream wrote (BN parameters): its other
+        # members may be weight gradients still running on the weight-gradient branch
+        br.join(keep=True)
     if rec is not None:
         rec.cut(acts)
     else:
@@ -515,6 +520,102 @@ def _rows(t):
     return t.numel() // t.shape[-1]
 
 
+# weight gradients on a second stream (a parallel branch of the captured backward graph): they
+# depend only on operands the dgrad chain has already produced, and nothing on the chain reads
+# them until the optimizer, so each one can run beside the next units' dgrad -> BN-backward
+# finalize -> fold chain.  Measured SLOWER on MI355X: batch 128 5.37 -> 5.96-5.99 ms, batch 1024
+# 24.93 -> 25.32 ms (profiles/r5/wgrad_branch_*.json) -- the ~50 cross-stream fork / join
+# dependencies per replayed backward cost more than the overlap returns, and the concurrent
+# weight-gradient grids take CUs from the critical-path chain.  Opt-in (FDT_WGRAD_BRANCH=1).
+WGRAD_BRANCH = os.environ.get("FDT_WGRAD_BRANCH", "0") == "1"
+WGRAD_BRANCH_KEEP = 8 << 30  # bytes of branch operands held before a full join
+
+
+class _WgradBranch:
+    """The weight-gradient branch of one backward.  Hazards: (1) every operand a branch kernel
+    reads stays referenced until the main stream has joined the branch, so the allocator cannot
+    hand its memory to a main-stream tensor while the branch still reads it; (2) the one
+    in-place overwrite of a branch operand -- an identity block's g_pre, accumulated into by
+    its first unit's dgrad (g_x aliases g_pre) -- waits for the event recorded after the wgrad
+    that reads it (``guard`` / ``wait``)."""
+
+    _streams: dict = {}
+
+    def __init__(self, dev):
+        s = _WgradBranch._streams.get(dev)
+        if s is None:
+            s = _WgradBranch._streams[dev] = torch.cuda.Stream(device=dev)
+        self.s = s
+        self.main = torch.cuda.current_stream(dev)
+        self.keep = []
+        self.kept = 0
+        self.event = None
+        self._seg = None
+
+    @staticmethod
+    def make(dev):
+        if not (WGRAD_BRANCH and dev.type == "cuda"):
+            return None
+        return _WgradBranch(dev)
+
+    def run(self, u, g, y, al, be, x, xs, xt, act, gs=None, guard=False):
+        rec = _graphs.active()
+        if rec is not None and (rec, len(rec.segments)) != self._seg:
+            # a graph segment may end at a hook's cut: the branch forked in it rejoins first
+            self._seg = (rec, len(rec.segments))
+            rec.joiners.append(lambda b=self.s: torch.cuda.current_stream().wait_stream(b))
+        self.s.wait_stream(self.main)
+        key = self._key()
+        with torch.cuda.stream(self.s):
+            wgrad_into(u, g, y, al, be, x, xs, xt, act, gs=gs)
+            # (a gradient hook inside may have cut the graph: the ended segment joined this
+            # branch, which is no longer part of the capture -- nothing to record then)
+            if guard and self._key() == key:
+                ev = torch.cuda.Event()
+                ev.record(self.s)
+                self.event = (ev, key)
+        ops = [t for t in (g, y, al, be, x, xs, xt, gs) if isinstance(t, torch.Tensor)]
+        self.keep.append(ops)
+        self.kept += sum(t.numel() * t.element_size() for t in ops)
+        if self.kept > WGRAD_BRANCH_KEEP:
+            self.join()
+
+    @staticmethod
+    def _key():
+        rec = _graphs.active()
+        return None if rec is None else (rec, len(rec.segments))
+
+    def _stale(self):
+        """Under a graph recording whose segment ended since the branch last forked: the
+        segment end already joined the branch (its joiner), and an event from the ended
+        capture would be a dependency on uncaptured work."""
+        rec = _graphs.active()
+        return rec is not None and (rec, len(rec.segments)) != self._seg
+
+    def wait(self):
+        """Main stream: after the guarded wgrad (before overwriting its operand in place) --
+        unless a segment ended since it was recorded (the segment end joined the branch)."""
+        if self.event is not None and self.event[1] == self._key():
+            self.main.wait_event(self.event[0])
+        self.event = None
+
+    def join(self, keep=False):
+        if not self._stale():
+            self.main.wait_stream(self.s)
+        if not keep:
+            self.keep, self.kept, self.event = [], 0, None
+
+
+_ACTIVE_BRANCH = None  # the weight-gradient branch of the backward in progress (grad_ready)
+
+
+def _wgrad(br, *args, guard=False, **kw):
+    if br is None:
+        wgrad_into(*args, **kw)
+    else:
+        br.run(*args, guard=guard, **kw)
+
+
 # ------------------------------------------------------------------ autograd node
 class ResNetBodyFn(torch.autograd.Function):
     @staticmethod
@@ -642,14 +743,26 @@ class ResNetBodyFn(torch.autograd.Function):
         dev = g.device
         recs = ctx.recs
         nblk = len(plan.blocks)
+        fs = plan.fsdp
+        global _ACTIVE_BRANCH
+        br = _ACTIVE_BRANCH = _WgradBranch.make(dev)
+        try:
+            return ResNetBodyFn._backward_blocks(ctx, plan, training, g, ghw, dev, recs, nblk, fs, br)
+        finally:
+            _ACTIVE_BRANCH = None
+
+    @staticmethod
+    def _backward_blocks(ctx, plan, training, g, ghw, dev, recs, nblk, fs, br):
+        nat = _native.native()
         joined = False  # g is already g_pre of the current block (its BN-backward coefficients
         joined_coef = None  # computed with the dgrad that completed it: joined_coef)
-        fs = plan.fsdp
         cur = None
         for bi in range(nblk - 1, -1, -1):
             b = plan.blocks[bi]
             if fs is not None and plan.stage_of[bi] != cur:
                 if cur is not None:
+                    if br is not None:
+                        br.join()  # the stage's gradients are complete before its reduce-scatter
                     plan.release_stage(cur, fwd=False)
                     fs.post_backward(cur)
                 cur = plan.stage_of[bi]
@@ -683,7 +796,7 @@ class ResNetBodyFn(torch.autograd.Function):
                 als, bes = coef_sc
                 g_x, _ = ci.conv_dgrad(gpre, sc[0], als, bes, u.wd, u.shp, tuple(x_in.shape), epi=ci.EPI_STORE,
                                        gs=sc[1])
-                wgrad_into(u, gpre, sc[0], als, bes, x_in, None, None, (ACT_NONE, 1.0), gs=sc[1])
+                _wgrad(br, u, gpre, sc[0], als, bes, x_in, None, None, (ACT_NONE, 1.0), gs=sc[1])
             else:
                 g_x = gpre  # identity: the x_in gradient accumulates onto g_pre in place
             # the block whose output is x_in: its join backward runs in the epilogue of the
@@ -712,18 +825,23 @@ class ResNetBodyFn(torch.autograd.Function):
                         g_prev, _ = ci.conv_dgrad(gf, None, None, None, u.wd, u.shp, tuple(yp.shape),
                                                   epi=ci.EPI_ACTBWD, ex=yp, es=sp_, et=tp, act=actp[0],
                                                   alpha=actp[1], part=pp, coef=cf)
-                        wgrad_into(u, gf, None, None, None, a_in if a_in is not None else yp,
-                                   None if a_in is not None else sp_, None if a_in is not None else tp,
-                                   (ACT_NONE, 1.0) if a_in is not None else actp)
+                        _wgrad(br, u, gf, None, None, None, a_in if a_in is not None else yp,
+                               None if a_in is not None else sp_, None if a_in is not None else tp,
+                               (ACT_NONE, 1.0) if a_in is not None else actp)
                     else:
                         g_prev, _ = ci.conv_dgrad(g_cur, y, al, be, u.wd, u.shp, tuple(yp.shape),
                                                   epi=ci.EPI_ACTBWD, ex=yp, es=sp_, et=tp, act=actp[0],
                                                   alpha=actp[1], part=pp, gs=gs_cur, coef=cf)
-                        wgrad_into(u, g_cur, y, al, be, yp, sp_, tp, actp, gs=gs_cur)
+                        # (the last unit reads g_pre: an identity block's first-unit dgrad
+                        # later accumulates into it in place -- guarded)
+                        _wgrad(br, u, g_cur, y, al, be, yp, sp_, tp, actp, gs=gs_cur,
+                               guard=(i == len(b.units) - 1 and sc is None))
                     coef_ready(up)
                     al, be = al_p, be_p
                     g_cur, gs_cur = g_prev, None
                 else:
+                    if br is not None and sc is None:
+                        br.wait()  # g_x aliases g_pre: its last reader (a branch wgrad) first
                     if prev is not None:
                         _, pys, psc, pout, pmask = prec
                         pul = prev.units[-1]
@@ -738,10 +856,12 @@ class ResNetBodyFn(torch.autograd.Function):
                     else:
                         ci.conv_dgrad(g_cur, y, al, be, u.wd, u.shp, tuple(x_in.shape), epi=ci.EPI_ADD, out=g_x,
                                       gs=gs_cur)
-                    wgrad_into(u, g_cur, y, al, be, x_in, None, None, (ACT_NONE, 1.0), gs=gs_cur)
+                    _wgrad(br, u, g_cur, y, al, be, x_in, None, None, (ACT_NONE, 1.0), gs=gs_cur)
             g = g_x
             joined = prev is not None
         if fs is not None and cur is not None:
+            if br is not None:
+                br.join()
             plan.release_stage(cur, fwd=False)
             fs.post_backward(cur)
             fs.pre_backward("conv1")
@@ -755,7 +875,9 @@ class ResNetBodyFn(torch.autograd.Function):
         nat.act_bwd_reduce(g.data_ptr(), y0.data_ptr(), s0.data_ptr(), t0.data_ptr(), gy0.data_ptr(),
                            part.data_ptr(), part.shape[0], M0, C0, st.act_out[0], float(st.act_out[1]), 1, _sp())
         (al, be), _ = bwd_finalize(part, 2, st, (sm0, sa0, M0), training=training, dev=dev)
-        wgrad_into(st, gy0, y0, al, be, x_img, None, None, (ACT_NONE, 1.0))
+        _wgrad(br, st, gy0, y0, al, be, x_img, None, None, (ACT_NONE, 1.0))
+        if br is not None:
+            br.join()
         if fs is not None:
             fs.post_backward("conv1")
         if not getattr(ctx, "keep", False):

@@ -141,7 +141,7 @@ def drive(gens, side=None, defer_out=None):
 
     ``defer_out`` (a list): the deferred work is appended to it instead of being solved (the
     HIP-graph path captures it as a separate graph on the side stream)."""
-    from ..ops.eigh import eigh_many
+    from ..ops.eigh import NGD_TOL, eigh_many
     results = [None] * len(gens)
     deferred = []
 
@@ -164,7 +164,7 @@ def drive(gens, side=None, defer_out=None):
             pending[i] = z
     while pending:
         idx = list(pending)
-        outs = eigh_many([pending[i] for i in idx])
+        outs = eigh_many([pending[i] for i in idx], tol=NGD_TOL)
         pending = {}
         for i, o in zip(idx, outs):
             z = advance(i, o)
@@ -178,13 +178,13 @@ def drive(gens, side=None, defer_out=None):
             return results, None
         side.wait_stream(torch.cuda.current_stream(side.device))
         with torch.cuda.stream(side):
-            for d, (c, U) in zip(deferred, eigh_many([d.Z for d in deferred])):
+            for d, (c, U) in zip(deferred, eigh_many([d.Z for d in deferred], tol=NGD_TOL)):
                 d.fn(c, U)
             done = torch.cuda.Event()
             done.record(side)
         return results, (done, deferred)
     if deferred:
-        for d, (c, U) in zip(deferred, eigh_many([d.Z for d in deferred])):
+        for d, (c, U) in zip(deferred, eigh_many([d.Z for d in deferred], tol=NGD_TOL)):
             d.fn(c, U)
     return results
 
@@ -734,7 +734,7 @@ class NGD(SGD):
     def _capture(self, grad_scale):
         """Capture one step kind: the main graph (preconditioning + momentum update) and, on
         update steps, the deferred eigensolves + state updates as a second graph."""
-        from ..ops.eigh import eigh_many
+        from ..ops.eigh import NGD_TOL, eigh_many
         from ..parallel.graphs import capture_guard
         self.sync_state()
         dev = self.flat.device
@@ -758,7 +758,7 @@ class NGD(SGD):
                     side_g = torch.cuda.CUDAGraph()
                     with torch.cuda.graph(side_g, pool=self._gpool, stream=cs, capture_error_mode="thread_local"), \
                             capture_guard():
-                        for d, (c, U) in zip(deferred, eigh_many([d.Z for d in deferred])):
+                        for d, (c, U) in zip(deferred, eigh_many([d.Z for d in deferred], tol=NGD_TOL)):
                             d.fn(c, U)
         finally:
             for st, t in zip(sts, t0):  # the captures ran the host schedule once: undo it

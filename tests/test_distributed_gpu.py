@@ -625,7 +625,11 @@ def _zero_ngd_graphs_transformer_worker(rank, world):
     b = torch.cat([v.flatten() for v in runs[False].values()])
     assert ((a - b).norm() / b.norm()).item() < 2e-3
     for k, v in runs[False].items():
-        assert ((runs[True][k] - v).norm() / v.norm().clamp_min(1e-6)).item() < 2e-2, k
+        # per tensor: 2 % relative, with an absolute floor of 2e-4 RMS per element for the
+        # small-norm tensors (zero-initialised LayerNorm biases: run-to-run atomics noise is
+        # amplified by the preconditioner at the scale of their few-step updates)
+        d = (runs[True][k] - v).norm().item()
+        assert d < 2e-2 * v.norm().item() + 2e-4 * v.numel() ** 0.5, (k, d, v.norm().item())
 
 
 def test_sharded_ngd_graphs_transformer_world2(cuda):
