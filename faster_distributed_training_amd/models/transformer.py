@@ -61,6 +61,19 @@ class Transformer(nn.Module):
         self.mix_override = None
         self.init_params()
 
+    def flat_adjacent(self):
+        """Parameter groups the flat buffers keep adjacent, in this order (utils/flat.py): all
+        parameters of one shape, in registration order.  Then (1) each attention block's Q / K / V
+        weights and biases sit back to back, so the fused projection reads the stacked bf16
+        weights as one view of the shadow buffer (no per-forward concatenation), and (2) NGD's
+        batched shape groups are views of the flat gradient (no stack / scatter copies,
+        optim/ngd.py ``_group_view``)."""
+        by_shape = {}
+        for p in self.parameters():
+            if p.requires_grad:
+                by_shape.setdefault(tuple(p.shape), []).append(p)
+        return [g for g in by_shape.values() if len(g) > 1]
+
     def sample_lam(self) -> float:
         """The manifold-mixup coefficient (host sample, as the reference's ``.item()``)."""
         if self.alpha > 0:
@@ -75,6 +88,9 @@ class Transformer(nn.Module):
         x = embeddings + encodings
         if mask is not None:
             mask = mask.reshape(mask.shape[0], mask.shape[-1])
+            if mask.dtype != torch.uint8:
+                # once per forward, not once per layer (the attention kernels take uint8)
+                mask = (mask != 0).to(torch.uint8)
         for i in range(self.n_layers):
             x = self.sublayer_attention[i](x, mask)
             x = self.sublayer_ffn[i](x)

@@ -198,6 +198,20 @@ def linear(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor | None = No
         return _Linear.apply(x, weight, bias, dt, bias_grad)
 
 
+def stacked(ts):
+    """``torch.cat(ts, 0)`` -- as a zero-copy view when the tensors already sit back to back in
+    one buffer (utils/flat.py keeps the Q / K / V shadows adjacent: ``flat_adjacent``)."""
+    t0 = ts[0]
+    if all(t.is_contiguous() and t.dtype == t0.dtype and t.shape[1:] == t0.shape[1:] for t in ts):
+        es = t0.element_size()
+        if all(ts[i + 1].data_ptr() == ts[i].data_ptr() + ts[i].numel() * es for i in range(len(ts) - 1)) and \
+                all(t.untyped_storage().data_ptr() == t0.untyped_storage().data_ptr() for t in ts):
+            rows = sum(t.shape[0] for t in ts)
+            shape = (rows,) + tuple(t0.shape[1:])
+            return t0.as_strided(shape, torch.empty(shape, device="meta").stride(), t0.storage_offset())
+    return torch.cat(ts, 0)
+
+
 class _LinearCat(torch.autograd.Function):
     """``F.linear(x, cat(ws), cat(bs))`` for row-stacked weights (the fused Q/K/V projection of
     three ``nn.Linear``s): the weight gradient is one split-K product over the stacked rows
@@ -209,8 +223,8 @@ class _LinearCat(torch.autograd.Function):
     def forward(ctx, x, dt, n, *params):
         ws, bs = params[:n], params[n:]
         xc = x.to(dt)
-        wc = torch.cat([cast_weight(w, dt) for w in ws], 0)
-        bc = torch.cat([cast_weight(b, dt) for b in bs], 0) if bs else None
+        wc = stacked([cast_weight(w, dt) for w in ws])
+        bc = stacked([cast_weight(b, dt) for b in bs]) if bs else None
         y = F.linear(xc, wc, bc)
         ctx.save_for_backward(xc, wc)
         ctx.params = (ws, bs)

@@ -512,6 +512,18 @@ class OnlineNaturalGradient:
         return Y.view(shp).transpose(-1, self.axis)
 
 
+def _group_view(grad, slots):
+    """The stacked [G, *shape] gradients of a shape group as a VIEW of the flat gradient when
+    its slots sit back to back without padding (models can ask for that: utils/flat.py
+    ``flat_adjacent``), else None (the caller stacks copies)."""
+    s0 = slots[0]
+    n = s0.numel
+    for i, s in enumerate(slots):
+        if s.offset != s0.offset + i * n or tuple(s.shape) != tuple(s0.shape):
+            return None
+    return grad[s0.offset:s0.offset + n * len(slots)].view(len(slots), *s0.shape)
+
+
 class _ShapeGroup:
     def __init__(self, shape, params, alpha, rank, update_period, eta, dtype, device):
         self.shape = tuple(shape)
@@ -622,8 +634,10 @@ class NGD(SGD):
             if self.groups is None:
                 self._build_groups()
             live = [(sg, slots) for sg, slots in self.groups if sg.axes]
-            gens = [sg.precondition_gen(torch.stack([grad[s.offset:s.offset + s.numel].view(s.shape) for s in slots]))
-                    for sg, slots in live]
+            views = [_group_view(grad, slots) for _, slots in live]
+            gens = [sg.precondition_gen(v if v is not None else
+                                        torch.stack([grad[s.offset:s.offset + s.numel].view(s.shape) for s in slots]))
+                    for (sg, slots), v in zip(live, views)]
             side = self._side_stream(grad)
             if defer_out is not None:
                 outs = drive(gens, defer_out=defer_out)
@@ -632,11 +646,16 @@ class NGD(SGD):
             else:
                 outs = drive(gens)
             dst, src = [], []
-            for (sg, slots), out in zip(live, outs):
+            for (sg, slots), out, v in zip(live, outs, views):
+                if v is not None:
+                    if out.data_ptr() != v.data_ptr():
+                        v.copy_(out)  # one contiguous copy per shape group
+                    continue
                 for i, s in enumerate(slots):
                     dst.append(grad[s.offset:s.offset + s.numel].view(s.shape))
                     src.append(out[i])
-            torch._foreach_copy_(dst, src)  # multi-tensor launches, not one copy per parameter
+            if dst:
+                torch._foreach_copy_(dst, src)  # multi-tensor launches, not one copy per parameter
 
     @torch.no_grad()
     def _step(self, grad_scale, found_inf, d_override=None):

@@ -30,7 +30,12 @@ class DeviceMeter:
         self.reset()
 
     def reset(self):
-        self.acc = torch.zeros(3, device=self.device, dtype=torch.float32)
+        # zeroed in place once allocated: a captured training step (the transformer's loss
+        # kernel inside its HIP graph) keeps adding into this buffer's address
+        if getattr(self, "acc", None) is None:
+            self.acc = torch.zeros(3, device=self.device, dtype=torch.float32)
+        else:
+            self.acc.zero_()
         self.steps = 0
         self.fused = False
 

@@ -28,6 +28,7 @@ from ..ops.mixup import mixup_criterion
 from ..optim.flat_optim import SGD, Adam, DeviceGradScaler, GradClipper, MirrorMADGRAD, MADGRAD
 from ..optim.ngd import NGD
 from ..parallel import dist as pdist
+from ..ops import _native
 from ..parallel.graphs import SegmentedStep, capture_guard as _graph_guard
 from ..utils.env import default_device, print0, seed_everything
 from ..utils.flat import FlatParams
@@ -310,7 +311,7 @@ class TransformerTrainer:
         with self._autocast():
             logits, perm, lam = self.model(tokens, types, self.pos_index, mask)
             prof.mark("loss")
-            loss = mixup_criterion(None, logits, labels, labels[perm], lam)
+            loss = mixup_criterion(None, logits, labels, labels[perm], lam, meter=self.meter)
         prof.mark("backward")
         self.scaler.scale_loss(loss).backward()
         return loss, logits, perm, lam
@@ -320,9 +321,18 @@ class TransformerTrainer:
         st["types"].copy_(types, non_blocking=True)
         st["masks"].copy_(masks, non_blocking=True)
         st["labels"].copy_(labels, non_blocking=True)
-        torch.randperm(tokens.shape[0], device=self.device, out=st["perm"])
         lam = self.model.sample_lam()
-        st["lam"].fill_(lam)
+        if st.get("prep"):
+            # one kernel (csrc/kernels/mixup.hip mixup_prep): the device permutation seeded from
+            # the host generator, the permuted labels and the lambda vector -- instead of
+            # randperm's sort passes, a label gather and a fill
+            seed = int(torch.randint(0, 2**62, (1,)).item())
+            _native.native().mixup_prep(st["labels"].data_ptr(), st["labels"].shape[0], float(lam), seed,
+                                        st["perm"].data_ptr(), st["yb"].data_ptr(), st["lam"].data_ptr(),
+                                        _native.stream_ptr())
+        else:
+            torch.randperm(tokens.shape[0], device=self.device, out=st["perm"])
+            st["lam"].fill_(lam)
         st["seed"].random_()
         return lam
 
@@ -344,16 +354,21 @@ class TransformerTrainer:
                 torch.cuda.current_stream().wait_stream(s)
                 return out
             B = tokens.shape[0]
+            prep = (labels.dtype == torch.int64 and 1 <= B <= 1024 and hasattr(_native.native(), "mixup_prep"))
             st = dict(tokens=torch.empty_like(tokens), types=torch.empty_like(types), masks=torch.empty_like(masks),
                       labels=torch.empty_like(labels),
-                      perm=torch.empty(B, dtype=torch.long, device=self.device),
+                      perm=torch.empty(B, dtype=torch.int32 if prep else torch.long, device=self.device),
+                      yb=torch.empty_like(labels),
                       lam=torch.empty(B, dtype=torch.float32, device=self.device),
-                      seed=torch.zeros(1, dtype=torch.int64, device=self.device))
+                      seed=torch.zeros(1, dtype=torch.int64, device=self.device), prep=prep)
             def fwd():
                 mask = st["masks"].view(B, 1, 1, st["masks"].shape[1])
                 with self._autocast(cache=False):  # no cast cache across a graph capture
                     logits, perm, _ = self.model(st["tokens"], st["types"], self.pos_index, mask)
-                    loss = mixup_cross_entropy(logits, st["labels"], st["labels"][perm], st["lam"])
+                    yb = st["yb"] if prep else st["labels"][perm]
+                    # the loss kernel also accumulates the step's loss / accuracy into the meter
+                    # (captured: every replay adds; DeviceMeter.reset zeroes in place)
+                    loss = mixup_cross_entropy(logits, st["labels"], yb, st["lam"], meter=self.meter)
                 return loss, logits
 
             torch.cuda.synchronize()
@@ -376,10 +391,13 @@ class TransformerTrainer:
             finally:
                 AN.DEVICE_SEED = None
                 self.model.mix_override = None
-            st.update(loss=loss, logits=logits)
+            st.update(loss=loss, logits=logits, meter=bool(self.meter.fused))
+            self.meter.fused = False
             self._graphs[key] = ent = st
         lam = self._graph_fill(ent, tokens, labels, types, masks)
         ent["replay"]()
+        if ent["meter"]:
+            self.meter.fused = True  # this replay accumulated the meter (train_step: count only)
         step = ent.get("step")
         if step is not None and step.rec.needs_check:
             # first replay with the bucket all-reduces captured in-graph: checked against eager
@@ -423,7 +441,7 @@ class TransformerTrainer:
                 self.scheduler, torch.optim.lr_scheduler.OneCycleLR):
             if self.scheduler.last_epoch + 1 < self.scheduler.total_steps:
                 self.scheduler.step()  # per batch, as OneCycleLR intends (Q9)
-        self.meter.update(loss, logits.detach(), labels, labels[perm], lam)
+        self.meter.update(loss, logits.detach(), labels, None if self.meter.fused else labels[perm.long()], lam)
         prof.end_step()
         self.global_step += 1
         return loss

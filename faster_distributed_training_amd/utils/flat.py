@@ -96,6 +96,38 @@ def ngd_balanced_order(shapes, world, slack=1.15):
     return order, runs
 
 
+def _adjacent_groups(named, groups):
+    """Reorder (name, param) so that each group's parameters (a list, in the given order) sit
+    next to each other where the group's first member was: e.g. the Q / K / V projections of
+    an attention block, whose stacked bf16 weights the fused projection can then read as ONE
+    contiguous view of the shadow buffer instead of concatenating them every forward
+    (ops/linear.py ``_LinearCat``)."""
+    pos = {id(p): i for i, (_, p) in enumerate(named)}
+    moved = {}
+    for grp in groups:
+        idx = [pos.get(id(p)) for p in grp]
+        if len(grp) < 2 or any(i is None for i in idx) or any(id(p) in moved for p in grp):
+            continue
+        first = min(idx)
+        for p in grp:
+            moved[id(p)] = first
+    if not moved:
+        return named
+    out, placed = [], set()
+    by_first = {}
+    for grp in groups:
+        if grp and id(grp[0]) in moved:
+            by_first.setdefault(moved[id(grp[0])], []).append(grp)
+    for i, (n, p) in enumerate(named):
+        for grp in by_first.get(i, []):
+            for q in grp:
+                out.append(named[pos[id(q)]])
+                placed.add(id(q))
+        if id(p) not in moved and id(p) not in placed:
+            out.append((n, p))
+    return out
+
+
 class FlatParams:
     """``partition=W``: the slots are split into W contiguous runs of whole parameters
     (balanced) and run r is placed at offset r*chunk (chunk = the longest run, aligned), so
@@ -113,6 +145,8 @@ class FlatParams:
             named = [(names[i] if names else f"p{i}", p) for i, p in enumerate(plist)]
         if reverse:
             named = named[::-1]
+        if isinstance(module_or_params, nn.Module) and hasattr(module_or_params, "flat_adjacent"):
+            named = _adjacent_groups(named, module_or_params.flat_adjacent())
         self.slots: list[Slot] = []
         self.runs = None
         self.chunk = 0

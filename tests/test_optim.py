@@ -242,3 +242,38 @@ def test_ngd_balanced_partition_resnet50():
             total = sum(p.numel() for p in m.parameters())
             assert f.chunk <= 1.15 * total / 8 + 4096
     assert spread["ngd"] < 1.1 and spread["ngd"] < spread["numel"], spread
+
+
+def test_ngd_shape_groups_as_flat_views_equal_stacked(monkeypatch):
+    """A model that asks for same-shape parameters to sit back to back in the flat buffers
+    (``flat_adjacent``, the Transformer does) gets its NGD shape groups as VIEWS of the flat
+    gradient (no stack / scatter copies, optim/ngd.py ``_group_view``) -- the same steps as
+    with stacked copies, and the fused Q/K/V projection reads its weights as one view."""
+    import faster_distributed_training_amd.optim.ngd as N
+    from faster_distributed_training_amd.models.transformer import Transformer
+    from faster_distributed_training_amd.ops.linear import stacked
+
+    def run(views):
+        torch.manual_seed(0)
+        m = Transformer(4, 300, n_layers=2, d_model=64, h=4, d_ff=128, d_hidden=128, maxlen=64).double()
+        f = FlatParams(m, dtype=torch.float64)
+        if not views:
+            monkeypatch.setattr(N, "_group_view", lambda grad, slots: None)
+        o = NGD(f, lr=0.05, momentum=0.9, weight_decay=1e-4)
+        g = torch.Generator().manual_seed(1)
+        for _ in range(12):
+            f.grad.copy_(torch.randn(f.numel, generator=g, dtype=torch.float64))
+            o.step()
+        monkeypatch.undo()
+        return f, m
+
+    fv, m = run(True)
+    fs, _ = run(False)
+    assert torch.equal(fv.data, fs.data)
+    o = NGD(fv, lr=0.05)
+    o._build_groups()
+    assert sum(N._group_view(fv.grad, slots) is not None for sg, slots in o.groups if sg.axes) >= 3
+    heads = m.sublayer_attention[0].multiheads.heads
+    w = stacked([l.weight for l in heads])
+    assert w.data_ptr() == heads[0].weight.data_ptr() and w.shape == (192, 64)
+    assert torch.equal(w, torch.cat([l.weight for l in heads]))

@@ -136,3 +136,24 @@ def test_capture_guard_refuses_data_dependent_ops(cuda):
     with pytest.raises(CaptureUnsafeOp):
         with capture_guard():
             out.backward()
+
+
+def test_graph_step_accumulates_meter_in_loss_kernel(cuda, monkeypatch):
+    """The replayed step's loss kernel adds the loss / lambda-weighted accuracy into the
+    DeviceMeter (no per-step accuracy kernels); the meter's buffer keeps its address across
+    resets.  Its loss sum equals the sum of the returned step losses, over warm-up, capture
+    and replays alike, and every sample is counted once."""
+    tr = _trainer(True, monkeypatch)
+    it = iter(tr.train_loader)
+    acc_ptr = tr.meter.acc.data_ptr()
+    losses = []
+    for _ in range(6):
+        losses.append(float(tr.train_step(*next(it))))
+    torch.cuda.synchronize()
+    assert any(isinstance(v, dict) and v.get("meter") for v in tr._graphs.values()), "fused meter not captured"
+    loss_sum, correct, total = tr.meter.acc.tolist()
+    assert abs(loss_sum - sum(losses)) <= 1e-4 * max(1.0, abs(sum(losses))), (loss_sum, losses)
+    assert total == 6 * 32 and 0.0 <= correct <= total
+    assert tr.meter.steps == 6
+    tr.meter.reset()
+    assert tr.meter.acc.data_ptr() == acc_ptr and float(tr.meter.acc.abs().sum()) == 0.0
