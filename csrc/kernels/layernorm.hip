@@ -124,7 +124,7 @@ __global__ __launch_bounds__(64 * kLnWaves) void layernorm_bwd_kernel(const TG* 
     int q = j / d, c = j % d;
     float acc = 0.f;
     for (int ww = 0; ww < kLnWaves; ++ww) acc += lds[(ww * 2 + q) * d + c];
-    part[((long)q * gridDim.x + blockIdx.x) * d + c] = acc;
+    part[((long)blockIdx.x * 2 + q) * d + c] = acc;  // [block][gamma | beta][d]
   }
 }
 

@@ -74,7 +74,7 @@ class _LayerNormNative(torch.autograd.Function):
         # ~8-16 rows per 4-wave block: enough workgroups to fill the chip at 32 samples / GPU
         # (4096 rows: 512 blocks; the old 32 rows per block left half the CUs idle)
         nblk = max(1, min(2048, (rows + 7) // 8))
-        part = torch.empty(2, nblk, d, device=x2.device, dtype=torch.float32)
+        part = torch.empty(nblk, 2, d, device=x2.device, dtype=torch.float32)  # [block][gamma | beta][d]
         gres = None
         if ctx.res is not None and ctx.res.g is not None:
             gres = ctx.res.g.reshape(rows, d)
@@ -83,17 +83,23 @@ class _LayerNormNative(torch.autograd.Function):
         nat.layernorm_bwd(gy2.data_ptr(), x2.data_ptr(), a.data_ptr(), mean.data_ptr(), rstd.data_ptr(),
                           gx.data_ptr(), 0 if gres is None else gres.data_ptr(), part.data_ptr(), rows, d, nblk,
                           DT[gy2.dtype], DT[x2.dtype], DT[a.dtype], float(ctx.eps), _native.stream_ptr())
-        from .linear import direct_target, mark_ready, slab_sum_into
+        from .linear import direct_target, mark_ready
         pa, pb = ctx.params
         ta = direct_target(pa) if ctx.needs_input_grad[1] else None
         tb = direct_target(pb) if ctx.needs_input_grad[2] else None
         if ta is not None and tb is not None:  # partials folded straight into the fp32 grads
-            slab_sum_into(part[0], ta)
-            slab_sum_into(part[1], tb)
+            sp = _native.stream_ptr()
+            if tb.data_ptr() == ta.data_ptr() + d * 4:
+                # gamma / beta adjacent in the flat gradient (utils/flat.py flat_adjacent): one
+                # pass over the [block][2][d] partials
+                nat.slab_sum_acc(part.data_ptr(), ta.data_ptr(), nblk, 2 * d, 2 * d, sp)
+            else:
+                nat.slab_sum_acc(part.data_ptr(), ta.data_ptr(), nblk, 2 * d, d, sp)
+                nat.slab_sum_acc(part.data_ptr() + d * 4, tb.data_ptr(), nblk, 2 * d, d, sp)
             mark_ready(pa)
             mark_ready(pb)
             return gx.view(ctx.shape), None, None, None, None, None
-        ga, gb = part.sum(1).unbind(0)
+        ga, gb = part.sum(0).unbind(0)
         return gx.view(ctx.shape), ga.to(a.dtype), gb.to(a.dtype), None, None, None
 
 

@@ -252,9 +252,14 @@ class _LinearCat(torch.autograd.Function):
                 try:
                     p = torch.bmm(g2.view(s, M // s, -1).transpose(1, 2), x2.view(s, M // s, -1),
                                   out_dtype=torch.float32)
-                    for i in range(n):
-                        _native.native().slab_sum_acc(p.data_ptr() + offs[i] * K * 4, tg[i].data_ptr(), s, R * K,
-                                                      rows[i] * K, _native.stream_ptr())
+                    if all(tg[i + 1].data_ptr() == tg[i].data_ptr() + rows[i] * K * 4 for i in range(n - 1)):
+                        # the parameters' gradients are adjacent (utils/flat.py flat_adjacent): one pass
+                        _native.native().slab_sum_acc(p.data_ptr(), tg[0].data_ptr(), s, R * K, R * K,
+                                                      _native.stream_ptr())
+                    else:
+                        for i in range(n):
+                            _native.native().slab_sum_acc(p.data_ptr() + offs[i] * K * 4, tg[i].data_ptr(), s,
+                                                          R * K, rows[i] * K, _native.stream_ptr())
                     done = True
                 except (TypeError, RuntimeError):
                     done = False

@@ -7,7 +7,7 @@ export TMPDIR=/tmp
 OUT=gpurun_out/${1:-r5y}
 mkdir -p "$OUT"
 FDT_NATIVE=1 timeout -k 10 120 python -c "from faster_distributed_training_amd.ops import _native; _native.native()" || { echo "native extension stale or missing"; exit 1; }
-timeout -k 10 900 python -u -m pytest tests/test_transformer_graphs.py tests/test_transformer_fusions.py tests/test_attention_gpu.py tests/test_linear.py tests/test_ngd_graphs.py -m gpu -q -p no:cacheprovider --timeout 300 --timeout-method thread > "$OUT/pytest.log" 2>&1; rc=$?
+timeout -k 10 900 python -u -m pytest tests/test_transformer_graphs.py tests/test_transformer_fusions.py tests/test_attention_gpu.py tests/test_linear.py tests/test_ngd_graphs.py tests/test_gpu_kernels.py -m gpu -q -p no:cacheprovider --timeout 300 --timeout-method thread > "$OUT/pytest.log" 2>&1; rc=$?
 echo "pytest rc=$rc"; tail -1 "$OUT/pytest.log"; grep -E "^(FAILED|ERROR)" "$OUT/pytest.log" | head; case $rc in 0|1) ;; *) exit 1;; esac
 run() {
   local name=$1; shift
