@@ -220,10 +220,25 @@ class _MixupCENative(torch.autograd.Function):
     def backward(ctx, gl):
         glog, dlam = ctx.saved_tensors
         glam = dlam * gl if (dlam is not None and ctx.needs_input_grad[3]) else None
-        g = glog * gl  # (0-dim fp32 gl: result stays in glog.dtype)
+        # (backward seeded with unit_grad(): d(loss) == 1 -- no scaling pass over d(logits))
+        g = glog if getattr(gl, "_fdt_unit", False) else glog * gl  # (0-dim fp32 gl: stays in glog.dtype)
         if g.dtype != ctx.out_dtype:
             g = g.to(ctx.out_dtype)  # fp16: cast AFTER the loss scale is applied
         return g, None, None, glam, None, None
+
+
+_UNIT: dict = {}
+
+
+def unit_grad(device):
+    """A persistent 0-dim fp32 one to seed ``loss.backward(unit_grad(dev))`` with: autograd
+    hands the same tensor to the loss node, whose backward then skips its scaling pass (and
+    autograd skips its ones_like fill) -- two launches per step."""
+    t = _UNIT.get(device)
+    if t is None:
+        t = _UNIT[device] = torch.ones((), device=device, dtype=torch.float32)
+        t._fdt_unit = True
+    return t
 
 
 def mixup_cross_entropy(logits, y_a, y_b, lam_vec, meter=None):

@@ -100,6 +100,7 @@ class BucketReducer:
             for i in idx:
                 self.bucket_of[id(flat.slots[i].param)] = b
         self.pending = [len(idx) for (_, _, idx) in self.buckets]
+        self.ready = set()  # parameters signalled ready this step
         self.works = [None] * len(self.buckets)
         # reduced-precision wire format: ONE persistent buffer shaped like the flat gradient,
         # each bucket a view of it (no per-step allocation; the cast in and out are the only
@@ -126,6 +127,13 @@ class BucketReducer:
         the capture is cut here and the launch runs between the replayed segments."""
         if not self.enabled:
             return None
+        if id(p) in self.ready:
+            # a second readiness signal for the same parameter in one step (autograd's
+            # post-accumulate hook AND the engine's grad-ready hook can both fire for a
+            # parameter whose gradient one path writes directly): counted once, or the bucket
+            # would launch before its last member is written
+            return None
+        self.ready.add(id(p))
         b = self.bucket_of[id(p)]
         self.pending[b] -= 1
         if self.pending[b] == 0:
@@ -205,6 +213,7 @@ class BucketReducer:
                 self.flat.grad[s:e].div_(self.ws)
         self.works = [None] * len(self.buckets)
         self.pending = [len(idx) for (_, _, idx) in self.buckets]
+        self.ready = set()
 
     # ------------------------------------------------------------------ sync
     @torch.no_grad()

@@ -283,7 +283,8 @@ class SegmentedStep:
         side.wait_stream(torch.cuda.current_stream(self.device))
         torch.cuda.synchronize(self.device)
         rec = Recorder(self.pool)
-        self.one = torch.ones((), device=self.device)  # static seed gradient of the loss
+        from ..ops.mixup import unit_grad
+        self.one = unit_grad(self.device)  # static seed gradient of the loss (the loss node skips its scaling)
         with torch.cuda.stream(side):
             # the forward is a Recorder too: FSDP's per-unit gathers (static mode) cut it into
             # segments, each unit's all-gather wait / next-unit prefetch between them

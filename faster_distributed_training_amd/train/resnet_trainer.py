@@ -21,7 +21,7 @@ import torch.nn as nn
 
 from ..data.cifar import CLASSES, CIFAR10, DeviceCIFARLoader, augment_order, synthetic_cifar
 from ..models import resnet as resnet_models
-from ..ops.mixup import MetaMixup, mixup_criterion, mixup_criterion_meta, mixup_data
+from ..ops.mixup import unit_grad, MetaMixup, mixup_criterion, mixup_criterion_meta, mixup_data
 from ..ops.resnet_fused import STAGES
 from ..optim.flat_optim import MADGRAD, SGD, Adam, DeviceGradScaler, GradClipper, MirrorMADGRAD
 from ..optim.ngd import NGD
@@ -292,7 +292,10 @@ class ResNetTrainer:
             else:
                 loss = mixup_criterion(None, out, ya, yb, lam, meter=self.meter)
         prof.mark("backward")
-        self.scaler.scale_loss(loss).backward()
+        if self.scaler.enabled or loss.dtype != torch.float32 or loss.dim() != 0:
+            self.scaler.scale_loss(loss).backward()
+        else:
+            loss.backward(unit_grad(loss.device))
         prof.mark("grad_sync")
         if self.reducer is not None:
             self.reducer.finish()

@@ -24,7 +24,7 @@ import torch.nn as nn
 
 from ..data.agnews import NUM_CLASSES, TextBatchLoader, download_agnews, get_tokenizer, load_agnews
 from ..models.transformer import Transformer
-from ..ops.mixup import mixup_criterion
+from ..ops.mixup import mixup_criterion, unit_grad
 from ..optim.flat_optim import SGD, Adam, DeviceGradScaler, GradClipper, MirrorMADGRAD, MADGRAD
 from ..optim.ngd import NGD
 from ..parallel import dist as pdist
@@ -313,7 +313,10 @@ class TransformerTrainer:
             prof.mark("loss")
             loss = mixup_criterion(None, logits, labels, labels[perm], lam, meter=self.meter)
         prof.mark("backward")
-        self.scaler.scale_loss(loss).backward()
+        if self.scaler.enabled or loss.dtype != torch.float32 or loss.dim() != 0:
+            self.scaler.scale_loss(loss).backward()
+        else:
+            loss.backward(unit_grad(loss.device))  # (no seed fill, no d(logits) scaling pass)
         return loss, logits, perm, lam
 
     def _graph_fill(self, st, tokens, labels, types, masks):
@@ -354,7 +357,8 @@ class TransformerTrainer:
                 torch.cuda.current_stream().wait_stream(s)
                 return out
             B = tokens.shape[0]
-            prep = (labels.dtype == torch.int64 and 1 <= B <= 1024 and hasattr(_native.native(), "mixup_prep"))
+            prep = (labels.dtype == torch.int64 and 1 <= B <= 1024 and hasattr(_native.native(), "mixup_prep")
+                    and os.environ.get("FDT_TR_MIXUP_PREP", "1") != "0")
             st = dict(tokens=torch.empty_like(tokens), types=torch.empty_like(types), masks=torch.empty_like(masks),
                       labels=torch.empty_like(labels),
                       perm=torch.empty(B, dtype=torch.int32 if prep else torch.long, device=self.device),
@@ -368,7 +372,9 @@ class TransformerTrainer:
                     yb = st["yb"] if prep else st["labels"][perm]
                     # the loss kernel also accumulates the step's loss / accuracy into the meter
                     # (captured: every replay adds; DeviceMeter.reset zeroes in place)
-                    loss = mixup_cross_entropy(logits, st["labels"], yb, st["lam"], meter=self.meter)
+                    loss = mixup_cross_entropy(logits, st["labels"], yb, st["lam"],
+                                               meter=self.meter if os.environ.get("FDT_TR_GRAPH_METER", "1") != "0"
+                                               else None)
                 return loss, logits
 
             torch.cuda.synchronize()
@@ -386,7 +392,7 @@ class TransformerTrainer:
                     g = torch.cuda.CUDAGraph()
                     with torch.cuda.graph(g, pool=self._graph_pool), _graph_guard():
                         loss, logits = fwd()
-                        loss.backward()
+                        loss.backward(unit_grad(loss.device))
                     st.update(replay=g.replay, segments=1)
             finally:
                 AN.DEVICE_SEED = None

@@ -23,6 +23,8 @@ from dataclasses import dataclass
 
 import math
 
+import os
+
 import torch
 import torch.nn as nn
 
@@ -145,7 +147,8 @@ class FlatParams:
             named = [(names[i] if names else f"p{i}", p) for i, p in enumerate(plist)]
         if reverse:
             named = named[::-1]
-        if isinstance(module_or_params, nn.Module) and hasattr(module_or_params, "flat_adjacent"):
+        if (isinstance(module_or_params, nn.Module) and hasattr(module_or_params, "flat_adjacent")
+                and os.environ.get("FDT_FLAT_ADJACENT", "1") != "0"):
             named = _adjacent_groups(named, module_or_params.flat_adjacent())
         self.slots: list[Slot] = []
         self.runs = None

@@ -3,9 +3,12 @@ steps on a learnable synthetic CIFAR task (scripts/convergence.py; VERDICT r3 #7
 
 The error budget is what bf16 arithmetic alone costs: a third run, plain PyTorch under bf16
 autocast (FDT_NATIVE=0) from the same weights on the same batches.  The engine must land at
-most twice as far from the fp32 run as that run does (plus a small epsilon for the step-to-
-step noise of a 60-step loss mean), on the final loss AND the held-out accuracy -- no
-absolute floor.  ResNet-18 (both optimizers) and ResNet-50 at batch 128, i.e. through the
+most twice as far from the fp32 run as that run does (plus a small epsilon), on the HELD-OUT
+loss and accuracy of the final weights -- no absolute floor.  (The per-step training losses
+at the end are heavy-tailed -- 0.005-0.17 step to step in every arm -- so their tail mean or
+median swung by 5-8x between repeats of identical code, profiles/r5/convergence_flaky.txt;
+the held-out loss of the final weights is a smooth function of them.)  Every run must also
+have learned the task (training-loss tail median below half the initial loss).  ResNet-18 (both optimizers) and ResNet-50 at batch 128, i.e. through the
 shipped tile table's batch-128 entries (the 8-GPU per-GPU batch).  Real CIFAR-10 is not
 available offline: parity on it is unpinned (reference README.md:56-73)."""
 import os
@@ -17,8 +20,11 @@ pytestmark = pytest.mark.gpu
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
-EPS_LOSS = 0.02   # absolute, on a mean over the last 60 steps
-EPS_ACC = 0.01    # 10 of 1024 held-out samples
+# the fp32 reference's OWN repeat-to-repeat spread on this task (non-deterministic GPU reductions
+# amplified over 300 steps): held-out loss 0.035-0.114, accuracy 0.966-0.988 across identical runs
+# (profiles/r5/convergence_flaky.txt) -- a smaller epsilon fails the reference against itself
+EPS_LOSS = 0.05   # absolute, on the held-out mean cross entropy
+EPS_ACC = 0.02    # 20 of 1024 held-out samples
 
 
 @pytest.mark.parametrize("opt,arch", [("madgrad", "resnet18"), ("ngd", "resnet18"), ("madgrad", "resnet50")])
@@ -30,8 +36,8 @@ def test_engine_converges_like_fp32_reference(cuda, opt, arch):
     for k in ("reference_final_loss", "engine_final_loss", "bf16_torch_final_loss"):
         assert r[k] < 0.5 * r["initial_loss"], (k, r[k])
     # ... and the engine lands as close to fp32 as bf16 arithmetic allows
-    d_loss = abs(r["engine_final_loss"] - r["reference_final_loss"])
-    b_loss = abs(r["bf16_torch_final_loss"] - r["reference_final_loss"])
+    d_loss = abs(r["engine_test_loss"] - r["reference_test_loss"])
+    b_loss = abs(r["bf16_torch_test_loss"] - r["reference_test_loss"])
     assert d_loss <= 2 * b_loss + EPS_LOSS, (d_loss, b_loss)
     d_acc = abs(r["engine_test_acc"] - r["reference_test_acc"])
     b_acc = abs(r["bf16_torch_test_acc"] - r["reference_test_acc"])
