@@ -64,7 +64,8 @@ def partition_runs(sizes, world):
 # fixed ~25 us of launches and small-matrix math whatever its size (measured: ResNet-50 NGD
 # with an element-balanced 8-way split ran 1.7 ms on the rank holding the stem + stage 1
 # -- dozens of small tensors -- and 0.3-0.5 ms on the others, scripts/bench_ngd.py --world)
-NGD_AXIS_COST = 200_000
+NGD_AXIS_COST = int(os.environ.get("FDT_NGD_AXIS_COST", "200000"))
+NGD_SLACK = float(os.environ.get("FDT_NGD_SLACK", "1.15"))
 
 
 def ngd_cost(shape) -> int:
@@ -74,12 +75,13 @@ def ngd_cost(shape) -> int:
     return n + NGD_AXIS_COST * sum(1 for d in shape if d > 1)
 
 
-def ngd_balanced_order(shapes, world, slack=1.15):
+def ngd_balanced_order(shapes, world, slack=None):
     """Order of parameters (indices into ``shapes``) such that cutting it into ``world``
     contiguous runs balances the NGD cost per rank while every run stays within
     ``slack`` x the even share of elements (the flat chunk, hence the reduce-scatter /
     all-gather size, is the largest run).  Greedy: largest cost first onto the cheapest
     rank with element room.  Returns (order, runs)."""
+    slack = NGD_SLACK if slack is None else slack
     sizes = [_aligned(math.prod(sh)) for sh in shapes]
     cap = max(max(sizes, default=0), int(slack * sum(sizes) / max(world, 1)) + ALIGN)
     cost, elems = [0] * world, [0] * world
