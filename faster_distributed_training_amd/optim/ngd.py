@@ -65,6 +65,9 @@ DEFER = os.environ.get("FDT_NGD_DEFER", "1") != "0"
 # forces it on everywhere; the ResNet trainer turns it on for the sharded path, where a rank
 # preconditions 1/world of the parameters and the step IS launch-bound (train/resnet_trainer.py)
 GRAPHS = os.environ.get("FDT_NGD_GRAPHS", "0") == "1"
+# plain (non-update) steps without weight decay: the clip coefficient applied by the SGD kernel
+# instead of a pass over the flat gradient (NGD._scale_deferrable)
+DEFER_SCALE = os.environ.get("FDT_NGD_DEFER_SCALE", "1") != "0"
 # the R x R products of an update step (K = J J^T, L = J W^T, W <- A (J + wc W)) on the
 # hand-written ngd.hip kernels (ngd_gram / ngd_wupdate) instead of batched library GEMMs
 SMALL_GEMM = os.environ.get("FDT_NGD_GEMM", "1") != "0"
@@ -621,12 +624,26 @@ class NGD(SGD):
             torch.cuda.current_stream().wait_event(done)
             self._pending = None
 
+    def _scale_deferrable(self, grad_scale) -> bool:
+        """On a step where no preconditioner updates (and without weight decay) the whole
+        preconditioning is homogeneous of degree one in the gradient -- fixed projections, then
+        a norm-preserving rescale -- so the clip coefficient can be applied by the final SGD
+        kernel (it reads the coefficient anyway) instead of by a separate pass over the flat
+        gradient before it: NGD(c g) = c NGD(g).  Update steps fold g into the Fisher estimate
+        and keep the reference order."""
+        if grad_scale is None or not DEFER_SCALE or self.group["weight_decay"] != 0 or not self.group["ngd"]:
+            return False
+        sts = [st for sg, _ in (self.groups or []) for _, st in sg.axes]
+        return bool(sts) and not any(st._updating() for st in sts)
+
     def _precondition(self, grad, grad_scale, defer_out=None):
         """grad <- NGD-preconditioned (grad * scale + wd * p), in place.  ``defer_out``: collect
-        the deferred eigensolves instead of running them (graph capture)."""
+        the deferred eigensolves instead of running them (graph capture).  Returns True when
+        the scale was left to the SGD kernel (``_scale_deferrable``)."""
         self.sync_state()
         g = self.group
-        if grad_scale is not None:
+        deferred_scale = self._scale_deferrable(grad_scale)
+        if grad_scale is not None and not deferred_scale:
             grad.mul_(grad_scale)
         if g["weight_decay"] != 0:
             grad.add_(self.flat.data, alpha=g["weight_decay"])
@@ -656,6 +673,7 @@ class NGD(SGD):
                     src.append(out[i])
             if dst:
                 torch._foreach_copy_(dst, src)  # multi-tensor launches, not one copy per parameter
+        return deferred_scale
 
     @torch.no_grad()
     def _step(self, grad_scale, found_inf, d_override=None):
@@ -671,11 +689,11 @@ class NGD(SGD):
         g = self.group
         if self.lr_dev is not None and not torch.cuda.is_current_stream_capturing():
             self._fill_hp()  # (the SGD kernel reads [lr, momentum] from it once graphs exist)
-        self._precondition(self.flat.grad, grad_scale, defer_out)
+        deferred_scale = self._precondition(self.flat.grad, grad_scale, defer_out)
         wd = g["weight_decay"]
         g["weight_decay"] = 0.0
         try:
-            super()._step(None, None)
+            super()._step(grad_scale if deferred_scale else None, None)
         finally:
             g["weight_decay"] = wd
 

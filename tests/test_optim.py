@@ -277,3 +277,27 @@ def test_ngd_shape_groups_as_flat_views_equal_stacked(monkeypatch):
     w = stacked([l.weight for l in heads])
     assert w.data_ptr() == heads[0].weight.data_ptr() and w.shape == (192, 64)
     assert torch.equal(w, torch.cat([l.weight for l in heads]))
+
+
+def test_ngd_plain_steps_defer_clip_scale_to_sgd(monkeypatch):
+    """On a plain (non-update) NGD step the preconditioning is homogeneous of degree one in the
+    gradient, so the clip coefficient applied by the final SGD kernel equals scaling the
+    gradient first (NGD._scale_deferrable): same parameters to fp64 rounding over the 10-step
+    initialisation schedule plus 3 update periods."""
+    import faster_distributed_training_amd.optim.ngd as N
+
+    def run(defer):
+        monkeypatch.setattr(N, "DEFER_SCALE", defer)
+        torch.manual_seed(0)
+        m = nn.Sequential(nn.Linear(40, 24), nn.Linear(24, 10)).double()
+        f = FlatParams(m, dtype=torch.float64)
+        o = NGD(f, lr=0.05, momentum=0.9)
+        g = torch.Generator().manual_seed(1)
+        scale = torch.tensor([0.37], dtype=torch.float64)
+        for _ in range(22):
+            f.grad.copy_(torch.randn(f.numel, generator=g, dtype=torch.float64))
+            o.step(grad_scale=scale)
+        return f.data.clone()
+
+    a, b = run(True), run(False)
+    assert ((a - b).norm() / b.norm()).item() < 1e-10
