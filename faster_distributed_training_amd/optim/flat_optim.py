@@ -35,6 +35,16 @@ def _p(t):
     return 0 if t is None else t.data_ptr()
 
 
+def _layout_key(flat) -> str:
+    """Fingerprint of a flat buffer's slot order (names, offsets, sizes): flat optimizer state
+    is only meaningful for the layout it was saved with."""
+    import hashlib
+    h = hashlib.sha1()
+    for sl in getattr(flat, "slots", []):
+        h.update(f"{sl.name}:{sl.offset}:{sl.numel};".encode())
+    return h.hexdigest()
+
+
 class FlatOptimizer(torch.optim.Optimizer):
     def __init__(self, flat: FlatParams, defaults: dict, zero_grad_in_step: bool = True):
         self.flat = flat
@@ -81,7 +91,7 @@ class FlatOptimizer(torch.optim.Optimizer):
         flat = {k: (v.detach().clone() if torch.is_tensor(v) else v)
                 for k, v in self.state.get("__flat__", {}).items()}
         return {"flat_state": flat, "param_groups": groups, "k": self.k, "kskip": self.kskip.detach().clone().cpu(),
-                "numel": self.flat.numel}
+                "numel": self.flat.numel, "layout": _layout_key(self.flat)}
 
     def load_state_dict(self, sd):
         if "flat_state" not in sd:  # a plain torch.optim state dict: hyper-parameters only
@@ -90,6 +100,10 @@ class FlatOptimizer(torch.optim.Optimizer):
             return
         if sd.get("numel", self.flat.numel) != self.flat.numel:
             raise ValueError("optimizer state was saved for a different parameter layout")
+        if "layout" in sd and sd["layout"] != _layout_key(self.flat):
+            # same element count, other slot order (e.g. a model's flat_adjacent groups): the
+            # flat state vectors would be applied to the wrong parameters
+            raise ValueError("optimizer state was saved for a different parameter order")
         for g, sg in zip(self.param_groups, sd["param_groups"]):
             g.update(sg)
         st = self.state.setdefault("__flat__", {})

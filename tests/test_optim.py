@@ -301,3 +301,20 @@ def test_ngd_plain_steps_defer_clip_scale_to_sgd(monkeypatch):
 
     a, b = run(True), run(False)
     assert ((a - b).norm() / b.norm()).item() < 1e-10
+
+
+def test_flat_optimizer_state_refuses_other_parameter_order():
+    """Flat optimizer state (momentum / second moments as flat vectors) loads only into the
+    slot order it was saved with: the same element count in another order (a model's
+    ``flat_adjacent`` groups, a reversed layout) is refused instead of silently applied to the
+    wrong parameters."""
+    m = nn.Sequential(nn.Linear(8, 8), nn.Linear(8, 8))
+    a = O.MADGRAD(FlatParams(m, reverse=True), lr=1e-3)
+    a.flat.grad.normal_()
+    a.step()
+    sd = a.state_dict()
+    b = O.MADGRAD(FlatParams(nn.Sequential(nn.Linear(8, 8), nn.Linear(8, 8)), reverse=False), lr=1e-3)
+    with pytest.raises(ValueError, match="parameter order"):
+        b.load_state_dict(sd)
+    c = O.MADGRAD(FlatParams(nn.Sequential(nn.Linear(8, 8), nn.Linear(8, 8)), reverse=True), lr=1e-3)
+    c.load_state_dict(sd)  # same layout: accepted
