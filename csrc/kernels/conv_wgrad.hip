@@ -19,6 +19,7 @@
 // Reference semantics: the conv2d(X^T, g^T) weight gradient of resnet.py:21-34 and the
 // autograd of nn.Conv2d for the strided convolutions.
 #include "common.h"
+#include "pack_layout.h"
 #include <vector>
 #include <algorithm>
 
@@ -520,31 +521,25 @@ struct PackTable {
   int n;
 };
 
-// One workgroup packs a 32 (co) x 64 (ci) x ntaps block: coalesced fp32 reads of the
-// OIHW source (ci, tap contiguous per co; 16 B per lane), a bf16 LDS image [co][tap][ci]
-// (row stride 66 elements: the co-strided reads of the dgrad pass hit distinct banks), then
-// 16-B stores of 8 consecutive bf16 per lane into both layouts (wf rows: 64 ci = 128 B; wd
-// rows: 32 co = 64 B) -- 2-byte stores left this kernel at ~1.6 TB/s.
-constexpr int kPackCo = 32;
-constexpr int kPackT = 64;  // ci per block
-constexpr int kPackLd = kPackT + 2;
-constexpr int kPackMaxTaps = 9;
-
-__device__ __forceinline__ uint32_t bf16_bits(bf16 v) { return (uint32_t)(*reinterpret_cast<uint16_t*>(&v)); }
+// One workgroup packs a 32 (co) x 64 (ci) x ntaps block: coalesced fp32 reads of the OIHW
+// source (ci, tap contiguous per co; 16 B per lane) into a bf16 LDS image [co][tap][ci], then
+// both packed layouts from the image (pack_layout.h, shared with the optimizer's fused
+// update-and-pack, optim_pack.hip).
+constexpr int kPackCo = pack::kCo;
+constexpr int kPackT = pack::kT;
+constexpr int kPackLd = pack::kLd;
+constexpr int kPackMaxTaps = pack::kMaxTaps;
 
 // T (taps per kernel: 1, 9, ...) is a compile-time constant in the body, so the per-element
 // index math is multiplies and shifts instead of integer divisions.
 template <int T>
 __device__ __forceinline__ void pack_block(const PackEntry& E, int b, bf16* img) {
-  const int nci = (E.Cxp + kPackT - 1) / kPackT;
-  const int co0 = (b / nci) * kPackCo, ci0 = (b % nci) * kPackT;
+  const pack::Block k = pack::block_of(b, E.Cout, E.Cin, E.Cxp);
   const int tid = threadIdx.x;
-  const int nco = min(kPackCo, E.Cout - co0);
-  const int nci_v = min(kPackT, E.Cxp - ci0);          // columns of the (padded) forward layout
-  const int nci_s = max(0, min(kPackT, E.Cin - ci0));  // columns present in the source
+  const int nco = k.nco, nci_s = k.nci_s;
   // load: for each co row the source run [ci0, ci0 + nci_s) x T is contiguous
   constexpr int run = kPackT * T;
-  const float* rowp = E.src + ((long)co0 * E.Cin + ci0) * T;
+  const float* rowp = E.src + ((long)k.co0 * E.Cin + k.ci0) * T;
   if (nci_s == kPackT && ((E.Cin * T) & 3) == 0) {
     // full block, 16-B aligned rows: float4 loads (4 consecutive (ci, t) elements)
     for (int e = tid; e < nco * (run / 4); e += 256) {
@@ -552,9 +547,9 @@ __device__ __forceinline__ void pack_block(const PackEntry& E, int b, bf16* img)
       const float4 v = *reinterpret_cast<const float4*>(rowp + (long)col * E.Cin * T + q);
       const float vv[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const int cl = (q + k) / T, t = (q + k) - cl * T;
-        img[(col * T + t) * kPackLd + cl] = __float2bfloat16(vv[k]);
+      for (int j = 0; j < 4; ++j) {
+        const int cl = (q + j) / T, t = (q + j) - cl * T;
+        img[(col * T + t) * kPackLd + cl] = __float2bfloat16(vv[j]);
       }
     }
   } else {
@@ -567,34 +562,7 @@ __device__ __forceinline__ void pack_block(const PackEntry& E, int b, bf16* img)
     }
   }
   __syncthreads();
-  // forward layout wf[co][t][ci] (Cxp-padded rows): ci fastest, 8 per lane
-  if (E.wf != nullptr) {
-    for (int e = tid; e < nco * T * (kPackT / 8); e += 256) {
-      const int c8 = (e % (kPackT / 8)) * 8, r = e / (kPackT / 8);  // r = col * T + t
-      if (c8 < nci_v) {
-        const int col = r / T, t = r - col * T;
-        const uint32_t* src = reinterpret_cast<const uint32_t*>(img + r * kPackLd + c8);  // 4-B aligned
-        const uint4 u = make_uint4(src[0], src[1], src[2], src[3]);
-        *reinterpret_cast<uint4*>(E.wf + ((long)(co0 + col) * T + t) * E.Cxp + ci0 + c8) = u;
-      }
-    }
-  }
-  // dgrad layout wd[ci][t][co]: co fastest, 8 per lane
-  if (E.wd != nullptr) {
-    for (int e = tid; e < nci_s * T * (kPackCo / 8); e += 256) {
-      const int c8 = (e % (kPackCo / 8)) * 8, r = e / (kPackCo / 8);  // r = cl * T + t
-      if (c8 < nco) {
-        const int cl = r / T, t = r - cl * T;
-        uint32_t w[4];
-#pragma unroll
-        for (int k = 0; k < 4; ++k)
-          w[k] = bf16_bits(img[((c8 + 2 * k) * T + t) * kPackLd + cl]) |
-                 (bf16_bits(img[((c8 + 2 * k + 1) * T + t) * kPackLd + cl]) << 16);
-        *reinterpret_cast<uint4*>(E.wd + ((long)(ci0 + cl) * T + t) * E.Cout + co0 + c8) =
-            make_uint4(w[0], w[1], w[2], w[3]);
-      }
-    }
-  }
+  pack::store_layouts<T>(img, k, E.wf, E.wd, E.Cout, E.Cxp);
 }
 
 __global__ __launch_bounds__(256) void pack_weights_kernel(const PackTable tab) {

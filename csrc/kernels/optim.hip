@@ -11,6 +11,7 @@
 // MirrorMADGRAD from the external madgrad package used at resnet50_test.py:493 and
 // transformer_test.py:220 (package not vendored; rules re-derived, see optim/madgrad.py).
 #include "common.h"
+#include "optim_ops.h"
 
 namespace fdt {
 
@@ -22,25 +23,11 @@ inline int opt_grid(long n4) {
   return g < 1 ? 1 : (int)g;
 }
 
-__device__ __forceinline__ bool skip_step(const int* found_inf) { return found_inf && *found_inf != 0; }
-
-// A skipped (non-finite / fp16-overflow) step still clears the gradient when the optimizer
-// owns zero_grad: otherwise the bad values would accumulate into every following step.
-__device__ __forceinline__ void skip_zero(float* __restrict__ g, long n, int zero_grad) {
-  if (!zero_grad) return;
-  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) g[i] = 0.f;
-}
-__device__ __forceinline__ float gscale(const float* p) { return p ? *p : 1.f; }
-
-// Step counters of MADGRAD / MirrorMADGRAD / Adam count APPLIED steps only (torch's
-// GradScaler skips optimizer.step() on an overflow, so the reference never advances them on
-// a skipped step).  The host passes the number of step() calls k; the device counter
-// kskip holds the number of skipped ones: a skipped step bumps it (one thread; no other
-// block reads it in a skipped step), an applied step uses k - kskip.
-__device__ __forceinline__ void count_skip(int* kskip) {
-  if (kskip && blockIdx.x == 0 && threadIdx.x == 0) *kskip += 1;
-}
-__device__ __forceinline__ long applied_k(long k, const int* kskip) { return kskip ? k - (long)*kskip : k; }
+using opt::applied_k;
+using opt::count_skip;
+using opt::gscale;
+using opt::skip_step;
+using opt::skip_zero;
 
 __device__ __forceinline__ void store_shadow(bf16* sh, long i, float4 v) {
   uint2 u;
@@ -147,39 +134,11 @@ __global__ __launch_bounds__(kOB) void sgd_kernel(float* __restrict__ p, float* 
   }
 }
 
-// --------------------------------------------------------------- MADGRAD (dual averaging)
-// k = step index (0-based).  lamb = (lr+eps)*sqrt(k+1).  momentum==0 -> x0 recomputed
-// from (p, s, old rms) like the reference package; else x0 is a stored state buffer.
-__global__ __launch_bounds__(kOB) void madgrad_kernel(float* __restrict__ p, float* __restrict__ g, float* __restrict__ gss,
-                                                      float* __restrict__ s, float* __restrict__ x0,
-                                                      bf16* __restrict__ shadow, long n4, float lr, float momentum,
-                                                      float wd, float eps, int decouple, long k, int* __restrict__ kskip,
-                                                      const float* __restrict__ gsc, const int* __restrict__ found_inf,
-                                                      int zero_grad) {
-  if (skip_step(found_inf)) { count_skip(kskip); skip_zero(g, n4 * 4, zero_grad); return; }
-  const float c = gscale(gsc);
-  const float lr_e = lr + eps;
-  const float lamb = lr_e * sqrtf((float)(applied_k(k, kskip) + 1));
-  const float ck = 1.f - momentum;
-  for (long i = (long)blockIdx.x * kOB + threadIdx.x; i < n4 * 4; i += (long)gridDim.x * kOB) {
-    float pv = p[i], gv = g[i] * c;
-    if (wd != 0.f && !decouple) gv += wd * pv;
-    float q = gss[i], sv = s[i];
-    float x0v;
-    if (momentum == 0.f) x0v = pv + sv / (cbrtf(q) + eps);
-    else x0v = x0[i];
-    q = fmaf(lamb * gv, gv, q);
-    float rms = cbrtf(q) + eps;
-    if (wd != 0.f && decouple) pv -= lr_e * wd * pv;
-    sv = fmaf(lamb, gv, sv);
-    float z = x0v - sv / rms;
-    pv = momentum == 0.f ? z : (1.f - ck) * pv + ck * z;
-    p[i] = pv;
-    gss[i] = q;
-    s[i] = sv;
-    if (shadow) shadow[i] = __float2bfloat16(pv);
-    if (zero_grad) g[i] = 0.f;
-  }
+// --------------------------------------------------------------- MADGRAD (optim_ops.h MadOp)
+__global__ __launch_bounds__(kOB) void madgrad_kernel(const opt::MadArgs args, long n) {
+  if (opt::MadOp::skipped(args)) { opt::MadOp::on_skip(args, n); return; }
+  const opt::MadOp op(args);
+  for (long i = (long)blockIdx.x * kOB + threadIdx.x; i < n; i += (long)gridDim.x * kOB) op(i);
 }
 
 // --------------------------------------------------------------- MirrorMADGRAD
@@ -279,10 +238,10 @@ void madgrad_step(uint64_t p, uint64_t g, uint64_t gss, uint64_t s, uint64_t x0,
                   uint64_t found_inf, int zero_grad, uint64_t stream) {
   FDT_CHECK(n % 4 == 0, "flat buffer must be padded to a multiple of 4");
   FDT_CHECK(momentum == 0.f || x0 != 0, "x0 buffer required with momentum");
-  madgrad_kernel<<<opt_grid(n / 4), kOB, 0, as_stream(stream)>>>(P<float>(p), P<float>(g), P<float>(gss), P<float>(s),
-                                                                  P<float>(x0), P<bf16>(shadow), n / 4, lr, momentum, wd,
-                                                                  eps, decouple, k, P<int>(kskip), P<const float>(gsc),
-                                                                  P<const int>(found_inf), zero_grad);
+  const opt::MadArgs a{P<float>(p), P<float>(g), P<float>(gss), P<float>(s), P<float>(x0), P<bf16>(shadow),
+                       lr, momentum, wd, eps, decouple, k, P<int>(kskip), P<const float>(gsc),
+                       P<const int>(found_inf), zero_grad};
+  madgrad_kernel<<<opt_grid(n / 4), kOB, 0, as_stream(stream)>>>(a, n);
   FDT_LAUNCH_CHECK();
 }
 

@@ -206,6 +206,11 @@ class Block:
 
 STAGES = ("conv2_x", "conv3_x", "conv4_x", "conv5_x")
 
+# The flat optimizer writes the packed conv weight layouts itself (optim_pack.hip: one fused
+# update-and-pack launch) when the model's weights live in its flat buffer; the forward then
+# skips its repack while nothing else has written the weights since (Plan.pack_fresh)
+PACK_IN_OPT = os.environ.get("FDT_PACK_IN_OPT", "1") != "0"
+
 
 class Plan:
     def __init__(self, model):
@@ -220,11 +225,77 @@ class Plan:
         self.fsdp = None  # parallel/fsdp.py FullyShardedDP driving the stages as wrap units
 
     def pack(self, dev, need_dgrad=True):
+        if self.pack_fresh():
+            return  # the optimizer's fused step already wrote both layouts from these weights
         ents = []
         for u in self.units:
             u.ensure_packed_buffers(dev, need_dgrad and u is not self.stem)
             ents.append((u.w.detach(), u.wf, u.wd, u.shp))
         ci.pack_weights(ents)
+
+    # ---- packed layouts written by the optimizer (optim_pack.hip)
+    def _weights_version(self, flat):
+        # torch in-place writes (load_state_dict, copy_ into the flat buffer or a parameter) bump
+        # these counters; the native optimizer kernels do not
+        return flat.data._version + sum(u.w._version for u in self.units)
+
+    def update_table(self, flat):
+        """Device tables of the fused update-and-pack step over ``flat`` (a FlatParams holding
+        every conv weight as a contiguous fp32 OIHW view): (entries int64 [n, 8], n, conv
+        blocks, rest ranges int64 [m, 3], m, rest elements), or None when the layouts are not
+        allocated yet (before the first training forward) or the weights are not all in
+        ``flat``."""
+        if not PACK_IN_OPT or self.fsdp is not None or not flat.data.is_cuda:
+            return None
+        c = self.__dict__.get("_upd")
+        if c is not None and c[0] is flat:
+            return c[1]
+        if any(u.wf is None or (u.wd is None and u.shp.cin >= 8) for u in self.units):
+            return None
+        base, n = flat.data.data_ptr(), flat.numel
+        rows, spans, blk = [], [], 0
+        for u in self.units:
+            w = u.w
+            off, rem = divmod(w.data_ptr() - base, 4)
+            if (w.dtype != torch.float32 or not w.is_contiguous() or rem or off < 0 or off + w.numel() > n
+                    or w.device != flat.data.device or w.dim() != 4):
+                return None
+            co, cin, kh, kw = w.shape
+            if kh * kw not in (1, 4, 9) or co % 8 or u.shp.cxp % 8 or u.wf.device != w.device:
+                return None
+            rows.append([off, u.wf.data_ptr(), 0 if u.wd is None else u.wd.data_ptr(), co, cin, u.shp.cxp, kh * kw, blk])
+            blk += -(-co // 32) * -(-u.shp.cxp // 64)
+            spans.append((off, off + w.numel()))
+        spans.sort()
+        rr, cur, cum = [], 0, 0
+        for a, b in spans:
+            if a < cur:
+                return None  # overlapping weights
+            if a > cur:
+                rr.append([cur, a - cur, cum])
+                cum += a - cur
+            cur = b
+        if cur < n:
+            rr.append([cur, n - cur, cum])
+            cum += n - cur
+        dev = flat.data.device
+        tab = torch.tensor(rows, dtype=torch.int64, device=dev)
+        rrt = torch.tensor(rr or [[0, 0, 0]], dtype=torch.int64, device=dev)
+        ent = (tab, len(rows), blk, rrt, len(rr), cum)
+        self._upd = (flat, ent)
+        return ent
+
+    def mark_opt_packed(self, flat):
+        """The optimizer step just written (or, when skipped on the device, left unchanged) the
+        weights together with both packed layouts."""
+        self._pk = (flat, self._weights_version(flat))
+
+    def invalidate_pack(self):
+        self.__dict__.pop("_pk", None)
+
+    def pack_fresh(self) -> bool:
+        pk = self.__dict__.get("_pk")
+        return pk is not None and pk[1] == self._weights_version(pk[0])
 
     # ---- FSDP: units are gathered stage by stage, so weights are packed per stage (the
     # forward layout before the stage's forward, the dgrad layout before its backward) and
@@ -999,6 +1070,7 @@ class _GraphState:
         self.inner = None
         self.fwd = None
         self.segments = None
+        self.repacks = True
 
 
 def graphs_enabled(plan) -> bool:
@@ -1031,6 +1103,7 @@ class _BodyWithDummy(torch.autograd.Function):
                 side.wait_stream(cur)
                 torch.cuda.synchronize()
                 rec = _graphs.Recorder(st.pool)
+                st.repacks = not plan.pack_fresh()  # does the captured forward repack the weights?
                 with torch.cuda.stream(side), _graphs.recording(rec), _graphs.capture_guard():
                     rec.begin()
                     try:
@@ -1042,6 +1115,10 @@ class _BodyWithDummy(torch.autograd.Function):
                 st.fwd.replay()
                 st.stage = "fwd"
             else:
+                if not st.repacks and not plan.pack_fresh():
+                    # captured without the repack (the optimizer packs): weights written since by
+                    # something else -- repack before the replay
+                    plan.pack(xin.device, need_dgrad=True)
                 st.x.copy_(xin)
                 st.fwd.replay()
         ctx.gstate = st if (st is not None and st.stage in ("fwd", "ready")) else None

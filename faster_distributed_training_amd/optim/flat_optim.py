@@ -78,9 +78,34 @@ class FlatOptimizer(torch.optim.Optimizer):
 
     def step(self, closure=None, grad_scale: torch.Tensor | None = None, found_inf: torch.Tensor | None = None):
         loss = closure() if closure is not None else None
+        self._packed = False
         self._step(grad_scale, found_inf)
+        plan = self._pack_plan()
+        if plan is not None:  # the packed conv layouts follow the weights only after a fused step
+            if self._packed:
+                plan.mark_opt_packed(self.flat)
+            else:
+                plan.invalidate_pack()
         self.k += 1
         return loss
+
+    # ------------------------------------------------------------ fused conv weight repack
+    # When the flat buffer holds the weights of a native-engine ResNet (``flat.pack_owner``, set
+    # by the trainer), SGD / MADGRAD steps also write the convolutions' packed bf16 layouts
+    # (csrc/kernels/optim_pack.hip) and the next forward skips its repack pass.
+    def _pack_plan(self):
+        return getattr(getattr(self.flat, "pack_owner", None), "_plan", None)
+
+    def _pack_args(self):
+        """Trailing table arguments of the fused update-and-pack launch, or None."""
+        plan = self._pack_plan()
+        if plan is None or not self._native:
+            return None
+        ent = plan.update_table(self.flat)
+        if ent is None:
+            return None
+        tab, ntab, nblk, rr, nrr, rest = ent
+        return [tab.data_ptr(), ntab, nblk, rr.data_ptr(), nrr, rest]
 
     # ------------------------------------------------------------ state dict
     # The optimizer state lives in whole-model flat buffers (self.state["__flat__"]), which
@@ -147,11 +172,16 @@ class SGD(FlatOptimizer):
         buf = self._state_buf("momentum_buffer") if g["momentum"] != 0 else None
         first = int(self.state["__flat__"].get("initialized", 0) == 0) if buf is not None else 0
         if self._native and d_override is None:
-            _native.native().sgd_step(
-                self.flat.data.data_ptr(), self.flat.grad.data_ptr(), _p(buf), _p(self.flat.shadow), self.flat.numel,
-                float(g["lr"]), float(g["momentum"]), float(g["dampening"]), float(g["weight_decay"]),
-                int(g["nesterov"]), first, _p(grad_scale), _p(found_inf), int(self.zero_grad_in_step),
-                _p(getattr(self, "lr_dev", None)), _sp())
+            args = [self.flat.data.data_ptr(), self.flat.grad.data_ptr(), _p(buf), _p(self.flat.shadow),
+                    self.flat.numel, float(g["lr"]), float(g["momentum"]), float(g["dampening"]),
+                    float(g["weight_decay"]), int(g["nesterov"]), first, _p(grad_scale), _p(found_inf),
+                    int(self.zero_grad_in_step), _p(getattr(self, "lr_dev", None))]
+            pk = self._pack_args()
+            if pk is not None:
+                _native.native().sgd_pack_step(*args, *pk, _sp())
+                self._packed = True
+            else:
+                _native.native().sgd_step(*args, _sp())
         else:
             gr = self._cpu_common(grad_scale, found_inf) if d_override is None else d_override
             if gr is None:
@@ -183,11 +213,16 @@ class MADGRAD(FlatOptimizer):
         s = self._state_buf("s")
         x0 = self._state_buf("x0", init="copy") if g["momentum"] != 0 else None
         if self._native:
-            _native.native().madgrad_step(
-                self.flat.data.data_ptr(), self.flat.grad.data_ptr(), gss.data_ptr(), s.data_ptr(), _p(x0),
-                _p(self.flat.shadow), self.flat.numel, float(g["lr"]), float(g["momentum"]), float(g["weight_decay"]),
-                float(g["eps"]), int(g["decouple_decay"]), self.k, self.kskip.data_ptr(), _p(grad_scale),
-                _p(found_inf), int(self.zero_grad_in_step), _sp())
+            args = [self.flat.data.data_ptr(), self.flat.grad.data_ptr(), gss.data_ptr(), s.data_ptr(), _p(x0),
+                    _p(self.flat.shadow), self.flat.numel, float(g["lr"]), float(g["momentum"]),
+                    float(g["weight_decay"]), float(g["eps"]), int(g["decouple_decay"]), self.k,
+                    self.kskip.data_ptr(), _p(grad_scale), _p(found_inf), int(self.zero_grad_in_step)]
+            pk = self._pack_args()
+            if pk is not None:
+                _native.native().madgrad_pack_step(*args, *pk, _sp())
+                self._packed = True
+            else:
+                _native.native().madgrad_step(*args, _sp())
             return
         gr = self._cpu_common(grad_scale, found_inf)
         if gr is None:

@@ -755,6 +755,7 @@ class NGD(SGD):
             ent = self._gcache[key] = self._capture(grad_scale)
         self.sync_state()  # the previous update's side-stream graph -> before this replay
         ent["main"].replay()
+        self._packed = ent.get("packed", False)  # (the captured SGD tail's fused conv repack)
         if ent["side"] is not None:
             cur = torch.cuda.current_stream()
             side = self._side_stream(self.flat.grad) or cur
@@ -801,7 +802,7 @@ class NGD(SGD):
             for st, t in zip(sts, t0):  # the captures ran the host schedule once: undo it
                 st.t = t
         cur.wait_stream(cs)
-        return {"main": main, "side": side_g, "keep": deferred}
+        return {"main": main, "side": side_g, "keep": deferred, "packed": getattr(self, "_packed", False)}
 
     def _states(self):
         """Every batched per-axis preconditioner state (empty before the first step)."""

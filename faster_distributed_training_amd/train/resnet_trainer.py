@@ -151,6 +151,8 @@ class ResNetTrainer:
                                            first_bucket_mb=cfg.first_bucket_mb, comm_dtype=cdt)
         else:
             self.flat = FlatParams(params_owner, device=self.device)
+            # SGD / MADGRAD steps write the engine's packed conv weights (ops/resnet_fused.py)
+            self.flat.pack_owner = self.model
             if cfg.distributed or cfg.force_ddp:
                 from ..parallel.ddp import BucketReducer
                 cdt = {"fp32": None, "bf16": torch.bfloat16}[cfg.comm_dtype]

@@ -224,7 +224,17 @@ class FlatParams:
                     want.view(s.shape).copy_(g)
                 s.param.grad = want.view(s.shape)
 
+    # a module whose native engine keeps packed copies of the weights (ops/resnet_fused.py Plan):
+    # the optimizer writes them in its fused step; out-of-band weight writes must drop that claim
+    pack_owner = None
+
+    def invalidate_packed(self):
+        plan = getattr(self.pack_owner, "_plan", None)
+        if plan is not None:
+            plan.invalidate_pack()
+
     def refresh_shadow(self):
+        self.invalidate_packed()
         if self.shadow is not None:
             with torch.no_grad():
                 self.shadow.copy_(self.data)
