@@ -209,7 +209,7 @@ STAGES = ("conv2_x", "conv3_x", "conv4_x", "conv5_x")
 # The flat optimizer writes the packed conv weight layouts itself (optim_pack.hip: one fused
 # update-and-pack launch) when the model's weights live in its flat buffer; the forward then
 # skips its repack while nothing else has written the weights since (Plan.pack_fresh)
-PACK_IN_OPT = os.environ.get("FDT_PACK_IN_OPT", "1") != "0"
+PACK_IN_OPT = os.environ.get("FDT_PACK_IN_OPT", "0") == "1"
 
 
 class Plan:
@@ -229,7 +229,10 @@ class Plan:
             return  # the optimizer's fused step already wrote both layouts from these weights
         ents = []
         for u in self.units:
+            had = (u.wf, u.wd)
             u.ensure_packed_buffers(dev, need_dgrad and u is not self.stem)
+            if u.wf is not had[0] or u.wd is not had[1]:
+                self.__dict__.pop("_upd", None)  # the optimizer's table points at the old buffers
             ents.append((u.w.detach(), u.wf, u.wd, u.shp))
         ci.pack_weights(ents)
 

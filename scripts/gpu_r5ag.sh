@@ -16,14 +16,14 @@ run() {
   echo "$name $(grep -o '"ms_per_step": [0-9.]*' "$OUT/$name.json")"
 }
 FDT_PACK_IN_OPT=0 run bs128_off_a --steps 40 --warmup 5 --global-batch 128
-run bs128_on_a --steps 40 --warmup 5 --global-batch 128
+FDT_PACK_IN_OPT=1 run bs128_on_a --steps 40 --warmup 5 --global-batch 128
 FDT_PACK_IN_OPT=0 run bs128_off_b --steps 40 --warmup 5 --global-batch 128
-run bs128_on_b --steps 40 --warmup 5 --global-batch 128
-run bs128_ddp_on --steps 40 --warmup 5 --global-batch 128 --ddp
+FDT_PACK_IN_OPT=1 run bs128_on_b --steps 40 --warmup 5 --global-batch 128
+FDT_PACK_IN_OPT=1 run bs128_ddp_on --steps 40 --warmup 5 --global-batch 128 --ddp
 FDT_PACK_IN_OPT=0 run bs1024_off --steps 30 --warmup 8
-run bs1024_on --steps 30 --warmup 8
-run ngd_on --steps 20 --warmup 12 --ngd --meta_learning
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_bs128" -o run -- python3 bench.py --steps 10 --warmup 5 --global-batch 128 > "$OUT/prof_bs128.log" 2>&1 || { echo "prof failed"; tail -5 "$OUT/prof_bs128.log"; exit 1; }
+FDT_PACK_IN_OPT=1 run bs1024_on --steps 30 --warmup 8
+FDT_PACK_IN_OPT=1 run ngd_on --steps 20 --warmup 12 --ngd --meta_learning
+FDT_PACK_IN_OPT=1 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_bs128" -o run -- python3 bench.py --steps 10 --warmup 5 --global-batch 128 > "$OUT/prof_bs128.log" 2>&1 || { echo "prof failed"; tail -5 "$OUT/prof_bs128.log"; exit 1; }
 f=$(find "$OUT/prof_bs128" -name '*kernel_stats.csv' | head -n 1)
 python scripts/kstats.py "$f" --steps 15 --top 70 > "$OUT/kstats_bs128.txt"
 head -16 "$OUT/kstats_bs128.txt" | cut -c1-150

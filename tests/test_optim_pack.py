@@ -46,6 +46,12 @@ class _FakePlan:
         ci.pack_weights([(u.w.detach(), u.wf, u.wd, u.shp) for u in self.units])
 
 
+@pytest.fixture(autouse=True)
+def _pack_in_opt(monkeypatch):
+    from faster_distributed_training_amd.ops import resnet_fused
+    monkeypatch.setattr(resnet_fused, "PACK_IN_OPT", True)
+
+
 def _setup(cuda, opt_name, seed=0):
     from faster_distributed_training_amd.optim.flat_optim import MADGRAD, SGD
     from faster_distributed_training_amd.utils.flat import FlatParams
