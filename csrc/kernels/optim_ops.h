@@ -58,29 +58,54 @@ struct MadOp {
     count_skip(a.kskip);
     skip_zero(a.g, n, a.zero_grad);
   }
-  __device__ __forceinline__ float operator()(long i) const {
-    float* __restrict__ p = a.p;
-    float* __restrict__ g = a.g;
-    float* __restrict__ gss = a.gss;
-    float* __restrict__ s = a.s;
-    float pv = p[i], gv = g[i] * c;
+  // the rule on loaded values: q = grad_sum_sq, sv = s (updated in place); returns the new p
+  __device__ __forceinline__ float rule(float pv, float gv, float& q, float& sv, float x0v) const {
+    gv *= c;
     if (a.wd != 0.f && !a.decouple) gv += a.wd * pv;
-    float q = gss[i], sv = s[i];
-    float x0v;
     if (a.momentum == 0.f) x0v = pv + sv / (cbrtf(q) + a.eps);
-    else x0v = a.x0[i];
     q = fmaf(lamb * gv, gv, q);
     float rms = cbrtf(q) + a.eps;
     if (a.wd != 0.f && a.decouple) pv -= lr_e * a.wd * pv;
     sv = fmaf(lamb, gv, sv);
     float z = x0v - sv / rms;
-    pv = a.momentum == 0.f ? z : (1.f - ck) * pv + ck * z;
-    p[i] = pv;
-    gss[i] = q;
-    s[i] = sv;
+    return a.momentum == 0.f ? z : (1.f - ck) * pv + ck * z;
+  }
+  __device__ __forceinline__ void store(long i, float pv, float q, float sv) const {
+    a.p[i] = pv;
+    a.gss[i] = q;
+    a.s[i] = sv;
     if (a.shadow) a.shadow[i] = __float2bfloat16(pv);
-    if (a.zero_grad) g[i] = 0.f;
+    if (a.zero_grad) a.g[i] = 0.f;
+  }
+  __device__ __forceinline__ float operator()(long i) const {
+    float q = a.gss[i], sv = a.s[i];
+    const float pv = rule(a.p[i], a.g[i], q, sv, a.momentum == 0.f ? 0.f : a.x0[i]);
+    store(i, pv, q, sv);
     return pv;
+  }
+  // U elements at once: every load issued before any math / store (latency-bound callers)
+  template <int U>
+  __device__ __forceinline__ void apply(const long (&i)[U], const bool (&ok)[U], float (&out)[U]) const {
+    float pv[U], gv[U], q[U], sv[U], x0v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (ok[u]) {
+        pv[u] = a.p[i[u]];
+        gv[u] = a.g[i[u]];
+        q[u] = a.gss[i[u]];
+        sv[u] = a.s[i[u]];
+        x0v[u] = a.momentum == 0.f ? 0.f : a.x0[i[u]];
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (ok[u]) {
+        out[u] = rule(pv[u], gv[u], q[u], sv[u], x0v[u]);
+        store(i[u], out[u], q[u], sv[u]);
+      } else {
+        out[u] = 0.f;
+      }
+    }
   }
 };
 
@@ -107,23 +132,49 @@ struct SgdOp {
   }
   __device__ __forceinline__ static bool skipped(const SgdArgs& a) { return skip_step(a.found_inf); }
   __device__ __forceinline__ static void on_skip(const SgdArgs& a, long n) { skip_zero(a.g, n, a.zero_grad); }
-  __device__ __forceinline__ float operator()(long i) const {
-    float* __restrict__ p = a.p;
-    float* __restrict__ g = a.g;
-    float pv = p[i], gv = g[i];
+  // the rule on loaded values: bv = momentum buffer (updated in place); returns the new p
+  __device__ __forceinline__ float rule(float pv, float gv, float& bv) const {
     float d = gv * c + a.wd * pv;
     if (momentum != 0.f) {
-      float bv = a.first ? d : a.buf[i];
-      if (!a.first) bv = momentum * bv + (1.f - a.dampening) * d;
-      a.buf[i] = bv;
+      if (a.first) bv = d;
+      else bv = momentum * bv + (1.f - a.dampening) * d;
       if (a.nesterov) d += momentum * bv;
       else d = bv;
     }
-    pv -= lr * d;
-    p[i] = pv;
+    return pv - lr * d;
+  }
+  __device__ __forceinline__ void store(long i, float pv, float bv) const {
+    if (momentum != 0.f) a.buf[i] = bv;
+    a.p[i] = pv;
     if (a.shadow) a.shadow[i] = __float2bfloat16(pv);
-    if (a.zero_grad) g[i] = 0.f;
+    if (a.zero_grad) a.g[i] = 0.f;
+  }
+  __device__ __forceinline__ float operator()(long i) const {
+    float bv = (momentum != 0.f && !a.first) ? a.buf[i] : 0.f;
+    const float pv = rule(a.p[i], a.g[i], bv);
+    store(i, pv, bv);
     return pv;
+  }
+  template <int U>
+  __device__ __forceinline__ void apply(const long (&i)[U], const bool (&ok)[U], float (&out)[U]) const {
+    float pv[U], gv[U], bv[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (ok[u]) {
+        pv[u] = a.p[i[u]];
+        gv[u] = a.g[i[u]];
+        bv[u] = (momentum != 0.f && !a.first) ? a.buf[i[u]] : 0.f;
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (ok[u]) {
+        out[u] = rule(pv[u], gv[u], bv[u]);
+        store(i[u], out[u], bv[u]);
+      } else {
+        out[u] = 0.f;
+      }
+    }
   }
 };
 

@@ -36,12 +36,28 @@ __device__ __forceinline__ void update_block(const Op& op, const PackUpdEntry& E
   const pack::Block k = pack::block_of(b, Cout, Cin, Cxp);
   constexpr int run = pack::kT * T;
   const long base = E.off + ((long)k.co0 * Cin + k.ci0) * T;
-  for (int e = threadIdx.x; e < k.nco * run; e += blockDim.x) {
-    const int col = e / run, rem = e - col * run;
-    const int cl = rem / T, t = rem - cl * T;
-    float v = 0.f;
-    if (cl < k.nci_s) v = op(base + (long)col * Cin * T + rem);
-    img[(col * T + t) * pack::kLd + cl] = __float2bfloat16(v);
+  // U elements per thread per trip, all their loads issued first: a block owns up to 18432
+  // elements (3x3) and the LDS image limits residency to 4 blocks per CU
+  constexpr int U = 4;
+  const int total = k.nco * run;
+  for (int e0 = threadIdx.x; e0 < total; e0 += blockDim.x * U) {
+    long idx[U];
+    bool ok[U];
+    int slot[U];
+    float v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int e = e0 + u * (int)blockDim.x;
+      const int col = e / run, rem = e - col * run;
+      const int cl = rem / T, t = rem - cl * T;
+      ok[u] = e < total && cl < k.nci_s;
+      idx[u] = base + (long)col * Cin * T + rem;
+      slot[u] = e < total ? (col * T + t) * pack::kLd + cl : -1;
+    }
+    op.template apply<U>(idx, ok, v);
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      if (slot[u] >= 0) img[slot[u]] = __float2bfloat16(v[u]);
   }
   __syncthreads();
   pack::store_layouts<T>(img, k, reinterpret_cast<bf16*>(E.wf), reinterpret_cast<bf16*>(E.wd), Cout, Cxp);
