@@ -95,42 +95,26 @@ __global__ void grad_norm_finalize_kernel(const float* __restrict__ part, int nb
 }
 
 // --------------------------------------------------------------- SGD (+momentum, NGD tail)
-__global__ __launch_bounds__(kOB) void sgd_kernel(float* __restrict__ p, float* __restrict__ g, float* __restrict__ buf,
-                                                  bf16* __restrict__ shadow, long n4, float lr, float momentum,
-                                                  float dampening, float wd, int nesterov, int first,
-                                                  const float* __restrict__ gsc, const int* __restrict__ found_inf,
-                                                  int zero_grad, const float* __restrict__ lr_dev) {
-  if (skip_step(found_inf)) { skip_zero(g, n4 * 4, zero_grad); return; }
-  const float c = gscale(gsc);
-  if (lr_dev) {  // device [lr, momentum]: a captured HIP graph follows the schedules (OneCycle cycles both)
-    lr = lr_dev[0];
-    momentum = lr_dev[1];
-  }
-  float4* p4 = reinterpret_cast<float4*>(p);
-  float4* g4 = reinterpret_cast<float4*>(g);
-  float4* b4 = reinterpret_cast<float4*>(buf);
+__global__ __launch_bounds__(kOB) void sgd_kernel(const opt::SgdArgs args, long n4) {
+  if (opt::SgdOp::skipped(args)) { opt::SgdOp::on_skip(args, n4 * 4); return; }
+  // (device [lr, momentum] in args.lr_dev: a captured HIP graph follows the schedules)
+  const opt::SgdOp op(args);
+  const bool mom = op.momentum != 0.f;
+  float4* p4 = reinterpret_cast<float4*>(args.p);
+  float4* g4 = reinterpret_cast<float4*>(args.g);
+  float4* b4 = reinterpret_cast<float4*>(args.buf);
   for (long i = (long)blockIdx.x * kOB + threadIdx.x; i < n4; i += (long)gridDim.x * kOB) {
-    float4 pv = p4[i], gv = g4[i];
-    float d[4] = {gv.x * c + wd * pv.x, gv.y * c + wd * pv.y, gv.z * c + wd * pv.z, gv.w * c + wd * pv.w};
-    if (momentum != 0.f) {
-      float4 bv = first ? make_float4(d[0], d[1], d[2], d[3]) : b4[i];
-      if (!first) {
-        bv.x = momentum * bv.x + (1.f - dampening) * d[0];
-        bv.y = momentum * bv.y + (1.f - dampening) * d[1];
-        bv.z = momentum * bv.z + (1.f - dampening) * d[2];
-        bv.w = momentum * bv.w + (1.f - dampening) * d[3];
-      }
-      b4[i] = bv;
-      if (nesterov) {
-        d[0] += momentum * bv.x; d[1] += momentum * bv.y; d[2] += momentum * bv.z; d[3] += momentum * bv.w;
-      } else {
-        d[0] = bv.x; d[1] = bv.y; d[2] = bv.z; d[3] = bv.w;
-      }
-    }
-    pv.x -= lr * d[0]; pv.y -= lr * d[1]; pv.z -= lr * d[2]; pv.w -= lr * d[3];
+    float4 pv = p4[i];
+    const float4 gv = g4[i];
+    float4 bv = (mom && !args.first) ? b4[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+    pv.x = op.rule(pv.x, gv.x, bv.x);
+    pv.y = op.rule(pv.y, gv.y, bv.y);
+    pv.z = op.rule(pv.z, gv.z, bv.z);
+    pv.w = op.rule(pv.w, gv.w, bv.w);
+    if (mom) b4[i] = bv;
     p4[i] = pv;
-    if (shadow) store_shadow(shadow, i * 4, pv);
-    if (zero_grad) g4[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (args.shadow) store_shadow(args.shadow, i * 4, pv);
+    if (args.zero_grad) g4[i] = make_float4(0.f, 0.f, 0.f, 0.f);
   }
 }
 
@@ -226,10 +210,10 @@ void sgd_step(uint64_t p, uint64_t g, uint64_t buf, uint64_t shadow, long n, flo
               uint64_t stream) {
   FDT_CHECK(n % 4 == 0, "flat buffer must be padded to a multiple of 4");
   FDT_CHECK(momentum == 0.f || buf != 0, "momentum buffer required");
-  sgd_kernel<<<opt_grid(n / 4), kOB, 0, as_stream(stream)>>>(P<float>(p), P<float>(g), P<float>(buf), P<bf16>(shadow),
-                                                              n / 4, lr, momentum, dampening, wd, nesterov, first,
-                                                              P<const float>(gsc), P<const int>(found_inf), zero_grad,
-                                                              P<const float>(lr_dev));
+  const opt::SgdArgs a{P<float>(p), P<float>(g), P<float>(buf), P<bf16>(shadow), lr, momentum, dampening, wd,
+                       nesterov, first, P<const float>(gsc), P<const int>(found_inf), zero_grad,
+                       P<const float>(lr_dev)};
+  sgd_kernel<<<opt_grid(n / 4), kOB, 0, as_stream(stream)>>>(a, n / 4);
   FDT_LAUNCH_CHECK();
 }
 

@@ -59,7 +59,9 @@ struct MadOp {
     skip_zero(a.g, n, a.zero_grad);
   }
   // the rule on loaded values: q = grad_sum_sq, sv = s (updated in place); returns the new p
+  // (no FMA contraction here: every caller -- wherever it inlines this -- rounds identically)
   __device__ __forceinline__ float rule(float pv, float gv, float& q, float& sv, float x0v) const {
+#pragma clang fp contract(off)
     gv *= c;
     if (a.wd != 0.f && !a.decouple) gv += a.wd * pv;
     if (a.momentum == 0.f) x0v = pv + sv / (cbrtf(q) + a.eps);
@@ -110,7 +112,7 @@ struct MadOp {
 };
 
 // ---------------------------------------------------------------- SGD (+momentum, NGD tail)
-// Scalar form of optim.hip sgd_kernel's per-lane math (same expressions, same rounding).
+// One rule for optim.hip sgd_kernel (float4 lanes) and the fused update-and-pack kernel.
 struct SgdArgs {
   float *p, *g, *buf;
   bf16* shadow;
@@ -134,6 +136,7 @@ struct SgdOp {
   __device__ __forceinline__ static void on_skip(const SgdArgs& a, long n) { skip_zero(a.g, n, a.zero_grad); }
   // the rule on loaded values: bv = momentum buffer (updated in place); returns the new p
   __device__ __forceinline__ float rule(float pv, float gv, float& bv) const {
+#pragma clang fp contract(off)
     float d = gv * c + a.wd * pv;
     if (momentum != 0.f) {
       if (a.first) bv = d;
