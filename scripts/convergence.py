@@ -119,31 +119,40 @@ def train_curve(native: bool, opt: str, steps: int, bs: int = 128, lr=None, devi
             os.environ["FDT_NATIVE"] = prev
 
 
-def compare(opt: str, steps: int, device="cuda", arch="resnet18", bs=128, tail_frac=0.2):
-    """Three runs from the same weights on the same batches: the HIP engine, fp32 PyTorch (the
+def compare(opt: str, steps: int, device="cuda", arch="resnet18", bs=128, tail_frac=0.2, repeats=1):
+    """Three arms from the same weights on the same batches: the HIP engine, fp32 PyTorch (the
     reference numerics) and PyTorch under bf16 autocast (FDT_NATIVE=0: how far bf16 arithmetic
     alone moves the result -- the engine's error budget).  Final loss = MEDIAN of the last
     ``tail_frac`` of the steps' (mixup, minibatch) losses: the per-step losses of every arm swing
     0.01-0.17 at the end and a late spike phase of one run would otherwise decide the mean (a
     ResNet-50 engine run measured a tail mean of 0.28 against 0.07 in a repeat of the same
-    code, with a 0.95 test accuracy)."""
+    code, with a 0.95 test accuracy).  ``repeats`` > 1: every arm runs that many times (GPU
+    reductions make repeats differ) and its held-out loss / accuracy are the means over them;
+    ``reference_spread_*`` is then the fp32 arm's own max - min across its repeats."""
     task = make_task(device=device)
     kw = dict(device=device, task=task, arch=arch, bs=bs)
-    eng = train_curve(True, opt, steps, **kw)
-    ref = train_curve(False, opt, steps, bf16=False, **kw)
-    b16 = train_curve(False, opt, steps, bf16=True, **kw)
+    arms = {"engine": [], "reference": [], "bf16_torch": []}
+    for _ in range(max(1, repeats)):
+        arms["engine"].append(train_curve(True, opt, steps, **kw))
+        arms["reference"].append(train_curve(False, opt, steps, bf16=False, **kw))
+        arms["bf16_torch"].append(train_curve(False, opt, steps, bf16=True, **kw))
     tail = max(10, int(steps * tail_frac))
     fin = lambda r: float(sorted(r["losses"][-tail:])[tail // 2])  # noqa: E731
-    return {"optimizer": opt, "arch": arch, "batch": bs, "steps": steps, "tail_steps": tail,
-            "engine_final_loss": fin(eng), "reference_final_loss": fin(ref), "bf16_torch_final_loss": fin(b16),
-            "engine_test_acc": eng["test_acc"], "reference_test_acc": ref["test_acc"],
-            "bf16_torch_test_acc": b16["test_acc"],
-            "engine_test_loss": eng["test_loss"], "reference_test_loss": ref["test_loss"],
-            "bf16_torch_test_loss": b16["test_loss"],
-            "initial_loss": sum(ref["losses"][:5]) / 5,
-            "engine_s": eng["seconds"], "reference_s": ref["seconds"], "bf16_torch_s": b16["seconds"],
-            "engine_curve": eng["losses"][::5], "reference_curve": ref["losses"][::5],
-            "bf16_torch_curve": b16["losses"][::5]}
+    mean = lambda xs: float(sum(xs) / len(xs))  # noqa: E731
+    out = {"optimizer": opt, "arch": arch, "batch": bs, "steps": steps, "tail_steps": tail, "repeats": max(1, repeats)}
+    for name, runs in arms.items():
+        out[f"{name}_final_loss"] = mean([fin(r) for r in runs])
+        out[f"{name}_test_acc"] = mean([r["test_acc"] for r in runs])
+        out[f"{name}_test_loss"] = mean([r["test_loss"] for r in runs])
+        out[f"{name}_test_losses"] = [r["test_loss"] for r in runs]
+        out[f"{name}_test_accs"] = [r["test_acc"] for r in runs]
+        out[f"{name}_s"] = runs[0]["seconds"]
+        out[f"{name}_curve"] = runs[0]["losses"][::5]
+    ref = arms["reference"]
+    out["reference_spread_loss"] = max(r["test_loss"] for r in ref) - min(r["test_loss"] for r in ref)
+    out["reference_spread_acc"] = max(r["test_acc"] for r in ref) - min(r["test_acc"] for r in ref)
+    out["initial_loss"] = sum(ref[0]["losses"][:5]) / 5
+    return out
 
 
 def main():
@@ -153,8 +162,9 @@ def main():
     ap.add_argument("--arch", default="resnet18")
     ap.add_argument("--bs", type=int, default=128)
     ap.add_argument("--out", default=None)
+    ap.add_argument("--repeats", type=int, default=1)
     a = ap.parse_args()
-    res = [compare(o, a.steps, arch=a.arch, bs=a.bs) for o in a.opts.split(",")]
+    res = [compare(o, a.steps, arch=a.arch, bs=a.bs, repeats=a.repeats) for o in a.opts.split(",")]
     for r in res:
         print(f"{r['optimizer']}: final loss engine {r['engine_final_loss']:.4f} vs fp32 {r['reference_final_loss']:.4f}"
               f" (start {r['initial_loss']:.3f}); test acc engine {r['engine_test_acc']:.3f} vs fp32 "

@@ -4,7 +4,8 @@ steps on a learnable synthetic CIFAR task (scripts/convergence.py; VERDICT r3 #7
 The error budget is what bf16 arithmetic alone costs: a third run, plain PyTorch under bf16
 autocast (FDT_NATIVE=0) from the same weights on the same batches.  The engine must land at
 most twice as far from the fp32 run as that run does (plus a small epsilon), on the HELD-OUT
-loss and accuracy of the final weights -- no absolute floor.  (The per-step training losses
+loss and accuracy of the final weights (means over two repeats of every arm), or twice the fp32
+run's own repeat spread if that is larger -- no absolute floor.  (The per-step training losses
 at the end are heavy-tailed -- 0.005-0.17 step to step in every arm -- so their tail mean or
 median swung by 5-8x between repeats of identical code, profiles/r5/convergence_flaky.txt;
 the held-out loss of the final weights is a smooth function of them.)  Every run must also
@@ -20,9 +21,12 @@ pytestmark = pytest.mark.gpu
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
-# the fp32 reference's OWN repeat-to-repeat spread on this task (non-deterministic GPU reductions
-# amplified over 300 steps): held-out loss 0.035-0.114, accuracy 0.966-0.988 across identical runs
-# (profiles/r5/convergence_flaky.txt) -- a smaller epsilon fails the reference against itself
+# every arm runs twice and is compared by its mean over the repeats; the budget is bf16
+# arithmetic's distance from fp32 OR the fp32 reference's own repeat-to-repeat spread measured in
+# the same test, whichever is larger (the fp32 held-out loss alone moved 0.035-0.29 across
+# repeats of identical code: non-deterministic GPU reductions amplified over 300 steps, the
+# cross entropy dominated by a few confident mistakes -- profiles/r5/convergence_flaky.txt)
+REPEATS = 2
 EPS_LOSS = 0.05   # absolute, on the held-out mean cross entropy
 EPS_ACC = 0.02    # 20 of 1024 held-out samples
 
@@ -30,15 +34,15 @@ EPS_ACC = 0.02    # 20 of 1024 held-out samples
 @pytest.mark.parametrize("opt,arch", [("madgrad", "resnet18"), ("ngd", "resnet18"), ("madgrad", "resnet50")])
 def test_engine_converges_like_fp32_reference(cuda, opt, arch):
     from scripts.convergence import compare
-    r = compare(opt, 300, arch=arch, bs=128)
+    r = compare(opt, 300, arch=arch, bs=128, repeats=REPEATS)
     print({k: v for k, v in r.items() if not k.endswith("curve")})
     # every run learns the task ...
     for k in ("reference_final_loss", "engine_final_loss", "bf16_torch_final_loss"):
         assert r[k] < 0.5 * r["initial_loss"], (k, r[k])
-    # ... and the engine lands as close to fp32 as bf16 arithmetic allows
+    # ... and the engine lands as close to fp32 as bf16 arithmetic or fp32's own spread allows
     d_loss = abs(r["engine_test_loss"] - r["reference_test_loss"])
-    b_loss = abs(r["bf16_torch_test_loss"] - r["reference_test_loss"])
+    b_loss = max(abs(r["bf16_torch_test_loss"] - r["reference_test_loss"]), r["reference_spread_loss"])
     assert d_loss <= 2 * b_loss + EPS_LOSS, (d_loss, b_loss)
     d_acc = abs(r["engine_test_acc"] - r["reference_test_acc"])
-    b_acc = abs(r["bf16_torch_test_acc"] - r["reference_test_acc"])
+    b_acc = max(abs(r["bf16_torch_test_acc"] - r["reference_test_acc"]), r["reference_spread_acc"])
     assert d_acc <= 2 * b_acc + EPS_ACC, (d_acc, b_acc)
