@@ -127,7 +127,8 @@ def compare(opt: str, steps: int, device="cuda", arch="resnet18", bs=128, tail_f
     0.01-0.17 at the end and a late spike phase of one run would otherwise decide the mean (a
     ResNet-50 engine run measured a tail mean of 0.28 against 0.07 in a repeat of the same
     code, with a 0.95 test accuracy).  ``repeats`` > 1: every arm runs that many times (GPU
-    reductions make repeats differ) and its held-out loss / accuracy are the means over them;
+    reductions make repeats differ) and its held-out loss / accuracy are the medians over them
+    (means for an even count);
     ``reference_spread_*`` is then the fp32 arm's own max - min across its repeats."""
     task = make_task(device=device)
     kw = dict(device=device, task=task, arch=arch, bs=bs)
@@ -138,7 +139,9 @@ def compare(opt: str, steps: int, device="cuda", arch="resnet18", bs=128, tail_f
         arms["bf16_torch"].append(train_curve(False, opt, steps, bf16=True, **kw))
     tail = max(10, int(steps * tail_frac))
     fin = lambda r: float(sorted(r["losses"][-tail:])[tail // 2])  # noqa: E731
-    mean = lambda xs: float(sum(xs) / len(xs))  # noqa: E731
+    # (median over repeats: one bf16 run in ~10 lands in a heavy tail of the held-out loss on this
+    # task, engine or PyTorch autocast alike -- profiles/r5/convergence_spread_resnet50.txt)
+    mean = lambda xs: float(sorted(xs)[len(xs) // 2]) if len(xs) % 2 else float(sum(xs) / len(xs))  # noqa: E731
     out = {"optimizer": opt, "arch": arch, "batch": bs, "steps": steps, "tail_steps": tail, "repeats": max(1, repeats)}
     for name, runs in arms.items():
         out[f"{name}_final_loss"] = mean([fin(r) for r in runs])

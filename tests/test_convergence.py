@@ -4,7 +4,7 @@ steps on a learnable synthetic CIFAR task (scripts/convergence.py; VERDICT r3 #7
 The error budget is what bf16 arithmetic alone costs: a third run, plain PyTorch under bf16
 autocast (FDT_NATIVE=0) from the same weights on the same batches.  The engine must land at
 most twice as far from the fp32 run as that run does (plus a small epsilon), on the HELD-OUT
-loss and accuracy of the final weights (means over two repeats of every arm), or twice the fp32
+loss and accuracy of the final weights (medians over three repeats of every arm), or twice the fp32
 run's own repeat spread if that is larger -- no absolute floor.  (The per-step training losses
 at the end are heavy-tailed -- 0.005-0.17 step to step in every arm -- so their tail mean or
 median swung by 5-8x between repeats of identical code, profiles/r5/convergence_flaky.txt;
@@ -21,12 +21,14 @@ pytestmark = pytest.mark.gpu
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
-# every arm runs twice and is compared by its mean over the repeats; the budget is bf16
+# every arm runs three times and is compared by its median over the repeats (one bf16 run in ~10 --
+# engine or PyTorch autocast -- lands in a heavy tail of the held-out loss on this task,
+# profiles/r5/convergence_spread_resnet50.txt); the budget is bf16
 # arithmetic's distance from fp32 OR the fp32 reference's own repeat-to-repeat spread measured in
 # the same test, whichever is larger (the fp32 held-out loss alone moved 0.035-0.29 across
 # repeats of identical code: non-deterministic GPU reductions amplified over 300 steps, the
 # cross entropy dominated by a few confident mistakes -- profiles/r5/convergence_flaky.txt)
-REPEATS = 2
+REPEATS = 3
 EPS_LOSS = 0.05   # absolute, on the held-out mean cross entropy
 EPS_ACC = 0.02    # 20 of 1024 held-out samples
 
