@@ -66,11 +66,11 @@ void cast_bf16(uint64_t x, uint64_t y, long n, uint64_t stream);
 void madgrad_pack_step(uint64_t p, uint64_t g, uint64_t gss, uint64_t s, uint64_t x0, uint64_t shadow, long n,
                        float lr, float momentum, float wd, float eps, int decouple, long k, uint64_t kskip,
                        uint64_t gsc, uint64_t found_inf, int zero_grad, uint64_t tab, int ntab, long nblk_pack,
-                       uint64_t rr, int nrr, long rest_total, uint64_t stream);
+                       uint64_t rr, int nrr, long rest_total, int maxt, int count_skips, uint64_t stream);
 void sgd_pack_step(uint64_t p, uint64_t g, uint64_t buf, uint64_t shadow, long n, float lr, float momentum,
                    float dampening, float wd, int nesterov, int first, uint64_t gsc, uint64_t found_inf,
                    int zero_grad, uint64_t lr_dev, uint64_t tab, int ntab, long nblk_pack, uint64_t rr, int nrr,
-                   long rest_total, uint64_t stream);
+                   long rest_total, int maxt, int count_skips, uint64_t stream);
 // head.hip
 void head_fwd(uint64_t h, uint64_t W, uint64_t b, uint64_t pooled, uint64_t logits, int N, int HW, int C, int K,
               uint64_t stream);

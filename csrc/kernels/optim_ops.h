@@ -42,6 +42,7 @@ struct MadArgs {
   const float* gsc;
   const int* found_inf;
   int zero_grad;
+  int count_skips = 1;  // 0: a second launch of the same step (the first one counts a skipped step)
 };
 
 struct MadOp {
@@ -55,7 +56,7 @@ struct MadOp {
   }
   __device__ __forceinline__ static bool skipped(const MadArgs& a) { return skip_step(a.found_inf); }
   __device__ __forceinline__ static void on_skip(const MadArgs& a, long n) {
-    count_skip(a.kskip);
+    if (a.count_skips) count_skip(a.kskip);
     skip_zero(a.g, n, a.zero_grad);
   }
   // the rule on loaded values: q = grad_sum_sq, sv = s (updated in place); returns the new p

@@ -4,7 +4,8 @@
 // pack_weights pass at the start of every forward (a read of all 23.5M fp32 conv weights and
 // a write of both bf16 layouts, ~50 us at ResNet-50) disappears.
 //
-// Grid: [conv blocks | rest blocks].  A conv block owns one 32 (co) x 64 (ci) x T slice of one
+// Grid: [conv blocks | rest blocks]; the caller splits a model into two launches (1x1 weights +
+// the rest ranges at a 4 KB LDS image, then the 3x3 / 2x2 weights at 38 KB).  A conv block owns one 32 (co) x 64 (ci) x T slice of one
 // conv weight (the repack's blocking): it applies the update rule (optim_ops.h, bitwise the
 // flat kernels' math) to each of its elements in flat (OIHW) order -- coalesced reads and writes
 // of p / g / state -- stages the new values as bf16 in LDS and stores both packed layouts.  The
@@ -63,7 +64,9 @@ __device__ __forceinline__ void update_block(const Op& op, const PackUpdEntry& E
   pack::store_layouts<T>(img, k, reinterpret_cast<bf16*>(E.wf), reinterpret_cast<bf16*>(E.wd), Cout, Cxp);
 }
 
-template <class Op, class Args>
+// MAXT: the largest tap count among the launch's entries -- the LDS image is sized for it, so the
+// 1x1 weights (most of the blocks) run as their own launch at 9x less LDS (more resident blocks)
+template <class Op, class Args, int MAXT>
 __global__ __launch_bounds__(256) void pack_update_kernel(const Args args, long n,
                                                           const PackUpdEntry* __restrict__ tab, int ntab,
                                                           long nblk_pack, const RestRange* __restrict__ rr, int nrr,
@@ -73,7 +76,7 @@ __global__ __launch_bounds__(256) void pack_update_kernel(const Args args, long 
     return;
   }
   const Op op(args);
-  __shared__ bf16 img[pack::kCo * pack::kMaxTaps * pack::kLd];
+  __shared__ bf16 img[pack::kCo * MAXT * pack::kLd];
   const long bid = blockIdx.x;
   if (bid < nblk_pack) {
     int lo = 0, hi = ntab - 1;
@@ -84,9 +87,13 @@ __global__ __launch_bounds__(256) void pack_update_kernel(const Args args, long 
     }
     const PackUpdEntry E = tab[lo];
     const int b = (int)(bid - E.blk0);
-    if (E.ntaps == 1) update_block<1>(op, E, b, img);
-    else if (E.ntaps == 9) update_block<9>(op, E, b, img);
-    else update_block<4>(op, E, b, img);  // launcher checks ntaps in {1, 4, 9}
+    if constexpr (MAXT == 1) {
+      update_block<1>(op, E, b, img);
+    } else {
+      if (E.ntaps == 1) update_block<1>(op, E, b, img);
+      else if (E.ntaps == 9) update_block<9>(op, E, b, img);
+      else update_block<4>(op, E, b, img);  // the table builder admits ntaps in {1, 4, 9}
+    }
     return;
   }
   const long nb = (long)gridDim.x - nblk_pack;
@@ -116,7 +123,7 @@ struct PackPlan {
 };
 
 PackPlan pack_plan(uint64_t tab, int ntab, long nblk_pack, uint64_t rr, int nrr, long rest_total) {
-  FDT_CHECK(tab != 0 && ntab >= 1 && nblk_pack >= 1, "pack-update table");
+  FDT_CHECK((tab != 0 && ntab >= 1 && nblk_pack >= 1) || (ntab == 0 && nblk_pack == 0), "pack-update table");
   FDT_CHECK(rest_total == 0 || (rr != 0 && nrr >= 1), "pack-update rest ranges");
   FDT_CHECK(nblk_pack + 1024 < (1L << 31), "pack-update grid");
   return PackPlan{P<const PackUpdEntry>(tab), ntab, nblk_pack, P<const RestRange>(rr), nrr, rest_total};
@@ -127,28 +134,39 @@ PackPlan pack_plan(uint64_t tab, int ntab, long nblk_pack, uint64_t rr, int nrr,
 void madgrad_pack_step(uint64_t p, uint64_t g, uint64_t gss, uint64_t s, uint64_t x0, uint64_t shadow, long n,
                        float lr, float momentum, float wd, float eps, int decouple, long k, uint64_t kskip,
                        uint64_t gsc, uint64_t found_inf, int zero_grad, uint64_t tab, int ntab, long nblk_pack,
-                       uint64_t rr, int nrr, long rest_total, uint64_t stream) {
+                       uint64_t rr, int nrr, long rest_total, int maxt, int count_skips, uint64_t stream) {
   FDT_CHECK(momentum == 0.f || x0 != 0, "x0 buffer required with momentum");
+  FDT_CHECK(maxt == 1 || maxt == 9, "pack-update: maxt 1 or 9");
   const PackPlan pl = pack_plan(tab, ntab, nblk_pack, rr, nrr, rest_total);
   const opt::MadArgs a{P<float>(p), P<float>(g), P<float>(gss), P<float>(s), P<float>(x0), P<bf16>(shadow),
                        lr, momentum, wd, eps, decouple, k, P<int>(kskip), P<const float>(gsc),
-                       P<const int>(found_inf), zero_grad};
-  hipLaunchKernelGGL((pack_update_kernel<opt::MadOp, opt::MadArgs>), pl.grid(), dim3(256), 0, as_stream(stream), a,
-                     n, pl.tab, pl.ntab, pl.nblk_pack, pl.rr, pl.nrr, pl.rest_total);
+                       P<const int>(found_inf), zero_grad, count_skips};
+  if (maxt == 1)
+    hipLaunchKernelGGL((pack_update_kernel<opt::MadOp, opt::MadArgs, 1>), pl.grid(), dim3(256), 0, as_stream(stream),
+                       a, n, pl.tab, pl.ntab, pl.nblk_pack, pl.rr, pl.nrr, pl.rest_total);
+  else
+    hipLaunchKernelGGL((pack_update_kernel<opt::MadOp, opt::MadArgs, 9>), pl.grid(), dim3(256), 0, as_stream(stream),
+                       a, n, pl.tab, pl.ntab, pl.nblk_pack, pl.rr, pl.nrr, pl.rest_total);
   FDT_LAUNCH_CHECK();
 }
 
 void sgd_pack_step(uint64_t p, uint64_t g, uint64_t buf, uint64_t shadow, long n, float lr, float momentum,
                    float dampening, float wd, int nesterov, int first, uint64_t gsc, uint64_t found_inf,
                    int zero_grad, uint64_t lr_dev, uint64_t tab, int ntab, long nblk_pack, uint64_t rr, int nrr,
-                   long rest_total, uint64_t stream) {
+                   long rest_total, int maxt, int count_skips, uint64_t stream) {
+  (void)count_skips;  // SGD keeps no step counter
   FDT_CHECK(momentum == 0.f || buf != 0, "momentum buffer required");
+  FDT_CHECK(maxt == 1 || maxt == 9, "pack-update: maxt 1 or 9");
   const PackPlan pl = pack_plan(tab, ntab, nblk_pack, rr, nrr, rest_total);
   const opt::SgdArgs a{P<float>(p), P<float>(g), P<float>(buf), P<bf16>(shadow), lr, momentum, dampening, wd,
                        nesterov, first, P<const float>(gsc), P<const int>(found_inf), zero_grad,
                        P<const float>(lr_dev)};
-  hipLaunchKernelGGL((pack_update_kernel<opt::SgdOp, opt::SgdArgs>), pl.grid(), dim3(256), 0, as_stream(stream), a,
-                     n, pl.tab, pl.ntab, pl.nblk_pack, pl.rr, pl.nrr, pl.rest_total);
+  if (maxt == 1)
+    hipLaunchKernelGGL((pack_update_kernel<opt::SgdOp, opt::SgdArgs, 1>), pl.grid(), dim3(256), 0, as_stream(stream),
+                       a, n, pl.tab, pl.ntab, pl.nblk_pack, pl.rr, pl.nrr, pl.rest_total);
+  else
+    hipLaunchKernelGGL((pack_update_kernel<opt::SgdOp, opt::SgdArgs, 9>), pl.grid(), dim3(256), 0, as_stream(stream),
+                       a, n, pl.tab, pl.ntab, pl.nblk_pack, pl.rr, pl.nrr, pl.rest_total);
   FDT_LAUNCH_CHECK();
 }
 

@@ -243,11 +243,12 @@ class Plan:
         return flat.data._version + sum(u.w._version for u in self.units)
 
     def update_table(self, flat):
-        """Device tables of the fused update-and-pack step over ``flat`` (a FlatParams holding
-        every conv weight as a contiguous fp32 OIHW view): (entries int64 [n, 8], n, conv
-        blocks, rest ranges int64 [m, 3], m, rest elements), or None when the layouts are not
-        allocated yet (before the first training forward) or the weights are not all in
-        ``flat``."""
+        """Launches of the fused update-and-pack step over ``flat`` (a FlatParams holding every
+        conv weight as a contiguous fp32 OIHW view): a list of (entries int64 [n, 8], n, conv
+        blocks, rest ranges int64 [m, 3], m, rest elements, max taps, counts a skipped step) --
+        the 1x1 weights with every non-conv range at a 4 KB LDS image, then the 3x3 / 2x2
+        weights at 38 KB -- or None when the layouts are not allocated yet (before the first
+        training forward) or the weights are not all in ``flat``."""
         if not PACK_IN_OPT or self.fsdp is not None or not flat.data.is_cuda:
             return None
         c = self.__dict__.get("_upd")
@@ -256,7 +257,9 @@ class Plan:
         if any(u.wf is None or (u.wd is None and u.shp.cin >= 8) for u in self.units):
             return None
         base, n = flat.data.data_ptr(), flat.numel
-        rows, spans, blk = [], [], 0
+        rows = {1: [], 9: []}
+        blks = {1: 0, 9: 0}
+        spans = []
         for u in self.units:
             w = u.w
             off, rem = divmod(w.data_ptr() - base, 4)
@@ -266,8 +269,10 @@ class Plan:
             co, cin, kh, kw = w.shape
             if kh * kw not in (1, 4, 9) or co % 8 or u.shp.cxp % 8 or u.wf.device != w.device:
                 return None
-            rows.append([off, u.wf.data_ptr(), 0 if u.wd is None else u.wd.data_ptr(), co, cin, u.shp.cxp, kh * kw, blk])
-            blk += -(-co // 32) * -(-u.shp.cxp // 64)
+            g = 1 if kh * kw == 1 else 9
+            rows[g].append([off, u.wf.data_ptr(), 0 if u.wd is None else u.wd.data_ptr(), co, cin, u.shp.cxp,
+                            kh * kw, blks[g]])
+            blks[g] += -(-co // 32) * -(-u.shp.cxp // 64)
             spans.append((off, off + w.numel()))
         spans.sort()
         rr, cur, cum = [], 0, 0
@@ -282,11 +287,19 @@ class Plan:
             rr.append([cur, n - cur, cum])
             cum += n - cur
         dev = flat.data.device
-        tab = torch.tensor(rows, dtype=torch.int64, device=dev)
-        rrt = torch.tensor(rr or [[0, 0, 0]], dtype=torch.int64, device=dev)
-        ent = (tab, len(rows), blk, rrt, len(rr), cum)
-        self._upd = (flat, ent)
-        return ent
+        keep, launches = [], []
+        for g in (1, 9):
+            with_rest = g == 1
+            if not rows[g] and not (with_rest and cum):
+                continue
+            tab = torch.tensor(rows[g] or [[0] * 8], dtype=torch.int64, device=dev)
+            rrt = torch.tensor(rr or [[0, 0, 0]], dtype=torch.int64, device=dev)
+            keep += [tab, rrt]
+            launches.append((tab.data_ptr() if rows[g] else 0, len(rows[g]), blks[g],
+                             rrt.data_ptr() if with_rest and rr else 0, len(rr) if with_rest else 0,
+                             cum if with_rest else 0, g, int(not launches)))
+        self._upd = (flat, launches, keep)
+        return launches
 
     def mark_opt_packed(self, flat):
         """The optimizer step just written (or, when skipped on the device, left unchanged) the

@@ -97,15 +97,11 @@ class FlatOptimizer(torch.optim.Optimizer):
         return getattr(getattr(self.flat, "pack_owner", None), "_plan", None)
 
     def _pack_args(self):
-        """Trailing table arguments of the fused update-and-pack launch, or None."""
+        """Trailing table arguments of each fused update-and-pack launch (a list), or None."""
         plan = self._pack_plan()
         if plan is None or not self._native:
             return None
-        ent = plan.update_table(self.flat)
-        if ent is None:
-            return None
-        tab, ntab, nblk, rr, nrr, rest = ent
-        return [tab.data_ptr(), ntab, nblk, rr.data_ptr(), nrr, rest]
+        return plan.update_table(self.flat)
 
     # ------------------------------------------------------------ state dict
     # The optimizer state lives in whole-model flat buffers (self.state["__flat__"]), which
@@ -178,7 +174,8 @@ class SGD(FlatOptimizer):
                     int(self.zero_grad_in_step), _p(getattr(self, "lr_dev", None))]
             pk = self._pack_args()
             if pk is not None:
-                _native.native().sgd_pack_step(*args, *pk, _sp())
+                for launch in pk:
+                    _native.native().sgd_pack_step(*args, *launch, _sp())
                 self._packed = True
             else:
                 _native.native().sgd_step(*args, _sp())
@@ -219,7 +216,8 @@ class MADGRAD(FlatOptimizer):
                     self.kskip.data_ptr(), _p(grad_scale), _p(found_inf), int(self.zero_grad_in_step)]
             pk = self._pack_args()
             if pk is not None:
-                _native.native().madgrad_pack_step(*args, *pk, _sp())
+                for launch in pk:
+                    _native.native().madgrad_pack_step(*args, *launch, _sp())
                 self._packed = True
             else:
                 _native.native().madgrad_step(*args, _sp())
