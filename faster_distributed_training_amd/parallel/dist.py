@@ -38,6 +38,13 @@ def _comm_env():
     get their own queue (``profiles/r3s3/ddp_queues.txt``)."""
     os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
     os.environ.setdefault("TORCH_NCCL_HIGH_PRIORITY", "1")
+    # No recycled collective events: the bucket all-reduces captured into the backward graph
+    # record their completion events inside the capture, and torch's event cache hands such an
+    # event to a later eager collective; once (closing run of round 5, the capture-check
+    # fallback test) RCCL's watchdog thread then failed querying "an event last recorded in a
+    # capturing stream" and aborted the process.  A fresh event per eager collective costs
+    # microseconds (in capture mode the step's collectives are graph nodes).
+    os.environ.setdefault("TORCH_NCCL_CUDA_EVENT_CACHE", "0")
 
 
 def _bind_device():

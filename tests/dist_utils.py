@@ -26,7 +26,8 @@ def _entry(rank, world, port, fn, args, errq, native=False, backend="gloo"):
         import torch.distributed as dist
         if backend == "nccl":  # RCCL: one process per device; bind it before the group exists
             import torch
-            os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+            from faster_distributed_training_amd.parallel.dist import _comm_env
+            _comm_env()  # (the package's RCCL environment defaults)
             torch.cuda.set_device(rank)
             dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", rank))
         else:
