@@ -68,6 +68,11 @@ def parse():
     ap.add_argument("--deterministic", action="store_true", help="bitwise-repeatable engine reductions (cost probe)")
     ap.add_argument("--model", default="resnet50", choices=["resnet50", "transformer"],
                     help="transformer: secondary benchmark (BASELINE.json config 4, AG-News-shaped)")
+    ap.add_argument("--simulate-world", type=int, default=0,
+                    help="rehearse ONE rank of a world-N job on this GPU (parallel/simulate.py): rank R's batch "
+                         "share, optimizer / FSDP shards, bucket plan and graph replay, collectives replaced by "
+                         "same-sized local copies (no xGMI time); the record is per-rank, not a scaling point")
+    ap.add_argument("--simulate-rank", type=int, default=0)
     ap.add_argument("--seq-buckets", default="128,256",
                     help="transformer: padded-length buckets (a batch pads to the smallest bucket >= its longest "
                          "sample; the largest bucket must cover the longest sample, so nothing is truncated)")
@@ -108,6 +113,10 @@ def main():
         sys.exit(f"bench.py: --gpus {args.gpus} but this launcher started WORLD_SIZE={world_env} ranks")
     if args.no_native:
         os.environ["FDT_NATIVE"] = "0"
+    if args.simulate_world:
+        assert world_env is None and args.gpus == 1, "--simulate-world runs in ONE process on one GPU"
+        from faster_distributed_training_amd.parallel import simulate
+        simulate.install(args.simulate_rank, args.simulate_world)
     if args.model == "transformer":
         return bench_transformer(args)
     import torch
@@ -115,7 +124,7 @@ def main():
 
     from faster_distributed_training_amd.train.resnet_trainer import ResNetConfig, ResNetTrainer
 
-    n = int(os.environ.get("WORLD_SIZE", "1"))
+    n = args.simulate_world or int(os.environ.get("WORLD_SIZE", "1"))
     gb = args.global_batch
     assert gb % n == 0, "global batch must divide evenly over ranks"
     cfg = ResNetConfig(arch=args.arch, bs=gb // n, synthetic=True, eval=False, plot=False,
@@ -152,9 +161,11 @@ def main():
     # warm-up); make sure that one-time capture is never inside the timed window.
     graphs = cuda and not args.no_graphs and not args.no_native
     untimed = max(args.warmup, 3) if graphs else args.warmup
-    for _ in range(untimed):
+    for i in range(untimed):
         x, y = next(it)
         tr.train_step(x, y)
+        if i == 0:
+            _first_step_comm()
     sync()
     t0 = time.perf_counter()
     for _ in range(args.steps):
@@ -193,15 +204,39 @@ def main():
     }
     _sharding_fields(tr, rec)
     _dist_fields(rec)
-    if tr.rank == 0:
+    if tr.rank == 0 or rec.get("simulated"):
         print(json.dumps(rec), flush=True)
     if dist.is_initialized():
         dist.destroy_process_group()
 
 
+_COMM0 = None
+
+
+def _first_step_comm():
+    """Collective bytes of the first (eager) step of a simulated rank: later steps replay graphs,
+    whose captured collectives never reach the Python counters."""
+    global _COMM0
+    from faster_distributed_training_amd.parallel import simulate
+    if simulate.active() is not None and _COMM0 is None:
+        _COMM0 = simulate.comm_bytes()
+
+
 def _dist_fields(rec):
     """The process group that actually ran: its size (must equal n_gpus) and backend."""
     import torch.distributed as dist
+    from faster_distributed_training_amd.parallel import simulate
+    sim = simulate.active()
+    if sim is not None:
+        # one GPU played rank R of world N: a per-rank step time, not a scaling point
+        rec["metric"] = f"simulated per-rank step: rank {sim.rank} of world {sim.world} on one GPU ({rec['metric']})"
+        rec["n_gpus"] = 1
+        rec["simulated"] = {"world": sim.world, "rank": sim.rank, "per_rank_batch": rec["config"]["global_batch"] // sim.world,
+                            "comm_bytes_first_step": _COMM0,
+                            "note": "collectives replaced by same-sized local copies; xGMI transfer time not included"}
+        rec["dist_world"] = sim.world
+        rec["backend"] = f"simulated({dist.get_backend()})"
+        return
     if dist.is_initialized():
         rec["dist_world"] = dist.get_world_size()
         rec["backend"] = dist.get_backend()
@@ -260,7 +295,7 @@ def bench_transformer(args):
 
     from faster_distributed_training_amd.train.transformer_trainer import TransformerConfig, TransformerTrainer
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+    world = args.simulate_world or int(os.environ.get("WORLD_SIZE", "1"))
     gb = 256 if args.global_batch == 1024 else args.global_batch
     assert gb % world == 0
     buckets = tuple(sorted(int(b) for b in args.seq_buckets.split(",")))
@@ -284,8 +319,10 @@ def bench_transformer(args):
             from faster_distributed_training_amd.parallel.dist import barrier
             barrier()
 
-    for _ in range(args.warmup):
+    for i in range(args.warmup):
         tr.train_step(*next(it))
+        if i == 0:
+            _first_step_comm()
     sync()
     t0 = time.perf_counter()
     for _ in range(args.steps):
@@ -311,7 +348,7 @@ def bench_transformer(args):
     rec["config"]["hip_graphs"] = bool(tr._graphs_on()) if cuda else False
     _sharding_fields(tr, rec)
     _dist_fields(rec)
-    if tr.rank == 0:
+    if tr.rank == 0 or rec.get("simulated"):
         print(json.dumps(rec), flush=True)
     if dist.is_initialized():
         dist.destroy_process_group()

@@ -40,7 +40,8 @@ void residual_act_lazy(uint64_t ya, const std::vector<uint64_t>& la_ptr, const s
                        uint64_t sb, uint64_t tb, uint64_t xid, uint64_t out, uint64_t mask, long M, int C, int act,
                        float alpha, int dt, uint64_t stream);
 void residual_act_bwd(uint64_t g, uint64_t out, uint64_t mask, uint64_t ya, uint64_t yb, uint64_t gpre, uint64_t part,
-                      int part_rows, long M, int C, int act, float alpha, int dt, uint64_t stream, int ghw);
+                      int part_rows, long M, int C, int act, float alpha, int dt, uint64_t stream, int ghw,
+                      const std::vector<uint64_t>& jz);
 // deterministic mode (common.h): no-wrap statistics slots, ordered split-K sums
 void set_deterministic_mode(bool on);
 bool deterministic_mode();
@@ -112,7 +113,7 @@ void conv_igemm(uint64_t x, uint64_t x2, uint64_t ps, uint64_t pt, uint64_t pg, 
                 const std::vector<int>& wt, int Cout, int ldw, int Hout, int Wout, int OS, int oy, int ox, int pro,
                 int pro_act, float pro_alpha, int epi, int epi_act, float epi_alpha, int BM, int BN, int BK, int nsplit,
                 uint64_t slab, uint64_t cnt, int kg, uint64_t stream, const std::vector<uint64_t>& lz_ptr,
-                const std::vector<double>& lz_val);
+                const std::vector<double>& lz_val, const std::vector<uint64_t>& jz);
 void conv_igemm_join(uint64_t y, uint64_t r, uint64_t s, uint64_t t, uint64_t s2, uint64_t t2, uint64_t w, uint64_t out,
                      uint64_t part, int part_rows, uint64_t jout, uint64_t jmask, long Nb, int H, int W, int Cx, int Cout,
                      int ldw, int BM, int BN, int BK, int nsplit, uint64_t slab, uint64_t cnt, int kg, uint64_t stream,

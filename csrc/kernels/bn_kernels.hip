@@ -516,11 +516,31 @@ __global__ __launch_bounds__(kBlk) void residual_act_bwd_kernel(const T* __restr
                                                                 T* __restrict__ gpre, float* __restrict__ part,
                                                                 unsigned slot_mask, long M, int C, int TPR, int RPP,
                                                                 long rows_per_blk, int act, float alpha, int ghw,
-                                                                int wt) {
+                                                                int wt, const float* __restrict__ zsa,
+                                                                const float* __restrict__ zta,
+                                                                const float* __restrict__ zsb,
+                                                                const float* __restrict__ ztb,
+                                                                const T* __restrict__ xid) {
   __shared__ float sm[kBlk * 24];
   const int tid = threadIdx.x;
   const int gi = tid % TPR, rr = tid / TPR;
   const int c0 = (blockIdx.y * TPR + gi) * 8;
+  // z mode (zsa set; CELU joins): act'(z) = exp(z/alpha) from the fp32 pre-activation, recomputed
+  // exactly as the forward join formed it, z = ya*sa + ta + (yb ? yb*sb + tb : xid).  The CELU
+  // output o is no substitute below z ~ -0.3: 1 + o/alpha from a bf16 o carries an absolute error
+  // of ~2^-11/alpha ~ 6.5e-3 against a true derivative of < 0.02, and o(z -> -inf) rounds to
+  // -0.07520 < -alpha, a sign-flipped derivative for every deeply negative z.
+  const bool zm = zsa != nullptr && !mask;
+  float sa8[8], ta8[8], sb8[8], tb8[8];
+  if (zm) {
+    load8f(zsa, c0, sa8);
+    load8f(zta, c0, ta8);
+    if (yb) {
+      load8f(zsb, c0, sb8);
+      load8f(ztb, c0, tb8);
+    }
+  }
+  const T* osrc = zm ? (yb ? nullptr : xid) : out;  // the 4th streamed operand: out | xid | none
   const long r_begin = (long)blockIdx.x * rows_per_blk;
   long r_end = r_begin + rows_per_blk;
   if (r_end > M) r_end = M;
@@ -532,7 +552,15 @@ __global__ __launch_bounds__(kBlk) void residual_act_bwd_kernel(const T* __restr
     float gp8[8];
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
-      const float gp = mask ? ((m >> i) & 1u ? gv[i] : 0.f) : gv[i] * act_grad_from_out(ov[i], act, alpha);
+      float gp;
+      if (mask) {
+        gp = (m >> i) & 1u ? gv[i] : 0.f;
+      } else if (zm) {
+        const float z = fmaf(av[i], sa8[i], ta8[i]) + (yb ? fmaf(bv[i], sb8[i], tb8[i]) : ov[i]);
+        gp = gv[i] * act_grad(z, act, alpha);
+      } else {
+        gp = gv[i] * act_grad_from_out(ov[i], act, alpha);
+      }
       gp8[i] = gp;
       p0[i] = fmaf(gp, av[i], p0[i]);
       p1[i] += gp;
@@ -554,7 +582,7 @@ __global__ __launch_bounds__(kBlk) void residual_act_bwd_kernel(const T* __restr
     Vec8<T>::load(ya + e1, a1);
     if (yb) { Vec8<T>::load(yb + e0, b0); Vec8<T>::load(yb + e1, b1); }
     if (mask) { m0 = mask[e0 >> 3]; m1 = mask[e1 >> 3]; }
-    else { Vec8<T>::load(out + e0, o0); Vec8<T>::load(out + e1, o1); }
+    else if (osrc) { Vec8<T>::load(osrc + e0, o0); Vec8<T>::load(osrc + e1, o1); }
     row(e0, g0, a0, b0, o0, m0);
     row(e1, g1, a1, b1, o1, m1);
   }
@@ -566,7 +594,7 @@ __global__ __launch_bounds__(kBlk) void residual_act_bwd_kernel(const T* __restr
     Vec8<T>::load(ya + e, av);
     if (yb) Vec8<T>::load(yb + e, bv);
     if (mask) m = mask[e >> 3];
-    else Vec8<T>::load(out + e, ov);
+    else if (osrc) Vec8<T>::load(osrc + e, ov);
     row(e, gv, av, bv, ov, m);
   }
 #pragma unroll
@@ -939,8 +967,14 @@ void residual_act_lazy(uint64_t ya, const std::vector<uint64_t>& la_ptr, const s
 }
 
 void residual_act_bwd(uint64_t g, uint64_t out, uint64_t mask, uint64_t ya, uint64_t yb, uint64_t gpre, uint64_t part,
-                      int part_rows, long M, int C, int act, float alpha, int dt, uint64_t stream, int ghw) {
-  FDT_CHECK(out != 0 || mask != 0, "residual_act_bwd needs the output or its mask");
+                      int part_rows, long M, int C, int act, float alpha, int dt, uint64_t stream, int ghw,
+                      const std::vector<uint64_t>& jz) {
+  // jz = {} or {sa, ta, sb, tb, xid}: act' from the recomputed pre-activation (z mode, see the kernel)
+  FDT_CHECK(jz.empty() || jz.size() == 5, "residual_act_bwd: jz = [] | [sa, ta, sb, tb, xid]");
+  const bool zm = jz.size() == 5;
+  FDT_CHECK(!zm || (jz[0] && jz[1] && (yb ? (jz[2] && jz[3]) : jz[4] != 0)),
+            "residual_act_bwd z mode: sa, ta and the shortcut's sb, tb (BN'd) or xid (identity)");
+  FDT_CHECK(out != 0 || mask != 0 || zm, "residual_act_bwd needs the output, its mask or the z operands");
   FDT_CHECK(ghw >= 0 && (ghw == 0 || M % ghw == 0), "residual_act_bwd: broadcast rows must divide M");
   ChanGeom gg = chan_geom(C);
   // ~1024 blocks: more waves in flight for this 4-5 stream kernel than the stats default
@@ -955,7 +989,9 @@ void residual_act_bwd(uint64_t g, uint64_t out, uint64_t mask, uint64_t ya, uint
   DISPATCH_T(dt, {
     residual_act_bwd_kernel<T><<<grid, kBlk, 0, as_stream(stream)>>>(
         P<const T>(g), P<const T>(out), P<const uint8_t>(mask), P<const T>(ya), P<const T>(yb), P<T>(gpre), P<float>(part),
-        smask, M, C, gg.TPR, gg.RPP, r, act, alpha, ghw, wt_flag());
+        smask, M, C, gg.TPR, gg.RPP, r, act, alpha, ghw, wt_flag(), zm ? P<const float>(jz[0]) : nullptr,
+        zm ? P<const float>(jz[1]) : nullptr, zm ? P<const float>(jz[2]) : nullptr,
+        zm ? P<const float>(jz[3]) : nullptr, zm ? P<const T>(jz[4]) : nullptr);
   });
   FDT_LAUNCH_CHECK();
 }

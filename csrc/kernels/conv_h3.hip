@@ -1,0 +1,323 @@
+// 3x3 stride-1 convolution with a halo-staged activation operand (MI355X / gfx950).
+//
+// Why a second main loop: the implicit-GEMM kernel (conv_igemm_impl.h) stages the activation
+// operand as im2col rows -- every input pixel is fetched from L2 once per TAP (9x) and every
+// 128-pixel workgroup re-reads all 9*Cx*BN weights.  At batch 1024 a 77-GFLOP 3x3 conv then
+// pulls ~1.2 GB through L2 -> CU for 128x128 tiles: ~20 B/clk/CU, the rate an L2-served
+// gather reaches at one workgroup per CU (MI355X_MICROARCH "Indexed rows: gather into LDS",
+// 66-73 GB/s per CU), so the 3x3 layers sat at 21-33 % of their MFMA bound whatever the tile
+// (profiles/pmc/r5_bs1024_roofline.md, profiles/r5/ring_probe_bs1024.txt).
+//
+// Here a workgroup owns BM = 256 CONSECUTIVE NHWC output pixels (whole image rows, or whole
+// small images) x BN output channels and walks K in 16-channel chunks.  Per chunk it stages
+//   * the zero-padded halo image of its pixels, [halo rows][16 ch] (rows padded to 48 B: 16
+//     consecutive rows hit 16 distinct bank quads -> conflict-free ds_read_b128), ONCE for all
+//     nine taps: a tap is a constant row offset dh*(W+2) + dw into the halo, so the B fragment
+//     of pixel p at tap t is the 16-B row segment q(p) + off(t) -- no im2col address math, no
+//     bounds checks in the MFMA loop (the padding is zeros in LDS);
+//   * the nine taps' weights [9][BN][16 ch] (16-B halves XOR-swizzled by row bit 3:
+//     conflict-free A-fragment reads),
+// register-staged one chunk ahead into a double-buffered LDS ring (one barrier per chunk =
+// 9 taps x TN x TM MFMAs per wave).  L2 -> CU traffic per 256 pixels drops from ~1.2 MB
+// (2 x 128-pixel im2col tiles) to ~0.38 MB (weights once + a ~1.3x halo), and the weight
+// bytes per FLOP halve with the 256-pixel tile.
+//
+// mfma_f32_32x32x16_bf16, weights = A (rows = output channels), halo pixels = B (columns):
+// the accumulator layout, and so the fused epilogue (conv_epilogue: BN statistics / the
+// producer's activation backward / plain store), are those of the implicit-GEMM kernel.
+// Used for the forward 3x3 convolutions on their materialised (normalised + activated)
+// inputs and the stride-1 3x3 data gradients on the pre-folded gradient (the taps of a
+// stride-1 dgrad are the flipped forward taps, |dh|, |dw| <= 1).
+//
+// Reference semantics: resnet.py:72-113 (FusedConvBN forward / backward), resnet.py:201-227.
+#include "conv_igemm_impl.h"
+
+namespace fdt {
+namespace conv {
+
+constexpr int kH3Taps = 9;
+constexpr int kH3Row = 24;  // halo row stride in bf16 elements (48 B)
+
+// one 16-B-per-lane LDS-DMA piece: lane l fills lds + 16 l (device-only helper)
+__device__ __forceinline__ void h3_dma16(__amdgpu_buffer_rsrc_t r, void* lds, uint32_t off) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)lds, 16, off, 0, 0, 0);
+}
+
+template <int BM>
+constexpr int h3_halo_rows_max() {  // BM/16 images of 4x4 -> 6x6 halo each, rounded up to 64 rows
+  return (BM / 16 * 36 + 63) / 64 * 64;                           // (whole 1-KiB LDS-DMA pieces)
+}
+
+template <int BM, int BN, int WM, int WN>
+constexpr size_t h3_stage_elems() { return (size_t)kH3Taps * BN * 16 + (size_t)h3_halo_rows_max<BM>() * kH3Row; }
+
+// DMA: the chunk's pieces move global -> LDS by LDS-DMA (buffer_load ... lds) issued at the top of
+// the previous chunk's MFMAs (no staging registers, no ds_write phase); otherwise register-staged.
+template <int BM, int BN, int EPI, int ACT, int WM, int WN, bool DMA>
+__global__ __launch_bounds__(64 * WM * WN, 1) void h3_kernel(const ConvArgs a) {
+  constexpr int NT = 64 * WM * WN;
+  constexpr int TN = BN / WN / 32, TM = BM / WM / 32;
+  static_assert(TN >= 1 && TM >= 1, "wave tile >= 32x32");
+  constexpr int WP = kH3Taps * BN * 2;         // weight 16-B pieces per chunk
+  constexpr int NWP = (WP + NT - 1) / NT;
+  constexpr int HRM = h3_halo_rows_max<BM>();
+  constexpr int NHP = (2 * HRM + NT - 1) / NT;  // halo 16-B pieces per thread (upper bound)
+  constexpr int NQ = EPI == kEpiJoinBwd ? 3 : 2;
+  constexpr int WTILE = kH3Taps * BN * 16;      // bf16 elements of the weight tile
+  constexpr int STAGE = (int)h3_stage_elems<BM, BN, WM, WN>();
+
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  float* red = reinterpret_cast<float*>(smem);              // [NT/64][NQ][BN]
+  int* ttab = reinterpret_cast<int*>(red + (NT / 64) * NQ * BN);  // [9]: wt | [9]: tap row offset
+  constexpr int HDR = (((NT / 64) * NQ * BN + 2 * kH3Taps) * 4 + 15) & ~15;
+  bf16* tiles = reinterpret_cast<bf16*>(smem + HDR);        // [2][STAGE]
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wn = wid % WN, wm = wid / WN;
+  const int rid = xcd_remap(blockIdx.x, a.nbm * a.nbn);
+  const int bn = rid % a.nbn, bm = rid / a.nbn;
+  const long m0 = (long)bm * BM;
+  const int n0 = bn * BN;
+  const float inv_alpha = ACT == kActCelu ? 1.f / a.epi_alpha : 1.f;
+
+  // ---- tile geometry: BM consecutive pixels = nbk blocks of Rb whole rows of one image each
+  const int W = a.Wi, H = a.Hi, W2 = W + 2, HW = H * W;
+  const int Rb = H < BM / W ? H : BM / W;
+  const int nbk = BM / (Rb * W), bhr = (Rb + 2) * W2, HR = nbk * bhr;
+  const int img0 = (int)(m0 / HW), h0 = (int)((m0 / W) % H);
+
+  if (tid < kH3Taps) {
+    ttab[tid] = a.wt[tid];
+    ttab[kH3Taps + tid] = a.dh[tid] * W2 + a.dw[tid];
+  }
+  __syncthreads();
+
+  const __amdgpu_buffer_rsrc_t rx_d = __builtin_amdgcn_make_buffer_rsrc((void*)a.x, (short)0,
+                                                                        (int)(a.Nb_HiWi_Cx_bytes), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rw_d = __builtin_amdgcn_make_buffer_rsrc((void*)a.w, (short)0, (int)(a.w_bytes),
+                                                                        0x00020000);
+
+  // ---- per-thread staging pieces (fixed across chunks: only the channel offset moves)
+  uint32_t woff[NWP], hoff[NHP];
+  int wdst[NWP], hdst[NHP];
+#pragma unroll
+  for (int j = 0; j < NWP; ++j) {
+    const int idx = tid + j * NT;
+    const bool v = idx < WP;
+    const int tap = v ? idx / (2 * BN) : 0;
+    const int rem = idx - tap * 2 * BN;
+    const int n = rem >> 1, lh = rem & 1;
+    woff[j] = v ? ((uint32_t)(n0 + n) * (uint32_t)a.ldw + (uint32_t)(ttab[tap] * a.Cx + 8 * lh)) * 2u : kOOB;
+    wdst[j] = v ? (tap * BN + n) * 16 + 8 * (lh ^ ((n >> 3) & 1)) : -1;
+  }
+#pragma unroll
+  for (int j = 0; j < NHP; ++j) {
+    const int idx = tid + j * NT;
+    const bool v = idx < 2 * HR;
+    const int q = idx >> 1, lh = idx & 1;
+    const int b = q / bhr, r2 = q - b * bhr;
+    const int hr = r2 / W2, hc = r2 - hr * W2;
+    const int h = h0 + hr - 1, w = hc - 1;
+    const bool in = v && (unsigned)h < (unsigned)H && (unsigned)w < (unsigned)W;
+    hoff[j] = in ? ((uint32_t)((img0 + b) * HW + h * W + w) * (uint32_t)a.Cx + 8u * lh) * 2u : kOOB;
+    hdst[j] = v ? WTILE + q * kH3Row + 8 * lh : -1;  // padding rows store the zeros the OOB load returned
+  }
+  // ---- per-thread B-fragment halo rows (tap (0, 0)) and the nine tap offsets
+  int qb[TM];
+#pragma unroll
+  for (int j = 0; j < TM; ++j) {
+    const int p = wm * (BM / WM) + j * 32 + (lane & 31);
+    const int b = p / (Rb * W), r = (p / W) % Rb, c = p % W;
+    qb[j] = b * bhr + (r + 1) * W2 + c + 1;
+  }
+  int toff[kH3Taps];
+#pragma unroll
+  for (int t = 0; t < kH3Taps; ++t) toff[t] = ttab[kH3Taps + t];
+  const int h = lane >> 5;
+  const int ahalf = 8 * (h ^ ((lane >> 3) & 1));  // A-fragment half (the weight tile's swizzle)
+
+  uint4 rw[NWP], rh[NHP];
+  auto gload = [&](int ch) {
+    const uint32_t cb = (uint32_t)ch * 32u;  // 16 channels * 2 B
+#pragma unroll
+    for (int j = 0; j < NWP; ++j) rw[j] = ld_buf16(rw_d, woff[j] == kOOB ? kOOB : woff[j] + cb);
+#pragma unroll
+    for (int j = 0; j < NHP; ++j) rh[j] = ld_buf16(rx_d, hoff[j] == kOOB ? kOOB : hoff[j] + cb);
+  };
+  auto lstore = [&](int buf) {
+    bf16* base = tiles + buf * STAGE;
+#pragma unroll
+    for (int j = 0; j < NWP; ++j)
+      if (wdst[j] >= 0) *reinterpret_cast<uint4*>(base + wdst[j]) = rw[j];
+#pragma unroll
+    for (int j = 0; j < NHP; ++j)
+      if (hdst[j] >= 0) *reinterpret_cast<uint4*>(base + hdst[j]) = rh[j];
+  };
+
+  f32x16 acc[TN][TM];
+#pragma unroll
+  for (int i = 0; i < TN; ++i)
+#pragma unroll
+    for (int j = 0; j < TM; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  auto compute = [&](int buf) {
+    const bf16* Wl = tiles + buf * STAGE;
+    const bf16* Hl = Wl + WTILE;
+#pragma unroll
+    for (int t = 0; t < kH3Taps; ++t) {
+      bf16x8_t wf[TN], xf[TM];
+#pragma unroll
+      for (int i = 0; i < TN; ++i) {
+        const int row = wn * (BN / WN) + i * 32 + (lane & 31);
+        wf[i] = *reinterpret_cast<const bf16x8_t*>(Wl + (t * BN + row) * 16 + ahalf);
+      }
+#pragma unroll
+      for (int j = 0; j < TM; ++j)
+        xf[j] = *reinterpret_cast<const bf16x8_t*>(Hl + (qb[j] + toff[t]) * kH3Row + 8 * h);
+#pragma unroll
+      for (int i = 0; i < TN; ++i)
+#pragma unroll
+        for (int j = 0; j < TM; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wf[i], xf[j], acc[i][j], 0, 0, 0);
+    }
+  };
+
+  const int nch = a.Cx >> 4;
+  if constexpr (DMA) {
+    // LDS image = piece-linear: weight piece (tap*BN + n)*2 + physical half at byte 16*piece;
+    // halo piece q*3 + part (part 2 = the row's pad slot) at WTILE*2 + 16*piece.  A wave
+    // instruction fills 64 consecutive pieces (1 KiB at the wave-uniform M0 base); WP is a
+    // multiple of 64 (every weight instruction full) and the halo region holds 3*HRM pieces, a
+    // multiple of 64, so a partly-valid last halo instruction's extra lanes land inside it
+    // (zeros from the OOB offset, rows nobody reads).
+    static_assert(WP % 64 == 0 && (3 * HRM) % 64 == 0, "whole 1-KiB DMA pieces");
+    constexpr int NWI = WP / 64, NHI = 3 * HRM / 64;  // wave-instructions per chunk
+    constexpr int NW = NT / 64;
+    const int wv = __builtin_amdgcn_readfirstlane(wid);
+    uint32_t wsrc[(NWI + NW - 1) / NW], hsrc[(NHI + NW - 1) / NW];
+#pragma unroll
+    for (int j = 0; j * NW < NWI; ++j) {
+      const int piece = (j * NW + wv) * 64 + lane;
+      const bool v = piece < WP;
+      const int tap = v ? piece / (2 * BN) : 0;
+      const int rem = piece - tap * 2 * BN;
+      const int n = rem >> 1, lh = (rem & 1) ^ ((n >> 3) & 1);
+      wsrc[j] = v ? ((uint32_t)(n0 + n) * (uint32_t)a.ldw + (uint32_t)(ttab[tap] * a.Cx + 8 * lh)) * 2u : kOOB;
+    }
+#pragma unroll
+    for (int j = 0; j * NW < NHI; ++j) {
+      const int piece = (j * NW + wv) * 64 + lane;
+      const int q = piece / 3, part = piece - q * 3;
+      const int b = q / bhr, r2 = q - b * bhr;
+      const int hr = r2 / W2, hc = r2 - hr * W2;
+      const int hh = h0 + hr - 1, w = hc - 1;
+      const bool in = q < HR && part < 2 && (unsigned)hh < (unsigned)H && (unsigned)w < (unsigned)W;
+      hsrc[j] = in ? ((uint32_t)((img0 + b) * HW + hh * W + w) * (uint32_t)a.Cx + 8u * part) * 2u : kOOB;
+    }
+    const int nhi = (3 * HR + 63) / 64;  // halo wave-instructions actually needed (uniform)
+    auto issue = [&](int ch, int buf) {
+      const uint32_t cb = (uint32_t)ch * 32u;
+      char* base = reinterpret_cast<char*>(tiles + buf * STAGE);
+#pragma unroll
+      for (int j = 0; j * NW < NWI; ++j) {
+        const int wi = j * NW + wv;
+        if (wi < NWI)
+          h3_dma16(rw_d, base + wi * 1024, wsrc[j] == kOOB ? kOOB : wsrc[j] + cb);
+      }
+#pragma unroll
+      for (int j = 0; j * NW < NHI; ++j) {
+        const int wi = j * NW + wv;
+        if (wi < nhi)
+          h3_dma16(rx_d, base + WTILE * 2 + wi * 1024, hsrc[j] == kOOB ? kOOB : hsrc[j] + cb);
+      }
+    };
+    issue(0, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    for (int c = 0; c < nch; ++c) {
+      // buffer (c+1)&1 was last read in chunk c-1: every wave retired those reads before the
+      // barrier that ended it
+      if (c + 1 < nch) issue(c + 1, (c + 1) & 1);
+      compute(c & 1);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMAs of chunk c+1 landed ...
+      __syncthreads();                                   // ... and everyone's: read in chunk c+1
+    }
+  } else {
+    gload(0);
+    lstore(0);
+    if (nch > 1) gload(1);
+    __syncthreads();
+    for (int c = 0; c < nch; ++c) {
+      compute(c & 1);
+      if (c + 1 < nch) {
+        lstore((c + 1) & 1);  // buffer (c+1)&1 was last read in chunk c-1, before the previous barrier
+        if (c + 2 < nch) gload(c + 2);
+      }
+      __syncthreads();
+    }
+  }
+
+  conv_epilogue<BM, BN, EPI, ACT, NT, WM, WN>(a, acc, m0, n0, bm, tid, reinterpret_cast<float*>(smem + HDR), red, true,
+                                              inv_alpha);
+}
+
+// host ------------------------------------------------------------------------------------
+template <int BM, int BN, int EPI, int ACT, int WM, int WN, bool DMA>
+static void h3_launch_one(const ConvArgs& a, hipStream_t st) {
+  constexpr int NT = 64 * WM * WN;
+  constexpr int NQ = EPI == kEpiJoinBwd ? 3 : 2;
+  constexpr size_t hdr = ((((size_t)(NT / 64) * NQ * BN + 2 * kH3Taps) * 4 + 15) & ~(size_t)15);
+  const size_t tiles = 2 * h3_stage_elems<BM, BN, WM, WN>() * 2, stage = (size_t)WM * 32 * (BN + 4) * 4;
+  const size_t lds = hdr + (tiles > stage ? tiles : stage);
+  auto kern = h3_kernel<BM, BN, EPI, ACT, WM, WN, DMA>;
+  static bool attr = false;
+  if (!attr) {
+    FDT_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                      (int)lds));
+    attr = true;
+  }
+  hipLaunchKernelGGL(kern, dim3(a.nbm * a.nbn), dim3(NT), lds, st, a);
+  FDT_LAUNCH_CHECK();
+}
+
+// Geometry the halo loop admits (checked on the host before any launch)
+bool h3_supported(const ConvArgs& a, int BM) {
+  if (a.ntaps != kH3Taps || a.S != 1 || a.Hi != a.Ho || a.Wi != a.Wo || a.OS != 1 || a.oy != 0 || a.ox != 0 ||
+      a.Hout != a.Ho || a.Wout != a.Wo || a.nsplit != 1 || (a.Cx & 15) != 0)
+    return false;
+  for (int t = 0; t < kH3Taps; ++t)
+    if (a.dh[t] < -1 || a.dh[t] > 1 || a.dw[t] < -1 || a.dw[t] > 1 || a.wt[t] < 0 || a.wt[t] >= kH3Taps) return false;
+  const int W = a.Wi, H = a.Hi;
+  if (W < 4 || (W & (W - 1)) != 0 || BM % W != 0 || a.M % BM != 0) return false;
+  const int Rb = H < BM / W ? H : BM / W;
+  if (Rb < H ? (H % Rb != 0) : (BM % (H * W) != 0)) return false;
+  const int nbk = BM / (Rb * W);
+  return nbk * (Rb + 2) * (W + 2) <= BM / 16 * 36;
+}
+
+bool launch_h3(int pro, int epi, int act, const ConvArgs& a, int BM, int BN, bool dma, hipStream_t st) {
+  if (pro != kProNone) return false;
+  FDT_CHECK(h3_supported(a, BM), "halo 3x3 conv: unsupported geometry");
+  FDT_CHECK(a.Cout % BN == 0, "halo 3x3 conv: Cout % BN");
+#define FDT_H3E(BM_, BN_, WM_, WN_, D_)                                                                       \
+  if (epi == kEpiStats && act == kActNone) { h3_launch_one<BM_, BN_, kEpiStats, kActNone, WM_, WN_, D_>(a, st); return true; } \
+  if (epi == kEpiActBwd && act == kActRelu) { h3_launch_one<BM_, BN_, kEpiActBwd, kActRelu, WM_, WN_, D_>(a, st); return true; } \
+  if (epi == kEpiActBwd && act == kActCelu) { h3_launch_one<BM_, BN_, kEpiActBwd, kActCelu, WM_, WN_, D_>(a, st); return true; } \
+  if (epi == kEpiStore && act == kActNone) { h3_launch_one<BM_, BN_, kEpiStore, kActNone, WM_, WN_, D_>(a, st); return true; }
+#define FDT_H3(BM_, BN_, WM_, WN_)            \
+  if (BM == BM_ && BN == BN_) {               \
+    if (dma) { FDT_H3E(BM_, BN_, WM_, WN_, true) } \
+    else { FDT_H3E(BM_, BN_, WM_, WN_, false) }    \
+    return false;                             \
+  }
+  FDT_H3(256, 128, 4, 2)
+  FDT_H3(256, 64, 8, 1)
+  FDT_H3(128, 128, 2, 2)
+#undef FDT_H3
+#undef FDT_H3E
+  return false;
+}
+
+}  // namespace conv
+}  // namespace fdt

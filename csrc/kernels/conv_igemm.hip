@@ -14,7 +14,8 @@ static void conv_igemm_impl(uint64_t x, uint64_t x2, uint64_t ps, uint64_t pt, u
                             int ldw, int Hout, int Wout, int OS, int oy, int ox, int pro, int pro_act, float pro_alpha,
                             int epi, int epi_act, float epi_alpha, int BM, int BN, int BK, int nsplit, uint64_t slab,
                             uint64_t cnt, uint64_t pt2, uint64_t pout, uint64_t pmask, int kg, uint64_t stream,
-                            const LazyStats& ls1 = LazyStats{}, const LazyStats& ls2 = LazyStats{}) {
+                            const LazyStats& ls1 = LazyStats{}, const LazyStats& ls2 = LazyStats{},
+                            const std::vector<uint64_t>& jz = {}) {
   using namespace conv;
   ConvArgs a{};
   a.ls1 = ls1;
@@ -43,8 +44,15 @@ static void conv_igemm_impl(uint64_t x, uint64_t x2, uint64_t ps, uint64_t pt, u
   a.jmask = P<const uint8_t>(jmask);
   a.jyb = P<const bf16>(jyb);
   a.jout = P<const bf16>(jout);
+  FDT_CHECK(jz.empty() || (jz.size() == 3 && epi == kEpiJoinBwd), "jz = [] | [sb, tb, xid] (join backward z mode)");
+  a.jsb = jz.empty() ? nullptr : P<const float>(jz[0]);
+  a.jtb = jz.empty() ? nullptr : P<const float>(jz[1]);
+  a.jx = jz.empty() ? nullptr : P<const bf16>(jz[2]);
   if (epi == kEpiJoinBwd) {
-    FDT_CHECK(ex != 0 && part != 0 && (jmask != 0 || jout != 0), "join backward needs y_res, slots and mask|out");
+    const bool zm = es != 0;  // z mode: es / et = the residual branch's (s, t)
+    FDT_CHECK(!zm || (epi_act == kActCelu && et != 0 && jz.size() == 3 && (jyb ? (jz[0] && jz[1]) : jz[2] != 0)),
+              "join backward z mode (CELU): es, et and jz = [sb, tb] (BN'd shortcut) | [.., .., xid] (identity)");
+    FDT_CHECK(ex != 0 && part != 0 && (jmask != 0 || jout != 0 || zm), "join backward needs y_res, slots and mask|out|z");
     FDT_CHECK(S == 1 && OS == 1 && Hout == Ho && Wout == Wo, "join backward needs a dense (stride-1) dgrad");
   }
   FDT_CHECK(Cx >= 8 && (Cx & (Cx - 1)) == 0, "Cx must be a power of two >= 8");
@@ -90,6 +98,11 @@ static void conv_igemm_impl(uint64_t x, uint64_t x2, uint64_t ps, uint64_t pt, u
   hipStream_t st = as_stream(stream);
   if (a.M == 0) return;
   const int act = (pro == kProAffineAct || pro == kProJoin) ? pro_act : ((epi == kEpiActBwd || epi == kEpiJoinBwd) ? epi_act : 0);
+  if (kg == 5 || kg == 6) {  // halo-staged 3x3 stride-1 loop (conv_h3.hip): prologue-free operands, no split-K
+    FDT_CHECK(pro == kProNone && a.nsplit == 1, "kg 5/6 (halo 3x3): prologue-free, nsplit 1");
+    FDT_CHECK(launch_h3(pro, epi, act, a, BM, BN, kg == 6, st), "kg 5/6 (halo 3x3): unsupported tile / epilogue");
+    return;
+  }
   if (kg == 2 && a.nsplit > 1) kg = 1;  // K groups and split-K are alternatives (kg 4: rotated loop, any split)
   if (kg == 3 && pro != kProNone) kg = 1;  // the LDS-DMA ring cannot apply a prologue
   if (launch_cases_fwd(pro, epi, act, a, BM, BN, BK, kg, pure, st) ||
@@ -107,11 +120,12 @@ void conv_igemm(uint64_t x, uint64_t x2, uint64_t ps, uint64_t pt, uint64_t pg, 
                 const std::vector<int>& dh, const std::vector<int>& dw, const std::vector<int>& wt, int Cout, int ldw,
                 int Hout, int Wout, int OS, int oy, int ox, int pro, int pro_act, float pro_alpha, int epi, int epi_act,
                 float epi_alpha, int BM, int BN, int BK, int nsplit, uint64_t slab, uint64_t cnt, int kg,
-                uint64_t stream, const std::vector<uint64_t>& lz_ptr, const std::vector<double>& lz_val) {
+                uint64_t stream, const std::vector<uint64_t>& lz_ptr, const std::vector<double>& lz_val,
+                const std::vector<uint64_t>& jz) {
   FDT_CHECK(pro != conv::kProJoin, "the join prologue goes through conv_igemm_join");
   conv_igemm_impl(x, x2, ps, pt, pg, w, out, part, part_rows, ex, es, et, jmask, jyb, jout, Nb, Hi, Wi, Cx, Ho, Wo, S, dh,
                   dw, wt, Cout, ldw, Hout, Wout, OS, oy, ox, pro, pro_act, pro_alpha, epi, epi_act, epi_alpha, BM, BN, BK,
-                  nsplit, slab, cnt, 0, 0, 0, kg, stream, make_lazy(lz_ptr, lz_val));
+                  nsplit, slab, cnt, 0, 0, 0, kg, stream, make_lazy(lz_ptr, lz_val), LazyStats{}, jz);
 }
 
 // Forward 1x1 convolution whose operand is the previous residual block's join (PRO_JOIN):

@@ -108,7 +108,15 @@ struct ConvArgs {
   const float* et;   // ACTBWD: producer shift t [Cout]
   const uint8_t* jmask;  // JOINBWD: ReLU join bit mask (bit i of byte e/8 = out[e] > 0), or nullptr
   const bf16* jyb;       // JOINBWD: shortcut-branch y (nullptr: identity shortcut)
-  const bf16* jout;      // JOINBWD: join output (CELU joins; read when jmask is nullptr)
+  const bf16* jout;      // JOINBWD: join output (CELU joins, legacy o-mode; read when jmask and es are nullptr)
+  // JOINBWD z mode (es / et = the residual branch's BN affine (s, t) set; CELU joins): act'(z) =
+  // exp(z/alpha) from the recomputed fp32 pre-activation z = ya*s + t + (jyb ? jyb*jsb + jtb : jx),
+  // exactly as the forward join formed it.  (From the bf16 output o, 1 + o/alpha is off by up to
+  // ~2^-11/alpha = 6.5e-3 -- against a true derivative below 0.02 for z < -0.3 -- and o(z -> -inf)
+  // rounds to -0.07520 < -alpha: a sign-flipped derivative for every deeply negative z.)
+  const float* jsb;      // shortcut BN scale / shift (jyb set)
+  const float* jtb;
+  const bf16* jx;        // identity shortcut operand (the block input; jyb nullptr)
   const float* fbias;    // GELU_FWD: per-column bias [Cout]
   bf16* out2;            // GELU_FWD: h = dropout(gelu(a)) [M][Cout]   (GELU_BWD: a is `ex`)
   float* gb;             // GELU_BWD: bias-gradient accumulator [Cout] (fp32 atomics)
@@ -227,6 +235,248 @@ template <int BM, int BN, int BK, int PRO, bool PURE>
 constexpr int kMinWavesPerEU =
     (BM == 128 && BN == 128 && BK == 32 && (PRO == kProNone || (PRO == kProAffineAct && PURE))) ? 4
     : (BM == 128 && BN == 128 && (BK == 32 || (PRO != 2 && PRO != 3))) ? 3 : 1;
+
+// ------------------------------------------------------------------ epilogue
+// The accumulators are transposed through LDS before touching memory: a lane's MFMA
+// result is 8 channels of ONE pixel, so a direct store / load covers 32 pixels x 32 B per
+// wave instruction (32 partial cache lines).  Staged as fp32 rows [WM x 32 pixels][BN] (one
+// pass per 32-pixel block j of every M-wave), each thread then owns 8 channels of whole rows and
+// every wave instruction moves full contiguous 128-256 B row segments; per-channel statistics
+// reduce over a thread's rows, then across the lanes sharing its channels (shuffles),
+// then across the waves in LDS.  Rows padded by 4 floats: conflict-free ds_write_b128
+// of the accumulator layout and ds_read_b128 of the row layout.
+// Wave layout WM x WN (wave w: wm = w / WN along the pixels, wn = w % WN along the channels),
+// NT threads; stg: >= WM*32*(BN+4) floats of LDS; red: [NT/64][NQ][BN] floats of LDS.
+// ew: this thread owns the epilogue (K group 1 of a KG = 2 launch only meets the barriers).
+template <int BM, int BN, int EPI, int ACT, int NT, int WM, int WN>
+__device__ __forceinline__ void conv_epilogue(const ConvArgs& a, f32x16 (&acc)[BN / WN / 32][BM / WM / 32], long m0,
+                                              int n0, int bm, int tid, float* stg, float* red, bool ew,
+                                              float inv_alpha) {
+  constexpr int TN = BN / WN / 32, TM = BM / WM / 32;
+  constexpr int NQ = EPI == kEpiJoinBwd ? 3 : 2;
+  constexpr int SW = BN + 4;     // staged row stride (floats)
+  constexpr int CG = BN / 8;     // 8-channel groups per row
+  constexpr int RPS = NT / CG;       // rows per sweep
+  constexpr int NSW = WM * 32 / RPS;  // sweeps per (WM x 32)-row pass
+  static_assert(NSW >= 1 && NSW * RPS == WM * 32, "epilogue sweep geometry");
+  constexpr int NW = NT / 64;
+  const int lane = tid & 63, wid = tid >> 6, wn = wid % WN, wm = wid / WN;
+  constexpr bool STATS = EPI == kEpiStats || EPI == kEpiActBwd || EPI == kEpiJoinBwd;
+  const int h = lane >> 5;
+  const __amdgpu_buffer_rsrc_t ro = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)a.out, (short)0, (int)0xFFFFFFFF, 0x00020000);
+  const int cg = tid % CG, rs = tid / CG;
+  const int c = n0 + cg * 8;  // this thread's 8 output channels
+  const bool dense = a.OS == 1 && a.oy == 0 && a.ox == 0 && a.Hout == a.Ho && a.Wout == a.Wo;
+  float sv[8], tv[8];
+  constexpr bool GELU = EPI == kEpiGeluFwd || EPI == kEpiGeluBwd;
+  uint64_t dseed = 0;
+  if constexpr (GELU) dseed = drop::live_seed(a.drop_seed, a.drop_seed_ptr);
+  if constexpr (EPI == kEpiGeluFwd) {
+    const float4* bp = reinterpret_cast<const float4*>(a.fbias + c);
+    const float4 b0 = bp[0], b1 = bp[1];
+    sv[0] = b0.x; sv[1] = b0.y; sv[2] = b0.z; sv[3] = b0.w; sv[4] = b1.x; sv[5] = b1.y; sv[6] = b1.z; sv[7] = b1.w;
+  }
+  float sbv[8], tbv[8];
+  const bool zm = EPI == kEpiJoinBwd && ACT == kActCelu && a.es != nullptr;
+  if (EPI == kEpiActBwd || zm) {
+    const float4* sp = reinterpret_cast<const float4*>(a.es + c);
+    const float4* tp = reinterpret_cast<const float4*>(a.et + c);
+    const float4 s0 = sp[0], s1 = sp[1], t0 = tp[0], t1 = tp[1];
+    sv[0] = s0.x; sv[1] = s0.y; sv[2] = s0.z; sv[3] = s0.w; sv[4] = s1.x; sv[5] = s1.y; sv[6] = s1.z; sv[7] = s1.w;
+    tv[0] = t0.x; tv[1] = t0.y; tv[2] = t0.z; tv[3] = t0.w; tv[4] = t1.x; tv[5] = t1.y; tv[6] = t1.z; tv[7] = t1.w;
+  }
+  if (zm && a.jyb != nullptr) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) { sbv[k] = a.jsb[c + k]; tbv[k] = a.jtb[c + k]; }
+  }
+  float q0[8], q1[8], q2[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) { q0[k] = 0.f; q1[k] = 0.f; q2[k] = 0.f; }
+  __syncthreads();  // every wave is done with the K tiles (and the split-K flag)
+#pragma unroll
+  for (int j = 0; j < TM; ++j) {
+    // ---- stage accumulator block j: local row = wm*32 + pixel, 8 channels per (i, p)
+#pragma unroll
+    for (int i = 0; i < TN; ++i) {
+      if (!ew) break;
+#pragma unroll
+      for (int p = 0; p < 2; ++p) {
+        const int g = 2 * p;
+        float v[8];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          float lo = acc[i][j][4 * g + q], hi = acc[i][j][4 * g + 4 + q];
+          swap32(lo, hi);
+          v[q] = lo;
+          v[4 + q] = hi;
+        }
+        float* dst = stg + (wm * 32 + (lane & 31)) * SW + wn * (BN / WN) + i * 32 + 16 * p + 8 * h;
+        *reinterpret_cast<float4*>(dst) = make_float4(v[0], v[1], v[2], v[3]);
+        *reinterpret_cast<float4*>(dst + 4) = make_float4(v[4], v[5], v[6], v[7]);
+      }
+    }
+    __syncthreads();
+    // ---- rows of this pass: 8 channels x NSW rows per thread
+#pragma unroll
+    for (int sw = 0; sw < NSW; ++sw) {
+      const int lr = rs + sw * RPS;
+      const long m = m0 + (lr >> 5) * (BM / WM) + j * 32 + (lr & 31);
+      if (ew && m < a.M) {
+        uint32_t orow;
+        if (dense) {
+          orow = (uint32_t)m;
+        } else {
+          const int mi = (int)m, hw = a.Ho * a.Wo;
+          const int n = mi / hw, rem = mi - n * hw;
+          const int oh = rem / a.Wo, ow = rem - oh * a.Wo;
+          orow = (uint32_t)((n * a.Hout + oh * a.OS + a.oy) * a.Wout + ow * a.OS + a.ox);
+        }
+        const uint32_t e = orow * (uint32_t)a.Cout + c;
+        const float4 va = *reinterpret_cast<const float4*>(stg + lr * SW + cg * 8);
+        const float4 vb = *reinterpret_cast<const float4*>(stg + lr * SW + cg * 8 + 4);
+        float v[8] = {va.x, va.y, va.z, va.w, vb.x, vb.y, vb.z, vb.w};
+        if constexpr (EPI == kEpiStats) {
+#pragma unroll
+          for (int k = 0; k < 8; ++k) { q0[k] += v[k]; q1[k] = fmaf(v[k], v[k], q1[k]); }
+          st_out(ro, e * 2u, a.out + e, v, a.wthru);
+        } else if constexpr (EPI == kEpiActBwd) {
+          float x8[8];
+          Vec8<bf16>::load(a.ex + e, x8);
+#pragma unroll
+          for (int k = 0; k < 8; ++k) {
+            const float gp = v[k] * actg<ACT>(fmaf(x8[k], sv[k], tv[k]), inv_alpha);
+            v[k] = gp * sv[k];
+            q0[k] = fmaf(gp, x8[k], q0[k]);
+            q1[k] += gp;
+          }
+          st_out(ro, e * 2u, a.out + e, v, a.wthru);
+        } else if constexpr (EPI == kEpiJoinBwd) {
+          float e8[8], ya[8], yb[8], o8[8];
+          Vec8<bf16>::load(a.out + e, e8);
+          Vec8<bf16>::load(a.ex + e, ya);
+          const bool hb = a.jyb != nullptr;
+          if (hb) Vec8<bf16>::load(a.jyb + e, yb);
+          uint32_t mk = 0;
+          if constexpr (ACT == kActRelu) mk = a.jmask[e >> 3];
+          else if (!zm) Vec8<bf16>::load(a.jout + e, o8);
+          else if (!hb) Vec8<bf16>::load(a.jx + e, o8);
+#pragma unroll
+          for (int k = 0; k < 8; ++k) {
+            const float gv = v[k] + e8[k];
+            float gp;
+            if constexpr (ACT == kActRelu) {
+              gp = ((mk >> k) & 1u) ? gv : 0.f;
+            } else if (zm) {
+              const float z = fmaf(ya[k], sv[k], tv[k]) + (hb ? fmaf(yb[k], sbv[k], tbv[k]) : o8[k]);
+              gp = gv * actg<ACT>(z, inv_alpha);
+            } else {
+              gp = gv * actg_out<ACT>(o8[k], inv_alpha);
+            }
+            v[k] = gp;
+            q0[k] = fmaf(gp, ya[k], q0[k]);
+            q1[k] += gp;
+            if (hb) q2[k] = fmaf(gp, yb[k], q2[k]);
+          }
+          st_out(ro, e * 2u, a.out + e, v, a.wthru);
+        } else if constexpr (EPI == kEpiAdd) {
+          float e8[8];
+          Vec8<bf16>::load(a.out + e, e8);
+#pragma unroll
+          for (int k = 0; k < 8; ++k) v[k] += e8[k];
+          st_out(ro, e * 2u, a.out + e, v, a.wthru);
+        } else if constexpr (EPI == kEpiGeluFwd) {
+          // a = acc + bias, rounded to bf16 as stored (the backward reads the stored a);
+          // h from the rounded a, exactly as the standalone GELU-dropout pass computes it
+          uint32_t pa[4];
+#pragma unroll
+          for (int q = 0; q < 4; ++q) pa[q] = pk_bf16(v[2 * q] + sv[2 * q], v[2 * q + 1] + sv[2 * q + 1]);
+          *reinterpret_cast<uint4*>(a.out + e) = make_uint4(pa[0], pa[1], pa[2], pa[3]);
+          const uint32_t mk = a.drop_thr ? drop::keep8((long)(e >> 3), dseed, a.drop_thr) : 0xffu;
+          float h[8];
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            h[2 * q] = bf16_lo(pa[q]);
+            h[2 * q + 1] = bf16_hi(pa[q]);
+          }
+#pragma unroll
+          for (int k = 0; k < 8; ++k) h[k] = ((mk >> k) & 1u) ? drop::gelu_erf(h[k]) * a.drop_scale : 0.f;
+          Vec8<bf16>::store(a.out2 + e, h);
+        } else if constexpr (EPI == kEpiGeluBwd) {
+          // ga = keep * scale * gelu'(a) * dL/dh; the bias gradient sums the stored ga
+          float a8[8];
+          Vec8<bf16>::load(a.ex + e, a8);
+          const uint32_t mk = a.drop_thr ? drop::keep8((long)(e >> 3), dseed, a.drop_thr) : 0xffu;
+          uint32_t pg[4];
+#pragma unroll
+          for (int k = 0; k < 8; ++k)
+            v[k] = ((mk >> k) & 1u) ? v[k] * a.drop_scale * drop::gelu_erf_grad(a8[k]) : 0.f;
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            pg[q] = pk_bf16(v[2 * q], v[2 * q + 1]);
+            q0[2 * q] += bf16_lo(pg[q]);
+            q0[2 * q + 1] += bf16_hi(pg[q]);
+          }
+          *reinterpret_cast<uint4*>(a.out + e) = make_uint4(pg[0], pg[1], pg[2], pg[3]);
+        } else {
+          st_out(ro, e * 2u, a.out + e, v, a.wthru);
+        }
+      }
+    }
+    if (j + 1 < TM) __syncthreads();  // the next pass overwrites the staging rows
+  }
+  if constexpr (EPI == kEpiGeluBwd) {
+    // column sums of ga: rows of a thread -> lanes sharing its columns -> 4 waves -> one
+    // fp32 atomic per column per workgroup into the bias gradient
+#pragma unroll
+    for (int o = CG; o < 64; o <<= 1) {
+      if (!ew) break;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) q0[k] += __shfl_xor(q0[k], o, 64);
+    }
+    if (ew && lane < CG) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) red[wid * BN + cg * 8 + k] = q0[k];
+    }
+    __syncthreads();
+    for (int e = tid; ew && e < BN; e += NT) {
+      float t = 0.f;
+#pragma unroll
+      for (int w = 0; w < NW; ++w) t += red[w * BN + e];
+      atomicAdd(&a.gb[n0 + e], t);
+    }
+  }
+  if constexpr (STATS) {
+    // lanes l, l + CG, l + 2CG, ... of a wave hold the same channels
+#pragma unroll
+    for (int o = CG; o < 64; o <<= 1) {
+      if (!ew) break;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        q0[k] += __shfl_xor(q0[k], o, 64);
+        q1[k] += __shfl_xor(q1[k], o, 64);
+        if constexpr (NQ == 3) q2[k] += __shfl_xor(q2[k], o, 64);
+      }
+    }
+    if (ew && lane < CG) {
+      float* rw = red + wid * NQ * BN + cg * 8;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        rw[k] = q0[k];
+        rw[BN + k] = q1[k];
+        if constexpr (NQ == 3) rw[2 * BN + k] = q2[k];
+      }
+    }
+    __syncthreads();
+    for (int e = tid; ew && e < NQ * BN; e += NT) {
+      float t = 0.f;
+#pragma unroll
+      for (int w = 0; w < NW; ++w) t += red[w * NQ * BN + e];
+      const int q = e / BN, cc2 = e - q * BN;
+      if (!(a.dbg & 1)) atomicAdd(&a.part[((long)(bm & a.slot_mask) * NQ + q) * a.Cout + n0 + cc2], t);
+    }
+  }
+}
 
 // KG: 1 = one 4-wave K group, register-staged (legacy K loop, see the main loop); 4 = the same with
 // the rotated K loop (a true 2-deep register prefetch); 2 = two K groups (see above);
@@ -742,220 +992,8 @@ igemm_kernel(const ConvArgs a) {
     }
   }
 
-  // ------------------------------------------------------------------ epilogue
-  // The accumulators are transposed through LDS before touching memory: a lane's MFMA
-  // result is 8 channels of ONE pixel, so a direct store / load covers 32 pixels x 32 B per
-  // wave instruction (32 partial cache lines).  Staged as fp32 rows [64 pixels][BN] (one
-  // pass per 32-pixel block j), each thread then owns 8 channels of whole rows and every
-  // wave instruction moves full contiguous 128-256 B row segments; per-channel statistics
-  // reduce over a thread's rows, then across the lanes sharing its channels (shuffles),
-  // then across the 4 waves in LDS.  Rows padded by 4 floats: conflict-free ds_write_b128
-  // of the accumulator layout and ds_read_b128 of the row layout.
-  {
-    constexpr int SW = BN + 4;     // staged row stride (floats)
-    constexpr int CG = BN / 8;     // 8-channel groups per row
-    constexpr int RPS = 256 / CG;  // rows per sweep
-    constexpr int NSW = 64 / RPS;  // sweeps per 64-row pass
-    constexpr bool STATS = EPI == kEpiStats || EPI == kEpiActBwd || EPI == kEpiJoinBwd;
-    const int h = lane >> 5;
-    float* stg = reinterpret_cast<float*>(smem + hdr);
-    const __amdgpu_buffer_rsrc_t ro = __builtin_amdgcn_make_buffer_rsrc(
-        (void*)a.out, (short)0, (int)0xFFFFFFFF, 0x00020000);
-    const int cg = tid % CG, rs = tid / CG;
-    const int c = n0 + cg * 8;  // this thread's 8 output channels
-    const bool dense = a.OS == 1 && a.oy == 0 && a.ox == 0 && a.Hout == a.Ho && a.Wout == a.Wo;
-    float sv[8], tv[8];
-    constexpr bool GELU = EPI == kEpiGeluFwd || EPI == kEpiGeluBwd;
-    uint64_t dseed = 0;
-    if constexpr (GELU) dseed = drop::live_seed(a.drop_seed, a.drop_seed_ptr);
-    if constexpr (EPI == kEpiGeluFwd) {
-      const float4* bp = reinterpret_cast<const float4*>(a.fbias + c);
-      const float4 b0 = bp[0], b1 = bp[1];
-      sv[0] = b0.x; sv[1] = b0.y; sv[2] = b0.z; sv[3] = b0.w; sv[4] = b1.x; sv[5] = b1.y; sv[6] = b1.z; sv[7] = b1.w;
-    }
-    if constexpr (EPI == kEpiActBwd) {
-      const float4* sp = reinterpret_cast<const float4*>(a.es + c);
-      const float4* tp = reinterpret_cast<const float4*>(a.et + c);
-      const float4 s0 = sp[0], s1 = sp[1], t0 = tp[0], t1 = tp[1];
-      sv[0] = s0.x; sv[1] = s0.y; sv[2] = s0.z; sv[3] = s0.w; sv[4] = s1.x; sv[5] = s1.y; sv[6] = s1.z; sv[7] = s1.w;
-      tv[0] = t0.x; tv[1] = t0.y; tv[2] = t0.z; tv[3] = t0.w; tv[4] = t1.x; tv[5] = t1.y; tv[6] = t1.z; tv[7] = t1.w;
-    }
-    float q0[8], q1[8], q2[8];
-#pragma unroll
-    for (int k = 0; k < 8; ++k) { q0[k] = 0.f; q1[k] = 0.f; q2[k] = 0.f; }
-    // K group 1 (KG == 2) only meets the barriers below; group 0 owns the whole epilogue
-    const bool ew = grp == 0;
-    __syncthreads();  // every wave is done with the K tiles (and the split-K flag)
-#pragma unroll
-    for (int j = 0; j < TM; ++j) {
-      // ---- stage accumulator block j: local row = wm*32 + pixel, 8 channels per (i, p)
-#pragma unroll
-      for (int i = 0; i < TN; ++i) {
-        if (!ew) break;
-#pragma unroll
-        for (int p = 0; p < 2; ++p) {
-          const int g = 2 * p;
-          float v[8];
-#pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            float lo = acc[i][j][4 * g + q], hi = acc[i][j][4 * g + 4 + q];
-            swap32(lo, hi);
-            v[q] = lo;
-            v[4 + q] = hi;
-          }
-          float* dst = stg + (wm * 32 + (lane & 31)) * SW + wn * (BN / 2) + i * 32 + 16 * p + 8 * h;
-          *reinterpret_cast<float4*>(dst) = make_float4(v[0], v[1], v[2], v[3]);
-          *reinterpret_cast<float4*>(dst + 4) = make_float4(v[4], v[5], v[6], v[7]);
-        }
-      }
-      __syncthreads();
-      // ---- rows of this pass: 8 channels x NSW rows per thread
-#pragma unroll
-      for (int sw = 0; sw < NSW; ++sw) {
-        const int lr = rs + sw * RPS;
-        const long m = m0 + (lr >> 5) * (BM / 2) + j * 32 + (lr & 31);
-        if (ew && m < a.M) {
-          uint32_t orow;
-          if (dense) {
-            orow = (uint32_t)m;
-          } else {
-            const int mi = (int)m, hw = a.Ho * a.Wo;
-            const int n = mi / hw, rem = mi - n * hw;
-            const int oh = rem / a.Wo, ow = rem - oh * a.Wo;
-            orow = (uint32_t)((n * a.Hout + oh * a.OS + a.oy) * a.Wout + ow * a.OS + a.ox);
-          }
-          const uint32_t e = orow * (uint32_t)a.Cout + c;
-          const float4 va = *reinterpret_cast<const float4*>(stg + lr * SW + cg * 8);
-          const float4 vb = *reinterpret_cast<const float4*>(stg + lr * SW + cg * 8 + 4);
-          float v[8] = {va.x, va.y, va.z, va.w, vb.x, vb.y, vb.z, vb.w};
-          if constexpr (EPI == kEpiStats) {
-#pragma unroll
-            for (int k = 0; k < 8; ++k) { q0[k] += v[k]; q1[k] = fmaf(v[k], v[k], q1[k]); }
-            st_out(ro, e * 2u, a.out + e, v, a.wthru);
-          } else if constexpr (EPI == kEpiActBwd) {
-            float x8[8];
-            Vec8<bf16>::load(a.ex + e, x8);
-#pragma unroll
-            for (int k = 0; k < 8; ++k) {
-              const float gp = v[k] * actg<ACT>(fmaf(x8[k], sv[k], tv[k]), inv_alpha);
-              v[k] = gp * sv[k];
-              q0[k] = fmaf(gp, x8[k], q0[k]);
-              q1[k] += gp;
-            }
-            st_out(ro, e * 2u, a.out + e, v, a.wthru);
-          } else if constexpr (EPI == kEpiJoinBwd) {
-            float e8[8], ya[8], yb[8], o8[8];
-            Vec8<bf16>::load(a.out + e, e8);
-            Vec8<bf16>::load(a.ex + e, ya);
-            const bool hb = a.jyb != nullptr;
-            if (hb) Vec8<bf16>::load(a.jyb + e, yb);
-            uint32_t mk = 0;
-            if constexpr (ACT == kActRelu) mk = a.jmask[e >> 3];
-            else Vec8<bf16>::load(a.jout + e, o8);
-#pragma unroll
-            for (int k = 0; k < 8; ++k) {
-              const float gv = v[k] + e8[k];
-              float gp;
-              if constexpr (ACT == kActRelu) gp = ((mk >> k) & 1u) ? gv : 0.f;
-              else gp = gv * actg_out<ACT>(o8[k], inv_alpha);
-              v[k] = gp;
-              q0[k] = fmaf(gp, ya[k], q0[k]);
-              q1[k] += gp;
-              if (hb) q2[k] = fmaf(gp, yb[k], q2[k]);
-            }
-            st_out(ro, e * 2u, a.out + e, v, a.wthru);
-          } else if constexpr (EPI == kEpiAdd) {
-            float e8[8];
-            Vec8<bf16>::load(a.out + e, e8);
-#pragma unroll
-            for (int k = 0; k < 8; ++k) v[k] += e8[k];
-            st_out(ro, e * 2u, a.out + e, v, a.wthru);
-          } else if constexpr (EPI == kEpiGeluFwd) {
-            // a = acc + bias, rounded to bf16 as stored (the backward reads the stored a);
-            // h from the rounded a, exactly as the standalone GELU-dropout pass computes it
-            uint32_t pa[4];
-#pragma unroll
-            for (int q = 0; q < 4; ++q) pa[q] = pk_bf16(v[2 * q] + sv[2 * q], v[2 * q + 1] + sv[2 * q + 1]);
-            *reinterpret_cast<uint4*>(a.out + e) = make_uint4(pa[0], pa[1], pa[2], pa[3]);
-            const uint32_t mk = a.drop_thr ? drop::keep8((long)(e >> 3), dseed, a.drop_thr) : 0xffu;
-            float h[8];
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-              h[2 * q] = bf16_lo(pa[q]);
-              h[2 * q + 1] = bf16_hi(pa[q]);
-            }
-#pragma unroll
-            for (int k = 0; k < 8; ++k) h[k] = ((mk >> k) & 1u) ? drop::gelu_erf(h[k]) * a.drop_scale : 0.f;
-            Vec8<bf16>::store(a.out2 + e, h);
-          } else if constexpr (EPI == kEpiGeluBwd) {
-            // ga = keep * scale * gelu'(a) * dL/dh; the bias gradient sums the stored ga
-            float a8[8];
-            Vec8<bf16>::load(a.ex + e, a8);
-            const uint32_t mk = a.drop_thr ? drop::keep8((long)(e >> 3), dseed, a.drop_thr) : 0xffu;
-            uint32_t pg[4];
-#pragma unroll
-            for (int k = 0; k < 8; ++k)
-              v[k] = ((mk >> k) & 1u) ? v[k] * a.drop_scale * drop::gelu_erf_grad(a8[k]) : 0.f;
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-              pg[q] = pk_bf16(v[2 * q], v[2 * q + 1]);
-              q0[2 * q] += bf16_lo(pg[q]);
-              q0[2 * q + 1] += bf16_hi(pg[q]);
-            }
-            *reinterpret_cast<uint4*>(a.out + e) = make_uint4(pg[0], pg[1], pg[2], pg[3]);
-          } else {
-            st_out(ro, e * 2u, a.out + e, v, a.wthru);
-          }
-        }
-      }
-      if (j + 1 < TM) __syncthreads();  // the next pass overwrites the staging rows
-    }
-    if constexpr (EPI == kEpiGeluBwd) {
-      // column sums of ga: rows of a thread -> lanes sharing its columns -> 4 waves -> one
-      // fp32 atomic per column per workgroup into the bias gradient
-#pragma unroll
-      for (int o = CG; o < 64; o <<= 1) {
-        if (!ew) break;
-#pragma unroll
-        for (int k = 0; k < 8; ++k) q0[k] += __shfl_xor(q0[k], o, 64);
-      }
-      if (ew && lane < CG) {
-#pragma unroll
-        for (int k = 0; k < 8; ++k) red[wid * BN + cg * 8 + k] = q0[k];
-      }
-      __syncthreads();
-      for (int e = tid; ew && e < BN; e += 256)
-        atomicAdd(&a.gb[n0 + e], red[e] + red[BN + e] + red[2 * BN + e] + red[3 * BN + e]);
-    }
-    if constexpr (STATS) {
-      // lanes l, l + CG, l + 2CG, ... of a wave hold the same channels
-#pragma unroll
-      for (int o = CG; o < 64; o <<= 1) {
-        if (!ew) break;
-#pragma unroll
-        for (int k = 0; k < 8; ++k) {
-          q0[k] += __shfl_xor(q0[k], o, 64);
-          q1[k] += __shfl_xor(q1[k], o, 64);
-          if constexpr (NQ == 3) q2[k] += __shfl_xor(q2[k], o, 64);
-        }
-      }
-      if (ew && lane < CG) {
-        float* rw = red + wid * NQ * BN + cg * 8;
-#pragma unroll
-        for (int k = 0; k < 8; ++k) {
-          rw[k] = q0[k];
-          rw[BN + k] = q1[k];
-          if constexpr (NQ == 3) rw[2 * BN + k] = q2[k];
-        }
-      }
-      __syncthreads();
-      for (int e = tid; ew && e < NQ * BN; e += 256) {
-        const float t = red[e] + red[NQ * BN + e] + red[2 * NQ * BN + e] + red[3 * NQ * BN + e];
-        const int q = e / BN, cc2 = e - q * BN;
-        if (!(a.dbg & 1)) atomicAdd(&a.part[((long)(bm & a.slot_mask) * NQ + q) * a.Cout + n0 + cc2], t);
-      }
-    }
-  }
+  conv_epilogue<BM, BN, EPI, ACT, 256, 2, 2>(a, acc, m0, n0, bm, tid, reinterpret_cast<float*>(smem + hdr), red,
+                                           grp == 0, inv_alpha);
 }
 
 // ---------------------------------------------------------------------- host side
@@ -1054,6 +1092,9 @@ bool launch_cases_plain(int pro, int epi, int act, const ConvArgs& a, int BM, in
                         hipStream_t st);
 bool launch_cases_ffn(int pro, int epi, int act, const ConvArgs& a, int BM, int BN, int BK, int kg, bool pure,
                       hipStream_t st);
+// halo-staged 3x3 stride-1 main loop (conv_h3.hip): kg 5 register-staged, kg 6 LDS-DMA
+bool h3_supported(const ConvArgs& a, int BM);
+bool launch_h3(int pro, int epi, int act, const ConvArgs& a, int BM, int BN, bool dma, hipStream_t st);
 
 }  // namespace conv
 }  // namespace fdt

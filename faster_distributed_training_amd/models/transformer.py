@@ -61,13 +61,25 @@ class Transformer(nn.Module):
         self.mix_override = None
         self.init_params()
 
-    def flat_adjacent(self):
-        """Parameter groups the flat buffers keep adjacent, in this order (utils/flat.py): all
-        parameters of one shape, in registration order.  Then (1) each attention block's Q / K / V
-        weights and biases sit back to back, so the fused projection reads the stacked bf16
-        weights as one view of the shadow buffer (no per-forward concatenation), and (2) NGD's
-        batched shape groups are views of the flat gradient (no stack / scatter copies,
-        optim/ngd.py ``_group_view``)."""
+    def flat_adjacent(self, scope="shape"):
+        """Parameter groups the flat buffers keep adjacent, in this order (utils/flat.py).
+        ``scope`` "shape": all parameters of one shape, in registration order.  Then (1) each
+        attention block's Q / K / V weights and biases sit back to back, so the fused projection
+        reads the stacked bf16 weights as one view of the shadow buffer (no per-forward
+        concatenation), and (2) NGD's batched shape groups are views of the flat gradient (no
+        stack / scatter copies, optim/ngd.py ``_group_view``).  ``scope`` "layer": (1) only --
+        each block's own Q / K / V (weights, biases), so the gradient buckets of a data-parallel
+        run keep following the backward's layer order."""
+        if scope == "layer":
+            out = []
+            for m in self.modules():
+                heads = getattr(m, "heads", None)
+                if isinstance(heads, nn.ModuleList) and len(heads) > 1 and all(isinstance(h, nn.Linear) for h in heads):
+                    for attr in ("weight", "bias"):
+                        grp = [getattr(h, attr) for h in heads]
+                        if all(p is not None and p.requires_grad for p in grp):
+                            out.append(grp)
+            return out
         by_shape = {}
         for p in self.parameters():
             if p.requires_grad:

@@ -197,6 +197,45 @@ GLDS = os.environ.get("FDT_CONV_GLDS", "0") == "1"
 # default (the legacy form: measured faster for most of the memory-bound batch-1024 layers)
 LOOP = os.environ.get("FDT_CONV_LOOP", "old")
 
+# Halo-staged 3x3 stride-1 main loop (csrc/kernels/conv_h3.hip, kg 5): the forward 3x3 convs on
+# their materialised inputs and the stride-1 3x3 data gradients on the pre-folded gradient, at
+# 256-pixel tiles.  FDT_CONV_H3=0 keeps the implicit-GEMM kernel's tuned tiles;
+# FDT_CONV_H3_MIN_TILES: below this many output tiles (small per-GPU batches) the tuned
+# implicit-GEMM launch (split-K / K groups) keeps the layer.
+H3 = os.environ.get("FDT_CONV_H3", "1") == "1"
+H3_MIN_TILES = int(os.environ.get("FDT_CONV_H3_MIN_TILES", "256"))
+H3_TILES = {(256, 128), (256, 64), (128, 128)}
+# staging of the halo loop: "dma" = LDS-DMA issued a chunk ahead (kg 6), "reg" = register-staged (kg 5)
+H3_LOOP = os.environ.get("FDT_CONV_H3_LOOP", "dma")
+
+
+def _h3_kg(kg):
+    return kg if kg in (5, 6) else (6 if H3_LOOP == "dma" else 5)
+
+
+def h3_tile(N, H, W, shp: "ConvShape", pro, cout, force=False, cx=None):
+    """(BM, BN) of the halo 3x3 loop for this launch, or None (csrc/kernels/conv_h3.hip
+    h3_supported: 3x3 pad-1 stride-1, prologue-free, whole image rows per 256-pixel tile).
+    ``force`` (an explicit kg 5): ignore FDT_CONV_H3 and the small-grid cut-off.  ``cx``: the
+    operand's channels (forward: cxp; data gradient: cout), a multiple of 16."""
+    if cx is None:
+        cx = shp.cxp
+    if not (H3 or force) or pro != PRO_NONE or cx % 16 or shp.k != 3 or shp.stride != 1 or shp.pad != 1 or W < 4 or W & (W - 1):
+        return None
+    bm = 256
+    M = N * H * W
+    if M % bm or bm % W:
+        return None
+    rb = min(H, bm // W)
+    if (rb < H and H % rb) or (rb == H and bm % (H * W)):
+        return None
+    if (bm // (rb * W)) * (rb + 2) * (W + 2) > bm // 16 * 36:
+        return None
+    bn = 128 if cout % 128 == 0 else (64 if cout % 64 == 0 else 0)
+    if not bn or (not force and (M // bm) * (cout // bn) < H3_MIN_TILES):
+        return None
+    return bm, bn
+
 
 def _loop_kg(ent, kgv):
     """kg 1 -> 4 when the launch takes the rotated K loop"""
@@ -309,14 +348,19 @@ def conv_fwd(x, wf, shp: ConvShape, s=None, t=None, act=0, alpha=1.0, tile=None,
     M = N * Ho * Wo
     pro = PRO_AFFINE_ACT if (s is not None or act != 0 or lazy is not None) else PRO_NONE
     ent = None
-    if tile is None:
+    h3 = h3_tile(N, H, W, shp, pro, shp.cout, kg in (5, 6)) if (kg in (5, 6) or (kg is None and tile is None)) else None
+    if tile is None and h3 is None:
         ent = tuned(f"fwd{pro}", N, H, shp) or tuned("fwd", N, H, shp)
         tile = tuple(ent["tile"]) if ent else None
-    bm, bn, bk = _tile3(tile, M, shp.cout)
-    if nsplit is not None:
-        ent = {"nsplit": nsplit}
-    ns, slab_p, cnt_p = _splitk_args(ent, M, shp.cout, shp.ntaps * C, bm, bn, bk, x.device)
-    kgv = _kg(ent, kg, (bm, bn, bk), ns, shp.ntaps * C, pro)
+    if h3 is not None:
+        ent, (bm, bn), bk = {"loop": "old"}, h3, 16
+        ns, slab_p, cnt_p, kgv = 1, 0, 0, _h3_kg(kg)
+    else:
+        bm, bn, bk = _tile3(tile, M, shp.cout)
+        if nsplit is not None:
+            ent = {"nsplit": nsplit}
+        ns, slab_p, cnt_p = _splitk_args(ent, M, shp.cout, shp.ntaps * C, bm, bn, bk, x.device)
+        kgv = _kg(ent, kg, (bm, bn, bk), ns, shp.ntaps * C, pro)
     _log("fwd", N, H, shp, ent, (bm, bn, bk), ns, kgv)
     y = torch.empty(N, Ho, Wo, shp.cout, device=x.device, dtype=torch.bfloat16)
     if part is None:
@@ -330,7 +374,7 @@ def conv_fwd(x, wf, shp: ConvShape, s=None, t=None, act=0, alpha=1.0, tile=None,
                    0, 0, 0, 0, 0, 0,
                    N, H, W, C, Ho, Wo, shp.stride, list(dh), list(dw), list(wt), shp.cout, shp.ntaps * shp.cxp,
                    Ho, Wo, 1, 0, 0, pro, int(act), float(alpha), EPI_STATS, 0, 1.0, bm, bn, bk, ns, slab_p, cnt_p,
-                   _loop_kg(ent, kgv), _sp(), lz[0], lz[1])
+                   _loop_kg(ent, kgv), _sp(), lz[0], lz[1], [])
     if fin is not None:
         _finalize_standalone(nat, 1, part, 2, shp.cout, fin[0], fin[1])
     return y, part
@@ -380,7 +424,7 @@ def conv_fwd_join(y, r, s, t, s2, t2, wf, shp: ConvShape, jout, jmask=None, tile
 
 def conv_dgrad(g, y, al, be, wd, shp: ConvShape, x_shape, epi=EPI_STORE, out=None, ex=None, es=None, et=None,
                act=0, alpha=1.0, tile=None, part=None, nsplit=None, gs=None, jmask=None, jyb=None, jout=None,
-               coef=None, kg=None):
+               coef=None, kg=None, jz=None):
     """Data gradient of y = conv(a): dA = conv^T(g*gs + al + be*y)  (gs None: 1).
 
     epi: EPI_STORE -> write dA; EPI_ADD -> out += dA; EPI_ACTBWD -> through the lazy
@@ -391,7 +435,10 @@ def conv_dgrad(g, y, al, be, wd, shp: ConvShape, x_shape, epi=EPI_STORE, out=Non
     becomes g_pre = (out + dA) * act'(join) with act' from ``jmask`` (ReLU bit mask) or
     ``jout`` (the join output, CELU), and ``part`` [STAT_SLOTS, 3, Cin] receives
     (sum g_pre*ex, sum g_pre, sum g_pre*jyb) -- ex / jyb = the block's residual / shortcut
-    branch outputs (jyb None: identity shortcut).
+    branch outputs (jyb None: identity shortcut).  CELU joins take act' from the recomputed fp32
+    pre-activation instead of ``jout`` (z mode): ``es`` / ``et`` = the residual branch's BN (s, t)
+    and ``jz`` = (sb, tb, xid) -- the shortcut's BN (s, t) or, identity shortcut, (None, None,
+    the block input).
     ``coef`` = (fptr, fval) with EPI_ACTBWD / EPI_JOINBWD: then turn the statistics into the
     producer units' BN-backward coefficients (stats_bwd_finalize arguments, units A and B:
     save_mean save_aux gamma alpha beta ggamma gbeta / mode eps count)."""
@@ -405,8 +452,16 @@ def conv_dgrad(g, y, al, be, wd, shp: ConvShape, x_shape, epi=EPI_STORE, out=Non
     if epi == EPI_ACTBWD and part is None:
         part = stat_slots(2, shp.cin, g.device, Nx * Hx * Wx)
     if epi == EPI_JOINBWD:
-        assert shp.stride == 1 and ex is not None and part is not None and (jmask is not None or jout is not None)
+        assert shp.stride == 1 and ex is not None and part is not None and (
+            jmask is not None or jout is not None or jz is not None)
+        assert (jz is None) == (es is None), "z mode: es / et with jz"
+        if jz is not None:
+            assert act == 2 and et is not None and len(jz) == 3
+            assert (jz[0] is not None and jz[1] is not None) if jyb is not None else jz[2] is not None
+            if jz[2] is not None:
+                assert jz[2].dtype == torch.bfloat16 and jz[2].is_contiguous() and tuple(jz[2].shape) == tuple(x_shape)
     ent = None
+    h3ok = kg in (5, 6) or (kg is None and tile is None)
     if tile is None:
         pro = PRO_FOLD if al is not None else PRO_NONE
         e = EPI_STORE if epi in (EPI_ADD, EPI_JOINBWD) else epi
@@ -422,10 +477,16 @@ def conv_dgrad(g, y, al, be, wd, shp: ConvShape, x_shape, epi=EPI_STORE, out=Non
         M = N * Ha * Wa
         if len(dh) == 0 and epi == EPI_ADD:
             continue
-        bm, bn, bk = _tile3(tile, M, shp.cin)
-        ns, slab_p, cnt_p = _splitk_args(ent, M, shp.cin, len(dh) * Cy, bm, bn, bk, g.device)
         pro = PRO_FOLD if al is not None else PRO_NONE  # al None: g is already folded
-        kgv = _kg(ent, kg, (bm, bn, bk), ns, len(dh) * Cy, pro)
+        h3 = h3_tile(N, Hx, Wx, shp, pro, shp.cin, kg in (5, 6), cx=Cy) if h3ok and epi in (EPI_ACTBWD, EPI_STORE) and len(
+            dh) == 9 else None
+        if h3 is not None:
+            (bm, bn), bk = h3, 16
+            ns, slab_p, cnt_p, kgv = 1, 0, 0, _h3_kg(kg)
+        else:
+            bm, bn, bk = _tile3(tile, M, shp.cin)
+            ns, slab_p, cnt_p = _splitk_args(ent, M, shp.cin, len(dh) * Cy, bm, bn, bk, g.device)
+            kgv = _kg(ent, kg, (bm, bn, bk), ns, len(dh) * Cy, pro)
         _log("dgrad", N, Hx, shp, ent, (bm, bn, bk), ns, kgv)
         assert gs is None or pro == PRO_FOLD, "gs needs the fold prologue (al/be)"
         nat.conv_igemm(g.data_ptr(), _p(y) if pro == PRO_FOLD else 0, _p(al), _p(be), _p(gs), wd.data_ptr(),
@@ -434,7 +495,7 @@ def conv_dgrad(g, y, al, be, wd, shp: ConvShape, x_shape, epi=EPI_STORE, out=Non
                        _p(jmask), _p(jyb), _p(jout), N, Hy, Wy, Cy, Ha, Wa, 1,
                        list(dh), list(dw), list(wt), shp.cin, shp.ntaps * shp.cout, Hx, Wx, shp.stride, py, px,
                        pro, 0, 1.0, epi, int(act), float(alpha), bm, bn, bk, ns, slab_p, cnt_p, _loop_kg(ent, kgv),
-                       _sp(), [], [])
+                       _sp(), [], [], [_p(v) for v in jz] if jz is not None else [])
     if coef is not None:
         _finalize_standalone(nat, 2, part, 3 if epi == EPI_JOINBWD else 2, shp.cin, coef[0], coef[1])
     return out, (part if epi in (EPI_ACTBWD, EPI_JOINBWD) else None)

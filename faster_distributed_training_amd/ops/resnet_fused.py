@@ -703,6 +703,22 @@ def _wgrad(br, *args, guard=False, **kw):
         br.run(*args, guard=guard, **kw)
 
 
+# CELU joins (BasicBlock, reference resnet.py:188-190): the backward takes act'(z) = exp(z/alpha)
+# from the fp32 pre-activation z = y*s + t + shortcut, recomputed from the stored bf16 branch
+# outputs exactly as the forward join formed it.  FDT_CELU_ZGRAD=0 restores the old derivative
+# 1 + o/alpha from the bf16 join OUTPUT o, which is wrong below z ~ -0.3 (bf16 ulp of o / alpha ~
+# 6.5e-3 against a derivative < 0.02) and sign-flipped for deeply negative z (o rounds below
+# -alpha): the ResNet-18 convergence gap of round 5 (profiles/r6/convergence_ablation.txt).
+CELU_ZGRAD = os.environ.get("FDT_CELU_ZGRAD", "1") == "1"
+
+
+def _celu_jz(b, ys, sc, x_in):
+    """[sa, ta, sb, tb, xid] of a CELU join's z-mode backward (None: ReLU join / disabled)."""
+    if b.join[0] != ACT_CELU or not CELU_ZGRAD:
+        return None
+    return [ys[-1][1], ys[-1][2], sc[1] if sc else None, sc[2] if sc else None, None if sc else x_in]
+
+
 # ------------------------------------------------------------------ autograd node
 class ResNetBodyFn(torch.autograd.Function):
     @staticmethod
@@ -866,10 +882,11 @@ class ResNetBodyFn(torch.autograd.Function):
                 # ONE gradient g_pre = g*act'(z) for both branches: each consumer folds in its
                 # own BN scale (gs = s3 / s_shortcut) in its prologue
                 gpre = torch.empty_like(y3)
-                nat.residual_act_bwd(g.data_ptr(), 0 if mask is not None else out.data_ptr(), _p(mask),
+                jz = _celu_jz(b, ys, sc, x_in)
+                nat.residual_act_bwd(g.data_ptr(), 0 if (mask is not None or jz) else out.data_ptr(), _p(mask),
                                      y3.data_ptr(), _p(sc[0] if sc else None), gpre.data_ptr(), part.data_ptr(),
                                      part.shape[0], M, C,
-                                     b.join[0], float(b.join[1]), 1, _sp(), ghw)
+                                     b.join[0], float(b.join[1]), 1, _sp(), ghw, [_p(v) for v in jz] if jz else [])
                 ghw = 0
             ul = b.units[-1]
             if joined:
@@ -930,14 +947,18 @@ class ResNetBodyFn(torch.autograd.Function):
                     if br is not None and sc is None:
                         br.wait()  # g_x aliases g_pre: its last reader (a branch wgrad) first
                     if prev is not None:
-                        _, pys, psc, pout, pmask = prec
+                        px_in, pys, psc, pout, pmask = prec
+                        pjz = _celu_jz(prev, pys, psc, px_in)
                         pul = prev.units[-1]
                         cf, ra, rb = coef_args(pul, (pys[-1][3], pys[-1][4], pys[-1][5]), prev.shortcut,
                                                (psc[3], psc[4], psc[5]) if psc else None, training, dev)
                         ci.conv_dgrad(g_cur, y, al, be, u.wd, u.shp, tuple(x_in.shape), epi=ci.EPI_JOINBWD, out=g_x,
                                       gs=gs_cur, ex=pys[-1][0], part=slots(3, x_in.shape[-1], dev, _rows(x_in)),
                                       act=prev.join[0], alpha=prev.join[1], jmask=pmask,
-                                      jyb=psc[0] if psc else None, jout=None if pmask is not None else pout, coef=cf)
+                                      jyb=psc[0] if psc else None,
+                                      jout=None if (pmask is not None or pjz) else pout, coef=cf,
+                                      es=pjz[0] if pjz else None, et=pjz[1] if pjz else None,
+                                      jz=pjz[2:] if pjz else None)
                         coef_ready(pul, prev.shortcut)
                         joined_coef = (ra, rb)
                     else:

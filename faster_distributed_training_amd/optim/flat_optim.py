@@ -45,6 +45,29 @@ def _layout_key(flat) -> str:
     return h.hexdigest()
 
 
+def _slot_table(flat) -> list:
+    return [(sl.name, int(sl.offset), int(sl.numel)) for sl in getattr(flat, "slots", [])]
+
+
+def _slot_remap(saved, flat):
+    """Function moving a saved per-element state vector (slot table ``saved``) onto ``flat``'s
+    slot order, matched by slot name; refuses a table whose names / sizes do not match."""
+    cur = {n: (o, k) for n, o, k in _slot_table(flat)}
+    old = {n: (o, k) for n, o, k in saved}
+    if set(cur) != set(old) or any(cur[n][1] != old[n][1] for n in cur):
+        raise ValueError("optimizer state was saved for different parameters (slot names / sizes differ)")
+    if all(cur[n][0] == old[n][0] for n in cur):
+        return lambda v: v
+    pairs = [(old[n][0], cur[n][0], cur[n][1]) for n in cur]
+
+    def move(v):
+        out = torch.zeros(flat.numel, dtype=v.dtype, device=v.device)
+        for so, do, k in pairs:
+            out[do:do + k].copy_(v[so:so + k])
+        return out
+    return move
+
+
 class FlatOptimizer(torch.optim.Optimizer):
     def __init__(self, flat: FlatParams, defaults: dict, zero_grad_in_step: bool = True):
         self.flat = flat
@@ -112,23 +135,37 @@ class FlatOptimizer(torch.optim.Optimizer):
         flat = {k: (v.detach().clone() if torch.is_tensor(v) else v)
                 for k, v in self.state.get("__flat__", {}).items()}
         return {"flat_state": flat, "param_groups": groups, "k": self.k, "kskip": self.kskip.detach().clone().cpu(),
-                "numel": self.flat.numel, "layout": _layout_key(self.flat)}
+                "numel": self.flat.numel, "layout": _layout_key(self.flat), "slots": _slot_table(self.flat)}
 
     def load_state_dict(self, sd):
         if "flat_state" not in sd:  # a plain torch.optim state dict: hyper-parameters only
             for g, sg in zip(self.param_groups, sd.get("param_groups", [])):
                 g.update({k: v for k, v in sg.items() if k != "params"})
             return
-        if sd.get("numel", self.flat.numel) != self.flat.numel:
+        remap = None
+        if "slots" in sd:
+            # per-slot (name, offset, numel): the saved vectors are moved slot by slot onto THIS
+            # buffer's order (a checkpoint from before a slot reordering, e.g. the transformer's
+            # flat_adjacent groups, lands on the right parameters)
+            remap = _slot_remap(sd["slots"], self.flat)
+        elif "layout" in sd:
+            if sd["layout"] != _layout_key(self.flat):
+                # same element count, other slot order: the flat state vectors would be applied
+                # to the wrong parameters
+                raise ValueError("optimizer state was saved for a different parameter order")
+        else:
+            # no slot table and no fingerprint (written before either existed): the numel check
+            # cannot tell a reordered buffer from the same one (every slot is padded on its own)
+            raise ValueError("flat optimizer state carries no slot table or layout fingerprint: its parameter "
+                             "order cannot be verified (re-save it, or load the model weights only)")
+        if sd.get("numel", self.flat.numel) != self.flat.numel and remap is None:
             raise ValueError("optimizer state was saved for a different parameter layout")
-        if "layout" in sd and sd["layout"] != _layout_key(self.flat):
-            # same element count, other slot order (e.g. a model's flat_adjacent groups): the
-            # flat state vectors would be applied to the wrong parameters
-            raise ValueError("optimizer state was saved for a different parameter order")
         for g, sg in zip(self.param_groups, sd["param_groups"]):
             g.update(sg)
         st = self.state.setdefault("__flat__", {})
         for k, v in sd["flat_state"].items():
+            if torch.is_tensor(v) and remap is not None and v.dim() == 1 and v.numel() == sd.get("numel", -1):
+                v = remap(v)
             st[k] = v.to(self.flat.device) if torch.is_tensor(v) else v
         self.k = int(sd.get("k", 0))
         if "kskip" in sd:

@@ -145,7 +145,10 @@ class TransformerTrainer:
             self.flat = self.fsdp.space
         else:
             part = self.world if (cfg.distributed and ngd_opt and cfg.shard_ngd) else 0
-            self.flat = FlatParams(self.model, device=self.device, with_shadow=shadow, partition=part, balance="ngd")
+            # world > 1: per-block Q / K / V adjacency only (whole-model shape runs put
+            # every layer's weights in the first buckets -> no all-reduce / backward overlap)
+            self.flat = FlatParams(self.model, device=self.device, with_shadow=shadow, partition=part, balance="ngd",
+                                   adjacent="layer" if cfg.distributed else "shape")
             if shadow:  # bf16 compute reads the optimizer-maintained bf16 copy (no per-step casts)
                 from ..ops.linear import enable_shadow_weights
                 enable_shadow_weights(self.flat)

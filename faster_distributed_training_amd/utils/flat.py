@@ -141,7 +141,7 @@ class FlatParams:
     not kept in model order) instead of the element count alone."""
 
     def __init__(self, module_or_params, device=None, reverse=True, with_shadow=False, names=None, partition=0,
-                 dtype=torch.float32, balance="numel"):
+                 dtype=torch.float32, balance="numel", adjacent="shape"):
         if isinstance(module_or_params, nn.Module):
             named = [(n, p) for n, p in module_or_params.named_parameters() if p.requires_grad]
         else:
@@ -149,9 +149,14 @@ class FlatParams:
             named = [(names[i] if names else f"p{i}", p) for i, p in enumerate(plist)]
         if reverse:
             named = named[::-1]
-        if (isinstance(module_or_params, nn.Module) and hasattr(module_or_params, "flat_adjacent")
+        # adjacent: "shape" = every same-shape parameter of the model in one run (single GPU: NGD's
+        # shape groups become views), "layer" = only one block's Q / K / V (data-parallel
+        # world > 1: whole-model shape runs would park every layer's weights in the first
+        # gradient buckets, which then wait for layer 0's backward -- no comm / backward
+        # overlap), None / FDT_FLAT_ADJACENT=0 = registration order
+        if (adjacent and isinstance(module_or_params, nn.Module) and hasattr(module_or_params, "flat_adjacent")
                 and os.environ.get("FDT_FLAT_ADJACENT", "1") != "0"):
-            named = _adjacent_groups(named, module_or_params.flat_adjacent())
+            named = _adjacent_groups(named, module_or_params.flat_adjacent(adjacent))
         self.slots: list[Slot] = []
         self.runs = None
         self.chunk = 0

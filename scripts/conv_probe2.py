@@ -24,7 +24,7 @@ def conv_direct(x, wf, shp, epi, part, tile, kg=1):
     nat.conv_igemm(x.data_ptr(), 0, 0, 0, 0, wf.data_ptr(), y.data_ptr(), part.data_ptr() if part is not None else 0,
                    part.shape[0] if part is not None else 0, 0, 0, 0, 0, 0, 0, N, H, W, C, Ho, Wo, shp.stride, list(dh),
                    list(dw), list(wt), shp.cout, shp.ntaps * shp.cxp, Ho, Wo, 1, 0, 0, 0, 0, 1.0, epi, 0, 1.0, bm, bn,
-                   bk, 1, 0, 0, kg, _native.stream_ptr(), [], [])
+                   bk, 1, 0, 0, kg, _native.stream_ptr(), [], [], [])
     return y
 
 

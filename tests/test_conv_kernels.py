@@ -11,6 +11,9 @@ pytestmark = pytest.mark.gpu
 BF = torch.bfloat16
 
 
+_p = ci._p
+
+
 def rel(a, b):
     a, b = a.float(), b.float()
     return ((a - b).norm() / (b.norm() + 1e-12)).item()
@@ -181,6 +184,71 @@ def test_conv_dgrad(cuda, case, epi):
             assert rel(ps[1], gp.reshape(-1, Cin).sum(0)) < 1e-2
 
 
+# halo-staged 3x3 loop (kg 5, csrc/kernels/conv_h3.hip): (N, H, Cin, Cout) -- whole image rows
+# per 256-pixel tile (H 32 / 16), whole images (H 8 / 4), BN 128 and 64
+H3_CASES = [(1, 32, 64, 64), (2, 16, 128, 128), (4, 8, 256, 256), (16, 4, 512, 512), (2, 16, 64, 128),
+            (4, 8, 128, 64), (32, 4, 64, 128)]
+
+
+@pytest.mark.parametrize("case", H3_CASES)
+@pytest.mark.parametrize("kg", [5, 6])
+def test_h3_conv_fwd(cuda, case, kg):
+    """Forward 3x3 on a materialised operand through the halo loop: output and BN statistics
+    against fp32 PyTorch, and the implicit-GEMM kernel on the same inputs."""
+    N, H, Cin, Cout = case
+    torch.manual_seed(7)
+    shp = ci.ConvShape(Cin, Cout, 3, 1, 1)
+    x = make((N, H, H, Cin), cuda)
+    w = torch.randn(Cout, Cin, 3, 3, device=cuda) / (Cin * 9) ** 0.5
+    wf, wd = ci.alloc_packed(shp, cuda)
+    ci.pack_weights([(w, wf, wd, shp)])
+    assert ci.h3_tile(N, H, H, shp, ci.PRO_NONE, Cout, force=True) is not None
+    y, part = ci.conv_fwd(x, wf, shp, kg=kg)
+    ref = nhwc(F.conv2d(nchw(x), w.to(BF).float(), padding=1))
+    assert rel(y, ref) < 1e-2, rel(y, ref)
+    assert ((y.float() - ref).abs() <= ref.abs() * 2 ** -7 + 2e-3 * ref.abs().max()).float().mean() > 0.999
+    ps = part.sum(0)
+    yf = ref.reshape(-1, Cout)
+    assert rel(ps[0], yf.sum(0)) < 2e-3
+    assert rel(ps[1], (yf * yf).sum(0)) < 2e-3
+    y1, _ = ci.conv_fwd(x, wf, shp, tile=(128, 64, 32), kg=1)
+    assert rel(y, y1) < 1e-2
+
+
+@pytest.mark.parametrize("case", H3_CASES)
+@pytest.mark.parametrize("epi", ["store", "actbwd_relu", "actbwd_celu"])
+@pytest.mark.parametrize("kg", [5, 6])
+def test_h3_conv_dgrad(cuda, case, epi, kg):
+    """Stride-1 3x3 data gradient of a pre-folded gradient through the halo loop (flipped taps):
+    plain store and the producer's activation backward + statistics, against fp32 PyTorch."""
+    N, H, Cin, Cout = case
+    torch.manual_seed(8)
+    shp = ci.ConvShape(Cin, Cout, 3, 1, 1)
+    w = torch.randn(Cout, Cin, 3, 3, device=cuda) / (Cin * 9) ** 0.5
+    wf, wd = ci.alloc_packed(shp, cuda)
+    ci.pack_weights([(w, wf, wd, shp)])
+    g = make((N, H, H, Cout), cuda)
+    ref = nhwc(torch.nn.grad.conv2d_input((N, Cin, H, H), w.to(BF).float(), nchw(g.float()), padding=1))
+    xs = (N, H, H, Cin)
+    if epi == "store":
+        out, _ = ci.conv_dgrad(g, None, None, None, wd, shp, xs, epi=ci.EPI_STORE, kg=kg)
+        assert rel(out, ref) < 1e-2
+        return
+    act, alpha = (1, 1.0) if epi == "actbwd_relu" else (2, 0.075)
+    ex = make(xs, cuda)
+    es = torch.rand(Cin, device=cuda) + 0.5
+    et = torch.randn(Cin, device=cuda) * 0.3
+    z = ex.float() * es + et
+    d = (z > 0).float() if act == 1 else torch.where(z > 0, torch.ones_like(z), torch.exp(z / alpha))
+    gp = ref * d
+    out, part = ci.conv_dgrad(g, None, None, None, wd, shp, xs, epi=ci.EPI_ACTBWD, ex=ex, es=es, et=et, act=act,
+                              alpha=alpha, kg=kg)
+    assert rel(out, gp * es) < 1e-2
+    ps = part.sum(0)
+    assert rel(ps[0], (gp * ex.float()).reshape(-1, Cin).sum(0)) < 1e-2
+    assert rel(ps[1], gp.reshape(-1, Cin).sum(0)) < 1e-2
+
+
 WGRAD_CASES = [
     (4, 8, 64, 128, 1, 1, 0),
     (2, 8, 64, 64, 3, 1, 1),
@@ -282,12 +350,14 @@ def test_fold_gradient_scale(cuda, case):
 
 
 @pytest.mark.parametrize("case", [(4, 8, 64, 256, 1, 1, 0), (3, 5, 128, 64, 1, 1, 0), (2, 4, 512, 1024, 1, 1, 0)])
-@pytest.mark.parametrize("join", ["relu_mask", "relu_mask_shortcut", "celu_out"])
+@pytest.mark.parametrize("join", ["relu_mask", "relu_mask_shortcut", "celu_z", "celu_z_shortcut"])
 @pytest.mark.parametrize("ns", [1, 3])
 def test_conv_dgrad_join_backward(cuda, case, join, ns):
     """EPI_JOINBWD: the dgrad that completes a block-output gradient also runs that block's
-    residual-join backward: g_pre = (prev + dA) * act'(out) stored in place, slots
-    (sum g_pre*y_res, sum g_pre, sum g_pre*y_sc)."""
+    residual-join backward: g_pre = (prev + dA) * act'(z) stored in place, slots
+    (sum g_pre*y_res, sum g_pre, sum g_pre*y_sc).  CELU joins: the oracle is the fp32
+    derivative exp(z/alpha) of the fp32 pre-activation z = ya*sa + ta + (yb*sb + tb | xid)
+    (reference nn.CELU autograd, resnet.py:188-190) -- NOT a formula of the bf16 join output."""
     from faster_distributed_training_amd.ops import _native
     nat = _native.native()
     N, H, Cin, Cout, k, stride, pad = case
@@ -305,15 +375,26 @@ def test_conv_dgrad_join_backward(cuda, case, join, ns):
     dA = nhwc(torch.nn.grad.conv2d_input((N, Cin, H, H), w.to(BF).float(), nchw(gt), stride=1, padding=pad))
     prev = make(xs, cuda)
     ya = make(xs, cuda)
-    yb = make(xs, cuda) if join == "relu_mask_shortcut" else None
-    out_join = make(xs, cuda)
-    if join == "celu_out":
+    yb = make(xs, cuda) if join.endswith("shortcut") else None
+    zkw = {}
+    if join.startswith("celu"):
         act, alpha = 2, 0.075
-        out_join = F.celu(out_join.float(), alpha).to(BF)
-        o = out_join.float()
-        dact = torch.where(o > 0, torch.ones_like(o), o / alpha + 1)
         mask = None
+        sa = torch.rand(Cin, device=cuda) * 0.5 + 0.2
+        ta = torch.randn(Cin, device=cuda) * 0.3 - 0.3   # most of z negative: the CELU tail
+        if yb is not None:
+            sb = torch.rand(Cin, device=cuda) * 0.5 + 0.2
+            tb = torch.randn(Cin, device=cuda) * 0.2
+            z = ya.float() * sa + ta + (yb.float() * sb + tb)
+            zkw = dict(es=sa, et=ta, jz=(sb, tb, None))
+        else:
+            xid = make(xs, cuda)
+            z = ya.float() * sa + ta + xid.float()
+            zkw = dict(es=sa, et=ta, jz=(None, None, xid))
+        assert (z < -0.5).float().mean() > 0.2  # the regime the bf16-output formula gets wrong
+        dact = torch.where(z > 0, torch.ones_like(z), torch.exp(z.double() / alpha).float())
     else:
+        out_join = make(xs, cuda)
         act, alpha = 1, 1.0
         dact = (out_join.float() > 0).float()
         mask = torch.empty(out_join.numel() // 8, device=cuda, dtype=torch.uint8)
@@ -327,7 +408,10 @@ def test_conv_dgrad_join_backward(cuda, case, join, ns):
     part = ci.stat_slots(3, Cin, cuda)
     out = prev.clone()
     ci.conv_dgrad(g, y, al, be, wd, shp, xs, epi=ci.EPI_JOINBWD, out=out, ex=ya, part=part, act=act, alpha=alpha,
-                  jmask=mask, jyb=yb, jout=None if mask is not None else out_join, nsplit=ns)
+                  jmask=mask, jyb=yb, nsplit=ns, **zkw)
+    # elementwise: bf16 rounding of the stored g_pre (and of dA's bf16 operand) only
+    err = (out.float() - gp).abs()
+    assert (err <= gp.abs() * 2 ** -7 + dact * 1e-3 + 1e-7).float().mean() > 0.999, err.max()
     assert rel(out, gp) < 1e-2
     ps = part.sum(0)
     assert rel(ps[0], (gp * ya.float()).reshape(-1, Cin).sum(0)) < 1e-2
@@ -336,6 +420,54 @@ def test_conv_dgrad_join_backward(cuda, case, join, ns):
         assert rel(ps[2], (gp * yb.float()).reshape(-1, Cin).sum(0)) < 1e-2
     else:
         assert torch.count_nonzero(ps[2]).item() == 0
+
+
+@pytest.mark.parametrize("shortcut", [False, True])
+def test_celu_join_backward_uses_preactivation(cuda, shortcut):
+    """The standalone join backward (residual_act_bwd, the last block / strided blocks) in z mode
+    matches the fp32 exp(z/alpha) oracle on the CELU tail, and the legacy derivative from the
+    bf16 OUTPUT (1 + o/alpha) does not -- the round-5 ResNet-18 convergence gap
+    (profiles/r6/convergence_ablation.txt)."""
+    from faster_distributed_training_amd.ops import _native
+    nat = _native.native()
+    torch.manual_seed(11)
+    N, H, C, alpha = 4, 8, 64, 0.075
+    M = N * H * H
+    ya, g = make((N, H, H, C), cuda), make((N, H, H, C), cuda)
+    sa = torch.rand(C, device=cuda) * 0.5 + 0.2
+    ta = torch.randn(C, device=cuda) * 0.3 - 0.4
+    yb = make((N, H, H, C), cuda) if shortcut else None
+    sb = torch.rand(C, device=cuda) * 0.5 + 0.2 if shortcut else None
+    tb = torch.randn(C, device=cuda) * 0.2 if shortcut else None
+    xid = None if shortcut else make((N, H, H, C), cuda)
+    # the forward join (bf16 output o), as the engine runs it
+    out = torch.empty_like(ya)
+    nat.residual_act_fwd(ya.data_ptr(), sa.data_ptr(), ta.data_ptr(), _p(yb), _p(sb), _p(tb),
+                         0 if shortcut else xid.data_ptr(), out.data_ptr(), 0, M, C, 2, alpha, 1,
+                         _native.stream_ptr())
+    z = ya.float() * sa + ta + (yb.float() * sb + tb if shortcut else xid.float())
+    want = g.float() * torch.where(z > 0, torch.ones_like(z), torch.exp(z.double() / alpha).float())
+
+    def run(jz):
+        gpre = torch.empty_like(ya)
+        part = ci.stat_slots(3, C, cuda)
+        nat.residual_act_bwd(g.data_ptr(), 0 if jz else out.data_ptr(), 0, ya.data_ptr(), _p(yb), gpre.data_ptr(),
+                             part.data_ptr(), part.shape[0], M, C, 2, alpha, 1, _native.stream_ptr(), 0,
+                             [_p(v) for v in jz] if jz else [])
+        return gpre.float(), part.sum(0)
+
+    tail = z < -0.5
+    assert tail.float().mean() > 0.2
+    got, ps = run([sa, ta, sb, tb, xid])
+    tol = want.abs() * 2 ** -7 + 1e-7
+    assert ((got - want).abs() <= tol).float().mean() > 0.999
+    assert rel(ps[1], want.reshape(-1, C).sum(0)) < 1e-2
+    assert rel(ps[0], (want * ya.float()).reshape(-1, C).sum(0)) < 1e-2
+    legacy, _ = run(None)
+    # on the tail the output-based derivative is mostly wrong by more than bf16 rounding ...
+    assert ((legacy - want).abs() > tol)[tail].float().mean() > 0.5
+    # ... including sign flips of g (o rounded below -alpha)
+    assert ((legacy * want) < 0)[tail].any()
 
 
 def test_strided_dgrad_store_writes_every_parity_class(cuda):

@@ -189,3 +189,35 @@ def test_fused_bias_grad_cpu_path_matches_plain_linear():
         fn(F.linear(h, w, b), None).backward(g)
         for a, r in zip(got, (h.grad, w.grad, b.grad)):
             torch.testing.assert_close(a, r)
+
+
+def test_flat_adjacent_scope_keeps_layer_order_for_data_parallel():
+    """utils/flat.py adjacency: "shape" (one GPU) moves every same-shape parameter of the model
+    next to the first member's slot (the LAST layer with the reversed buffer), "layer" (data
+    parallel, world > 1) only each attention block's own Q / K / V -- so the gradient buckets
+    still follow the backward's layer order."""
+    from faster_distributed_training_amd.models import transformer as T
+    from faster_distributed_training_amd.utils.flat import FlatParams
+    torch.manual_seed(0)
+    m = T.Transformer(4, 1000, n_layers=3, h=4, d_model=64, d_ff=128, d_hidden=64)
+    names = [n for n, p in m.named_parameters() if p.requires_grad]
+    def layer_of(n):
+        for kind in ("sublayer_attention.", "sublayer_ffn."):
+            if n.startswith(kind):
+                return (kind, int(n[len(kind):].split(".")[0]))
+        return None
+    lay = FlatParams(m, adjacent="layer")
+    order = [s.name for s in lay.slots]
+    assert sorted(order) == sorted(names)
+    def layer_seq(slots, kind):
+        return [layer_of(n)[1] for n in slots if layer_of(n) is not None and layer_of(n)[0] == kind]
+    for kind in ("sublayer_attention.", "sublayer_ffn."):
+        seq = layer_seq(order, kind)
+        assert seq == sorted(seq, reverse=True), "per-layer adjacency keeps the layers in backward order"
+    # each block's Q / K / V weights back to back
+    for i in range(3):
+        qkv = [k for k, n in enumerate(order) if layer_of(n) == ("sublayer_attention.", i) and ".heads." in n
+               and n.endswith("weight")]
+        assert len(qkv) == 3 and qkv == list(range(qkv[0], qkv[0] + 3))
+    shp = layer_seq([s.name for s in FlatParams(m, adjacent="shape").slots], "sublayer_ffn.")
+    assert shp != sorted(shp, reverse=True), "shape adjacency groups layers together (single-GPU layout)"

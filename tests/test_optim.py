@@ -303,18 +303,38 @@ def test_ngd_plain_steps_defer_clip_scale_to_sgd(monkeypatch):
     assert ((a - b).norm() / b.norm()).item() < 1e-10
 
 
-def test_flat_optimizer_state_refuses_other_parameter_order():
-    """Flat optimizer state (momentum / second moments as flat vectors) loads only into the
-    slot order it was saved with: the same element count in another order (a model's
-    ``flat_adjacent`` groups, a reversed layout) is refused instead of silently applied to the
-    wrong parameters."""
-    m = nn.Sequential(nn.Linear(8, 8), nn.Linear(8, 8))
+def test_flat_optimizer_state_follows_parameter_order():
+    """Flat optimizer state (momentum / second moments as flat vectors) is saved with its slot
+    table (name, offset, numel): loaded into another slot order of the same parameters (a
+    model's ``flat_adjacent`` groups, a reversed layout) it is moved slot by slot onto the
+    right parameters.  A dict with only the layout fingerprint loads into that exact layout
+    only, and one with neither (written before both existed) is refused -- the element count
+    alone cannot tell a reordered buffer from the same one."""
+    torch.manual_seed(0)
+    m = nn.Sequential(nn.Linear(8, 8), nn.Linear(8, 6))
     a = O.MADGRAD(FlatParams(m, reverse=True), lr=1e-3)
     a.flat.grad.normal_()
     a.step()
     sd = a.state_dict()
-    b = O.MADGRAD(FlatParams(nn.Sequential(nn.Linear(8, 8), nn.Linear(8, 8)), reverse=False), lr=1e-3)
+    fb = FlatParams(nn.Sequential(nn.Linear(8, 8), nn.Linear(8, 6)), reverse=False)
+    b = O.MADGRAD(fb, lr=1e-3)
+    b.load_state_dict(sd)
+    sa, sb = a.state["__flat__"], b.state["__flat__"]
+    moved = 0
+    for k, v in sa.items():
+        if torch.is_tensor(v) and v.dim() == 1 and v.numel() == a.flat.numel:
+            for sl in a.flat.slots:
+                dst = next(t for t in fb.slots if t.name == sl.name)
+                assert torch.equal(sb[k][dst.offset:dst.offset + dst.numel], v[sl.offset:sl.offset + sl.numel])
+            moved += 1
+    assert moved >= 2
+    legacy = {k: v for k, v in sd.items() if k not in ("slots",)}
     with pytest.raises(ValueError, match="parameter order"):
-        b.load_state_dict(sd)
-    c = O.MADGRAD(FlatParams(nn.Sequential(nn.Linear(8, 8), nn.Linear(8, 8)), reverse=True), lr=1e-3)
-    c.load_state_dict(sd)  # same layout: accepted
+        O.MADGRAD(FlatParams(nn.Sequential(nn.Linear(8, 8), nn.Linear(8, 6)), reverse=False), lr=1e-3).load_state_dict(legacy)
+    O.MADGRAD(FlatParams(nn.Sequential(nn.Linear(8, 8), nn.Linear(8, 6)), reverse=True), lr=1e-3).load_state_dict(legacy)
+    older = {k: v for k, v in sd.items() if k not in ("slots", "layout")}
+    with pytest.raises(ValueError, match="cannot be verified"):
+        O.MADGRAD(FlatParams(nn.Sequential(nn.Linear(8, 8), nn.Linear(8, 6)), reverse=True), lr=1e-3).load_state_dict(older)
+    other = O.MADGRAD(FlatParams(nn.Sequential(nn.Linear(8, 8), nn.Linear(8, 7)), reverse=True), lr=1e-3)
+    with pytest.raises(ValueError):
+        other.load_state_dict(sd)
