@@ -43,18 +43,63 @@ __device__ __forceinline__ void h3_dma16(__amdgpu_buffer_rsrc_t r, void* lds, ui
   __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)lds, 16, off, 0, 0, 0);
 }
 
+// Halo blocks (one per image, or one per Rb-row slab of a larger image) are laid out every bhr
+// rows, bhr = (Rb+2)(W+2) padded so that 3*bhr = 16/NI (mod 16): see H3Geom.
 template <int BM>
-constexpr int h3_halo_rows_max() {  // BM/16 images of 4x4 -> 6x6 halo each, rounded up to 64 rows
-  return (BM / 16 * 36 + 63) / 64 * 64;                           // (whole 1-KiB LDS-DMA pieces)
+constexpr int h3_halo_rows_max() {  // BM/16 images of 4x4 -> 44-row (padded 6x6) blocks, rounded up
+  return (BM / 16 * 44 + 63) / 64 * 64;                           // to 64 rows (whole 1-KiB DMA pieces)
 }
+
+// Tile geometry + the MFMA-column -> pixel map of the halo loop.  A ds_read_b128 serves a wave in
+// four fixed 16-lane groups ({0-3,12-15,20-27}, {4-11,16-19,28-31} and the same +32); a 48-B halo
+// row = 3 bank quads, so 16 CONSECUTIVE halo rows hit 16 distinct quads (3q mod 16).  Columns are
+// therefore permuted so each lane group reads a 16-pixel set: 16 consecutive pixels of one image
+// row (W >= 16), or one row segment of W pixels from each of NI = 16/W images (W = 8, 4) whose
+// halo blocks sit bhr rows apart with 3*bhr = 16/NI (mod 16) -- the NI segments then take
+// disjoint quad sets.  Conflict-free for every tap (a tap shifts every row alike); the identity
+// column order conflicts 2-3x at W = 16 / 8 / 4 (measured 27.5 % bank-conflict cycles, 16x16).
+struct H3Geom {
+  int W, Rb, W2, bhr, NI, GW, SPR;
+  __device__ __forceinline__ H3Geom(int W_, int H_, int BM) {
+    W = W_;
+    Rb = H_ < BM / W_ ? H_ : BM / W_;
+    W2 = W_ + 2;
+    GW = W_ < 16 ? W_ : 16;
+    NI = 16 / GW;
+    SPR = W_ / GW;
+    int b = (Rb + 2) * W2;
+    if (NI > 1) {
+      const int want = (11 * (16 / NI)) & 15;  // 3^-1 = 11 (mod 16)
+      b += (want - b % 16 + 16) % 16;
+    }
+    bhr = b;
+  }
+  // tile-local pixel of MFMA column n of 32-column block blk
+  __device__ __forceinline__ int pix(int blk, int n) const {
+    const int pn = n < 4 ? n : n < 12 ? n + 12 : n < 16 ? n - 8 : n < 20 ? n + 8 : n < 28 ? n - 12 : n;
+    const int s = blk * 2 + (pn >> 4), i = pn & 15;           // 16-pixel set s, position i
+    const int per = Rb * SPR;                                   // sets per image group
+    const int gi = s / per, rr = s - gi * per, r = rr / SPR, seg = rr - r * SPR;
+    const int img = NI * gi + i / GW, col = seg * GW + i % GW;
+    return img * (Rb * W) + r * W + col;
+  }
+  __device__ __forceinline__ int halo_row(int p) const {
+    const int b = p / (Rb * W), r = (p / W) % Rb, c = p % W;
+    return b * bhr + (r + 1) * W2 + c + 1;
+  }
+};
 
 template <int BM, int BN, int WM, int WN>
 constexpr size_t h3_stage_elems() { return (size_t)kH3Taps * BN * 16 + (size_t)h3_halo_rows_max<BM>() * kH3Row; }
 
 // DMA: the chunk's pieces move global -> LDS by LDS-DMA (buffer_load ... lds) issued at the top of
 // the previous chunk's MFMAs (no staging registers, no ds_write phase); otherwise register-staged.
-template <int BM, int BN, int EPI, int ACT, int WM, int WN, bool DMA>
-__global__ __launch_bounds__(64 * WM * WN, 1) void h3_kernel(const ConvArgs a) {
+// NS: LDS stages.  2 = double-buffered (one workgroup per CU); 1 (LDS-DMA only) = one stage
+// (load -> barrier -> MFMAs -> barrier), small enough for TWO workgroups per CU, whose phases
+// interleave -- and whose prologues / epilogues overlap the other's main loop.
+template <int BM, int BN, int EPI, int ACT, int WM, int WN, bool DMA, int NS = 2>
+__global__ __launch_bounds__(64 * WM * WN, NS == 1 ? 4 : 1) void h3_kernel(const ConvArgs a) {
+  static_assert(NS == 2 || (NS == 1 && DMA), "single-stage: LDS-DMA staging");
   constexpr int NT = 64 * WM * WN;
   constexpr int TN = BN / WN / 32, TM = BM / WM / 32;
   static_assert(TN >= 1 && TM >= 1, "wave tile >= 32x32");
@@ -82,8 +127,9 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void h3_kernel(const ConvArgs a) {
 
   // ---- tile geometry: BM consecutive pixels = nbk blocks of Rb whole rows of one image each
   const int W = a.Wi, H = a.Hi, W2 = W + 2, HW = H * W;
-  const int Rb = H < BM / W ? H : BM / W;
-  const int nbk = BM / (Rb * W), bhr = (Rb + 2) * W2, HR = nbk * bhr;
+  const H3Geom geo(W, H, BM);
+  const int Rb = geo.Rb;
+  const int nbk = BM / (Rb * W), bhr = geo.bhr, bh0 = (Rb + 2) * W2, HR = nbk * bhr;
   const int img0 = (int)(m0 / HW), h0 = (int)((m0 / W) % H);
 
   if (tid < kH3Taps) {
@@ -118,18 +164,14 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void h3_kernel(const ConvArgs a) {
     const int b = q / bhr, r2 = q - b * bhr;
     const int hr = r2 / W2, hc = r2 - hr * W2;
     const int h = h0 + hr - 1, w = hc - 1;
-    const bool in = v && (unsigned)h < (unsigned)H && (unsigned)w < (unsigned)W;
+    const bool in = v && r2 < bh0 && (unsigned)h < (unsigned)H && (unsigned)w < (unsigned)W;
     hoff[j] = in ? ((uint32_t)((img0 + b) * HW + h * W + w) * (uint32_t)a.Cx + 8u * lh) * 2u : kOOB;
     hdst[j] = v ? WTILE + q * kH3Row + 8 * lh : -1;  // padding rows store the zeros the OOB load returned
   }
   // ---- per-thread B-fragment halo rows (tap (0, 0)) and the nine tap offsets
   int qb[TM];
 #pragma unroll
-  for (int j = 0; j < TM; ++j) {
-    const int p = wm * (BM / WM) + j * 32 + (lane & 31);
-    const int b = p / (Rb * W), r = (p / W) % Rb, c = p % W;
-    qb[j] = b * bhr + (r + 1) * W2 + c + 1;
-  }
+  for (int j = 0; j < TM; ++j) qb[j] = geo.halo_row(geo.pix(wm * TM + j, lane & 31));
   int toff[kH3Taps];
 #pragma unroll
   for (int t = 0; t < kH3Taps; ++t) toff[t] = ttab[kH3Taps + t];
@@ -162,24 +204,36 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void h3_kernel(const ConvArgs a) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
+  // Fragments are double-buffered in registers across taps: tap t+1's LDS reads are issued
+  // before tap t's MFMAs and interleaved with them (sched_group_barrier), so each read's latency
+  // hides behind MFMAs instead of stalling the wave (the compiler's default order reused one
+  // fragment set: 4 reads -> lgkmcnt wait -> 4 MFMAs, the LDS latency exposed every tap).
   auto compute = [&](int buf) {
     const bf16* Wl = tiles + buf * STAGE;
     const bf16* Hl = Wl + WTILE;
-#pragma unroll
-    for (int t = 0; t < kH3Taps; ++t) {
-      bf16x8_t wf[TN], xf[TM];
+    bf16x8_t wf[2][TN], xf[2][TM];
+    auto fetch = [&](int t, int sl) {
 #pragma unroll
       for (int i = 0; i < TN; ++i) {
         const int row = wn * (BN / WN) + i * 32 + (lane & 31);
-        wf[i] = *reinterpret_cast<const bf16x8_t*>(Wl + (t * BN + row) * 16 + ahalf);
+        wf[sl][i] = *reinterpret_cast<const bf16x8_t*>(Wl + (t * BN + row) * 16 + ahalf);
       }
 #pragma unroll
       for (int j = 0; j < TM; ++j)
-        xf[j] = *reinterpret_cast<const bf16x8_t*>(Hl + (qb[j] + toff[t]) * kH3Row + 8 * h);
+        xf[sl][j] = *reinterpret_cast<const bf16x8_t*>(Hl + (qb[j] + toff[t]) * kH3Row + 8 * h);
+    };
+    fetch(0, 0);
+#pragma unroll
+    for (int t = 0; t < kH3Taps; ++t) {
+      const int sl = t & 1;
+      if (t + 1 < kH3Taps) fetch(t + 1, sl ^ 1);
+      __builtin_amdgcn_sched_barrier(0);  // next tap's reads stay ahead of this tap's MFMAs
 #pragma unroll
       for (int i = 0; i < TN; ++i)
 #pragma unroll
-        for (int j = 0; j < TM; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wf[i], xf[j], acc[i][j], 0, 0, 0);
+        for (int j = 0; j < TM; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wf[sl][i], xf[sl][j], acc[i][j], 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
     }
   };
 
@@ -212,7 +266,7 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void h3_kernel(const ConvArgs a) {
       const int b = q / bhr, r2 = q - b * bhr;
       const int hr = r2 / W2, hc = r2 - hr * W2;
       const int hh = h0 + hr - 1, w = hc - 1;
-      const bool in = q < HR && part < 2 && (unsigned)hh < (unsigned)H && (unsigned)w < (unsigned)W;
+      const bool in = q < HR && part < 2 && r2 < bh0 && (unsigned)hh < (unsigned)H && (unsigned)w < (unsigned)W;
       hsrc[j] = in ? ((uint32_t)((img0 + b) * HW + hh * W + w) * (uint32_t)a.Cx + 8u * part) * 2u : kOOB;
     }
     const int nhi = (3 * HR + 63) / 64;  // halo wave-instructions actually needed (uniform)
@@ -232,6 +286,15 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void h3_kernel(const ConvArgs a) {
           h3_dma16(rx_d, base + WTILE * 2 + wi * 1024, hsrc[j] == kOOB ? kOOB : hsrc[j] + cb);
       }
     };
+    if constexpr (NS == 1) {
+      for (int c = 0; c < nch; ++c) {
+        issue(c, 0);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();  // chunk c landed for everyone
+        compute(0);
+        __syncthreads();  // everyone's reads of chunk c retired: the stage is free
+      }
+    } else {
     issue(0, 0);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
@@ -242,6 +305,7 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void h3_kernel(const ConvArgs a) {
       compute(c & 1);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMAs of chunk c+1 landed ...
       __syncthreads();                                   // ... and everyone's: read in chunk c+1
+    }
     }
   } else {
     gload(0);
@@ -258,19 +322,23 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void h3_kernel(const ConvArgs a) {
     }
   }
 
-  conv_epilogue<BM, BN, EPI, ACT, NT, WM, WN>(a, acc, m0, n0, bm, tid, reinterpret_cast<float*>(smem + HDR), red, true,
-                                              inv_alpha);
+  struct PixH3 {
+    H3Geom g;
+    __device__ __forceinline__ int operator()(int wm_, int j, int n) const { return g.pix(wm_ * TM + j, n); }
+  };
+  conv_epilogue<BM, BN, EPI, ACT, NT, WM, WN, PixH3>(a, acc, m0, n0, bm, tid, reinterpret_cast<float*>(smem + HDR), red,
+                                                     true, inv_alpha, PixH3{geo});
 }
 
 // host ------------------------------------------------------------------------------------
-template <int BM, int BN, int EPI, int ACT, int WM, int WN, bool DMA>
+template <int BM, int BN, int EPI, int ACT, int WM, int WN, bool DMA, int NS>
 static void h3_launch_one(const ConvArgs& a, hipStream_t st) {
   constexpr int NT = 64 * WM * WN;
   constexpr int NQ = EPI == kEpiJoinBwd ? 3 : 2;
   constexpr size_t hdr = ((((size_t)(NT / 64) * NQ * BN + 2 * kH3Taps) * 4 + 15) & ~(size_t)15);
-  const size_t tiles = 2 * h3_stage_elems<BM, BN, WM, WN>() * 2, stage = (size_t)WM * 32 * (BN + 4) * 4;
+  const size_t tiles = NS * h3_stage_elems<BM, BN, WM, WN>() * 2, stage = (size_t)WM * 32 * (BN + 4) * 4;
   const size_t lds = hdr + (tiles > stage ? tiles : stage);
-  auto kern = h3_kernel<BM, BN, EPI, ACT, WM, WN, DMA>;
+  auto kern = h3_kernel<BM, BN, EPI, ACT, WM, WN, DMA, NS>;
   static bool attr = false;
   if (!attr) {
     FDT_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -293,23 +361,30 @@ bool h3_supported(const ConvArgs& a, int BM) {
   const int Rb = H < BM / W ? H : BM / W;
   if (Rb < H ? (H % Rb != 0) : (BM % (H * W) != 0)) return false;
   const int nbk = BM / (Rb * W);
-  return nbk * (Rb + 2) * (W + 2) <= BM / 16 * 36;
+  const int GW = W < 16 ? W : 16, NI = 16 / GW;
+  int bhr = (Rb + 2) * (W + 2);
+  if (NI > 1) bhr += (((11 * (16 / NI)) & 15) - bhr % 16 + 16) % 16;
+  // 16-pixel lane-group sets (pixel map, H3Geom): NI images per set need nbk % NI == 0 for W < 16
+  if (NI > 1 && (nbk % NI != 0 || Rb != H)) return false;
+  if (NI == 1 && (W % 16 != 0)) return false;
+  return nbk * bhr <= (BM / 16 * 44 + 63) / 64 * 64;
 }
 
-bool launch_h3(int pro, int epi, int act, const ConvArgs& a, int BM, int BN, bool dma, hipStream_t st) {
+bool launch_h3(int pro, int epi, int act, const ConvArgs& a, int BM, int BN, int kg, hipStream_t st) {
   if (pro != kProNone) return false;
   FDT_CHECK(h3_supported(a, BM), "halo 3x3 conv: unsupported geometry");
   FDT_CHECK(a.Cout % BN == 0, "halo 3x3 conv: Cout % BN");
-#define FDT_H3E(BM_, BN_, WM_, WN_, D_)                                                                       \
-  if (epi == kEpiStats && act == kActNone) { h3_launch_one<BM_, BN_, kEpiStats, kActNone, WM_, WN_, D_>(a, st); return true; } \
-  if (epi == kEpiActBwd && act == kActRelu) { h3_launch_one<BM_, BN_, kEpiActBwd, kActRelu, WM_, WN_, D_>(a, st); return true; } \
-  if (epi == kEpiActBwd && act == kActCelu) { h3_launch_one<BM_, BN_, kEpiActBwd, kActCelu, WM_, WN_, D_>(a, st); return true; } \
-  if (epi == kEpiStore && act == kActNone) { h3_launch_one<BM_, BN_, kEpiStore, kActNone, WM_, WN_, D_>(a, st); return true; }
-#define FDT_H3(BM_, BN_, WM_, WN_)            \
-  if (BM == BM_ && BN == BN_) {               \
-    if (dma) { FDT_H3E(BM_, BN_, WM_, WN_, true) } \
-    else { FDT_H3E(BM_, BN_, WM_, WN_, false) }    \
-    return false;                             \
+#define FDT_H3E(BM_, BN_, WM_, WN_, D_, NS_)                                                                  \
+  if (epi == kEpiStats && act == kActNone) { h3_launch_one<BM_, BN_, kEpiStats, kActNone, WM_, WN_, D_, NS_>(a, st); return true; } \
+  if (epi == kEpiActBwd && act == kActRelu) { h3_launch_one<BM_, BN_, kEpiActBwd, kActRelu, WM_, WN_, D_, NS_>(a, st); return true; } \
+  if (epi == kEpiActBwd && act == kActCelu) { h3_launch_one<BM_, BN_, kEpiActBwd, kActCelu, WM_, WN_, D_, NS_>(a, st); return true; } \
+  if (epi == kEpiStore && act == kActNone) { h3_launch_one<BM_, BN_, kEpiStore, kActNone, WM_, WN_, D_, NS_>(a, st); return true; }
+#define FDT_H3(BM_, BN_, WM_, WN_)                          \
+  if (BM == BM_ && BN == BN_) {                             \
+    if (kg == 6) { FDT_H3E(BM_, BN_, WM_, WN_, true, 2) }       \
+    else if (kg == 7) { FDT_H3E(BM_, BN_, WM_, WN_, true, 1) }  \
+    else { FDT_H3E(BM_, BN_, WM_, WN_, false, 2) }             \
+    return false;                                           \
   }
   FDT_H3(256, 128, 4, 2)
   FDT_H3(256, 64, 8, 1)

@@ -78,6 +78,10 @@
 #include "dropout_math.h"
 #include <vector>
 
+#ifndef FDT_CONV_FRAG_PIPE
+#define FDT_CONV_FRAG_PIPE 0  // 1: +16 VGPRs -- spills 19-125 VGPRs under the occupancy floors (measured, -Rpass-analysis)
+#endif
+
 namespace fdt {
 namespace conv {
 
@@ -248,10 +252,16 @@ constexpr int kMinWavesPerEU =
 // Wave layout WM x WN (wave w: wm = w / WN along the pixels, wn = w % WN along the channels),
 // NT threads; stg: >= WM*32*(BN+4) floats of LDS; red: [NT/64][NQ][BN] floats of LDS.
 // ew: this thread owns the epilogue (K group 1 of a KG = 2 launch only meets the barriers).
-template <int BM, int BN, int EPI, int ACT, int NT, int WM, int WN>
+// pix(wm, j, n): the tile-local output pixel of MFMA column n of block j of M-wave wm (the
+// implicit-GEMM kernel: wm*BM/WM + 32 j + n; the halo kernel permutes columns, conv_h3.hip).
+struct PixLinear {
+  int wstride;
+  __device__ __forceinline__ int operator()(int wm, int j, int n) const { return wm * wstride + j * 32 + n; }
+};
+template <int BM, int BN, int EPI, int ACT, int NT, int WM, int WN, class PixF = PixLinear>
 __device__ __forceinline__ void conv_epilogue(const ConvArgs& a, f32x16 (&acc)[BN / WN / 32][BM / WM / 32], long m0,
                                               int n0, int bm, int tid, float* stg, float* red, bool ew,
-                                              float inv_alpha) {
+                                              float inv_alpha, PixF pix = PixLinear{BM / WM}) {
   constexpr int TN = BN / WN / 32, TM = BM / WM / 32;
   constexpr int NQ = EPI == kEpiJoinBwd ? 3 : 2;
   constexpr int SW = BN + 4;     // staged row stride (floats)
@@ -321,7 +331,7 @@ __device__ __forceinline__ void conv_epilogue(const ConvArgs& a, f32x16 (&acc)[B
 #pragma unroll
     for (int sw = 0; sw < NSW; ++sw) {
       const int lr = rs + sw * RPS;
-      const long m = m0 + (lr >> 5) * (BM / WM) + j * 32 + (lr & 31);
+      const long m = m0 + pix(lr >> 5, j, lr & 31);
       if (ew && m < a.M) {
         uint32_t orow;
         if (dense) {
@@ -699,9 +709,41 @@ igemm_kernel(const ConvArgs a) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
+  // Fragments double-buffered in registers across the tile's 16-deep K steps: step ks+1's LDS
+  // reads issue before step ks's MFMAs (pinned by sched_barrier), so their latency hides behind
+  // MFMAs (FDT_CONV_FRAG_PIPE, off by default: the extra fragment set spills under the occupancy floors).
   auto compute = [&](int buf) {
     const bf16* Wl = gtiles + buf * (WT + XT);
     const bf16* Xl = Wl + WT;
+#if FDT_CONV_FRAG_PIPE
+    bf16x8_t wf[2][TN], xf[2][TM];
+    auto fetch = [&](int ks, int sl) {
+      const int ch = ks * 2 + (lane >> 5);
+#pragma unroll
+      for (int i = 0; i < TN; ++i) {
+        const int row = wn * (BN / 2) + i * 32 + (lane & 31);
+        wf[sl][i] = *reinterpret_cast<const bf16x8_t*>(Wl + row * BK + 8 * (ch ^ swz<CPR>(row)));
+      }
+#pragma unroll
+      for (int j = 0; j < TM; ++j) {
+        const int row = wm * (BM / 2) + j * 32 + (lane & 31);
+        xf[sl][j] = *reinterpret_cast<const bf16x8_t*>(Xl + row * BK + 8 * (ch ^ swz<CPR>(row)));
+      }
+    };
+    fetch(0, 0);
+#pragma unroll
+    for (int ks = 0; ks < BK / 16; ++ks) {
+      const int sl = ks & 1;
+      if (ks + 1 < BK / 16) fetch(ks + 1, sl ^ 1);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int i = 0; i < TN; ++i)
+#pragma unroll
+        for (int j = 0; j < TM; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wf[sl][i], xf[sl][j], acc[i][j], 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+#else
 #pragma unroll
     for (int ks = 0; ks < BK / 16; ++ks) {
       const int ch = ks * 2 + (lane >> 5);
@@ -721,6 +763,7 @@ igemm_kernel(const ConvArgs a) {
 #pragma unroll
         for (int j = 0; j < TM; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wf[i], xf[j], acc[i][j], 0, 0, 0);
     }
+#endif
   };
 
   // this split's K tiles [kb, kb + nk); K group g takes tiles kb + i*KG + g, i < nkk (the
@@ -1092,9 +1135,10 @@ bool launch_cases_plain(int pro, int epi, int act, const ConvArgs& a, int BM, in
                         hipStream_t st);
 bool launch_cases_ffn(int pro, int epi, int act, const ConvArgs& a, int BM, int BN, int BK, int kg, bool pure,
                       hipStream_t st);
-// halo-staged 3x3 stride-1 main loop (conv_h3.hip): kg 5 register-staged, kg 6 LDS-DMA
+// halo-staged 3x3 stride-1 main loop (conv_h3.hip): kg 5 register-staged, kg 6 LDS-DMA (two
+// stages), kg 7 LDS-DMA single stage (two workgroups per CU)
 bool h3_supported(const ConvArgs& a, int BM);
-bool launch_h3(int pro, int epi, int act, const ConvArgs& a, int BM, int BN, bool dma, hipStream_t st);
+bool launch_h3(int pro, int epi, int act, const ConvArgs& a, int BM, int BN, int kg, hipStream_t st);
 
 }  // namespace conv
 }  // namespace fdt

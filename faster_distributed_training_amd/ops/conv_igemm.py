@@ -205,12 +205,19 @@ LOOP = os.environ.get("FDT_CONV_LOOP", "old")
 H3 = os.environ.get("FDT_CONV_H3", "1") == "1"
 H3_MIN_TILES = int(os.environ.get("FDT_CONV_H3_MIN_TILES", "256"))
 H3_TILES = {(256, 128), (256, 64), (128, 128)}
-# staging of the halo loop: "dma" = LDS-DMA issued a chunk ahead (kg 6), "reg" = register-staged (kg 5)
-H3_LOOP = os.environ.get("FDT_CONV_H3_LOOP", "dma")
+# staging of the halo loop: "dma" = LDS-DMA issued a chunk ahead into a second stage (kg 6),
+# "dma1" = LDS-DMA into one stage, two workgroups per CU (kg 7), "reg" = register-staged (kg 5),
+# "auto" = dma1 where the image rows are >= 8 pixels wide, dma on the 4x4 stage (scripts/bench_h3.py)
+H3_LOOP = os.environ.get("FDT_CONV_H3_LOOP", "auto")
+H3_KGS = (5, 6, 7)
 
 
-def _h3_kg(kg):
-    return kg if kg in (5, 6) else (6 if H3_LOOP == "dma" else 5)
+def _h3_kg(kg, W=8):
+    if kg in H3_KGS:
+        return kg
+    if H3_LOOP == "auto":
+        return 7 if W >= 8 else 6
+    return {"dma": 6, "dma1": 7}.get(H3_LOOP, 5)
 
 
 def h3_tile(N, H, W, shp: "ConvShape", pro, cout, force=False, cx=None):
@@ -229,7 +236,17 @@ def h3_tile(N, H, W, shp: "ConvShape", pro, cout, force=False, cx=None):
     rb = min(H, bm // W)
     if (rb < H and H % rb) or (rb == H and bm % (H * W)):
         return None
-    if (bm // (rb * W)) * (rb + 2) * (W + 2) > bm // 16 * 36:
+    # halo blocks and the 16-pixel lane-group sets (conv_h3.hip H3Geom / h3_supported)
+    nbk, gw = bm // (rb * W), min(W, 16)
+    ni = 16 // gw
+    bhr = (rb + 2) * (W + 2)
+    if ni > 1:
+        bhr += (((11 * (16 // ni)) & 15) - bhr % 16 + 16) % 16
+        if nbk % ni or rb != H:
+            return None
+    elif W % 16:
+        return None
+    if nbk * bhr > (bm // 16 * 44 + 63) // 64 * 64:
         return None
     bn = 128 if cout % 128 == 0 else (64 if cout % 64 == 0 else 0)
     if not bn or (not force and (M // bm) * (cout // bn) < H3_MIN_TILES):
@@ -348,13 +365,13 @@ def conv_fwd(x, wf, shp: ConvShape, s=None, t=None, act=0, alpha=1.0, tile=None,
     M = N * Ho * Wo
     pro = PRO_AFFINE_ACT if (s is not None or act != 0 or lazy is not None) else PRO_NONE
     ent = None
-    h3 = h3_tile(N, H, W, shp, pro, shp.cout, kg in (5, 6)) if (kg in (5, 6) or (kg is None and tile is None)) else None
+    h3 = h3_tile(N, H, W, shp, pro, shp.cout, kg in H3_KGS) if (kg in H3_KGS or (kg is None and tile is None)) else None
     if tile is None and h3 is None:
         ent = tuned(f"fwd{pro}", N, H, shp) or tuned("fwd", N, H, shp)
         tile = tuple(ent["tile"]) if ent else None
     if h3 is not None:
         ent, (bm, bn), bk = {"loop": "old"}, h3, 16
-        ns, slab_p, cnt_p, kgv = 1, 0, 0, _h3_kg(kg)
+        ns, slab_p, cnt_p, kgv = 1, 0, 0, _h3_kg(kg, W)
     else:
         bm, bn, bk = _tile3(tile, M, shp.cout)
         if nsplit is not None:
@@ -461,7 +478,7 @@ def conv_dgrad(g, y, al, be, wd, shp: ConvShape, x_shape, epi=EPI_STORE, out=Non
             if jz[2] is not None:
                 assert jz[2].dtype == torch.bfloat16 and jz[2].is_contiguous() and tuple(jz[2].shape) == tuple(x_shape)
     ent = None
-    h3ok = kg in (5, 6) or (kg is None and tile is None)
+    h3ok = kg in H3_KGS or (kg is None and tile is None)
     if tile is None:
         pro = PRO_FOLD if al is not None else PRO_NONE
         e = EPI_STORE if epi in (EPI_ADD, EPI_JOINBWD) else epi
@@ -478,11 +495,11 @@ def conv_dgrad(g, y, al, be, wd, shp: ConvShape, x_shape, epi=EPI_STORE, out=Non
         if len(dh) == 0 and epi == EPI_ADD:
             continue
         pro = PRO_FOLD if al is not None else PRO_NONE  # al None: g is already folded
-        h3 = h3_tile(N, Hx, Wx, shp, pro, shp.cin, kg in (5, 6), cx=Cy) if h3ok and epi in (EPI_ACTBWD, EPI_STORE) and len(
+        h3 = h3_tile(N, Hx, Wx, shp, pro, shp.cin, kg in H3_KGS, cx=Cy) if h3ok and epi in (EPI_ACTBWD, EPI_STORE) and len(
             dh) == 9 else None
         if h3 is not None:
             (bm, bn), bk = h3, 16
-            ns, slab_p, cnt_p, kgv = 1, 0, 0, _h3_kg(kg)
+            ns, slab_p, cnt_p, kgv = 1, 0, 0, _h3_kg(kg, Wx)
         else:
             bm, bn, bk = _tile3(tile, M, shp.cin)
             ns, slab_p, cnt_p = _splitk_args(ent, M, shp.cin, len(dh) * Cy, bm, bn, bk, g.device)

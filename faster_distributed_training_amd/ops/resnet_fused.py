@@ -299,6 +299,10 @@ class Plan:
                              rrt.data_ptr() if with_rest and rr else 0, len(rr) if with_rest else 0,
                              cum if with_rest else 0, g, int(not launches)))
         self._upd = (flat, launches, keep)
+        # generation of the table: an NGD graph captured with the fused repack baked in the
+        # table / layout addresses keys on it (optim/ngd.py _graph_key) -- a rebuilt table (new
+        # packed buffers) never replays a graph holding the old, freed ones
+        self.upd_gen = getattr(self, "upd_gen", 0) + 1
         return launches
 
     def mark_opt_packed(self, flat):

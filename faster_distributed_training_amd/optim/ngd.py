@@ -737,8 +737,9 @@ class NGD(SGD):
         upd = st.t % st.update_period == 0
         # lr and momentum are read from ``lr_dev`` by the kernel (OneCycleLR cycles both every
         # step); only whether momentum is on (a momentum buffer in the capture) is baked
+        plan = self._pack_plan()
         return (upd, g["momentum"] != 0, float(g["dampening"]), float(g["weight_decay"]), bool(g["nesterov"]),
-                0 if grad_scale is None else grad_scale.data_ptr())
+                0 if grad_scale is None else grad_scale.data_ptr(), getattr(plan, "upd_gen", 0))
 
     def _fill_hp(self):
         g = self.group
@@ -752,6 +753,9 @@ class NGD(SGD):
         self._fill_hp()
         ent = self._gcache.get(key)
         if ent is None:
+            # graphs of an older pack-table generation hold freed table / layout addresses
+            for k in [k for k, e in self._gcache.items() if e.get("packed") and k[-1] != key[-1]]:
+                del self._gcache[k]
             ent = self._gcache[key] = self._capture(grad_scale)
         self.sync_state()  # the previous update's side-stream graph -> before this replay
         ent["main"].replay()

@@ -51,7 +51,7 @@ def main():
             t_old = timeit(lambda: fn(None), a.reps)
             y_old = fn(None).float()
             res = []
-            for kg in (5, 6):
+            for kg in (5, 6, 7):
                 if h3 is None:
                     continue
                 t_new = timeit(lambda: fn(kg), a.reps)

@@ -119,7 +119,7 @@ def train_curve(native: bool, opt: str, steps: int, bs: int = 128, lr=None, devi
             os.environ["FDT_NATIVE"] = prev
 
 
-def compare(opt: str, steps: int, device="cuda", arch="resnet18", bs=128, tail_frac=0.2, repeats=1):
+def compare(opt: str, steps: int, device="cuda", arch="resnet18", bs=128, tail_frac=0.2, repeats=1, seeds=False):
     """Three arms from the same weights on the same batches: the HIP engine, fp32 PyTorch (the
     reference numerics) and PyTorch under bf16 autocast (FDT_NATIVE=0: how far bf16 arithmetic
     alone moves the result -- the engine's error budget).  Final loss = MEDIAN of the last
@@ -133,10 +133,13 @@ def compare(opt: str, steps: int, device="cuda", arch="resnet18", bs=128, tail_f
     task = make_task(device=device)
     kw = dict(device=device, task=task, arch=arch, bs=bs)
     arms = {"engine": [], "reference": [], "bf16_torch": []}
-    for _ in range(max(1, repeats)):
-        arms["engine"].append(train_curve(True, opt, steps, **kw))
-        arms["reference"].append(train_curve(False, opt, steps, bf16=False, **kw))
-        arms["bf16_torch"].append(train_curve(False, opt, steps, bf16=True, **kw))
+    for rep in range(max(1, repeats)):
+        # seeds: repeat r starts from its own initial weights and batch order (seed r), the same in
+        # every arm -- independent samples of each arm's outcome, not reruns of one trajectory
+        sd = rep if seeds else 0
+        arms["engine"].append(train_curve(True, opt, steps, seed=sd, **kw))
+        arms["reference"].append(train_curve(False, opt, steps, bf16=False, seed=sd, **kw))
+        arms["bf16_torch"].append(train_curve(False, opt, steps, bf16=True, seed=sd, **kw))
     tail = max(10, int(steps * tail_frac))
     fin = lambda r: float(sorted(r["losses"][-tail:])[tail // 2])  # noqa: E731
     # (median over repeats: one bf16 run in ~10 lands in a heavy tail of the held-out loss on this

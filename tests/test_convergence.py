@@ -3,9 +3,9 @@ steps on a learnable synthetic CIFAR task (scripts/convergence.py; VERDICT r3 #7
 
 The error budget is what bf16 arithmetic alone costs: a third run, plain PyTorch under bf16
 autocast (FDT_NATIVE=0) from the same weights on the same batches.  The engine must land at
-most twice as far from the fp32 run as that run does (plus a small epsilon), on the HELD-OUT
-loss and accuracy of the final weights (medians over three repeats of every arm), or twice the fp32
-run's own repeat spread if that is larger -- no absolute floor.  (The per-step training losses
+most twice as far from the fp32 run as that run does (plus a small epsilon: half the fp32 loss,
+at most 0.05), on the HELD-OUT loss and accuracy of the final weights (medians over five seeds
+of every arm), or twice the fp32 run's own seed-to-seed spread if that is larger.  (The per-step training losses
 at the end are heavy-tailed -- 0.005-0.17 step to step in every arm -- so their tail mean or
 median swung by 5-8x between repeats of identical code, profiles/r5/convergence_flaky.txt;
 the held-out loss of the final weights is a smooth function of them.)  Every run must also
@@ -21,27 +21,27 @@ pytestmark = pytest.mark.gpu
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
-# every arm runs three times and is compared by its median over the repeats (one bf16 run in ~10 --
-# engine or PyTorch autocast -- lands in a heavy tail of the held-out loss on this task,
-# profiles/r5/convergence_spread_resnet50.txt); the budget is bf16
-# arithmetic's distance from fp32 OR the fp32 reference's own repeat-to-repeat spread measured in
-# the same test, whichever is larger (the fp32 held-out loss alone moved 0.035-0.29 across
-# repeats of identical code: non-deterministic GPU reductions amplified over 300 steps, the
-# cross entropy dominated by a few confident mistakes -- profiles/r5/convergence_flaky.txt)
-REPEATS = 3
-# Known gap (README "Known gaps"): pooled over the round-5 GPU runs, the engine's held-out cross
-# entropy on ResNet-18 / MADGRAD has a median ~0.07 against ~0.05 for PyTorch bf16 autocast and
-# ~0.04 for fp32, with a heavier tail (medians of three repeats up to 0.14); its held-out ACCURACY
-# stays within the bf16 / fp32-spread budget.  The loss epsilon covers that measured gap so the
-# test flags regressions beyond it, not the gap itself.
-EPS_LOSS = 0.12   # absolute, on the held-out mean cross entropy
-EPS_ACC = 0.02    # 20 of 1024 held-out samples
+# Every arm runs from SEEDS different initial weights / batch orders (the same seeds in every
+# arm) and is compared by its median over them.  profiles/r6/convergence_ablation.txt (ResNet-18 /
+# MADGRAD, 5 seeds, 6 arms): single held-out cross entropies range 0.012-0.13 in EVERY arm --
+# fp32 0.035-0.084 (median 0.056), PyTorch bf16 autocast 0.015-0.075 (0.032), the engine 0.015-0.13
+# (0.035), the engine with the round-5 CELU derivative 0.012-0.041 (0.037), engine + PyTorch
+# MADGRAD 0.025-0.065, PyTorch + HIP MADGRAD 0.027-0.125 -- and the engine-trained weights give
+# the same loss through the fp32 eval forward (trained running statistics included).  The
+# round-5 "engine gap" (three repeats of ONE seed) was this spread, not a systematic offset; the
+# CELU-join derivative (now exp(z/alpha) from the fp32 pre-activation) is pinned by its own
+# kernel test (tests/test_conv_kernels.py::test_celu_join_backward_uses_preactivation).
+SEEDS = 5
+EPS_LOSS_REL = 0.5    # slack, relative to the fp32 median held-out cross entropy ...
+EPS_LOSS_MAX = 0.05   # ... and never above this (absolute)
+EPS_ACC = 0.02        # 20 of 1024 held-out samples
 
 
 @pytest.mark.parametrize("opt,arch", [("madgrad", "resnet18"), ("ngd", "resnet18"), ("madgrad", "resnet50")])
+@pytest.mark.timeout(900)
 def test_engine_converges_like_fp32_reference(cuda, opt, arch):
     from scripts.convergence import compare
-    r = compare(opt, 300, arch=arch, bs=128, repeats=REPEATS)
+    r = compare(opt, 300, arch=arch, bs=128, repeats=SEEDS, seeds=True)
     print({k: v for k, v in r.items() if not k.endswith("curve")})
     # every run learns the task ...
     for k in ("reference_final_loss", "engine_final_loss", "bf16_torch_final_loss"):
@@ -49,7 +49,8 @@ def test_engine_converges_like_fp32_reference(cuda, opt, arch):
     # ... and the engine lands as close to fp32 as bf16 arithmetic or fp32's own spread allows
     d_loss = abs(r["engine_test_loss"] - r["reference_test_loss"])
     b_loss = max(abs(r["bf16_torch_test_loss"] - r["reference_test_loss"]), r["reference_spread_loss"])
-    assert d_loss <= 2 * b_loss + EPS_LOSS, (d_loss, b_loss)
+    eps = min(EPS_LOSS_MAX, EPS_LOSS_REL * r["reference_test_loss"])
+    assert d_loss <= 2 * b_loss + eps, (d_loss, b_loss, eps)
     d_acc = abs(r["engine_test_acc"] - r["reference_test_acc"])
     b_acc = max(abs(r["bf16_torch_test_acc"] - r["reference_test_acc"]), r["reference_spread_acc"])
     assert d_acc <= 2 * b_acc + EPS_ACC, (d_acc, b_acc)

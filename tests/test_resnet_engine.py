@@ -50,7 +50,8 @@ def test_engine_at_shipped_batch128_config(cuda, arch):
     finally:
         CI.LAUNCH_LOG = None
     convs = [e for e in log if e[1].startswith("128:")]
-    assert convs and all(e[2] for e in convs), [e for e in convs if not e[2]][:5]  # every launch tuned
+    # every launch tuned, or the halo 3x3 loop (kg 5-7: chosen by geometry, not by the table)
+    assert convs and all(e[2] or e[5] in (5, 6, 7) for e in convs), [e for e in convs if not e[2]][:5]
     assert any(e[4] > 1 for e in convs), "no split-K launch"
     assert any(e[5] == 2 for e in convs), "no K-group launch"
     print(f"{len(convs)} conv launches, {sum(e[4] > 1 for e in convs)} split-K, {sum(e[5] == 2 for e in convs)} K-group")
@@ -91,9 +92,11 @@ def _train_step_vs_reference(cuda, arch, batch=64):
         assert e_e <= max(2.0 * e_b, 1.5e-2 if n == "fc.bias" else 5e-3), (n, e_e, e_b)
     worst.sort(reverse=True)
     print("worst engine/autocast gradient error ratios:", [(n, round(r, 2)) for r, n, _, _ in worst[:5]])
-    for (n, br), (_, be) in zip(m_ref.named_buffers(), m_eng.named_buffers()):
+    # BN running statistics: within 2x what the bf16-autocast reference run's own update misses
+    # (plus 1e-3: running_var of channels whose batch variance is ~exact in both)
+    for (n, br), (_, be), (_, bb) in zip(m_ref.named_buffers(), m_eng.named_buffers(), m_rb.named_buffers()):
         if br.dtype.is_floating_point:
-            assert rel(be, br) < 2e-2, n
+            assert rel(be, br) <= max(2.0 * rel(bb, br), 1e-3), (n, rel(be, br), rel(bb, br))
         else:
             assert int(be) == int(br), n
 
@@ -112,6 +115,42 @@ def test_engine_eval_matches_reference(cuda, arch):
     # fresh running stats (mean 0, var 1) leave the strided-block activations
     # un-normalised in eval, which amplifies rounding: budget relative to bf16 autocast
     assert e_eng < max(2.0 * e_ref, 3e-2), (e_eng, e_ref)
+
+
+@pytest.mark.parametrize("arch", ["resnet18", "resnet50"])
+def test_engine_eval_after_training_matches_fp32(cuda, arch):
+    """Eval with TRAINED running statistics: 50 engine training steps
+    (SGD + momentum on a learnable random-label-free task), then the engine's eval forward vs
+    the fp32 PyTorch eval of the same weights and buffers, within 2x the error of PyTorch's own
+    bf16-autocast eval of them."""
+    m_ref, m_eng = _pair(arch, cuda)
+    torch.manual_seed(2)
+    protos = torch.randn(10, 3, 32, 32, device=cuda)
+    opt = torch.optim.SGD(m_eng.parameters(), lr=0.02, momentum=0.9)
+    m_eng.train()
+    for _ in range(50):
+        y = torch.randint(0, 10, (64,), device=cuda)
+        x = protos[y] + 0.5 * torch.randn(64, 3, 32, 32, device=cuda)
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            out = m_eng(x)
+        F.cross_entropy(out.float(), y).backward()
+        opt.step()
+        opt.zero_grad(set_to_none=True)
+    m_ref.load_state_dict(m_eng.state_dict())
+    rv = [b for n, b in m_ref.named_buffers() if n.endswith("running_var")]
+    assert any(float((v - 1).abs().max()) > 0.05 for v in rv), "running statistics did not move"
+    m_ref.eval()
+    m_eng.eval()
+    y = torch.randint(0, 10, (128,), device=cuda)
+    x = protos[y] + 0.5 * torch.randn(128, 3, 32, 32, device=cuda)
+    with torch.no_grad():
+        out_r = m_ref(x)
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            out_rb = m_ref(x)
+            out_e = m_eng(x)
+    e_eng, e_ref = rel(out_e, out_r), rel(out_rb, out_r)
+    assert e_eng < max(2.0 * e_ref, 1e-2), (e_eng, e_ref)
+    assert (out_e.float().argmax(1) == out_r.argmax(1)).float().mean() > 0.97
 
 
 def test_engine_grad_ready_hooks_fire(cuda):
