@@ -46,6 +46,8 @@ def parse():
                     help="--fsdp: parameter all-gather wire / compute-copy precision (masters stay fp32)")
     ap.add_argument("--fsdp-offload", action="store_true",
                     help="--fsdp: shards + optimizer state in pinned host memory (the reference's CPUOffload; eager)")
+    ap.add_argument("--fsdp-offload-optimizer", default="device", choices=["device", "host"],
+                    help="--fsdp-offload: optimizer on the GPU over the staged shard, or on the host (reference)")
     ap.add_argument("--fsdp-wrap", default="model", choices=["sublayer", "model"],
                     help="--model transformer --fsdp: wrap units (sublayers, or the whole model as one unit "
                          "like the reference's FSDP(model))")
@@ -134,7 +136,7 @@ def main():
                        fast_path=False if args.no_native else None, graphs=not args.no_graphs,
                        deterministic=args.deterministic, force_sharded=args.sharded_ngd, force_ddp=args.ddp,
                        fsdp_param_dtype=args.fsdp_param_dtype, fsdp_schedule=args.fsdp_schedule,
-                       fsdp_offload=args.fsdp_offload,
+                       fsdp_offload=args.fsdp_offload, fsdp_offload_optimizer=args.fsdp_offload_optimizer,
                        **({} if args.first_bucket_mb is None else {"first_bucket_mb": args.first_bucket_mb}))
     tr = ResNetTrainer(cfg)
     dev = tr.device
@@ -167,11 +169,14 @@ def main():
         if i == 0:
             _first_step_comm()
     sync()
+    stager = getattr(tr.train_loader, "stager", None)
+    w0 = stager.wait_s if stager is not None else 0.0
     t0 = time.perf_counter()
     for _ in range(args.steps):
         x, y = next(it)
         tr.train_step(x, y)
     host = time.perf_counter() - t0  # host submission time of the K steps (no sync inside)
+    waited = (stager.wait_s - w0) if stager is not None else 0.0
     sync()
     elapsed = time.perf_counter() - t0
     if dist.is_initialized():
@@ -200,6 +205,7 @@ def main():
                    "native_kernels": native, "hip_graphs": graphs, "deterministic": args.deterministic},
         "epoch_time_s": round(50000.0 / value, 3),
         "host_ms_per_step": round(host / args.steps * 1e3, 3),
+        "host_busy_ms_per_step": round((host - waited) / args.steps * 1e3, 3),
         "peak_mem_gb": round(torch.cuda.max_memory_allocated() / 2**30, 2) if cuda else None,
     }
     _sharding_fields(tr, rec)
@@ -277,6 +283,8 @@ def _sharding_fields(tr, rec):
         cfg["fsdp_schedule"] = "shard_grad_op" if (tr.fsdp.static and not tr.fsdp.ring) else "full_shard"
         cfg["fsdp_param_dtype"] = str(tr.fsdp.param_dtype or torch.float32).replace("torch.", "")
         cfg["fsdp_offload"] = bool(tr.fsdp.offload)
+        if tr.fsdp.offload:
+            cfg["fsdp_offload_optimizer"] = "device" if tr.fsdp.opt_on_device else "host"
     elif tr.zero is not None:
         cfg["optimizer_sharding"] = "ngd-owner-shards (bucketed all-reduce overlapped with backward + all-gather)"
         cfg["owner_shard_numel"] = int(tr.zero.view.numel)
@@ -303,7 +311,7 @@ def bench_transformer(args):
                             ngd=True, precision=args.precision, length_buckets=buckets,
                             bucket_mb=args.bucket_mb, fsdp=args.fsdp, epoch=1, fsdp_param_dtype=args.fsdp_param_dtype,
                             fsdp_schedule=args.fsdp_schedule, fsdp_wrap=args.fsdp_wrap,
-                            fsdp_offload=args.fsdp_offload)
+                            fsdp_offload=args.fsdp_offload, fsdp_offload_optimizer=args.fsdp_offload_optimizer)
     tr = TransformerTrainer(cfg)
     longest = int(tr.train_loader.store.lengths.max())
     assert longest <= buckets[-1], f"largest bucket {buckets[-1]} would truncate samples of length {longest}"
@@ -325,9 +333,12 @@ def bench_transformer(args):
             _first_step_comm()
     sync()
     t0 = time.perf_counter()
+    stager = getattr(tr.train_loader, "stager", None)
+    w0 = stager.wait_s if stager is not None else 0.0
     for _ in range(args.steps):
         tr.train_step(*next(it))
     host = time.perf_counter() - t0
+    waited = (stager.wait_s - w0) if stager is not None else 0.0
     sync()
     elapsed = time.perf_counter() - t0
     if dist.is_initialized():
@@ -344,7 +355,10 @@ def bench_transformer(args):
                       "truncation": "none (pad to the smallest bucket >= the batch's longest sample)",
                       "parallelism": f"{'fsdp' if args.fsdp else 'dp'}{world}", "optimizer": "ngd"},
            "peak_mem_gb": round(torch.cuda.max_memory_allocated() / 2**30, 2) if cuda else None,
-           "host_ms_per_step": round(host / args.steps * 1e3, 3)}
+           "host_ms_per_step": round(host / args.steps * 1e3, 3),
+           # host_ms minus the time the training thread sat blocked on the staging ring's
+           # backpressure (waiting for the GPU to free a slot): the host's own work per step
+           "host_busy_ms_per_step": round((host - waited) / args.steps * 1e3, 3)}
     rec["config"]["hip_graphs"] = bool(tr._graphs_on()) if cuda else False
     _sharding_fields(tr, rec)
     _dist_fields(rec)

@@ -36,7 +36,7 @@ namespace fdt {
 namespace conv {
 
 constexpr int kH3Taps = 9;
-constexpr int kH3Row = 24;  // halo row stride in bf16 elements (48 B)
+constexpr int kH3Row = 16;  // halo row stride in bf16 elements (32 B: the chunk's 16 channels)
 
 // one 16-B-per-lane LDS-DMA piece: lane l fills lds + 16 l (device-only helper)
 __device__ __forceinline__ void h3_dma16(__amdgpu_buffer_rsrc_t r, void* lds, uint32_t off) {
@@ -44,20 +44,22 @@ __device__ __forceinline__ void h3_dma16(__amdgpu_buffer_rsrc_t r, void* lds, ui
 }
 
 // Halo blocks (one per image, or one per Rb-row slab of a larger image) are laid out every bhr
-// rows, bhr = (Rb+2)(W+2) padded so that 3*bhr = 16/NI (mod 16): see H3Geom.
+// rows, bhr = (Rb+2)(W+2) padded so that bhr = 16/NI (mod 16): see H3Geom.
 template <int BM>
-constexpr int h3_halo_rows_max() {  // BM/16 images of 4x4 -> 44-row (padded 6x6) blocks, rounded up
-  return (BM / 16 * 44 + 63) / 64 * 64;                           // to 64 rows (whole 1-KiB DMA pieces)
+constexpr int h3_halo_rows_max() {  // BM/16 images of 4x4 -> 36-row (6x6) blocks (BM = 128 / 256:
+  return BM / 16 * 36;              // 288 / 576 rows, whole 1-KiB LDS-DMA pieces of 32 rows)
 }
 
 // Tile geometry + the MFMA-column -> pixel map of the halo loop.  A ds_read_b128 serves a wave in
-// four fixed 16-lane groups ({0-3,12-15,20-27}, {4-11,16-19,28-31} and the same +32); a 48-B halo
-// row = 3 bank quads, so 16 CONSECUTIVE halo rows hit 16 distinct quads (3q mod 16).  Columns are
+// four fixed 16-lane groups ({0-3,12-15,20-27}, {4-11,16-19,28-31} and the same +32); a 32-B halo
+// row = 2 bank quads whose 16-B halves are XOR-swizzled by row bit 3 (quad of row q, half h:
+// 2q + (h ^ q>>3 & 1) mod 16), so 16 CONSECUTIVE halo rows hit 16 distinct quads.  Columns are
 // therefore permuted so each lane group reads a 16-pixel set: 16 consecutive pixels of one image
 // row (W >= 16), or one row segment of W pixels from each of NI = 16/W images (W = 8, 4) whose
-// halo blocks sit bhr rows apart with 3*bhr = 16/NI (mod 16) -- the NI segments then take
-// disjoint quad sets.  Conflict-free for every tap (a tap shifts every row alike); the identity
-// column order conflicts 2-3x at W = 16 / 8 / 4 (measured 27.5 % bank-conflict cycles, 16x16).
+// halo blocks sit bhr rows apart with bhr = 16/NI (mod 16) -- the NI segments then take disjoint
+// quad sets.  Conflict-free for every tap (a tap shifts every row alike; checked exhaustively
+// for every CIFAR geometry); the identity column order on 48-B rows conflicted 2-3x at W = 16 /
+// 8 / 4 (measured 27.5 % bank-conflict cycles, 16x16).
 struct H3Geom {
   int W, Rb, W2, bhr, NI, GW, SPR;
   __device__ __forceinline__ H3Geom(int W_, int H_, int BM) {
@@ -68,10 +70,7 @@ struct H3Geom {
     NI = 16 / GW;
     SPR = W_ / GW;
     int b = (Rb + 2) * W2;
-    if (NI > 1) {
-      const int want = (11 * (16 / NI)) & 15;  // 3^-1 = 11 (mod 16)
-      b += (want - b % 16 + 16) % 16;
-    }
+    if (NI > 1) b += ((16 / NI) - b % 16 + 16) % 16;
     bhr = b;
   }
   // tile-local pixel of MFMA column n of 32-column block blk
@@ -83,6 +82,8 @@ struct H3Geom {
     const int img = NI * gi + i / GW, col = seg * GW + i % GW;
     return img * (Rb * W) + r * W + col;
   }
+  // bf16 element offset of half h of halo row q (the XOR swizzle)
+  static __device__ __forceinline__ int elem(int q, int h) { return q * kH3Row + 8 * (h ^ ((q >> 3) & 1)); }
   __device__ __forceinline__ int halo_row(int p) const {
     const int b = p / (Rb * W), r = (p / W) % Rb, c = p % W;
     return b * bhr + (r + 1) * W2 + c + 1;
@@ -98,7 +99,7 @@ constexpr size_t h3_stage_elems() { return (size_t)kH3Taps * BN * 16 + (size_t)h
 // (load -> barrier -> MFMAs -> barrier), small enough for TWO workgroups per CU, whose phases
 // interleave -- and whose prologues / epilogues overlap the other's main loop.
 template <int BM, int BN, int EPI, int ACT, int WM, int WN, bool DMA, int NS = 2>
-__global__ __launch_bounds__(64 * WM * WN, NS == 1 ? 4 : 1) void h3_kernel(const ConvArgs a) {
+__global__ __launch_bounds__(64 * WM * WN, (NS == 1 || BN == 64) ? 4 : 1) void h3_kernel(const ConvArgs a) {
   static_assert(NS == 2 || (NS == 1 && DMA), "single-stage: LDS-DMA staging");
   constexpr int NT = 64 * WM * WN;
   constexpr int TN = BN / WN / 32, TM = BM / WM / 32;
@@ -166,7 +167,7 @@ __global__ __launch_bounds__(64 * WM * WN, NS == 1 ? 4 : 1) void h3_kernel(const
     const int h = h0 + hr - 1, w = hc - 1;
     const bool in = v && r2 < bh0 && (unsigned)h < (unsigned)H && (unsigned)w < (unsigned)W;
     hoff[j] = in ? ((uint32_t)((img0 + b) * HW + h * W + w) * (uint32_t)a.Cx + 8u * lh) * 2u : kOOB;
-    hdst[j] = v ? WTILE + q * kH3Row + 8 * lh : -1;  // padding rows store the zeros the OOB load returned
+    hdst[j] = v ? WTILE + H3Geom::elem(q, lh) : -1;  // padding rows store the zeros the OOB load returned
   }
   // ---- per-thread B-fragment halo rows (tap (0, 0)) and the nine tap offsets
   int qb[TM];
@@ -220,7 +221,7 @@ __global__ __launch_bounds__(64 * WM * WN, NS == 1 ? 4 : 1) void h3_kernel(const
       }
 #pragma unroll
       for (int j = 0; j < TM; ++j)
-        xf[sl][j] = *reinterpret_cast<const bf16x8_t*>(Hl + (qb[j] + toff[t]) * kH3Row + 8 * h);
+        xf[sl][j] = *reinterpret_cast<const bf16x8_t*>(Hl + H3Geom::elem(qb[j] + toff[t], h));
     };
     fetch(0, 0);
 #pragma unroll
@@ -240,13 +241,14 @@ __global__ __launch_bounds__(64 * WM * WN, NS == 1 ? 4 : 1) void h3_kernel(const
   const int nch = a.Cx >> 4;
   if constexpr (DMA) {
     // LDS image = piece-linear: weight piece (tap*BN + n)*2 + physical half at byte 16*piece;
-    // halo piece q*3 + part (part 2 = the row's pad slot) at WTILE*2 + 16*piece.  A wave
+    // halo piece q*2 + physical half at WTILE*2 + 16*piece (the lane filling physical half ph
+    // fetches logical half ph ^ (q>>3 & 1): the swizzle applied on the source side).  A wave
     // instruction fills 64 consecutive pieces (1 KiB at the wave-uniform M0 base); WP is a
-    // multiple of 64 (every weight instruction full) and the halo region holds 3*HRM pieces, a
+    // multiple of 64 (every weight instruction full) and the halo region holds 2*HRM pieces, a
     // multiple of 64, so a partly-valid last halo instruction's extra lanes land inside it
     // (zeros from the OOB offset, rows nobody reads).
-    static_assert(WP % 64 == 0 && (3 * HRM) % 64 == 0, "whole 1-KiB DMA pieces");
-    constexpr int NWI = WP / 64, NHI = 3 * HRM / 64;  // wave-instructions per chunk
+    static_assert(WP % 64 == 0 && (2 * HRM) % 64 == 0, "whole 1-KiB DMA pieces");
+    constexpr int NWI = WP / 64, NHI = 2 * HRM / 64;  // wave-instructions per chunk
     constexpr int NW = NT / 64;
     const int wv = __builtin_amdgcn_readfirstlane(wid);
     uint32_t wsrc[(NWI + NW - 1) / NW], hsrc[(NHI + NW - 1) / NW];
@@ -262,14 +264,14 @@ __global__ __launch_bounds__(64 * WM * WN, NS == 1 ? 4 : 1) void h3_kernel(const
 #pragma unroll
     for (int j = 0; j * NW < NHI; ++j) {
       const int piece = (j * NW + wv) * 64 + lane;
-      const int q = piece / 3, part = piece - q * 3;
+      const int q = piece >> 1, part = (piece & 1) ^ ((q >> 3) & 1);  // logical half
       const int b = q / bhr, r2 = q - b * bhr;
       const int hr = r2 / W2, hc = r2 - hr * W2;
       const int hh = h0 + hr - 1, w = hc - 1;
-      const bool in = q < HR && part < 2 && r2 < bh0 && (unsigned)hh < (unsigned)H && (unsigned)w < (unsigned)W;
+      const bool in = q < HR && r2 < bh0 && (unsigned)hh < (unsigned)H && (unsigned)w < (unsigned)W;
       hsrc[j] = in ? ((uint32_t)((img0 + b) * HW + hh * W + w) * (uint32_t)a.Cx + 8u * part) * 2u : kOOB;
     }
-    const int nhi = (3 * HR + 63) / 64;  // halo wave-instructions actually needed (uniform)
+    const int nhi = (2 * HR + 63) / 64;  // halo wave-instructions actually needed (uniform)
     auto issue = [&](int ch, int buf) {
       const uint32_t cb = (uint32_t)ch * 32u;
       char* base = reinterpret_cast<char*>(tiles + buf * STAGE);
@@ -286,12 +288,15 @@ __global__ __launch_bounds__(64 * WM * WN, NS == 1 ? 4 : 1) void h3_kernel(const
           h3_dma16(rx_d, base + WTILE * 2 + wi * 1024, hsrc[j] == kOOB ? kOOB : hsrc[j] + cb);
       }
     };
+    // cost probes (scripts/h3_probe.py; a.dbg, wave-uniform): bit 1 skips the DMA, bit 2 the MFMA
+    // phase -- timing only, the output is garbage
+    const bool no_dma = a.dbg & 2, no_mma = a.dbg & 4;
     if constexpr (NS == 1) {
       for (int c = 0; c < nch; ++c) {
-        issue(c, 0);
+        if (!no_dma) issue(c, 0);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();  // chunk c landed for everyone
-        compute(0);
+        if (!no_mma) compute(0);
         __syncthreads();  // everyone's reads of chunk c retired: the stage is free
       }
     } else {
@@ -301,8 +306,8 @@ __global__ __launch_bounds__(64 * WM * WN, NS == 1 ? 4 : 1) void h3_kernel(const
     for (int c = 0; c < nch; ++c) {
       // buffer (c+1)&1 was last read in chunk c-1: every wave retired those reads before the
       // barrier that ended it
-      if (c + 1 < nch) issue(c + 1, (c + 1) & 1);
-      compute(c & 1);
+      if (c + 1 < nch && !no_dma) issue(c + 1, (c + 1) & 1);
+      if (!no_mma) compute(c & 1);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMAs of chunk c+1 landed ...
       __syncthreads();                                   // ... and everyone's: read in chunk c+1
     }
@@ -322,6 +327,7 @@ __global__ __launch_bounds__(64 * WM * WN, NS == 1 ? 4 : 1) void h3_kernel(const
     }
   }
 
+  if (a.dbg & 8) return;  // cost probe: no epilogue (every wave returns: no barrier is left waiting)
   struct PixH3 {
     H3Geom g;
     __device__ __forceinline__ int operator()(int wm_, int j, int n) const { return g.pix(wm_ * TM + j, n); }
@@ -363,11 +369,11 @@ bool h3_supported(const ConvArgs& a, int BM) {
   const int nbk = BM / (Rb * W);
   const int GW = W < 16 ? W : 16, NI = 16 / GW;
   int bhr = (Rb + 2) * (W + 2);
-  if (NI > 1) bhr += (((11 * (16 / NI)) & 15) - bhr % 16 + 16) % 16;
+  if (NI > 1) bhr += ((16 / NI) - bhr % 16 + 16) % 16;
   // 16-pixel lane-group sets (pixel map, H3Geom): NI images per set need nbk % NI == 0 for W < 16
   if (NI > 1 && (nbk % NI != 0 || Rb != H)) return false;
   if (NI == 1 && (W % 16 != 0)) return false;
-  return nbk * bhr <= (BM / 16 * 44 + 63) / 64 * 64;
+  return nbk * bhr <= BM / 16 * 36;
 }
 
 bool launch_h3(int pro, int epi, int act, const ConvArgs& a, int BM, int BN, int kg, hipStream_t st) {

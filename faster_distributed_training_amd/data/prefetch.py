@@ -28,6 +28,7 @@ from __future__ import annotations
 
 import queue
 import threading
+import time
 
 import numpy as np
 import torch
@@ -61,6 +62,10 @@ class PinnedStager:
         self.copy_stream.wait_event(ev)
         self.next = 0
         self.staged = 0  # batches staged (tests / diagnostics)
+        # host seconds spent blocked in acquire(): the ring's backpressure (the worker waits for
+        # the GPU to release a slot before it can issue the next copy) -- time the training
+        # thread is idle because the GPU is behind, not host work (bench.py host_busy_ms_per_step)
+        self.wait_s = 0.0
         self._keep: list = [None] * nslots  # sources + release event alive until the job is issued
 
     def stage(self, arrays):
@@ -99,7 +104,9 @@ class PinnedStager:
     def acquire(self, s: int):
         """Order the current compute stream after slot ``s``'s H2D copy (device-side wait; the
         host only waits for the worker to have ISSUED the copy)."""
+        t0 = time.perf_counter()
         self.pf.wait(s, _native.stream_ptr(self.device))
+        self.wait_s += time.perf_counter() - t0
         self._keep[s] = None
 
     def release(self, s: int):

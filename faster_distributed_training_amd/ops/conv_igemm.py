@@ -205,9 +205,12 @@ LOOP = os.environ.get("FDT_CONV_LOOP", "old")
 H3 = os.environ.get("FDT_CONV_H3", "1") == "1"
 H3_MIN_TILES = int(os.environ.get("FDT_CONV_H3_MIN_TILES", "256"))
 H3_TILES = {(256, 128), (256, 64), (128, 128)}
-# staging of the halo loop: "dma" = LDS-DMA issued a chunk ahead into a second stage (kg 6),
-# "dma1" = LDS-DMA into one stage, two workgroups per CU (kg 7), "reg" = register-staged (kg 5),
-# "auto" = dma1 where the image rows are >= 8 pixels wide, dma on the 4x4 stage (scripts/bench_h3.py)
+# staging of the halo loop: "dma" = LDS-DMA issued a chunk ahead into a second stage (kg 6, 128
+# output channels per workgroup: one workgroup per CU), "dma64" = the same at 64 output channels
+# per workgroup (78 KB of LDS: TWO workgroups per CU, each double-buffered), "dma1" = LDS-DMA
+# into one stage, two workgroups per CU (kg 7; the probe shows the two phase-locked: they load
+# and compute together, profiles/r6/h3_probe_1024.txt), "reg" = register-staged (kg 5);
+# "auto" = the measured per-shape choice (h3_auto)
 H3_LOOP = os.environ.get("FDT_CONV_H3_LOOP", "auto")
 H3_KGS = (5, 6, 7)
 
@@ -215,12 +218,10 @@ H3_KGS = (5, 6, 7)
 def _h3_kg(kg, W=8):
     if kg in H3_KGS:
         return kg
-    if H3_LOOP == "auto":
-        return 7 if W >= 8 else 6
-    return {"dma": 6, "dma1": 7}.get(H3_LOOP, 5)
+    return {"dma": 6, "dma64": 6, "auto": 6, "dma1": 7}.get(H3_LOOP, 5)
 
 
-def h3_tile(N, H, W, shp: "ConvShape", pro, cout, force=False, cx=None):
+def h3_tile(N, H, W, shp: "ConvShape", pro, cout, force=False, cx=None, bn=None):
     """(BM, BN) of the halo 3x3 loop for this launch, or None (csrc/kernels/conv_h3.hip
     h3_supported: 3x3 pad-1 stride-1, prologue-free, whole image rows per 256-pixel tile).
     ``force`` (an explicit kg 5): ignore FDT_CONV_H3 and the small-grid cut-off.  ``cx``: the
@@ -241,17 +242,41 @@ def h3_tile(N, H, W, shp: "ConvShape", pro, cout, force=False, cx=None):
     ni = 16 // gw
     bhr = (rb + 2) * (W + 2)
     if ni > 1:
-        bhr += (((11 * (16 // ni)) & 15) - bhr % 16 + 16) % 16
+        bhr += ((16 // ni) - bhr % 16 + 16) % 16
         if nbk % ni or rb != H:
             return None
     elif W % 16:
         return None
-    if nbk * bhr > (bm // 16 * 44 + 63) // 64 * 64:
+    if nbk * bhr > bm // 16 * 36:
         return None
-    bn = 128 if cout % 128 == 0 else (64 if cout % 64 == 0 else 0)
+    if bn is None:
+        bn = 64 if H3_LOOP == "dma64" else 128
+    bn = bn if cout % bn == 0 else (64 if cout % 64 == 0 else 0)
     if not bn or (not force and (M // bm) * (cout // bn) < H3_MIN_TILES):
         return None
     return bm, bn
+
+
+def h3_auto(N, H, W, shp: "ConvShape", pro, cout, cx=None):
+    """The halo loop's measured per-shape choice (scripts/bench_h3.py, profiles/r6/bench_h3_*.txt):
+    ((BM, BN), kg) or None for the implicit-GEMM kernel.  At 32x32 the double-buffered 64-channel
+    tiles (two workgroups per CU); at 16x16 / 8x8 the single-stage 128-channel tiles when the grid
+    holds >= 512 of them, else (16x16 at the 8-GPU share) the 64-channel double-buffered tiles;
+    at 4x4 the double-buffered 128-channel tiles over >= 256 tiles; smaller grids (8x8 / 4x4 at
+    batch 128) stay on the tuned implicit-GEMM launches."""
+    if H3_LOOP != "auto":
+        t = h3_tile(N, H, W, shp, pro, cout, cx=cx)
+        return None if t is None else (t, _h3_kg(None, W))
+    if h3_tile(N, H, W, shp, pro, cout, force=True, cx=cx, bn=64) is None:
+        return None
+    tiles128 = (N * H * W // 256) * (cout // 128) if cout % 128 == 0 else 0
+    if W >= 32:
+        return (256, 64), 6
+    if W >= 8:
+        if tiles128 >= 512:
+            return (256, 128), 7
+        return ((256, 64), 6) if W >= 16 else None
+    return ((256, 128), 6) if tiles128 >= 256 else None
 
 
 def _loop_kg(ent, kgv):
@@ -365,13 +390,18 @@ def conv_fwd(x, wf, shp: ConvShape, s=None, t=None, act=0, alpha=1.0, tile=None,
     M = N * Ho * Wo
     pro = PRO_AFFINE_ACT if (s is not None or act != 0 or lazy is not None) else PRO_NONE
     ent = None
-    h3 = h3_tile(N, H, W, shp, pro, shp.cout, kg in H3_KGS) if (kg in H3_KGS or (kg is None and tile is None)) else None
+    h3 = None
+    if kg in H3_KGS:
+        t = h3_tile(N, H, W, shp, pro, shp.cout, True)
+        h3 = None if t is None else (t, kg)
+    elif kg is None and tile is None and H3:
+        h3 = h3_auto(N, H, W, shp, pro, shp.cout)
     if tile is None and h3 is None:
         ent = tuned(f"fwd{pro}", N, H, shp) or tuned("fwd", N, H, shp)
         tile = tuple(ent["tile"]) if ent else None
     if h3 is not None:
-        ent, (bm, bn), bk = {"loop": "old"}, h3, 16
-        ns, slab_p, cnt_p, kgv = 1, 0, 0, _h3_kg(kg, W)
+        ent, ((bm, bn), kgv), bk = {"loop": "old"}, h3, 16
+        ns, slab_p, cnt_p = 1, 0, 0
     else:
         bm, bn, bk = _tile3(tile, M, shp.cout)
         if nsplit is not None:
@@ -495,11 +525,16 @@ def conv_dgrad(g, y, al, be, wd, shp: ConvShape, x_shape, epi=EPI_STORE, out=Non
         if len(dh) == 0 and epi == EPI_ADD:
             continue
         pro = PRO_FOLD if al is not None else PRO_NONE  # al None: g is already folded
-        h3 = h3_tile(N, Hx, Wx, shp, pro, shp.cin, kg in H3_KGS, cx=Cy) if h3ok and epi in (EPI_ACTBWD, EPI_STORE) and len(
-            dh) == 9 else None
+        h3 = None
+        if h3ok and epi in (EPI_ACTBWD, EPI_STORE) and len(dh) == 9:
+            if kg in H3_KGS:
+                t = h3_tile(N, Hx, Wx, shp, pro, shp.cin, True, cx=Cy)
+                h3 = None if t is None else (t, kg)
+            elif H3:
+                h3 = h3_auto(N, Hx, Wx, shp, pro, shp.cin, cx=Cy)
         if h3 is not None:
-            (bm, bn), bk = h3, 16
-            ns, slab_p, cnt_p, kgv = 1, 0, 0, _h3_kg(kg, Wx)
+            ((bm, bn), kgv), bk = h3, 16
+            ns, slab_p, cnt_p = 1, 0, 0
         else:
             bm, bn, bk = _tile3(tile, M, shp.cin)
             ns, slab_p, cnt_p = _splitk_args(ent, M, shp.cin, len(dh) * Cy, bm, bn, bk, g.device)

@@ -30,7 +30,12 @@ MI355X design (``FullyShardedDP``):
   next forward gathers the new values -- no post-step all-gather.
 * **offload**: ``offload=True`` keeps shards (and optimizer state) in pinned host memory
   like the reference's ``CPUOffload``: gathers copy the shard H2D first, gradients come back
-  D2H after the reduce-scatter, and the optimizer runs on the host.
+  D2H after the reduce-scatter, and the optimizer runs on the host (``offload_optimizer=
+  "host"``, the faithful mode).  ``offload_optimizer="device"``: the parameter shards still
+  live in pinned host memory between steps (every gather stages them H2D; after each step the
+  updated shard is mirrored back D2H on the copy stream, ahead of the next step's gathers on
+  that same stream), but the optimizer -- NGD / MADGRAD math and state -- runs on the GPU over
+  the device staging copies, and the averaged gradient never leaves the device.
 * the fused ResNet engine (one autograd node for the whole body) drives its units itself at
   stage boundaries (``pre_forward`` / ``post_forward`` / ``pre_backward`` / ``post_backward``,
   ``ops/resnet_fused.py``) and packs / releases its bf16 weight layouts per stage.
@@ -309,7 +314,7 @@ class Unit:
         op = dist.ReduceOp.AVG if (fs.use_avg and fs.ws > 1) else dist.ReduceOp.SUM  # (1 rank: sum)
         self.rs_work = dist.reduce_scatter_tensor(fs.grad_chunk(self), self.gfull, op=op, group=fs.pg,
                                                   async_op=True)
-        if fs.offload and fs.copy_stream is not None:
+        if fs.offload and fs.copy_stream is not None and not fs.opt_on_device:
             # the averaged shard gradient goes back to pinned host memory on the copy stream as
             # soon as its reduce-scatter lands, overlapping the rest of backward
             with torch.cuda.stream(fs.copy_stream):
@@ -344,7 +349,8 @@ class FullyShardedDP:
     sharded_optimizer = True
 
     def __init__(self, model: nn.Module, device=None, units=None, mode="flat", offload=False, process_group=None,
-                 prefetch=True, engine_units=(), static=False, param_dtype=None, reshard_after_forward=True):
+                 prefetch=True, engine_units=(), static=False, param_dtype=None, reshard_after_forward=True,
+                 offload_optimizer="host"):
         """units: [(name, module)] (None: ``default_units``; ``[("", model)]``: the whole model
         as one unit, the reference's ``FSDP(model)`` without an auto-wrap policy); mode: 'flat' |
         'param' (NGD);
@@ -362,6 +368,9 @@ class FullyShardedDP:
         self.device = torch.device(device) if device is not None else next(model.parameters()).device
         self.use_avg = dist.get_backend(process_group) == "nccl"
         self.offload = offload
+        if offload_optimizer not in ("host", "device"):
+            raise ValueError(f"offload_optimizer {offload_optimizer!r}")
+        self.opt_on_device = bool(offload and offload_optimizer == "device" and self.device.type == "cuda")
         self.prefetch = prefetch
         self.mode = mode
         # identical initial parameters on every rank (rank 0's), before sharding
@@ -437,6 +446,9 @@ class FullyShardedDP:
         self.stage16 = (torch.empty(total, device=self.device, dtype=self.param_dtype)
                         if self.param_dtype is not None else None)
         self.view = self.space  # (trainer interface shared with the sharded-optimizer DP)
+        if self.opt_on_device:
+            # the optimizer / clipper work on the device staging copies of the shard (same slots)
+            self.view = SpaceView(self.stage_data, self.stage_grad, list(slots), self.device)
         self.peak_full_bytes = 0
         self.last_rs = None  # unit whose reduce-scatter was launched last
         self.engine_units = set(engine_units)
@@ -447,6 +459,11 @@ class FullyShardedDP:
             u._free(u.gfull)
         self._account()
         model._fsdp_sharded = self  # checkpoint I/O gathers through summon_full_params
+
+    def _quiesce(self):
+        """Host code is about to touch the pinned shard: finish the copy stream's transfers."""
+        if self.offload and self.copy_stream is not None:
+            self.copy_stream.synchronize()
 
     # ------------------------------------------------------------ shard views
     def shard_chunk(self, u, lowp=False):
@@ -653,7 +670,7 @@ class FullyShardedDP:
                     for _, q in u.params:
                         q.grad = None
         self.last_rs = None
-        if self.offload:
+        if self.offload and not self.opt_on_device:
             if self.copy_stream is not None:
                 # the per-unit D2H copies were queued on the copy stream as each reduce-scatter
                 # landed; the host optimizer reads the shard next
@@ -661,14 +678,21 @@ class FullyShardedDP:
             else:
                 self.shard_grad.copy_(self.stage_grad, non_blocking=False)
         if not self.use_avg and self.ws > 1:
-            self.shard_grad.div_(self.ws)
+            self.view.grad.div_(self.ws)
         for u in self.units:
             if not u.root:
                 u.reshard()
 
     def after_step(self):
         """Nothing to all-gather: the next forward gathers the updated shards (any copy still
-        gathered -- the root unit, every unit in static mode -- is marked stale)."""
+        gathered -- the root unit, every unit in static mode -- is marked stale).  Device
+        optimizer offload: the updated device shard is mirrored to the pinned host shard on the
+        copy stream, ahead of the next gathers' H2D copies on that stream."""
+        if self.opt_on_device:
+            cs = self.copy_stream
+            cs.wait_stream(torch.cuda.current_stream(self.device))
+            with torch.cuda.stream(cs):
+                self.shard_data.copy_(self.stage_data, non_blocking=True)
         for u in self.units:
             if u.root or self.static:
                 u.gathered = False
@@ -709,6 +733,7 @@ class FullyShardedDP:
             with torch.no_grad():
                 for u in self.units:
                     lo = self.rank * u.chunk
+                    self._quiesce()
                     self.shard_data[u.shard_off:u.shard_off + u.chunk].copy_(u.full[lo:lo + u.chunk])
         return res
 
@@ -759,6 +784,7 @@ class FullyShardedDP:
                 if n in sd:
                     p.data.copy_(sd[n].to(p.device, p.dtype).view(p.shape))
             lo = self.rank * u.chunk
+            self._quiesce()
             self.shard_data[u.shard_off:u.shard_off + u.chunk].copy_(u.full[lo:lo + u.chunk])
             if u.slot is not None:
                 u.gathered = False

@@ -9,13 +9,15 @@ BE rank R of a world-N ``nccl`` job as far as the framework can tell, with every
 replaced by a same-sized local operation on the device:
 
 * ``all_reduce(t)``: SUM -> ``t *= N`` (the magnitude an all-reduce of N similar contributions
-  has), AVG / MAX / MIN -> ``t`` rewritten through a scratch copy -- one read + one write of the
-  buffer, the HBM traffic of RCCL's reduction kernels on this rank;
-* ``reduce_scatter_tensor(out, inp)``: out = inp[R-th slice] (x N for SUM), plus one full read of
-  ``inp``;
+  has), AVG / MAX / MIN -> ``t *= 1`` -- one read + one write of the buffer in place, the HBM
+  traffic of RCCL's reduction kernels on this rank;
+* ``reduce_scatter_tensor(out, inp)``: out = inp[R-th slice] (x N for SUM), plus one in-place
+  read + write of ``inp``;
 * ``all_gather_into_tensor(out, inp)``: out[R-th slice] = inp (the other slices keep this rank's
-  replica of those parameters, which every rank initialised identically), plus one full write of
-  ``out``;
+  replica of those parameters, which every rank initialised identically), plus one in-place
+  read + write of ``out``;
+(no scratch buffers: a collective captured into a HIP graph must not allocate from the capture's
+private pool and keep the block past it)
 * ``broadcast`` / ``barrier``: no-ops (rank-0 values are this rank's own).
 
 ``async_op=True`` collectives run on a side stream forked from the current one and joined by
@@ -49,15 +51,8 @@ class _Sim:
         assert 0 <= rank < world, (rank, world)
         self.rank, self.world = rank, world
         self.side = None
-        self.scratch = None
         self.bytes = {"all_reduce": 0, "reduce_scatter": 0, "all_gather": 0}
         self.saved = {}
-
-    def _scr(self, t: torch.Tensor) -> torch.Tensor:
-        n = t.numel() * t.element_size()
-        if self.scratch is None or self.scratch.numel() < n or self.scratch.device != t.device:
-            self.scratch = torch.empty(max(n, 1 << 20), dtype=torch.uint8, device=t.device)
-        return self.scratch[:n].view(t.dtype).view(t.shape)
 
     def _run(self, fn, t: torch.Tensor, async_op: bool):
         if not (async_op and t.is_cuda):
@@ -78,19 +73,14 @@ class _Sim:
         self.bytes["all_reduce"] += t.numel() * t.element_size()
 
         def fn():
-            if op == dist.ReduceOp.SUM:
-                t.mul_(self.world)
-            else:
-                s = self._scr(t)
-                s.copy_(t)
-                t.copy_(s)
+            t.mul_(self.world if op == dist.ReduceOp.SUM else 1)
         return self._run(fn, t, async_op)
 
     def reduce_scatter_tensor(self, out, inp, op=dist.ReduceOp.SUM, group=None, async_op=False):
         self.bytes["reduce_scatter"] += inp.numel() * inp.element_size()
 
         def fn():
-            self._scr(inp).copy_(inp)
+            inp.mul_(1)
             out.copy_(inp.view(self.world, -1)[self.rank].view(out.shape))
             if op == dist.ReduceOp.SUM:
                 out.mul_(self.world)
@@ -100,7 +90,7 @@ class _Sim:
         self.bytes["all_gather"] += out.numel() * out.element_size()
 
         def fn():
-            self._scr(out).copy_(out)
+            out.mul_(1)
             out.view(self.world, -1)[self.rank].copy_(inp.reshape(-1))
         return self._run(fn, out, async_op)
 

@@ -60,6 +60,7 @@ class ResNetConfig:
     comm_dtype: str = "fp32"
     fsdp: bool = False
     fsdp_offload: bool = False         # FSDP shards + optimizer state in pinned host memory (CPUOffload)
+    fsdp_offload_optimizer: str = "device"  # "device": optimizer on the GPU over the staged shard; "host": on the CPU
     fsdp_param_dtype: str = "fp32"     # fp32 | bf16: all-gather wire / compute copy of the parameters
     fsdp_schedule: str = "full_shard"  # full_shard (reshard after forward) | shard_grad_op (graph path only)
     shard_ngd: bool = True             # distributed NGD: each rank owns + preconditions 1/world of the params
@@ -135,6 +136,7 @@ class ResNetTrainer:
             self.model.graph_engine = static
             self.fsdp = FullyShardedDP(self.model, self.device, mode="param" if ngd_opt else "flat",
                                        offload=cfg.fsdp_offload, static=static,
+                                       offload_optimizer="host" if cfg.faithful else cfg.fsdp_offload_optimizer,
                                        reshard_after_forward=cfg.fsdp_schedule == "full_shard",
                                        param_dtype={"fp32": None, "bf16": torch.bfloat16}[cfg.fsdp_param_dtype],
                                        engine_units=("conv1",) + STAGES if engine else ())

@@ -62,6 +62,10 @@ class TransformerConfig:
     faithful: bool = False
     fsdp: bool = False
     fsdp_offload: bool = False       # FSDP shards + optimizer state in pinned host memory (reference CPUOffload)
+    # where the offloaded run's optimizer runs: "device" = NGD / MADGRAD math + state on the GPU over
+    # the staged shard (params still live in pinned host memory between steps), "host" = the
+    # reference's CPUOffload optimizer on the CPU (selected by --faithful)
+    fsdp_offload_optimizer: str = "device"
     fsdp_param_dtype: str = "fp32"   # fp32 | bf16: all-gather wire / compute copy of the parameters
     fsdp_schedule: str = "full_shard"  # full_shard | shard_grad_op (the HIP-graph path's static FSDP)
     # FSDP wrap units: "model" = the whole model as ONE unit, as the reference wraps it
@@ -140,6 +144,7 @@ class TransformerTrainer:
             self.fsdp = FullyShardedDP(self.model, self.device, mode="param" if ngd_opt else "flat",
                                        units=[("", self.model)] if cfg.fsdp_wrap == "model" else None,
                                        offload=cfg.fsdp_offload, static=static,
+                                       offload_optimizer="host" if cfg.faithful else cfg.fsdp_offload_optimizer,
                                        reshard_after_forward=cfg.fsdp_schedule == "full_shard",
                                        param_dtype={"fp32": None, "bf16": torch.bfloat16}[cfg.fsdp_param_dtype])
             self.flat = self.fsdp.space
@@ -190,7 +195,8 @@ class TransformerTrainer:
         if self.fsdp is not None:
             wrap = "whole model as one unit" if cfg.fsdp_wrap == "model" else "one unit per sublayer"
             mode = "static, HIP-graph segments" if self.fsdp.static else "eager"
-            off = ", CPU offload (host optimizer)" if cfg.fsdp_offload else ""
+            off = ((", CPU offload (host optimizer)" if (cfg.faithful or cfg.fsdp_offload_optimizer == "host")
+                    else ", CPU offload (device optimizer)") if cfg.fsdp_offload else "")
             ref = " -- the reference's FSDP(model, CPUOffload)" if (cfg.fsdp_offload and cfg.fsdp_wrap == "model") else ""
             return f"FSDP {cfg.fsdp_schedule} ({wrap}, {mode}{off}), world {self.world}{ref}"
         if self.zero is not None:
@@ -414,6 +420,10 @@ class TransformerTrainer:
             # (capture mode stands) or with cuts (fallback)
             step.rec.check_collectives()
             self._graphs[key] = 2
+            # the checking step's graphs are dropped here: their private pool's use count falls to
+            # zero, and a capture into a pool in that state trips the caching allocator's assert
+            # (found by the world-8 rehearsal, bench.py --simulate-world 8): recapture into a new pool
+            self._graph_pool = torch.cuda.graph_pool_handle()
         return ent["loss"], ent["logits"], ent["perm"], lam
 
     def train_step(self, tokens, labels, types, masks):

@@ -43,7 +43,10 @@ def parse(argv=None):
     p.add_argument("--fsdp", action="store_true")
     p.add_argument("--fsdp_schedule", default="full_shard", choices=["full_shard", "shard_grad_op"])
     p.add_argument("--fsdp_offload", action="store_true",
-                   help="--fsdp: shards + optimizer state in pinned host memory (reference CPUOffload; eager, host optimizer)")
+                   help="--fsdp: parameter shards in pinned host memory (reference CPUOffload; eager)")
+    p.add_argument("--fsdp_offload_optimizer", default="device", choices=["device", "host"],
+                   help="--fsdp_offload: optimizer on the GPU over the staged shard (default) or on the host "
+                        "(the reference's CPUOffload; --faithful)")
     p.add_argument("--bucket_mb", default=25.0, type=float)
     p.add_argument("--comm_dtype", default="fp32", choices=["fp32", "bf16"])
     p.add_argument("--faithful", action="store_true", help="reproduce reference quirks (lr x4, mixup loss form)")
@@ -80,7 +83,7 @@ def config_from_args(a):
                         optimizer=a.optimizer, weight_decay=a.weight_decay, precision=a.precision,
                         synthetic=a.synthetic, data_root=a.data_root, seed=a.seed, faithful=a.faithful,
                         lr_scaling="faithful4" if a.faithful else "world", bucket_mb=a.bucket_mb,
-                        comm_dtype=a.comm_dtype, fsdp=a.fsdp, fsdp_schedule=a.fsdp_schedule, fsdp_offload=a.fsdp_offload, scheduler=sched, resume=a.resume,
+                        comm_dtype=a.comm_dtype, fsdp=a.fsdp, fsdp_schedule=a.fsdp_schedule, fsdp_offload=a.fsdp_offload, fsdp_offload_optimizer=a.fsdp_offload_optimizer, scheduler=sched, resume=a.resume,
                         checkpoint_dir=a.checkpoint_dir, steps_per_epoch=a.steps, eval=not a.no_eval,
                         log_path=a.log, plot=not a.no_plot, workers=a.workers, auto_resume=a.auto_resume,
                         save_last=a.save_last, nonfinite_guard=not a.no_nonfinite_guard,

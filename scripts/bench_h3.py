@@ -51,13 +51,16 @@ def main():
             t_old = timeit(lambda: fn(None), a.reps)
             y_old = fn(None).float()
             res = []
-            for kg in (5, 6, 7):
+            for loop, kg in (("dma", 5), ("dma", 6), ("dma", 7), ("dma64", 6), ("dma64", 7)):
                 if h3 is None:
                     continue
+                ci.H3_LOOP = loop
                 t_new = timeit(lambda: fn(kg), a.reps)
                 y_new = fn(kg).float()
+                ci.H3_LOOP = "auto"
                 d = ((y_new - y_old).norm() / y_old.norm()).item()
-                res.append(f"kg{kg} {t_new * 1e3:6.1f} us ({flop / t_new / 1e9:5.0f} TF/s, rel diff {d:.1e})")
+                res.append(f"kg{kg}/{'64' if loop == 'dma64' else '128'} {t_new * 1e3:6.1f} us "
+                           f"({flop / t_new / 1e9:5.0f} TF/s, {d:.0e})")
             ci.H3 = True
             print(f"N {N} {H}x{H} {C}->{Co} {name:5s}: tuned {t_old * 1e3:6.1f} us ({flop / t_old / 1e9:5.0f} TF/s)"
                   f"  halo {h3}: " + "  ".join(res), flush=True)

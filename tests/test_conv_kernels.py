@@ -192,9 +192,11 @@ H3_CASES = [(1, 32, 64, 64), (2, 16, 128, 128), (4, 8, 256, 256), (16, 4, 512, 5
 
 @pytest.mark.parametrize("case", H3_CASES)
 @pytest.mark.parametrize("kg", [5, 6, 7])
-def test_h3_conv_fwd(cuda, case, kg):
+@pytest.mark.parametrize("loop", ["dma", "dma64"])  # 128 / 64 output channels per workgroup
+def test_h3_conv_fwd(cuda, case, kg, loop, monkeypatch):
     """Forward 3x3 on a materialised operand through the halo loop: output and BN statistics
     against fp32 PyTorch, and the implicit-GEMM kernel on the same inputs."""
+    monkeypatch.setattr(ci, "H3_LOOP", loop)
     N, H, Cin, Cout = case
     torch.manual_seed(7)
     shp = ci.ConvShape(Cin, Cout, 3, 1, 1)
@@ -218,9 +220,11 @@ def test_h3_conv_fwd(cuda, case, kg):
 @pytest.mark.parametrize("case", H3_CASES)
 @pytest.mark.parametrize("epi", ["store", "actbwd_relu", "actbwd_celu"])
 @pytest.mark.parametrize("kg", [5, 6, 7])
-def test_h3_conv_dgrad(cuda, case, epi, kg):
+@pytest.mark.parametrize("loop", ["dma", "dma64"])
+def test_h3_conv_dgrad(cuda, case, epi, kg, loop, monkeypatch):
     """Stride-1 3x3 data gradient of a pre-folded gradient through the halo loop (flipped taps):
     plain store and the producer's activation backward + statistics, against fp32 PyTorch."""
+    monkeypatch.setattr(ci, "H3_LOOP", loop)
     N, H, Cin, Cout = case
     torch.manual_seed(8)
     shp = ci.ConvShape(Cin, Cout, 3, 1, 1)

@@ -58,3 +58,19 @@ def test_bench_simulate_rank_runs_the_sharded_path():
     assert rec["config"]["owner_shard_numel"] < n / 4  # ~1/8 of the parameters (balanced by NGD cost)
     cb = rec["simulated"]["comm_bytes_first_step"]
     assert cb["all_reduce"] > 0 and cb["all_gather"] > 0
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(600)
+def test_simulated_world8_transformer_step_with_graph_comm_check(cuda):
+    """Rank 3 of a simulated world-8 transformer run on the GPU: ZeRO-2 sharded NGD, bucket
+    all-reduces captured into the step graph, the in-run capture check, and the recapture after
+    it (which used to reuse the dropped graphs' private pool and trip the caching allocator's
+    use-count assert -- a crash the first real 8-GPU transformer run would have hit)."""
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--model", "transformer", "--simulate-world",
+                        "8", "--simulate-rank", "3", "--steps", "4", "--warmup", "6"],
+                       capture_output=True, text=True, timeout=580)
+    assert r.returncode == 0, r.stderr[-3000:]
+    rec = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    assert rec["simulated"]["rank"] == 3 and rec["config"]["hip_graphs"]
+    assert rec["config"].get("graph_comm", "").startswith("capture"), rec["config"]

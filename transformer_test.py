@@ -45,7 +45,10 @@ def parse(argv=None):
     p.add_argument("--fsdp", action="store_true", help="flat-sharded data parallel (reference: FSDP)")
     p.add_argument("--fsdp_schedule", default="full_shard", choices=["full_shard", "shard_grad_op"])
     p.add_argument("--fsdp_offload", action="store_true",
-                   help="--fsdp: shards + optimizer state in pinned host memory (reference CPUOffload; eager, host optimizer)")
+                   help="--fsdp: parameter shards in pinned host memory (reference CPUOffload; eager)")
+    p.add_argument("--fsdp_offload_optimizer", default="device", choices=["device", "host"],
+                   help="--fsdp_offload: optimizer on the GPU over the staged shard (default) or on the host "
+                        "(the reference's CPUOffload; --faithful)")
     p.add_argument("--fsdp_wrap", default="model", choices=["model", "sublayer"],
                    help="FSDP units: the whole model (the reference's FSDP(model)) or one per sublayer")
     p.add_argument("--bucket_mb", default=25.0, type=float)
@@ -79,7 +82,7 @@ def config_from_args(a):
                              distributed=a.distributed, ngd=a.ngd, optimizer=a.optimizer,
                              weight_decay=a.weight_decay, precision=a.precision, synthetic=a.synthetic,
                              data_root=a.data_root, tokenizer=a.tokenizer, seed=a.seed, faithful=a.faithful,
-                             fsdp=a.fsdp, fsdp_schedule=a.fsdp_schedule, fsdp_wrap=a.fsdp_wrap, fsdp_offload=a.fsdp_offload, bucket_mb=a.bucket_mb, resume=a.resume, checkpoint_dir=a.checkpoint_dir,
+                             fsdp=a.fsdp, fsdp_schedule=a.fsdp_schedule, fsdp_wrap=a.fsdp_wrap, fsdp_offload=a.fsdp_offload, fsdp_offload_optimizer=a.fsdp_offload_optimizer, bucket_mb=a.bucket_mb, resume=a.resume, checkpoint_dir=a.checkpoint_dir,
                              steps_per_epoch=a.steps, eval=not a.no_eval, log_path=a.log, plot=not a.no_plot,
                              workers=a.workers, n_layers=a.layers, d_model=a.d_model, heads=heads,
                              d_ff=2 * a.d_model, d_hidden=2 * a.d_model, auto_resume=a.auto_resume,
