@@ -392,6 +392,14 @@ bool launch_h3(int pro, int epi, int act, const ConvArgs& a, int BM, int BN, int
     else { FDT_H3E(BM_, BN_, WM_, WN_, false, 2) }             \
     return false;                                           \
   }
+  // kg 8: the double-buffered LDS-DMA loop with 16 waves (1024 threads) on the 256 x 128 tile:
+  // four waves per SIMD (the MFMA issue rate of the single-stage two-workgroup form) AND the DMA of
+  // chunk c+1 under chunk c's MFMAs, in ONE workgroup per CU (the phase-lock of two identical
+  // workgroups cannot happen)
+  if (kg == 8) {
+    if (BM == 256 && BN == 128) { FDT_H3E(256, 128, 8, 2, true, 2) }
+    return false;
+  }
   FDT_H3(256, 128, 4, 2)
   FDT_H3(256, 64, 8, 1)
   FDT_H3(128, 128, 2, 2)

@@ -98,9 +98,9 @@ static void conv_igemm_impl(uint64_t x, uint64_t x2, uint64_t ps, uint64_t pt, u
   hipStream_t st = as_stream(stream);
   if (a.M == 0) return;
   const int act = (pro == kProAffineAct || pro == kProJoin) ? pro_act : ((epi == kEpiActBwd || epi == kEpiJoinBwd) ? epi_act : 0);
-  if (kg >= 5 && kg <= 7) {  // halo-staged 3x3 stride-1 loop (conv_h3.hip): prologue-free operands, no split-K
-    FDT_CHECK(pro == kProNone && a.nsplit == 1, "kg 5-7 (halo 3x3): prologue-free, nsplit 1");
-    FDT_CHECK(launch_h3(pro, epi, act, a, BM, BN, kg, st), "kg 5-7 (halo 3x3): unsupported tile / epilogue");
+  if (kg >= 5 && kg <= 8) {  // halo-staged 3x3 stride-1 loop (conv_h3.hip): prologue-free operands, no split-K
+    FDT_CHECK(pro == kProNone && a.nsplit == 1, "kg 5-8 (halo 3x3): prologue-free, nsplit 1");
+    FDT_CHECK(launch_h3(pro, epi, act, a, BM, BN, kg, st), "kg 5-8 (halo 3x3): unsupported tile / epilogue");
     return;
   }
   if (kg == 2 && a.nsplit > 1) kg = 1;  // K groups and split-K are alternatives (kg 4: rotated loop, any split)

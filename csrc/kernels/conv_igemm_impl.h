@@ -1136,7 +1136,7 @@ bool launch_cases_plain(int pro, int epi, int act, const ConvArgs& a, int BM, in
 bool launch_cases_ffn(int pro, int epi, int act, const ConvArgs& a, int BM, int BN, int BK, int kg, bool pure,
                       hipStream_t st);
 // halo-staged 3x3 stride-1 main loop (conv_h3.hip): kg 5 register-staged, kg 6 LDS-DMA (two
-// stages), kg 7 LDS-DMA single stage (two workgroups per CU)
+// stages), kg 7 LDS-DMA single stage (two workgroups per CU), kg 8 LDS-DMA two stages, 16 waves
 bool h3_supported(const ConvArgs& a, int BM);
 bool launch_h3(int pro, int epi, int act, const ConvArgs& a, int BM, int BN, int kg, hipStream_t st);
 

@@ -212,7 +212,7 @@ H3_TILES = {(256, 128), (256, 64), (128, 128)}
 # and compute together, profiles/r6/h3_probe_1024.txt), "reg" = register-staged (kg 5);
 # "auto" = the measured per-shape choice (h3_auto)
 H3_LOOP = os.environ.get("FDT_CONV_H3_LOOP", "auto")
-H3_KGS = (5, 6, 7)
+H3_KGS = (5, 6, 7, 8)
 
 
 def _h3_kg(kg, W=8):
@@ -392,8 +392,8 @@ def conv_fwd(x, wf, shp: ConvShape, s=None, t=None, act=0, alpha=1.0, tile=None,
     ent = None
     h3 = None
     if kg in H3_KGS:
-        t = h3_tile(N, H, W, shp, pro, shp.cout, True)
-        h3 = None if t is None else (t, kg)
+        t3 = h3_tile(N, H, W, shp, pro, shp.cout, True)
+        h3 = None if t3 is None else (t3, kg)
     elif kg is None and tile is None and H3:
         h3 = h3_auto(N, H, W, shp, pro, shp.cout)
     if tile is None and h3 is None:
@@ -528,8 +528,8 @@ def conv_dgrad(g, y, al, be, wd, shp: ConvShape, x_shape, epi=EPI_STORE, out=Non
         h3 = None
         if h3ok and epi in (EPI_ACTBWD, EPI_STORE) and len(dh) == 9:
             if kg in H3_KGS:
-                t = h3_tile(N, Hx, Wx, shp, pro, shp.cin, True, cx=Cy)
-                h3 = None if t is None else (t, kg)
+                t3 = h3_tile(N, Hx, Wx, shp, pro, shp.cin, True, cx=Cy)
+                h3 = None if t3 is None else (t3, kg)
             elif H3:
                 h3 = h3_auto(N, Hx, Wx, shp, pro, shp.cin, cx=Cy)
         if h3 is not None:
