@@ -48,6 +48,8 @@ bool deterministic_mode();
 // optim.hip
 void grad_sumsq(uint64_t g, long n, uint64_t inv_scale, int unscale, uint64_t part, int nb, uint64_t found_inf,
                 uint64_t stream);
+// test aid: fill every CU's LDS with a NaN pattern (conv_h3.hip)
+void lds_poison(uint64_t sink, int nblocks, uint64_t stream);
 void grad_norm_finalize(uint64_t part, int nb, float max_norm, uint64_t out, uint64_t total, int phase,
                         uint64_t stream);
 void sgd_step(uint64_t p, uint64_t g, uint64_t buf, uint64_t shadow, long n, float lr, float momentum, float dampening,

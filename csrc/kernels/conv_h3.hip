@@ -410,3 +410,34 @@ bool launch_h3(int pro, int epi, int act, const ConvArgs& a, int BM, int BN, int
 
 }  // namespace conv
 }  // namespace fdt
+
+// ---------------------------------------------------------------------------- LDS poison (test aid)
+// Fills the whole LDS of every CU with 0xFFFF (a bf16 / fp32 NaN pattern) so a following kernel
+// that reads LDS it never wrote shows NaNs instead of the previous kernel's leftovers
+// (scripts/h3_repeat.py --poison).  ``flag`` is never set by callers: it only keeps the stores
+// observable to the compiler.
+namespace fdt {
+namespace {
+constexpr int kPoisonBytes = 160 * 1024;
+__global__ __launch_bounds__(256) void lds_poison_kernel(uint32_t* __restrict__ sink, int flag) {
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  uint4* p = reinterpret_cast<uint4*>(lds);
+  const uint4 v = make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu);
+  for (int i = threadIdx.x; i < kPoisonBytes / 16; i += 256) p[i] = v;
+  __syncthreads();
+  if (flag) sink[blockIdx.x * 256 + threadIdx.x] = p[(threadIdx.x * 977) % (kPoisonBytes / 16)].x;
+}
+}  // namespace
+
+void lds_poison(uint64_t sink, int nblocks, uint64_t stream) {
+  static bool attr = false;
+  if (!attr) {
+    FDT_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(lds_poison_kernel),
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, kPoisonBytes));
+    attr = true;
+  }
+  FDT_CHECK(nblocks > 0 && sink != 0, "lds_poison: sink buffer of nblocks * 256 words");
+  lds_poison_kernel<<<nblocks, 256, kPoisonBytes, as_stream(stream)>>>(reinterpret_cast<uint32_t*>(sink), 0);
+  FDT_HIP_CHECK(hipGetLastError());
+}
+}  // namespace fdt

@@ -690,9 +690,12 @@ class FullyShardedDP:
         copy stream, ahead of the next gathers' H2D copies on that stream."""
         if self.opt_on_device:
             cs = self.copy_stream
-            cs.wait_stream(torch.cuda.current_stream(self.device))
-            with torch.cuda.stream(cs):
-                self.shard_data.copy_(self.stage_data, non_blocking=True)
+            if cs is None:
+                self.shard_data.copy_(self.stage_data)
+            else:
+                cs.wait_stream(torch.cuda.current_stream(self.device))
+                with torch.cuda.stream(cs):
+                    self.shard_data.copy_(self.stage_data, non_blocking=True)
         for u in self.units:
             if u.root or self.static:
                 u.gathered = False

@@ -1,5 +1,6 @@
 #!/usr/bin/env python3
-"""Diagnostic: per-slot update differences of FSDP(model) NGD, plain vs offload-device optimizer."""
+"""Diagnostic: FSDP(model) NGD, plain vs offload with the device optimizer -- the optimizer's
+inputs (gradient, parameters) and output (parameters) compared at every step, per slot."""
 import os
 import sys
 
@@ -11,35 +12,44 @@ import torch  # noqa: E402
 from faster_distributed_training_amd.train.transformer_trainer import TransformerConfig, TransformerTrainer  # noqa
 
 
-def run(arm, steps):
-    cfg = TransformerConfig(batch_size=16, synthetic=True, eval=False, plot=False, ngd=True, optimizer="ngd", fsdp=True,
-                            fsdp_offload=arm != "plain", fsdp_offload_optimizer="device", length_buckets=(128, 256),
-                            epoch=1, seed=0, extra={"fsdp_static": False})
+def run(arm, steps, opt):
+    cfg = TransformerConfig(batch_size=16, synthetic=True, eval=False, plot=False, ngd=opt == "ngd", optimizer=opt,
+                            fsdp=True, fsdp_offload=arm != "plain", fsdp_offload_optimizer="device",
+                            length_buckets=(128, 256), epoch=1, seed=0, extra={"fsdp_static": False})
     tr = TransformerTrainer(cfg)
-    fs = tr.fsdp
+    rec = []
+    inner = tr.optimizer.step
+
+    def step(*a, **k):
+        torch.cuda.synchronize()
+        g0, d0 = tr.space.grad.detach().cpu().clone(), tr.space.data.detach().cpu().clone()
+        out = inner(*a, **k)
+        torch.cuda.synchronize()
+        rec.append((g0, d0, tr.space.data.detach().cpu().clone()))
+        return out
+    tr.optimizer.step = step
     it = iter(tr.train_loader)
     tr.model.train()
-    fs._quiesce()
-    init = fs.shard_data.clone().cpu()
-    g = []
     for _ in range(steps):
         tr.train_step(*next(it))
-        torch.cuda.synchronize()
-        fs._quiesce()
-        g.append(tr.space.grad.detach().cpu().clone())
-    upd = fs.shard_data.cpu() - init
-    return upd, g, [s for s in tr.space.slots], tr.optimizer
+    torch.cuda.synchronize()
+    tr.fsdp._quiesce()
+    return rec, list(tr.space.slots)
 
 
-for steps in (1, 2, 3):
-    a, ga, slots, oa = run("plain", steps)
-    b, gb, _, ob = run("device", steps)
-    print(f"steps {steps}: update rel diff {((a - b).norm() / a.norm()).item():.3e}; grad rel diff per step",
-          [f"{((x - y).norm() / (x.norm() + 1e-30)).item():.2e}" for x, y in zip(ga, gb)])
-    rows = []
-    for s in slots:
-        da, db = a[s.offset:s.offset + s.numel], b[s.offset:s.offset + s.numel]
-        rows.append((((da - db).norm() / (da.norm() + 1e-30)).item(), s.name, s.numel))
-    rows.sort(reverse=True)
-    print("   worst slots:", [(n, f"{r:.2e}") for r, n, _ in rows[:6]])
-    print("   opt state keys plain:", sorted(getattr(oa, "state", {}).get("__flat__", {}).keys())[:8])
+def rel(x, y):
+    return ((x - y).norm() / (y.norm() + 1e-30)).item()
+
+
+for opt, arm in (("ngd", "plain"), ("ngd", "device"), ("madgrad", "device")):
+    a, slots = run("plain", 2, opt)
+    b, _ = run(arm, 2, opt)
+    for i, ((ga, da, pa), (gb, db, pb)) in enumerate(zip(a, b)):
+        print(f"{opt} plain vs {arm} step {i}: grad in {rel(gb, ga):.2e}  data in {rel(db, da):.2e}  data out {rel(pb, pa):.2e}  "
+              f"update {rel(pb - db, pa - da):.2e}", flush=True)
+        rows = []
+        for s in slots:
+            sl = slice(s.offset, s.offset + s.numel)
+            rows.append((rel((pb - db)[sl], (pa - da)[sl]), rel(gb[sl], ga[sl]), s.name, tuple(s.shape)))
+        rows.sort(reverse=True)
+        print("   worst update slots (upd, grad):", [(n, sh, f"{r:.1e}", f"{q:.1e}") for r, q, n, sh in rows[:5]])

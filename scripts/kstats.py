@@ -13,7 +13,8 @@ ap.add_argument("--top", type=int, default=25)
 a = ap.parse_args()
 rows = list(csv.DictReader(open(a.csv)))
 tot = sum(float(r["TotalDurationNs"]) for r in rows)
-print(f"total kernel time {tot / 1e6 / a.steps:.3f} ms/step over {a.steps} steps")
+ncall = sum(int(r["Calls"]) for r in rows)
+print(f"total kernel time {tot / 1e6 / a.steps:.3f} ms/step over {a.steps} steps, {ncall / a.steps:.1f} launches/step")
 for r in rows[: a.top]:
     print(f"{float(r['TotalDurationNs']) / 1e6 / a.steps:8.3f} ms/step {int(r['Calls']) / a.steps:7.1f} calls/step  "
           f"{r['Name'][:110]}")

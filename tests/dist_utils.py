@@ -34,6 +34,9 @@ def _entry(rank, world, port, fn, args, errq, native=False, backend="gloo"):
             dist.init_process_group("gloo", rank=rank, world_size=world)
         try:
             fn(rank, world, *args)
+            # gloo tears down its pair threads in destroy_process_group; a rank that leaves while
+            # its peer still has a send in flight can abort the peer (std::terminate) under load
+            dist.barrier()
         finally:
             dist.destroy_process_group()
     except Exception:  # report to the parent

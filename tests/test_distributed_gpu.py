@@ -642,12 +642,19 @@ def test_fsdp_offload_device_optimizer_matches_host_optimizer(cuda, opt, monkeyp
     ``fsdp_offload_optimizer="device"``): three eager transformer steps from the same weights and
     batches, world 1 over RCCL, against (a) FSDP without offload -- the same device optimizer on
     a device shard: the offload plumbing (H2D staging, no gradient D2H, the post-step D2H mirror)
-    must not change a bit -- and (b) the reference's host optimizer (a different implementation
-    of the same update: close, not equal).  The pinned host shard holds the updated parameters."""
+    must hand the optimizer the same gradient and parameters and land its result in the pinned
+    host shard -- and (b) the reference's host optimizer (a different implementation of the same
+    update: close, not equal).
+
+    The transformer's backward is not bitwise repeatable (atomics: ~3e-8 relative between two
+    identical runs), and NGD's first updates amplify that to ~40 % of the UPDATE between two
+    plain runs (scripts/diag_offload_ngd.py, profiles/r6/diag_offload_ngd.txt: degenerate
+    spectra in the initial per-axis Fisher estimates) while the parameters agree to ~1e-6: so
+    NGD is checked on the optimizer's inputs and on the parameters, MADGRAD also on its update."""
     monkeypatch.setenv("MASTER_ADDR", "127.0.0.1")
     monkeypatch.setenv("MASTER_PORT", "29641")
     from faster_distributed_training_amd.train.transformer_trainer import TransformerConfig, TransformerTrainer
-    upd = {}
+    upd, fin, first = {}, {}, {}
     for arm in ("plain", "device", "host"):
         cfg = TransformerConfig(batch_size=16, synthetic=True, eval=False, plot=False, ngd=opt == "ngd",
                                 optimizer=opt, fsdp=True, fsdp_offload=arm != "plain", fsdp_offload_optimizer=arm
@@ -656,6 +663,15 @@ def test_fsdp_offload_device_optimizer_matches_host_optimizer(cuda, opt, monkeyp
         tr = TransformerTrainer(cfg)
         fs = tr.fsdp
         assert fs.opt_on_device == (arm == "device") and not fs.static
+        inner = tr.optimizer.step
+
+        def step(*a, _inner=inner, _arm=arm, _tr=tr, **k):
+            if _arm not in first:  # what the optimizer is handed on the first step
+                _tr.fsdp._quiesce()
+                torch.cuda.synchronize()
+                first[_arm] = (_tr.space.grad.detach().cpu().clone(), _tr.space.data.detach().cpu().clone())
+            return _inner(*a, **k)
+        tr.optimizer.step = step
         it = iter(tr.train_loader)
         tr.model.train()
         fs._quiesce()
@@ -665,13 +681,23 @@ def test_fsdp_offload_device_optimizer_matches_host_optimizer(cuda, opt, monkeyp
         torch.cuda.synchronize()
         fs._quiesce()
         upd[arm] = fs.shard_data.cpu() - init  # the three steps' update
+        fin[arm] = fs.shard_data.cpu().clone()
         if arm == "device":
             assert torch.equal(fs.stage_data.cpu(), fs.shard_data), "host mirror == device shard"
+
+    def rel(x, y):
+        return ((x - y).norm() / y.norm()).item()
+    for arm in ("device", "host"):
+        assert torch.equal(first[arm][1], first["plain"][1]), "first step: same parameters"
+        assert rel(first[arm][0], first["plain"][0]) < 1e-6, "first step: same gradient (up to atomics order)"
     a, b, c = upd["plain"], upd["device"], upd["host"]
     assert torch.isfinite(b).all() and a.norm() > 0
-    assert ((b - a).norm() / a.norm()).item() < 1e-6, "offload plumbing changed the device update"
-    err = ((c - b).norm() / b.norm()).item()
-    # host (PyTorch fp32) vs device (HIP kernel) arithmetic over 3 steps: MADGRAD's first steps
-    # divide by the cube root of a tiny second-moment sum (eps 1e-6), which amplifies rounding on
-    # near-zero gradient elements (measured 3 % of the update norm); NGD's eigensolver < 2 %
-    assert err < (6e-2 if opt == "madgrad" else 2e-2), err
+    assert rel(fin["device"], fin["plain"]) < 1e-5, "offload plumbing changed the parameters"
+    if opt == "madgrad":
+        assert rel(b, a) < 1e-5, "offload plumbing changed the device update"
+        # host (PyTorch fp32) vs device (HIP kernel) arithmetic over 3 steps: MADGRAD's first steps
+        # divide by the cube root of a tiny second-moment sum (eps 1e-6), which amplifies rounding on
+        # near-zero gradient elements (measured 3 % of the update norm)
+        assert rel(c, b) < 6e-2, rel(c, b)
+    else:
+        assert rel(fin["host"], fin["device"]) < 1e-4, rel(fin["host"], fin["device"])
