@@ -553,6 +553,50 @@ def conv_dgrad(g, y, al, be, wd, shp: ConvShape, x_shape, epi=EPI_STORE, out=Non
     return out, (part if epi in (EPI_ACTBWD, EPI_JOINBWD) else None)
 
 
+# Halo-staged 3x3 stride-1 weight gradient (csrc/kernels/conv_wh3.hip) on the materialised
+# operands (folded gradient, normalised input): a workgroup owns (co, ci) x all nine taps and
+# stages each 128-pixel chunk's input halo once instead of once per tap.  FDT_WGRAD_H3=0 keeps
+# the implicit-GEMM weight gradient; FDT_WGRAD_H3_WGS: target workgroups (one per CU: ~110 KB
+# of LDS each), the pixel split follows.
+WH3 = os.environ.get("FDT_WGRAD_H3", "1") == "1"
+WH3_WGS = int(os.environ.get("FDT_WGRAD_H3_WGS", "256"))
+WH3_PX = 128
+
+
+def wh3_plan(N, H, W, shp: "ConvShape", cx, fold=False, xaff=False, force=False):
+    """((BMC, BNC), nsplit) of the halo weight gradient, or None (conv_wh3.hip's geometry:
+    3x3 pad-1 stride-1, power-of-two images >= 4x4, 128-pixel chunks of whole rows whose halo fits
+    288 rows, no fused fold / input transform)."""
+    if not (WH3 or force) or fold or xaff or shp.k != 3 or shp.stride != 1 or shp.pad != 1:
+        return None
+    if H < 4 or W < 4 or H & (H - 1) or W & (W - 1) or W > WH3_PX:
+        return None
+    M = N * H * W
+    if M % WH3_PX:
+        return None
+    rb = min(H, WH3_PX // W)
+    if (WH3_PX // (rb * W)) * (rb + 2) * (W + 2) > WH3_PX // 16 * 36:
+        return None
+    co = shp.cout
+    if co % 128 == 0 and cx % 32 == 0:
+        t = (128, 32)
+    elif co % 64 == 0 and cx % 64 == 0:
+        t = (64, 64)
+    else:
+        return None
+    # measured (scripts/bench_h3.py --only wgrad, profiles/r6/bench_wh3_*.txt): a win on every
+    # batch-1024 layer (32x32 211 -> 118 us, 16x16 156 -> 95, 8x8 114 -> 94, 4x4 119 -> 94) and on
+    # the 32x32 / 16x16 layers at batch 128; the small 8x8 / 4x4 layers at batch 128 (~30 us,
+    # latency-bound either way) keep the implicit-GEMM kernel
+    if not force and W < 16 and M * co * cx < (1 << 31):
+        return None
+    tiles = (co // t[0]) * (cx // t[1])
+    chunks = M // WH3_PX
+    ns = max(1, min(chunks, WH3_WGS // tiles))
+    cps = -(-chunks // ns)
+    return t, -(-chunks // cps)
+
+
 def wgrad_split(M: int, tiles: int, want: int = 512, min_px: int = 1024) -> int:
     s = max(1, want // max(tiles, 1))
     s = min(s, max(1, M // min_px))
@@ -560,15 +604,32 @@ def wgrad_split(M: int, tiles: int, want: int = 512, min_px: int = 1024) -> int:
 
 
 def conv_wgrad(g, y, al, be, x, shp: ConvShape, out, xs=None, xt=None, act=0, alpha=1.0, accumulate=False,
-               tile=None, nsplit=None, slab=None, gs=None):
+               tile=None, nsplit=None, slab=None, gs=None, h3=None):
     """out (fp32 OIHW [Cout, Cin, k, k]) = dL/dW of y = conv(act(x*xs+xt)) given
-    g (gradient wrt y, corrected to g*gs + al + be*y in the kernel; gs None: 1)."""
+    g (gradient wrt y, corrected to g*gs + al + be*y in the kernel; gs None: 1).  ``h3``: the
+    halo weight gradient (``wh3_plan``) -- None = where it applies (no explicit tile), True =
+    forced, False = the implicit-GEMM kernel."""
     nat = _native.native()
     N, Hy, Wy, Cy = g.shape
     Nx, H, W, Cx = x.shape
     assert Cx == shp.cxp and Cy == shp.cout
     M = N * Hy * Wy
     ldw = shp.ntaps * shp.cxp
+    wp = None
+    if h3 is True or (h3 is None and tile is None and nsplit is None):
+        wp = wh3_plan(N, H, W, shp, Cx, al is not None, xs is not None or act != 0, force=h3 is True)
+        assert wp is not None or h3 is not True, "halo weight gradient: unsupported geometry"
+    if wp is not None:
+        assert g.is_contiguous() and x.is_contiguous() and g.dtype == torch.bfloat16 and x.dtype == torch.bfloat16
+        assert out.is_contiguous() and tuple(out.shape) == (shp.cout, shp.cin, 3, 3)
+        (bmc, bnc), ns = wp
+        _log("wgrad_h3", N, H, shp, None, (bmc, bnc, WH3_PX), ns, 9)  # (kg 9 marks the halo wgrad)
+        if slab is None or slab.numel() < ns * shp.cout * ldw:
+            slab = torch.empty(ns * shp.cout * ldw, device=g.device, dtype=torch.float32)
+        nat.conv_wgrad_h3(g.data_ptr(), x.data_ptr(), slab.data_ptr(), N, H, W, Cx, shp.cout, bmc, bnc, ns, _sp())
+        nat.wgrad_reduce(slab.data_ptr(), out.data_ptr(), ns, shp.cout, shp.cin, shp.ntaps, shp.cxp,
+                         int(accumulate), _sp())
+        return out
     ent = None
     if tile is None:
         ent = tuned(f"wgrad{int(al is not None)}{int(xs is not None or act != 0)}", N, H, shp) or \

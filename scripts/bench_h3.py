@@ -24,6 +24,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--batch", type=int, default=1024)
     ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--only", default=None, help="comma list of ops (wgrad,fwd,dgrad)")
     a = ap.parse_args()
     dev = torch.device("cuda")
     N = a.batch
@@ -40,12 +41,26 @@ def main():
         flop = 2.0 * N * H * H * Co * C * 9
         part = ci.stat_slots(2, Co, dev, N * H * H)
         pd = ci.stat_slots(2, C, dev, N * H * H)
+        out = torch.zeros(Co, C, 3, 3, device=dev)
         ops = {
+            "wgrad": lambda kg: ci.conv_wgrad(g, None, None, None, x, shp, out, h3=kg is not None),
             "fwd": lambda kg: ci.conv_fwd(x, wf, shp, part=part, kg=kg)[0],
             "dgrad": lambda kg: ci.conv_dgrad(g, None, None, None, wd, shp, (N, H, H, C), epi=ci.EPI_ACTBWD, ex=ex,
                                               es=es, et=et, act=1, part=pd, kg=kg)[0],
         }
         for name, fn in ops.items():
+            if a.only and name not in a.only.split(","):
+                continue
+            if name == "wgrad":
+                plan = ci.wh3_plan(N, H, H, shp, C, force=True)
+                t_old = timeit(lambda: fn(None), a.reps)
+                y_old = fn(None).clone()
+                t_new = timeit(lambda: fn(True), a.reps)
+                y_new = fn(True).clone()
+                d = ((y_new - y_old).norm() / y_old.norm()).item()
+                print(f"N {N} {H}x{H} {C}->{Co} wgrad: implicit GEMM {t_old * 1e3:6.1f} us ({flop / t_old / 1e9:5.0f} TF/s)"
+                      f"  halo {plan}: {t_new * 1e3:6.1f} us ({flop / t_new / 1e9:5.0f} TF/s, {d:.0e})", flush=True)
+                continue
             h3 = ci.h3_tile(N, H, H, shp, ci.PRO_NONE, Co if name == "fwd" else C, force=True)
             ci.H3 = False
             t_old = timeit(lambda: fn(None), a.reps)

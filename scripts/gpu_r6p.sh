@@ -1,0 +1,15 @@
+#!/usr/bin/env bash
+# Round 6: halo-staged 3x3 weight gradient -- numerics and per-layer timing.
+set -o pipefail
+cd "$(dirname "$0")/.."
+export TMPDIR=/tmp
+OUT=gpurun_out/${1:-r6p}
+mkdir -p "$OUT"
+FDT_NATIVE=1 timeout -k 10 120 python -c "from faster_distributed_training_amd.ops import _native; _native.native()" || { echo "native extension stale or missing"; exit 1; }
+timeout -k 10 300 python -u -m pytest tests/test_conv_kernels.py -m gpu -q -p no:cacheprovider --timeout 120 --timeout-method thread -k "h3_conv_wgrad" > "$OUT/pytest_wh3.log" 2>&1; rc=$?
+echo "pytest wh3 rc=$rc"; tail -1 "$OUT/pytest_wh3.log"
+case $rc in 0) ;; 1) grep -E "^(FAILED|E )" "$OUT/pytest_wh3.log" | head -20; exit 1;; *) echo aborted; tail -20 "$OUT/pytest_wh3.log"; exit 1;; esac
+timeout -k 10 300 python -u scripts/bench_h3.py --batch 1024 --only wgrad > "$OUT/bench_wh3_1024.txt" 2>&1 || { echo "bench failed"; tail -20 "$OUT/bench_wh3_1024.txt"; exit 1; }
+grep -v amdgpu.ids "$OUT/bench_wh3_1024.txt"
+timeout -k 10 300 python -u scripts/bench_h3.py --batch 128 --only wgrad > "$OUT/bench_wh3_128.txt" 2>&1 || { echo "bench failed"; tail -20 "$OUT/bench_wh3_128.txt"; exit 1; }
+grep -v amdgpu.ids "$OUT/bench_wh3_128.txt"

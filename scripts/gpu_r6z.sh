@@ -5,23 +5,24 @@ set -o pipefail
 cd "$(dirname "$0")/.."
 export TMPDIR=/tmp
 OUT=gpurun_out/${1:-r6z}
-SKIP_TESTS=${SKIP_TESTS:-0}
+MODE=${MODE:-bench}  # tests | bench
 mkdir -p "$OUT"
 FDT_NATIVE=1 timeout -k 10 120 python -c "from faster_distributed_training_amd.ops import _native; _native.native()" || { echo "native extension stale or missing"; exit 1; }
 j() { grep -h '"value"' "$OUT/$1.log" > "$OUT/$1.json"; echo "$1 $(grep -o '"ms_per_step": [0-9.]*' $OUT/$1.json) $(grep -o '"host_ms_per_step": [0-9.]*' $OUT/$1.json) $(grep -o '"host_busy_ms_per_step": [0-9.]*' $OUT/$1.json)"; }
+if [ "$MODE" = tests ]; then
+  timeout -k 10 1080 python -u -m pytest tests -m gpu -v -p no:cacheprovider --timeout 300 --timeout-method thread > "$OUT/pytest_gpu.log" 2>&1; rc=$?
+  echo "pytest gpu rc=$rc"; tail -1 "$OUT/pytest_gpu.log"
+  case $rc in 0) ;; 1) grep -E "^(FAILED|ERROR)" "$OUT/pytest_gpu.log" | head -20;; *) echo aborted; tail -20 "$OUT/pytest_gpu.log"; exit 1;; esac
+  timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > "$OUT/smoke.log" 2>&1 || { echo "smoke failed"; tail -5 "$OUT/smoke.log"; exit 1; }
+  tail -1 "$OUT/smoke.log"
+  exit 0
+fi
 timeout -k 10 300 python bench.py > "$OUT/bench_default.log" 2>&1 || { echo "bench failed"; tail -5 "$OUT/bench_default.log"; exit 1; }
 j bench_default
 timeout -k 10 300 python bench.py --global-batch 128 --steps 40 > "$OUT/bs128.log" 2>&1 || { echo "bs128 failed"; exit 1; }
 j bs128
 timeout -k 10 300 python bench.py --global-batch 128 --steps 40 --ddp > "$OUT/bs128_ddp.log" 2>&1 || { echo "bs128 ddp failed"; exit 1; }
 j bs128_ddp
-if [ "$SKIP_TESTS" != 1 ]; then
-  timeout -k 10 1500 python -u -m pytest tests -m gpu -v -p no:cacheprovider --timeout 600 --timeout-method thread > "$OUT/pytest_gpu.log" 2>&1; rc=$?
-  echo "pytest gpu rc=$rc"; tail -1 "$OUT/pytest_gpu.log"
-  case $rc in 0) ;; 1) grep -E "^(FAILED|ERROR)" "$OUT/pytest_gpu.log" | head -20;; *) echo aborted; tail -20 "$OUT/pytest_gpu.log"; exit 1;; esac
-  timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > "$OUT/smoke.log" 2>&1 || { echo "smoke failed"; tail -5 "$OUT/smoke.log"; exit 1; }
-  tail -1 "$OUT/smoke.log"
-fi
 timeout -k 10 300 python bench.py --model transformer > "$OUT/tr_b256.log" 2>&1 || { echo "tr failed"; exit 1; }
 j tr_b256
 timeout -k 10 300 python bench.py --model transformer --global-batch 32 --steps 40 --warmup 15 > "$OUT/tr_b32.log" 2>&1 || { echo "tr b32 failed"; exit 1; }

@@ -257,6 +257,34 @@ def test_h3_conv_dgrad(cuda, case, epi, kg, loop, monkeypatch):
     assert rel(ps[1], gp.reshape(-1, Cin).sum(0)) < 1e-2
 
 
+WH3_CASES = [(2, 32, 64, 64), (4, 16, 128, 128), (4, 8, 256, 256), (16, 4, 512, 512), (2, 16, 64, 128),
+             (4, 8, 128, 64), (32, 4, 64, 128), (8, 32, 64, 64)]
+
+
+@pytest.mark.parametrize("case", WH3_CASES)
+@pytest.mark.parametrize("wgs", [256, 7])
+def test_h3_conv_wgrad(cuda, case, wgs, monkeypatch):
+    """Halo-staged 3x3 weight gradient (conv_wh3.hip) against fp32 PyTorch and the implicit-GEMM
+    weight gradient, fresh and accumulating; ``wgs`` 7: few workgroups -> long pixel ranges per
+    split (uneven last split)."""
+    monkeypatch.setattr(ci, "WH3_WGS", wgs)
+    N, H, Cin, Cout = case
+    torch.manual_seed(9)
+    shp = ci.ConvShape(Cin, Cout, 3, 1, 1)
+    x = make((N, H, H, Cin), cuda)
+    g = make((N, H, H, Cout), cuda)
+    assert ci.wh3_plan(N, H, H, shp, Cin, force=True) is not None
+    ref = torch.nn.grad.conv2d_weight(nchw(x.float()), (Cout, Cin, 3, 3), nchw(g.float()), padding=1)
+    out = torch.zeros(Cout, Cin, 3, 3, device=cuda)
+    ci.conv_wgrad(g, None, None, None, x, shp, out, h3=True)
+    assert rel(out, ref) < 2e-3, rel(out, ref)
+    old = torch.zeros_like(out)
+    ci.conv_wgrad(g, None, None, None, x, shp, old, h3=False)
+    assert rel(out, old) < 2e-3
+    ci.conv_wgrad(g, None, None, None, x, shp, out, accumulate=True, h3=True)
+    assert rel(out, 2 * ref) < 2e-3
+
+
 WGRAD_CASES = [
     (4, 8, 64, 128, 1, 1, 0),
     (2, 8, 64, 64, 3, 1, 1),
