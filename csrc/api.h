@@ -51,7 +51,7 @@ void grad_sumsq(uint64_t g, long n, uint64_t inv_scale, int unscale, uint64_t pa
 // halo-staged 3x3 stride-1 weight gradient into per-split fp32 slabs [nsplit][Cout][9*Cx]
 // (conv_wh3.hip; wgrad_reduce combines them)
 void conv_wgrad_h3(uint64_t g, uint64_t x, uint64_t slab, int N, int H, int W, int Cx, int Cout, int BMC, int BNC,
-                   int nsplit, uint64_t stream);
+                   int nsplit, int pipe, uint64_t stream);
 // test aid: fill every CU's LDS with a NaN pattern (conv_h3.hip)
 void lds_poison(uint64_t sink, int nblocks, uint64_t stream);
 void grad_norm_finalize(uint64_t part, int nb, float max_norm, uint64_t out, uint64_t total, int phase,

@@ -63,9 +63,13 @@ __device__ __forceinline__ int wh3_swz(int row) {
   else return 0;
 }
 
-template <int BMC, int BNC>
+// CPW: 32-row output-channel blocks per wave (each fragment read then feeds more MFMAs; CPW = 2
+// needs 288 accumulator registers and spilled ~350 VGPRs: only CPW = 1 is instantiated); PIPE:
+// register double-buffered fragments across 16-pixel steps (measured: a win on the 64 x 64
+// tile, a loss on 128 x 32, profiles/r6/bench_wh3_1024*.txt)
+template <int BMC, int BNC, int CPW, bool PIPE>
 __global__ __launch_bounds__(256, 1) void wh3_kernel(const Wh3Args a) {
-  static_assert((BMC / 32) * (BNC / 32) == 4, "one 32 x 32 (co, ci) block per wave");
+  static_assert((BMC / 32 / CPW) * (BNC / 32) == 4, "four waves of CPW x 1 32 x 32 (co, ci) blocks");
   constexpr int GT = kWh3Px * BMC;         // gradient tile, bf16 elements
   constexpr int XS = wh3_xs<BNC>();
   constexpr int XT = kWh3HaloMax * XS;     // halo tile
@@ -81,7 +85,8 @@ __global__ __launch_bounds__(256, 1) void wh3_kernel(const Wh3Args a) {
   const int split = rid / ntile, tile = rid - split * ntile;
   const int bco = tile / a.nbci, bci = tile - bco * a.nbci;
   const int co0 = bco * BMC, ci0 = bci * BNC;
-  const int cb = wid % (BMC / 32), nb = wid / (BMC / 32);  // this wave's 32 x 32 block
+  constexpr int NCP = BMC / 32 / CPW;
+  const int cb = (wid % NCP) * CPW, nb = wid / NCP;  // this wave's first co block, its ci block
   const int c_begin = split * a.cps;
   int c_end = c_begin + a.cps;
   if (c_end > a.nchunks) c_end = a.nchunks;
@@ -144,11 +149,13 @@ __global__ __launch_bounds__(256, 1) void wh3_kernel(const Wh3Args a) {
       if (xdst[j] >= 0) *reinterpret_cast<uint4*>(Xl + xdst[j]) = rxv[j];
   };
 
-  f32x16 acc[9];
+  f32x16 acc[CPW][9];
 #pragma unroll
-  for (int t = 0; t < 9; ++t)
+  for (int i = 0; i < CPW; ++i)
 #pragma unroll
-    for (int r = 0; r < 16; ++r) acc[t][r] = 0.f;
+    for (int t = 0; t < 9; ++t)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][t][r] = 0.f;
 
   // transposed fragment reads (conv_wgrad.hip): lane (gq, gp) of a 16-lane group supplies row
   // gq's 4 columns 4gp..4gp+3; lane l receives column l & 31, rows 8h..8h+7 of the 16-row step
@@ -167,31 +174,60 @@ __global__ __launch_bounds__(256, 1) void wh3_kernel(const Wh3Args a) {
     hq[ks][1] = halo_row(r0 + 4) * XS + xcol;
   }
 
+  // Fragments double-buffered in registers across the 16-pixel steps: step ks+1's ten reads are
+  // issued before step ks's nine MFMAs (sched_barrier pins the order), so their LDS latency hides
+  // behind the MFMAs of the one wave per SIMD (the default schedule issued each read just before
+  // its MFMA and waited on it).
   auto compute = [&](int buf) {
     const bf16* Gl = tiles + buf * (GT + XT);
     const bf16* Xl = Gl + GT;
-#pragma unroll
-    for (int ks = 0; ks < kWh3Px / 16; ++ks) {
+    constexpr int NSL = PIPE ? 2 : 1;
+    bf16x8_t af[NSL][CPW], bfv[NSL][9];
+    auto fetch = [&](int ks, int sl) {
       const int r0 = ks * 16 + 8 * h + gq, r1 = r0 + 4;
-      bf16x8_t af;
-      {
-        const bf16* p0 = Gl + r0 * BMC + 8 * ((gcol >> 3) ^ wh3_swz<BMC * 2>(r0)) + (gcol & 7);
-        const bf16* p1 = Gl + r1 * BMC + 8 * ((gcol >> 3) ^ wh3_swz<BMC * 2>(r1)) + (gcol & 7);
+#pragma unroll
+      for (int i = 0; i < CPW; ++i) {
+        const int col = gcol + 32 * i;
+        const bf16* p0 = Gl + r0 * BMC + 8 * ((col >> 3) ^ wh3_swz<BMC * 2>(r0)) + (col & 7);
+        const bf16* p1 = Gl + r1 * BMC + 8 * ((col >> 3) ^ wh3_swz<BMC * 2>(r1)) + (col & 7);
         const bf16x4w_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_bf16x4w*)(p0));
         const bf16x4w_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_bf16x4w*)(p1));
-        af = bf16x8_t{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        af[sl][i] = bf16x8_t{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
       }
-      bf16x8_t bfv[9];
 #pragma unroll
       for (int t = 0; t < 9; ++t) {
         const bf16* p0 = Xl + hq[ks][0] + toff[t];
         const bf16* p1 = Xl + hq[ks][1] + toff[t];
         const bf16x4w_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_bf16x4w*)(p0));
         const bf16x4w_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_bf16x4w*)(p1));
-        bfv[t] = bf16x8_t{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        bfv[sl][t] = bf16x8_t{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
       }
+    };
+    auto mma = [&](int sl) {
 #pragma unroll
-      for (int t = 0; t < 9; ++t) acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, bfv[t], acc[t], 0, 0, 0);
+      for (int t = 0; t < 9; ++t)
+#pragma unroll
+        for (int i = 0; i < CPW; ++i)
+          acc[i][t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[sl][i], bfv[sl][t], acc[i][t], 0, 0, 0);
+    };
+    if constexpr (PIPE) {
+      // step ks+1's reads issued before step ks's MFMAs (sched_barrier pins the order): their
+      // LDS latency hides behind the MFMAs of the one wave per SIMD
+      fetch(0, 0);
+#pragma unroll
+      for (int ks = 0; ks < kWh3Px / 16; ++ks) {
+        const int sl = ks & 1;
+        if (ks + 1 < kWh3Px / 16) fetch(ks + 1, sl ^ 1);
+        __builtin_amdgcn_sched_barrier(0);
+        mma(sl);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    } else {
+#pragma unroll
+      for (int ks = 0; ks < kWh3Px / 16; ++ks) {
+        fetch(ks, 0);
+        mma(0);
+      }
     }
   };
 
@@ -216,12 +252,14 @@ __global__ __launch_bounds__(256, 1) void wh3_kernel(const Wh3Args a) {
   float* dst = a.slab + (long)split * a.Cout * 9 * a.Cx;
   const int ci = ci0 + nb * 32 + (lane & 31);
 #pragma unroll
-  for (int t = 0; t < 9; ++t)
+  for (int i = 0; i < CPW; ++i)
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int co = co0 + cb * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-      dst[((long)co * 9 + t) * a.Cx + ci] = acc[t][r];
-    }
+    for (int t = 0; t < 9; ++t)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int co = co0 + (cb + i) * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+        dst[((long)co * 9 + t) * a.Cx + ci] = acc[i][t][r];
+      }
 }
 
 }  // namespace conv
@@ -229,7 +267,7 @@ __global__ __launch_bounds__(256, 1) void wh3_kernel(const Wh3Args a) {
 // Host: shapes checked here (the kernel trusts them).  Returns the number of pixel splits used
 // (the slab holds nsplit x Cout x 9*Cx floats).
 void conv_wgrad_h3(uint64_t g, uint64_t x, uint64_t slab, int N, int H, int W, int Cx, int Cout, int BMC, int BNC,
-                   int nsplit, uint64_t stream) {
+                   int nsplit, int pipe, uint64_t stream) {
   using namespace conv;
   auto ispow2 = [](int v) { return v > 0 && (v & (v - 1)) == 0; };
   FDT_CHECK(ispow2(W) && ispow2(H) && W >= 4 && H >= 4, "wgrad_h3: power-of-two image >= 4x4");
@@ -262,20 +300,22 @@ void conv_wgrad_h3(uint64_t g, uint64_t x, uint64_t slab, int N, int H, int W, i
   const size_t lds = (size_t)2 * (kWh3Px * BMC + kWh3HaloMax * (BNC == 64 ? 72 : BNC)) * 2;
   const int grid = a.nbco * a.nbci * a.nsplit;
   hipStream_t st = as_stream(stream);
-#define FDT_WH3(BMC_, BNC_)                                                                              \
-  if (BMC == BMC_ && BNC == BNC_) {                                                                      \
+#define FDT_WH3(BMC_, BNC_, CPW_, PIPE_)                                                                 \
+  if (BMC == BMC_ && BNC == BNC_ && pipe == PIPE_) {                                                     \
     static bool attr = false;                                                                            \
     if (!attr) {                                                                                         \
-      FDT_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(wh3_kernel<BMC_, BNC_>),            \
+      FDT_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(wh3_kernel<BMC_, BNC_, CPW_, PIPE_>), \
                                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));          \
       attr = true;                                                                                       \
     }                                                                                                    \
-    hipLaunchKernelGGL((wh3_kernel<BMC_, BNC_>), dim3(grid), dim3(256), lds, st, a);                      \
+    hipLaunchKernelGGL((wh3_kernel<BMC_, BNC_, CPW_, PIPE_>), dim3(grid), dim3(256), lds, st, a);         \
     FDT_LAUNCH_CHECK();                                                                                  \
     return;                                                                                              \
   }
-  FDT_WH3(128, 32)
-  FDT_WH3(64, 64)
+  FDT_WH3(128, 32, 1, false)
+  FDT_WH3(128, 32, 1, true)
+  FDT_WH3(64, 64, 1, false)
+  FDT_WH3(64, 64, 1, true)
 #undef FDT_WH3
 }
 

@@ -561,6 +561,8 @@ def conv_dgrad(g, y, al, be, wd, shp: ConvShape, x_shape, epi=EPI_STORE, out=Non
 WH3 = os.environ.get("FDT_WGRAD_H3", "1") == "1"
 WH3_WGS = int(os.environ.get("FDT_WGRAD_H3_WGS", "256"))
 WH3_PX = 128
+# register-pipelined fragments (conv_wh3.hip PIPE): None = the measured choice (the 64 x 64 tile)
+WH3_PIPE = {"1": True, "0": False}.get(os.environ.get("FDT_WGRAD_H3_PIPE", ""))
 
 
 def wh3_plan(N, H, W, shp: "ConvShape", cx, fold=False, xaff=False, force=False):
@@ -626,7 +628,8 @@ def conv_wgrad(g, y, al, be, x, shp: ConvShape, out, xs=None, xt=None, act=0, al
         _log("wgrad_h3", N, H, shp, None, (bmc, bnc, WH3_PX), ns, 9)  # (kg 9 marks the halo wgrad)
         if slab is None or slab.numel() < ns * shp.cout * ldw:
             slab = torch.empty(ns * shp.cout * ldw, device=g.device, dtype=torch.float32)
-        nat.conv_wgrad_h3(g.data_ptr(), x.data_ptr(), slab.data_ptr(), N, H, W, Cx, shp.cout, bmc, bnc, ns, _sp())
+        nat.conv_wgrad_h3(g.data_ptr(), x.data_ptr(), slab.data_ptr(), N, H, W, Cx, shp.cout, bmc, bnc, ns,
+                          int(WH3_PIPE if WH3_PIPE is not None else bnc == 64), _sp())
         nat.wgrad_reduce(slab.data_ptr(), out.data_ptr(), ns, shp.cout, shp.cin, shp.ntaps, shp.cxp,
                          int(accumulate), _sp())
         return out

@@ -45,6 +45,8 @@ for _ in range(a.reps):
             ci.conv_fwd(x, wf, shp, sv, tv, 1, 1.0, tile=tile, kg=a.kg)
     elif a.op == "dgrad":
         ci.conv_dgrad(g, yy, al, be, wd, shp, (N, H, H, Cin), tile=tile)
+    elif a.op == "wgrad_plain":  # materialised operands (the engine's 3x3 weight gradients); --kg 9: halo
+        ci.conv_wgrad(g, None, None, None, x, shp, gw, h3=a.kg == 9)
     else:
         ci.conv_wgrad(g, yy, al, be, x, shp, gw, sv, tv, 1, tile=tile)
 torch.cuda.synchronize()
