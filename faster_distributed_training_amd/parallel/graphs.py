@@ -19,6 +19,8 @@ from __future__ import annotations
 import contextlib
 import os
 
+import time
+
 import torch
 from torch.utils._python_dispatch import TorchDispatchMode
 
@@ -104,6 +106,21 @@ def _comm_side_stream(device):
     return st
 
 
+def drain_comm_watch():
+    """Finish every eager collective and give RCCL's watchdog thread a polling interval (100 ms)
+    to retire them, before a capture that can take collectives.  The watchdog polls the
+    completion event of every eager collective still on its list; once that collective's stream
+    has joined a graph capture (the first captured collective makes it join), HIP refuses the
+    query ("operation not permitted on an event last recorded in a capturing stream") and the
+    watchdog aborts the process -- seen in the closing runs of rounds 5 and 6, in the
+    capture-check test, whose eager check all-reduces are followed at once by the recapture."""
+    import torch.distributed as dist
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_backend() != "nccl":
+        return
+    torch.cuda.synchronize()
+    time.sleep(0.25)
+
+
 class Recorder:
     """Capture split into graph segments at deferred hook actions.
 
@@ -128,6 +145,8 @@ class Recorder:
 
     def begin(self):
         if self.stream is None:
+            # (autograd's device thread; the capture has not begun: synchronising is allowed)
+            drain_comm_watch()
             self.stream = torch.cuda.current_stream()
         with torch.cuda.stream(self.stream):
             self.cur = torch.cuda.CUDAGraph()
