@@ -560,6 +560,9 @@ def conv_dgrad(g, y, al, be, wd, shp: ConvShape, x_shape, epi=EPI_STORE, out=Non
 # of LDS each), the pixel split follows.
 WH3 = os.environ.get("FDT_WGRAD_H3", "1") == "1"
 WH3_WGS = int(os.environ.get("FDT_WGRAD_H3_WGS", "256"))
+# ... and at least this many 128-pixel chunks per workgroup (fewer splits: a smaller fp32 slab to
+# write and reduce when the pixel count is small)
+WH3_MIN_CPS = int(os.environ.get("FDT_WGRAD_H3_MIN_CPS", "1"))
 WH3_PX = 128
 # register-pipelined fragments (conv_wh3.hip PIPE): None = the measured choice (the 64 x 64 tile)
 WH3_PIPE = {"1": True, "0": False}.get(os.environ.get("FDT_WGRAD_H3_PIPE", ""))
@@ -594,7 +597,7 @@ def wh3_plan(N, H, W, shp: "ConvShape", cx, fold=False, xaff=False, force=False)
         return None
     tiles = (co // t[0]) * (cx // t[1])
     chunks = M // WH3_PX
-    ns = max(1, min(chunks, WH3_WGS // tiles))
+    ns = max(1, min(chunks // max(1, WH3_MIN_CPS), WH3_WGS // tiles))
     cps = -(-chunks // ns)
     return t, -(-chunks // cps)
 

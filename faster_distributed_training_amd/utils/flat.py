@@ -64,7 +64,12 @@ def partition_runs(sizes, world):
 # fixed ~25 us of launches and small-matrix math whatever its size (measured: ResNet-50 NGD
 # with an element-balanced 8-way split ran 1.7 ms on the rank holding the stem + stage 1
 # -- dozens of small tensors -- and 0.3-0.5 ms on the others, scripts/bench_ngd.py --world)
-NGD_AXIS_COST = int(os.environ.get("FDT_NGD_AXIS_COST", "200000"))
+# Round 6: 200000 -> 400000 from a sweep of every simulated world-8 rank on one box, back to back
+# (bench.py --simulate-world 8, profiles/r6/sim/balance/axis_cost_sweep.txt): slowest rank of
+# ResNet-50 NGD + meta-mixup 7.23 / 7.46 -> 7.19 / 7.14 ms, of the transformer at B=32 4.52 ->
+# 4.39 ms (the per-axis fixed cost -- launches, small-matrix math -- was underweighted: the rank
+# holding the most shape groups was the slowest)
+NGD_AXIS_COST = int(os.environ.get("FDT_NGD_AXIS_COST", "400000"))
 NGD_SLACK = float(os.environ.get("FDT_NGD_SLACK", "1.15"))
 
 
