@@ -90,27 +90,31 @@ struct H3Geom {
   }
 };
 
-template <int BM, int BN, int WM, int WN>
-constexpr size_t h3_stage_elems() { return (size_t)kH3Taps * BN * 16 + (size_t)h3_halo_rows_max<BM>() * kH3Row; }
+template <int BM, int BN, int WM, int WN, int TP = kH3Taps>
+constexpr size_t h3_stage_elems() { return (size_t)TP * BN * 16 + (size_t)h3_halo_rows_max<BM>() * kH3Row; }
 
 // DMA: the chunk's pieces move global -> LDS by LDS-DMA (buffer_load ... lds) issued at the top of
 // the previous chunk's MFMAs (no staging registers, no ds_write phase); otherwise register-staged.
 // NS: LDS stages.  2 = double-buffered (one workgroup per CU); 1 (LDS-DMA only) = one stage
 // (load -> barrier -> MFMAs -> barrier), small enough for TWO workgroups per CU, whose phases
 // interleave -- and whose prologues / epilogues overlap the other's main loop.
-template <int BM, int BN, int EPI, int ACT, int WM, int WN, bool DMA, int NS = 2>
+// TP: taps (9 = a stride-1 3x3; 4 / 2 = an output-parity class of a stride-2 3x3 data gradient,
+// whose taps are the class's subset of the flipped 3x3 neighbourhood on the output-gradient grid;
+// the epilogue scatters the class grid into the full-resolution gradient, conv_epilogue's OS / oy
+// / ox mapping)
+template <int BM, int BN, int EPI, int ACT, int WM, int WN, bool DMA, int NS = 2, int TP = kH3Taps>
 __global__ __launch_bounds__(64 * WM * WN, (NS == 1 || BN == 64) ? 4 : 1) void h3_kernel(const ConvArgs a) {
   static_assert(NS == 2 || (NS == 1 && DMA), "single-stage: LDS-DMA staging");
   constexpr int NT = 64 * WM * WN;
   constexpr int TN = BN / WN / 32, TM = BM / WM / 32;
   static_assert(TN >= 1 && TM >= 1, "wave tile >= 32x32");
-  constexpr int WP = kH3Taps * BN * 2;         // weight 16-B pieces per chunk
+  constexpr int WP = TP * BN * 2;              // weight 16-B pieces per chunk
   constexpr int NWP = (WP + NT - 1) / NT;
   constexpr int HRM = h3_halo_rows_max<BM>();
   constexpr int NHP = (2 * HRM + NT - 1) / NT;  // halo 16-B pieces per thread (upper bound)
   constexpr int NQ = EPI == kEpiJoinBwd ? 3 : 2;
-  constexpr int WTILE = kH3Taps * BN * 16;      // bf16 elements of the weight tile
-  constexpr int STAGE = (int)h3_stage_elems<BM, BN, WM, WN>();
+  constexpr int WTILE = TP * BN * 16;           // bf16 elements of the weight tile
+  constexpr int STAGE = (int)h3_stage_elems<BM, BN, WM, WN, TP>();
 
   extern __shared__ __attribute__((aligned(16))) char smem[];
   float* red = reinterpret_cast<float*>(smem);              // [NT/64][NQ][BN]
@@ -133,7 +137,7 @@ __global__ __launch_bounds__(64 * WM * WN, (NS == 1 || BN == 64) ? 4 : 1) void h
   const int nbk = BM / (Rb * W), bhr = geo.bhr, bh0 = (Rb + 2) * W2, HR = nbk * bhr;
   const int img0 = (int)(m0 / HW), h0 = (int)((m0 / W) % H);
 
-  if (tid < kH3Taps) {
+  if (tid < TP) {
     ttab[tid] = a.wt[tid];
     ttab[kH3Taps + tid] = a.dh[tid] * W2 + a.dw[tid];
   }
@@ -173,9 +177,9 @@ __global__ __launch_bounds__(64 * WM * WN, (NS == 1 || BN == 64) ? 4 : 1) void h
   int qb[TM];
 #pragma unroll
   for (int j = 0; j < TM; ++j) qb[j] = geo.halo_row(geo.pix(wm * TM + j, lane & 31));
-  int toff[kH3Taps];
+  int toff[TP];
 #pragma unroll
-  for (int t = 0; t < kH3Taps; ++t) toff[t] = ttab[kH3Taps + t];
+  for (int t = 0; t < TP; ++t) toff[t] = ttab[kH3Taps + t];
   const int h = lane >> 5;
   const int ahalf = 8 * (h ^ ((lane >> 3) & 1));  // A-fragment half (the weight tile's swizzle)
 
@@ -225,9 +229,9 @@ __global__ __launch_bounds__(64 * WM * WN, (NS == 1 || BN == 64) ? 4 : 1) void h
     };
     fetch(0, 0);
 #pragma unroll
-    for (int t = 0; t < kH3Taps; ++t) {
+    for (int t = 0; t < TP; ++t) {
       const int sl = t & 1;
-      if (t + 1 < kH3Taps) fetch(t + 1, sl ^ 1);
+      if (t + 1 < TP) fetch(t + 1, sl ^ 1);
       __builtin_amdgcn_sched_barrier(0);  // next tap's reads stay ahead of this tap's MFMAs
 #pragma unroll
       for (int i = 0; i < TN; ++i)
@@ -337,14 +341,14 @@ __global__ __launch_bounds__(64 * WM * WN, (NS == 1 || BN == 64) ? 4 : 1) void h
 }
 
 // host ------------------------------------------------------------------------------------
-template <int BM, int BN, int EPI, int ACT, int WM, int WN, bool DMA, int NS>
+template <int BM, int BN, int EPI, int ACT, int WM, int WN, bool DMA, int NS, int TP = kH3Taps>
 static void h3_launch_one(const ConvArgs& a, hipStream_t st) {
   constexpr int NT = 64 * WM * WN;
   constexpr int NQ = EPI == kEpiJoinBwd ? 3 : 2;
   constexpr size_t hdr = ((((size_t)(NT / 64) * NQ * BN + 2 * kH3Taps) * 4 + 15) & ~(size_t)15);
-  const size_t tiles = NS * h3_stage_elems<BM, BN, WM, WN>() * 2, stage = (size_t)WM * 32 * (BN + 4) * 4;
+  const size_t tiles = NS * h3_stage_elems<BM, BN, WM, WN, TP>() * 2, stage = (size_t)WM * 32 * (BN + 4) * 4;
   const size_t lds = hdr + (tiles > stage ? tiles : stage);
-  auto kern = h3_kernel<BM, BN, EPI, ACT, WM, WN, DMA, NS>;
+  auto kern = h3_kernel<BM, BN, EPI, ACT, WM, WN, DMA, NS, TP>;
   static bool attr = false;
   if (!attr) {
     FDT_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -357,10 +361,15 @@ static void h3_launch_one(const ConvArgs& a, hipStream_t st) {
 
 // Geometry the halo loop admits (checked on the host before any launch)
 bool h3_supported(const ConvArgs& a, int BM) {
-  if (a.ntaps != kH3Taps || a.S != 1 || a.Hi != a.Ho || a.Wi != a.Wo || a.OS != 1 || a.oy != 0 || a.ox != 0 ||
-      a.Hout != a.Ho || a.Wout != a.Wo || a.nsplit != 1 || (a.Cx & 15) != 0)
+  // 9 taps: a stride-1 3x3 (dense output); 2 / 4 taps: a parity class of a stride-2 3x3 data
+  // gradient (output scattered to every OS-th pixel of the full-resolution gradient)
+  const bool dense = a.OS == 1 && a.oy == 0 && a.ox == 0 && a.Hout == a.Ho && a.Wout == a.Wo;
+  const bool cls = (a.ntaps == 2 || a.ntaps == 4) && a.OS == 2 && a.oy >= 0 && a.oy < 2 && a.ox >= 0 && a.ox < 2 &&
+                   a.Hout == 2 * a.Ho && a.Wout == 2 * a.Wo;
+  if (!((a.ntaps == kH3Taps && dense) || cls) || a.S != 1 || a.Hi != a.Ho || a.Wi != a.Wo || a.nsplit != 1 ||
+      (a.Cx & 15) != 0)
     return false;
-  for (int t = 0; t < kH3Taps; ++t)
+  for (int t = 0; t < a.ntaps; ++t)
     if (a.dh[t] < -1 || a.dh[t] > 1 || a.dw[t] < -1 || a.dw[t] > 1 || a.wt[t] < 0 || a.wt[t] >= kH3Taps) return false;
   const int W = a.Wi, H = a.Hi;
   if (W < 4 || (W & (W - 1)) != 0 || BM % W != 0 || a.M % BM != 0) return false;
@@ -380,6 +389,23 @@ bool launch_h3(int pro, int epi, int act, const ConvArgs& a, int BM, int BN, int
   if (pro != kProNone) return false;
   FDT_CHECK(h3_supported(a, BM), "halo 3x3 conv: unsupported geometry");
   FDT_CHECK(a.Cout % BN == 0, "halo 3x3 conv: Cout % BN");
+  if (a.ntaps != kH3Taps) {
+    // stride-2 data-gradient parity classes: the double-buffered LDS-DMA loop (kg 6) only
+    FDT_CHECK(kg == 6, "halo 3x3 conv: parity classes run kg 6");
+#define FDT_H3C(BM_, BN_, WM_, WN_, TP_)                                                                                 \
+    if (BM == BM_ && BN == BN_ && a.ntaps == TP_) {                                                                     \
+      if (epi == kEpiActBwd && act == kActRelu) { h3_launch_one<BM_, BN_, kEpiActBwd, kActRelu, WM_, WN_, true, 2, TP_>(a, st); return true; } \
+      if (epi == kEpiActBwd && act == kActCelu) { h3_launch_one<BM_, BN_, kEpiActBwd, kActCelu, WM_, WN_, true, 2, TP_>(a, st); return true; } \
+      if (epi == kEpiStore && act == kActNone) { h3_launch_one<BM_, BN_, kEpiStore, kActNone, WM_, WN_, true, 2, TP_>(a, st); return true; } \
+      return false;                                                                                                     \
+    }
+    FDT_H3C(256, 128, 4, 2, 4)
+    FDT_H3C(256, 128, 4, 2, 2)
+    FDT_H3C(256, 64, 8, 1, 4)
+    FDT_H3C(256, 64, 8, 1, 2)
+#undef FDT_H3C
+    return false;
+  }
 #define FDT_H3E(BM_, BN_, WM_, WN_, D_, NS_)                                                                  \
   if (epi == kEpiStats && act == kActNone) { h3_launch_one<BM_, BN_, kEpiStats, kActNone, WM_, WN_, D_, NS_>(a, st); return true; } \
   if (epi == kEpiActBwd && act == kActRelu) { h3_launch_one<BM_, BN_, kEpiActBwd, kActRelu, WM_, WN_, D_, NS_>(a, st); return true; } \

@@ -213,6 +213,12 @@ H3_TILES = {(256, 128), (256, 64), (128, 128)}
 # "auto" = the measured per-shape choice (h3_auto)
 H3_LOOP = os.environ.get("FDT_CONV_H3_LOOP", "auto")
 H3_KGS = (5, 6, 7, 8)
+# the 2- and 4-tap output-parity classes of the stride-2 3x3 data gradients through the halo loop
+# (kg 6; H, W = the output-gradient grid); the 1-tap class stays a plain GEMM.  Measured SLOWER
+# (scripts/bench_s2.py, profiles/r6/bench_s2_*.txt: batch 1024 32x32 265 -> 318 us, 16x16 197 ->
+# 211, 8x8 137 -> 142; whole step 24.53-24.60 -> 24.59-24.73 ms): with 2-4 taps per chunk the halo
+# staging is not amortised.  Opt-in (tests keep it correct).
+H3_S2 = os.environ.get("FDT_CONV_H3_S2", "0") == "1"
 
 
 def _h3_kg(kg, W=8):
@@ -221,14 +227,15 @@ def _h3_kg(kg, W=8):
     return {"dma": 6, "dma64": 6, "auto": 6, "dma1": 7}.get(H3_LOOP, 5)
 
 
-def h3_tile(N, H, W, shp: "ConvShape", pro, cout, force=False, cx=None, bn=None):
+def h3_tile(N, H, W, shp: "ConvShape", pro, cout, force=False, cx=None, bn=None, s2cls=False):
     """(BM, BN) of the halo 3x3 loop for this launch, or None (csrc/kernels/conv_h3.hip
     h3_supported: 3x3 pad-1 stride-1, prologue-free, whole image rows per 256-pixel tile).
     ``force`` (an explicit kg 5): ignore FDT_CONV_H3 and the small-grid cut-off.  ``cx``: the
     operand's channels (forward: cxp; data gradient: cout), a multiple of 16."""
     if cx is None:
         cx = shp.cxp
-    if not (H3 or force) or pro != PRO_NONE or cx % 16 or shp.k != 3 or shp.stride != 1 or shp.pad != 1 or W < 4 or W & (W - 1):
+    conv_ok = shp.k == 3 and shp.pad == 1 and shp.stride == (2 if s2cls else 1)
+    if not (H3 or force) or pro != PRO_NONE or cx % 16 or not conv_ok or W < 4 or W & (W - 1):
         return None
     bm = 256
     M = N * H * W
@@ -532,6 +539,10 @@ def conv_dgrad(g, y, al, be, wd, shp: ConvShape, x_shape, epi=EPI_STORE, out=Non
                 h3 = None if t3 is None else (t3, kg)
             elif H3:
                 h3 = h3_auto(N, Hx, Wx, shp, pro, shp.cin, cx=Cy)
+        elif (h3ok and epi in (EPI_ACTBWD, EPI_STORE) and len(dh) in (2, 4) and shp.k == 3 and shp.stride == 2
+              and Ha == Hy and Wa == Wy and (H3_S2 or kg in H3_KGS)):
+            t3 = h3_tile(N, Ha, Wa, shp, pro, shp.cin, force=kg in H3_KGS, cx=Cy, s2cls=True)
+            h3 = None if t3 is None else (t3, 6)
         if h3 is not None:
             ((bm, bn), kgv), bk = h3, 16
             ns, slab_p, cnt_p = 1, 0, 0

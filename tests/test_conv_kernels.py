@@ -257,6 +257,47 @@ def test_h3_conv_dgrad(cuda, case, epi, kg, loop, monkeypatch):
     assert rel(ps[1], gp.reshape(-1, Cin).sum(0)) < 1e-2
 
 
+H3S2_CASES = [(4, 32, 128, 128), (8, 16, 256, 256), (16, 8, 512, 512), (4, 16, 64, 64), (4, 32, 64, 128)]
+
+
+@pytest.mark.parametrize("case", H3S2_CASES)
+@pytest.mark.parametrize("epi", ["store", "actbwd_relu"])
+def test_h3_conv_dgrad_stride2_classes(cuda, case, epi):
+    """Stride-2 3x3 data gradient whose 2- and 4-tap output-parity classes run through the halo
+    loop (kg 6, the class grid = the output-gradient grid, scattered to every other pixel), the
+    1-tap class through the implicit GEMM: against fp32 PyTorch."""
+    N, Hx, Cin, Cout = case
+    torch.manual_seed(11)
+    shp = ci.ConvShape(Cin, Cout, 3, 2, 1)
+    w = torch.randn(Cout, Cin, 3, 3, device=cuda) / (Cin * 9) ** 0.5
+    wf, wd = ci.alloc_packed(shp, cuda)
+    ci.pack_weights([(w, wf, wd, shp)])
+    Hy = Hx // 2
+    g = make((N, Hy, Hy, Cout), cuda)
+    ref = nhwc(torch.nn.grad.conv2d_input((N, Cin, Hx, Hx), w.to(BF).float(), nchw(g.float()), stride=2, padding=1))
+    xs = (N, Hx, Hx, Cin)
+    ci.LAUNCH_LOG = []
+    try:
+        if epi == "store":
+            out, _ = ci.conv_dgrad(g, None, None, None, wd, shp, xs, epi=ci.EPI_STORE, kg=6)
+            assert rel(out, ref) < 1e-2, rel(out, ref)
+        else:
+            ex = make(xs, cuda)
+            es = torch.rand(Cin, device=cuda) + 0.5
+            et = torch.randn(Cin, device=cuda) * 0.3
+            gp = ref * ((ex.float() * es + et) > 0).float()
+            out, part = ci.conv_dgrad(g, None, None, None, wd, shp, xs, epi=ci.EPI_ACTBWD, ex=ex, es=es, et=et, act=1,
+                                      kg=6)
+            assert rel(out, gp * es) < 1e-2
+            ps = part.sum(0)
+            assert rel(ps[0], (gp * ex.float()).reshape(-1, Cin).sum(0)) < 1e-2
+            assert rel(ps[1], gp.reshape(-1, Cin).sum(0)) < 1e-2
+        log = list(ci.LAUNCH_LOG)
+    finally:
+        ci.LAUNCH_LOG = None
+    assert sum(1 for e in log if e[0] == "dgrad" and e[5] == 6) == 3, log  # the 2-, 2- and 4-tap classes
+
+
 WH3_CASES = [(2, 32, 64, 64), (4, 16, 128, 128), (4, 8, 256, 256), (16, 4, 512, 512), (2, 16, 64, 128),
              (4, 8, 128, 64), (32, 4, 64, 128), (8, 32, 64, 64)]
 
