@@ -65,17 +65,23 @@ __device__ __forceinline__ int wh3_swz(int row) {
 
 // CPW: 32-row output-channel blocks per wave (each fragment read then feeds more MFMAs; CPW = 2
 // needs 288 accumulator registers and spilled ~350 VGPRs: only CPW = 1 is instantiated); PIPE:
-// register double-buffered fragments across 16-pixel steps (measured: a win on the 64 x 64
-// tile, a loss on 128 x 32, profiles/r6/bench_wh3_1024*.txt)
-template <int BMC, int BNC, int CPW, bool PIPE>
-__global__ __launch_bounds__(256, 1) void wh3_kernel(const Wh3Args a) {
-  static_assert((BMC / 32 / CPW) * (BNC / 32) == 4, "four waves of CPW x 1 32 x 32 (co, ci) blocks");
+// register double-buffered fragments across 16-pixel steps (measured at the final register
+// allocation: slower on every tile, profiles/r6/wh3_ts*_p*_*.txt -- opt-in)
+// TS: waves per (co, ci) block, each holding ceil(9 / TS) of the nine tap accumulators (TS = 2:
+// eight waves, two per SIMD -- one wave's LDS reads under the other's MFMAs -- at <= 256
+// registers each)
+template <int BMC, int BNC, int CPW, bool PIPE, int TS = 1>
+__global__ __launch_bounds__(256 * TS, 1) void wh3_kernel(const Wh3Args a) {
+  static_assert((BMC / 32 / CPW) * (BNC / 32) == 4, "four (co, ci) block groups of CPW x 1 32 x 32 blocks");
+  static_assert(TS == 1 || CPW == 1, "tap split: one co block per wave");
+  constexpr int NTH = 256 * TS;             // threads
+  constexpr int TPW = (9 + TS - 1) / TS;    // tap accumulators per wave
   constexpr int GT = kWh3Px * BMC;         // gradient tile, bf16 elements
   constexpr int XS = wh3_xs<BNC>();
   constexpr int XT = kWh3HaloMax * XS;     // halo tile
   constexpr int GCH = BMC / 8, XCH = BNC / 8;      // 16-B chunks per row
-  constexpr int NGP = kWh3Px * GCH / 256;          // gradient pieces per thread
-  constexpr int NXP = (kWh3HaloMax * XCH + 255) / 256;
+  constexpr int NGP = kWh3Px * GCH / NTH;          // gradient pieces per thread
+  constexpr int NXP = (kWh3HaloMax * XCH + NTH - 1) / NTH;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   bf16* tiles = reinterpret_cast<bf16*>(smem);  // [2][GT + XT]
 
@@ -86,7 +92,9 @@ __global__ __launch_bounds__(256, 1) void wh3_kernel(const Wh3Args a) {
   const int bco = tile / a.nbci, bci = tile - bco * a.nbci;
   const int co0 = bco * BMC, ci0 = bci * BNC;
   constexpr int NCP = BMC / 32 / CPW;
-  const int cb = (wid % NCP) * CPW, nb = wid / NCP;  // this wave's first co block, its ci block
+  const int blk = wid & 3, t0 = (wid >> 2) * TPW;  // (co, ci) block group; first tap of this wave
+  const int cb = (blk % NCP) * CPW, nb = blk / NCP;  // this wave's first co block, its ci block
+  const int ntw = 9 - t0 < TPW ? 9 - t0 : TPW;       // taps of this wave (wave-uniform)
   const int c_begin = split * a.cps;
   int c_end = c_begin + a.cps;
   if (c_end > a.nchunks) c_end = a.nchunks;
@@ -104,7 +112,7 @@ __global__ __launch_bounds__(256, 1) void wh3_kernel(const Wh3Args a) {
   int gdst[NGP];
 #pragma unroll
   for (int j = 0; j < NGP; ++j) {
-    const int i = tid + j * 256, row = i / GCH, cc = i - row * GCH;
+    const int i = tid + j * NTH, row = i / GCH, cc = i - row * GCH;
     goffl[j] = ((uint32_t)row * (uint32_t)a.Cout + (uint32_t)(co0 + 8 * cc)) * 2u;
     gdst[j] = row * BMC + 8 * (cc ^ wh3_swz<BMC * 2>(row));
   }
@@ -112,7 +120,7 @@ __global__ __launch_bounds__(256, 1) void wh3_kernel(const Wh3Args a) {
   int xpk[NXP], xdst[NXP];
 #pragma unroll
   for (int j = 0; j < NXP; ++j) {
-    const int i = tid + j * 256, q = i / XCH, cc = i - q * XCH;
+    const int i = tid + j * NTH, q = i / XCH, cc = i - q * XCH;
     const bool v = q < a.HR;
     const int b = q / bhr, r2 = q - b * bhr, hr = r2 / W2, hc = r2 - hr * W2;
     xpk[j] = v ? (b | (hr << 4) | (hc << 10) | (cc << 17)) : -1;
@@ -149,11 +157,11 @@ __global__ __launch_bounds__(256, 1) void wh3_kernel(const Wh3Args a) {
       if (xdst[j] >= 0) *reinterpret_cast<uint4*>(Xl + xdst[j]) = rxv[j];
   };
 
-  f32x16 acc[CPW][9];
+  f32x16 acc[CPW][TPW];
 #pragma unroll
   for (int i = 0; i < CPW; ++i)
 #pragma unroll
-    for (int t = 0; t < 9; ++t)
+    for (int t = 0; t < TPW; ++t)
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][t][r] = 0.f;
 
@@ -162,9 +170,12 @@ __global__ __launch_bounds__(256, 1) void wh3_kernel(const Wh3Args a) {
   const int gq = (lane & 15) >> 2, gp = lane & 3, h = lane >> 5;
   const int colg = ((lane >> 4) & 1) * 16;
   const int gcol = cb * 32 + colg + 4 * gp, xcol = nb * 32 + colg + 4 * gp;
-  int toff[9];  // a tap = a constant element shift of the halo fragment addresses
+  int toff[TPW];  // a tap = a constant element shift of the halo fragment addresses
 #pragma unroll
-  for (int t = 0; t < 9; ++t) toff[t] = ((t / 3 - 1) * W2 + (t % 3 - 1)) * XS;
+  for (int tt = 0; tt < TPW; ++tt) {
+    const int t = t0 + tt;
+    toff[tt] = ((t / 3 - 1) * W2 + (t % 3 - 1)) * XS;
+  }
   // halo fragment addresses of this lane's pixels (tap (1, 1)), per 16-pixel step: rows r0, r0 + 4
   int hq[kWh3Px / 16][2];
 #pragma unroll
@@ -182,7 +193,7 @@ __global__ __launch_bounds__(256, 1) void wh3_kernel(const Wh3Args a) {
     const bf16* Gl = tiles + buf * (GT + XT);
     const bf16* Xl = Gl + GT;
     constexpr int NSL = PIPE ? 2 : 1;
-    bf16x8_t af[NSL][CPW], bfv[NSL][9];
+    bf16x8_t af[NSL][CPW], bfv[NSL][TPW];
     auto fetch = [&](int ks, int sl) {
       const int r0 = ks * 16 + 8 * h + gq, r1 = r0 + 4;
 #pragma unroll
@@ -205,10 +216,11 @@ __global__ __launch_bounds__(256, 1) void wh3_kernel(const Wh3Args a) {
     };
     auto mma = [&](int sl) {
 #pragma unroll
-      for (int t = 0; t < 9; ++t)
+      for (int t = 0; t < TPW; ++t)
 #pragma unroll
         for (int i = 0; i < CPW; ++i)
-          acc[i][t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[sl][i], bfv[sl][t], acc[i][t], 0, 0, 0);
+          if (TS == 1 || t < ntw)  // (the last wave of a tap split holds fewer taps)
+            acc[i][t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[sl][i], bfv[sl][t], acc[i][t], 0, 0, 0);
     };
     if constexpr (PIPE) {
       // step ks+1's reads issued before step ks's MFMAs (sched_barrier pins the order): their
@@ -254,11 +266,13 @@ __global__ __launch_bounds__(256, 1) void wh3_kernel(const Wh3Args a) {
 #pragma unroll
   for (int i = 0; i < CPW; ++i)
 #pragma unroll
-    for (int t = 0; t < 9; ++t)
+    for (int t = 0; t < TPW; ++t)
+      if (TS == 1 || t < ntw) {
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int co = co0 + (cb + i) * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-        dst[((long)co * 9 + t) * a.Cx + ci] = acc[i][t][r];
+        for (int r = 0; r < 16; ++r) {
+          const int co = co0 + (cb + i) * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+          dst[((long)co * 9 + t0 + t) * a.Cx + ci] = acc[i][t][r];
+        }
       }
 }
 
@@ -300,22 +314,28 @@ void conv_wgrad_h3(uint64_t g, uint64_t x, uint64_t slab, int N, int H, int W, i
   const size_t lds = (size_t)2 * (kWh3Px * BMC + kWh3HaloMax * (BNC == 64 ? 72 : BNC)) * 2;
   const int grid = a.nbco * a.nbci * a.nsplit;
   hipStream_t st = as_stream(stream);
-#define FDT_WH3(BMC_, BNC_, CPW_, PIPE_)                                                                 \
-  if (BMC == BMC_ && BNC == BNC_ && pipe == PIPE_) {                                                     \
+#define FDT_WH3(BMC_, BNC_, CPW_, PIPE_, TS_)                                                             \
+  if (BMC == BMC_ && BNC == BNC_ && (pipe & 1) == PIPE_ && ts == TS_) {                                  \
+    auto k = wh3_kernel<BMC_, BNC_, CPW_, PIPE_, TS_>;                                                   \
     static bool attr = false;                                                                            \
     if (!attr) {                                                                                         \
-      FDT_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(wh3_kernel<BMC_, BNC_, CPW_, PIPE_>), \
+      FDT_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(k),                                \
                                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));          \
       attr = true;                                                                                       \
     }                                                                                                    \
-    hipLaunchKernelGGL((wh3_kernel<BMC_, BNC_, CPW_, PIPE_>), dim3(grid), dim3(256), lds, st, a);         \
+    hipLaunchKernelGGL(k, dim3(grid), dim3(256 * TS_), lds, st, a);                                      \
     FDT_LAUNCH_CHECK();                                                                                  \
     return;                                                                                              \
   }
-  FDT_WH3(128, 32, 1, false)
-  FDT_WH3(128, 32, 1, true)
-  FDT_WH3(64, 64, 1, false)
-  FDT_WH3(64, 64, 1, true)
+  const int ts = (pipe & 4) ? 2 : 1;
+  // (the tap split with pipelined fragments computed wrong results: not instantiated)
+  FDT_CHECK(ts == 1 || (pipe & 1) == 0, "wgrad_h3: the tap split runs without the fragment pipeline");
+  FDT_WH3(128, 32, 1, false, 1)
+  FDT_WH3(128, 32, 1, true, 1)
+  FDT_WH3(64, 64, 1, false, 1)
+  FDT_WH3(64, 64, 1, true, 1)
+  FDT_WH3(128, 32, 1, false, 2)
+  FDT_WH3(64, 64, 1, false, 2)
 #undef FDT_WH3
 }
 

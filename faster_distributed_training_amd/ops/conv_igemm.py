@@ -575,8 +575,11 @@ WH3_WGS = int(os.environ.get("FDT_WGRAD_H3_WGS", "256"))
 # write and reduce when the pixel count is small)
 WH3_MIN_CPS = int(os.environ.get("FDT_WGRAD_H3_MIN_CPS", "1"))
 WH3_PX = 128
-# register-pipelined fragments (conv_wh3.hip PIPE): None = the measured choice (the 64 x 64 tile)
-WH3_PIPE = {"1": True, "0": False}.get(os.environ.get("FDT_WGRAD_H3_PIPE", ""))
+# register-pipelined fragments (conv_wh3.hip PIPE) and waves per (co, ci) block (TS: 2 = eight
+# waves, each with half the tap accumulators; not combinable with PIPE).  Both measured neutral
+# or slower at the final register allocation (profiles/r6/wh3_ts*_p*_*.txt): off by default
+WH3_PIPE = os.environ.get("FDT_WGRAD_H3_PIPE", "0") == "1"
+WH3_TS = int(os.environ.get("FDT_WGRAD_H3_TS", "1"))
 
 
 def wh3_plan(N, H, W, shp: "ConvShape", cx, fold=False, xaff=False, force=False):
@@ -643,7 +646,7 @@ def conv_wgrad(g, y, al, be, x, shp: ConvShape, out, xs=None, xt=None, act=0, al
         if slab is None or slab.numel() < ns * shp.cout * ldw:
             slab = torch.empty(ns * shp.cout * ldw, device=g.device, dtype=torch.float32)
         nat.conv_wgrad_h3(g.data_ptr(), x.data_ptr(), slab.data_ptr(), N, H, W, Cx, shp.cout, bmc, bnc, ns,
-                          int(WH3_PIPE if WH3_PIPE is not None else bnc == 64), _sp())
+                          int(WH3_PIPE) | (4 if WH3_TS == 2 else 0), _sp())
         nat.wgrad_reduce(slab.data_ptr(), out.data_ptr(), ns, shp.cout, shp.cin, shp.ntaps, shp.cxp,
                          int(accumulate), _sp())
         return out

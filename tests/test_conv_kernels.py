@@ -304,11 +304,15 @@ WH3_CASES = [(2, 32, 64, 64), (4, 16, 128, 128), (4, 8, 256, 256), (16, 4, 512, 
 
 @pytest.mark.parametrize("case", WH3_CASES)
 @pytest.mark.parametrize("wgs", [256, 7])
-def test_h3_conv_wgrad(cuda, case, wgs, monkeypatch):
+@pytest.mark.parametrize("variant", ["default", "pipe", "ts2"])
+def test_h3_conv_wgrad(cuda, case, wgs, variant, monkeypatch):
     """Halo-staged 3x3 weight gradient (conv_wh3.hip) against fp32 PyTorch and the implicit-GEMM
     weight gradient, fresh and accumulating; ``wgs`` 7: few workgroups -> long pixel ranges per
-    split (uneven last split)."""
+    split (uneven last split); variants: register-pipelined fragments, the tap split over two
+    waves per block."""
     monkeypatch.setattr(ci, "WH3_WGS", wgs)
+    monkeypatch.setattr(ci, "WH3_PIPE", variant == "pipe")
+    monkeypatch.setattr(ci, "WH3_TS", 2 if variant == "ts2" else 1)
     N, H, Cin, Cout = case
     torch.manual_seed(9)
     shp = ci.ConvShape(Cin, Cout, 3, 1, 1)
