@@ -74,3 +74,23 @@ def test_simulated_world8_transformer_step_with_graph_comm_check(cuda):
     rec = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
     assert rec["simulated"]["rank"] == 3 and rec["config"]["hip_graphs"]
     assert rec["config"].get("graph_comm", "").startswith("capture"), rec["config"]
+
+
+def test_comm_watch_drain_only_for_nccl(monkeypatch):
+    """parallel/graphs.drain_comm_watch: before a capture that can take collectives, eager RCCL
+    collectives are finished and RCCL's watchdog gets one polling interval; without an nccl
+    process group (here: none, then a simulated gloo rank) it returns at once."""
+    import time
+    from faster_distributed_training_amd.parallel import graphs as G
+    from faster_distributed_training_amd.parallel import simulate as S
+    slept = []
+    monkeypatch.setattr(time, "sleep", lambda s: slept.append(s))
+    G.drain_comm_watch()
+    assert slept == []
+    S.install(0, 2)
+    try:
+        assert dist.get_backend() == ("nccl" if torch.cuda.is_available() else "gloo")
+        G.drain_comm_watch()
+        assert slept == ([0.25] if torch.cuda.is_available() else [])
+    finally:
+        S.uninstall()
