@@ -265,6 +265,9 @@ def main():
                 if kind not in a.ops.split(","):
                     continue
                 op_key = lookup_key(fn, orig)
+                if op_key is None:  # the call consults no table entry (a halo loop): nothing to tune
+                    print(f"b{N} {key:22s} {kind}: no table lookup (halo loop), skipped", flush=True)
+                    continue
                 cur = table.get(key, {}).get(op_key)
                 ci._TUNED = None
                 timeit(fn, a.reps)  # warm-up (first captures of a shape run slow)
